@@ -1,0 +1,98 @@
+"""Shared, deterministic test cases (configs, weights, inputs) — used by the golden generator and by the tests.
+
+Nothing here reads `/root/reference`; weights and inputs are regenerated bit-exactly from counter-based RNG
+(`videopainter_amd.weights`).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from videopainter_amd.config import full_config, state_dict_shapes
+from videopainter_amd.weights import counter_uniform, synth_state_dict, synth_tensor
+from oracle.cogvideox_oracle import prepare_rotary_positional_embeddings
+
+TINY_CFG = dict(num_attention_heads=2, attention_head_dim=64, num_layers=4, in_channels=32, out_channels=16,
+                time_embed_dim=32, text_embed_dim=32, use_rotary_positional_embeddings=True,
+                use_learned_positional_embeddings=True, sample_height=16, sample_width=24, sample_frames=9,
+                max_text_seq_length=8)
+TINY_BRANCH_CFG = dict(TINY_CFG, num_layers=2)
+TINY_T = 8
+TINY_F, TINY_H, TINY_W = 3, 16, 24
+
+
+def tiny_weights(seed: int = 0):
+    tsd = synth_state_dict(state_dict_shapes(full_config(TINY_CFG)), seed)
+    bsd = synth_state_dict({("B." + k): v for k, v in state_dict_shapes(full_config(TINY_BRANCH_CFG, True), True)
+                            .items()}, seed)
+    bsd = {k[2:]: v for k, v in bsd.items()}
+    return tsd, bsd
+
+
+def make_mask(b, f, h, w, key="mask", first_frame_gt=True):
+    """Binary latent mask [B, F, 1, H, W]: centred rectangle (about 50% x 50%), jittered per batch/frame; frame 0
+    all-zero (first_frame_gt, infer/inpaint.py:425-430)."""
+    m = np.zeros((b, f, 1, h, w), dtype=np.float32)
+    u = counter_uniform(key, b * f * 4).reshape(b, f, 4)
+    for i in range(b):
+        for j in range(f):
+            if first_frame_gt and j == 0:
+                continue
+            y0 = int(h * 0.25 + (u[i, j, 0] - 0.5) * 2)
+            x0 = int(w * 0.25 + (u[i, j, 1] - 0.5) * 2)
+            y1 = y0 + h // 2 + int(u[i, j, 2] * 2)
+            x1 = x0 + w // 2 + int(u[i, j, 3] * 3)
+            m[i, j, 0, max(0, y0):min(h, y1), max(0, x0):min(w, x1)] = 1.0
+    return m
+
+
+def tiny_inputs(dtype=torch.float32):
+    b, f, h, w, t = 2, TINY_F, TINY_H, TINY_W, TINY_T
+    video = synth_tensor("tiny.video", (b, f, 16, h, w))
+    image = synth_tensor("tiny.image", (b, f, 16, h, w))
+    image[:, 1:] = 0.0
+    hidden = np.concatenate([video, image], axis=2)
+    hidden2 = np.concatenate([synth_tensor("tiny.video2", (b, f, 16, h, w)), image], axis=2)
+    mask = make_mask(b, f, h, w, "tiny.mask")
+    masked = synth_tensor("tiny.masked", (b, f, 16, h, w)) * (1.0 - mask)
+    branch_cond = np.concatenate([masked, mask], axis=2)
+    enc = synth_tensor("tiny.enc", (b, t, 32))
+    cos, sin = prepare_rotary_positional_embeddings(h * 8, w * 8, f, 64)
+    cv = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dtype)  # noqa: E731
+    return dict(hidden=cv(hidden), hidden2=cv(hidden2), video=cv(video), mask=cv(mask), branch_cond=cv(branch_cond),
+                enc=cv(enc), timestep=torch.tensor([999, 377], dtype=torch.int64), rope=(cos, sin))
+
+
+def full_block_case(seed: int = 0, dtype=torch.float32):
+    """One full-width block (D=3072, 48 heads x 64, temb 512) at config-1 shape: T=226, video 3x16x24 = 1152."""
+    from videopainter_amd.config import block_shapes
+    shapes = block_shapes(3072, 512)
+    s2 = {}
+    for k, v in shapes.items():
+        if k == "attn1.to_q.weight":
+            for n in ("norm_q", "norm_k"):
+                s2[f"attn1.{n}.weight"] = (64,)
+                s2[f"attn1.{n}.bias"] = (64,)
+        s2[k] = v
+    w = synth_state_dict({"FB." + k: v for k, v in s2.items()}, seed)
+    w = {k[3:]: v for k, v in w.items()}
+    h = torch.from_numpy(synth_tensor("fb.h", (1, 1152, 3072))).to(dtype)
+    e = torch.from_numpy(synth_tensor("fb.e", (1, 226, 3072))).to(dtype)
+    temb = torch.from_numpy(synth_tensor("fb.temb", (1, 512))).to(dtype)
+    rope = prepare_rotary_positional_embeddings(256, 384, 3, 64)
+    return dict(weights=w, h=h, e=e, temb=temb, rope=rope)
+
+
+PIPE_CASE = dict(num_frames=9, total_frames=18, stride=9, height=128, width=192, steps=2, prev_clip_weight=0.5,
+                 id_pool_resample_learnable=True)
+
+
+def pipe_inputs():
+    c = PIPE_CASE
+    n, h, w = c["total_frames"], c["height"], c["width"]
+    frames = (counter_uniform("pipe.frames", n * h * w * 3).reshape(n, h, w, 3) * 255).astype(np.uint8)
+    m = make_mask(1, n, h, w, "pipe.mask", first_frame_gt=True)[0, :, 0]
+    masks = np.repeat((m * 255).astype(np.uint8)[..., None], 3, axis=-1)
+    pe = torch.from_numpy(synth_tensor("pipe.prompt", (1, TINY_T, 32)))
+    ne = torch.from_numpy(synth_tensor("pipe.neg", (1, TINY_T, 32)))
+    return dict(frames=frames, masks=masks, prompt_embeds=pe, negative_prompt_embeds=ne)

@@ -1,0 +1,238 @@
+"""Generate golden vectors from the REFERENCE implementation (run in the survey/build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+Imports the reference's vendored diffusers (`/root/reference/diffusers/src`, 0.31.0.dev0 fork) read-only, builds the
+reference modules with deterministic counter-based weights (`videopainter_amd.weights`), runs them in fp32 on CPU and
+stores inputs-independent outputs as small safetensors fixtures next to this script.  Inputs and weights are NOT
+stored: they are regenerated bit-exactly from (name, seed) by `videopainter_amd.weights` on any host.
+
+Fixtures (all fp32):
+  tiny_*.safetensors    — tiny config (2 heads x 64, 4 layers, 2-layer branch, latent 3x16x24, T=8), the branch,
+                          the transformer in std / mask-less / add_first / ID-resample (window 0 and prev-window) /
+                          prev-clip modes.
+  sched.safetensors     — CogVideoXDPMScheduler: trailing timesteps, 3 steps incl. the 2nd-order branch, add_noise.
+  pipe_tiny.safetensors — CogVideoXI2VDualInpaintAnyLPipeline, tiny model + tiny VAE, 2 windows x 2 steps, ID-resample
+                          with prev_clip_weight 0.5: the VAE-side latents it produced (captured), every scheduler noise
+                          it drew (captured) and the final latents.
+  block_full.safetensors— one full-width CogVideoXBlock (3072 = 48 x 64) at N = 226 + 1152 (config-1 shape), B=1:
+                          strided slice + digest of the output.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, "/root/reference/diffusers/src")
+
+import transformers.utils as _tu  # noqa: E402
+
+_tu.FLAX_WEIGHTS_NAME = "flax_model.msgpack"  # attribute removed in transformers 5; pipelines import it
+
+from safetensors.torch import save_file  # noqa: E402
+
+from tests.golden.cases import (TINY_CFG, TINY_BRANCH_CFG, tiny_inputs, tiny_weights, full_block_case,  # noqa: E402
+                                PIPE_CASE, pipe_inputs)
+
+torch.manual_seed(0)
+torch.set_num_threads(8)
+
+
+def _save(name, tensors, meta=None):
+    path = os.path.join(HERE, name)
+    save_file({k: v.detach().float().contiguous() for k, v in tensors.items()}, path,
+              metadata={k: json.dumps(v) for k, v in (meta or {}).items()})
+    print("wrote", path, sum(v.numel() for v in tensors.values()) * 4 / 1e6, "MB")
+
+
+def build_models(resample=False):
+    from diffusers.models.transformers.cogvideox_transformer_3d import CogVideoXTransformer3DModel
+    from diffusers.models.branch_cogvideox import CogvideoXBranchModel
+    cfg = dict(TINY_CFG)
+    cfg["id_pool_resample_learnable"] = resample
+    tr = CogVideoXTransformer3DModel(**cfg).eval()
+    br = CogvideoXBranchModel(**TINY_BRANCH_CFG).eval()
+    tsd, bsd = tiny_weights()
+    tr.load_state_dict({k: torch.from_numpy(v) for k, v in tsd.items()}, strict=True)
+    br.load_state_dict({k: torch.from_numpy(v) for k, v in bsd.items()}, strict=True)
+    return tr, br
+
+
+@torch.no_grad()
+def make_tiny():
+    inp = tiny_inputs()
+    tr, br = build_models(False)
+    rope = inp["rope"]
+    out = {}
+    bs = br(hidden_states=inp["video"], encoder_hidden_states=inp["enc"], branch_cond=inp["branch_cond"],
+            timestep=inp["timestep"], image_rotary_emb=rope, return_dict=False)[0]
+    for j, s in enumerate(bs):
+        out[f"branch.{j}"] = s
+    o, hs, rm = tr(hidden_states=inp["hidden"], encoder_hidden_states=inp["enc"], timestep=inp["timestep"],
+                   image_rotary_emb=rope, branch_block_samples=bs, branch_block_masks=inp["mask"],
+                   return_hidden_states=True, return_resample_mask=True, return_dict=False)
+    out["std.out"] = o
+    for i, h in enumerate(hs):
+        out[f"std.hs.{i}"] = h
+    out["std.resample_mask"] = rm.float()
+    o = tr(hidden_states=inp["hidden"], encoder_hidden_states=inp["enc"], timestep=inp["timestep"],
+           image_rotary_emb=rope, branch_block_samples=bs, branch_block_masks=None, return_dict=False)[0]
+    out["nomask.out"] = o
+    o = tr(hidden_states=inp["hidden"], encoder_hidden_states=inp["enc"], timestep=inp["timestep"],
+           image_rotary_emb=rope, branch_block_samples=bs, branch_block_masks=inp["mask"], add_first=True,
+           return_dict=False)[0]
+    out["addfirst.out"] = o
+    # prev-clip through the standard processor (a8): previous window states = this window's hidden states
+    prev = {i: h for i, h in enumerate(hs)}
+    o = tr(hidden_states=inp["hidden"], encoder_hidden_states=inp["enc"], timestep=inp["timestep"],
+           image_rotary_emb=rope, branch_block_samples=bs, branch_block_masks=inp["mask"],
+           attention_kwargs={"prev_hidden_states": prev, "prev_clip_weight": 0.5, "prev_resample_mask": rm},
+           return_dict=False)[0]
+    out["prevclip.out"] = o
+
+    # ID-resample transformer (a9)
+    trr, _ = build_models(True)
+    o, hs_r, rm_r = trr(hidden_states=inp["hidden"], encoder_hidden_states=inp["enc"], timestep=inp["timestep"],
+                        image_rotary_emb=rope, branch_block_samples=bs, branch_block_masks=inp["mask"],
+                        id_pool_resample_learnable=True, return_hidden_states=True, return_resample_mask=True,
+                        return_dict=False)
+    out["resample0.out"] = o
+    out["resample0.hs.3"] = hs_r[3]
+    prev = {i: h for i, h in enumerate(hs_r)}
+    o = trr(hidden_states=inp["hidden2"], encoder_hidden_states=inp["enc"], timestep=inp["timestep"],
+            image_rotary_emb=rope, branch_block_samples=bs, branch_block_masks=inp["mask"],
+            attention_kwargs={"prev_hidden_states": prev, "prev_clip_weight": 0.5, "prev_resample_mask": rm_r},
+            id_pool_resample_learnable=True, return_hidden_states=True, return_resample_mask=True,
+            return_dict=False)[0]
+    out["resample1.out"] = o
+    _save("tiny.safetensors", out)
+
+
+@torch.no_grad()
+def make_sched():
+    from diffusers import CogVideoXDPMScheduler
+    sch = CogVideoXDPMScheduler(snr_shift_scale=1.0, prediction_type="v_prediction", rescale_betas_zero_snr=True,
+                                clip_sample=False, set_alpha_to_one=True, timestep_spacing="trailing",
+                                beta_start=0.00085, beta_end=0.012)
+    sch.set_timesteps(50)
+    ts = sch.timesteps
+    shape = (1, 3, 4, 8, 12)
+    from videopainter_amd.weights import synth_tensor
+    sample = torch.from_numpy(synth_tensor("sched.sample", shape)).to(torch.bfloat16)
+    gen = torch.Generator().manual_seed(11)
+    old = None
+    out = {"timesteps": ts.float(), "alphas_cumprod": sch.alphas_cumprod.float()}
+    for i in range(3):
+        mo = torch.from_numpy(synth_tensor(f"sched.model_output.{i}", shape, bf16=False))
+        sample, old = sch.step(mo, old, ts[i], ts[i - 1] if i > 0 else None, sample, generator=gen,
+                               return_dict=False)
+        sample = sample.to(torch.bfloat16)
+        out[f"step{i}.prev_sample"] = sample
+        out[f"step{i}.pred_original"] = old
+    gt = torch.from_numpy(synth_tensor("sched.gt", shape)).to(torch.bfloat16)
+    nz = torch.from_numpy(synth_tensor("sched.noise", shape)).to(torch.bfloat16)
+    out["add_noise"] = sch.add_noise(gt, nz, torch.tensor([int(ts[5])]))
+    _save("sched.safetensors", out, {"noise_seed": 11})
+
+
+@torch.no_grad()
+def make_pipe():
+    """Run the reference any-length pipeline on a tiny model and record what the step loop saw."""
+    import diffusers.schedulers.scheduling_dpm_cogvideox as dpm_mod
+    from diffusers import AutoencoderKLCogVideoX, CogVideoXDPMScheduler
+    from diffusers.pipelines.cogvideo.pipeline_cogvideox_inpainting_i2v_branch_anyl import (
+        CogVideoXI2VDualInpaintAnyLPipeline)
+    from PIL import Image
+
+    c = PIPE_CASE
+    tr, br = build_models(resample=c["id_pool_resample_learnable"])
+    torch.manual_seed(1234)
+    vae = AutoencoderKLCogVideoX(block_out_channels=(32, 32, 32, 32), layers_per_block=1, latent_channels=16,
+                                 norm_num_groups=32, temporal_compression_ratio=4).eval()
+    sch = CogVideoXDPMScheduler(snr_shift_scale=1.0, prediction_type="v_prediction", rescale_betas_zero_snr=True,
+                                clip_sample=False, set_alpha_to_one=True, timestep_spacing="trailing",
+                                beta_start=0.00085, beta_end=0.012)
+    pipe = CogVideoXI2VDualInpaintAnyLPipeline(tokenizer=None, text_encoder=None, vae=vae, transformer=tr,
+                                               scheduler=sch, branch=br)
+    rec = {"latents": [], "mask": [], "noise": [], "sched_noise": []}
+    orig_prep = pipe.prepare_latents
+    orig_mask = pipe.prepare_mask_latents
+
+    def prep(*a, **k):
+        outs = orig_prep(*a, **k)
+        rec["latents"].append([o.clone() for o in outs])
+        return outs
+
+    def prepm(*a, **k):
+        outs = orig_mask(*a, **k)
+        rec["mask"].append([o.clone() for o in outs])
+        return outs
+
+    orig_randn = dpm_mod.randn_tensor
+
+    def rn(*a, **k):
+        x = orig_randn(*a, **k)
+        rec["sched_noise"].append(x.clone())
+        return x
+
+    pipe.prepare_latents = prep
+    pipe.prepare_mask_latents = prepm
+    dpm_mod.randn_tensor = rn
+    inp = pipe_inputs()
+    frames = [Image.fromarray(f) for f in inp["frames"]]
+    masks = [Image.fromarray(m) for m in inp["masks"]]
+    res = pipe(prompt_embeds=inp["prompt_embeds"], negative_prompt_embeds=inp["negative_prompt_embeds"],
+               image=frames[0], video=frames, masks=masks, num_frames=c["num_frames"], height=c["height"],
+               width=c["width"], num_inference_steps=c["steps"], use_dynamic_cfg=True, guidance_scale=6.0,
+               generator=torch.Generator().manual_seed(42), strength=1.0, replace_gt=True, mask_add=True,
+               stride=c["stride"], prev_clip_weight=c["prev_clip_weight"],
+               id_pool_resample_learnable=c["id_pool_resample_learnable"], output_type="latent",
+               return_dict=False)[0]
+    dpm_mod.randn_tensor = orig_randn
+    out = {"final": res}
+    for w, (lat, img, noise, vid) in enumerate(rec["latents"]):
+        out[f"w{w}.latents"] = lat
+        out[f"w{w}.image_latents"] = img
+        out[f"w{w}.noise"] = noise
+        out[f"w{w}.video_latents"] = vid
+    for w, (m, mv) in enumerate(rec["mask"]):
+        out[f"w{w}.mask"] = m
+        out[f"w{w}.masked_video_latents"] = mv
+    for i, n in enumerate(rec["sched_noise"]):
+        out[f"sched_noise.{i}"] = n
+    _save("pipe_tiny.safetensors", out, {"case": c, "n_sched_noise": len(rec["sched_noise"])})
+
+
+@torch.no_grad()
+def make_full_block():
+    from diffusers.models.transformers.cogvideox_transformer_3d import CogVideoXBlock
+    case = full_block_case()
+    blk = CogVideoXBlock(dim=3072, num_attention_heads=48, attention_head_dim=64, time_embed_dim=512,
+                         attention_bias=True).eval()
+    blk.load_state_dict({k: torch.from_numpy(v) for k, v in case["weights"].items()}, strict=True)
+    h, e = blk(hidden_states=case["h"], encoder_hidden_states=case["e"], temb=case["temb"],
+               image_rotary_emb=case["rope"])
+    out = torch.cat([e, h], dim=1)
+    flat = out.reshape(-1)
+    _save("block_full.safetensors", {"slice": flat[::97].clone(),
+                                     "digest": torch.tensor([flat.sum(), flat.abs().sum(), flat.norm()],
+                                                            dtype=torch.float64)})
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["tiny", "sched", "pipe", "block"]
+    if "tiny" in which:
+        make_tiny()
+    if "sched" in which:
+        make_sched()
+    if "pipe" in which:
+        make_pipe()
+    if "block" in which:
+        make_full_block()

@@ -1,0 +1,139 @@
+"""Pin the CPU oracle (oracle/cogvideox_oracle.py) against golden vectors recorded from the reference.
+
+CPU-only (no `gpu` marker).  Tolerance: fp32 vs fp32, rel-L2 <= 1e-5 (same torch ops, same order of operations; the
+only differences are in how tensors are sliced/concatenated).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+from safetensors.torch import load_file
+
+from oracle import cogvideox_oracle as O
+from tests.golden.cases import (TINY_CFG, TINY_BRANCH_CFG, tiny_inputs, tiny_weights, full_block_case, PIPE_CASE)
+from videopainter_amd.config import full_config
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel(a, b):
+    a = a.double()
+    b = b.double()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    tsd, bsd = tiny_weights()
+    tsd = {k: torch.from_numpy(v) for k, v in tsd.items()}
+    bsd = {k: torch.from_numpy(v) for k, v in bsd.items()}
+    return dict(tsd=tsd, bsd=bsd, inp=tiny_inputs(), gold=load_file(os.path.join(GOLD, "tiny.safetensors")),
+                tcfg=full_config(TINY_CFG), bcfg=full_config(TINY_BRANCH_CFG, True))
+
+
+def _branch(t):
+    i = t["inp"]
+    return O.branch_forward(t["bsd"], t["bcfg"], i["video"], i["enc"], i["branch_cond"], i["timestep"], i["rope"])
+
+
+def test_branch(tiny):
+    bs = _branch(tiny)
+    for j, s in enumerate(bs):
+        assert rel(s, tiny["gold"][f"branch.{j}"]) < 1e-5
+
+
+def test_transformer_std_with_hidden_states(tiny):
+    i = tiny["inp"]
+    bs = [tiny["gold"]["branch.0"], tiny["gold"]["branch.1"]]
+    out, hs, rm = O.transformer_forward(tiny["tsd"], tiny["tcfg"], i["hidden"], i["enc"], i["timestep"], i["rope"],
+                                        branch_block_samples=bs, branch_block_masks=i["mask"],
+                                        return_hidden_states=True, return_resample_mask=True)
+    g = tiny["gold"]
+    assert rel(out, g["std.out"]) < 1e-5
+    for k, h in enumerate(hs):
+        assert rel(h, g[f"std.hs.{k}"]) < 1e-5
+    assert torch.equal(rm.float(), g["std.resample_mask"])
+
+
+@pytest.mark.parametrize("mode", ["nomask", "addfirst", "prevclip"])
+def test_transformer_modes(tiny, mode):
+    i = tiny["inp"]
+    g = tiny["gold"]
+    bs = [g["branch.0"], g["branch.1"]]
+    kw = dict(branch_block_samples=bs, branch_block_masks=i["mask"])
+    if mode == "nomask":
+        kw["branch_block_masks"] = None
+    if mode == "addfirst":
+        kw["add_first"] = True
+    if mode == "prevclip":
+        prev = {k: g[f"std.hs.{k}"] for k in range(4)}
+        kw["attention_kwargs"] = {"prev_hidden_states": prev, "prev_clip_weight": 0.5,
+                                  "prev_resample_mask": g["std.resample_mask"].bool()}
+    out = O.transformer_forward(tiny["tsd"], tiny["tcfg"], i["hidden"], i["enc"], i["timestep"], i["rope"], **kw)[0]
+    assert rel(out, g[f"{mode}.out"]) < 1e-5
+
+
+def test_transformer_resample(tiny):
+    i = tiny["inp"]
+    g = tiny["gold"]
+    cfg = dict(tiny["tcfg"], id_pool_resample_learnable=True)
+    bs = [g["branch.0"], g["branch.1"]]
+    out, hs, rm = O.transformer_forward(tiny["tsd"], cfg, i["hidden"], i["enc"], i["timestep"], i["rope"],
+                                        branch_block_samples=bs, branch_block_masks=i["mask"],
+                                        return_hidden_states=True, return_resample_mask=True,
+                                        id_pool_resample_learnable=True)
+    assert rel(out, g["resample0.out"]) < 1e-5
+    assert rel(hs[3], g["resample0.hs.3"]) < 1e-5
+    prev = {k: h for k, h in enumerate(hs)}
+    out1 = O.transformer_forward(tiny["tsd"], cfg, i["hidden2"], i["enc"], i["timestep"], i["rope"],
+                                 attention_kwargs={"prev_hidden_states": prev, "prev_clip_weight": 0.5,
+                                                   "prev_resample_mask": rm},
+                                 branch_block_samples=bs, branch_block_masks=i["mask"], return_hidden_states=True,
+                                 return_resample_mask=True, id_pool_resample_learnable=True)[0]
+    assert rel(out1, g["resample1.out"]) < 1e-5
+
+
+def test_scheduler():
+    g = load_file(os.path.join(GOLD, "sched.safetensors"))
+    from videopainter_amd.weights import synth_tensor
+    s = O.DPMSchedulerOracle()
+    ts = s.set_timesteps(50)
+    assert torch.equal(ts.float(), g["timesteps"])
+    assert torch.allclose(s.alphas_cumprod.float(), g["alphas_cumprod"])
+    shape = (1, 3, 4, 8, 12)
+    sample = torch.from_numpy(synth_tensor("sched.sample", shape)).to(torch.bfloat16)
+    gen = torch.Generator().manual_seed(11)
+    old = None
+    for i in range(3):
+        mo = torch.from_numpy(synth_tensor(f"sched.model_output.{i}", shape, bf16=False))
+        n1 = torch.randn(shape, generator=gen, dtype=torch.bfloat16)
+        n2 = torch.randn(shape, generator=gen, dtype=torch.bfloat16) if (old is not None) else None
+        sample, old = s.step(mo, old, int(ts[i]), int(ts[i - 1]) if i > 0 else None, sample, n1, n2)
+        sample = sample.to(torch.bfloat16)
+        assert torch.equal(sample.float(), g[f"step{i}.prev_sample"])
+        assert torch.equal(old.float(), g[f"step{i}.pred_original"])
+    gt = torch.from_numpy(synth_tensor("sched.gt", shape)).to(torch.bfloat16)
+    nz = torch.from_numpy(synth_tensor("sched.noise", shape)).to(torch.bfloat16)
+    assert torch.equal(s.add_noise(gt, nz, torch.tensor([int(ts[5])])).float(), g["add_noise"])
+
+
+def test_rope_tables_match_pipeline_convention():
+    cos, sin = O.prepare_rotary_positional_embeddings(480, 720, 13, 64)
+    assert cos.shape == (13 * 30 * 45, 64)
+    # t block = 16 dims, h/w = 24 dims each; pairs are interleaved (repeat_interleave)
+    assert torch.equal(cos[:, 0::2], cos[:, 1::2])
+    assert torch.allclose(cos[0], torch.ones(64))
+
+
+def test_full_width_block():
+    g = load_file(os.path.join(GOLD, "block_full.safetensors"))
+    c = full_block_case()
+    sd = {"b." + k: torch.from_numpy(v) for k, v in c["weights"].items()}
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    h, e = O.block_forward(sd, "b", dict(num_attention_heads=48, norm_eps=1e-5), c["h"], c["e"], c["temb"], c["rope"])
+    flat = torch.cat([e, h], dim=1).reshape(-1)
+    assert rel(flat[::97], g["slice"]) < 1e-5
+    d = g["digest"]
+    # digest was reduced in fp32 by the generator; compare like with like
+    assert abs(float(flat.norm()) - float(d[2])) / float(d[2]) < 1e-5
