@@ -1,0 +1,215 @@
+/* vp_hip.h — C ABI of the MI355X (gfx950) VideoPainter denoising hot path (libvp_hip.so).
+ *
+ * Every entry point takes plain device pointers, sizes and element strides, plus the HIP stream to launch on
+ * (`void* stream` = hipStream_t; NULL = default stream).  No torch types cross this boundary.
+ *   - Ownership: the caller allocates every output and workspace; no entry point allocates or frees.
+ *   - Errors: return 0 on success, VP_ERR_* (>= 1000) for an argument error detected on the host, or the
+ *     hipError_t of the failed launch.  Nothing is printed.
+ *   - Threading: stateless and re-entrant; each call is asynchronous on `stream` and may be captured in a graph.
+ *   - Storage dtype: bf16 (`__bf16` / torch.bfloat16) unless stated; accumulation is fp32.
+ *
+ * Each entry point cites the reference interface it replaces (paths relative to
+ * /root/reference/diffusers/src/diffusers/, abbreviated DF/).  The Python host mirror that binds them by ctypes is
+ * videopainter_amd/_native.py; the reference-side binding a maintainer would add is shown in INTEGRATION.md.
+ */
+#ifndef VP_HIP_H
+#define VP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VP_OK 0
+#define VP_ERR_ARG 1000      /* invalid size / stride / pointer combination */
+#define VP_ERR_UNSUPPORTED 1001
+
+/* ABI version: bump when any struct layout or signature below changes. */
+#define VP_ABI_VERSION 1
+int vp_abi_version(void);
+/* sizeof of the descriptor structs as compiled into the library: out[0..2] = gemm, attn, dpm (ABI self-check) */
+void vp_struct_sizes(int64_t* out);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * GEMM  C = epilogue(A · Wᵀ)   — replaces every nn.Linear / patch-embed conv on the path:
+ *   attn.to_q/to_k/to_v/to_out.0 (DF/models/attention_processor.py:2132-2134,2202), FeedForward net.0.proj + GELU
+ *   and net.2 (DF/models/attention.py:1177,1191; activations.py:65-90), the gated residuals
+ *   (DF/models/transformers/cogvideox_transformer_3d.py:169-170,181-182), the branch injection (:596-609), the
+ *   patch-embed conv + text_proj + pos-emb (DF/models/embeddings.py:400-454), the branch zero-linears
+ *   (DF/models/branch_cogvideox.py:415-421) and proj_out (cogvideox_transformer_3d.py:624).
+ * A: bf16 [M, K] (row stride lda); W: up to 3 weight segments, each bf16 [n_seg, K] (nn.Linear layout), columns
+ * [s*n_seg, (s+1)*n_seg) of C come from segment s (fused QKV without packing the weights).  K % 64 == 0.
+ * Output row remap: C row of GEMM row m = (m / rows_per_group) * group_stride + row_offset + (m % rows_per_group).
+ * ------------------------------------------------------------------------------------------------------------- */
+enum {
+  VP_EPI_BIAS = 0,        /* C = rnd(acc + bias)                                                            */
+  VP_EPI_BIAS_GELU = 1,   /* C = rnd(gelu_tanh(rnd(acc + bias)))                                             */
+  VP_EPI_BIAS_SCALE = 2,  /* C = rnd(rnd(acc + bias) * alpha)            (branch conditioning_scale)         */
+  VP_EPI_GATED = 3,       /* C = rnd(R + rnd(gate * rnd(acc + bias))) [then rnd(C + inject) on video rows]   */
+  VP_EPI_BIAS_ADDROWS = 4 /* C = rnd(rnd(acc + bias) + addrows[(m % rows_per_group) + addrows_offset, n])   */
+};
+
+typedef struct vp_gemm_desc {
+  int32_t M, N, K, epilogue;
+  const void* A;
+  int64_t lda;
+  const void* W[3];
+  const void* bias[3]; /* bf16 [n_seg] per segment, or NULL */
+  int32_t n_seg, pad0;
+  void* C;
+  int64_t ldc;
+  int32_t rows_per_group, pad1;
+  int64_t group_stride, row_offset;
+  float alpha;
+  int32_t pad2;
+  /* VP_EPI_GATED: rows are (batch, token) of a [B, tokens_per_batch, N] stream; text tokens (token < text_len)
+   * take gate_text[b], video tokens gate[b]; gate vectors bf16 [N] at batch stride gate_bstride.  R may alias C. */
+  const void* R;
+  int64_t ldr;
+  const void* gate;
+  const void* gate_text;
+  int64_t gate_bstride;
+  int32_t tokens_per_batch, text_len;
+  /* optional branch injection on video rows: C += inject[b, token - text_len, :] where inject_mask[b, v] == 0
+   * (or always when inject_mask == NULL) */
+  const void* inject;
+  int64_t inject_ld, inject_bstride;
+  const uint8_t* inject_mask;
+  int64_t inject_mask_bstride;
+  /* VP_EPI_BIAS_ADDROWS */
+  const void* addrows;
+  int64_t addrows_ld, addrows_offset;
+} vp_gemm_desc;
+
+int vp_gemm_bf16(const vp_gemm_desc* d, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Flash attention forward, head_dim 64, non-causal, no mask — replaces F.scaled_dot_product_attention in
+ * CogVideoXAttnProcessor2_0 (DF/models/attention_processor.py:2177-2197) and CogVideoXAttnProcessor2_0_resample
+ * (:2283-2290; the doubled K/V is passed as two segments instead of being concatenated).
+ * Element (b, h, n, d) of Q is Q[b*q_sb + n*q_sn + h*64 + d]; likewise K, V, K2, V2, O.
+ * O = rnd(out_scale * rnd(softmax(scale Q Kᵀ) V)) (+ O_old when accumulate) — the prev-clip blend.
+ * ------------------------------------------------------------------------------------------------------------- */
+typedef struct vp_attn_desc {
+  int32_t B, H, Nq, head_dim;
+  const void* Q;
+  int64_t q_sb, q_sn;
+  const void* K;
+  const void* V;
+  int64_t k_sb, k_sn, v_sb, v_sn;
+  int32_t Nk, Nk2;
+  const void* K2; /* optional second key/value segment (Nk2 == 0: none) */
+  const void* V2;
+  int64_t k2_sb, k2_sn, v2_sb, v2_sn;
+  void* O;
+  int64_t o_sb, o_sn;
+  float scale, out_scale;
+  int32_t accumulate, pad;
+} vp_attn_desc;
+
+int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * AdaLN-Zero modulate — CogVideoXLayerNormZero.forward (DF/models/normalization.py:373-379):
+ * y = rnd(rnd(rnd(LN(x)) * rnd(1 + scale)) + shift) over rows of x [B, Ntok, D] (contiguous).  mod is the bf16
+ * output of the block's norm linear, [B, 6D] = shift | scale | gate | enc_shift | enc_scale | enc_gate at batch
+ * stride mod_bstride; text rows (token < text_len) use the enc_* chunks.  LN affine (ln_w, ln_b), eps.
+ * ------------------------------------------------------------------------------------------------------------- */
+int vp_adaln_modulate_bf16(const void* x, void* y, int32_t B, int32_t Ntok, int32_t D, int32_t text_len,
+                           const void* ln_w, const void* ln_b, float eps, const void* mod, int64_t mod_bstride,
+                           void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Per-head LayerNorm(64) + interleaved-pair RoPE — attn.norm_q / norm_k (attention_processor.py:2143-2146) and
+ * apply_rotary_emb on tokens >= text_len (:2149-2154; DF/models/embeddings.py:655-701).
+ * x_in/x_out: [B, Ntok, H*64] with row stride ld_* and batch stride bs_*; may alias.  cos/sin fp32 [Ntok-text_len,
+ * 64] (NULL: no RoPE).  Optional pre-mask (resample processor, attention_processor.py:2251-2256): if tok_mask !=
+ * NULL the input row is first replaced by rnd(rnd(x * tok_mask[b, n]) * pre_scale) — LN of a zeroed row gives the
+ * LN bias (the "null key").
+ * ------------------------------------------------------------------------------------------------------------- */
+int vp_head_norm_rope_bf16(const void* x_in, int64_t ld_in, int64_t bs_in, void* x_out, int64_t ld_out,
+                           int64_t bs_out, int32_t B, int32_t Ntok, int32_t H, int32_t text_len, const void* ln_w,
+                           const void* ln_b, float eps, const float* cos, const float* sin, const uint8_t* tok_mask,
+                           int64_t mask_bstride, float pre_scale, void* stream);
+
+/* y[b, n, :] = rnd(rnd(x[b, n, :] * tok_mask[b, n]) * scale) — the masked value copy of the resample processor. */
+int vp_mask_scale_rows_bf16(const void* x_in, int64_t ld_in, int64_t bs_in, void* y, int64_t ld_out, int64_t bs_out,
+                            int32_t B, int32_t Ntok, int32_t D, const uint8_t* tok_mask, int64_t mask_bstride,
+                            float scale, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Output head norms — norm_final (cogvideox_transformer_3d.py:617-620) then AdaLayerNorm(chunk_dim=1)
+ * (DF/models/normalization.py:73-85, shift|scale order): for video rows only,
+ * y[b, v] = rnd(rnd(rnd(LN2(rnd(LN1(x[b, text_len + v])))) * rnd(1 + scale)) + shift);  mod bf16 [B, 2D].
+ * ------------------------------------------------------------------------------------------------------------- */
+int vp_final_norm_bf16(const void* x, void* y, int32_t B, int32_t Ntok, int32_t D, int32_t text_len,
+                       const void* ln1_w, const void* ln1_b, const void* ln2_w, const void* ln2_b, float eps,
+                       const void* mod, int64_t mod_bstride, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Small-M linear for the conditioning path: y[m, n] = act_out(Σ_k act_in(x[m, k]) W[n, k] + bias[n]), M <= 16.
+ * act: 0 none, 1 SiLU (rounded to bf16 like the reference's bf16 nn.SiLU).  Replaces TimestepEmbedding
+ * (DF/models/embeddings.py:729-774) and the AdaLN linears (normalization.py:64,370).
+ * ------------------------------------------------------------------------------------------------------------- */
+int vp_linear_small_bf16(const void* x, int64_t ldx, const void* W, const void* bias, void* y, int64_t ldy, int32_t M,
+                         int32_t N, int32_t K, int32_t act_in, int32_t act_out, void* stream);
+
+/* sinusoidal timestep embedding, flip_sin_to_cos: out bf16 [B, dim] — get_timestep_embedding
+ * (DF/models/embeddings.py:27-78); timesteps: device fp32 [B] (the reference casts to float). */
+int vp_timestep_embedding_bf16(const float* timesteps, void* out, int32_t B, int32_t dim, float freq_shift,
+                               void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Patch embedding data movement (DF/models/embeddings.py:413-430; branch concat branch_cogvideox.py:359):
+ * im2col of src1 [B,F,C1,H,W] ⊕ src2 [B,F,C2,H,W] (channel concat) into rows (b, f, y, x) of out [B*F*(H/p)*(W/p),
+ * Kpad], column c*p*p + dy*p + dx, zero-padded to Kpad.
+ * ------------------------------------------------------------------------------------------------------------- */
+int vp_patchify_bf16(const void* src1, int32_t C1, const void* src2, int32_t C2, void* out, int32_t Kpad, int32_t B,
+                     int32_t F, int32_t H, int32_t W, int32_t p, void* stream);
+
+/* token mask: out[b, v] = (Σ of mask[b, f, 0, patch(v)] > 0) — avg_pool2d(p) > 0 (embeddings.py:421-428).
+ * mask_is_f32: 1 if mask is fp32, 0 if bf16. */
+int vp_patch_mask(const void* mask, int32_t mask_is_f32, uint8_t* out, int32_t B, int32_t F, int32_t H, int32_t W,
+                  int32_t p, void* stream);
+
+/* unpatchify (cogvideox_transformer_3d.py:630-632): out[b,f,c,y*p+py,x*p+px] = proj[b, (f,y,x), c*p*p+py*p+px] */
+int vp_unpatchify_bf16(const void* proj, int64_t ld, void* out, int32_t B, int32_t F, int32_t C, int32_t H, int32_t W,
+                       int32_t p, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * One denoising-step glue, fused: CFG combine (anyl.py:995-997), CogVideoXDPMScheduler.step
+ * (DF/schedulers/scheduling_dpm_cogvideox.py:330-439, v-prediction, incl. the 2nd-order branch) and the replace-gt
+ * blend with add_noise (anyl.py:1017-1034; scheduler :442-466).  Scalars are precomputed on the host in the
+ * reference's dtypes (bf16-rounded where the reference multiplies a bf16 tensor by a 0-dim fp64 tensor).
+ * ------------------------------------------------------------------------------------------------------------- */
+typedef struct vp_dpm_desc {
+  int64_t n;
+  const void* noise_pred; /* bf16 [2, n] when do_cfg (uncond, text), else [n] */
+  int32_t do_cfg;
+  float guidance;
+  const void* sample;     /* bf16 [n] */
+  const float* old_pred;  /* fp32 [n] or NULL */
+  float* pred_out;        /* fp32 [n] */
+  const void* noise1;     /* bf16 [n] */
+  const void* noise2;     /* bf16 [n] (second-order step only) */
+  int32_t second_order, replace_gt;
+  float sa, sb, m1, m2, mn, m3, m4; /* sqrt(a_t) (bf16-rounded), sqrt(1-a_t), mult1 (bf16), mult2, mult_noise
+                                       (bf16), mult3, mult4 */
+  int32_t gt_add_noise, mask_background;
+  const void* gt;         /* bf16 [n] video latents */
+  const void* gt_noise;   /* bf16 [n] */
+  const void* mask;       /* bf16 [n] */
+  float gsa, gsb;         /* add_noise scalars, bf16-rounded */
+  void* latents_out;      /* bf16 [n] */
+} vp_dpm_desc;
+
+int vp_dpm_step_bf16(const vp_dpm_desc* d, void* stream);
+
+/* deterministic N(mean, std²) fill (splitmix64 + Box-Muller) for synthetic weights on the device */
+int vp_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float mean, float std, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VP_HIP_H */

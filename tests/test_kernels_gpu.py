@@ -1,0 +1,253 @@
+"""Numerics of each HIP kernel against a plain-PyTorch fp32 reference of the same op (GPU only)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from videopainter_amd import _native
+    _native.lib()
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def rnd(*shape, std=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * std)
+
+
+def test_gemm_layout_exact():
+    """Small-integer operands: every product and sum is exact in fp32 -> bit-exact check of the fragment maps."""
+    from videopainter_amd import kernels as K
+    g = torch.Generator().manual_seed(1)
+    M, Nn, Kk = 300, 512, 128
+    a = torch.randint(-3, 4, (M, Kk), generator=g).float()
+    w = torch.randint(-3, 4, (Nn, Kk), generator=g).float()
+    w[:, 0] += torch.arange(Nn).float() % 7  # asymmetric
+    b = torch.randint(-4, 5, (Nn,), generator=g).float()
+    out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    K.gemm(bf(a).to(dev), [bf(w).to(dev)], [bf(b).to(dev)], out)
+    ref = a @ w.T + b
+    assert torch.equal(out.float().cpu(), bf(ref).float())
+
+
+@pytest.mark.parametrize("M,Nn,Kk", [(1000, 768, 512), (35, 64, 3072), (513, 256, 192)])
+def test_gemm_bias_random(M, Nn, Kk):
+    from videopainter_amd import kernels as K
+    a, w, b = bf(rnd(M, Kk, seed=2)), bf(rnd(Nn, Kk, std=Kk ** -0.5, seed=3)), bf(rnd(Nn, std=0.1, seed=4))
+    out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    K.gemm(a.to(dev), [w.to(dev)], [b.to(dev)], out)
+    ref = a.float() @ w.float().T + b.float()
+    assert rel(out, ref) < 4e-3
+
+
+def test_gemm_segments_gelu_scale():
+    from videopainter_amd import kernels as K
+    from videopainter_amd import _native as N
+    M, D, Kk = 700, 256, 256
+    a = bf(rnd(M, Kk, seed=5))
+    ws = [bf(rnd(D, Kk, std=Kk ** -0.5, seed=6 + i)) for i in range(3)]
+    bs = [bf(rnd(D, std=0.1, seed=16 + i)) for i in range(3)]
+    out = torch.empty(M, 3 * D, device=dev, dtype=torch.bfloat16)
+    K.gemm(a.to(dev), [w.to(dev) for w in ws], [b.to(dev) for b in bs], out)
+    ref = a.float() @ torch.cat(ws).float().T + torch.cat(bs).float()
+    assert rel(out, ref) < 4e-3
+    out2 = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    K.gemm(a.to(dev), [ws[0].to(dev)], [bs[0].to(dev)], out2, epilogue=N.EPI_BIAS_GELU)
+    ref2 = F.gelu(a.float() @ ws[0].float().T + bs[0].float(), approximate="tanh")
+    assert rel(out2, ref2) < 6e-3
+    K.gemm(a.to(dev), [ws[0].to(dev)], [bs[0].to(dev)], out2, epilogue=N.EPI_BIAS_SCALE, alpha=0.37)
+    assert rel(out2, (a.float() @ ws[0].float().T + bs[0].float()) * 0.37) < 6e-3
+
+
+def test_gemm_gated_inject_and_remap():
+    from videopainter_amd import kernels as K
+    from videopainter_amd import _native as N
+    B, T, Nv, D, Kk = 2, 10, 250, 256, 512
+    Ntok = T + Nv
+    a = bf(rnd(B * Ntok, Kk, seed=30))
+    w = bf(rnd(D, Kk, std=Kk ** -0.5, seed=31))
+    b = bf(rnd(D, std=0.1, seed=32))
+    resid = bf(rnd(B, Ntok, D, seed=33))
+    mod = bf(rnd(B, 6 * D, seed=34))
+    inj = bf(rnd(B, Nv, D, seed=35))
+    tm = (torch.rand(B, Nv, generator=torch.Generator().manual_seed(3)) > 0.5).to(torch.uint8)
+    out = torch.empty(B, Ntok, D, device=dev, dtype=torch.bfloat16)
+    K.gemm(a.to(dev), [w.to(dev)], [b.to(dev)], out.view(-1, D), epilogue=N.EPI_GATED, resid=resid.to(dev),
+           mod=mod.to(dev), tokens_per_batch=Ntok, text_len=T, inject=inj.to(dev), inject_ld=D,
+           inject_bstride=Nv * D, inject_mask=tm.to(dev))
+    y = (a.float() @ w.float().T + b.float()).view(B, Ntok, D)
+    gate = mod.float()[:, 2 * D:3 * D][:, None]
+    egate = mod.float()[:, 5 * D:6 * D][:, None]
+    ref = resid.float().clone()
+    ref[:, :T] += egate * y[:, :T]
+    ref[:, T:] += gate * y[:, T:]
+    ref[:, T:] += inj.float() * (tm[..., None] == 0)
+    assert rel(out, ref) < 5e-3
+    # row remap + addrows (patch-embed video rows placed after the text rows of each batch)
+    out2 = torch.zeros(B, Ntok, D, device=dev, dtype=torch.bfloat16)
+    pos = bf(rnd(Ntok, D, seed=36))
+    a2 = bf(rnd(B * Nv, 128, seed=37))
+    w2 = bf(rnd(D, 128, std=128 ** -0.5, seed=38))
+    K.gemm(a2.to(dev), [w2.to(dev)], [b.to(dev)], out2.view(-1, D), epilogue=N.EPI_BIAS_ADDROWS, rows_per_group=Nv,
+           group_stride=Ntok, row_offset=T, addrows=pos.to(dev), addrows_offset=T)
+    ref2 = (a2.float() @ w2.float().T + b.float()).view(B, Nv, D) + pos.float()[T:]
+    assert rel(out2[:, T:], ref2) < 5e-3
+    assert float(out2[:, :T].abs().max()) == 0.0
+
+
+def _sdpa(q, k, v):
+    return F.scaled_dot_product_attention(q.float(), k.float(), v.float())
+
+
+@pytest.mark.parametrize("Nq,Nk", [(300, 300), (64, 1000), (517, 77)])
+def test_attention_random(Nq, Nk):
+    from videopainter_amd import kernels as K
+    B, H = 2, 3
+    q, k, v = (bf(rnd(B, n, H * 64, seed=s)) for s, n in ((40, Nq), (41, Nk), (42, Nk)))
+    out = torch.empty(B, Nq, H * 64, device=dev, dtype=torch.bfloat16)
+    K.attention(q.to(dev), k.to(dev), v.to(dev), out, H)
+    hd = lambda x: x.view(B, -1, H, 64).transpose(1, 2)  # noqa: E731
+    ref = _sdpa(hd(q), hd(k), hd(v)).transpose(1, 2).reshape(B, Nq, H * 64)
+    assert rel(out, ref) < 1e-2
+
+
+def test_attention_strided_qkv_and_segments_and_blend():
+    """Q/K/V read straight out of a fused [B, N, 3D] projection buffer; a second K/V segment (resample) and the
+    prev-clip blend (out = (1-w) A1 + w A2)."""
+    from videopainter_amd import kernels as K
+    B, H, Nn, N2 = 2, 2, 333, 200
+    D = H * 64
+    qkv = bf(rnd(B, Nn, 3 * D, seed=50)).to(dev)
+    k2, v2 = bf(rnd(B, N2, D, seed=51)).to(dev), bf(rnd(B, N2, D, seed=52)).to(dev)
+    q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
+    out = torch.empty(B, Nn, D, device=dev, dtype=torch.bfloat16)
+    K.attention(q, k, v, out, H, k2=k2, v2=v2)
+    hd = lambda x: x.float().cpu().reshape(B, -1, H, 64).transpose(1, 2)  # noqa: E731
+    ref = _sdpa(hd(q), torch.cat([hd(k), hd(k2)], 2), torch.cat([hd(v), hd(v2)], 2))
+    ref = ref.transpose(1, 2).reshape(B, Nn, D)
+    assert rel(out, ref) < 1e-2
+    w = 0.3
+    K.attention(q, k, v, out, H, out_scale=1 - w)
+    K.attention(q, k2, v2, out, H, out_scale=w, accumulate=True)
+    r1 = _sdpa(hd(q), hd(k), hd(v)).transpose(1, 2).reshape(B, Nn, D)
+    r2 = _sdpa(hd(q), hd(k2), hd(v2)).transpose(1, 2).reshape(B, Nn, D)
+    assert rel(out, (1 - w) * r1 + w * r2) < 1e-2
+
+
+def test_attention_forced_rescale():
+    """Spike one key so the running max jumps in a late tile (cdna_hip_programming.md §5.4 rule 26)."""
+    from videopainter_amd import kernels as K
+    B, H, Nn = 1, 1, 640
+    q = rnd(B, Nn, 64, seed=60)
+    k = rnd(B, Nn, 64, seed=61)
+    v = rnd(B, Nn, 64, seed=62)
+    k[0, 600] = q[0, :].mean(0) * 12  # large logit late in the sequence for many queries
+    k[0, 70] = -k[0, 600]
+    q, k, v = bf(q), bf(k), bf(v)
+    out = torch.empty(B, Nn, 64, device=dev, dtype=torch.bfloat16)
+    K.attention(q.to(dev), k.to(dev), v.to(dev), out, H)
+    ref = _sdpa(q[:, None], k[:, None], v[:, None])[:, 0]
+    assert rel(out, ref) < 1e-2
+
+
+def test_adaln_and_final_norm():
+    from videopainter_amd import kernels as K
+    B, T, Nv, D = 2, 7, 100, 3072
+    x = bf(rnd(B, T + Nv, D, seed=70) * 3 + 1)
+    lw, lb = bf(1 + 0.1 * rnd(D, seed=71)), bf(0.1 * rnd(D, seed=72))
+    mod = bf(rnd(B, 6 * D, seed=73) * 0.5)
+    y = K.adaln_modulate(x.to(dev), lw.to(dev), lb.to(dev), mod.to(dev), T, 1e-5)
+    n = F.layer_norm(x.float(), (D,), lw.float(), lb.float(), 1e-5)
+    m = mod.float()
+    ref = torch.empty_like(n)
+    ref[:, T:] = n[:, T:] * (1 + m[:, None, D:2 * D]) + m[:, None, 0:D]
+    ref[:, :T] = n[:, :T] * (1 + m[:, None, 4 * D:5 * D]) + m[:, None, 3 * D:4 * D]
+    assert rel(y, ref) < 8e-3
+    mod2 = bf(rnd(B, 2 * D, seed=74) * 0.5)
+    lw2, lb2 = bf(1 + 0.1 * rnd(D, seed=75)), bf(0.1 * rnd(D, seed=76))
+    z = K.final_norm(x.to(dev), T, lw.to(dev), lb.to(dev), lw2.to(dev), lb2.to(dev), 1e-5, mod2.to(dev))
+    n1 = F.layer_norm(x.float()[:, T:], (D,), lw.float(), lb.float(), 1e-5)
+    n2 = F.layer_norm(n1, (D,), lw2.float(), lb2.float(), 1e-5)
+    ref2 = n2 * (1 + mod2.float()[:, None, D:]) + mod2.float()[:, None, :D]
+    assert rel(z, ref2) < 8e-3
+
+
+def test_head_norm_rope_and_masked_null_key():
+    from videopainter_amd import kernels as K
+    from oracle.cogvideox_oracle import apply_rotary_emb, prepare_rotary_positional_embeddings
+    B, T, H = 2, 8, 2
+    cos, sin = prepare_rotary_positional_embeddings(128, 192, 3, 64)
+    Nv = cos.shape[0]
+    Ntok = T + Nv
+    x = bf(rnd(B, Ntok, 3 * H * 64, seed=80))
+    lw, lb = bf(1 + 0.1 * rnd(64, seed=81)), bf(0.1 * rnd(64, seed=82))
+    xd = x.to(dev)
+    k_in = xd[..., H * 64:2 * H * 64]
+    mask = (torch.rand(B, Ntok, generator=torch.Generator().manual_seed(4)) > 0.4).to(torch.uint8)
+    mask[:, :T] = 0
+    k2 = torch.empty(B, Ntok, H * 64, device=dev, dtype=torch.bfloat16)
+    K.head_norm_rope(k_in, k2, H, T, lw.to(dev), lb.to(dev), 1e-6, (cos.to(dev), sin.to(dev)), tok_mask=mask.to(dev),
+                     pre_scale=0.5)
+    K.head_norm_rope(k_in, k_in, H, T, lw.to(dev), lb.to(dev), 1e-6, (cos.to(dev), sin.to(dev)))
+    kr = x.float()[..., H * 64:2 * H * 64].view(B, Ntok, H, 64).transpose(1, 2)
+    n = F.layer_norm(kr, (64,), lw.float(), lb.float(), 1e-6)
+    n[:, :, T:] = apply_rotary_emb(n[:, :, T:], cos, sin)
+    ref = n.transpose(1, 2).reshape(B, Ntok, H * 64)
+    assert rel(xd[..., H * 64:2 * H * 64], ref) < 8e-3
+    km = kr * mask[:, None, :, None].float() * 0.5
+    n2 = F.layer_norm(km, (64,), lw.float(), lb.float(), 1e-6)
+    n2[:, :, T:] = apply_rotary_emb(n2[:, :, T:], cos, sin)
+    ref2 = n2.transpose(1, 2).reshape(B, Ntok, H * 64)
+    assert rel(k2, ref2) < 8e-3
+    # masked rows are the (rotated) LN bias exactly in the first text rows
+    assert torch.equal(k2[0, 0, :64].cpu(), lb)
+
+
+def test_linear_small_timestep_patchify_unpatchify_mask():
+    from videopainter_amd import kernels as K
+    from oracle.cogvideox_oracle import timestep_embedding
+    ts = torch.tensor([999, 377, 3, 0])
+    e = K.timestep_embedding(ts.to(dev), 3072)
+    assert rel(e, timestep_embedding(ts, 3072)) < 4e-3
+    x = bf(rnd(4, 512, seed=90))
+    w, b = bf(rnd(18432, 512, std=512 ** -0.5, seed=91)), bf(rnd(18432, std=0.1, seed=92))
+    y = K.linear_small(x.to(dev), w.to(dev), b.to(dev), act_in=K.ACT_SILU)
+    ref = F.linear(bf(F.silu(x.float())).float(), w.float(), b.float())
+    assert rel(y, ref) < 4e-3
+    y2 = K.linear_small(x.to(dev), w[:512].contiguous().to(dev), b[:512].contiguous().to(dev), act_out=K.ACT_SILU)
+    assert rel(y2, F.silu(F.linear(x.float(), w[:512].float(), b[:512].float()))) < 6e-3
+    B, Fr, H, W = 2, 3, 16, 24
+    s1, s2 = bf(rnd(B, Fr, 16, H, W, seed=93)), bf(rnd(B, Fr, 17, H, W, seed=94))
+    cols = K.patchify(s1.to(dev), s2.to(dev), 2, 192)
+    wconv = rnd(64, 33, 2, 2, seed=95)
+    got = cols.float().cpu()[:, :132] @ wconv.reshape(64, -1).T
+    ref = F.conv2d(torch.cat([s1, s2], 2).float().reshape(-1, 33, H, W), wconv, stride=2)
+    ref = ref.view(B, Fr, 64, -1).transpose(2, 3).reshape(-1, 64)
+    assert rel(got, ref) < 1e-5
+    assert float(cols[:, 132:].float().abs().max()) == 0.0
+    proj = bf(rnd(B * Fr * (H // 2) * (W // 2), 64, seed=96))
+    up = K.unpatchify(proj.to(dev), B, Fr, 16, H, W, 2)
+    ref = proj.reshape(B, Fr, H // 2, W // 2, -1, 2, 2).permute(0, 1, 4, 2, 5, 3, 6).flatten(5, 6).flatten(3, 4)
+    assert torch.equal(up.cpu(), ref)
+    m = (torch.rand(B, Fr, 1, H, W, generator=torch.Generator().manual_seed(5)) > 0.8).float()
+    tm = K.patch_mask(m.to(dev), 2)
+    ref = (F.avg_pool2d(m.reshape(-1, 1, H, W), 2) > 0).view(B, Fr, -1).reshape(B, -1)
+    assert torch.equal(tm.cpu().bool(), ref)

@@ -1,0 +1,79 @@
+"""Micro-benchmark of the hot kernels at config-2 shapes (B=2 CFG, N=17776, D=3072) on one MI355X.
+
+    python tools/bench_kernels.py [--iters 10]
+
+Prints TFLOP/s (algorithmic flops) per kernel and shape.  Random data (cdna_hip_programming.md §5.4 rule 25).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from videopainter_amd import kernels as K  # noqa: E402
+from videopainter_amd import _native as N  # noqa: E402
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters / 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--quick", action="store_true")
+    args = ap.parse_args()
+    dev = "cuda"
+    B, T, Nv, D, H = 2, 226, 17550, 3072, 48
+    Ntok = T + Nv
+    M = B * Ntok
+    res = {}
+    x = torch.randn(M, 4 * D, device=dev).to(torch.bfloat16)
+    shapes = [("qkv", 3 * D, D), ("out", D, D), ("ff1", 4 * D, D), ("ff2", D, 4 * D)]
+    for name, Nn, Kk in shapes:
+        w = (torch.randn(Nn, Kk, device=dev) * Kk ** -0.5).to(torch.bfloat16)
+        b = torch.randn(Nn, device=dev).to(torch.bfloat16) * 0.1
+        out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+        a = x[:, :Kk]
+        t = timeit(lambda: K.gemm(a, [w], [b], out, lda=x.stride(0)), args.iters)
+        res[f"gemm_{name}_{M}x{Nn}x{Kk}"] = dict(ms=t * 1e3, tflops=2 * M * Nn * Kk / t / 1e12)
+        print(name, res[f"gemm_{name}_{M}x{Nn}x{Kk}"], flush=True)
+    del x
+    qkv = torch.randn(B, Ntok, 3 * D, device=dev).to(torch.bfloat16)
+    o = torch.empty(B, Ntok, D, device=dev, dtype=torch.bfloat16)
+    q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
+    t = timeit(lambda: K.attention(q, k, v, o, H), max(2, args.iters // 2))
+    fl = 4 * B * H * Ntok * Ntok * 64
+    res["attention"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
+    print("attention", res["attention"], flush=True)
+    xin = torch.randn(B, Ntok, D, device=dev).to(torch.bfloat16)
+    mod = torch.randn(B, 6 * D, device=dev).to(torch.bfloat16)
+    lw = torch.ones(D, device=dev, dtype=torch.bfloat16)
+    lb = torch.zeros(D, device=dev, dtype=torch.bfloat16)
+    y = torch.empty_like(xin)
+    t = timeit(lambda: K.adaln_modulate(xin, lw, lb, mod, T, 1e-5, out=y), args.iters)
+    res["adaln"] = dict(ms=t * 1e3, gbps=2 * xin.numel() * 2 / t / 1e9)
+    print("adaln", res["adaln"], flush=True)
+    cos = torch.randn(Nv, 64, device=dev)
+    sin = torch.randn(Nv, 64, device=dev)
+    lw64 = torch.ones(64, device=dev, dtype=torch.bfloat16)
+    lb64 = torch.zeros(64, device=dev, dtype=torch.bfloat16)
+    t = timeit(lambda: K.head_norm_rope(q, q, H, T, lw64, lb64, 1e-6, (cos, sin)), args.iters)
+    res["qk_norm_rope(q)"] = dict(ms=t * 1e3, gbps=2 * B * Ntok * D * 2 / t / 1e9)
+    print("qknorm", res["qk_norm_rope(q)"], flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,121 @@
+"""ctypes binding of libvp_hip.so (the C ABI declared in include/vp_hip.h).
+
+This is the only place Python touches the native library.  There is no fallback: if the library is missing or was
+built against a different ABI, `lib()` raises — the product path never silently runs a non-HIP implementation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
+ABI_VERSION = 1
+
+vp = C.c_void_p
+i32 = C.c_int32
+i64 = C.c_int64
+f32 = C.c_float
+
+
+class GemmDesc(C.Structure):
+    _fields_ = [("M", i32), ("N", i32), ("K", i32), ("epilogue", i32),
+                ("A", vp), ("lda", i64),
+                ("W", vp * 3), ("bias", vp * 3),
+                ("n_seg", i32), ("pad0", i32),
+                ("C", vp), ("ldc", i64),
+                ("rows_per_group", i32), ("pad1", i32),
+                ("group_stride", i64), ("row_offset", i64),
+                ("alpha", f32), ("pad2", i32),
+                ("R", vp), ("ldr", i64), ("gate", vp), ("gate_text", vp), ("gate_bstride", i64),
+                ("tokens_per_batch", i32), ("text_len", i32),
+                ("inject", vp), ("inject_ld", i64), ("inject_bstride", i64), ("inject_mask", vp),
+                ("inject_mask_bstride", i64),
+                ("addrows", vp), ("addrows_ld", i64), ("addrows_offset", i64)]
+
+
+class AttnDesc(C.Structure):
+    _fields_ = [("B", i32), ("H", i32), ("Nq", i32), ("head_dim", i32),
+                ("Q", vp), ("q_sb", i64), ("q_sn", i64),
+                ("K", vp), ("V", vp), ("k_sb", i64), ("k_sn", i64), ("v_sb", i64), ("v_sn", i64),
+                ("Nk", i32), ("Nk2", i32),
+                ("K2", vp), ("V2", vp), ("k2_sb", i64), ("k2_sn", i64), ("v2_sb", i64), ("v2_sn", i64),
+                ("O", vp), ("o_sb", i64), ("o_sn", i64),
+                ("scale", f32), ("out_scale", f32), ("accumulate", i32), ("pad", i32)]
+
+
+class DpmDesc(C.Structure):
+    _fields_ = [("n", i64), ("noise_pred", vp), ("do_cfg", i32), ("guidance", f32),
+                ("sample", vp), ("old_pred", vp), ("pred_out", vp), ("noise1", vp), ("noise2", vp),
+                ("second_order", i32), ("replace_gt", i32),
+                ("sa", f32), ("sb", f32), ("m1", f32), ("m2", f32), ("mn", f32), ("m3", f32), ("m4", f32),
+                ("gt_add_noise", i32), ("mask_background", i32),
+                ("gt", vp), ("gt_noise", vp), ("mask", vp), ("gsa", f32), ("gsb", f32), ("latents_out", vp)]
+
+
+EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS = range(5)
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "vp_abi_version": (i32, []),
+    "vp_struct_sizes": (None, [C.POINTER(i64)]),
+    "vp_gemm_bf16": (i32, [C.POINTER(GemmDesc), vp]),
+    "vp_attention_fwd_bf16": (i32, [C.POINTER(AttnDesc), vp]),
+    "vp_adaln_modulate_bf16": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, f32, vp, i64, vp]),
+    "vp_head_norm_rope_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, i64,
+                                     f32, vp]),
+    "vp_mask_scale_rows_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, vp, i64, f32, vp]),
+    "vp_final_norm_bf16": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp, i64, vp]),
+    "vp_linear_small_bf16": (i32, [vp, i64, vp, vp, vp, i64, i32, i32, i32, i32, i32, vp]),
+    "vp_timestep_embedding_bf16": (i32, [vp, vp, i32, i32, f32, vp]),
+    "vp_patchify_bf16": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "vp_patch_mask": (i32, [vp, i32, vp, i32, i32, i32, i32, i32, vp]),
+    "vp_unpatchify_bf16": (i32, [vp, i64, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "vp_dpm_step_bf16": (i32, [C.POINTER(DpmDesc), vp]),
+    "vp_fill_normal_bf16": (i32, [vp, i64, C.c_uint64, f32, f32, vp]),
+}
+
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+_lock = threading.Lock()
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the native library; raise if it is missing or ABI-incompatible."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise HipLibraryError(f"{LIB_PATH} not found: build it with `python -m videopainter_amd.build` "
+                                  "(the HIP path has no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.vp_abi_version() != ABI_VERSION:
+            raise HipLibraryError(f"libvp_hip ABI {L.vp_abi_version()} != {ABI_VERSION}; rebuild")
+        sizes = (i64 * 3)()
+        L.vp_struct_sizes(sizes)
+        want = (C.sizeof(GemmDesc), C.sizeof(AttnDesc), C.sizeof(DpmDesc))
+        if tuple(sizes) != want:
+            raise HipLibraryError(f"descriptor size mismatch lib={tuple(sizes)} python={want}; rebuild")
+        _lib = L
+        return L
+
+
+_ERRS = {1000: "VP_ERR_ARG (invalid size/stride/pointer)", 1001: "VP_ERR_UNSUPPORTED"}
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {_ERRS.get(rc, f'hipError {rc}')}")

@@ -1,0 +1,171 @@
+"""The attention module and the two CogVideoX attention processors, on the HIP kernels.
+
+Secondary drop-in boundary: `Attention.set_processor` / `set_attn_processor` and the processor
+call signature `(attn, hidden_states, encoder_hidden_states, attention_mask=None, resample_mask=None,
+image_rotary_emb=None, prev_hidden_states=None, prev_clip_weight=None, prev_resample_mask=None)
+-> (hidden_states, encoder_hidden_states)` of DF/models/attention_processor.py:2107-2118 / :2223-2234.
+The processors work on any `attn` object exposing to_q/to_k/to_v/to_out[0]/norm_q/norm_k/heads (ours, or a
+reference `Attention` holding bf16 device weights).
+
+`attend()` is the fused core (QKV projection -> qk-LN + RoPE -> flash attention, everything before to_out); the
+block calls it directly so that to_out runs as one GEMM with the gated residual fused in its epilogue.
+"""
+from __future__ import annotations
+
+import inspect
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+from .modules import Dropout, LayerNorm, Linear
+
+BF16 = torch.bfloat16
+
+
+def _rope_dev(rope, device):
+    if rope is None:
+        return None
+    cos, sin = rope
+    if cos.device != device or cos.dtype != torch.float32 or not cos.is_contiguous():
+        cos = cos.to(device=device, dtype=torch.float32).contiguous()
+    if sin.device != device or sin.dtype != torch.float32 or not sin.is_contiguous():
+        sin = sin.to(device=device, dtype=torch.float32).contiguous()
+    return cos, sin
+
+
+def _u8(mask: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    if mask is None:
+        return None
+    if mask.dtype == torch.bool:
+        return mask.contiguous().view(torch.uint8)
+    return (mask != 0).to(torch.uint8).contiguous()
+
+
+class Attention(nn.Module):
+    """Parameter layout of the reference `Attention` as CogVideoXBlock builds it (attention_processor.py:96-264:
+    qk_norm="layer_norm" eps 1e-6, bias=True, out_bias=True, scale = dim_head**-0.5)."""
+
+    def __init__(self, query_dim: int, dim_head: int = 64, heads: int = 8, bias: bool = True, out_bias: bool = True,
+                 eps: float = 1e-6, processor=None):
+        super().__init__()
+        self.inner_dim = dim_head * heads
+        self.heads = heads
+        self.dim_head = dim_head
+        self.scale = dim_head ** -0.5
+        self.is_cross_attention = False
+        self.norm_q = LayerNorm(dim_head, eps=eps)
+        self.norm_k = LayerNorm(dim_head, eps=eps)
+        self.to_q = Linear(query_dim, self.inner_dim, bias=bias)
+        self.to_k = Linear(query_dim, self.inner_dim, bias=bias)
+        self.to_v = Linear(query_dim, self.inner_dim, bias=bias)
+        self.to_out = nn.ModuleList([Linear(self.inner_dim, query_dim, bias=out_bias), Dropout()])
+        self.set_processor(processor if processor is not None else CogVideoXAttnProcessor2_0())
+
+    def set_processor(self, processor) -> None:
+        self.processor = processor
+
+    def get_processor(self, return_deprecated_lora: bool = False):
+        return self.processor
+
+    def forward(self, hidden_states, encoder_hidden_states=None, attention_mask=None, **cross_attention_kwargs):
+        # kwargs the processor does not declare are dropped, as in the reference (:479-488)
+        params = set(inspect.signature(self.processor.__call__).parameters.keys())
+        kw = {k: v for k, v in cross_attention_kwargs.items() if k in params}
+        return self.processor(self, hidden_states, encoder_hidden_states=encoder_hidden_states,
+                              attention_mask=attention_mask, **kw)
+
+
+def _qkv(attn, x: torch.Tensor) -> torch.Tensor:
+    B, Ntok, D = x.shape
+    out = torch.empty(B, Ntok, 3 * attn.inner_dim if hasattr(attn, "inner_dim") else 3 * D, device=x.device,
+                      dtype=BF16)
+    K.gemm(x.reshape(-1, D), [attn.to_q.weight, attn.to_k.weight, attn.to_v.weight],
+           [attn.to_q.bias, attn.to_k.bias, attn.to_v.bias], out.view(B * Ntok, -1))
+    return out
+
+
+def _kv(attn, x: torch.Tensor) -> torch.Tensor:
+    B, Ntok, D = x.shape
+    out = torch.empty(B, Ntok, 2 * D, device=x.device, dtype=BF16)
+    K.gemm(x.reshape(-1, D), [attn.to_k.weight, attn.to_v.weight], [attn.to_k.bias, attn.to_v.bias],
+           out.view(B * Ntok, -1))
+    return out
+
+
+class CogVideoXAttnProcessor2_0:
+    """HIP restatement of `CogVideoXAttnProcessor2_0.__call__` (attention_processor.py:2107-2209)."""
+
+    def attend(self, attn, x: torch.Tensor, text_len: int, image_rotary_emb=None, prev_hidden_states=None,
+               prev_clip_weight=None, resample_mask=None, prev_resample_mask=None) -> torch.Tensor:
+        B, Ntok, D = x.shape
+        H = attn.heads
+        rope = _rope_dev(image_rotary_emb, x.device)
+        qkv = _qkv(attn, x)
+        q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
+        eps_q, eps_k = attn.norm_q.eps, attn.norm_k.eps
+        K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, eps_q, rope)
+        K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, eps_k, rope)
+        o = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
+        if prev_hidden_states is not None and prev_clip_weight is not None and prev_clip_weight > 0.0:
+            pkv = _kv(attn, prev_hidden_states.to(BF16).contiguous())
+            pk, pv = pkv[..., :D], pkv[..., D:]
+            K.head_norm_rope(pk, pk, H, text_len, attn.norm_k.weight, attn.norm_k.bias, eps_k, rope)
+            w = float(prev_clip_weight)
+            K.attention(q, k, v, o, H, scale=attn.scale, out_scale=1.0 - w)
+            K.attention(q, pk, pv, o, H, scale=attn.scale, out_scale=w, accumulate=True)
+        else:
+            K.attention(q, k, v, o, H, scale=attn.scale)
+        return o
+
+    def __call__(self, attn, hidden_states: torch.Tensor, encoder_hidden_states: torch.Tensor,
+                 attention_mask: Optional[torch.Tensor] = None, resample_mask: Optional[torch.Tensor] = None,
+                 image_rotary_emb=None, prev_hidden_states: Optional[torch.Tensor] = None,
+                 prev_clip_weight: Optional[float] = None, prev_resample_mask: Optional[torch.Tensor] = None
+                 ) -> Tuple[torch.Tensor, torch.Tensor]:
+        if attention_mask is not None:
+            raise NotImplementedError("attention_mask is never set on the CogVideoX path (SURVEY.md §3.2)")
+        t = encoder_hidden_states.size(1)
+        x = torch.cat([encoder_hidden_states, hidden_states], dim=1).to(BF16).contiguous()
+        o = self.attend(attn, x, t, image_rotary_emb, prev_hidden_states, prev_clip_weight, resample_mask,
+                        prev_resample_mask)
+        out = K.linear(o, attn.to_out[0].weight, attn.to_out[0].bias)
+        return out[:, t:], out[:, :t]
+
+
+class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
+    """HIP restatement of `CogVideoXAttnProcessor2_0_resample.__call__` (attention_processor.py:2223-2304).
+
+    The doubled K/V (cat along the sequence, :2283-2284) is not materialised: the masked copy is built once
+    (LN of the zero-masked projection -> the LN bias "null key", then RoPE) and passed to the flash kernel as a
+    second K/V segment."""
+
+    def attend(self, attn, x: torch.Tensor, text_len: int, image_rotary_emb=None, prev_hidden_states=None,
+               prev_clip_weight=None, resample_mask=None, prev_resample_mask=None) -> torch.Tensor:
+        B, Ntok, D = x.shape
+        H = attn.heads
+        rope = _rope_dev(image_rotary_emb, x.device)
+        qkv = _qkv(attn, x)
+        q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
+        k2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
+        v2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
+        if prev_hidden_states is not None and prev_clip_weight is not None and prev_clip_weight > 0.0:
+            m = _u8(prev_resample_mask)
+            pkv = _kv(attn, prev_hidden_states.to(BF16).contiguous())
+            w = float(prev_clip_weight)
+            K.head_norm_rope(pkv[..., :D], k2, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps,
+                             rope, tok_mask=m, pre_scale=w)
+            K.mask_scale_rows(pkv[..., D:], v2, m, w)
+        else:
+            if resample_mask is None:
+                raise ValueError("the resample processor needs resample_mask (id_pool_resample needs masks)")
+            m = _u8(resample_mask)
+            K.head_norm_rope(k, k2, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope,
+                             tok_mask=m, pre_scale=1.0)
+            K.mask_scale_rows(v, v2, m, 1.0)
+        K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, attn.norm_q.eps, rope)
+        K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope)
+        o = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
+        K.attention(q, k, v, o, H, k2=k2, v2=v2, scale=attn.scale)
+        return o

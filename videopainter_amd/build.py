@@ -1,0 +1,74 @@
+"""Build libvp_hip.so (gfx950) in-tree with hipcc — no JIT cache, so the .so travels with the repo snapshot.
+
+    python -m videopainter_amd.build [--force]
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import hashlib
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "_lib")
+LIB = os.path.join(LIBDIR, "libvp_hip.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-result",
+          "-Wno-unused-function", "-munsafe-fp-atomics"]
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def _digest() -> str:
+    h = hashlib.sha256()
+    for p in _sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "vp_hip.h")]:
+        with open(p, "rb") as f:
+            h.update(p.encode())
+            h.update(f.read())
+    h.update(" ".join(CFLAGS).encode())
+    return h.hexdigest()
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    stamp = os.path.join(LIBDIR, "libvp_hip.sha256")
+    dg = _digest()
+    if not force and os.path.exists(LIB) and os.path.exists(stamp) and open(stamp).read().strip() == dg:
+        return LIB
+    objs = []
+
+    def cc(src):
+        obj = os.path.join(LIBDIR, os.path.basename(src).replace(".hip", ".o"))
+        cmd = [HIPCC, *CFLAGS, "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+        return obj
+
+    jobs = max(1, min(len(_sources()), int(os.environ.get("MAX_JOBS", "8"))))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(cc, _sources()))
+    tmp = LIB + ".tmp"
+    r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], capture_output=True,
+                       text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    with open(stamp, "w") as f:
+        f.write(dg)
+    if verbose:
+        print(f"[videopainter_amd] built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

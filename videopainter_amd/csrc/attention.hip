@@ -1,0 +1,256 @@
+// Flash-attention forward for CogVideoX joint 3D attention on gfx950 (MI355X): head_dim 64, non-causal, no mask,
+// N up to ~47k tokens, optional second K/V segment (the ID-resample processor's doubled K/V, reference
+// DF/models/attention_processor.py:2283-2290) and an output blend (the prev-clip path :2177-2189).
+//
+// Layout of the math (one wave = 32 queries, one workgroup = 8 waves = 256 queries of one (batch, head)):
+//   S^T[key][q] = K · Q^T        v_mfma_f32_32x32x16_bf16, A = K rows from LDS (ds_read_b128, XOR-swizzled),
+//                                B = Q^T held in registers for the whole key loop.
+//   The accumulator has the query on the lane, so the online-softmax state (running max m, sum l) is per lane and
+//   the row max is 31 in-register fmax + one cross-half shuffle.
+//   O^T[d][q] += V^T · P^T      A = V^T read with ds_read_b64_tr_b16 (hardware transpose) from a padded V image,
+//                                B = P^T taken straight from the S^T accumulator registers (bf16-packed, with the
+//                                k-order permutation of cdna_hip_programming.md §3 "accumulator tile as operand").
+//   O^T keeps the query on the lane too, so the rescale by exp(m_old - m_new) is a per-lane scalar.
+// K/V tiles of 64 keys are double-buffered in LDS with register staging (global loads issued before the tile's
+// MFMAs, LDS writes after them; one barrier per tile).
+// Roofline: MFMA-bound in principle (4·N²·64 flop per (b,h)); at d=64 the softmax VALU (one exp per 256 MFMA
+// flops) is the co-bottleneck.
+#include "vp_common.h"
+
+namespace {
+
+constexpr int NWAVES = 8;
+constexpr int NTHREADS = NWAVES * 64;
+constexpr int QBLK = NWAVES * 32;   // 256 queries per workgroup
+constexpr int KBLK = 64;            // keys per tile
+constexpr int K_TILE_BYTES = KBLK * 128;
+constexpr int V_STRIDE = 192;       // bytes per V row in LDS (128 data + 64 pad: conflict-free transposed reads)
+constexpr int V_TILE_BYTES = KBLK * V_STRIDE;
+constexpr int STAGE_BYTES = K_TILE_BYTES + V_TILE_BYTES;
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+VP_DEV int swz(int row) { return (row >> 1) & 7; }
+
+struct Seg {
+  const bf16* k;
+  const bf16* v;
+  int64_t k_sn, v_sn;
+  int n;
+  int key0;
+};
+
+VP_DEV Seg tile_seg(const vp_attn_desc& d, int ti, int tiles1, int b, int h) {
+  Seg s;
+  if (ti < tiles1) {
+    s.k = (const bf16*)d.K + (int64_t)b * d.k_sb + h * 64;
+    s.v = (const bf16*)d.V + (int64_t)b * d.v_sb + h * 64;
+    s.k_sn = d.k_sn;
+    s.v_sn = d.v_sn;
+    s.n = d.Nk;
+    s.key0 = ti * KBLK;
+  } else {
+    s.k = (const bf16*)d.K2 + (int64_t)b * d.k2_sb + h * 64;
+    s.v = (const bf16*)d.V2 + (int64_t)b * d.v2_sb + h * 64;
+    s.k_sn = d.k2_sn;
+    s.v_sn = d.v2_sn;
+    s.n = d.Nk2;
+    s.key0 = (ti - tiles1) * KBLK;
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(NTHREADS, 2) void attn_fwd_kernel(const vp_attn_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hl = lane >> 5;  // lane half
+
+  const int nqb = (d.Nq + QBLK - 1) / QBLK;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb;
+  const int qb = t - bh * nqb;
+  const int b = bh / d.H;
+  const int h = bh - b * d.H;
+
+  const int tiles1 = (d.Nk + KBLK - 1) / KBLK;
+  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KBLK - 1) / KBLK : 0;
+  const int ntiles = tiles1 + tiles2;
+
+  // ---- Q^T fragments (B operand), 4 k-steps of 16 dims ----
+  const int q = qb * QBLK + wave * 32 + (lane & 31);
+  const int qc = q < d.Nq ? q : d.Nq - 1;
+  const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
+
+  // ---- staging assignment: one 16-byte chunk of K and one of V per thread ----
+  const int srow = tid >> 3;    // key row within tile (0..63)
+  const int schunk = tid & 7;   // 16-byte chunk within the 128-byte row
+  const int k_lds_off = srow * 128 + ((schunk ^ swz(srow)) << 4);
+  const int v_lds_off = srow * V_STRIDE + schunk * 16;
+
+  auto gload = [&](int ti, bf16x8& kr, bf16x8& vr) {
+    Seg s = tile_seg(d, ti, tiles1, b, h);
+    int key = s.key0 + srow;
+    key = key < s.n ? key : s.n - 1;
+    kr = *(const bf16x8*)(s.k + (int64_t)key * s.k_sn + schunk * 8);
+    vr = *(const bf16x8*)(s.v + (int64_t)key * s.v_sn + schunk * 8);
+  };
+
+  bf16x8 kreg, vreg;
+  gload(0, kreg, vreg);
+  *(bf16x8*)(smem + k_lds_off) = kreg;
+  *(bf16x8*)(smem + K_TILE_BYTES + v_lds_off) = vreg;
+  __syncthreads();
+
+  const float c = d.scale * 1.4426950408889634f;  // softmax in base 2
+  float m_run = -1e30f, l_run = 0.f;
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    o[0][i] = 0.f;
+    o[1][i] = 0.f;
+  }
+
+  // transposed-read address pieces (see header): group g = lane>>4, i = lane&15
+  const int g = lane >> 4;
+  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);      // key row within a 16-key step (+8 for 2nd read)
+  const int tcol = 16 * (g & 1) + 4 * (lane & 3);          // column within a 32-wide d half
+
+  for (int ti = 0; ti < ntiles; ++ti) {
+    const char* Kl = smem + (ti & 1) * STAGE_BYTES;
+    const char* Vl = Kl + K_TILE_BYTES;
+    const bool has_next = ti + 1 < ntiles;
+    if (has_next) gload(ti + 1, kreg, vreg);
+
+    // ---- S^T = K Q^T ----
+    f32x16 s[2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
+      const int row = kh * 32 + (lane & 31);
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) {
+        const int ch = ds * 2 + hl;
+        const bf16x8 kf = *(const bf16x8*)(Kl + row * 128 + ((ch ^ swz(row)) << 4));
+        s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], s[kh], 0, 0, 0);
+      }
+    }
+
+    // ---- mask the key tail of a partial tile ----
+    {
+      Seg sg = tile_seg(d, ti, tiles1, b, h);
+      if (sg.key0 + KBLK > sg.n) {
+        const int lim = sg.n - sg.key0;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = kh * 32 + (i & 3) + 8 * (i >> 2) + 4 * hl;
+            if (key >= lim) s[kh][i] = -INFINITY;
+          }
+      }
+    }
+
+    // ---- online softmax (query on the lane) ----
+    float mx = s[0][0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[0][i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+    m_run = m_new;
+    const float mc = m_new * c;
+    float psum = 0.f;
+    bf16x8 pf[4];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[kh][i], c, -mc));
+        psum += p;
+        pf[kh * 2 + (i >> 3)][i & 7] = f2bf(p);
+      }
+    l_run = l_run * alpha + psum;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o[0][i] *= alpha;
+      o[1][i] *= alpha;
+    }
+
+    // ---- O^T += V^T P^T ----
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const char* base = Vl + (ks * 16 + trow) * V_STRIDE + (dh * 32 + tcol) * 2;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * V_STRIDE));
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[ks], o[dh], 0, 0, 0);
+      }
+    }
+
+    if (has_next) {
+      char* Kn = smem + ((ti + 1) & 1) * STAGE_BYTES;
+      *(bf16x8*)(Kn + k_lds_off) = kreg;
+      *(bf16x8*)(Kn + K_TILE_BYTES + v_lds_off) = vreg;
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: O = O^T / l, query on the lane, 4 consecutive dims per register quad ----
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.f / l_tot;
+  if (q < d.Nq) {
+    bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int dd = dh * 32 + 8 * gq + 4 * hl;
+        bf16x4 ov;
+        bf16x4 old;
+        if (d.accumulate) old = *(const bf16x4*)(orow + dd);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = rbf(o[dh][4 * gq + r] * inv);
+          if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
+          if (d.accumulate) v = bf2f(old[r]) + v;
+          ov[r] = f2bf(v);
+        }
+        *(bf16x4*)(orow + dd) = ov;
+      }
+  }
+}
+
+}  // namespace
+
+extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
+  if (d == nullptr || d->Q == nullptr || d->K == nullptr || d->V == nullptr || d->O == nullptr) return VP_ERR_ARG;
+  if (d->head_dim != 64) return VP_ERR_UNSUPPORTED;
+  if (d->B <= 0 || d->H <= 0 || d->Nq <= 0 || d->Nk <= 0 || d->Nk2 < 0) return VP_ERR_ARG;
+  if (d->Nk2 > 0 && (d->K2 == nullptr || d->V2 == nullptr)) return VP_ERR_ARG;
+  if ((d->q_sn % 8) || (d->k_sn % 8) || (d->v_sn % 8) || (d->o_sn % 4) || (d->q_sb % 8) || (d->k_sb % 8) ||
+      (d->v_sb % 8) || (d->o_sb % 4))
+    return VP_ERR_ARG;
+  if (d->Nk2 > 0 && ((d->k2_sn % 8) || (d->v2_sn % 8) || (d->k2_sb % 8) || (d->v2_sb % 8))) return VP_ERR_ARG;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    attr_set = true;
+  }
+  const int nqb = (d->Nq + QBLK - 1) / QBLK;
+  const int64_t grid = (int64_t)d->B * d->H * nqb;
+  if (grid > 0x7fffffff) return VP_ERR_ARG;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)grid), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}

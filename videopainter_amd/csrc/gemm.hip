@@ -1,0 +1,217 @@
+// bf16 MFMA GEMM with fused epilogues for every projection on the CogVideoX block path (gfx950 / MI355X).
+//
+//   C[m, n] = epilogue( Σ_k A[m, k] · W[n, k] )          A: activations [M, K], W: nn.Linear weight [N, K]
+//
+// Both operands are K-contiguous, so both MFMA fragments are 16-byte row reads.  The MFMA is issued with W as the
+// A-operand and the activation as the B-operand, so each lane's accumulator holds 4 *consecutive output columns*
+// of one output row (C/D map of v_mfma_f32_16x16x32_bf16: col = lane&15 -> m, row = 4*(lane>>4)+r -> n); the
+// epilogue packs them into 8-byte LDS writes and streams the tile out as full 16-byte rows.
+//
+// Tile 256x256x64, 512 threads (8 waves = 2 (M) x 4 (N), 128x64 per wave, 8x4 16x16 fragments), 2-stage LDS ring
+// filled by global_load_lds_dwordx4 (LDS-DMA, lane-linear destination; the bank swizzle is applied on the SOURCE
+// address and undone on the read, cdna_hip_programming.md §5.4 rule 21), XCD-aware grouped tile order.
+// Roofline: MFMA-bound (AI = 2*256*256*64 flop / 64 KB staged per k-step).
+#include "vp_common.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int NTHREADS = 512;
+constexpr int WM = 128, WN = 64;
+constexpr int FM = WM / 16, FN = WN / 16;
+constexpr int TILE_BYTES = BM * BK * 2;       // 32 KB per operand tile
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;   // A + B
+constexpr int CT_STRIDE = BN * 2 + 8;         // bytes per C row in the epilogue LDS image (bank-conflict pad)
+constexpr int LDS_BYTES = (2 * STAGE_BYTES > BM * CT_STRIDE) ? 2 * STAGE_BYTES : BM * CT_STRIDE;
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void g_void;
+
+VP_DEV int swz(int row) { return (row >> 1) & 7; }
+
+// Stage one 256x64 bf16 operand tile (rows [row0, row0+256) clamped to [0, rows_valid), cols [k0, k0+64)) into
+// `tile` as [256][8 chunks of 16 B], physical chunk = logical ^ swz(row).  4 LDS-DMA instructions per wave.
+VP_DEV void stage_tile(const bf16* __restrict__ base, int64_t ld, int row0, int rows_valid, int k0, char* tile,
+                       int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rb = i * 8 + wave;              // 8-row block written by this wave instruction
+    const int r = rb * 8 + (lane >> 3);       // tile row of this lane
+    const int p = lane & 7;                   // physical chunk this lane lands in
+    const int c = p ^ swz(r);                 // logical chunk it must fetch
+    int gr = row0 + r;
+    gr = gr < rows_valid ? gr : rows_valid - 1;
+    const bf16* src = base + (int64_t)gr * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(tile + rb * 1024), 16, 0, 0);
+  }
+}
+
+VP_DEV bf16x8 lds_frag(const char* tile, int row, int chunk) {
+  return *(const bf16x8*)(tile + row * 128 + ((chunk ^ swz(row)) << 4));
+}
+
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2;  // 0..1  (M)
+  const int wc = wave & 3;   // 0..3  (N)
+
+  const int tiles_m = (d.M + BM - 1) / BM;
+  const int tiles_n = (d.N + BN - 1) / BN;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int group_id = t / per_group;
+  const int first_m = group_id * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + ((t % per_group) % gsz);
+  const int tn = (t % per_group) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // weight segment of this column tile
+  const int seg = n0 / d.n_seg;
+  const bf16* Wseg = (const bf16*)d.W[seg];
+  const bf16* bseg = (const bf16*)d.bias[seg];
+  const int nl0 = n0 - seg * d.n_seg;
+  const int n_valid_seg = min(d.n_seg, d.N - seg * d.n_seg);
+  const bf16* A = (const bf16*)d.A;
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = d.K / BK;
+  stage_tile(A, d.lda, m0, d.M, 0, smem, wave, lane);
+  stage_tile(Wseg, d.K, nl0, n_valid_seg, 0, smem + TILE_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE_BYTES;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
+      stage_tile(A, d.lda, m0, d.M, (kt + 1) * BK, nxt, wave, lane);
+      stage_tile(Wseg, d.K, nl0, n_valid_seg, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+    }
+    const char* As = cur;
+    const char* Bs = cur + TILE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[FM], wf[FN];
+      const int ch = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = lds_frag(As, wr * WM + i * 16 + (lane & 15), ch);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) wf[j] = lds_frag(Bs, wc * WN + j * 16 + (lane & 15), ch);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue phase 1: per-fragment bias / activation, bf16 into the LDS C image ----
+  const int epi = d.epilogue;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nloc = wc * WN + j * 16 + (lane >> 4) * 4;  // 4 consecutive columns
+    const int ng = nl0 + nloc;                             // column within the weight segment
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bseg != nullptr) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = (ng + r < n_valid_seg) ? bf2f(bseg[ng + r]) : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int mloc = wr * WM + i * 16 + (lane & 15);
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = rbf(acc[j][i][r] + bv[r]);
+        if (epi == VP_EPI_BIAS_GELU) v = gelu_tanh(v);
+        else if (epi == VP_EPI_BIAS_SCALE) v = v * d.alpha;
+        o[r] = f2bf(v);
+      }
+      *(bf16x4*)(smem + mloc * CT_STRIDE + nloc * 2) = o;
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue phase 2: coalesced 16-byte row stores (+ residual / gate / injection / pos-emb) ----
+  bf16* C = (bf16*)d.C;
+  const int chunk = tid & 31;         // 16-byte chunk within the 512-byte tile row
+  const int ncol = n0 + chunk * 8;
+#pragma unroll 1
+  for (int it = 0; it < BM / 16; ++it) {
+    const int mloc = it * 16 + (tid >> 5);
+    const int m = m0 + mloc;
+    if (m >= d.M || ncol >= d.N) continue;
+    bf16x8 v = *(const bf16x8*)(smem + mloc * CT_STRIDE + chunk * 16);
+    const int64_t orow = (int64_t)(m / d.rows_per_group) * d.group_stride + d.row_offset + (m % d.rows_per_group);
+    if (epi == VP_EPI_GATED) {
+      const int b = m / d.tokens_per_batch;
+      const int tok = m - b * d.tokens_per_batch;
+      const bf16* g = (const bf16*)(tok < d.text_len ? d.gate_text : d.gate) + (int64_t)b * d.gate_bstride + ncol;
+      const bf16x8 gv = *(const bf16x8*)g;
+      const bf16x8 rv = *(const bf16x8*)((const bf16*)d.R + orow * d.ldr + ncol);
+      bool inj = false;
+      bf16x8 iv;
+      if (d.inject != nullptr && tok >= d.text_len) {
+        const int vtok = tok - d.text_len;
+        inj = (d.inject_mask == nullptr) || (d.inject_mask[(int64_t)b * d.inject_mask_bstride + vtok] == 0);
+        if (inj) iv = *(const bf16x8*)((const bf16*)d.inject + (int64_t)b * d.inject_bstride +
+                                       (int64_t)vtok * d.inject_ld + ncol);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float o = rbf(bf2f(rv[e]) + rbf(bf2f(gv[e]) * bf2f(v[e])));
+        if (inj) o = rbf(o + bf2f(iv[e]));
+        v[e] = f2bf(o);
+      }
+    } else if (epi == VP_EPI_BIAS_ADDROWS) {
+      const bf16x8 pv = *(const bf16x8*)((const bf16*)d.addrows +
+                                         (int64_t)((m % d.rows_per_group) + d.addrows_offset) * d.addrows_ld + ncol);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(pv[e]));
+    }
+    *(bf16x8*)(C + orow * d.ldc + ncol) = v;
+  }
+}
+
+}  // namespace
+
+extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
+  if (d == nullptr || d->A == nullptr || d->W[0] == nullptr || d->C == nullptr) return VP_ERR_ARG;
+  if (d->M <= 0 || d->N <= 0 || d->K <= 0 || (d->K % BK) != 0 || (d->N % 8) != 0) return VP_ERR_ARG;
+  if (d->lda < d->K || d->ldc < d->N || (d->lda % 8) != 0 || (d->ldc % 8) != 0) return VP_ERR_ARG;
+  if (d->rows_per_group <= 0) return VP_ERR_ARG;
+  const int nsegs = d->W[2] ? 3 : (d->W[1] ? 2 : 1);
+  if (nsegs > 1) {
+    if (d->n_seg <= 0 || (d->n_seg % BN) != 0 || d->n_seg * nsegs != d->N) return VP_ERR_ARG;
+  } else if (d->n_seg != d->N) {
+    return VP_ERR_ARG;
+  }
+  if (d->epilogue < VP_EPI_BIAS || d->epilogue > VP_EPI_BIAS_ADDROWS) return VP_ERR_ARG;
+  if (d->epilogue == VP_EPI_GATED) {
+    if (d->R == nullptr || d->gate == nullptr || d->gate_text == nullptr || d->tokens_per_batch <= 0) return VP_ERR_ARG;
+    if ((d->ldr % 8) != 0 || (d->gate_bstride % 8) != 0) return VP_ERR_ARG;
+    if (d->inject != nullptr && ((d->inject_ld % 8) != 0 || (d->inject_bstride % 8) != 0)) return VP_ERR_ARG;
+  }
+  if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_bf16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    attr_set = true;
+  }
+  const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
+  hipLaunchKernelGGL(gemm_bf16_kernel, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}

@@ -1,0 +1,272 @@
+// Conditioning-path and data-movement kernels of the denoising step (gfx950): small-M linears (time embedding,
+// AdaLN modulation vectors), sinusoidal timestep embedding, patchify / token mask / unpatchify, the fused
+// CFG + DPM-Solver + replace-gt step glue, and a device-side synthetic-weight generator.
+#include "vp_common.h"
+
+namespace {
+
+// ---- small-M linear: y[m, n] = act_out(Σ_k act_in(x[m, k]) W[n, k] + b[n]) ----
+constexpr int LS_THREADS = 256;
+constexpr int LS_COLS_PER_WAVE = 4;
+
+__global__ __launch_bounds__(LS_THREADS) void linear_small_kernel(const bf16* __restrict__ x, int64_t ldx,
+                                                                 const bf16* __restrict__ W,
+                                                                 const bf16* __restrict__ bias, bf16* __restrict__ y,
+                                                                 int64_t ldy, int M, int N, int K, int act_in,
+                                                                 int act_out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* xs = (bf16*)smem;  // [M][K] act_in(x), bf16
+  for (int i = threadIdx.x; i < M * K; i += LS_THREADS) {
+    const int m = i / K, k = i - m * K;
+    float v = bf2f(x[(int64_t)m * ldx + k]);
+    if (act_in == 1) v = rbf(silu(v));
+    xs[i] = f2bf(v);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nch = K / 8;
+  for (int cc = 0; cc < LS_COLS_PER_WAVE; ++cc) {
+    const int n = (blockIdx.x * (LS_THREADS / 64) + wave) * LS_COLS_PER_WAVE + cc;
+    if (n >= N) break;
+    float acc[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) acc[m] = 0.f;
+    for (int c = lane; c < nch; c += 64) {
+      const bf16x8 w = *(const bf16x8*)(W + (int64_t)n * K + c * 8);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        if (m < M) {
+          const bf16x8 xv = *(const bf16x8*)(xs + m * K + c * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[m] = fmaf(bf2f(w[e]), bf2f(xv[e]), acc[m]);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if (m < M) {
+        float s = wave_sum(acc[m]);
+        if (lane == 0) {
+          float v = rbf(s + (bias ? bf2f(bias[n]) : 0.f));
+          if (act_out == 1) v = rbf(silu(v));
+          y[(int64_t)m * ldy + n] = f2bf(v);
+        }
+      }
+    }
+  }
+}
+
+// ---- get_timestep_embedding (embeddings.py:27-78), flip_sin_to_cos = True ----
+__global__ void timestep_embedding_kernel(const float* __restrict__ ts, bf16* __restrict__ out, int B, int dim,
+                                          float shift) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int half = dim / 2;
+  if (i >= B * half) return;
+  const int b = i / half, j = i - b * half;
+  const float expo = -9.210340371976184f * (float)j / ((float)half - shift);  // -ln(10000) * j / (half - shift)
+  const float freq = expf(expo);
+  const float arg = ts[b] * freq;
+  out[(int64_t)b * dim + j] = f2bf(cosf(arg));
+  out[(int64_t)b * dim + half + j] = f2bf(sinf(arg));
+}
+
+// ---- patchify: rows (b, f, y, x), cols c*p*p + dy*p + dx ----
+__global__ void patchify_kernel(const bf16* __restrict__ s1, int C1, const bf16* __restrict__ s2, int C2,
+                                bf16* __restrict__ out, int Kpad, int B, int F, int H, int W, int p) {
+  const int Hp = H / p, Wp = W / p;
+  const int C = C1 + C2;
+  const int64_t total = (int64_t)B * F * Hp * Wp * (Kpad / (p * p));
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int cslots = Kpad / (p * p);
+  const int c = (int)(i % cslots);
+  const int64_t row = i / cslots;
+  const int x = (int)(row % Wp);
+  const int yy = (int)((row / Wp) % Hp);
+  const int f = (int)((row / ((int64_t)Wp * Hp)) % F);
+  const int b = (int)(row / ((int64_t)Wp * Hp * F));
+  bf16* o = out + row * Kpad + c * p * p;
+  if (c >= C) {
+    for (int k = 0; k < p * p; ++k) o[k] = f2bf(0.f);
+    return;
+  }
+  const bf16* src = c < C1 ? s1 + (((int64_t)b * F + f) * C1 + c) * H * W
+                           : s2 + (((int64_t)b * F + f) * C2 + (c - C1)) * H * W;
+  for (int dy = 0; dy < p; ++dy)
+    for (int dx = 0; dx < p; ++dx) o[dy * p + dx] = src[(int64_t)(yy * p + dy) * W + x * p + dx];
+}
+
+__global__ void patch_mask_kernel(const void* __restrict__ mask, int is_f32, uint8_t* __restrict__ out, int B, int F,
+                                  int H, int W, int p) {
+  const int Hp = H / p, Wp = W / p;
+  const int64_t total = (int64_t)B * F * Hp * Wp;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int x = (int)(i % Wp);
+  const int yy = (int)((i / Wp) % Hp);
+  const int64_t bf = i / ((int64_t)Wp * Hp);
+  float s = 0.f;
+  for (int dy = 0; dy < p; ++dy)
+    for (int dx = 0; dx < p; ++dx) {
+      const int64_t off = bf * H * W + (int64_t)(yy * p + dy) * W + x * p + dx;
+      s += is_f32 ? ((const float*)mask)[off] : bf2f(((const bf16*)mask)[off]);
+    }
+  out[i] = (s / (float)(p * p)) > 0.f ? 1 : 0;
+}
+
+__global__ void unpatchify_kernel(const bf16* __restrict__ proj, int64_t ld, bf16* __restrict__ out, int B, int F,
+                                  int C, int H, int W, int p) {
+  const int64_t total = (int64_t)B * F * C * H * W;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int xx = (int)(i % W);
+  const int yy = (int)((i / W) % H);
+  const int c = (int)((i / ((int64_t)W * H)) % C);
+  const int64_t bf = i / ((int64_t)W * H * C);
+  const int Hp = H / p, Wp = W / p;
+  const int64_t row = bf * Hp * Wp + (int64_t)(yy / p) * Wp + (xx / p);
+  out[i] = proj[row * ld + c * p * p + (yy % p) * p + (xx % p)];
+}
+
+// ---- fused CFG + DPM step + replace-gt (see vp_hip.h) ----
+__global__ void dpm_step_kernel(const vp_dpm_desc d) {
+#pragma clang fp contract(off)  // the reference evaluates every product / sum as a separate rounded torch op
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.n) return;
+  const bf16* np = (const bf16*)d.noise_pred;
+  float mo;
+  if (d.do_cfg) {
+    const float u = bf2f(np[i]), t = bf2f(np[d.n + i]);
+    mo = u + d.guidance * (t - u);
+  } else {
+    mo = bf2f(np[i]);
+  }
+  const float x = bf2f(((const bf16*)d.sample)[i]);
+  // pred_original_sample = sqrt(a_t) * sample (bf16 op) - sqrt(1 - a_t) * model_output (fp32 op)
+  const float pred = rbf(d.sa * x) - d.sb * mo;
+  d.pred_out[i] = pred;
+  const float x1 = rbf(d.m1 * x);
+  float prev;
+  if (d.second_order) {
+    const float old = d.old_pred[i];
+    const float den = d.m3 * pred - d.m4 * old;
+    prev = (x1 - d.m2 * den) + rbf(d.mn * bf2f(((const bf16*)d.noise2)[i]));
+  } else {
+    prev = (x1 - d.m2 * pred) + rbf(d.mn * bf2f(((const bf16*)d.noise1)[i]));
+  }
+  float lat = rbf(prev);
+  if (d.replace_gt) {
+    const float g = bf2f(((const bf16*)d.gt)[i]);
+    float init = g;
+    if (d.gt_add_noise) init = rbf(rbf(d.gsa * g) + rbf(d.gsb * bf2f(((const bf16*)d.gt_noise)[i])));
+    const float m = bf2f(((const bf16*)d.mask)[i]);
+    if (d.mask_background) lat = rbf(rbf(m * init) + rbf(rbf(1.f - m) * lat));
+    else lat = rbf(rbf(rbf(1.f - m) * init) + rbf(m * lat));
+  }
+  ((bf16*)d.latents_out)[i] = f2bf(lat);
+}
+
+VP_DEV uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void fill_normal_kernel(bf16* __restrict__ out, int64_t n, uint64_t seed, float mean, float std) {
+#pragma clang fp contract(off)  // z * std + mean rounded like the numpy generator (weights.synth_param)
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t r1 = splitmix64(seed + 2ull * (uint64_t)i);
+  const uint64_t r2 = splitmix64(seed + 2ull * (uint64_t)i + 1ull);
+  const double u1 = ((double)(r1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);
+  const double u2 = (double)(r2 >> 11) * (1.0 / 9007199254740992.0);
+  const float z = (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+  out[i] = f2bf(z * std + mean);
+}
+
+}  // namespace
+
+extern "C" int vp_abi_version(void) { return VP_ABI_VERSION; }
+
+extern "C" void vp_struct_sizes(int64_t* out) {
+  out[0] = (int64_t)sizeof(vp_gemm_desc);
+  out[1] = (int64_t)sizeof(vp_attn_desc);
+  out[2] = (int64_t)sizeof(vp_dpm_desc);
+}
+
+extern "C" int vp_linear_small_bf16(const void* x, int64_t ldx, const void* W, const void* bias, void* y,
+                                    int64_t ldy, int32_t M, int32_t N, int32_t K, int32_t act_in, int32_t act_out,
+                                    void* stream) {
+  if (!x || !W || !y || M <= 0 || M > 16 || N <= 0 || K <= 0 || (K % 8) || ldx < K || ldy < N) return VP_ERR_ARG;
+  const size_t lds = (size_t)M * K * 2;
+  if (lds > 160 * 1024) return VP_ERR_ARG;
+  const int cols_per_block = (LS_THREADS / 64) * LS_COLS_PER_WAVE;
+  const int grid = (N + cols_per_block - 1) / cols_per_block;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)linear_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(linear_small_kernel, dim3(grid), dim3(LS_THREADS), lds, (hipStream_t)stream, (const bf16*)x, ldx,
+                     (const bf16*)W, (const bf16*)bias, (bf16*)y, ldy, M, N, K, act_in, act_out);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_timestep_embedding_bf16(const float* timesteps, void* out, int32_t B, int32_t dim,
+                                          float freq_shift, void* stream) {
+  if (!timesteps || !out || B <= 0 || dim <= 0 || (dim % 2)) return VP_ERR_ARG;
+  const int total = B * (dim / 2);
+  hipLaunchKernelGGL(timestep_embedding_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     timesteps, (bf16*)out, B, dim, freq_shift);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_patchify_bf16(const void* src1, int32_t C1, const void* src2, int32_t C2, void* out, int32_t Kpad,
+                                int32_t B, int32_t F, int32_t H, int32_t W, int32_t p, void* stream) {
+  if (!src1 || !out || C1 <= 0 || C2 < 0 || (C2 > 0 && !src2) || p <= 0 || (H % p) || (W % p)) return VP_ERR_ARG;
+  if (Kpad < (C1 + C2) * p * p || (Kpad % (p * p))) return VP_ERR_ARG;
+  const int64_t total = (int64_t)B * F * (H / p) * (W / p) * (Kpad / (p * p));
+  hipLaunchKernelGGL(patchify_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)src1, C1, (const bf16*)src2, C2, (bf16*)out, Kpad, B, F, H, W, p);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_patch_mask(const void* mask, int32_t mask_is_f32, uint8_t* out, int32_t B, int32_t F, int32_t H,
+                             int32_t W, int32_t p, void* stream) {
+  if (!mask || !out || p <= 0 || (H % p) || (W % p)) return VP_ERR_ARG;
+  const int64_t total = (int64_t)B * F * (H / p) * (W / p);
+  hipLaunchKernelGGL(patch_mask_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mask,
+                     mask_is_f32, out, B, F, H, W, p);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_unpatchify_bf16(const void* proj, int64_t ld, void* out, int32_t B, int32_t F, int32_t C, int32_t H,
+                                  int32_t W, int32_t p, void* stream) {
+  if (!proj || !out || p <= 0 || (H % p) || (W % p) || ld < C * p * p) return VP_ERR_ARG;
+  const int64_t total = (int64_t)B * F * C * H * W;
+  hipLaunchKernelGGL(unpatchify_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)proj, ld, (bf16*)out, B, F, C, H, W, p);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_dpm_step_bf16(const vp_dpm_desc* d, void* stream) {
+  if (!d || d->n <= 0 || !d->noise_pred || !d->sample || !d->pred_out || !d->latents_out || !d->noise1)
+    return VP_ERR_ARG;
+  if (d->second_order && (!d->old_pred || !d->noise2)) return VP_ERR_ARG;
+  if (d->replace_gt && (!d->gt || !d->mask || (d->gt_add_noise && !d->gt_noise))) return VP_ERR_ARG;
+  hipLaunchKernelGGL(dpm_step_kernel, dim3((unsigned)((d->n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *d);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float mean, float std, void* stream) {
+  if (!out || n <= 0) return VP_ERR_ARG;
+  hipLaunchKernelGGL(fill_normal_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (bf16*)out, n, seed, mean, std);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}

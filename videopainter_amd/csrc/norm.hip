@@ -1,0 +1,290 @@
+// Row normalisations on the CogVideoX block path (gfx950).  All HBM-bound: one pass over bf16 rows, 16-byte
+// vector loads/stores, fp32 statistics (two-pass mean/variance from registers, like torch's LayerNorm), bf16
+// rounding at the same points as the reference's bf16 module chain.
+#include "vp_common.h"
+
+namespace {
+
+constexpr int ROW_THREADS = 256;   // 4 waves, one row per wave
+constexpr int MAXC = 8;            // up to 8 x 16-byte chunks per lane  ->  D <= 4096
+
+// Load one row of D bf16 (D % 8 == 0) into per-lane registers, chunk c of the row handled by lane c % 64.
+struct RowRegs {
+  float v[MAXC][8];
+};
+
+VP_DEV void load_row(const bf16* row, int nch, int lane, RowRegs& r) {
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + i * 64;
+    if (c < nch) {
+      const bf16x8 x = *(const bf16x8*)(row + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r.v[i][e] = bf2f(x[e]);
+    }
+  }
+}
+
+VP_DEV void row_stats(const RowRegs& r, int nch, int lane, int D, float& mean, float& rstd, float eps) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i)
+    if (lane + i * 64 < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += r.v[i][e];
+  mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i)
+    if (lane + i * 64 < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float t = r.v[i][e] - mean;
+        q += t * t;
+      }
+  rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+}
+
+// ---- AdaLN-Zero modulate (DF/models/normalization.py:373-379) ----
+__global__ __launch_bounds__(ROW_THREADS) void adaln_modulate_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                                     int rows, int Ntok, int D, int text_len,
+                                                                     const bf16* __restrict__ lw,
+                                                                     const bf16* __restrict__ lb, float eps,
+                                                                     const bf16* __restrict__ mod, int64_t mod_bs) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int b = row / Ntok;
+  const int tok = row - b * Ntok;
+  const int nch = D / 8;
+  RowRegs r;
+  load_row(x + (int64_t)row * D, nch, lane, r);
+  float mean, rstd;
+  row_stats(r, nch, lane, D, mean, rstd, eps);
+  const bool text = tok < text_len;
+  const bf16* shift = mod + (int64_t)b * mod_bs + (text ? 3 : 0) * D;
+  const bf16* scale = mod + (int64_t)b * mod_bs + (text ? 4 : 1) * D;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + i * 64;
+    if (c < nch) {
+      const bf16x8 w = *(const bf16x8*)(lw + c * 8);
+      const bf16x8 bb = *(const bf16x8*)(lb + c * 8);
+      const bf16x8 sh = *(const bf16x8*)(shift + c * 8);
+      const bf16x8 sc = *(const bf16x8*)(scale + c * 8);
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float n = rbf((r.v[i][e] - mean) * rstd * bf2f(w[e]) + bf2f(bb[e]));
+        const float s1 = rbf(1.f + bf2f(sc[e]));
+        o[e] = f2bf(rbf(n * s1) + bf2f(sh[e]));
+      }
+      *(bf16x8*)(y + (int64_t)row * D + c * 8) = o;
+    }
+  }
+}
+
+// ---- final norm_final + norm_out (cogvideox_transformer_3d.py:617-624; normalization.py:73-85) ----
+__global__ __launch_bounds__(ROW_THREADS) void final_norm_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                                 int rows, int Nv, int Ntok, int D, int text_len,
+                                                                 const bf16* __restrict__ w1,
+                                                                 const bf16* __restrict__ b1,
+                                                                 const bf16* __restrict__ w2,
+                                                                 const bf16* __restrict__ b2, float eps,
+                                                                 const bf16* __restrict__ mod, int64_t mod_bs) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int b = row / Nv;
+  const int v = row - b * Nv;
+  const int nch = D / 8;
+  RowRegs r;
+  load_row(x + ((int64_t)b * Ntok + text_len + v) * D, nch, lane, r);
+  float mean, rstd;
+  row_stats(r, nch, lane, D, mean, rstd, eps);
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + i * 64;
+    if (c < nch) {
+      const bf16x8 w = *(const bf16x8*)(w1 + c * 8);
+      const bf16x8 bb = *(const bf16x8*)(b1 + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r.v[i][e] = rbf((r.v[i][e] - mean) * rstd * bf2f(w[e]) + bf2f(bb[e]));
+    }
+  }
+  row_stats(r, nch, lane, D, mean, rstd, eps);
+  const bf16* shift = mod + (int64_t)b * mod_bs;
+  const bf16* scale = shift + D;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int c = lane + i * 64;
+    if (c < nch) {
+      const bf16x8 w = *(const bf16x8*)(w2 + c * 8);
+      const bf16x8 bb = *(const bf16x8*)(b2 + c * 8);
+      const bf16x8 sh = *(const bf16x8*)(shift + c * 8);
+      const bf16x8 sc = *(const bf16x8*)(scale + c * 8);
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float n = rbf((r.v[i][e] - mean) * rstd * bf2f(w[e]) + bf2f(bb[e]));
+        o[e] = f2bf(rbf(n * rbf(1.f + bf2f(sc[e]))) + bf2f(sh[e]));
+      }
+      *(bf16x8*)(y + (int64_t)row * D + c * 8) = o;
+    }
+  }
+}
+
+// ---- per-head LN(64) + RoPE (attention_processor.py:2143-2154; embeddings.py:655-701) ----
+// 8 lanes per 64-wide head vector (8 elements each); 32 vectors per 256-thread block.
+__global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restrict__ xin, int64_t ld_in,
+                                                            int64_t bs_in, bf16* __restrict__ xout, int64_t ld_out,
+                                                            int64_t bs_out, int64_t nvec, int Ntok, int H,
+                                                            int text_len, const bf16* __restrict__ lw,
+                                                            const bf16* __restrict__ lb, float eps,
+                                                            const float* __restrict__ cosp,
+                                                            const float* __restrict__ sinp,
+                                                            const uint8_t* __restrict__ tok_mask, int64_t mask_bs,
+                                                            float pre_scale) {
+  const int64_t vec = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const int sub = threadIdx.x & 7;
+  const bool valid = vec < nvec;
+  const int64_t vv = valid ? vec : nvec - 1;
+  const int h = (int)(vv % H);
+  const int64_t bn = vv / H;
+  const int n = (int)(bn % Ntok);
+  const int b = (int)(bn / Ntok);
+  const bf16x8 xr = *(const bf16x8*)(xin + (int64_t)b * bs_in + (int64_t)n * ld_in + h * 64 + sub * 8);
+  float x[8];
+  float m = 1.f;
+  if (tok_mask != nullptr) m = tok_mask[(int64_t)b * mask_bs + n] ? 1.f : 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float t = bf2f(xr[e]);
+    if (tok_mask != nullptr) t = rbf(rbf(t * m) * pre_scale);
+    x[e] = t;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s += x[e];
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  const float mean = s * (1.f / 64.f);
+  float q = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float t = x[e] - mean;
+    q += t * t;
+  }
+  q += __shfl_xor(q, 1, 64);
+  q += __shfl_xor(q, 2, 64);
+  q += __shfl_xor(q, 4, 64);
+  const float rstd = rsqrtf(q * (1.f / 64.f) + eps);
+  const bf16x8 w = *(const bf16x8*)(lw + sub * 8);
+  const bf16x8 bb = *(const bf16x8*)(lb + sub * 8);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = rbf((x[e] - mean) * rstd * bf2f(w[e]) + bf2f(bb[e]));
+  if (cosp != nullptr && n >= text_len) {
+    const float* cr = cosp + (int64_t)(n - text_len) * 64 + sub * 8;
+    const float* sr = sinp + (int64_t)(n - text_len) * 64 + sub * 8;
+    const f32x4 c0 = *(const f32x4*)cr, c1 = *(const f32x4*)(cr + 4);
+    const f32x4 s0 = *(const f32x4*)sr, s1 = *(const f32x4*)(sr + 4);
+    const float cs[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+    const float sn[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    float y[8];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      y[e] = x[e] * cs[e] + (-x[e + 1]) * sn[e];
+      y[e + 1] = x[e + 1] * cs[e + 1] + x[e] * sn[e + 1];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = y[e];
+  }
+  if (valid) {
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(x[e]);
+    *(bf16x8*)(xout + (int64_t)b * bs_out + (int64_t)n * ld_out + h * 64 + sub * 8) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void mask_scale_rows_kernel(const bf16* __restrict__ xin, int64_t ld_in,
+                                                             int64_t bs_in, bf16* __restrict__ y, int64_t ld_out,
+                                                             int64_t bs_out, int64_t nchunks, int Ntok, int D,
+                                                             const uint8_t* __restrict__ tok_mask, int64_t mask_bs,
+                                                             float scale) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nchunks) return;
+  const int cpr = D / 8;
+  const int c = (int)(i % cpr);
+  const int64_t bn = i / cpr;
+  const int n = (int)(bn % Ntok);
+  const int b = (int)(bn / Ntok);
+  const float m = tok_mask[(int64_t)b * mask_bs + n] ? 1.f : 0.f;
+  const bf16x8 x = *(const bf16x8*)(xin + (int64_t)b * bs_in + (int64_t)n * ld_in + c * 8);
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = f2bf(rbf(rbf(bf2f(x[e]) * m) * scale));
+  *(bf16x8*)(y + (int64_t)b * bs_out + (int64_t)n * ld_out + c * 8) = o;
+}
+
+}  // namespace
+
+extern "C" int vp_adaln_modulate_bf16(const void* x, void* y, int32_t B, int32_t Ntok, int32_t D, int32_t text_len,
+                                      const void* ln_w, const void* ln_b, float eps, const void* mod,
+                                      int64_t mod_bstride, void* stream) {
+  if (!x || !y || !ln_w || !ln_b || !mod || B <= 0 || Ntok <= 0 || D <= 0 || (D % 8) || D > MAXC * 512)
+    return VP_ERR_ARG;
+  if (mod_bstride % 8) return VP_ERR_ARG;
+  const int rows = B * Ntok;
+  const int grid = (rows + 3) / 4;
+  hipLaunchKernelGGL(adaln_modulate_kernel, dim3(grid), dim3(ROW_THREADS), 0, (hipStream_t)stream, (const bf16*)x,
+                     (bf16*)y, rows, Ntok, D, text_len, (const bf16*)ln_w, (const bf16*)ln_b, eps, (const bf16*)mod,
+                     mod_bstride);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_final_norm_bf16(const void* x, void* y, int32_t B, int32_t Ntok, int32_t D, int32_t text_len,
+                                  const void* ln1_w, const void* ln1_b, const void* ln2_w, const void* ln2_b,
+                                  float eps, const void* mod, int64_t mod_bstride, void* stream) {
+  if (!x || !y || !ln1_w || !ln1_b || !ln2_w || !ln2_b || !mod) return VP_ERR_ARG;
+  if (B <= 0 || Ntok <= text_len || D <= 0 || (D % 8) || D > MAXC * 512 || (mod_bstride % 8)) return VP_ERR_ARG;
+  const int Nv = Ntok - text_len;
+  const int rows = B * Nv;
+  hipLaunchKernelGGL(final_norm_kernel, dim3((rows + 3) / 4), dim3(ROW_THREADS), 0, (hipStream_t)stream,
+                     (const bf16*)x, (bf16*)y, rows, Nv, Ntok, D, text_len, (const bf16*)ln1_w, (const bf16*)ln1_b,
+                     (const bf16*)ln2_w, (const bf16*)ln2_b, eps, (const bf16*)mod, mod_bstride);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_head_norm_rope_bf16(const void* x_in, int64_t ld_in, int64_t bs_in, void* x_out, int64_t ld_out,
+                                      int64_t bs_out, int32_t B, int32_t Ntok, int32_t H, int32_t text_len,
+                                      const void* ln_w, const void* ln_b, float eps, const float* cos,
+                                      const float* sin, const uint8_t* tok_mask, int64_t mask_bstride,
+                                      float pre_scale, void* stream) {
+  if (!x_in || !x_out || !ln_w || !ln_b || B <= 0 || Ntok <= 0 || H <= 0) return VP_ERR_ARG;
+  if ((ld_in % 8) || (ld_out % 8) || (bs_in % 8) || (bs_out % 8)) return VP_ERR_ARG;
+  if ((cos == nullptr) != (sin == nullptr)) return VP_ERR_ARG;
+  const int64_t nvec = (int64_t)B * Ntok * H;
+  const int64_t grid = (nvec + 31) / 32;
+  hipLaunchKernelGGL(head_norm_rope_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)x_in, ld_in, bs_in, (bf16*)x_out, ld_out, bs_out, nvec, Ntok, H, text_len,
+                     (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, tok_mask, mask_bstride, pre_scale);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_mask_scale_rows_bf16(const void* x_in, int64_t ld_in, int64_t bs_in, void* y, int64_t ld_out,
+                                       int64_t bs_out, int32_t B, int32_t Ntok, int32_t D, const uint8_t* tok_mask,
+                                       int64_t mask_bstride, float scale, void* stream) {
+  if (!x_in || !y || !tok_mask || B <= 0 || Ntok <= 0 || D <= 0 || (D % 8)) return VP_ERR_ARG;
+  if ((ld_in % 8) || (ld_out % 8) || (bs_in % 8) || (bs_out % 8)) return VP_ERR_ARG;
+  const int64_t nchunks = (int64_t)B * Ntok * (D / 8);
+  hipLaunchKernelGGL(mask_scale_rows_kernel, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const bf16*)x_in, ld_in, bs_in, (bf16*)y, ld_out, bs_out, nchunks, Ntok,
+                     D, tok_mask, mask_bstride, scale);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}

@@ -1,0 +1,280 @@
+"""Torch-tensor front end of the HIP kernels (thin: validate, take pointers + current stream, call the C ABI).
+
+Tensors are plumbing here — device memory and streams.  Every arithmetic op on the hot path runs in libvp_hip.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import torch
+
+from . import _native as N
+
+BF16 = torch.bfloat16
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _chk(t: torch.Tensor, name: str, dtype=BF16):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a CUDA/HIP device tensor")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+
+
+def _rowmajor(t: torch.Tensor, name: str) -> int:
+    """Return the row stride of a 2-D (or last-dim-contiguous) tensor viewed as rows."""
+    if t.stride(-1) != 1:
+        raise ValueError(f"{name} must have a contiguous last dimension")
+    return t.stride(-2) if t.dim() >= 2 else t.shape[-1]
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# GEMM
+# ------------------------------------------------------------------------------------------------------------------
+
+def gemm(a: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[Optional[torch.Tensor]],
+         out: torch.Tensor, *, epilogue: int = N.EPI_BIAS, M: Optional[int] = None, lda: Optional[int] = None,
+         ldc: Optional[int] = None, rows_per_group: Optional[int] = None, group_stride: int = 0, row_offset: int = 0,
+         alpha: float = 1.0, resid: Optional[torch.Tensor] = None, ldr: Optional[int] = None,
+         mod: Optional[torch.Tensor] = None, gate_chunk: int = 2, gate_text_chunk: int = 5,
+         tokens_per_batch: int = 1, text_len: int = 0, inject: Optional[torch.Tensor] = None,
+         inject_ld: int = 0, inject_bstride: int = 0, inject_mask: Optional[torch.Tensor] = None,
+         addrows: Optional[torch.Tensor] = None, addrows_offset: int = 0) -> torch.Tensor:
+    """out = epilogue(a @ cat(weights).T).  `a` rows: M rows of length K at stride lda."""
+    _chk(a, "a")
+    _chk(out, "out")
+    K = weights[0].shape[1]
+    nseg = weights[0].shape[0]
+    for w in weights:
+        _chk(w, "weight")
+        if w.shape != weights[0].shape or not w.is_contiguous():
+            raise ValueError("weight segments must be contiguous and of equal shape")
+    Ntot = nseg * len(weights)
+    M = a.numel() // a.shape[-1] if M is None else M
+    lda = _rowmajor(a, "a") if lda is None else lda
+    if a.shape[-1] < K:
+        raise ValueError(f"a has K={a.shape[-1]} < weight K={K}")
+    d = N.GemmDesc()
+    d.M, d.N, d.K, d.epilogue = M, Ntot, K, epilogue
+    d.A, d.lda = _p(a), lda
+    for i, w in enumerate(weights):
+        d.W[i] = _p(w)
+        b = biases[i] if biases is not None and i < len(biases) else None
+        if b is not None:
+            _chk(b, "bias")
+        d.bias[i] = _p(b)
+    d.n_seg = nseg
+    d.C = _p(out)
+    d.ldc = _rowmajor(out, "out") if ldc is None else ldc
+    d.rows_per_group = M if rows_per_group is None else rows_per_group
+    d.group_stride, d.row_offset = group_stride, row_offset
+    d.alpha = alpha
+    if epilogue == N.EPI_GATED:
+        _chk(resid, "resid")
+        _chk(mod, "mod")
+        D = Ntot
+        d.R = _p(resid)
+        d.ldr = _rowmajor(resid, "resid") if ldr is None else ldr
+        d.gate = mod.data_ptr() + gate_chunk * D * mod.element_size()
+        d.gate_text = mod.data_ptr() + gate_text_chunk * D * mod.element_size()
+        d.gate_bstride = mod.stride(0)
+        d.tokens_per_batch, d.text_len = tokens_per_batch, text_len
+        if inject is not None:
+            _chk(inject, "inject")
+            d.inject, d.inject_ld, d.inject_bstride = _p(inject), inject_ld, inject_bstride
+            if inject_mask is not None:
+                _chk(inject_mask, "inject_mask", torch.uint8)
+                d.inject_mask = _p(inject_mask)
+                d.inject_mask_bstride = inject_mask.stride(0)
+    if epilogue == N.EPI_BIAS_ADDROWS:
+        _chk(addrows, "addrows")
+        d.addrows, d.addrows_ld, d.addrows_offset = _p(addrows), _rowmajor(addrows, "addrows"), addrows_offset
+    N.check(N.lib().vp_gemm_bf16(C.byref(d), _stream()), "vp_gemm_bf16")
+    return out
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
+           gelu: bool = False, scale: Optional[float] = None) -> torch.Tensor:
+    """nn.Linear (+ GELU-tanh, + output scale) on the last dim of a contiguous activation."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if out is None:
+        out = torch.empty(*x.shape[:-1], weight.shape[0], device=x.device, dtype=BF16)
+    epi = N.EPI_BIAS_GELU if gelu else (N.EPI_BIAS_SCALE if scale is not None and scale != 1.0 else N.EPI_BIAS)
+    gemm(x2, [weight], [bias], out.view(-1, weight.shape[0]), epilogue=epi, alpha=1.0 if scale is None else scale)
+    return out
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# attention
+# ------------------------------------------------------------------------------------------------------------------
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, heads: int, *,
+              k2: Optional[torch.Tensor] = None, v2: Optional[torch.Tensor] = None, scale: float = 0.125,
+              out_scale: float = 1.0, accumulate: bool = False) -> torch.Tensor:
+    """q, k, v, out: [B, N, heads*64] views (last dim contiguous, any row/batch stride)."""
+    for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
+        _chk(t, n)
+        if t.dim() != 3 or t.stride(-1) != 1 or t.shape[-1] != heads * 64:
+            raise ValueError(f"{n} must be [B, N, heads*64] with a contiguous last dim, got {tuple(t.shape)}")
+    d = N.AttnDesc()
+    d.B, d.H, d.Nq, d.head_dim = q.shape[0], heads, q.shape[1], 64
+    d.Q, d.q_sb, d.q_sn = _p(q), q.stride(0), q.stride(1)
+    d.K, d.V = _p(k), _p(v)
+    d.k_sb, d.k_sn, d.v_sb, d.v_sn = k.stride(0), k.stride(1), v.stride(0), v.stride(1)
+    d.Nk = k.shape[1]
+    if v.shape[1] != k.shape[1]:
+        raise ValueError("k and v lengths differ")
+    if k2 is not None:
+        _chk(k2, "k2")
+        _chk(v2, "v2")
+        d.K2, d.V2 = _p(k2), _p(v2)
+        d.k2_sb, d.k2_sn, d.v2_sb, d.v2_sn = k2.stride(0), k2.stride(1), v2.stride(0), v2.stride(1)
+        d.Nk2 = k2.shape[1]
+    d.O, d.o_sb, d.o_sn = _p(out), out.stride(0), out.stride(1)
+    d.scale, d.out_scale, d.accumulate = scale, out_scale, int(accumulate)
+    N.check(N.lib().vp_attention_fwd_bf16(C.byref(d), _stream()), "vp_attention_fwd_bf16")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# norms
+# ------------------------------------------------------------------------------------------------------------------
+
+def adaln_modulate(x: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, mod: torch.Tensor, text_len: int,
+                   eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _chk(x, "x")
+    if not x.is_contiguous():
+        raise ValueError("x must be contiguous [B, N, D]")
+    B, Ntok, D = x.shape
+    out = torch.empty_like(x) if out is None else out
+    N.check(N.lib().vp_adaln_modulate_bf16(_p(x), _p(out), B, Ntok, D, text_len, _p(ln_w), _p(ln_b), eps, _p(mod),
+                                           mod.stride(0), _stream()), "vp_adaln_modulate_bf16")
+    return out
+
+
+def head_norm_rope(x_in: torch.Tensor, x_out: torch.Tensor, heads: int, text_len: int, ln_w, ln_b, eps: float,
+                   rope=None, tok_mask: Optional[torch.Tensor] = None, pre_scale: float = 1.0) -> torch.Tensor:
+    """x_in / x_out: [B, N, heads*64] views with contiguous last dim."""
+    _chk(x_in, "x_in")
+    _chk(x_out, "x_out")
+    B, Ntok, _ = x_in.shape
+    cos = sin = None
+    if rope is not None:
+        cos, sin = rope
+        _chk(cos, "cos", torch.float32)
+        _chk(sin, "sin", torch.float32)
+        if cos.shape[0] != Ntok - text_len or cos.shape[1] != 64 or not cos.is_contiguous() or not sin.is_contiguous():
+            raise ValueError(f"rope tables must be fp32 [{Ntok - text_len}, 64], got {tuple(cos.shape)}")
+    mb = 0
+    if tok_mask is not None:
+        _chk(tok_mask, "tok_mask", torch.uint8)
+        mb = tok_mask.stride(0)
+    N.check(N.lib().vp_head_norm_rope_bf16(_p(x_in), x_in.stride(1), x_in.stride(0), _p(x_out), x_out.stride(1),
+                                           x_out.stride(0), B, Ntok, heads, text_len, _p(ln_w), _p(ln_b), eps,
+                                           _p(cos), _p(sin), _p(tok_mask), mb, pre_scale, _stream()),
+            "vp_head_norm_rope_bf16")
+    return x_out
+
+
+def mask_scale_rows(x_in: torch.Tensor, out: torch.Tensor, tok_mask: torch.Tensor, scale: float) -> torch.Tensor:
+    _chk(x_in, "x_in")
+    _chk(out, "out")
+    _chk(tok_mask, "tok_mask", torch.uint8)
+    B, Ntok, D = x_in.shape
+    N.check(N.lib().vp_mask_scale_rows_bf16(_p(x_in), x_in.stride(1), x_in.stride(0), _p(out), out.stride(1),
+                                            out.stride(0), B, Ntok, D, _p(tok_mask), tok_mask.stride(0), scale,
+                                            _stream()), "vp_mask_scale_rows_bf16")
+    return out
+
+
+def final_norm(x: torch.Tensor, text_len: int, ln1_w, ln1_b, ln2_w, ln2_b, eps: float, mod: torch.Tensor,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _chk(x, "x")
+    B, Ntok, D = x.shape
+    out = torch.empty(B, Ntok - text_len, D, device=x.device, dtype=BF16) if out is None else out
+    N.check(N.lib().vp_final_norm_bf16(_p(x), _p(out), B, Ntok, D, text_len, _p(ln1_w), _p(ln1_b), _p(ln2_w),
+                                       _p(ln2_b), eps, _p(mod), mod.stride(0), _stream()), "vp_final_norm_bf16")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# conditioning path / data movement / step glue
+# ------------------------------------------------------------------------------------------------------------------
+
+ACT_NONE, ACT_SILU = 0, 1
+
+
+def linear_small(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], act_in: int = ACT_NONE,
+                 act_out: int = ACT_NONE, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _chk(x, "x")
+    _chk(weight, "weight")
+    M, K = x.shape
+    Nn = weight.shape[0]
+    out = torch.empty(M, Nn, device=x.device, dtype=BF16) if out is None else out
+    N.check(N.lib().vp_linear_small_bf16(_p(x), x.stride(0), _p(weight), _p(bias), _p(out), out.stride(0), M, Nn, K,
+                                         act_in, act_out, _stream()), "vp_linear_small_bf16")
+    return out
+
+
+def timestep_embedding(timesteps: torch.Tensor, dim: int, freq_shift: float = 0.0) -> torch.Tensor:
+    ts = timesteps.to(dtype=torch.float32).contiguous()
+    _chk(ts, "timesteps", torch.float32)
+    out = torch.empty(ts.shape[0], dim, device=ts.device, dtype=BF16)
+    N.check(N.lib().vp_timestep_embedding_bf16(_p(ts), _p(out), ts.shape[0], dim, freq_shift, _stream()),
+            "vp_timestep_embedding_bf16")
+    return out
+
+
+def patchify(src1: torch.Tensor, src2: Optional[torch.Tensor], p: int, kpad: int) -> torch.Tensor:
+    _chk(src1, "src1")
+    B, F, C1, H, W = src1.shape
+    C2 = 0
+    if src2 is not None:
+        _chk(src2, "src2")
+        C2 = src2.shape[2]
+        if src2.shape[:2] != src1.shape[:2] or src2.shape[3:] != src1.shape[3:]:
+            raise ValueError("branch_cond must match hidden_states in batch/frames/height/width")
+    out = torch.empty(B * F * (H // p) * (W // p), kpad, device=src1.device, dtype=BF16)
+    N.check(N.lib().vp_patchify_bf16(_p(src1), C1, _p(src2), C2, _p(out), kpad, B, F, H, W, p, _stream()),
+            "vp_patchify_bf16")
+    return out
+
+
+def patch_mask(mask: torch.Tensor, p: int) -> torch.Tensor:
+    if mask.dtype not in (torch.float32, BF16):
+        mask = mask.to(torch.float32)
+    mask = mask.contiguous()
+    B, F, _, H, W = mask.shape
+    out = torch.empty(B, F * (H // p) * (W // p), device=mask.device, dtype=torch.uint8)
+    N.check(N.lib().vp_patch_mask(_p(mask), int(mask.dtype == torch.float32), _p(out), B, F, H, W, p, _stream()),
+            "vp_patch_mask")
+    return out
+
+
+def unpatchify(proj: torch.Tensor, B: int, F: int, Cout: int, H: int, W: int, p: int) -> torch.Tensor:
+    _chk(proj, "proj")
+    out = torch.empty(B, F, Cout, H, W, device=proj.device, dtype=BF16)
+    N.check(N.lib().vp_unpatchify_bf16(_p(proj), proj.stride(0), _p(out), B, F, Cout, H, W, p, _stream()),
+            "vp_unpatchify_bf16")
+    return out
+
+
+def dpm_step(desc: "N.DpmDesc") -> None:
+    N.check(N.lib().vp_dpm_step_bf16(C.byref(desc), _stream()), "vp_dpm_step_bf16")
+
+
+def fill_normal_(t: torch.Tensor, seed: int, mean: float = 0.0, std: float = 1.0) -> torch.Tensor:
+    _chk(t, "t")
+    if not t.is_contiguous():
+        raise ValueError("fill target must be contiguous")
+    N.check(N.lib().vp_fill_normal_bf16(_p(t), t.numel(), seed & 0xFFFFFFFFFFFFFFFF, mean, std, _stream()),
+            "vp_fill_normal_bf16")
+    return t

@@ -38,9 +38,14 @@ def _splitmix64(x: np.ndarray) -> np.ndarray:
         return z ^ (z >> np.uint64(31))
 
 
+def counter_seed(key: str, seed: int = 0) -> int:
+    """64-bit stream base for (key, seed); the device generator (`vp_fill_normal_bf16`) uses the same base."""
+    return (_fnv1a64(key) ^ ((seed * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF)) & 0xFFFFFFFFFFFFFFFF
+
+
 def counter_normal(key: str, n: int, seed: int = 0) -> np.ndarray:
     """n standard normals (float32), a pure function of (key, seed, index)."""
-    base = np.uint64((_fnv1a64(key) ^ ((seed * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF)) & 0xFFFFFFFFFFFFFFFF)
+    base = np.uint64(counter_seed(key, seed))
     out = np.empty(n, dtype=np.float32)
     chunk = 1 << 22
     for s in range(0, n, chunk):
