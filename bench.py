@@ -1,0 +1,226 @@
+"""Denoising steps/s of the VideoPainter hot path on MI355X (BASELINE.json config 2, data-parallel clips for N>1).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--cpu-baseline-only]
+    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+
+One step = one iteration of the any-length pipeline's denoising loop (anyl.py:933-1034): 2-layer branch forward +
+42-layer CogVideoX-5b-I2V transformer forward at B=2 (CFG) with return_hidden_states / resample mask as the pipeline
+requests them, then the fused CFG + DPM-Solver + replace-gt kernel.  Random-init weights of the 5b-I2V architecture
+(no checkpoints offline), synthetic latents of the 49f 480x720 shape (latent 13x60x90, N = 226 + 17550 tokens).
+N GPUs: each rank runs its own clip (weak scaling, no per-step collective); weights are initialised on rank 0 and
+broadcast over RCCL (config 3).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "denoising steps/sec, CogVideoX-5b+branch 49f 480×720, 1→8 MI355X; MFMA util%"
+PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA peak, MI355X_MICROARCH.md
+B, T, F, HL, WL, D, H, L, LB = 2, 226, 13, 60, 90, 3072, 48, 42, 2
+NV = F * (HL // 2) * (WL // 2)
+NTOK = T + NV
+
+
+def step_flops() -> float:
+    """Algorithmic FLOP per denoising step: transformer + branch at B=2."""
+    blk = 24 * NTOK * D * D + 4 * NTOK * NTOK * D
+    tr = B * (L * blk + 2 * NV * 128 * D + 2 * T * 4096 * D + 2 * NV * D * 64)
+    br = B * (LB * blk + 2 * NV * 132 * D + 2 * T * 4096 * D + LB * 2 * NTOK * D * D)
+    return float(tr + br)
+
+
+def attn_flops_per_launch() -> float:
+    return 4.0 * B * H * NTOK * NTOK * 64
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(seconds_budget: float = 30.0) -> dict:
+    """The oracle (plain PyTorch CPU restatement of the reference) on this host's cores: one full-size
+    CogVideoXBlock forward at B=2, N=17776 in bf16 (the reference's inference dtype), extrapolated to a step as
+    (42 + 2) block-forwards (blocks are >99% of the step's FLOPs)."""
+    from oracle import cogvideox_oracle as O
+    from videopainter_amd.config import block_shapes
+    threads = torch.get_num_threads()
+    g = torch.Generator().manual_seed(0)
+    sd = {}
+    for k, shp in block_shapes(D, 512).items():
+        std = 0.02 if len(shp) == 1 else (1.0 / math.sqrt(shp[1]))
+        sd["b." + k] = (torch.randn(shp, generator=g) * std + (1.0 if (len(shp) == 1 and ".norm" in k and
+                                                                        k.endswith("weight")) else 0.0)).bfloat16()
+    for n in ("norm_q", "norm_k"):
+        sd[f"b.attn1.{n}.weight"] = torch.ones(64, dtype=torch.bfloat16)
+        sd[f"b.attn1.{n}.bias"] = torch.zeros(64, dtype=torch.bfloat16)
+    h = torch.randn(B, NV, D, generator=g).bfloat16()
+    e = torch.randn(B, T, D, generator=g).bfloat16()
+    temb = torch.randn(B, 512, generator=g).bfloat16()
+    rope = O.prepare_rotary_positional_embeddings(480, 720, F, 64)
+    t0 = time.time()
+    with torch.no_grad():
+        O.block_forward(sd, "b", dict(num_attention_heads=H, norm_eps=1e-5), h, e, temb, rope)
+    dt = time.time() - t0
+    step_s = (L + LB) * dt
+    return {"value": 1.0 / step_s, "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (plain PyTorch CPU restatement) bf16: 1 full CogVideoXBlock fwd at B=2, N={NTOK} took "
+                      f"{dt:.1f}s on {threads} threads; step = (42+2) block-forwards = {step_s:.0f}s"}
+
+
+def build_models(device, seed: int, rank: int, world: int):
+    from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, device_scope
+    from videopainter_amd.config import COGVIDEOX_5B_I2V
+    with device_scope(device):
+        tr = CogVideoXTransformer3DModel(**COGVIDEOX_5B_I2V)
+        br = CogvideoXBranchModel(**dict(COGVIDEOX_5B_I2V, num_layers=LB))
+    if rank == 0 or world == 1:
+        tr.init_synthetic_weights_(seed)
+        br.init_synthetic_weights_(seed + 1)
+    if world > 1:
+        import torch.distributed as dist
+        for m in (tr, br):
+            for p in m.state_dict().values():
+                dist.broadcast(p, src=0)
+    torch.cuda.synchronize()
+    return tr, br
+
+
+def make_state(harness, device, seed: int):
+    """Synthetic config-2 window inputs: N(0,1) latents, image latent frame 0 only, centred
+    50% x 50% mask with frame 0 unmasked (first_frame_gt), masked latents zeroed inside the mask."""
+    g = torch.Generator().manual_seed(seed)
+    lat = torch.randn(1, F, 16, HL, WL, generator=g)
+    img = torch.zeros(1, F, 16, HL, WL)
+    img[:, 0] = torch.randn(1, 16, HL, WL, generator=g) * 0.7
+    mask = torch.zeros(1, 1, F, HL, WL)
+    mask[:, :, 1:, HL // 4:HL // 4 + HL // 2, WL // 4:WL // 4 + WL // 2] = 1.0
+    vid = torch.randn(1, F, 16, HL, WL, generator=g)
+    masked = vid * (1 - mask.permute(0, 2, 1, 3, 4))
+    st = harness.make_window(lat, img, torch.cat([masked] * 2), torch.cat([mask] * 2), vid, lat.clone())
+    pe = torch.randn(2, T, 4096, generator=g).to(device, torch.bfloat16)
+    return st, pe
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-only", action="store_true")
+    args = ap.parse_args()
+
+    if args.cpu_baseline_only:
+        print(json.dumps({"cpu_baseline": cpu_baseline()}))
+        return
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+
+    from videopainter_amd import kernels as K
+    from videopainter_amd.pipeline import CogVideoXI2VDualInpaintAnyLHarness
+    from videopainter_amd.scheduler import CogVideoXDPMScheduler
+
+    t_setup = time.time()
+    tr, br = build_models(device, 1234, rank, world)
+    sch = CogVideoXDPMScheduler(snr_shift_scale=1.0, prediction_type="v_prediction", rescale_betas_zero_snr=True,
+                                clip_sample=False, set_alpha_to_one=True, timestep_spacing="trailing")
+    sch.set_timesteps(50)
+    timesteps = sch.timesteps.cpu()
+    harness = CogVideoXI2VDualInpaintAnyLHarness(tr, br, sch)
+    st, pe = make_state(harness, device, 42 + rank)
+    rope = harness.rope_for(F, HL, WL)
+    gen = torch.Generator().manual_seed(42 + rank)
+    log(f"[bench] setup {time.time() - t_setup:.1f}s; rank {rank}/{world}")
+
+    def one(i):
+        k = i % len(timesteps)
+        if k == 0:
+            st.old_pred = None
+        harness.step(st, k, timesteps, pe, rope, guidance_scale=6.0, use_dynamic_cfg=True, replace_gt=True,
+                     mask_add=True, generator=gen)
+
+    with torch.no_grad():
+        for i in range(args.warmup):
+            one(i)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        with K.timed_launches("attention", "gemm") as tl:
+            t0 = time.perf_counter()
+            for i in range(args.warmup, args.warmup + args.steps):
+                one(i)
+            torch.cuda.synchronize()
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    steps_per_s = world * args.steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    attn_ms = tl.mean_ms("attention")
+    attn_tf = attn_flops_per_launch() / (attn_ms * 1e-3) / 1e12
+    gemm_ev = tl.events.get("gemm", [])
+    torch.cuda.synchronize()
+    gemm_ms_total = sum(s.elapsed_time(e) for s, e in gemm_ev)
+    step_frac = step_flops() * (steps_per_s / world) / (PEAK_BF16_TFLOPS * 1e12)
+    if not math.isfinite(steps_per_s):
+        raise RuntimeError("non-finite timing")
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        del st
+        cpu = cpu_baseline()
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": steps_per_s, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic latents/prompt embeds of the 49f 480x720 shape; random-init CogVideoX-5b-I2V (42 "
+                    "layers) + 2-layer branch weights (no checkpoints offline)",
+            "config": {"workload": "BASELINE config 2: CogVideoX-5b-I2V + 2-layer branch, 49f 480x720 (latent "
+                                   "13x60x90), CFG batch 2, 226+17550=17776 tokens, 1 denoising step = branch + "
+                                   "transformer + CFG/DPM/replace-gt", "clips_per_gpu": 1, "cfg_batch": B,
+                       "tokens": NTOK, "layers": L, "branch_layers": LB,
+                       "parallelism": f"dp{world} (independent clips, weights broadcast over RCCL)"},
+            "roofline": {"kernel": "attention (vp_attention_fwd_bf16, dominant by time)", "bound": "mfma",
+                         "achieved": attn_tf, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": attn_tf / PEAK_BF16_TFLOPS, "traffic": None,
+                         "per_launch_ms": attn_ms, "launches": tl.count("attention"),
+                         "algorithmic_flop_per_launch": attn_flops_per_launch()},
+            "step_mfma_frac": step_frac,
+            "step_flop": step_flops(),
+            "gemm_ms_per_step": gemm_ms_total / args.steps,
+            "attention_ms_per_step": attn_ms * tl.count("attention") / args.steps,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

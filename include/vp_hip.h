@@ -39,7 +39,8 @@ void vp_struct_sizes(int64_t* out);
  *   patch-embed conv + text_proj + pos-emb (DF/models/embeddings.py:400-454), the branch zero-linears
  *   (DF/models/branch_cogvideox.py:415-421) and proj_out (cogvideox_transformer_3d.py:624).
  * A: bf16 [M, K] (row stride lda); W: up to 3 weight segments, each bf16 [n_seg, K] (nn.Linear layout), columns
- * [s*n_seg, (s+1)*n_seg) of C come from segment s (fused QKV without packing the weights).  K % 64 == 0.
+ * [s*n_seg, (s+1)*n_seg) of C come from segment s (fused QKV without packing the weights).  K % 8 == 0
+ * (a K tail is zero-filled on the device).
  * Output row remap: C row of GEMM row m = (m / rows_per_group) * group_stride + row_offset + (m % rows_per_group).
  * ------------------------------------------------------------------------------------------------------------- */
 enum {
@@ -185,9 +186,10 @@ int vp_unpatchify_bf16(const void* proj, int64_t ld, void* out, int32_t B, int32
  * ------------------------------------------------------------------------------------------------------------- */
 typedef struct vp_dpm_desc {
   int64_t n;
-  const void* noise_pred; /* bf16 [2, n] when do_cfg (uncond, text), else [n] */
+  const void* noise_pred; /* bf16 [2, n] when do_cfg (uncond, text), else [n]                               */
   int32_t do_cfg;
   float guidance;
+  const float* model_output; /* fp32 [n]: used instead of noise_pred when non-NULL (scheduler.step API)     */
   const void* sample;     /* bf16 [n] */
   const float* old_pred;  /* fp32 [n] or NULL */
   float* pred_out;        /* fp32 [n] */
@@ -201,7 +203,8 @@ typedef struct vp_dpm_desc {
   const void* gt_noise;   /* bf16 [n] */
   const void* mask;       /* bf16 [n] */
   float gsa, gsb;         /* add_noise scalars, bf16-rounded */
-  void* latents_out;      /* bf16 [n] */
+  void* latents_out;      /* bf16 [n] (cast + replace-gt) or NULL */
+  float* prev_out;        /* fp32 [n] pre-cast prev_sample (scheduler.step API) or NULL */
 } vp_dpm_desc;
 
 int vp_dpm_step_bf16(const vp_dpm_desc* d, void* stream);

@@ -48,7 +48,8 @@ def test_gemm_layout_exact():
     assert torch.equal(out.float().cpu(), bf(ref).float())
 
 
-@pytest.mark.parametrize("M,Nn,Kk", [(1000, 768, 512), (35, 64, 3072), (513, 256, 192)])
+@pytest.mark.parametrize("M,Nn,Kk", [(1000, 768, 512), (35, 64, 3072), (513, 256, 192), (300, 128, 32),
+                                     (77, 384, 136)])
 def test_gemm_bias_random(M, Nn, Kk):
     from videopainter_amd import kernels as K
     a, w, b = bf(rnd(M, Kk, seed=2)), bf(rnd(Nn, Kk, std=Kk ** -0.5, seed=3)), bf(rnd(Nn, std=0.1, seed=4))
@@ -58,10 +59,11 @@ def test_gemm_bias_random(M, Nn, Kk):
     assert rel(out, ref) < 4e-3
 
 
-def test_gemm_segments_gelu_scale():
+@pytest.mark.parametrize("D,Kk", [(256, 256), (128, 96)])
+def test_gemm_segments_gelu_scale(D, Kk):
     from videopainter_amd import kernels as K
     from videopainter_amd import _native as N
-    M, D, Kk = 700, 256, 256
+    M = 700
     a = bf(rnd(M, Kk, seed=5))
     ws = [bf(rnd(D, Kk, std=Kk ** -0.5, seed=6 + i)) for i in range(3)]
     bs = [bf(rnd(D, std=0.1, seed=16 + i)) for i in range(3)]

@@ -53,10 +53,14 @@ def main():
     qkv = torch.randn(B, Ntok, 3 * D, device=dev).to(torch.bfloat16)
     o = torch.empty(B, Ntok, D, device=dev, dtype=torch.bfloat16)
     q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
-    t = timeit(lambda: K.attention(q, k, v, o, H), max(2, args.iters // 2))
     fl = 4 * B * H * Ntok * Ntok * 64
-    res["attention"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
-    print("attention", res["attention"], flush=True)
+    for rnd in range(2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
+        for var in ("v1", "v2"):
+            os.environ["VP_ATTN_V1"] = "1" if var == "v1" else "0"
+            t = timeit(lambda: K.attention(q, k, v, o, H), max(2, args.iters // 2))
+            res[f"attention_{var}_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
+            print("attention", var, res[f"attention_{var}_r{rnd}"], flush=True)
+    os.environ["VP_ATTN_V1"] = "0"
     xin = torch.randn(B, Ntok, D, device=dev).to(torch.bfloat16)
     mod = torch.randn(B, 6 * D, device=dev).to(torch.bfloat16)
     lw = torch.ones(D, device=dev, dtype=torch.bfloat16)

@@ -1,0 +1,23 @@
+#!/bin/bash
+# One GPU session: tests, smoke, bench. Every GPU step has its own time limit; a crash/timeout stops the script.
+set -u
+mkdir -p gpurun_out
+run() {  # name timeout cmd...
+  local name=$1; shift; local to=$1; shift
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    ktests) run ktests 600 python -m pytest tests/test_kernels_gpu.py -q -x -rA ;;
+    mtests) run mtests 900 python -m pytest tests/test_model_gpu.py -q -rA ;;
+    gtests) run gtests 1200 python -m pytest tests -q -m gpu -rA ;;
+    smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  run bench 900 python bench.py --steps 5 --warmup 2 ;;
+    benchq) run bench 900 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    kbench) run kbench 300 python tools/bench_kernels.py --iters 5 ;;
+  esac
+done

@@ -46,12 +46,13 @@ class AttnDesc(C.Structure):
 
 
 class DpmDesc(C.Structure):
-    _fields_ = [("n", i64), ("noise_pred", vp), ("do_cfg", i32), ("guidance", f32),
+    _fields_ = [("n", i64), ("noise_pred", vp), ("do_cfg", i32), ("guidance", f32), ("model_output", vp),
                 ("sample", vp), ("old_pred", vp), ("pred_out", vp), ("noise1", vp), ("noise2", vp),
                 ("second_order", i32), ("replace_gt", i32),
                 ("sa", f32), ("sb", f32), ("m1", f32), ("m2", f32), ("mn", f32), ("m3", f32), ("m4", f32),
                 ("gt_add_noise", i32), ("mask_background", i32),
-                ("gt", vp), ("gt_noise", vp), ("mask", vp), ("gsa", f32), ("gsb", f32), ("latents_out", vp)]
+                ("gt", vp), ("gt_noise", vp), ("mask", vp), ("gsa", f32), ("gsb", f32), ("latents_out", vp),
+                ("prev_out", vp)]
 
 
 EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS = range(5)

@@ -1,0 +1,139 @@
+"""VideoPainter context encoder on the HIP kernels — drop-in for the reference `CogvideoXBranchModel`
+(DF/models/branch_cogvideox.py:43-434): same constructor kwargs, state-dict keys (incl. the unused head and
+`branch_x_embedder`), `from_transformer`, and `forward` signature / return forms.
+
+The branch's patch embedding sees cat(noisy latents 16ch, masked-video latents 16ch, mask 1ch) = 33 channels; the
+channel concat is folded into the im2col kernel (two sources), and K = 132 is zero-padded to 192 for the MFMA GEMM.
+The per-block zero-init linears run over the block outputs' video rows; `conditioning_scale` is fused into the GEMM
+epilogue.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+from . import _native as NAT
+from .attention_processor import _rope_dev
+from .config import patch_in_channels
+from .modules import Linear
+from .transformer import BF16, CogVideoXTransformer3DModel, _bf
+
+
+@dataclass
+class CogvideoxBranchOutput:
+    branch_block_samples: Tuple[torch.Tensor]
+
+
+class CogvideoXBranchModel(CogVideoXTransformer3DModel):
+    _is_branch = True
+
+    def __init__(self, num_attention_heads: int = 30, attention_head_dim: int = 64, in_channels: int = 16,
+                 out_channels: Optional[int] = 16, flip_sin_to_cos: bool = True, freq_shift: int = 0,
+                 time_embed_dim: int = 512, text_embed_dim: int = 4096, num_layers: int = 30, dropout: float = 0.0,
+                 attention_bias: bool = True, sample_width: int = 90, sample_height: int = 60,
+                 sample_frames: int = 49, patch_size: int = 2, temporal_compression_ratio: int = 4,
+                 max_text_seq_length: int = 226, activation_fn: str = "gelu-approximate",
+                 timestep_activation_fn: str = "silu", norm_elementwise_affine: bool = True, norm_eps: float = 1e-5,
+                 spatial_interpolation_scale: float = 1.875, temporal_interpolation_scale: float = 1.0,
+                 use_rotary_positional_embeddings: bool = False, use_learned_positional_embeddings: bool = False,
+                 wo_text: bool = False, id_pool_resample_learnable: bool = False):
+        kw = {k: v for k, v in locals().items() if k not in ("self", "__class__")}
+        self._pending_cfg = kw
+        super().__init__(**{k: v for k, v in kw.items() if k != "wo_text"})
+        if wo_text:
+            raise NotImplementedError("wo_text branches are not used by the VideoPainter inference scripts")
+        inner = num_attention_heads * attention_head_dim
+        self.branch_blocks = nn.ModuleList([Linear(inner, inner) for _ in range(num_layers)])
+        self.branch_x_embedder = Linear(in_channels, inner)
+
+    def _init_config(self, kwargs: dict):
+        super()._init_config(self._pending_cfg)
+
+    def _patch_channels(self):
+        return patch_in_channels(dict(self.config), True)
+
+    def _block_resample(self):
+        return False  # branch blocks always use the standard processor (branch_cogvideox.py:124)
+
+    @classmethod
+    def from_transformer(cls, transformer, num_layers: int = 4, attention_head_dim: int = 128,
+                         num_attention_heads: int = 24, load_weights_from_transformer=True, wo_text: bool = False):
+        """branch_cogvideox.py:255-293."""
+        cfg = {k: v for k, v in dict(transformer.config).items() if not k.startswith("_")}
+        cfg.update(num_layers=num_layers, attention_head_dim=attention_head_dim,
+                   num_attention_heads=num_attention_heads, wo_text=wo_text)
+        dev = transformer.proj_out.weight.device
+        branch = cls.from_config(cfg, device=dev, dtype=transformer.proj_out.weight.dtype)
+        if load_weights_from_transformer:
+            with torch.no_grad():
+                w = torch.zeros_like(branch.patch_embed.proj.weight)
+                tw = transformer.patch_embed.proj.weight
+                c = cfg["in_channels"]
+                if c == 16:
+                    w[:, :c] = tw
+                    w[:, c:2 * c] = tw
+                elif c == 32:
+                    w[:, :c // 2] = tw[:, :c // 2]
+                    w[:, c // 2:c] = tw[:, :c // 2]
+                else:
+                    raise ValueError(f"in_channels {c} is not supported")
+                branch.patch_embed.proj.weight.copy_(w)
+                branch.patch_embed.proj.bias.copy_(transformer.patch_embed.proj.bias)
+                te, bte = transformer.time_embedding, branch.time_embedding
+                for a, b in ((bte.linear_1, te.linear_1), (bte.linear_2, te.linear_2)):
+                    a.weight.copy_(b.weight)
+                    a.bias.copy_(b.bias)
+                tsd = transformer.transformer_blocks.state_dict()
+                bsd = branch.transformer_blocks.state_dict()
+                for k, v in bsd.items():  # strict=False: the first `num_layers` blocks
+                    if k in tsd and tsd[k].shape == v.shape:
+                        v.copy_(tsd[k])
+                for lin in list(branch.branch_blocks) + [branch.branch_x_embedder]:  # zero_module
+                    lin.weight.zero_()
+                    lin.bias.zero_()
+        return branch
+
+    def forward(self, hidden_states: torch.Tensor, encoder_hidden_states: torch.Tensor = None,
+                branch_cond: torch.Tensor = None, branch_mode: torch.Tensor = None, conditioning_scale=1.0,
+                timestep: Union[int, float, torch.LongTensor] = None, timestep_cond: Optional[torch.Tensor] = None,
+                image_rotary_emb: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                attention_kwargs: Optional[Dict[str, Any]] = None, mask_add: Optional[bool] = False,
+                wo_text: Optional[bool] = False, return_dict: bool = True):
+        """branch_cogvideox.py:295-434.  Returns a list of [B, Nv, D] bf16 injection tensors (views of one
+        [B, T + Nv, D] buffer per block; the text rows of that buffer are scratch)."""
+        self._check_inference(hidden_states, encoder_hidden_states, branch_cond)
+        if wo_text:
+            raise NotImplementedError("wo_text branches are not used by the VideoPainter inference scripts")
+        if timestep_cond is not None:
+            raise ValueError("timestep_cond requires a cond_proj, which CogVideoX's TimestepEmbedding does not have")
+        dev = self.proj_out.weight.device
+        B, F, C, H, W = hidden_states.shape
+        cfg = self.config
+        hs = _bf(hidden_states.to(dev))
+        bc = _bf(branch_cond.to(dev))
+        enc = _bf(encoder_hidden_states.to(dev))
+        T = enc.shape[1]
+        D = cfg.num_attention_heads * cfg.attention_head_dim
+        emb = self._time_embed(timestep, B, dev)
+        x = self.patch_embed.embed(enc, hs, bc)
+        Ntok = x.shape[1]
+        rope = _rope_dev(image_rotary_emb, dev)
+        samples = []
+        for i, block in enumerate(self.transformer_blocks):
+            x = block.forward_joint(x, T, emb, rope)
+            samples.append(x)
+        scale = float(conditioning_scale)
+        outs = []
+        for s, lin in zip(samples, self.branch_blocks):
+            o = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
+            epi = NAT.EPI_BIAS if scale == 1.0 else NAT.EPI_BIAS_SCALE
+            K.gemm(s.view(B * Ntok, D), [lin.weight], [lin.bias], o.view(B * Ntok, D), epilogue=epi, alpha=scale)
+            outs.append(o[:, T:])
+        outs = None if len(outs) == 0 else outs
+        if not return_dict:
+            return (outs,)
+        return CogvideoxBranchOutput(branch_block_samples=outs)

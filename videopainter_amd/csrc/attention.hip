@@ -15,6 +15,8 @@
 // MFMAs, LDS writes after them; one barrier per tile).
 // Roofline: MFMA-bound in principle (4·N²·64 flop per (b,h)); at d=64 the softmax VALU (one exp per 256 MFMA
 // flops) is the co-bottleneck.
+#include <stdlib.h>
+
 #include "vp_common.h"
 
 namespace {
@@ -231,6 +233,200 @@ __global__ __launch_bounds__(NTHREADS, 2) void attn_fwd_kernel(const vp_attn_des
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// v2: software-pipelined tile loop.  Within one wave the next tile's S^T = K Q^T MFMAs are issued ahead of the
+// current tile's softmax VALU work (they are independent), so the matrix pipe and the VALU overlap inside each
+// wave instead of alternating at every barrier; 3-slot LDS ring (tile t: V in use, t+1: K in use, t+2: landing),
+// register staging one tile ahead; the O rescale is skipped when no query's running max moved.
+// ------------------------------------------------------------------------------------------------------------
+constexpr int RING = 3;
+constexpr int LDS_BYTES_V2 = RING * STAGE_BYTES;
+
+VP_DEV void qk_tile(const char* Kl, const bf16x8 (&qf)[4], f32x16 (&s)[2], int lane) {
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    const int row = kh * 32 + (lane & 31);
+    bf16x8 kf[4];
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) {
+      const int ch = ds * 2 + hl;
+      kf[ds] = *(const bf16x8*)(Kl + row * 128 + ((ch ^ swz(row)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ds], qf[ds], s[kh], 0, 0, 0);
+  }
+}
+
+VP_DEV void mask_tail(f32x16 (&s)[2], int lim, int hl) {
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = kh * 32 + (i & 3) + 8 * (i >> 2) + 4 * hl;
+      if (key >= lim) s[kh][i] = -INFINITY;
+    }
+}
+
+VP_DEV void softmax_tile(f32x16 (&s)[2], float& m_run, float& l_run, f32x16 (&o)[2], bf16x8 (&pf)[4], float c) {
+  float mx = fmaxf(s[0][0], s[0][1]);
+#pragma unroll
+  for (int i = 2; i < 16; i += 2) mx = fmaxf(mx, fmaxf(s[0][i], s[0][i + 1]));
+#pragma unroll
+  for (int i = 0; i < 16; i += 2) mx = fmaxf(mx, fmaxf(s[1][i], s[1][i + 1]));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float m_new = fmaxf(m_run, mx);
+  if (__ballot(m_new > m_run) != 0ull) {  // wave-uniform: some query's max moved -> rescale O and l
+    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+    l_run *= alpha;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o[0][i] *= alpha;
+      o[1][i] *= alpha;
+    }
+    m_run = m_new;
+  }
+  const float mc = m_run * c;
+  float psum = 0.f;
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = __builtin_amdgcn_exp2f(fmaf(s[kh][i], c, -mc));
+      psum += p;
+      pf[kh * 2 + (i >> 3)][i & 7] = f2bf(p);
+    }
+  l_run += psum;
+}
+
+VP_DEV void pv_tile(const char* Vl, const bf16x8 (&pf)[4], f32x16 (&o)[2], int trow, int tcol) {
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const char* base = Vl + (ks * 16 + trow) * V_STRIDE + (dh * 32 + tcol) * 2;
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * V_STRIDE));
+      const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[ks], o[dh], 0, 0, 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(NTHREADS, 2) void attn_fwd_kernel_v2(const vp_attn_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hl = lane >> 5;
+
+  const int nqb = (d.Nq + QBLK - 1) / QBLK;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb;
+  const int qb = t - bh * nqb;
+  const int b = bh / d.H;
+  const int h = bh - b * d.H;
+
+  const int tiles1 = (d.Nk + KBLK - 1) / KBLK;
+  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KBLK - 1) / KBLK : 0;
+  const int ntiles = tiles1 + tiles2;
+
+  const int q = qb * QBLK + wave * 32 + (lane & 31);
+  const int qc = q < d.Nq ? q : d.Nq - 1;
+  const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
+
+  const int srow = tid >> 3;
+  const int schunk = tid & 7;
+  const int k_lds_off = srow * 128 + ((schunk ^ swz(srow)) << 4);
+  const int v_lds_off = K_TILE_BYTES + srow * V_STRIDE + schunk * 16;
+  auto slot = [&](int ti) -> char* { return smem + (ti % RING) * STAGE_BYTES; };
+  auto gload = [&](int ti, bf16x8& kr, bf16x8& vr) {
+    Seg s = tile_seg(d, ti, tiles1, b, h);
+    int key = s.key0 + srow;
+    key = key < s.n ? key : s.n - 1;
+    kr = *(const bf16x8*)(s.k + (int64_t)key * s.k_sn + schunk * 8);
+    vr = *(const bf16x8*)(s.v + (int64_t)key * s.v_sn + schunk * 8);
+  };
+  auto tile_limit = [&](int ti) -> int {  // valid keys in tile ti (64 unless it is a segment's partial tail)
+    Seg s = tile_seg(d, ti, tiles1, b, h);
+    return min(KBLK, s.n - s.key0);
+  };
+
+  bf16x8 kreg, vreg;
+  gload(0, kreg, vreg);
+  *(bf16x8*)(slot(0) + k_lds_off) = kreg;
+  *(bf16x8*)(slot(0) + v_lds_off) = vreg;
+  if (ntiles > 1) {
+    gload(1, kreg, vreg);
+    *(bf16x8*)(slot(1) + k_lds_off) = kreg;
+    *(bf16x8*)(slot(1) + v_lds_off) = vreg;
+  }
+  __syncthreads();
+  if (ntiles > 2) gload(2, kreg, vreg);
+
+  const float c = d.scale * 1.4426950408889634f;
+  float m_run = -1e30f, l_run = 0.f;
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    o[0][i] = 0.f;
+    o[1][i] = 0.f;
+  }
+  const int g = lane >> 4;
+  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
+  const int tcol = 16 * (g & 1) + 4 * (lane & 3);
+
+  f32x16 sa[2], sb[2];
+  qk_tile(slot(0), qf, sa, lane);
+
+  auto body = [&](f32x16 (&scur)[2], f32x16 (&snxt)[2], int ti) {
+    if (ti + 1 < ntiles) qk_tile(slot(ti + 1), qf, snxt, lane);
+    const int lim = tile_limit(ti);
+    if (lim < KBLK) mask_tail(scur, lim, hl);
+    bf16x8 pf[4];
+    softmax_tile(scur, m_run, l_run, o, pf, c);
+    pv_tile(slot(ti) + K_TILE_BYTES, pf, o, trow, tcol);
+    if (ti + 2 < ntiles) {
+      *(bf16x8*)(slot(ti + 2) + k_lds_off) = kreg;
+      *(bf16x8*)(slot(ti + 2) + v_lds_off) = vreg;
+    }
+    __syncthreads();
+    if (ti + 3 < ntiles) gload(ti + 3, kreg, vreg);
+  };
+  for (int ti = 0; ti < ntiles; ti += 2) {
+    body(sa, sb, ti);
+    if (ti + 1 < ntiles) body(sb, sa, ti + 1);
+  }
+
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.f / l_tot;
+  if (q < d.Nq) {
+    bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int dd = dh * 32 + 8 * gq + 4 * hl;
+        bf16x4 ov;
+        bf16x4 old;
+        if (d.accumulate) old = *(const bf16x4*)(orow + dd);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = rbf(o[dh][4 * gq + r] * inv);
+          if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
+          if (d.accumulate) v = bf2f(old[r]) + v;
+          ov[r] = f2bf(v);
+        }
+        *(bf16x4*)(orow + dd) = ov;
+      }
+  }
+}
+
 }  // namespace
 
 extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
@@ -243,14 +439,22 @@ extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
     return VP_ERR_ARG;
   if (d->Nk2 > 0 && ((d->k2_sn % 8) || (d->v2_sn % 8) || (d->k2_sb % 8) || (d->v2_sb % 8))) return VP_ERR_ARG;
   static bool attr_set = false;
+  const char* e = getenv("VP_ATTN_V1");  // A/B switch for benchmarking the first version
+  const int variant = (e != nullptr && e[0] == '1') ? 1 : 2;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr_set = true;
+    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel_v2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES_V2);
   }
   const int nqb = (d->Nq + QBLK - 1) / QBLK;
   const int64_t grid = (int64_t)d->B * d->H * nqb;
   if (grid > 0x7fffffff) return VP_ERR_ARG;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)grid), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+  if (variant == 1)
+    hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)grid), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel_v2, dim3((unsigned)grid), dim3(NTHREADS), LDS_BYTES_V2, (hipStream_t)stream,
+                       *d);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }

@@ -29,19 +29,23 @@ typedef __attribute__((address_space(1))) void g_void;
 
 VP_DEV int swz(int row) { return (row >> 1) & 7; }
 
-// Stage one 256x64 bf16 operand tile (rows [row0, row0+256) clamped to [0, rows_valid), cols [k0, k0+64)) into
-// `tile` as [256][8 chunks of 16 B], physical chunk = logical ^ swz(row).  4 LDS-DMA instructions per wave.
-VP_DEV void stage_tile(const bf16* __restrict__ base, int64_t ld, int row0, int rows_valid, int k0, char* tile,
-                       int wave, int lane) {
+__device__ __attribute__((aligned(16))) bf16 g_zero_chunk[8];  // 16 zero bytes: source of the K tail
+
+// Tile rows each lane stages (4 LDS-DMA wave-instructions per operand per k-step): instruction i, lane l ->
+// tile row r = (i*8 + wave)*8 + l/8, physical 16-byte chunk p = l%8, logical chunk c = p ^ swz(r).
+VP_DEV int stage_row(int i, int wave, int lane) { return (i * 8 + wave) * 8 + (lane >> 3); }
+
+// Stage one 256x64 bf16 operand tile into `tile` as [256][8 chunks of 16 B], physical chunk = logical ^ swz(row).
+// rows[i] = this lane's source row pointer for instruction i (clamped to a valid row, hoisted out of the k-loop);
+// chunks past K read a zero chunk.
+VP_DEV void stage_tile(const bf16* const (&rows)[4], int K, int k0, char* tile, int wave, int lane) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int rb = i * 8 + wave;              // 8-row block written by this wave instruction
-    const int r = rb * 8 + (lane >> 3);       // tile row of this lane
-    const int p = lane & 7;                   // physical chunk this lane lands in
-    const int c = p ^ swz(r);                 // logical chunk it must fetch
-    int gr = row0 + r;
-    gr = gr < rows_valid ? gr : rows_valid - 1;
-    const bf16* src = base + (int64_t)gr * ld + k0 + c * 8;
+    const int rb = i * 8 + wave;
+    const int r = stage_row(i, wave, lane);
+    const int c = (lane & 7) ^ swz(r);
+    const int kc = k0 + c * 8;
+    const bf16* src = kc < K ? rows[i] + kc : g_zero_chunk;
     __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(tile + rb * 1024), 16, 0, 0);
   }
 }
@@ -70,13 +74,18 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
   const int tn = (t % per_group) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  // weight segment of this column tile
-  const int seg = n0 / d.n_seg;
-  const bf16* Wseg = (const bf16*)d.W[seg];
-  const bf16* bseg = (const bf16*)d.bias[seg];
-  const int nl0 = n0 - seg * d.n_seg;
-  const int n_valid_seg = min(d.n_seg, d.N - seg * d.n_seg);
-  const bf16* A = (const bf16*)d.A;
+  // per-lane source rows of the two operand tiles (the weight rows may come from up to 3 segments: fused QKV)
+  const bf16* arow[4];
+  const bf16* wrow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = stage_row(i, wave, lane);
+    const int m = min(m0 + r, d.M - 1);
+    arow[i] = (const bf16*)d.A + (int64_t)m * d.lda;
+    const int n = min(n0 + r, d.N - 1);
+    const int sg = n / d.n_seg;
+    wrow[i] = (const bf16*)d.W[sg] + (int64_t)(n - sg * d.n_seg) * d.K;
+  }
 
   f32x4 acc[FN][FM];
 #pragma unroll
@@ -84,9 +93,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = d.K / BK;
-  stage_tile(A, d.lda, m0, d.M, 0, smem, wave, lane);
-  stage_tile(Wseg, d.K, nl0, n_valid_seg, 0, smem + TILE_BYTES, wave, lane);
+  const int nk = (d.K + BK - 1) / BK;
+  stage_tile(arow, d.K, 0, smem, wave, lane);
+  stage_tile(wrow, d.K, 0, smem + TILE_BYTES, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -94,8 +103,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     char* cur = smem + (kt & 1) * STAGE_BYTES;
     if (kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
-      stage_tile(A, d.lda, m0, d.M, (kt + 1) * BK, nxt, wave, lane);
-      stage_tile(Wseg, d.K, nl0, n_valid_seg, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+      stage_tile(arow, d.K, (kt + 1) * BK, nxt, wave, lane);
+      stage_tile(wrow, d.K, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
     }
     const char* As = cur;
     const char* Bs = cur + TILE_BYTES;
@@ -122,11 +131,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int nloc = wc * WN + j * 16 + (lane >> 4) * 4;  // 4 consecutive columns
-    const int ng = nl0 + nloc;                             // column within the weight segment
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (bseg != nullptr) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bv[r] = (ng + r < n_valid_seg) ? bf2f(bseg[ng + r]) : 0.f;
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + nloc + r;
+      if (n < d.N) {
+        const int sg = n / d.n_seg;
+        const bf16* bp = (const bf16*)d.bias[sg];
+        if (bp != nullptr) bv[r] = bf2f(bp[n - sg * d.n_seg]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
@@ -189,15 +202,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 
 extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   if (d == nullptr || d->A == nullptr || d->W[0] == nullptr || d->C == nullptr) return VP_ERR_ARG;
-  if (d->M <= 0 || d->N <= 0 || d->K <= 0 || (d->K % BK) != 0 || (d->N % 8) != 0) return VP_ERR_ARG;
+  if (d->M <= 0 || d->N <= 0 || d->K <= 0 || (d->K % 8) != 0 || (d->N % 8) != 0) return VP_ERR_ARG;
   if (d->lda < d->K || d->ldc < d->N || (d->lda % 8) != 0 || (d->ldc % 8) != 0) return VP_ERR_ARG;
   if (d->rows_per_group <= 0) return VP_ERR_ARG;
   const int nsegs = d->W[2] ? 3 : (d->W[1] ? 2 : 1);
-  if (nsegs > 1) {
-    if (d->n_seg <= 0 || (d->n_seg % BN) != 0 || d->n_seg * nsegs != d->N) return VP_ERR_ARG;
-  } else if (d->n_seg != d->N) {
-    return VP_ERR_ARG;
-  }
+  if (d->n_seg <= 0 || d->n_seg * nsegs != d->N) return VP_ERR_ARG;
   if (d->epilogue < VP_EPI_BIAS || d->epilogue > VP_EPI_BIAS_ADDROWS) return VP_ERR_ARG;
   if (d->epilogue == VP_EPI_GATED) {
     if (d->R == nullptr || d->gate == nullptr || d->gate_text == nullptr || d->tokens_per_batch <= 0) return VP_ERR_ARG;

@@ -136,7 +136,9 @@ __global__ void dpm_step_kernel(const vp_dpm_desc d) {
   if (i >= d.n) return;
   const bf16* np = (const bf16*)d.noise_pred;
   float mo;
-  if (d.do_cfg) {
+  if (d.model_output != nullptr) {
+    mo = d.model_output[i];
+  } else if (d.do_cfg) {
     const float u = bf2f(np[i]), t = bf2f(np[d.n + i]);
     mo = u + d.guidance * (t - u);
   } else {
@@ -155,6 +157,8 @@ __global__ void dpm_step_kernel(const vp_dpm_desc d) {
   } else {
     prev = (x1 - d.m2 * pred) + rbf(d.mn * bf2f(((const bf16*)d.noise1)[i]));
   }
+  if (d.prev_out != nullptr) d.prev_out[i] = prev;
+  if (d.latents_out == nullptr) return;
   float lat = rbf(prev);
   if (d.replace_gt) {
     const float g = bf2f(((const bf16*)d.gt)[i]);
@@ -254,8 +258,9 @@ extern "C" int vp_unpatchify_bf16(const void* proj, int64_t ld, void* out, int32
 }
 
 extern "C" int vp_dpm_step_bf16(const vp_dpm_desc* d, void* stream) {
-  if (!d || d->n <= 0 || !d->noise_pred || !d->sample || !d->pred_out || !d->latents_out || !d->noise1)
+  if (!d || d->n <= 0 || (!d->noise_pred && !d->model_output) || !d->sample || !d->pred_out || !d->noise1)
     return VP_ERR_ARG;
+  if (!d->latents_out && !d->prev_out) return VP_ERR_ARG;
   if (d->second_order && (!d->old_pred || !d->noise2)) return VP_ERR_ARG;
   if (d->replace_gt && (!d->gt || !d->mask || (d->gt_add_noise && !d->gt_noise))) return VP_ERR_ARG;
   hipLaunchKernelGGL(dpm_step_kernel, dim3((unsigned)((d->n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *d);

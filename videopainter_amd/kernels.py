@@ -18,6 +18,47 @@ def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+# Optional per-launch timing (bench.py's roofline): name -> list of (start, end) HIP events on the launch stream.
+_TIMED: dict = {}
+
+
+class timed_launches:
+    """Context manager recording HIP events around every launch of the named kernels (on their stream)."""
+
+    def __init__(self, *names):
+        self.names = names
+
+    def __enter__(self):
+        for n in self.names:
+            _TIMED[n] = []
+        return self
+
+    def __exit__(self, *exc):
+        self.events = {n: _TIMED.pop(n, []) for n in self.names}
+
+    def mean_ms(self, name: str) -> float:
+        ev = self.events.get(name, [])
+        torch.cuda.synchronize()
+        return sum(s.elapsed_time(e) for s, e in ev) / max(1, len(ev))
+
+    def count(self, name: str) -> int:
+        return len(self.events.get(name, []))
+
+
+def _t0(name):
+    if name in _TIMED:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        return ev
+    return None
+
+
+def _t1(name, ev):
+    if ev is not None:
+        ev[1].record()
+        _TIMED[name].append(ev)
+
+
 def _p(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
@@ -97,7 +138,9 @@ def gemm(a: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[Opti
     if epilogue == N.EPI_BIAS_ADDROWS:
         _chk(addrows, "addrows")
         d.addrows, d.addrows_ld, d.addrows_offset = _p(addrows), _rowmajor(addrows, "addrows"), addrows_offset
+    ev = _t0("gemm")
     N.check(N.lib().vp_gemm_bf16(C.byref(d), _stream()), "vp_gemm_bf16")
+    _t1("gemm", ev)
     return out
 
 
@@ -140,7 +183,9 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
         d.Nk2 = k2.shape[1]
     d.O, d.o_sb, d.o_sn = _p(out), out.stride(0), out.stride(1)
     d.scale, d.out_scale, d.accumulate = scale, out_scale, int(accumulate)
+    ev = _t0("attention")
     N.check(N.lib().vp_attention_fwd_bf16(C.byref(d), _stream()), "vp_attention_fwd_bf16")
+    _t1("attention", ev)
     return out
 
 

@@ -1,0 +1,224 @@
+"""Latent-space harness of the any-length VideoPainter pipeline's hot loop.
+
+Restates the step loop of `CogVideoXI2VDualInpaintAnyLPipeline.__call__`
+(DF/pipelines/cogvideo/pipeline_cogvideox_inpainting_i2v_branch_anyl.py:932-1050) and its window loop
+(:759, 828-872, 962-988, 1052-1069) on the HIP models, starting from the latents the VAE / T5 stages would have
+produced (those stages run once per window and are out of scope this round).  One denoising step =
+branch forward + transformer forward at B=2 (CFG) + one fused CFG/DPM/replace-gt kernel.
+
+Reference quirks reproduced on purpose:
+  * dynamic CFG uses the raw timestep t (anyl.py:991-994);
+  * `prev_resample_mask` is re-bound to the transformer's output EVERY step (anyl.py:967), so from the second step
+    of a window k>0 the "previous" mask is the current window's own mask;
+  * window k>0 conditions on the previous window's last latent frame (anyl.py:866-872).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from . import kernels as K
+from . import _native as NAT
+from .embeddings import prepare_rotary_positional_embeddings
+from .scheduler import randn_tensor
+
+BF16 = torch.bfloat16
+
+
+@dataclass
+class WindowState:
+    latents: torch.Tensor            # bf16 [1, F, C, h, w]
+    image_in: torch.Tensor           # bf16 [2, F, C, h, w]   (cat([image_latents]*2))
+    branch_in: torch.Tensor          # bf16 [2, F, C+1, h, w] (masked latents ++ mask)
+    mask1: torch.Tensor              # bf16 [2, F, 1, h, w]   branch_block_masks
+    init_mask: torch.Tensor          # bf16 [1, F, C, h, w]   replace-gt blend mask
+    video_latents: Optional[torch.Tensor]
+    noise: Optional[torch.Tensor]
+    old_pred: Optional[torch.Tensor] = None
+    last_states: Optional[Dict[int, torch.Tensor]] = None
+    extra: dict = field(default_factory=dict)
+
+
+class CogVideoXI2VDualInpaintAnyLHarness:
+    def __init__(self, transformer, branch, scheduler, vae_scale_factor_spatial: int = 8,
+                 vae_scale_factor_temporal: int = 4):
+        self.transformer = transformer
+        self.branch = branch
+        self.scheduler = scheduler
+        self.vae_scale_factor_spatial = vae_scale_factor_spatial
+        self.vae_scale_factor_temporal = vae_scale_factor_temporal
+        self.prev_resample_mask = None
+
+    @property
+    def device(self):
+        return self.transformer.proj_out.weight.device
+
+    # ------------------------------------------------------------------------------------------------------------
+    def make_window(self, latents, image_latents, masked_video_latents, mask, video_latents=None, noise=None
+                    ) -> WindowState:
+        """mask: [2, 1, F, h, w] (prepare_mask_latents output, CFG-duplicated); masked_video_latents [2, F, C, h, w];
+        image_latents [1, F, C, h, w] (frame 0 = conditioning latent, rest zero)."""
+        dev = self.device
+        lat = latents.to(dev, BF16).contiguous()
+        C = lat.shape[2]
+        m = mask.to(dev, BF16).permute(0, 2, 1, 3, 4).repeat(1, 1, C, 1, 1)  # anyl.py:920
+        image_in = torch.cat([image_latents.to(dev, BF16)] * 2).contiguous()
+        branch_in = torch.cat([masked_video_latents.to(dev, BF16), m[:, :, :1]], dim=-3).contiguous()
+        mask1 = m[:, :, :1].contiguous()
+        init_mask = m.chunk(2)[0].contiguous()
+        return WindowState(latents=lat, image_in=image_in, branch_in=branch_in, mask1=mask1, init_mask=init_mask,
+                           video_latents=None if video_latents is None else video_latents.to(dev, BF16).contiguous(),
+                           noise=None if noise is None else noise.to(dev, BF16).contiguous())
+
+    def rope_for(self, latent_frames: int, height_lat: int, width_lat: int):
+        return prepare_rotary_positional_embeddings(height_lat * self.vae_scale_factor_spatial,
+                                                    width_lat * self.vae_scale_factor_spatial, latent_frames,
+                                                    self.transformer.config.attention_head_dim,
+                                                    self.vae_scale_factor_spatial, self.transformer.config.patch_size,
+                                                    device=self.device)
+
+    # ------------------------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def step(self, st: WindowState, i: int, timesteps: torch.Tensor, prompt_embeds: torch.Tensor, rope, *,
+             guidance_scale: float = 6.0, use_dynamic_cfg: bool = True, conditioning_scale: float = 1.0,
+             replace_gt: bool = True, mask_add: bool = True, mask_background: bool = False, add_first: bool = False,
+             id_pool_resample_learnable: bool = False, attention_kwargs: Optional[dict] = None,
+             prev_window_states: Optional[Dict[int, torch.Tensor]] = None, prev_clip_weight: float = 0.0,
+             capture_last_states: bool = False, step_noise: Optional[Callable[[], torch.Tensor]] = None,
+             generator=None) -> None:
+        """One denoising step (anyl.py:933-1034); updates `st` in place."""
+        t = timesteps[i]
+        t_int = int(t)
+        dev = self.device
+        lat = st.latents
+        lvi = torch.cat([lat] * 2)
+        lmi = torch.cat([lvi, st.image_in], dim=2)
+        ts = torch.full((2,), t_int, device=dev, dtype=torch.int64)
+        bs = self.branch(hidden_states=lvi, encoder_hidden_states=prompt_embeds, branch_cond=st.branch_in,
+                         conditioning_scale=conditioning_scale, timestep=ts, image_rotary_emb=rope,
+                         attention_kwargs=attention_kwargs, return_dict=False)[0]
+        akw = dict(attention_kwargs) if attention_kwargs else {}
+        if prev_window_states is not None:
+            akw["prev_hidden_states"] = prev_window_states
+            akw["prev_clip_weight"] = prev_clip_weight
+            akw["prev_resample_mask"] = self.prev_resample_mask
+        noise_pred, hs_list, self.prev_resample_mask = self.transformer(
+            hidden_states=lmi, encoder_hidden_states=prompt_embeds, branch_block_samples=bs, timestep=ts,
+            image_rotary_emb=rope, attention_kwargs=akw, add_first=add_first,
+            branch_block_masks=st.mask1 if mask_add else None, id_pool_resample_learnable=id_pool_resample_learnable,
+            return_hidden_states=True, return_resample_mask=True, return_dict=False)
+        if capture_last_states and t_int == int(timesteps[-1]):
+            st.last_states = {k: h for k, h in enumerate(hs_list)}
+        del hs_list, bs
+        n_steps = len(timesteps)
+        g = guidance_scale
+        if use_dynamic_cfg:
+            g = 1 + guidance_scale * ((1 - math.cos(math.pi * ((n_steps - t_int) / n_steps) ** 5.0)) / 2)
+        d = NAT.DpmDesc()
+        second = self.scheduler.fill_desc(d, t_int, int(timesteps[i - 1]) if i > 0 else None, st.old_pred is not None)
+
+        def draw():
+            if step_noise is not None:
+                return step_noise().to(dev, BF16).contiguous()
+            return randn_tensor(lat.shape, generator=generator, device=dev, dtype=BF16).contiguous()
+
+        noise1 = draw()
+        noise2 = draw() if second else None
+        n = lat.numel()
+        pred = torch.empty(lat.shape, device=dev, dtype=torch.float32)
+        new_lat = torch.empty_like(lat)
+        d.n = n
+        d.noise_pred = noise_pred.data_ptr()
+        d.do_cfg = 1
+        d.guidance = g
+        d.sample = lat.data_ptr()
+        d.old_pred = st.old_pred.data_ptr() if second else None
+        d.pred_out = pred.data_ptr()
+        d.noise1 = noise1.data_ptr()
+        d.noise2 = noise2.data_ptr() if noise2 is not None else None
+        d.latents_out = new_lat.data_ptr()
+        if replace_gt:
+            if st.video_latents is None:
+                raise ValueError("replace_gt needs the window's video latents")
+            d.replace_gt = 1
+            d.mask_background = int(mask_background)
+            d.gt = st.video_latents.data_ptr()
+            d.mask = st.init_mask.data_ptr()
+            if i < n_steps - 1:
+                d.gt_add_noise = 1
+                d.gt_noise = st.noise.data_ptr()
+                d.gsa, d.gsb = self.scheduler.add_noise_scalars(int(timesteps[i + 1]), BF16)
+        if not noise_pred.is_contiguous() or noise_pred.dtype != BF16:
+            raise RuntimeError("transformer output must be contiguous bf16")
+        K.dpm_step(d)
+        st.extra["keep"] = (noise_pred, noise1, noise2)  # keep sources alive until the kernel is ordered
+        st.latents = new_lat
+        st.old_pred = pred
+
+    # ------------------------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def __call__(self, windows: List[dict], prompt_embeds: torch.Tensor, negative_prompt_embeds: torch.Tensor, *,
+                 num_inference_steps: int = 50, num_frames: int = 49, stride: Optional[int] = None,
+                 guidance_scale: float = 6.0, use_dynamic_cfg: bool = True, conditioning_scale: float = 1.0,
+                 replace_gt: bool = True, mask_add: bool = True, prev_clip_weight: float = 0.0,
+                 id_pool_resample_learnable: bool = False, add_first: bool = False,
+                 step_noise: Optional[Callable[[], torch.Tensor]] = None, generator=None) -> torch.Tensor:
+        """Window loop (anyl.py:759-1069) with output_type="latent".  windows[k] holds what prepare_latents /
+        prepare_mask_latents produced for window k: latents, noise, video_latents, mask, masked_video_latents, and
+        (window 0 only) image_latents.  Returns the overlap-averaged latent video [1, F_total, C, h, w]."""
+        dev = self.device
+        stride = num_frames if stride is None else stride
+        pe = torch.cat([negative_prompt_embeds, prompt_embeds], dim=0).to(dev, BF16).contiguous()
+        self.scheduler.set_timesteps(num_inference_steps)
+        timesteps = self.scheduler.timesteps.cpu()
+        n_windows = len(windows)
+        vt = self.vae_scale_factor_temporal
+        if stride < num_frames:
+            nfl = ((num_frames - 1) // vt + 1) * n_windows - (n_windows - 1) * ((num_frames - stride) // vt + 1)
+        elif stride == num_frames:
+            nfl = ((num_frames - 1) // vt) * n_windows + 1
+        else:
+            raise ValueError(f"stride: {stride}, num_frames: {num_frames}")
+        lat0 = windows[0]["latents"]
+        C, hh, ww = lat0.shape[2], lat0.shape[3], lat0.shape[4]
+        acc = torch.zeros(1, nfl, C, hh, ww, device=dev, dtype=BF16)
+        counts = torch.zeros(nfl)
+        prev_states = None
+        latents = None
+        self.prev_resample_mask = None
+        for w, win in enumerate(windows):
+            if w == 0:
+                image_latents = win["image_latents"]
+            else:
+                back = int((num_frames - stride) // vt)
+                img = latents[:, -back - 1:-back + 1 - 1] if -back < 0 else latents[:, -1:]
+                pad = torch.zeros(1, latents.shape[1] - 1, C, hh, ww, device=dev, dtype=BF16)
+                image_latents = torch.cat([img, pad], dim=1)
+            st = self.make_window(win["latents"], image_latents, win["masked_video_latents"], win["mask"],
+                                  win.get("video_latents"), win.get("noise"))
+            rope = self.rope_for(st.latents.shape[1], hh, ww)
+            for i in range(len(timesteps)):
+                self.step(st, i, timesteps, pe, rope, guidance_scale=guidance_scale, use_dynamic_cfg=use_dynamic_cfg,
+                          conditioning_scale=conditioning_scale, replace_gt=replace_gt, mask_add=mask_add,
+                          add_first=add_first, id_pool_resample_learnable=id_pool_resample_learnable,
+                          prev_window_states=prev_states if w > 0 else None, prev_clip_weight=prev_clip_weight,
+                          capture_last_states=w < n_windows - 1, step_noise=step_noise, generator=generator)
+            latents = st.latents
+            if w < n_windows - 1:
+                prev_states = st.last_states
+            Fw = latents.shape[1]
+            for i in range(Fw):
+                start = w * Fw
+                if w > 0 and stride < num_frames:
+                    start -= (int((num_frames - stride) // vt) + 1) * w
+                elif w > 0 and stride == num_frames:
+                    start -= w
+                acc[:, start + i] += latents[:, i]
+                counts[start + i] += 1
+        for i in range(nfl):
+            if counts[i] > 0:
+                acc[:, i] /= counts[i]
+        return acc

@@ -1,0 +1,458 @@
+"""CogVideoX-5b-I2V DiT on the HIP kernels — drop-in for the reference `CogVideoXTransformer3DModel` /
+`CogVideoXBlock` (DF/models/transformers/cogvideox_transformer_3d.py:38-646): same constructor kwargs, same
+state-dict keys, same `forward` signature and return forms.
+
+MI355X data layout: the text and video token streams live in ONE resident bf16 buffer [B, T + Nv, D] (text first),
+which is exactly the reference's `cat([encoder_hidden_states, hidden_states], dim=1)`, so every per-block
+`cat`/`split` of the reference disappears; per-segment behaviour (text vs video modulation, gates, RoPE only on
+video tokens, injection only on video tokens) is selected per row inside the kernels.  Each block is 10 launches:
+
+  norm1 linear (small-M) -> AdaLN modulate -> fused QKV GEMM -> qk-LN+RoPE (q, k) -> flash attention
+  -> to_out GEMM (+ gate * . + residual) -> norm2 linear -> AdaLN modulate -> FF1 GEMM (+GELU-tanh)
+  -> FF2 GEMM (+ gate * . + residual + masked branch injection)
+
+With `return_hidden_states=True` every block writes its output into a fresh buffer that IS the returned
+`hidden_states_list[i]` (no copies).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+from . import _native as NAT
+from .attention_processor import (Attention, CogVideoXAttnProcessor2_0, CogVideoXAttnProcessor2_0_resample,
+                                  _rope_dev, _u8)
+from .embeddings import joint_sincos_pos_embedding
+from .modules import Conv2dPatch, Dropout, LayerNorm, Linear, ModelMixin, _empty
+
+BF16 = torch.bfloat16
+
+
+@dataclass
+class Transformer2DModelOutput:
+    sample: torch.Tensor
+
+
+def _bf(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    if t is None:
+        return None
+    if t.dtype != BF16:
+        t = t.to(BF16)
+    return t.contiguous()
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# sub-modules with the reference's parameter names
+# ------------------------------------------------------------------------------------------------------------------
+
+class CogVideoXLayerNormZero(nn.Module):
+    """DF/models/normalization.py:358-386 — linear: 6*D x temb, norm: LayerNorm(D)."""
+
+    def __init__(self, conditioning_dim: int, embedding_dim: int, elementwise_affine: bool = True, eps: float = 1e-5,
+                 bias: bool = True):
+        super().__init__()
+        self.linear = Linear(conditioning_dim, 6 * embedding_dim, bias=bias)
+        self.norm = LayerNorm(embedding_dim, eps=eps, elementwise_affine=elementwise_affine)
+
+    def modulation(self, temb: torch.Tensor) -> torch.Tensor:
+        """silu(temb) @ W + b -> bf16 [B, 6D] = shift|scale|gate|enc_shift|enc_scale|enc_gate."""
+        return K.linear_small(temb, self.linear.weight, self.linear.bias, act_in=K.ACT_SILU)
+
+
+class GELUProj(nn.Module):
+    def __init__(self, dim_in, dim_out, bias=True):
+        super().__init__()
+        self.proj = Linear(dim_in, dim_out, bias=bias)
+        self.approximate = "tanh"
+
+
+class FeedForward(nn.Module):
+    """DF/models/attention.py:1144-1202 with activation_fn="gelu-approximate": net = [GELU(proj), Dropout, Linear,
+    Dropout] (non-gated; SURVEY.md finding 1)."""
+
+    def __init__(self, dim: int, inner_dim: Optional[int] = None, bias: bool = True, final_dropout: bool = True):
+        super().__init__()
+        inner_dim = inner_dim or 4 * dim
+        mods = [GELUProj(dim, inner_dim, bias=bias), Dropout(), Linear(inner_dim, dim, bias=bias)]
+        if final_dropout:
+            mods.append(Dropout())
+        self.net = nn.ModuleList(mods)
+
+
+class TimestepEmbedding(nn.Module):
+    """DF/models/embeddings.py:729-774 (linear_1 -> SiLU -> linear_2)."""
+
+    def __init__(self, in_channels: int, time_embed_dim: int):
+        super().__init__()
+        self.linear_1 = Linear(in_channels, time_embed_dim)
+        self.linear_2 = Linear(time_embed_dim, time_embed_dim)
+
+
+class CogVideoXPatchEmbed(nn.Module):
+    """DF/models/embeddings.py:337-454 — parameters only; `embed()` runs im2col + two GEMMs with fused bias and
+    positional-embedding add, writing text rows then video rows of the joint buffer."""
+
+    def __init__(self, patch_size: int, in_channels: int, embed_dim: int, text_embed_dim: int, sample_width: int,
+                 sample_height: int, sample_frames: int, temporal_compression_ratio: int, max_text_seq_length: int,
+                 spatial_interpolation_scale: float, temporal_interpolation_scale: float,
+                 use_positional_embeddings: bool, use_learned_positional_embeddings: bool):
+        super().__init__()
+        self.patch_size = patch_size
+        self.embed_dim = embed_dim
+        self.sample_height, self.sample_width, self.sample_frames = sample_height, sample_width, sample_frames
+        self.temporal_compression_ratio = temporal_compression_ratio
+        self.max_text_seq_length = max_text_seq_length
+        self.spatial_interpolation_scale = spatial_interpolation_scale
+        self.temporal_interpolation_scale = temporal_interpolation_scale
+        self.use_positional_embeddings = use_positional_embeddings
+        self.use_learned_positional_embeddings = use_learned_positional_embeddings
+        self.proj = Conv2dPatch(in_channels, embed_dim, patch_size)
+        self.text_proj = Linear(text_embed_dim, embed_dim)
+        self._pos_cache = {}
+        self._wpad = None
+        if use_positional_embeddings or use_learned_positional_embeddings:
+            pe = self._sincos(sample_height, sample_width, sample_frames)
+            if use_learned_positional_embeddings:
+                self.register_buffer("pos_embedding", _empty(*pe.shape).data, persistent=True)
+                with torch.no_grad():
+                    self.pos_embedding.copy_(pe)
+            else:
+                self.register_buffer("pos_embedding", pe.to(self.proj.weight.device, BF16), persistent=False)
+
+    def _sincos(self, h, w, frames):
+        return joint_sincos_pos_embedding(self.embed_dim, self.patch_size, self.max_text_seq_length, h, w, frames,
+                                          self.temporal_compression_ratio, self.spatial_interpolation_scale,
+                                          self.temporal_interpolation_scale)
+
+    def _padded_conv_weight(self) -> Tuple[torch.Tensor, int]:
+        w = self.proj.weight
+        kk = w.shape[1] * w.shape[2] * w.shape[3]
+        kpad = (kk + 63) // 64 * 64
+        key = (w.data_ptr(), w._version, kpad)
+        if self._wpad is None or self._wpad[0] != key:
+            wp = torch.zeros(w.shape[0], kpad, device=w.device, dtype=BF16)
+            wp[:, :kk] = w.reshape(w.shape[0], kk)
+            self._wpad = (key, wp)
+        return self._wpad[1], kpad
+
+    def _pos_for(self, h: int, w: int, frames_latent: int, device) -> Optional[torch.Tensor]:
+        """Reference :431-450: learned buffer at the sample resolution / frame count; 3D sin-cos recomputed for
+        other frame counts; ValueError for another resolution with learned embeddings."""
+        if not (self.use_positional_embeddings or self.use_learned_positional_embeddings):
+            return None
+        if self.use_learned_positional_embeddings and (self.sample_width != w or self.sample_height != h):
+            raise ValueError(
+                "It is currently not possible to generate videos at a different resolution that the defaults. This "
+                "should only be the case with 'THUDM/CogVideoX-5b-I2V'.If you think this is incorrect, please open "
+                "an issue at https://github.com/huggingface/diffusers/issues.")
+        pre = (frames_latent - 1) * self.temporal_compression_ratio + 1
+        if self.sample_height != h or self.sample_width != w or self.sample_frames != pre:
+            key = (h, w, pre, str(device))
+            if key not in self._pos_cache:
+                self._pos_cache[key] = self._sincos(h, w, pre)[0].to(device=device, dtype=BF16).contiguous()
+            return self._pos_cache[key]
+        return self.pos_embedding[0]
+
+    def embed(self, text: torch.Tensor, video: torch.Tensor, video2: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """text [B, T, Ct], video [B, F, C1, H, W] (+ video2 [B, F, C2, H, W] concatenated on channels)
+        -> joint bf16 [B, T + F*(H/p)*(W/p), D]."""
+        B, T, _ = text.shape
+        _, F, _, H, W = video.shape
+        p = self.patch_size
+        Nv = F * (H // p) * (W // p)
+        Ntok = T + Nv
+        D = self.embed_dim
+        if T != self.max_text_seq_length and (self.use_learned_positional_embeddings or self.use_positional_embeddings):
+            raise ValueError(f"text length {T} != max_text_seq_length {self.max_text_seq_length}")
+        pos = self._pos_for(H, W, F, video.device)
+        x = torch.empty(B, Ntok, D, device=video.device, dtype=BF16)
+        xf = x.view(B * Ntok, D)
+        epi = NAT.EPI_BIAS_ADDROWS if pos is not None else NAT.EPI_BIAS
+        K.gemm(text.reshape(B * T, -1), [self.text_proj.weight], [self.text_proj.bias], xf, epilogue=epi,
+               rows_per_group=T, group_stride=Ntok, row_offset=0, addrows=pos, addrows_offset=0)
+        wp, kpad = self._padded_conv_weight()
+        cols = K.patchify(video, video2, p, kpad)
+        K.gemm(cols, [wp], [self.proj.bias], xf, epilogue=epi, rows_per_group=Nv, group_stride=Ntok, row_offset=T,
+               addrows=pos, addrows_offset=T)
+        return x
+
+
+class CogVideoXBlock(nn.Module):
+    """DF/models/transformers/cogvideox_transformer_3d.py:38-216."""
+
+    def __init__(self, dim: int, num_attention_heads: int, attention_head_dim: int, time_embed_dim: int,
+                 dropout: float = 0.0, activation_fn: str = "gelu-approximate", attention_bias: bool = False,
+                 qk_norm: bool = True, norm_elementwise_affine: bool = True, norm_eps: float = 1e-5,
+                 final_dropout: bool = True, ff_inner_dim: Optional[int] = None, ff_bias: bool = True,
+                 attention_out_bias: bool = True, wo_text: bool = False, id_pool_resample_learnable: bool = False):
+        super().__init__()
+        if activation_fn != "gelu-approximate":
+            raise NotImplementedError(f"activation_fn={activation_fn!r}: CogVideoX uses gelu-approximate")
+        if wo_text:
+            raise NotImplementedError("wo_text branch blocks are not on the VideoPainter inference path")
+        if not qk_norm:
+            raise NotImplementedError("CogVideoX uses qk_norm=True")
+        self.norm1 = CogVideoXLayerNormZero(time_embed_dim, dim, norm_elementwise_affine, norm_eps, bias=True)
+        self.processor = CogVideoXAttnProcessor2_0_resample() if id_pool_resample_learnable else \
+            CogVideoXAttnProcessor2_0()
+        self.attn1 = Attention(query_dim=dim, dim_head=attention_head_dim, heads=num_attention_heads, eps=1e-6,
+                               bias=attention_bias, out_bias=attention_out_bias, processor=self.processor)
+        self.norm2 = CogVideoXLayerNormZero(time_embed_dim, dim, norm_elementwise_affine, norm_eps, bias=True)
+        self.ff = FeedForward(dim, inner_dim=ff_inner_dim, bias=ff_bias, final_dropout=final_dropout)
+        self.dim = dim
+
+    # -- joint-buffer fast path used by the models --
+    def forward_joint(self, x: torch.Tensor, text_len: int, temb: torch.Tensor, rope=None,
+                      resample_mask: Optional[torch.Tensor] = None, prev_joint: Optional[torch.Tensor] = None,
+                      prev_clip_weight: Optional[float] = None, prev_resample_mask: Optional[torch.Tensor] = None,
+                      inject: Optional[torch.Tensor] = None, inject_mask: Optional[torch.Tensor] = None,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        B, Ntok, D = x.shape
+        xf = x.view(B * Ntok, D)
+        processor = self.attn1.processor
+        if not isinstance(processor, CogVideoXAttnProcessor2_0):
+            raise ValueError(f"Unsupported processor type: {type(processor)}")
+        mod1 = self.norm1.modulation(temb)
+        xn = K.adaln_modulate(x, self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len, self.norm1.norm.eps)
+        pn = None
+        if prev_joint is not None:
+            # the block normalises the previous window's states with its own norm1 (reference :141-146)
+            pn = K.adaln_modulate(_bf(prev_joint), self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len,
+                                  self.norm1.norm.eps)
+        o = processor.attend(self.attn1, xn, text_len, rope, pn, prev_clip_weight, resample_mask,
+                             prev_resample_mask)
+        del xn, pn
+        x_mid = torch.empty_like(x)
+        to_out = self.attn1.to_out[0]
+        K.gemm(o.view(B * Ntok, D), [to_out.weight], [to_out.bias], x_mid.view(B * Ntok, D), epilogue=NAT.EPI_GATED,
+               resid=xf, mod=mod1, gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok, text_len=text_len)
+        del o
+        mod2 = self.norm2.modulation(temb)
+        xn2 = K.adaln_modulate(x_mid, self.norm2.norm.weight, self.norm2.norm.bias, mod2, text_len,
+                               self.norm2.norm.eps)
+        ff0 = self.ff.net[0].proj
+        ff2 = self.ff.net[2]
+        h1 = K.linear(xn2, ff0.weight, ff0.bias, gelu=True)
+        del xn2
+        if out is None:
+            out = torch.empty_like(x)
+        kw = {}
+        if inject is not None:
+            kw = dict(inject=inject, inject_ld=inject.stride(1), inject_bstride=inject.stride(0),
+                      inject_mask=inject_mask)
+        K.gemm(h1.view(B * Ntok, -1), [ff2.weight], [ff2.bias], out.view(B * Ntok, D), epilogue=NAT.EPI_GATED,
+               resid=x_mid.view(B * Ntok, D), mod=mod2, gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok,
+               text_len=text_len, **kw)
+        return out
+
+    def forward(self, hidden_states: torch.Tensor, encoder_hidden_states: torch.Tensor, temb: torch.Tensor,
+                image_rotary_emb=None, attention_mask=None, resample_mask=None,
+                attention_kwargs: Optional[Dict[str, Any]] = None):
+        """Reference signature (:125-134); returns (hidden_states, encoder_hidden_states)."""
+        if attention_mask is not None:
+            raise NotImplementedError("attention_mask is never set on the CogVideoX path")
+        t = encoder_hidden_states.size(1)
+        x = torch.cat([_bf(encoder_hidden_states), _bf(hidden_states)], dim=1).contiguous()
+        kw = attention_kwargs or {}
+        prev = kw.get("prev_hidden_states")
+        prev = prev if isinstance(prev, torch.Tensor) else None
+        out = self.forward_joint(x, t, _bf(temb), _rope_dev(image_rotary_emb, x.device), _u8(resample_mask), prev,
+                                 kw.get("prev_clip_weight"), _u8(kw.get("prev_resample_mask")))
+        return out[:, t:], out[:, :t]
+
+
+class CogVideoXTransformer3DModel(ModelMixin):
+    """Drop-in for DF/models/transformers/cogvideox_transformer_3d.py:218-646."""
+
+    _is_branch = False
+
+    def __init__(self, num_attention_heads: int = 30, attention_head_dim: int = 64, in_channels: int = 16,
+                 out_channels: Optional[int] = 16, flip_sin_to_cos: bool = True, freq_shift: int = 0,
+                 time_embed_dim: int = 512, text_embed_dim: int = 4096, num_layers: int = 30, dropout: float = 0.0,
+                 attention_bias: bool = True, sample_width: int = 90, sample_height: int = 60,
+                 sample_frames: int = 49, patch_size: int = 2, temporal_compression_ratio: int = 4,
+                 max_text_seq_length: int = 226, activation_fn: str = "gelu-approximate",
+                 timestep_activation_fn: str = "silu", norm_elementwise_affine: bool = True, norm_eps: float = 1e-5,
+                 spatial_interpolation_scale: float = 1.875, temporal_interpolation_scale: float = 1.0,
+                 use_rotary_positional_embeddings: bool = False, use_learned_positional_embeddings: bool = False,
+                 id_pool_resample_learnable: Optional[bool] = False):
+        super().__init__()
+        self._init_config(dict(locals_without_self(locals())))
+        inner_dim = num_attention_heads * attention_head_dim
+        if not use_rotary_positional_embeddings and use_learned_positional_embeddings:
+            raise ValueError(
+                "There are no CogVideoX checkpoints available with disable rotary embeddings and learned positional "
+                "embeddings. If you're using a custom model and/or believe this should be supported, please open an "
+                "issue at https://github.com/huggingface/diffusers/issues.")
+        if timestep_activation_fn != "silu" or not flip_sin_to_cos:
+            raise NotImplementedError("CogVideoX uses silu time embedding with flip_sin_to_cos=True")
+        self.patch_embed = CogVideoXPatchEmbed(
+            patch_size, self._patch_channels(), inner_dim, text_embed_dim, sample_width, sample_height,
+            sample_frames, temporal_compression_ratio, max_text_seq_length, spatial_interpolation_scale,
+            temporal_interpolation_scale, not use_rotary_positional_embeddings, use_learned_positional_embeddings)
+        self.embedding_dropout = Dropout()
+        self.time_embedding = TimestepEmbedding(inner_dim, time_embed_dim)
+        self.transformer_blocks = nn.ModuleList([
+            CogVideoXBlock(dim=inner_dim, num_attention_heads=num_attention_heads,
+                           attention_head_dim=attention_head_dim, time_embed_dim=time_embed_dim, dropout=dropout,
+                           activation_fn=activation_fn, attention_bias=attention_bias,
+                           norm_elementwise_affine=norm_elementwise_affine, norm_eps=norm_eps,
+                           id_pool_resample_learnable=self._block_resample())
+            for _ in range(num_layers)])
+        self.norm_final = LayerNorm(inner_dim, norm_eps, norm_elementwise_affine)
+        self._build_head(inner_dim, time_embed_dim, norm_elementwise_affine, norm_eps, patch_size, out_channels)
+
+    def _patch_channels(self):
+        return self.config.in_channels
+
+    def _block_resample(self):
+        return bool(self.config.id_pool_resample_learnable)
+
+    def _build_head(self, inner_dim, time_embed_dim, affine, eps, patch_size, out_channels):
+        self.norm_out = AdaLayerNorm(time_embed_dim, 2 * inner_dim, affine, eps)
+        self.proj_out = Linear(inner_dim, patch_size * patch_size * out_channels)
+
+    # -- processor plumbing (reference :372-430) --
+    @property
+    def attn_processors(self):
+        procs = {}
+        for name, m in self.named_modules():
+            if hasattr(m, "get_processor"):
+                procs[f"{name}.processor"] = m.get_processor()
+        return procs
+
+    def set_attn_processor(self, processor):
+        count = len(self.attn_processors)
+        if isinstance(processor, dict) and len(processor) != count:
+            raise ValueError(f"A dict of processors was passed, but the number of processors {len(processor)} does "
+                             f"not match the number of attention layers: {count}.")
+        processor = dict(processor) if isinstance(processor, dict) else processor
+        for name, m in self.named_modules():
+            if hasattr(m, "set_processor"):
+                m.set_processor(processor.pop(f"{name}.processor") if isinstance(processor, dict) else processor)
+
+    # -- shared pieces --
+    def _time_embed(self, timestep, batch: int, device) -> torch.Tensor:
+        if not torch.is_tensor(timestep):
+            timestep = torch.tensor([timestep] * batch, device=device)
+        timestep = timestep.to(device)
+        if timestep.dim() == 0:
+            timestep = timestep.expand(batch)
+        temb0 = K.timestep_embedding(timestep, self.config.num_attention_heads * self.config.attention_head_dim,
+                                     float(self.config.freq_shift))
+        te = self.time_embedding
+        h = K.linear_small(temb0, te.linear_1.weight, te.linear_1.bias, act_out=K.ACT_SILU)
+        return K.linear_small(h, te.linear_2.weight, te.linear_2.bias)
+
+    def forward(self, hidden_states: torch.Tensor, encoder_hidden_states: torch.Tensor,
+                timestep: Union[int, float, torch.LongTensor], timestep_cond: Optional[torch.Tensor] = None,
+                image_rotary_emb: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                attention_kwargs: Optional[Dict[str, Any]] = None, branch_block_samples=None,
+                branch_block_masks: Optional[torch.Tensor] = None, add_first: Optional[bool] = False,
+                self_guidance_hidden_states=None, self_guidance_masks=None,
+                return_hidden_states: Optional[bool] = False, return_resample_mask: Optional[bool] = False,
+                id_pool_resample_learnable: Optional[bool] = False, return_dict: bool = True):
+        """Reference :472-646."""
+        self._check_inference(hidden_states, encoder_hidden_states)
+        if timestep_cond is not None:
+            raise ValueError("timestep_cond requires a cond_proj, which CogVideoX's TimestepEmbedding does not have")
+        if self_guidance_hidden_states is not None or self_guidance_masks is not None:
+            raise NotImplementedError("self-guidance inputs belong to the self-guidance pipelines (out of scope)")
+        attention_kwargs = dict(attention_kwargs) if attention_kwargs is not None else None
+        if attention_kwargs is not None:
+            attention_kwargs.pop("scale", None)  # LoRA scale: adapters are folded into the weights at load time
+        dev = self.proj_out.weight.device
+        B, F, C, H, W = hidden_states.shape
+        cfg = self.config
+        p = cfg.patch_size
+        hs = _bf(hidden_states.to(dev))
+        enc = _bf(encoder_hidden_states.to(dev))
+        T = enc.shape[1]
+        Nv = F * (H // p) * (W // p)
+        Ntok = T + Nv
+        D = cfg.num_attention_heads * cfg.attention_head_dim
+
+        emb = self._time_embed(timestep, B, dev)
+        x = self.patch_embed.embed(enc, hs)
+        tok_mask = None
+        if branch_block_masks is not None:
+            tok_mask = K.patch_mask(branch_block_masks.to(dev), p)
+        resample_mask = None
+        if id_pool_resample_learnable or return_resample_mask:
+            if tok_mask is None:
+                # the reference reads an unbound `masks` here (UnboundLocalError); we fail explicitly
+                raise ValueError("id_pool_resample needs masks")
+            resample_mask = torch.zeros(B, Ntok, device=dev, dtype=torch.bool)
+            resample_mask[:, T:] = tok_mask.bool()
+        rope = _rope_dev(image_rotary_emb, dev)
+        rm_u8 = _u8(resample_mask)
+
+        prev_states = None
+        prev_w = None
+        prev_mask = None
+        if attention_kwargs and "prev_hidden_states" in attention_kwargs:
+            prev_states = attention_kwargs["prev_hidden_states"]
+            prev_w = attention_kwargs.get("prev_clip_weight")
+            prev_mask = _u8(attention_kwargs.get("prev_resample_mask"))
+
+        bs = None
+        if branch_block_samples is not None:
+            bs = [_bf(s.to(dev)) for s in branch_block_samples]
+        nl = len(self.transformer_blocks)
+        interval = int(np.ceil(nl / len(bs))) if bs else 1
+        hidden_states_list: List[torch.Tensor] = []
+        ping = None
+        for i, block in enumerate(self.transformer_blocks):
+            inj = None
+            if bs is not None:
+                if not add_first:
+                    inj = bs[i // interval]
+                elif i < len(bs):
+                    inj = bs[i]
+            pj = None
+            if prev_states is not None:
+                pj = prev_states.get(i) if isinstance(prev_states, dict) else prev_states
+            if return_hidden_states:
+                out = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
+            else:
+                out = ping if (ping is not None and ping.data_ptr() != x.data_ptr()) else torch.empty_like(x)
+                ping = x
+            x = block.forward_joint(x, T, emb, rope, rm_u8, pj, prev_w if pj is not None else None,
+                                    prev_mask if pj is not None else None, inj,
+                                    tok_mask if (inj is not None and branch_block_masks is not None) else None, out)
+            if return_hidden_states:
+                hidden_states_list.append(x)
+
+        mod = K.linear_small(emb, self.norm_out.linear.weight, self.norm_out.linear.bias, act_in=K.ACT_SILU)
+        if not cfg.use_rotary_positional_embeddings:
+            raise NotImplementedError("CogVideoX-2B head (norm_final on video rows only) is not on the 5B-I2V path")
+        y = K.final_norm(x, T, self.norm_final.weight, self.norm_final.bias, self.norm_out.norm.weight,
+                         self.norm_out.norm.bias, self.norm_out.norm.eps, mod)
+        proj = K.linear(y.view(B * Nv, D), self.proj_out.weight, self.proj_out.bias)
+        output = K.unpatchify(proj, B, F, cfg.out_channels, H, W, p)
+
+        if not return_dict:
+            if return_hidden_states:
+                if return_resample_mask:
+                    return (output, hidden_states_list, resample_mask)
+                return (output, hidden_states_list)
+            return (output,)
+        return Transformer2DModelOutput(sample=output)
+
+
+class AdaLayerNorm(nn.Module):
+    """DF/models/normalization.py:31-85 with chunk_dim=1 (shift, scale order)."""
+
+    def __init__(self, embedding_dim: int, output_dim: int, norm_elementwise_affine: bool, norm_eps: float):
+        super().__init__()
+        self.linear = Linear(embedding_dim, output_dim)
+        self.norm = LayerNorm(output_dim // 2, norm_eps, norm_elementwise_affine)
+
+
+def locals_without_self(loc: dict) -> dict:
+    return {k: v for k, v in loc.items() if k not in ("self", "__class__")}
