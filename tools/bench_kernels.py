@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--only", default="", help="attention | gemm: run just that kernel (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
     dev = "cuda"
     B, T, Nv, D, H = 2, 226, 17550, 3072, 48
@@ -41,6 +42,8 @@ def main():
     res = {}
     x = torch.randn(M, 4 * D, device=dev).to(torch.bfloat16)
     shapes = [("qkv", 3 * D, D), ("out", D, D), ("ff1", 4 * D, D), ("ff2", D, 4 * D)]
+    if args.only == "attention":
+        shapes = []
     for name, Nn, Kk in shapes:
         w = (torch.randn(Nn, Kk, device=dev) * Kk ** -0.5).to(torch.bfloat16)
         b = torch.randn(Nn, device=dev).to(torch.bfloat16) * 0.1
@@ -54,13 +57,20 @@ def main():
     o = torch.empty(B, Ntok, D, device=dev, dtype=torch.bfloat16)
     q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
     fl = 4 * B * H * Ntok * Ntok * 64
-    for rnd in range(2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
-        for var in ("v1", "v2"):
-            os.environ["VP_ATTN_V1"] = "1" if var == "v1" else "0"
+    if args.only == "gemm":
+        print(json.dumps(res))
+        return
+    variants = ("v1",) if args.only == "attention" else ("v1", "v2")
+    for rnd in range(1 if args.only else 2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
+        for var in variants:
+            os.environ["VP_ATTN_VARIANT"] = var[1]
             t = timeit(lambda: K.attention(q, k, v, o, H), max(2, args.iters // 2))
             res[f"attention_{var}_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
             print("attention", var, res[f"attention_{var}_r{rnd}"], flush=True)
-    os.environ["VP_ATTN_V1"] = "0"
+    os.environ.pop("VP_ATTN_VARIANT", None)
+    if args.only == "attention":
+        print(json.dumps(res))
+        return
     xin = torch.randn(B, Ntok, D, device=dev).to(torch.bfloat16)
     mod = torch.randn(B, 6 * D, device=dev).to(torch.bfloat16)
     lw = torch.ones(D, device=dev, dtype=torch.bfloat16)

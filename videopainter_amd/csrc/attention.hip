@@ -439,8 +439,8 @@ extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
     return VP_ERR_ARG;
   if (d->Nk2 > 0 && ((d->k2_sn % 8) || (d->v2_sn % 8) || (d->k2_sb % 8) || (d->v2_sb % 8))) return VP_ERR_ARG;
   static bool attr_set = false;
-  const char* e = getenv("VP_ATTN_V1");  // A/B switch for benchmarking the first version
-  const int variant = (e != nullptr && e[0] == '1') ? 1 : 2;
+  const char* e = getenv("VP_ATTN_VARIANT");  // A/B switch for benchmarking kernel variants
+  const int variant = (e != nullptr && e[0] == '2') ? 2 : 1;
   if (!attr_set) {
     attr_set = true;
     (void)hipFuncSetAttribute((const void*)attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);

@@ -1,5 +1,5 @@
 """CogVideoX DPM-Solver++ scheduler — drop-in for the reference `CogVideoXDPMScheduler`
-(DF/schedulers/scheduling_dpm_cogvideox.py:181-486).
+(DF/schedulers/scheduling_dpm_cogvideox.py:127-491).
 
 Host side: the fp64 noise-schedule scalars (betas, SNR shift, zero-terminal-SNR rescale, λ multipliers) exactly as
 the reference computes them with 0-dim fp64 tensors.  Device side: one fused HIP launch per step
