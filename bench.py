@@ -43,6 +43,18 @@ def attn_flops_per_launch() -> float:
     return 4.0 * B * H * NTOK * NTOK * 64
 
 
+def profiled_traffic():
+    """Latest committed PMC-derived HBM traffic per attention launch (profiles/<round>_attention_traffic.json,
+    written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_attention_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -187,6 +199,7 @@ def main():
     gemm_ev = tl.events.get("gemm", [])
     torch.cuda.synchronize()
     gemm_ms_total = sum(s.elapsed_time(e) for s, e in gemm_ev)
+    traffic, traffic_src = profiled_traffic()
     step_frac = step_flops() * (steps_per_s / world) / (PEAK_BF16_TFLOPS * 1e12)
     if not math.isfinite(steps_per_s):
         raise RuntimeError("non-finite timing")
@@ -208,7 +221,8 @@ def main():
                        "parallelism": f"dp{world} (independent clips, weights broadcast over RCCL)"},
             "roofline": {"kernel": "attention (vp_attention_fwd_bf16, dominant by time)", "bound": "mfma",
                          "achieved": attn_tf, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": attn_tf / PEAK_BF16_TFLOPS, "traffic": None,
+                         "frac": attn_tf / PEAK_BF16_TFLOPS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                         "traffic_source": traffic_src,
                          "per_launch_ms": attn_ms, "launches": tl.count("attention"),
                          "algorithmic_flop_per_launch": attn_flops_per_launch()},
             "step_mfma_frac": step_frac,

@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--variant", default="", help="attention kernel variant(s), e.g. 1 or 1,3")
     ap.add_argument("--only", default="", help="attention | gemm: run just that kernel (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
     dev = "cuda"
@@ -60,7 +61,9 @@ def main():
     if args.only == "gemm":
         print(json.dumps(res))
         return
-    variants = ("v1",) if args.only == "attention" else ("v1", "v2")
+    variants = ("v1",) if args.only == "attention" else ("v1", "v3", "v2")
+    if args.variant:
+        variants = tuple("v" + v for v in args.variant.split(","))
     for rnd in range(1 if args.only else 2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
         for var in variants:
             os.environ["VP_ATTN_VARIANT"] = var[1]

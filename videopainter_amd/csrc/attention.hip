@@ -63,176 +63,6 @@ VP_DEV Seg tile_seg(const vp_attn_desc& d, int ti, int tiles1, int b, int h) {
   return s;
 }
 
-__global__ __launch_bounds__(NTHREADS, 2) void attn_fwd_kernel(const vp_attn_desc d) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hl = lane >> 5;  // lane half
-
-  const int nqb = (d.Nq + QBLK - 1) / QBLK;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = t / nqb;
-  const int qb = t - bh * nqb;
-  const int b = bh / d.H;
-  const int h = bh - b * d.H;
-
-  const int tiles1 = (d.Nk + KBLK - 1) / KBLK;
-  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KBLK - 1) / KBLK : 0;
-  const int ntiles = tiles1 + tiles2;
-
-  // ---- Q^T fragments (B operand), 4 k-steps of 16 dims ----
-  const int q = qb * QBLK + wave * 32 + (lane & 31);
-  const int qc = q < d.Nq ? q : d.Nq - 1;
-  const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
-
-  // ---- staging assignment: one 16-byte chunk of K and one of V per thread ----
-  const int srow = tid >> 3;    // key row within tile (0..63)
-  const int schunk = tid & 7;   // 16-byte chunk within the 128-byte row
-  const int k_lds_off = srow * 128 + ((schunk ^ swz(srow)) << 4);
-  const int v_lds_off = srow * V_STRIDE + schunk * 16;
-
-  auto gload = [&](int ti, bf16x8& kr, bf16x8& vr) {
-    Seg s = tile_seg(d, ti, tiles1, b, h);
-    int key = s.key0 + srow;
-    key = key < s.n ? key : s.n - 1;
-    kr = *(const bf16x8*)(s.k + (int64_t)key * s.k_sn + schunk * 8);
-    vr = *(const bf16x8*)(s.v + (int64_t)key * s.v_sn + schunk * 8);
-  };
-
-  bf16x8 kreg, vreg;
-  gload(0, kreg, vreg);
-  *(bf16x8*)(smem + k_lds_off) = kreg;
-  *(bf16x8*)(smem + K_TILE_BYTES + v_lds_off) = vreg;
-  __syncthreads();
-
-  const float c = d.scale * 1.4426950408889634f;  // softmax in base 2
-  float m_run = -1e30f, l_run = 0.f;
-  f32x16 o[2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    o[0][i] = 0.f;
-    o[1][i] = 0.f;
-  }
-
-  // transposed-read address pieces (see header): group g = lane>>4, i = lane&15
-  const int g = lane >> 4;
-  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);      // key row within a 16-key step (+8 for 2nd read)
-  const int tcol = 16 * (g & 1) + 4 * (lane & 3);          // column within a 32-wide d half
-
-  for (int ti = 0; ti < ntiles; ++ti) {
-    const char* Kl = smem + (ti & 1) * STAGE_BYTES;
-    const char* Vl = Kl + K_TILE_BYTES;
-    const bool has_next = ti + 1 < ntiles;
-    if (has_next) gload(ti + 1, kreg, vreg);
-
-    // ---- S^T = K Q^T ----
-    f32x16 s[2];
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
-      const int row = kh * 32 + (lane & 31);
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) {
-        const int ch = ds * 2 + hl;
-        const bf16x8 kf = *(const bf16x8*)(Kl + row * 128 + ((ch ^ swz(row)) << 4));
-        s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], s[kh], 0, 0, 0);
-      }
-    }
-
-    // ---- mask the key tail of a partial tile ----
-    {
-      Seg sg = tile_seg(d, ti, tiles1, b, h);
-      if (sg.key0 + KBLK > sg.n) {
-        const int lim = sg.n - sg.key0;
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = kh * 32 + (i & 3) + 8 * (i >> 2) + 4 * hl;
-            if (key >= lim) s[kh][i] = -INFINITY;
-          }
-      }
-    }
-
-    // ---- online softmax (query on the lane) ----
-    float mx = s[0][0];
-#pragma unroll
-    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[0][i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
-    m_run = m_new;
-    const float mc = m_new * c;
-    float psum = 0.f;
-    bf16x8 pf[4];
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(s[kh][i], c, -mc));
-        psum += p;
-        pf[kh * 2 + (i >> 3)][i & 7] = f2bf(p);
-      }
-    l_run = l_run * alpha + psum;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o[0][i] *= alpha;
-      o[1][i] *= alpha;
-    }
-
-    // ---- O^T += V^T P^T ----
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-#pragma unroll
-      for (int dh = 0; dh < 2; ++dh) {
-        const char* base = Vl + (ks * 16 + trow) * V_STRIDE + (dh * 32 + tcol) * 2;
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * V_STRIDE));
-        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[ks], o[dh], 0, 0, 0);
-      }
-    }
-
-    if (has_next) {
-      char* Kn = smem + ((ti + 1) & 1) * STAGE_BYTES;
-      *(bf16x8*)(Kn + k_lds_off) = kreg;
-      *(bf16x8*)(Kn + K_TILE_BYTES + v_lds_off) = vreg;
-    }
-    __syncthreads();
-  }
-
-  // ---- epilogue: O = O^T / l, query on the lane, 4 consecutive dims per register quad ----
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.f / l_tot;
-  if (q < d.Nq) {
-    bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int dd = dh * 32 + 8 * gq + 4 * hl;
-        bf16x4 ov;
-        bf16x4 old;
-        if (d.accumulate) old = *(const bf16x4*)(orow + dd);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = rbf(o[dh][4 * gq + r] * inv);
-          if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
-          if (d.accumulate) v = bf2f(old[r]) + v;
-          ov[r] = f2bf(v);
-        }
-        *(bf16x4*)(orow + dd) = ov;
-      }
-  }
-}
-
 // ------------------------------------------------------------------------------------------------------------
 // v2: software-pipelined tile loop.  Within one wave the next tile's S^T = K Q^T MFMAs are issued ahead of the
 // current tile's softmax VALU work (they are independent), so the matrix pipe and the VALU overlap inside each
@@ -244,19 +74,22 @@ constexpr int LDS_BYTES_V2 = RING * STAGE_BYTES;
 
 VP_DEV void qk_tile(const char* Kl, const bf16x8 (&qf)[4], f32x16 (&s)[2], int lane) {
   const int hl = lane >> 5;
+  bf16x8 kf[2][4];  // all 8 fragment reads in flight before the first MFMA
 #pragma unroll
   for (int kh = 0; kh < 2; ++kh) {
     const int row = kh * 32 + (lane & 31);
-    bf16x8 kf[4];
 #pragma unroll
     for (int ds = 0; ds < 4; ++ds) {
       const int ch = ds * 2 + hl;
-      kf[ds] = *(const bf16x8*)(Kl + row * 128 + ((ch ^ swz(row)) << 4));
+      kf[kh][ds] = *(const bf16x8*)(Kl + row * 128 + ((ch ^ swz(row)) << 4));
     }
+  }
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
 #pragma unroll
-    for (int ds = 0; ds < 4; ++ds) s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ds], qf[ds], s[kh], 0, 0, 0);
+    for (int ds = 0; ds < 4; ++ds) s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kh][ds], qf[ds], s[kh], 0, 0, 0);
   }
 }
 
@@ -312,6 +145,125 @@ VP_DEV void pv_tile(const char* Vl, const bf16x8 (&pf)[4], f32x16 (&o)[2], int t
       const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[ks], o[dh], 0, 0, 0);
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Main kernel: NW waves x 32 queries per workgroup, one barrier per 64-key tile, 2-slot LDS ring with register
+// staging (global loads for tile t+1 issued before tile t's MFMAs, written to LDS after them).  With NW = 4 two
+// workgroups share a CU, so their waves are not barrier-locked to each other and one workgroup's softmax VALU runs
+// beside the other's MFMAs.
+// ------------------------------------------------------------------------------------------------------------
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 2) void attn_fwd_t(const vp_attn_desc d) {
+  constexpr int NT = NW * 64;
+  constexpr int QB = NW * 32;
+  constexpr int CH_PER_THREAD = (KBLK * 8) / NT;  // 16-byte chunks of a K (and of a V) tile per thread
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hl = lane >> 5;
+
+  const int nqb = (d.Nq + QB - 1) / QB;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb;
+  const int qb = t - bh * nqb;
+  const int b = bh / d.H;
+  const int h = bh - b * d.H;
+  const int tiles1 = (d.Nk + KBLK - 1) / KBLK;
+  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KBLK - 1) / KBLK : 0;
+  const int ntiles = tiles1 + tiles2;
+
+  const int q = qb * QB + wave * 32 + (lane & 31);
+  const int qc = q < d.Nq ? q : d.Nq - 1;
+  const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
+
+  int k_off[CH_PER_THREAD], v_off[CH_PER_THREAD], srow[CH_PER_THREAD], sch[CH_PER_THREAD];
+#pragma unroll
+  for (int i = 0; i < CH_PER_THREAD; ++i) {
+    const int cidx = tid + i * NT;
+    srow[i] = cidx >> 3;
+    sch[i] = cidx & 7;
+    k_off[i] = srow[i] * 128 + ((sch[i] ^ swz(srow[i])) << 4);
+    v_off[i] = K_TILE_BYTES + srow[i] * V_STRIDE + sch[i] * 16;
+  }
+  bf16x8 kreg[CH_PER_THREAD], vreg[CH_PER_THREAD];
+  auto gload = [&](int ti) {
+    Seg sg = tile_seg(d, ti, tiles1, b, h);
+#pragma unroll
+    for (int i = 0; i < CH_PER_THREAD; ++i) {
+      const int key = min(sg.key0 + srow[i], sg.n - 1);
+      kreg[i] = *(const bf16x8*)(sg.k + (int64_t)key * sg.k_sn + sch[i] * 8);
+      vreg[i] = *(const bf16x8*)(sg.v + (int64_t)key * sg.v_sn + sch[i] * 8);
+    }
+  };
+  auto lstore = [&](char* slotp) {
+#pragma unroll
+    for (int i = 0; i < CH_PER_THREAD; ++i) {
+      *(bf16x8*)(slotp + k_off[i]) = kreg[i];
+      *(bf16x8*)(slotp + v_off[i]) = vreg[i];
+    }
+  };
+
+  gload(0);
+  lstore(smem);
+  __syncthreads();
+
+  const float c = d.scale * 1.4426950408889634f;
+  float m_run = -1e30f, l_run = 0.f;
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    o[0][i] = 0.f;
+    o[1][i] = 0.f;
+  }
+  const int g = lane >> 4;
+  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
+  const int tcol = 16 * (g & 1) + 4 * (lane & 3);
+
+  for (int ti = 0; ti < ntiles; ++ti) {
+    const char* Kl = smem + (ti & 1) * STAGE_BYTES;
+    const bool has_next = ti + 1 < ntiles;
+    if (has_next) gload(ti + 1);
+    f32x16 s[2];
+    qk_tile(Kl, qf, s, lane);
+    {
+      Seg sg = tile_seg(d, ti, tiles1, b, h);
+      const int lim = sg.n - sg.key0;
+      if (lim < KBLK) mask_tail(s, lim, hl);
+    }
+    bf16x8 pf[4];
+    softmax_tile(s, m_run, l_run, o, pf, c);
+    pv_tile(Kl + K_TILE_BYTES, pf, o, trow, tcol);
+    if (has_next) lstore(smem + ((ti + 1) & 1) * STAGE_BYTES);
+    __syncthreads();
+  }
+
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.f / l_tot;
+  if (q < d.Nq) {
+    bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int dd = dh * 32 + 8 * gq + 4 * hl;
+        bf16x4 ov;
+        bf16x4 old;
+        if (d.accumulate) old = *(const bf16x4*)(orow + dd);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = rbf(o[dh][4 * gq + r] * inv);
+          if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
+          if (d.accumulate) v = bf2f(old[r]) + v;
+          ov[r] = f2bf(v);
+        }
+        *(bf16x4*)(orow + dd) = ov;
+      }
   }
 }
 
@@ -440,21 +392,25 @@ extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
   if (d->Nk2 > 0 && ((d->k2_sn % 8) || (d->v2_sn % 8) || (d->k2_sb % 8) || (d->v2_sb % 8))) return VP_ERR_ARG;
   static bool attr_set = false;
   const char* e = getenv("VP_ATTN_VARIANT");  // A/B switch for benchmarking kernel variants
-  const int variant = (e != nullptr && e[0] == '2') ? 2 : 1;
+  const int variant = (e != nullptr && e[0] >= '1' && e[0] <= '9') ? e[0] - '0' : 1;
   if (!attr_set) {
     attr_set = true;
-    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_t<8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_t<4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)attn_fwd_kernel_v2, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES_V2);
   }
-  const int nqb = (d->Nq + QBLK - 1) / QBLK;
+  const int nw = (variant == 3) ? 4 : 8;
+  const int nqb = (d->Nq + nw * 32 - 1) / (nw * 32);
   const int64_t grid = (int64_t)d->B * d->H * nqb;
   if (grid > 0x7fffffff) return VP_ERR_ARG;
-  if (variant == 1)
-    hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)grid), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
-  else
+  if (variant == 2)
     hipLaunchKernelGGL(attn_fwd_kernel_v2, dim3((unsigned)grid), dim3(NTHREADS), LDS_BYTES_V2, (hipStream_t)stream,
                        *d);
+  else if (variant == 3)
+    hipLaunchKernelGGL(attn_fwd_t<4>, dim3((unsigned)grid), dim3(256), LDS_BYTES, (hipStream_t)stream, *d);
+  else
+    hipLaunchKernelGGL(attn_fwd_t<8>, dim3((unsigned)grid), dim3(512), LDS_BYTES, (hipStream_t)stream, *d);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
