@@ -18,6 +18,18 @@ def _lib():
     _native.lib()
 
 
+@pytest.fixture(params=["1", "2"], ids=["gemm_v1", "gemm_v2"])
+def gemm_variant(request, monkeypatch):
+    monkeypatch.setenv("VP_GEMM_VARIANT", request.param)
+    return request.param
+
+
+@pytest.fixture(params=["1", "3", "2"], ids=["attn_v1", "attn_v3", "attn_v2"])
+def attn_variant(request, monkeypatch):
+    monkeypatch.setenv("VP_ATTN_VARIANT", request.param)
+    return request.param
+
+
 def rel(a, b):
     a = a.double().cpu()
     b = b.double().cpu()
@@ -33,7 +45,7 @@ def rnd(*shape, std=1.0, seed=0):
     return (torch.randn(*shape, generator=g) * std)
 
 
-def test_gemm_layout_exact():
+def test_gemm_layout_exact(gemm_variant):
     """Small-integer operands: every product and sum is exact in fp32 -> bit-exact check of the fragment maps."""
     from videopainter_amd import kernels as K
     g = torch.Generator().manual_seed(1)
@@ -50,7 +62,7 @@ def test_gemm_layout_exact():
 
 @pytest.mark.parametrize("M,Nn,Kk", [(1000, 768, 512), (35, 64, 3072), (513, 256, 192), (300, 128, 32),
                                      (77, 384, 136)])
-def test_gemm_bias_random(M, Nn, Kk):
+def test_gemm_bias_random(M, Nn, Kk, gemm_variant):
     from videopainter_amd import kernels as K
     a, w, b = bf(rnd(M, Kk, seed=2)), bf(rnd(Nn, Kk, std=Kk ** -0.5, seed=3)), bf(rnd(Nn, std=0.1, seed=4))
     out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
@@ -60,7 +72,7 @@ def test_gemm_bias_random(M, Nn, Kk):
 
 
 @pytest.mark.parametrize("D,Kk", [(256, 256), (128, 96)])
-def test_gemm_segments_gelu_scale(D, Kk):
+def test_gemm_segments_gelu_scale(D, Kk, gemm_variant):
     from videopainter_amd import kernels as K
     from videopainter_amd import _native as N
     M = 700
@@ -79,7 +91,7 @@ def test_gemm_segments_gelu_scale(D, Kk):
     assert rel(out2, (a.float() @ ws[0].float().T + bs[0].float()) * 0.37) < 6e-3
 
 
-def test_gemm_gated_inject_and_remap():
+def test_gemm_gated_inject_and_remap(gemm_variant):
     from videopainter_amd import kernels as K
     from videopainter_amd import _native as N
     B, T, Nv, D, Kk = 2, 10, 250, 256, 512
@@ -120,7 +132,7 @@ def _sdpa(q, k, v):
 
 
 @pytest.mark.parametrize("Nq,Nk", [(300, 300), (64, 1000), (517, 77)])
-def test_attention_random(Nq, Nk):
+def test_attention_random(Nq, Nk, attn_variant):
     from videopainter_amd import kernels as K
     B, H = 2, 3
     q, k, v = (bf(rnd(B, n, H * 64, seed=s)) for s, n in ((40, Nq), (41, Nk), (42, Nk)))
@@ -131,7 +143,7 @@ def test_attention_random(Nq, Nk):
     assert rel(out, ref) < 1e-2
 
 
-def test_attention_strided_qkv_and_segments_and_blend():
+def test_attention_strided_qkv_and_segments_and_blend(attn_variant):
     """Q/K/V read straight out of a fused [B, N, 3D] projection buffer; a second K/V segment (resample) and the
     prev-clip blend (out = (1-w) A1 + w A2)."""
     from videopainter_amd import kernels as K
@@ -154,7 +166,7 @@ def test_attention_strided_qkv_and_segments_and_blend():
     assert rel(out, (1 - w) * r1 + w * r2) < 1e-2
 
 
-def test_attention_forced_rescale():
+def test_attention_forced_rescale(attn_variant):
     """Spike one key so the running max jumps in a late tile (cdna_hip_programming.md §5.4 rule 26)."""
     from videopainter_amd import kernels as K
     B, H, Nn = 1, 1, 640

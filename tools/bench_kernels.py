@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--gemm-variants", default="1,2")
     ap.add_argument("--variant", default="", help="attention kernel variant(s), e.g. 1 or 1,3")
     ap.add_argument("--only", default="", help="attention | gemm: run just that kernel (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
@@ -50,9 +51,12 @@ def main():
         b = torch.randn(Nn, device=dev).to(torch.bfloat16) * 0.1
         out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
         a = x[:, :Kk]
-        t = timeit(lambda: K.gemm(a, [w], [b], out, lda=x.stride(0)), args.iters)
-        res[f"gemm_{name}_{M}x{Nn}x{Kk}"] = dict(ms=t * 1e3, tflops=2 * M * Nn * Kk / t / 1e12)
-        print(name, res[f"gemm_{name}_{M}x{Nn}x{Kk}"], flush=True)
+        for gv in args.gemm_variants.split(","):
+            os.environ["VP_GEMM_VARIANT"] = gv
+            t = timeit(lambda: K.gemm(a, [w], [b], out, lda=x.stride(0)), args.iters)
+            res[f"gemm{gv}_{name}_{M}x{Nn}x{Kk}"] = dict(ms=t * 1e3, tflops=2 * M * Nn * Kk / t / 1e12)
+            print(f"gemm v{gv}", name, res[f"gemm{gv}_{name}_{M}x{Nn}x{Kk}"], flush=True)
+        os.environ.pop("VP_GEMM_VARIANT", None)
     del x
     qkv = torch.randn(B, Ntok, 3 * D, device=dev).to(torch.bfloat16)
     o = torch.empty(B, Ntok, D, device=dev, dtype=torch.bfloat16)

@@ -18,6 +18,9 @@ LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libvp_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
+# attention: no NaN semantics needed (masked scores are -inf, never NaN); without this hipcc inserts a
+# canonicalising v_max before every fmaxf of an MFMA result (cdna_hip_programming.md, attention pitfalls)
+PER_FILE_FLAGS = {"attention.hip": ["-fno-honor-nans"]}
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-result",
           "-Wno-unused-function", "-munsafe-fp-atomics"]
 
@@ -33,6 +36,7 @@ def _digest() -> str:
             h.update(p.encode())
             h.update(f.read())
     h.update(" ".join(CFLAGS).encode())
+    h.update(repr(sorted(PER_FILE_FLAGS.items())).encode())
     return h.hexdigest()
 
 
@@ -46,7 +50,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
 
     def cc(src):
         obj = os.path.join(LIBDIR, os.path.basename(src).replace(".hip", ".o"))
-        cmd = [HIPCC, *CFLAGS, "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+        extra = PER_FILE_FLAGS.get(os.path.basename(src), [])
+        cmd = [HIPCC, *CFLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")

@@ -104,11 +104,13 @@ VP_DEV void mask_tail(f32x16 (&s)[2], int lim, int hl) {
 }
 
 VP_DEV void softmax_tile(f32x16 (&s)[2], float& m_run, float& l_run, f32x16 (&o)[2], bf16x8 (&pf)[4], float c) {
+  // linear max chain -> v_max3_f32 (2 new values per instruction; the file is built with -fno-honor-nans so no
+  // canonicalising v_max is inserted on the MFMA results)
   float mx = fmaxf(s[0][0], s[0][1]);
 #pragma unroll
-  for (int i = 2; i < 16; i += 2) mx = fmaxf(mx, fmaxf(s[0][i], s[0][i + 1]));
+  for (int i = 2; i < 16; i += 2) mx = fmaxf(fmaxf(mx, s[0][i]), s[0][i + 1]);
 #pragma unroll
-  for (int i = 0; i < 16; i += 2) mx = fmaxf(mx, fmaxf(s[1][i], s[1][i + 1]));
+  for (int i = 0; i < 16; i += 2) mx = fmaxf(fmaxf(mx, s[1][i]), s[1][i + 1]);
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   const float m_new = fmaxf(m_run, mx);
   if (__ballot(m_new > m_run) != 0ull) {  // wave-uniform: some query's max moved -> rescale O and l
@@ -192,13 +194,25 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_t(const vp_attn_desc d) {
     v_off[i] = K_TILE_BYTES + srow[i] * V_STRIDE + sch[i] * 16;
   }
   bf16x8 kreg[CH_PER_THREAD], vreg[CH_PER_THREAD];
+  // Per-chunk source pointers advance by one tile per call; recomputed (with the row clamp) only at a segment start
+  // or for a segment's partial last tile, so the steady-state address math is one 64-bit add per chunk.
+  const bf16* kp[CH_PER_THREAD];
+  const bf16* vp[CH_PER_THREAD];
   auto gload = [&](int ti) {
     Seg sg = tile_seg(d, ti, tiles1, b, h);
+    const bool fresh = (ti == 0) || (ti == tiles1) || (sg.key0 + KBLK > sg.n);
 #pragma unroll
     for (int i = 0; i < CH_PER_THREAD; ++i) {
-      const int key = min(sg.key0 + srow[i], sg.n - 1);
-      kreg[i] = *(const bf16x8*)(sg.k + (int64_t)key * sg.k_sn + sch[i] * 8);
-      vreg[i] = *(const bf16x8*)(sg.v + (int64_t)key * sg.v_sn + sch[i] * 8);
+      if (fresh) {
+        const int key = min(sg.key0 + srow[i], sg.n - 1);
+        kp[i] = sg.k + (int64_t)key * sg.k_sn + sch[i] * 8;
+        vp[i] = sg.v + (int64_t)key * sg.v_sn + sch[i] * 8;
+      } else {
+        kp[i] += KBLK * sg.k_sn;
+        vp[i] += KBLK * sg.v_sn;
+      }
+      kreg[i] = *(const bf16x8*)kp[i];
+      vreg[i] = *(const bf16x8*)vp[i];
     }
   };
   auto lstore = [&](char* slotp) {

@@ -11,6 +11,8 @@
 // filled by global_load_lds_dwordx4 (LDS-DMA, lane-linear destination; the bank swizzle is applied on the SOURCE
 // address and undone on the read, cdna_hip_programming.md §5.4 rule 21), XCD-aware grouped tile order.
 // Roofline: MFMA-bound (AI = 2*256*256*64 flop / 64 KB staged per k-step).
+#include <stdlib.h>
+
 #include "vp_common.h"
 
 namespace {
@@ -54,6 +56,31 @@ VP_DEV bf16x8 lds_frag(const char* tile, int row, int chunk) {
   return *(const bf16x8*)(tile + row * 128 + ((chunk ^ swz(row)) << 4));
 }
 
+// ---- variant 2 main-loop pieces: BK = 32 half-steps, 4-slot LDS ring (128 KB), 3 half-steps of LDS-DMA in flight
+// across raw barriers (counted vmcnt, never 0 in the loop: cdna_hip_programming.md §5 "Pipelining across barriers").
+constexpr int HK = 32;                      // k per half-step
+constexpr int HTILE = BM * HK * 2;          // 16 KB per operand half-tile
+constexpr int HSLOT = 2 * HTILE;            // A + B
+VP_DEV int swz64(int row) { return ((row >> 2) & 1) << 1; }  // conflict-free ds_read_b128 on 64-byte rows
+
+VP_DEV void stage_half(const bf16* const (&rows)[2], int K, int k0, char* tile, int wave, int lane) {
+  // wave-instruction i covers 16 rows x 64 B: lane l -> row (i*8 + wave)*16 + l/4, physical chunk l%4
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rb = i * 8 + wave;
+    const int r = rb * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ swz64(r);
+    const int kc = k0 + c * 8;
+    const bf16* src = kc < K ? rows[i] + kc : g_zero_chunk;
+    __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(tile + rb * 1024), 16, 0, 0);
+  }
+}
+
+VP_DEV bf16x8 lds_frag64(const char* tile, int row, int chunk) {
+  return *(const bf16x8*)(tile + row * 64 + ((chunk ^ swz64(row)) << 4));
+}
+
+template <int VAR>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_desc d) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -93,37 +120,83 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (d.K + BK - 1) / BK;
-  stage_tile(arow, d.K, 0, smem, wave, lane);
-  stage_tile(wrow, d.K, 0, smem + TILE_BYTES, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if constexpr (VAR == 1) {
+    const int nk = (d.K + BK - 1) / BK;
+    stage_tile(arow, d.K, 0, smem, wave, lane);
+    stage_tile(wrow, d.K, 0, smem + TILE_BYTES, wave, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * STAGE_BYTES;
-    if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
-      stage_tile(arow, d.K, (kt + 1) * BK, nxt, wave, lane);
-      stage_tile(wrow, d.K, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+    for (int kt = 0; kt < nk; ++kt) {
+      char* cur = smem + (kt & 1) * STAGE_BYTES;
+      if (kt + 1 < nk) {
+        char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
+        stage_tile(arow, d.K, (kt + 1) * BK, nxt, wave, lane);
+        stage_tile(wrow, d.K, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+      }
+      const char* As = cur;
+      const char* Bs = cur + TILE_BYTES;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[FM], wf[FN];
+        const int ch = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = lds_frag(As, wr * WM + i * 16 + (lane & 15), ch);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) wf[j] = lds_frag(Bs, wc * WN + j * 16 + (lane & 15), ch);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
-    const char* As = cur;
-    const char* Bs = cur + TILE_BYTES;
+  } else {
+    // per-lane half-tile source rows (2 LDS-DMA instructions per operand per half-step)
+    const bf16* ah[2];
+    const bf16* wh[2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int i = 0; i < 2; ++i) {
+      const int r = (i * 8 + wave) * 16 + (lane >> 2);
+      ah[i] = (const bf16*)d.A + (int64_t)min(m0 + r, d.M - 1) * d.lda;
+      const int n = min(n0 + r, d.N - 1);
+      const int sg = n / d.n_seg;
+      wh[i] = (const bf16*)d.W[sg] + (int64_t)(n - sg * d.n_seg) * d.K;
+    }
+    const int nh = (d.K + HK - 1) / HK;
+    auto issue = [&](int t) {
+      char* slot = smem + (t & 3) * HSLOT;
+      stage_half(ah, d.K, t * HK, slot, wave, lane);
+      stage_half(wh, d.K, t * HK, slot + HTILE, wave, lane);
+    };
+    issue(0);
+    if (nh > 1) issue(1);
+    if (nh > 2) issue(2);
+    for (int t = 0; t < nh; ++t) {
+      // retire half-step t (4 LDS-DMA per half-step per lane); keep the later ones in flight
+      if (t + 2 < nh) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (t + 1 < nh) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + 3 < nh) issue(t + 3);
+      const char* As = smem + (t & 3) * HSLOT;
+      const char* Bs = As + HTILE;
       bf16x8 af[FM], wf[FN];
-      const int ch = ks * 4 + (lane >> 4);
+      const int ch = lane >> 4;
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = lds_frag(As, wr * WM + i * 16 + (lane & 15), ch);
+      for (int i = 0; i < FM; ++i) af[i] = lds_frag64(As, wr * WM + i * 16 + (lane & 15), ch);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) wf[j] = lds_frag(Bs, wc * WN + j * 16 + (lane & 15), ch);
+      for (int j = 0; j < FN; ++j) wf[j] = lds_frag64(Bs, wc * WN + j * 16 + (lane & 15), ch);
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int i = 0; i < FM; ++i)
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // all waves done with the ring before the epilogue reuses the LDS
   }
 
   // ---- epilogue phase 1: per-fragment bias / activation, bf16 into the LDS C image ----
@@ -216,11 +289,19 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_bf16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
     attr_set = true;
   }
+  const char* e = getenv("VP_GEMM_VARIANT");  // A/B switch for benchmarking main-loop variants
+  const int variant = (e != nullptr && e[0] == '2') ? 2 : 1;
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
-  hipLaunchKernelGGL(gemm_bf16_kernel, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+  if (variant == 2)
+    hipLaunchKernelGGL(gemm_bf16_kernel<2>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+  else
+    hipLaunchKernelGGL(gemm_bf16_kernel<1>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
