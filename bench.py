@@ -100,10 +100,9 @@ def build_models(device, seed: int, rank: int, world: int):
         tr.init_synthetic_weights_(seed)
         br.init_synthetic_weights_(seed + 1)
     if world > 1:
-        import torch.distributed as dist
+        from videopainter_amd.distributed import broadcast_module
         for m in (tr, br):
-            for p in m.state_dict().values():
-                dist.broadcast(p, src=0)
+            broadcast_module(m, src=0)
     torch.cuda.synchronize()
     return tr, br
 
@@ -147,7 +146,8 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        from videopainter_amd.distributed import init as dist_init
+        dist_init("nccl", device)
 
     from videopainter_amd import kernels as K
     from videopainter_amd.pipeline import CogVideoXI2VDualInpaintAnyLHarness
@@ -189,9 +189,8 @@ def main():
             torch.cuda.synchronize()
             elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        from videopainter_amd.distributed import max_over_ranks
+        elapsed = max_over_ranks(elapsed, device)
     steps_per_s = world * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     attn_ms = tl.mean_ms("attention")

@@ -1,0 +1,83 @@
+"""Host-side logic on CPU (no GPU): configs/state-dict layout, checkpoint round trip, position tables and the
+scheduler's host scalars against the oracle."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import cogvideox_oracle as O
+from tests.golden.cases import TINY_CFG, TINY_BRANCH_CFG, tiny_weights
+
+
+def test_5b_i2v_state_dict_layout_on_meta():
+    from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, COGVIDEOX_5B_I2V, device_scope
+    from videopainter_amd.config import full_config, state_dict_shapes
+    with device_scope("meta"):
+        tr = CogVideoXTransformer3DModel(**COGVIDEOX_5B_I2V)
+        br = CogvideoXBranchModel(**dict(COGVIDEOX_5B_I2V, num_layers=2))
+    for m, branch in ((tr, False), (br, True)):
+        sd = m.state_dict()
+        ref = state_dict_shapes(full_config(dict(m.config), branch), branch)
+        assert list(sd) == list(ref)
+        assert all(tuple(sd[k].shape) == ref[k] for k in ref)
+    n = sum(p.numel() for p in tr.state_dict().values())
+    assert abs(n - (5.570e9 + 54.6e6)) / 5.6e9 < 0.01  # SURVEY.md Appendix A (+ learned pos-emb buffer)
+
+
+def test_checkpoint_round_trip_and_config_overrides(tmp_path):
+    from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel
+    tsd, bsd = tiny_weights()
+    tr = CogVideoXTransformer3DModel(**TINY_CFG)
+    tr.load_diffusers_state_dict({k: torch.from_numpy(v) for k, v in tsd.items()})
+    tr.save_pretrained(str(tmp_path / "transformer"))
+    tr2 = CogVideoXTransformer3DModel.from_pretrained(str(tmp_path), subfolder="transformer",
+                                                      id_pool_resample_learnable=True)
+    assert tr2.config.id_pool_resample_learnable is True
+    assert all(torch.equal(a, b) for a, b in zip(tr.state_dict().values(), tr2.state_dict().values()))
+    from videopainter_amd.attention_processor import CogVideoXAttnProcessor2_0_resample
+    assert isinstance(tr2.transformer_blocks[0].attn1.processor, CogVideoXAttnProcessor2_0_resample)
+    br = CogvideoXBranchModel.from_transformer(tr, num_layers=2, attention_head_dim=64, num_attention_heads=2)
+    w = br.patch_embed.proj.weight
+    assert w.shape[1] == 33
+    assert torch.equal(w[:, :16], tr.patch_embed.proj.weight[:, :16]) and torch.equal(w[:, 16:32], w[:, :16])
+    assert float(w[:, 32:].abs().max()) == 0.0
+    assert float(br.branch_blocks[0].weight.abs().max()) == 0.0  # zero_module
+    with pytest.raises(ValueError):
+        CogVideoXTransformer3DModel(**dict(TINY_CFG, use_rotary_positional_embeddings=False))
+
+
+def test_rope_and_sincos_tables_match_oracle():
+    from videopainter_amd.embeddings import prepare_rotary_positional_embeddings, joint_sincos_pos_embedding
+    for (h, w, f) in ((480, 720, 13), (256, 384, 3), (720, 1280, 13)):
+        c1, s1 = prepare_rotary_positional_embeddings(h, w, f, 64)
+        c2, s2 = O.prepare_rotary_positional_embeddings(h, w, f, 64)
+        assert torch.equal(c1, c2) and torch.equal(s1, s2)
+    cfg = dict(num_attention_heads=2, attention_head_dim=64, patch_size=2, max_text_seq_length=8,
+               temporal_compression_ratio=4, spatial_interpolation_scale=1.875, temporal_interpolation_scale=1.0)
+    a = joint_sincos_pos_embedding(128, 2, 8, 16, 24, 9)
+    b = O.sincos_joint_pos_embedding(cfg, 16, 24, 9)
+    assert torch.equal(a, b)
+
+
+def test_scheduler_host_scalars_match_oracle():
+    from videopainter_amd.scheduler import CogVideoXDPMScheduler
+    s = CogVideoXDPMScheduler(snr_shift_scale=1.0, prediction_type="v_prediction", rescale_betas_zero_snr=True,
+                              clip_sample=False, set_alpha_to_one=True, timestep_spacing="trailing")
+    s.set_timesteps(50)
+    o = O.DPMSchedulerOracle()
+    o.set_timesteps(50)
+    assert torch.equal(s.timesteps, o.timesteps)
+    ts = [int(t) for t in s.timesteps]
+    for i, t in enumerate(ts):
+        c = s.coefficients(t, ts[i - 1] if i else None)
+        r = o.coefficients(t, ts[i - 1] if i else None)
+        for k in ("m1", "m2", "mn"):
+            assert c[k] == float(r["mult" + k[1:]] if k != "mn" else r["mult_noise"])
+    assert ts[0] == 999 and ts[-1] == 19
+
+
+def test_dynamic_cfg_matches_reference_formula():
+    g = O.dynamic_cfg_scale(6.0, 50, 999)
+    assert math.isclose(g, 1 + 6.0 * ((1 - math.cos(math.pi * ((50 - 999) / 50) ** 5.0)) / 2))

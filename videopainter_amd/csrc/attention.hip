@@ -104,13 +104,18 @@ VP_DEV void mask_tail(f32x16 (&s)[2], int lim, int hl) {
 }
 
 VP_DEV void softmax_tile(f32x16 (&s)[2], float& m_run, float& l_run, f32x16 (&o)[2], bf16x8 (&pf)[4], float c) {
-  // linear max chain -> v_max3_f32 (2 new values per instruction; the file is built with -fno-honor-nans so no
-  // canonicalising v_max is inserted on the MFMA results)
-  float mx = fmaxf(s[0][0], s[0][1]);
+  // max over the lane's 32 scores as 4 independent v_max3_f32 chains (short dependency chains: the wave has
+  // little other work to hide latency behind); the file is built with -fno-honor-nans so no canonicalising v_max
+  // is inserted on the MFMA results
+  float m4[4];
 #pragma unroll
-  for (int i = 2; i < 16; i += 2) mx = fmaxf(fmaxf(mx, s[0][i]), s[0][i + 1]);
-#pragma unroll
-  for (int i = 0; i < 16; i += 2) mx = fmaxf(fmaxf(mx, s[1][i]), s[1][i + 1]);
+  for (int j = 0; j < 4; ++j) {
+    const f32x16& v = s[j >> 1];
+    const int o = (j & 1) * 8;
+    m4[j] = fmaxf(fmaxf(fmaxf(v[o], v[o + 1]), v[o + 2]), fmaxf(fmaxf(v[o + 3], v[o + 4]), v[o + 5]));
+    m4[j] = fmaxf(fmaxf(m4[j], v[o + 6]), v[o + 7]);
+  }
+  float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   const float m_new = fmaxf(m_run, mx);
   if (__ballot(m_new > m_run) != 0ull) {  // wave-uniform: some query's max moved -> rescale O and l
@@ -124,16 +129,16 @@ VP_DEV void softmax_tile(f32x16 (&s)[2], float& m_run, float& l_run, f32x16 (&o)
     m_run = m_new;
   }
   const float mc = m_run * c;
-  float psum = 0.f;
+  float ps[4] = {0.f, 0.f, 0.f, 0.f};  // 4 independent partial sums (8-deep chains instead of one 32-deep)
 #pragma unroll
   for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float p = __builtin_amdgcn_exp2f(fmaf(s[kh][i], c, -mc));
-      psum += p;
+      ps[i & 3] += p;
       pf[kh * 2 + (i >> 3)][i & 7] = f2bf(p);
     }
-  l_run += psum;
+  l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
 }
 
 VP_DEV void pv_tile(const char* Vl, const bf16x8 (&pf)[4], f32x16 (&o)[2], int trow, int tcol) {
