@@ -24,7 +24,7 @@ def gemm_variant(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["1", "3", "2"], ids=["attn_v1", "attn_v3", "attn_v2"])
+@pytest.fixture(params=["4", "1", "3", "6"], ids=lambda v: f"attn_v{v}")
 def attn_variant(request, monkeypatch):
     monkeypatch.setenv("VP_ATTN_VARIANT", request.param)
     return request.param
@@ -179,6 +179,28 @@ def test_attention_forced_rescale(attn_variant):
     out = torch.empty(B, Nn, 64, device=dev, dtype=torch.bfloat16)
     K.attention(q.to(dev), k.to(dev), v.to(dev), out, H)
     ref = _sdpa(q[:, None], k[:, None], v[:, None])[:, 0]
+    assert rel(out, ref) < 1e-2
+
+
+def test_attention_stepwise_max_growth(attn_variant):
+    """Running max grows by 0 / 0.5 / 3 / 8 nats at tile seams, so the deferred-max test (tile sum > 2^8) takes both
+    branches many times within one query block (cdna_hip_programming.md §5.4 rule 26)."""
+    from videopainter_amd import kernels as K
+    B, H, Nn = 1, 2, 1100
+    g = torch.Generator().manual_seed(80)
+    u = torch.randn(64, generator=g)
+    u = u / u.norm()
+    q = rnd(B, Nn, 2 * 64, seed=81) + 2.0 * torch.cat([u, -u])
+    k = rnd(B, Nn, 2 * 64, seed=82)
+    steps = torch.tensor([0.0, 0.5, 3.0, 8.0])[torch.randint(0, 4, (Nn // 64 + 1,), generator=g)]
+    coef = 4.0 * torch.cumsum(steps, 0)[torch.arange(Nn) // 64]  # logit += 2 * coef / 8 per key
+    k = k + coef[None, :, None] * torch.cat([u, -u])
+    v = rnd(B, Nn, 2 * 64, seed=83)
+    q, k, v = bf(q), bf(k), bf(v)
+    out = torch.empty(B, Nn, 2 * 64, device=dev, dtype=torch.bfloat16)
+    K.attention(q.to(dev), k.to(dev), v.to(dev), out, H)
+    hd = lambda t: t.view(B, Nn, H, 64).transpose(1, 2)
+    ref = _sdpa(hd(q), hd(k), hd(v)).transpose(1, 2).reshape(B, Nn, 2 * 64)
     assert rel(out, ref) < 1e-2
 
 

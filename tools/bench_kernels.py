@@ -65,12 +65,15 @@ def main():
     if args.only == "gemm":
         print(json.dumps(res))
         return
-    variants = ("v1",) if args.only == "attention" else ("v1", "v3", "v2")
+    variants = ("vdefault",) if args.only == "attention" else ("vdefault", "v1", "v3")
     if args.variant:
         variants = tuple("v" + v for v in args.variant.split(","))
     for rnd in range(1 if args.only else 2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
         for var in variants:
-            os.environ["VP_ATTN_VARIANT"] = var[1]
+            if var == "vdefault":
+                os.environ.pop("VP_ATTN_VARIANT", None)
+            else:
+                os.environ["VP_ATTN_VARIANT"] = var[1:]
             t = timeit(lambda: K.attention(q, k, v, o, H), max(2, args.iters // 2))
             res[f"attention_{var}_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
             print("attention", var, res[f"attention_{var}_r{rnd}"], flush=True)

@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--prof", default="gpurun_out/prof")
     ap.add_argument("--fetch", default="gpurun_out/pmc_fetch")
     ap.add_argument("--write", default="gpurun_out/pmc_write")
-    ap.add_argument("--kernel", default="attn_fwd_kernel")
+    ap.add_argument("--kernel", default="attn_fwd")
     ap.add_argument("--algorithmic-bytes", type=float, default=4 * 2 * 17776 * 3072 * 2.0,
                     help="Q+K+V+O bytes per config-2 attention launch")
     a = ap.parse_args()

@@ -14,7 +14,13 @@
 // K/V tiles of 64 keys are double-buffered in LDS with register staging (global loads issued before the tile's
 // MFMAs, LDS writes after them; one barrier per tile).
 // Roofline: MFMA-bound in principle (4·N²·64 flop per (b,h)); at d=64 the softmax VALU (one exp per 256 MFMA
-// flops) is the co-bottleneck.
+// flops) is the co-bottleneck, so the lever is latency hiding across waves: the default variant consumes each
+// 64-key tile in two 32-key halves (16 score + 8 packed-P registers live), which fits 128 VGPRs and runs 4 waves
+// per SIMD (two 8-wave workgroups per CU).  Measured at config 2 (B=2, H=48, N=17776): 2 waves/SIMD 773-800
+// TFLOP/s, 3 waves/SIMD 835-863, 4 waves/SIMD half tiles 888.  Tried and dropped (slower at this shape):
+// an 8-wave ping-pong schedule (two wave groups alternating MFMA and softmax phases between barriers: 735, the
+// softmax phase is twice the MFMA phase at d=64 so the MFMA group idles), deferred-max softmax (register cost
+// outweighs the skipped max), software-pipelined S tiles (spills).
 #include <stdlib.h>
 
 #include "vp_common.h"
@@ -30,6 +36,7 @@ constexpr int V_STRIDE = 192;       // bytes per V row in LDS (128 data + 64 pad
 constexpr int V_TILE_BYTES = KBLK * V_STRIDE;
 constexpr int STAGE_BYTES = K_TILE_BYTES + V_TILE_BYTES;
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;
+constexpr int DEFAULT_VARIANT = 4;
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
@@ -63,33 +70,34 @@ VP_DEV Seg tile_seg(const vp_attn_desc& d, int ti, int tiles1, int b, int h) {
   return s;
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// v2: software-pipelined tile loop.  Within one wave the next tile's S^T = K Q^T MFMAs are issued ahead of the
-// current tile's softmax VALU work (they are independent), so the matrix pipe and the VALU overlap inside each
-// wave instead of alternating at every barrier; 3-slot LDS ring (tile t: V in use, t+1: K in use, t+2: landing),
-// register staging one tile ahead; the O rescale is skipped when no query's running max moved.
-// ------------------------------------------------------------------------------------------------------------
-constexpr int RING = 3;
-constexpr int LDS_BYTES_V2 = RING * STAGE_BYTES;
-
+// S^T = K Q^T for one 64-key tile; PRE = K fragments read ahead of the first MFMA (8: all, 4: one key half at a
+// time, 16 fewer VGPRs)
+template <int PRE>
 VP_DEV void qk_tile(const char* Kl, const bf16x8 (&qf)[4], f32x16 (&s)[2], int lane) {
   const int hl = lane >> 5;
-  bf16x8 kf[2][4];  // all 8 fragment reads in flight before the first MFMA
+  static_assert(PRE == 8 || PRE == 4, "PRE");
+  constexpr int KH_PER = PRE / 4;
 #pragma unroll
-  for (int kh = 0; kh < 2; ++kh) {
-    const int row = kh * 32 + (lane & 31);
+  for (int kh0 = 0; kh0 < 2; kh0 += KH_PER) {
+    bf16x8 kf[KH_PER][4];
 #pragma unroll
-    for (int ds = 0; ds < 4; ++ds) {
-      const int ch = ds * 2 + hl;
-      kf[kh][ds] = *(const bf16x8*)(Kl + row * 128 + ((ch ^ swz(row)) << 4));
+    for (int j = 0; j < KH_PER; ++j) {
+      const int row = (kh0 + j) * 32 + (lane & 31);
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) {
+        const int ch = ds * 2 + hl;
+        kf[j][ds] = *(const bf16x8*)(Kl + row * 128 + ((ch ^ swz(row)) << 4));
+      }
     }
-  }
 #pragma unroll
-  for (int kh = 0; kh < 2; ++kh) {
+    for (int j = 0; j < KH_PER; ++j) {
+      const int kh = kh0 + j;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
+      for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
 #pragma unroll
-    for (int ds = 0; ds < 4; ++ds) s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kh][ds], qf[ds], s[kh], 0, 0, 0);
+      for (int ds = 0; ds < 4; ++ds)
+        s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[j][ds], qf[ds], s[kh], 0, 0, 0);
+    }
   }
 }
 
@@ -155,14 +163,168 @@ VP_DEV void pv_tile(const char* Vl, const bf16x8 (&pf)[4], f32x16 (&o)[2], int t
   }
 }
 
+// Row-sum-on-MFMA softmax: the tile's row sums come out of 4 extra MFMAs (ones^T x P^T, accumulated in lsum where
+// every entry of a lane holds its query's running sum), so the VALU does only max, exp, scale and bf16 packing — at
+// head_dim 64 the VALU, not the matrix pipe, is the bottleneck.  The sum is then over the bf16-rounded P that also
+// feeds O (numerator and denominator see the same P).
+VP_DEV void softmax_tile_rs(f32x16 (&s)[2], float& m_run, f32x16 (&o)[2], f32x16& lsum, bf16x8 (&pf)[4], float c) {
+  float m4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x16& v = s[j >> 1];
+    const int o8 = (j & 1) * 8;
+    m4[j] = fmaxf(fmaxf(fmaxf(v[o8], v[o8 + 1]), v[o8 + 2]), fmaxf(fmaxf(v[o8 + 3], v[o8 + 4]), v[o8 + 5]));
+    m4[j] = fmaxf(fmaxf(m4[j], v[o8 + 6]), v[o8 + 7]);
+  }
+  float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  }
+  const float m_new = fmaxf(m_run, mx);
+  if (__ballot(m_new > m_run) != 0ull) {
+    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o[0][i] *= alpha;
+      o[1][i] *= alpha;
+      lsum[i] *= alpha;
+    }
+    m_run = m_new;
+  }
+  const float mc = m_run * c;
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) pf[kh * 2 + (i >> 3)][i & 7] = f2bf(__builtin_amdgcn_exp2f(fmaf(s[kh][i], c, -mc)));
+}
+
+VP_DEV void pv_tile_rs(const char* Vl, const bf16x8 (&pf)[4], f32x16 (&o)[2], f32x16& lsum, int trow, int tcol) {
+  const bf16 one = f2bf(1.f);
+  const bf16x8 ones = {one, one, one, one, one, one, one, one};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const char* base = Vl + (ks * 16 + trow) * V_STRIDE + (dh * 32 + tcol) * 2;
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * V_STRIDE));
+      const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[ks], o[dh], 0, 0, 0);
+    }
+    lsum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[ks], lsum, 0, 0, 0);
+  }
+}
+
+// ---- half-tile (32-key) helpers: the 64-key LDS tile is consumed in two 32-key halves so only 16 score
+// registers, 8 packed-P registers and 16 K-fragment registers are live (the register budget of 4 waves/SIMD) ----
+VP_DEV void qk_half(const char* Kl, int kh, const bf16x8 (&qf)[4], f32x16& s, int lane) {
+  const int hl = lane >> 5;
+  const int row = kh * 32 + (lane & 31);
+  bf16x8 kf[4];
+#pragma unroll
+  for (int ds = 0; ds < 4; ++ds) {
+    const int ch = ds * 2 + hl;
+    kf[ds] = *(const bf16x8*)(Kl + row * 128 + ((ch ^ swz(row)) << 4));
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s[i] = 0.f;
+#pragma unroll
+  for (int ds = 0; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ds], qf[ds], s, 0, 0, 0);
+}
+
+VP_DEV void mask_half(f32x16& s, int lim, int kh, int hl) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int key = kh * 32 + (i & 3) + 8 * (i >> 2) + 4 * hl;
+    if (key >= lim) s[i] = -INFINITY;
+  }
+}
+
+VP_DEV void softmax_half(f32x16& s, float& m_run, float& l_run, f32x16 (&o)[2], bf16x8 (&pf)[2], float c) {
+  float m2[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int o8 = j * 8;
+    m2[j] = fmaxf(fmaxf(fmaxf(s[o8], s[o8 + 1]), s[o8 + 2]), fmaxf(fmaxf(s[o8 + 3], s[o8 + 4]), s[o8 + 5]));
+    m2[j] = fmaxf(fmaxf(m2[j], s[o8 + 6]), s[o8 + 7]);
+  }
+  float mx = fmaxf(m2[0], m2[1]);
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  }
+  const float m_new = fmaxf(m_run, mx);
+  if (__ballot(m_new > m_run) != 0ull) {
+    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
+    l_run *= alpha;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o[0][i] *= alpha;
+      o[1][i] *= alpha;
+    }
+    m_run = m_new;
+  }
+  const float mc = m_run * c;
+  float ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float p = __builtin_amdgcn_exp2f(fmaf(s[i], c, -mc));
+    ps[i & 3] += p;
+    pf[i >> 3][i & 7] = f2bf(p);
+  }
+  l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+}
+
+VP_DEV void pv_half(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)[2], int trow, int tcol) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ks = kh * 2 + j;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const char* base = Vl + (ks * 16 + trow) * V_STRIDE + (dh * 32 + tcol) * 2;
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * V_STRIDE));
+      const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[j], o[dh], 0, 0, 0);
+    }
+  }
+}
+
+// O = O^T accumulator / l, rounded to bf16 like the reference's SDPA output, then the optional prev-clip blend
+VP_DEV void store_out(const vp_attn_desc& d, const f32x16 (&o)[2], float l_run, int q, int b, int h, int hl,
+                      bool split_sum = true) {
+  const float l_tot = split_sum ? l_run + __shfl_xor(l_run, 32, 64) : l_run;
+  const float inv = 1.f / l_tot;
+  if (q >= d.Nq) return;
+  bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int dd = dh * 32 + 8 * gq + 4 * hl;
+      bf16x4 ov;
+      bf16x4 old;
+      if (d.accumulate) old = *(const bf16x4*)(orow + dd);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = rbf(o[dh][4 * gq + r] * inv);
+        if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
+        if (d.accumulate) v = bf2f(old[r]) + v;
+        ov[r] = f2bf(v);
+      }
+      *(bf16x4*)(orow + dd) = ov;
+    }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Main kernel: NW waves x 32 queries per workgroup, one barrier per 64-key tile, 2-slot LDS ring with register
 // staging (global loads for tile t+1 issued before tile t's MFMAs, written to LDS after them).  With NW = 4 two
 // workgroups share a CU, so their waves are not barrier-locked to each other and one workgroup's softmax VALU runs
 // beside the other's MFMAs.
 // ------------------------------------------------------------------------------------------------------------
-template <int NW>
-__global__ __launch_bounds__(NW * 64, 2) void attn_fwd_t(const vp_attn_desc d) {
+template <int NW, int OCC, int PRE, bool RS = false, bool HALF = false>
+__global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_t(const vp_attn_desc d) {
   constexpr int NT = NW * 64;
   constexpr int QB = NW * 32;
   constexpr int CH_PER_THREAD = (KBLK * 8) / NT;  // 16-byte chunks of a K (and of a V) tile per thread
@@ -234,11 +396,12 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_t(const vp_attn_desc d) {
 
   const float c = d.scale * 1.4426950408889634f;
   float m_run = -1e30f, l_run = 0.f;
-  f32x16 o[2];
+  f32x16 o[2], lsum;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     o[0][i] = 0.f;
     o[1][i] = 0.f;
+    lsum[i] = 0.f;
   }
   const int g = lane >> 4;
   const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
@@ -248,155 +411,47 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_t(const vp_attn_desc d) {
     const char* Kl = smem + (ti & 1) * STAGE_BYTES;
     const bool has_next = ti + 1 < ntiles;
     if (has_next) gload(ti + 1);
+    if constexpr (HALF) {
+      Seg sg = tile_seg(d, ti, tiles1, b, h);
+      const int lim = sg.n - sg.key0;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        f32x16 sh;
+        qk_half(Kl, kh, qf, sh, lane);
+        if (lim < KBLK) mask_half(sh, lim, kh, hl);
+        bf16x8 pf[2];
+        softmax_half(sh, m_run, l_run, o, pf, c);
+        pv_half(Kl + K_TILE_BYTES, kh, pf, o, trow, tcol);
+      }
+      if (has_next) lstore(smem + ((ti + 1) & 1) * STAGE_BYTES);
+      __syncthreads();
+      continue;
+    }
     f32x16 s[2];
-    qk_tile(Kl, qf, s, lane);
+    qk_tile<PRE>(Kl, qf, s, lane);
     {
       Seg sg = tile_seg(d, ti, tiles1, b, h);
       const int lim = sg.n - sg.key0;
       if (lim < KBLK) mask_tail(s, lim, hl);
     }
     bf16x8 pf[4];
-    softmax_tile(s, m_run, l_run, o, pf, c);
-    pv_tile(Kl + K_TILE_BYTES, pf, o, trow, tcol);
+    if constexpr (RS) {
+      softmax_tile_rs(s, m_run, o, lsum, pf, c);
+      pv_tile_rs(Kl + K_TILE_BYTES, pf, o, lsum, trow, tcol);
+    } else {
+      softmax_tile(s, m_run, l_run, o, pf, c);
+      pv_tile(Kl + K_TILE_BYTES, pf, o, trow, tcol);
+    }
     if (has_next) lstore(smem + ((ti + 1) & 1) * STAGE_BYTES);
     __syncthreads();
   }
 
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.f / l_tot;
-  if (q < d.Nq) {
-    bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int dd = dh * 32 + 8 * gq + 4 * hl;
-        bf16x4 ov;
-        bf16x4 old;
-        if (d.accumulate) old = *(const bf16x4*)(orow + dd);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = rbf(o[dh][4 * gq + r] * inv);
-          if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
-          if (d.accumulate) v = bf2f(old[r]) + v;
-          ov[r] = f2bf(v);
-        }
-        *(bf16x4*)(orow + dd) = ov;
-      }
-  }
+  if constexpr (RS)
+    store_out(d, o, lsum[0], q, b, h, hl, false);
+  else
+    store_out(d, o, l_run, q, b, h, hl);
 }
 
-__global__ __launch_bounds__(NTHREADS, 2) void attn_fwd_kernel_v2(const vp_attn_desc d) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hl = lane >> 5;
-
-  const int nqb = (d.Nq + QBLK - 1) / QBLK;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = t / nqb;
-  const int qb = t - bh * nqb;
-  const int b = bh / d.H;
-  const int h = bh - b * d.H;
-
-  const int tiles1 = (d.Nk + KBLK - 1) / KBLK;
-  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KBLK - 1) / KBLK : 0;
-  const int ntiles = tiles1 + tiles2;
-
-  const int q = qb * QBLK + wave * 32 + (lane & 31);
-  const int qc = q < d.Nq ? q : d.Nq - 1;
-  const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
-
-  const int srow = tid >> 3;
-  const int schunk = tid & 7;
-  const int k_lds_off = srow * 128 + ((schunk ^ swz(srow)) << 4);
-  const int v_lds_off = K_TILE_BYTES + srow * V_STRIDE + schunk * 16;
-  auto slot = [&](int ti) -> char* { return smem + (ti % RING) * STAGE_BYTES; };
-  auto gload = [&](int ti, bf16x8& kr, bf16x8& vr) {
-    Seg s = tile_seg(d, ti, tiles1, b, h);
-    int key = s.key0 + srow;
-    key = key < s.n ? key : s.n - 1;
-    kr = *(const bf16x8*)(s.k + (int64_t)key * s.k_sn + schunk * 8);
-    vr = *(const bf16x8*)(s.v + (int64_t)key * s.v_sn + schunk * 8);
-  };
-  auto tile_limit = [&](int ti) -> int {  // valid keys in tile ti (64 unless it is a segment's partial tail)
-    Seg s = tile_seg(d, ti, tiles1, b, h);
-    return min(KBLK, s.n - s.key0);
-  };
-
-  bf16x8 kreg, vreg;
-  gload(0, kreg, vreg);
-  *(bf16x8*)(slot(0) + k_lds_off) = kreg;
-  *(bf16x8*)(slot(0) + v_lds_off) = vreg;
-  if (ntiles > 1) {
-    gload(1, kreg, vreg);
-    *(bf16x8*)(slot(1) + k_lds_off) = kreg;
-    *(bf16x8*)(slot(1) + v_lds_off) = vreg;
-  }
-  __syncthreads();
-  if (ntiles > 2) gload(2, kreg, vreg);
-
-  const float c = d.scale * 1.4426950408889634f;
-  float m_run = -1e30f, l_run = 0.f;
-  f32x16 o[2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    o[0][i] = 0.f;
-    o[1][i] = 0.f;
-  }
-  const int g = lane >> 4;
-  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
-  const int tcol = 16 * (g & 1) + 4 * (lane & 3);
-
-  f32x16 sa[2], sb[2];
-  qk_tile(slot(0), qf, sa, lane);
-
-  auto body = [&](f32x16 (&scur)[2], f32x16 (&snxt)[2], int ti) {
-    if (ti + 1 < ntiles) qk_tile(slot(ti + 1), qf, snxt, lane);
-    const int lim = tile_limit(ti);
-    if (lim < KBLK) mask_tail(scur, lim, hl);
-    bf16x8 pf[4];
-    softmax_tile(scur, m_run, l_run, o, pf, c);
-    pv_tile(slot(ti) + K_TILE_BYTES, pf, o, trow, tcol);
-    if (ti + 2 < ntiles) {
-      *(bf16x8*)(slot(ti + 2) + k_lds_off) = kreg;
-      *(bf16x8*)(slot(ti + 2) + v_lds_off) = vreg;
-    }
-    __syncthreads();
-    if (ti + 3 < ntiles) gload(ti + 3, kreg, vreg);
-  };
-  for (int ti = 0; ti < ntiles; ti += 2) {
-    body(sa, sb, ti);
-    if (ti + 1 < ntiles) body(sb, sa, ti + 1);
-  }
-
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.f / l_tot;
-  if (q < d.Nq) {
-    bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int dd = dh * 32 + 8 * gq + 4 * hl;
-        bf16x4 ov;
-        bf16x4 old;
-        if (d.accumulate) old = *(const bf16x4*)(orow + dd);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = rbf(o[dh][4 * gq + r] * inv);
-          if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
-          if (d.accumulate) v = bf2f(old[r]) + v;
-          ov[r] = f2bf(v);
-        }
-        *(bf16x4*)(orow + dd) = ov;
-      }
-  }
-}
 
 }  // namespace
 
@@ -409,27 +464,40 @@ extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
       (d->v_sb % 8) || (d->o_sb % 4))
     return VP_ERR_ARG;
   if (d->Nk2 > 0 && ((d->k2_sn % 8) || (d->v2_sn % 8) || (d->k2_sb % 8) || (d->v2_sb % 8))) return VP_ERR_ARG;
+  // kernel variants (A/B switch VP_ATTN_VARIANT for benchmarking): waves per workgroup, waves/SIMD occupancy
+  // target, deferred-max softmax, K fragments read ahead
+  struct Var {
+    const void* fn;
+    int nw;
+    int lds = LDS_BYTES;
+  };
+  static const Var vars[] = {
+      {(const void*)attn_fwd_t<8, 2, 8>, 8},                      // 1: 8 waves x 32 queries, 2 waves/SIMD
+      {(const void*)attn_fwd_t<4, 2, 8>, 4},                      // 2: 4-wave workgroups, 2 per CU
+      {(const void*)attn_fwd_t<4, 3, 8>, 4},                      // 3: 4-wave workgroups, 3 per CU
+      {(const void*)attn_fwd_t<8, 4, 8, false, true>, 8},         // 4: half tiles, 4 waves/SIMD (default)
+      {(const void*)attn_fwd_t<4, 4, 8, false, true>, 4},         // 5: half tiles, 4-wave workgroups
+      {(const void*)attn_fwd_t<8, 2, 8, true>, 8},                // 6: row sums on the MFMA
+  };
+
+  constexpr int NVAR = sizeof(vars) / sizeof(vars[0]);
   static bool attr_set = false;
-  const char* e = getenv("VP_ATTN_VARIANT");  // A/B switch for benchmarking kernel variants
-  const int variant = (e != nullptr && e[0] >= '1' && e[0] <= '9') ? e[0] - '0' : 1;
   if (!attr_set) {
     attr_set = true;
-    (void)hipFuncSetAttribute((const void*)attn_fwd_t<8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_t<4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel_v2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES_V2);
+    for (int i = 0; i < NVAR; ++i)
+      (void)hipFuncSetAttribute(vars[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize, vars[i].lds);
   }
-  const int nw = (variant == 3) ? 4 : 8;
-  const int nqb = (d->Nq + nw * 32 - 1) / (nw * 32);
+  const char* e = getenv("VP_ATTN_VARIANT");
+  int variant = e != nullptr ? atoi(e) : 0;
+  if (variant < 1 || variant > NVAR) variant = DEFAULT_VARIANT;
+  const Var& v = vars[variant - 1];
+  const int nqb = (d->Nq + v.nw * 32 - 1) / (v.nw * 32);
   const int64_t grid = (int64_t)d->B * d->H * nqb;
   if (grid > 0x7fffffff) return VP_ERR_ARG;
-  if (variant == 2)
-    hipLaunchKernelGGL(attn_fwd_kernel_v2, dim3((unsigned)grid), dim3(NTHREADS), LDS_BYTES_V2, (hipStream_t)stream,
-                       *d);
-  else if (variant == 3)
-    hipLaunchKernelGGL(attn_fwd_t<4>, dim3((unsigned)grid), dim3(256), LDS_BYTES, (hipStream_t)stream, *d);
-  else
-    hipLaunchKernelGGL(attn_fwd_t<8>, dim3((unsigned)grid), dim3(512), LDS_BYTES, (hipStream_t)stream, *d);
+  void* args[] = {(void*)d};
+  const hipError_t le = hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(v.nw * 64), args, v.lds,
+                                        (hipStream_t)stream);
+  if (le != hipSuccess) return (int)le;
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
