@@ -18,7 +18,7 @@ def _lib():
     _native.lib()
 
 
-@pytest.fixture(params=["1", "2"], ids=["gemm_v1", "gemm_v2"])
+@pytest.fixture(params=["5", "1"], ids=["gemm_v5", "gemm_v1"])
 def gemm_variant(request, monkeypatch):
     monkeypatch.setenv("VP_GEMM_VARIANT", request.param)
     return request.param
@@ -61,7 +61,7 @@ def test_gemm_layout_exact(gemm_variant):
 
 
 @pytest.mark.parametrize("M,Nn,Kk", [(1000, 768, 512), (35, 64, 3072), (513, 256, 192), (300, 128, 32),
-                                     (77, 384, 136)])
+                                     (77, 384, 136), (200, 320, 64), (129, 256, 320), (64, 512, 448)])
 def test_gemm_bias_random(M, Nn, Kk, gemm_variant):
     from videopainter_amd import kernels as K
     a, w, b = bf(rnd(M, Kk, seed=2)), bf(rnd(Nn, Kk, std=Kk ** -0.5, seed=3)), bf(rnd(Nn, std=0.1, seed=4))

@@ -13,6 +13,8 @@
 // Roofline: MFMA-bound (AI = 2*256*256*64 flop / 64 KB staged per k-step).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "vp_common.h"
 
 namespace {
@@ -50,6 +52,14 @@ VP_DEV void stage_tile(const bf16* const (&rows)[4], int K, int k0, char* tile, 
     const bf16* src = kc < K ? rows[i] + kc : g_zero_chunk;
     __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(tile + rb * 1024), 16, 0, 0);
   }
+}
+
+// LDS-DMA of 16 bytes per lane with saddr + 32-bit voffset addressing: global [sbase + voff] -> LDS [m0 + 16*lane]
+// (inline asm: the builtin form makes the compiler keep a 64-bit address per lane and instruction)
+VP_DEV void glds16(const char* sbase, int voff, char* lds) {
+  const unsigned la = (unsigned)(uintptr_t)(lds_void*)lds;
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(la), "v"(voff), "s"(sbase)
+               : "memory", "m0");
 }
 
 VP_DEV bf16x8 lds_frag(const char* tile, int row, int chunk) {
@@ -120,7 +130,205 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (VAR == 1) {
+  if constexpr (VAR == 5) {
+    // Quadrant-phase pipeline.  Each wave's 128x64 C block is split into 4 quadrants (64 rows x 32 cols); a K-tile
+    // (BK = 64) runs as 4 phases of 16 MFMAs, in the quadrant order (A0,B0) (A0,B1) (A1,B1) (A1,B0) so each phase
+    // needs ONE new operand subtile, which is read from LDS into registers during the previous phase.  The LDS
+    // holds two K-tiles as 4 "units" each (A rows of quadrant-row 0 / 1, W rows of quadrant-col 0 / 1, 16 KB = two
+    // LDS-DMA instructions per thread).  Phase slot s issues one unit (B0 and B1 and A1 of tile k+2 in phases 0-2
+    // of tile k, A0 of tile k+3 in phase 3), so every unit is in flight for 7 phases before it is read; at the top of
+    // each slot a wave waits for the unit issued 7 slots earlier (vmcnt(12): 6 units stay in flight) and for its
+    // own LDS reads, then ONE barrier both publishes that unit and retires the reads of the region the slot's DMA
+    // overwrites (each unit's region is last read in the slot just before the one that refills it).
+    const int nk = (d.K + BK - 1) / BK;
+    using Z = std::integral_constant<int, 0>;
+    using O = std::integral_constant<int, 1>;
+    // Per-lane 32-bit byte offsets of the 4 units' source rows (2 LDS-DMA instructions each) from a wave-uniform
+    // base (the activation, or the weight segment that holds the 8-row block: blocks never straddle a segment since
+    // n_seg % 8 == 0), so the DMA uses saddr + voffset addressing and the per-tile advance is a scalar add.
+    int uoff[4][2];
+    const char* ubase[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int g = i * 8 + wave;
+        const int rb = (u < 2) ? (g >> 3) * 128 + u * 64 + (g & 7) * 8 : (g >> 2) * 64 + (u - 2) * 32 + (g & 3) * 8;
+        const int r = rb + (lane >> 3);
+        const int c = (lane & 7) ^ swz(r);
+        if (u < 2) {
+          ubase[u][i] = (const char*)d.A;
+          uoff[u][i] = (min(m0 + r, d.M - 1) * d.lda + c * 8) * 2;
+        } else {
+          const int sg = __builtin_amdgcn_readfirstlane(min(n0 + rb, d.N - 1) / d.n_seg);
+          ubase[u][i] = (const char*)d.W[sg];
+          uoff[u][i] = ((min(n0 + r, d.N - 1) - sg * d.n_seg) * d.K + c * 8) * 2;
+        }
+      }
+    // unit u: 0 = A quadrant-row 0, 1 = A quadrant-row 1, 2 = W quadrant-col 0, 3 = W quadrant-col 1
+    // (this variant runs only for K % 64 == 0, so there is no K tail here)
+    auto issue_unit = [&](int u, int tile) {
+      char* base = smem + (tile & 1) * STAGE_BYTES + (u >= 2 ? TILE_BYTES : 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int g = i * 8 + wave;
+        const int rb = (u < 2) ? (g >> 3) * 128 + u * 64 + (g & 7) * 8 : (g >> 2) * 64 + (u - 2) * 32 + (g & 3) * 8;
+        glds16(ubase[u][i] + tile * (BK * 2), uoff[u][i], base + rb * 128);
+      }
+    };
+    auto slot_tile = [&](int sl, int& u) -> int {  // unit and tile issued by slot sl (sl >= -9)
+      const int k = (sl + 12) / 4 - 3;
+      const int p = sl - 4 * k;
+      u = p == 0 ? 2 : p == 1 ? 3 : p == 2 ? 1 : 0;
+      return p < 3 ? k + 2 : k + 3;
+    };
+    auto exists = [&](int sl) {
+      int u;
+      return slot_tile(sl, u) < nk;
+    };
+    auto issue_slot = [&](int sl) {
+      int u;
+      const int tile = slot_tile(sl, u);
+      if (tile < nk) issue_unit(u, tile);
+    };
+    auto top = [&](int sl) {
+      if (exists(sl - 1)) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    };
+    // LDS fragment addresses: swz(row) depends only on lane&15 here (rows step by 16), so every read is one of two
+    // lane bases (k-halves) plus a compile-time offset (buffer parity, quadrant, fragment)
+    const int lrow = lane & 15;
+    int lbase[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) lbase[ks] = lrow * 128 + (((ks * 4 + (lane >> 4)) ^ swz(lrow)) << 4);
+    auto readA = [&](bf16x8 (&a)[8], auto par_c, auto qm_c) {
+      constexpr int par = decltype(par_c)::value, qm = decltype(qm_c)::value;
+      const char* As = smem + par * STAGE_BYTES + (wr * WM + qm * 64) * 128;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[ks * 4 + i] = *(const bf16x8*)(As + lbase[ks] + i * 16 * 128);
+    };
+    auto readB = [&](bf16x8 (&bb)[4], auto par_c, auto qn_c) {
+      constexpr int par = decltype(par_c)::value, qn = decltype(qn_c)::value;
+      const char* Bs = smem + par * STAGE_BYTES + TILE_BYTES + (wc * WN + qn * 32) * 128;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bb[ks * 2 + j] = *(const bf16x8*)(Bs + lbase[ks] + j * 16 * 128);
+    };
+    auto mma = [&](const bf16x8 (&a)[8], const bf16x8 (&bb)[4], auto qm_c, auto qn_c) {
+      constexpr int qm = decltype(qm_c)::value, qn = decltype(qn_c)::value;
+      __builtin_amdgcn_sched_barrier(0);  // keep the next subtile's reads above this phase's MFMAs
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[qn * 2 + j][qm * 4 + i] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[ks * 2 + j], a[ks * 4 + i], acc[qn * 2 + j][qm * 4 + i], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    bf16x8 a0[8], a1[8], bx[4], by[4];
+    // prologue: slots -9..-2 (tiles 0 and 1, and nothing that overwrites tile 0's quadrant-row-0 A before it is
+    // read), then the first subtiles, then slot -1 (A quadrant-row 0 of tile 2 into tile 0's region)
+    for (int sl = -9; sl < -1; ++sl) issue_slot(sl);
+    if (exists(-2)) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // units of slots -9, -8 landed
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    readA(a0, Z{}, Z{});
+    readB(bx, Z{}, Z{});
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_slot(-1);
+    // one K-tile; PAR = k & 1 selects the LDS buffer and which of bx/by holds quadrant-col 0.  STEADY: every slot
+    // of this tile issues a unit and 6 later units exist (k + 3 < nk), so the waits are the fixed vmcnt(12).
+    auto tile_body = [&](int k, auto par_c, auto steady_c, bf16x8 (&b0)[4], bf16x8 (&b1)[4]) {
+      using P = decltype(par_c);
+      using NP = std::integral_constant<int, 1 - P::value>;
+      constexpr bool STEADY = decltype(steady_c)::value;
+      const int s0 = 4 * k;
+      auto slot = [&](int sl) {
+        if constexpr (STEADY) {
+          asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          int u;
+          const int tile = slot_tile(sl, u);
+          issue_unit(u, tile);
+        } else {
+          top(sl);
+          issue_slot(sl);
+        }
+      };
+      const bool more = STEADY || k + 1 < nk;
+      slot(s0);
+      readB(b1, P{}, O{});
+      mma(a0, b0, Z{}, Z{});
+      slot(s0 + 1);
+      readA(a1, P{}, O{});
+      mma(a0, b1, Z{}, O{});
+      slot(s0 + 2);
+      if (more) readA(a0, NP{}, Z{});
+      mma(a1, b1, O{}, O{});
+      slot(s0 + 3);
+      if (more) readB(b1, NP{}, Z{});  // b1's registers carry the next tile's quadrant-col 0
+      mma(a1, b0, O{}, Z{});
+    };
+    using T_ = std::integral_constant<bool, true>;
+    using F_ = std::integral_constant<bool, false>;
+    int k = 0;
+    for (; k + 4 < nk; k += 2) {
+      tile_body(k, Z{}, T_{}, bx, by);
+      tile_body(k + 1, O{}, T_{}, by, bx);
+    }
+    // tail (at most 4 tiles; k is even here, so the parities are static)
+    if (k < nk) tile_body(k, Z{}, F_{}, bx, by);
+    if (k + 1 < nk) tile_body(k + 1, O{}, F_{}, by, bx);
+    if (k + 2 < nk) tile_body(k + 2, Z{}, F_{}, bx, by);
+    if (k + 3 < nk) tile_body(k + 3, O{}, F_{}, by, bx);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else if constexpr (VAR == 4) {
+    // VAR 1 with both k-halves' fragments read right after the barrier (24 reads in flight, 96 VGPRs), so the
+    // second half's LDS latency hides under the first half's 32 MFMAs
+    const int nk = (d.K + BK - 1) / BK;
+    stage_tile(arow, d.K, 0, smem, wave, lane);
+    stage_tile(wrow, d.K, 0, smem + TILE_BYTES, wave, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      char* cur = smem + (kt & 1) * STAGE_BYTES;
+      const char* As = cur;
+      const char* Bs = cur + TILE_BYTES;
+      bf16x8 af[2][FM], wf[2][FN];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) wf[ks][j] = lds_frag(Bs, wc * WN + j * 16 + (lane & 15), ch);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[ks][i] = lds_frag(As, wr * WM + i * 16 + (lane & 15), ch);
+      }
+      if (kt + 1 < nk) {
+        char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
+        stage_tile(arow, d.K, (kt + 1) * BK, nxt, wave, lane);
+        stage_tile(wrow, d.K, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][j], af[ks][i], acc[j][i], 0, 0, 0);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else if constexpr (VAR == 1) {
     const int nk = (d.K + BK - 1) / BK;
     stage_tile(arow, d.K, 0, smem, wave, lane);
     stage_tile(wrow, d.K, 0, smem + TILE_BYTES, wave, lane);
@@ -153,6 +361,69 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+  } else if constexpr (VAR == 3) {
+    // BK = 32 half-steps through the 4-slot ring with the NEXT half-step's fragments read into registers while the
+    // current half-step's 32 MFMAs run, so no LDS latency sits between a barrier and the matrix pipe.  At the top of
+    // half-step t the wave waits for its own loads of t+1 (vmcnt(4): only t+2 still in flight), one barrier makes
+    // t+1 visible and retires every wave's reads of t-1, then the LDS-DMA for t+3 goes into t-1's slot.
+    const bf16* ah[2];
+    const bf16* wh[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (i * 8 + wave) * 16 + (lane >> 2);
+      ah[i] = (const bf16*)d.A + (int64_t)min(m0 + r, d.M - 1) * d.lda;
+      const int n = min(n0 + r, d.N - 1);
+      const int sg = n / d.n_seg;
+      wh[i] = (const bf16*)d.W[sg] + (int64_t)(n - sg * d.n_seg) * d.K;
+    }
+    const int nh = (d.K + HK - 1) / HK;
+    auto issue = [&](int t) {
+      char* slot = smem + (t & 3) * HSLOT;
+      stage_half(ah, d.K, t * HK, slot, wave, lane);
+      stage_half(wh, d.K, t * HK, slot + HTILE, wave, lane);
+    };
+    const int ch = lane >> 4;
+    auto read = [&](int t, bf16x8 (&af)[FM], bf16x8 (&wf)[FN]) {
+      const char* As = smem + (t & 3) * HSLOT;
+      const char* Bs = As + HTILE;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = lds_frag64(As, wr * WM + i * 16 + (lane & 15), ch);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) wf[j] = lds_frag64(Bs, wc * WN + j * 16 + (lane & 15), ch);
+    };
+    auto mma = [&](const bf16x8 (&af)[FM], const bf16x8 (&wf)[FN]) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+    };
+    issue(0);
+    if (nh > 1) issue(1);
+    if (nh > 2) issue(2);
+    if (nh > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // half-step 0 landed (1, 2 in flight)
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    bf16x8 afA[FM], wfA[FN], afB[FM], wfB[FN];
+    read(0, afA, wfA);
+    auto step = [&](int t, const bf16x8 (&afc)[FM], const bf16x8 (&wfc)[FN], bf16x8 (&afn)[FM],
+                    bf16x8 (&wfn)[FN]) {
+      // make t+1 visible, free slot (t-1)&3
+      if (t + 2 < nh) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + 3 < nh) issue(t + 3);
+      if (t + 1 < nh) read(t + 1, afn, wfn);
+      mma(afc, wfc);
+    };
+    int t = 0;
+    for (; t + 1 < nh; t += 2) {
+      step(t, afA, wfA, afB, wfB);
+      step(t + 1, afB, wfB, afA, wfA);
+    }
+    if (t < nh) step(t, afA, wfA, afB, wfB);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
   } else {
     // per-lane half-tile source rows (2 LDS-DMA instructions per operand per half-step)
     const bf16* ah[2];
@@ -293,12 +564,27 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
     attr_set = true;
   }
   const char* e = getenv("VP_GEMM_VARIANT");  // A/B switch for benchmarking main-loop variants
-  const int variant = (e != nullptr && e[0] == '2') ? 2 : 1;
+  int variant = (e != nullptr && e[0] >= '1' && e[0] <= '5') ? e[0] - '0' : 5;
+  if (variant == 5 && ((d->K % BK) != 0 || (int64_t)d->M * d->lda * 2 >= (int64_t)1 << 31 ||
+                       (int64_t)d->n_seg * d->K * 2 >= (int64_t)1 << 31))
+    variant = 1;  // the quadrant pipeline needs whole K-tiles and 32-bit source offsets
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
-  if (variant == 2)
+  if (variant == 5)
+    hipLaunchKernelGGL(gemm_bf16_kernel<5>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+  else if (variant == 4)
+    hipLaunchKernelGGL(gemm_bf16_kernel<4>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+  else if (variant == 3)
+    hipLaunchKernelGGL(gemm_bf16_kernel<3>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+  else if (variant == 2)
     hipLaunchKernelGGL(gemm_bf16_kernel<2>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
   else
     hipLaunchKernelGGL(gemm_bf16_kernel<1>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
