@@ -36,7 +36,7 @@ constexpr int V_STRIDE = 192;       // bytes per V row in LDS (128 data + 64 pad
 constexpr int V_TILE_BYTES = KBLK * V_STRIDE;
 constexpr int STAGE_BYTES = K_TILE_BYTES + V_TILE_BYTES;
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;
-constexpr int DEFAULT_VARIANT = 4;
+constexpr int DEFAULT_VARIANT = 10;
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
@@ -291,6 +291,82 @@ VP_DEV void pv_half(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)[2
   }
 }
 
+// ---- C-init half tiles: the QK^T MFMA chain starts from C = -m_run (per lane = per query; Q pre-multiplied by
+// scale*log2e when loaded), so the accumulator already holds the exponent s - m and the softmax is exp2 + sum +
+// pack per score — no per-score scale/subtract FMA.  A lane rescales only when its tile max exceeds its running
+// max by more than `thr` (thr = -inf before the first tile, so the first tile always sets m; afterwards RESCALE_THR:
+// P stays <= 2^RESCALE_THR, exact in bf16's exponent range, and the ratio O / l is unchanged). ----
+constexpr float RESCALE_THR = 8.f;
+
+VP_DEV void qk_half_ci(const char* Kl, int kh, const bf16x8 (&qf)[4], const f32x16& negm, f32x16& s, int lane) {
+  const int hl = lane >> 5;
+  const int row = kh * 32 + (lane & 31);
+  const char* kr = Kl + row * 128;
+  const int sw = swz(row);
+  // two K fragments in flight at a time (8 VGPRs instead of 16: the 4-waves/SIMD budget is 128)
+  bf16x8 k0 = *(const bf16x8*)(kr + ((hl ^ sw) << 4));
+  bf16x8 k1 = *(const bf16x8*)(kr + (((2 + hl) ^ sw) << 4));
+  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[0], negm, 0, 0, 0);
+  k0 = *(const bf16x8*)(kr + (((4 + hl) ^ sw) << 4));
+  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[1], s, 0, 0, 0);
+  k1 = *(const bf16x8*)(kr + (((6 + hl) ^ sw) << 4));
+  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[2], s, 0, 0, 0);
+  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[3], s, 0, 0, 0);
+}
+
+VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f32x16& negm, f32x16 (&o)[2],
+                            bf16x8 (&pf)[2]) {
+  float m2[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int o8 = j * 8;
+    m2[j] = fmaxf(fmaxf(fmaxf(s[o8], s[o8 + 1]), s[o8 + 2]), fmaxf(fmaxf(s[o8 + 3], s[o8 + 4]), s[o8 + 5]));
+    m2[j] = fmaxf(fmaxf(m2[j], s[o8 + 6]), s[o8 + 7]);
+  }
+  float mx = fmaxf(m2[0], m2[1]);
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  }
+  if (__ballot(mx > thr) != 0ull) {  // wave-uniform: some query's tile max passed its threshold
+    const float dm = mx > thr ? mx : 0.f;
+    const float alpha = __builtin_amdgcn_exp2f(-dm);
+    l_run *= alpha;
+    m_run += dm;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o[0][i] *= alpha;
+      o[1][i] *= alpha;
+      s[i] -= dm;
+      negm[i] = -m_run;
+    }
+    thr = RESCALE_THR;
+  }
+  float ps[4];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float p = __builtin_amdgcn_exp2f(s[i]);
+    ps[i & 3] = i < 4 ? p : ps[i & 3] + p;
+    pf[i >> 3][i & 7] = f2bf(p);
+  }
+  l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+}
+
+// ---- LDS-DMA staging (global_load_lds_dwordx4, saddr + 32-bit voffset): the LDS destination is lane-linear, so
+// both images are unpadded [64 rows][128 B] and their bank swizzles are applied on the SOURCE address
+// (cdna_hip_programming.md §5.4 rule 21).  K: chunk ^ swz(row) (conflict-free ds_read_b128).  V: chunk ^
+// vswz(row) with vswz(r) = 4*((r>>1)&1): the 4-row x 16-column blocks a 32-lane half reads with
+// ds_read_b64_tr_b16 (rows r..r+3, 64 contiguous bytes) then land on 4 disjoint 16-bank groups. ----
+VP_DEV int vswz(int row) { return ((row >> 1) & 1) << 2; }
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+VP_DEV void glds16(const char* sbase, int voff, char* lds) {
+  const unsigned la = (unsigned)(uintptr_t)(lds_void_t*)lds;
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(la), "v"(voff), "s"(sbase)
+               : "memory", "m0");
+}
+
 // O = O^T accumulator / l, rounded to bf16 like the reference's SDPA output, then the optional prev-clip blend
 VP_DEV void store_out(const vp_attn_desc& d, const f32x16 (&o)[2], float l_run, int q, int b, int h, int hl,
                       bool split_sum = true) {
@@ -323,7 +399,7 @@ VP_DEV void store_out(const vp_attn_desc& d, const f32x16 (&o)[2], float l_run, 
 // workgroups share a CU, so their waves are not barrier-locked to each other and one workgroup's softmax VALU runs
 // beside the other's MFMAs.
 // ------------------------------------------------------------------------------------------------------------
-template <int NW, int OCC, int PRE, bool RS = false, bool HALF = false>
+template <int NW, int OCC, int PRE, bool RS = false, bool HALF = false, bool CINIT = false>
 __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_t(const vp_attn_desc d) {
   constexpr int NT = NW * 64;
   constexpr int QB = NW * 32;
@@ -350,6 +426,13 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_t(const vp_attn_desc d)
   bf16x8 qf[4];
 #pragma unroll
   for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
+  if constexpr (CINIT) {  // scores come out of the MFMA in log2 units
+    const float cq = d.scale * 1.4426950408889634f;
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ds][j] = f2bf(bf2f(qf[ds][j]) * cq);
+  }
 
   int k_off[CH_PER_THREAD], v_off[CH_PER_THREAD], srow[CH_PER_THREAD], sch[CH_PER_THREAD];
 #pragma unroll
@@ -406,11 +489,34 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_t(const vp_attn_desc d)
   const int g = lane >> 4;
   const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
   const int tcol = 16 * (g & 1) + 4 * (lane & 3);
+  f32x16 negm;
+  float thr = -INFINITY;
+  if constexpr (CINIT) {
+    m_run = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) negm[i] = 0.f;
+  }
 
   for (int ti = 0; ti < ntiles; ++ti) {
     const char* Kl = smem + (ti & 1) * STAGE_BYTES;
     const bool has_next = ti + 1 < ntiles;
     if (has_next) gload(ti + 1);
+    if constexpr (CINIT) {
+      Seg sg = tile_seg(d, ti, tiles1, b, h);
+      const int lim = sg.n - sg.key0;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        f32x16 sh;
+        qk_half_ci(Kl, kh, qf, negm, sh, lane);
+        if (lim < KBLK) mask_half(sh, lim, kh, hl);
+        bf16x8 pf[2];
+        softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf);
+        pv_half(Kl + K_TILE_BYTES, kh, pf, o, trow, tcol);
+      }
+      if (has_next) lstore(smem + ((ti + 1) & 1) * STAGE_BYTES);
+      __syncthreads();
+      continue;
+    }
     if constexpr (HALF) {
       Seg sg = tile_seg(d, ti, tiles1, b, h);
       const int lim = sg.n - sg.key0;
@@ -453,6 +559,126 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_t(const vp_attn_desc d)
 }
 
 
+// V^T fragments for one 32-key half from the swizzled V image (vo[dh]: this lane's byte offset of its first
+// 4-row block in the 16-key slab, constant over the slabs because vswz depends only on row bit 1)
+VP_DEV void pv_half_x(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)[2], const int (&vo)[2]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ks = kh * 2 + j;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const char* base = Vl + ks * 16 * 128 + vo[dh];
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * 128));
+      const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[j], o[dh], 0, 0, 0);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// LDS-DMA kernel: NW waves x 32 queries, 64-key tiles in a 2-slot ring filled by global_load_lds (no staging
+// registers, no LDS write pass), C-init half tiles (see softmax_half_ci).  Tile t+1 is issued at the top of tile t
+// (its slot was released by the barrier that closed tile t-1) and retired by vmcnt(0) + barrier at the bottom.
+// ------------------------------------------------------------------------------------------------------------
+template <int NW, int OCC>
+__global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc d) {
+  constexpr int QB = NW * 32;
+  constexpr int KT = KBLK * 128;  // 8 KB per K (or V) tile
+  constexpr int ST = 2 * KT;
+  constexpr int PPW = 8 / NW;     // 1-KB DMA pieces (8 rows) per wave per operand
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hl = lane >> 5;
+
+  const int nqb = (d.Nq + QB - 1) / QB;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb;
+  const int qb = t - bh * nqb;
+  const int b = bh / d.H;
+  const int h = bh - b * d.H;
+  const int tiles1 = (d.Nk + KBLK - 1) / KBLK;
+  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KBLK - 1) / KBLK : 0;
+  const int ntiles = tiles1 + tiles2;
+
+  const int q = qb * QB + wave * 32 + (lane & 31);
+  const int qc = q < d.Nq ? q : d.Nq - 1;
+  const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
+  {
+    const float cq = d.scale * 1.4426950408889634f;  // scores leave the MFMA in log2 units
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ds][j] = f2bf(bf2f(qf[ds][j]) * cq);
+  }
+
+  // this lane's DMA rows / source chunks (piece i of this wave covers tile rows (wave*PPW + i)*8 .. +7)
+  int prow[PPW], kch[PPW], vch[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    prow[i] = (wave * PPW + i) * 8 + (lane >> 3);
+    kch[i] = (lane & 7) ^ swz(prow[i]);
+    vch[i] = (lane & 7) ^ vswz(prow[i]);
+  }
+  auto issue = [&](int ti) {
+    const Seg sg = tile_seg(d, ti, tiles1, b, h);
+    char* slot = smem + (ti & 1) * ST;
+    const int last = sg.n - 1 - sg.key0;  // rows past the segment end re-read its last key (masked later)
+    const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
+    const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
+    const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int r = min(prow[i], last);
+      glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + (wave * PPW + i) * 1024);
+      glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + (wave * PPW + i) * 1024);
+    }
+  };
+
+  const int g = lane >> 4;
+  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
+  const int tcol = 16 * (g & 1) + 4 * (lane & 3);
+  int vo[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh) vo[dh] = trow * 128 + (((dh * 4 + (tcol >> 3)) ^ vswz(trow)) << 4) + (tcol & 7) * 2;
+
+  float m_run = 0.f, l_run = 0.f, thr = -INFINITY;
+  f32x16 o[2], negm;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    o[0][i] = 0.f;
+    o[1][i] = 0.f;
+    negm[i] = 0.f;
+  }
+
+  issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int ti = 0; ti < ntiles; ++ti) {
+    if (ti + 1 < ntiles) issue(ti + 1);
+    const char* Kl = smem + (ti & 1) * ST;
+    const Seg sg = tile_seg(d, ti, tiles1, b, h);
+    const int lim = sg.n - sg.key0;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      f32x16 sh;
+      qk_half_ci(Kl, kh, qf, negm, sh, lane);
+      if (lim < KBLK) mask_half(sh, lim, kh, hl);
+      bf16x8 pf[2];
+      softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf);
+      pv_half_x(Kl + KT, kh, pf, o, vo);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  store_out(d, o, l_run, q, b, h, hl);
+}
+
 }  // namespace
 
 extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
@@ -478,6 +704,12 @@ extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
       {(const void*)attn_fwd_t<8, 4, 8, false, true>, 8},         // 4: half tiles, 4 waves/SIMD (default)
       {(const void*)attn_fwd_t<4, 4, 8, false, true>, 4},         // 5: half tiles, 4-wave workgroups
       {(const void*)attn_fwd_t<8, 2, 8, true>, 8},                // 6: row sums on the MFMA
+      {(const void*)attn_fwd_t<8, 4, 8, false, true, true>, 8},   // 7: C-init half tiles, 4 waves/SIMD
+      {(const void*)attn_fwd_t<4, 3, 8, false, true, true>, 4},   // 8: C-init half tiles, 4-wave WGs, 3/SIMD
+      {(const void*)attn_fwd_t<8, 2, 8, false, true, true>, 8},   // 9: C-init half tiles, 2 waves/SIMD
+      {(const void*)attn_fwd_dma<8, 4>, 8, 4 * KBLK * 128},       // 10: LDS-DMA ring + C-init, 4 waves/SIMD
+      {(const void*)attn_fwd_dma<8, 2>, 8, 4 * KBLK * 128},       // 11: LDS-DMA ring + C-init, 2 waves/SIMD
+      {(const void*)attn_fwd_dma<4, 4>, 4, 4 * KBLK * 128},       // 12: LDS-DMA ring + C-init, 4-wave WGs
   };
 
   constexpr int NVAR = sizeof(vars) / sizeof(vars[0]);
