@@ -586,7 +586,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
   constexpr int QB = NW * 32;
   constexpr int KT = KBLK * 128;  // 8 KB per K (or V) tile
   constexpr int ST = 2 * KT;
-  constexpr int PPW = 8 / NW;     // 1-KB DMA pieces (8 rows) per wave per operand
+  constexpr int PPW = (8 + NW - 1) / NW;  // 1-KB DMA pieces (8 rows) per wave per operand (piece p -> wave p % NW)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -617,11 +617,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
       for (int j = 0; j < 8; ++j) qf[ds][j] = f2bf(bf2f(qf[ds][j]) * cq);
   }
 
-  // this lane's DMA rows / source chunks (piece i of this wave covers tile rows (wave*PPW + i)*8 .. +7)
+  // this lane's DMA rows / source chunks (piece p = wave + i*NW covers tile rows p*8 .. p*8+7)
   int prow[PPW], kch[PPW], vch[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
-    prow[i] = (wave * PPW + i) * 8 + (lane >> 3);
+    prow[i] = (wave + i * NW) * 8 + (lane >> 3);
     kch[i] = (lane & 7) ^ swz(prow[i]);
     vch[i] = (lane & 7) ^ vswz(prow[i]);
   }
@@ -634,9 +634,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
     const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
+      const int pc = wave + i * NW;
+      if (8 % NW != 0 && pc >= 8) break;  // wave-uniform
       const int r = min(prow[i], last);
-      glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + (wave * PPW + i) * 1024);
-      glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + (wave * PPW + i) * 1024);
+      glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + pc * 1024);
+      glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
     }
   };
 
@@ -656,6 +658,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
     negm[i] = 0.f;
   }
 
+  // a wave whose 32 queries all lie past Nq (the last query block of a head) only helps with the DMA and the
+  // barriers, leaving its SIMD to the co-resident workgroups
+  const bool active = qb * QB + wave * 32 < d.Nq;  // wave-uniform
   issue(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -666,6 +671,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
     const int lim = sg.n - sg.key0;
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
+      if (!active) break;
       f32x16 sh;
       qk_half_ci(Kl, kh, qf, negm, sh, lane);
       if (lim < KBLK) mask_half(sh, lim, kh, hl);
@@ -710,6 +716,8 @@ extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
       {(const void*)attn_fwd_dma<8, 4>, 8, 4 * KBLK * 128},       // 10: LDS-DMA ring + C-init, 4 waves/SIMD
       {(const void*)attn_fwd_dma<8, 2>, 8, 4 * KBLK * 128},       // 11: LDS-DMA ring + C-init, 2 waves/SIMD
       {(const void*)attn_fwd_dma<4, 4>, 4, 4 * KBLK * 128},       // 12: LDS-DMA ring + C-init, 4-wave WGs
+      {(const void*)attn_fwd_dma<5, 4>, 5, 4 * KBLK * 128},       // 13: 5-wave WGs (3 per CU: no grid tail at N=17776)
+      {(const void*)attn_fwd_dma<7, 4>, 7, 4 * KBLK * 128},       // 14: 7-wave WGs (2 per CU)
   };
 
   constexpr int NVAR = sizeof(vars) / sizeof(vars[0]);
