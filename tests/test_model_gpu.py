@@ -254,3 +254,81 @@ def test_anyl_harness_matches_reference_pipeline(env):
     assert out.shape == gold.shape
     r = rel(out, gold)
     assert r < 3e-2, r
+
+
+@torch.no_grad()
+def test_cfg_split_halves_bit_exact(env):
+    """CFG split (SURVEY.md §8e latency mode) is exact: each CFG half run alone at B=1 — what one rank of a
+    `CFGPair` computes — reproduces its half of the B=2 forward bit for bit (branch, noise prediction, hidden-state
+    list, resample mask), including the ID-resample processor with prev-window states.  Every kernel works per
+    sample and each output element's reduction order does not depend on the batch size."""
+    i, g = env["inp"], env["g"]
+    bs = env["br"](hidden_states=_d(i["video"]), encoder_hidden_states=_d(i["enc"]), branch_cond=_d(i["branch_cond"]),
+                   timestep=i["timestep"].to(dev), image_rotary_emb=i["rope"], return_dict=False)[0]
+    for model, resample in ((env["tr"], False), (env["trr"], True)):
+        kw = dict(image_rotary_emb=i["rope"], return_hidden_states=True, return_resample_mask=True,
+                  return_dict=False, id_pool_resample_learnable=resample)
+        full = model(hidden_states=_d(i["hidden"]), encoder_hidden_states=_d(i["enc"]),
+                     timestep=i["timestep"].to(dev), branch_block_samples=bs, branch_block_masks=_d(i["mask"]), **kw)
+        prev = {k: h for k, h in enumerate(full[1])}
+        full2 = model(hidden_states=_d(i["hidden2"]), encoder_hidden_states=_d(i["enc"]),
+                      timestep=i["timestep"].to(dev), branch_block_samples=bs, branch_block_masks=_d(i["mask"]),
+                      attention_kwargs={"prev_hidden_states": prev, "prev_clip_weight": 0.5,
+                                        "prev_resample_mask": full[2]}, **kw)
+        for c in range(2):
+            sl = slice(c, c + 1)
+            bsc = env["br"](hidden_states=_d(i["video"])[sl], encoder_hidden_states=_d(i["enc"])[sl],
+                            branch_cond=_d(i["branch_cond"])[sl], timestep=i["timestep"][sl].to(dev),
+                            image_rotary_emb=i["rope"], return_dict=False)[0]
+            for j in range(2):
+                assert torch.equal(bsc[j], bs[j][sl]), ("branch", c, j)
+            half = model(hidden_states=_d(i["hidden"])[sl], encoder_hidden_states=_d(i["enc"])[sl],
+                         timestep=i["timestep"][sl].to(dev), branch_block_samples=bsc,
+                         branch_block_masks=_d(i["mask"])[sl], **kw)
+            assert torch.equal(half[0], full[0][sl]), ("noise_pred", resample, c)
+            assert all(torch.equal(a, b[sl]) for a, b in zip(half[1], full[1])), ("hidden states", resample, c)
+            assert torch.equal(half[2], full[2][sl])
+            half2 = model(hidden_states=_d(i["hidden2"])[sl], encoder_hidden_states=_d(i["enc"])[sl],
+                          timestep=i["timestep"][sl].to(dev), branch_block_samples=bsc,
+                          branch_block_masks=_d(i["mask"])[sl],
+                          attention_kwargs={"prev_hidden_states": {k: h[sl] for k, h in prev.items()},
+                                            "prev_clip_weight": 0.5, "prev_resample_mask": full[2][sl]}, **kw)
+            assert torch.equal(half2[0], full2[0][sl]), ("noise_pred prev-window", resample, c)
+
+
+@torch.no_grad()
+def test_pipelined_window_chain_driver_matches_serial(env):
+    """`run_any_length_pipelined` (the config-4 stage pipeline driver) on a 1-rank group reproduces the serial
+    harness bit for bit on the HIP models (the multi-rank hand-offs themselves are covered by the gloo tests)."""
+    import socket
+    import torch.distributed as dist
+    from videopainter_amd.distributed import WindowStages
+    from videopainter_amd.pipeline import CogVideoXI2VDualInpaintAnyLHarness, run_any_length_pipelined
+    from videopainter_amd.scheduler import CogVideoXDPMScheduler
+    from tests.golden.cases import pipe_inputs
+    g = load_file(os.path.join(GOLD, "pipe_tiny.safetensors"))
+    c = PIPE_CASE
+    mk = lambda: CogVideoXDPMScheduler(snr_shift_scale=1.0, prediction_type="v_prediction",  # noqa: E731
+                                       rescale_betas_zero_snr=True, clip_sample=False, set_alpha_to_one=True,
+                                       timestep_spacing="trailing")
+    windows = [dict(latents=g[f"w{w}.latents"], image_latents=g[f"w{w}.image_latents"], noise=g[f"w{w}.noise"],
+                    video_latents=g[f"w{w}.video_latents"], mask=g[f"w{w}.mask"],
+                    masked_video_latents=g[f"w{w}.masked_video_latents"]) for w in range(2)]
+    inp = pipe_inputs()
+    kw = dict(num_inference_steps=c["steps"], num_frames=c["num_frames"], stride=c["stride"],
+              prev_clip_weight=c["prev_clip_weight"], id_pool_resample_learnable=c["id_pool_resample_learnable"])
+    ref = CogVideoXI2VDualInpaintAnyLHarness(env["trr"], env["br"], mk())(
+        windows, inp["prompt_embeds"], inp["negative_prompt_embeds"], generator=torch.Generator().manual_seed(7), **kw)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        h = CogVideoXI2VDualInpaintAnyLHarness(env["trr"], env["br"], mk())
+        vids = run_any_length_pipelined(h, WindowStages(), [{"windows": windows,
+                                                             "generator": torch.Generator().manual_seed(7)}],
+                                        inp["prompt_embeds"], inp["negative_prompt_embeds"], **kw)
+    finally:
+        dist.destroy_process_group()
+    assert torch.equal(vids[0], ref)

@@ -3,14 +3,20 @@
 What shards:
   * independent clips (configs 2/3 scaled to N GPUs): data-parallel replicas — weights broadcast once from rank 0,
     no per-step collective ("weak" scaling);
-  * the any-length window chain (config 4) does NOT shard a single clip: window k needs window k-1's final latents
-    and last-step hidden states (anyl.py:866-872, 962-988), so it stays serial on one rank.
+  * the two CFG halves of one clip (latency mode, `CFGPair`): each rank of a pair runs B=1; one all-gather of the
+    fp32/bf16 noise prediction [1,13,16,60,90] per step; both ranks then run the identical CFG + DPM step;
+  * the any-length window chain (config 4, `WindowStages`): window k needs window k-1's final latents and, with
+    prev_clip_weight > 0, its last-step 42-layer hidden states (anyl.py:866-872, 962-988), so a single clip is a
+    serial chain.  It is placed as a pipeline — window w on stage w % S, S = world / (2 if CFG-split else 1) — with a
+    point-to-point hand-off (latents + hidden states + resample mask, ncclSend/Recv over xGMI) between consecutive
+    stages, so several clips stream through the stages concurrently; at the end every rank all-gathers the
+    windows' latents and averages the overlaps exactly as the serial loop does (anyl.py:1052-1069).
 Collectives here are issued in large flat buckets (few, big messages suit point-to-point xGMI rings).
 """
 from __future__ import annotations
 
 import os
-from typing import Iterable, List
+from typing import Callable, Dict, Iterable, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -82,3 +88,170 @@ def barrier(device=None):
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# CFG split: one clip on a pair of ranks
+# ----------------------------------------------------------------------------------------------------------------
+
+def _pair_groups(world: int, size: int):
+    """Every rank must create every group (torch.distributed.new_group contract)."""
+    groups = []
+    for p in range(world // size):
+        groups.append(dist.new_group(list(range(p * size, (p + 1) * size))))
+    return groups
+
+
+class CFGPair:
+    """Ranks (2p, 2p+1) share one clip: cfg_index 0 runs the unconditional half of the CFG batch, 1 the text half
+    (the order of `torch.cat([negative_prompt_embeds, prompt_embeds])`, anyl.py:805-806)."""
+
+    def __init__(self, group=None, cfg_index: Optional[int] = None):
+        rank, world = dist.get_rank(), dist.get_world_size()
+        if group is None:
+            if world % 2:
+                raise ValueError(f"CFG split needs an even world size, got {world}")
+            group = _pair_groups(world, 2)[rank // 2]
+        self.group = group
+        self.cfg_index = rank % 2 if cfg_index is None else cfg_index
+        self.backend = dist.get_backend(group)
+
+    def allgather(self, half: torch.Tensor) -> torch.Tensor:
+        """[1, ...] on each rank of the pair -> [2, ...] = (uncond, text) on both."""
+        if half.shape[0] != 1:
+            raise ValueError("each CFG rank holds a batch of 1")
+        half = half.contiguous()
+        out = torch.empty((2,) + tuple(half.shape[1:]), dtype=half.dtype, device=half.device)
+        if self.backend == "nccl":
+            dist.all_gather_into_tensor(out, half, group=self.group)
+        else:
+            dist.all_gather([out[0:1], out[1:2]], half, group=self.group)
+        return out
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# any-length window chain as a pipeline over stages
+# ----------------------------------------------------------------------------------------------------------------
+
+class WindowStages:
+    """Stage placement of the window chain: S = world / cfg stages; rank = stage * cfg + cfg_index."""
+
+    def __init__(self, cfg_split: bool = False):
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.cfg = 2 if cfg_split else 1
+        if self.world % self.cfg:
+            raise ValueError(f"world size {self.world} is not a multiple of the CFG group size {self.cfg}")
+        self.stages = self.world // self.cfg
+        self.stage = self.rank // self.cfg
+        self.cfg_index = self.rank % self.cfg
+        self.pair = CFGPair() if cfg_split else None
+
+    def stage_of(self, window: int) -> int:
+        return window % self.stages
+
+    def peer(self, stage: int) -> int:
+        """The rank of `stage` that holds this rank's CFG half."""
+        return stage * self.cfg + self.cfg_index
+
+    # hand-off payload: latents [1,F,C,h,w]; last-step hidden states {layer: [b,N,D]}; resample mask [b,N] bool;
+    # the CPU generator's state (the reference draws every window's scheduler noise from ONE generator, so the
+    # next window continues the stream exactly where this one stopped)
+    def send_handoff(self, dst_stage: int, latents: torch.Tensor, states: Optional[dict],
+                     mask: Optional[torch.Tensor], generator: Optional[torch.Generator] = None) -> None:
+        dst = self.peer(dst_stage)
+        dev = latents.device
+        dist.send(latents.contiguous(), dst)
+        gs = generator.get_state() if generator is not None else None
+        flags = torch.tensor([0 if states is None else len(states), 0 if mask is None else 1,
+                              0 if gs is None else gs.numel()], dtype=torch.int64, device=dev)
+        dist.send(flags, dst)
+        if states is not None:
+            for k in sorted(states):
+                dist.send(states[k].contiguous(), dst)
+        if mask is not None:
+            dist.send(mask.to(torch.uint8).contiguous(), dst)
+        if gs is not None:
+            dist.send(gs.to(dev), dst)
+
+    def recv_handoff(self, src_stage: int, lat_like: torch.Tensor, state_shape, mask_shape,
+                     generator: Optional[torch.Generator] = None):
+        src = self.peer(src_stage)
+        dev = lat_like.device
+        lat = torch.empty_like(lat_like)
+        dist.recv(lat, src)
+        flags = torch.empty(3, dtype=torch.int64, device=dev)
+        dist.recv(flags, src)
+        n_states, has_mask, gs_n = (int(x) for x in flags.tolist())
+        states = None
+        if n_states:
+            states = {}
+            for k in range(n_states):
+                t = torch.empty(state_shape, dtype=lat_like.dtype, device=dev)
+                dist.recv(t, src)
+                states[k] = t
+        mask = None
+        if has_mask:
+            m = torch.empty(mask_shape, dtype=torch.uint8, device=dev)
+            dist.recv(m, src)
+            mask = m.bool()
+        if gs_n:
+            g = torch.empty(gs_n, dtype=torch.uint8, device=dev)
+            dist.recv(g, src)
+            if generator is None:
+                raise ValueError("the previous stage handed off a generator state but this rank has no generator")
+            generator.set_state(g.cpu())
+        return lat, states, mask
+
+    def gather_windows(self, local: Dict[int, torch.Tensor], n_windows: int, like: torch.Tensor) -> List[torch.Tensor]:
+        """All-gather every window's final latents (each stage holds the windows placed on it)."""
+        if self.world == 1:
+            return [local[w] for w in range(n_windows)]
+        per = (n_windows + self.stages - 1) // self.stages
+        buf = torch.zeros((per,) + tuple(like.shape), dtype=like.dtype, device=like.device)
+        for w, t in local.items():
+            buf[w // self.stages] = t
+        allb = torch.empty((self.world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
+        if dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(allb, buf)
+        else:
+            dist.all_gather(list(allb.unbind(0)), buf)
+        return [allb[self.peer(self.stage_of(w))][w // self.stages] for w in range(n_windows)]
+
+
+def run_window_chain(stages: WindowStages, clips: List[dict], run_window: Callable, image_latents_for: Callable,
+                     assemble: Callable, lat_like: torch.Tensor, state_shape, mask_shape) -> List[torch.Tensor]:
+    """Pipeline-parallel any-length loop over several clips.
+
+    clips[j] = {"windows": [...], "generator": torch.Generator or None};
+    run_window(j, w, win, image_latents, prev_states, prev_mask, capture) -> (latents, states, mask);
+    image_latents_for(w, win, prev_latents) -> conditioning latents; assemble(list of window latents) -> video.
+    lat_like: a device tensor shaped/typed like one window's latents.  Each stage walks the clips in order and,
+    within a clip, its own windows in order, so every receive waits only on an earlier window of the same clip (no
+    cycle, hence no deadlock, for any window count).  Returns the assembled video of every clip on every rank."""
+    videos = []
+    for j, clip in enumerate(clips):
+        wins = clip["windows"]
+        gen = clip.get("generator")
+        n = len(wins)
+        local = {}
+        carry = (None, None, None)  # hand-off between two windows placed on the same stage stays in place
+        for w in range(n):
+            if stages.stage_of(w) != stages.stage:
+                continue
+            prev_lat, prev_states, prev_mask = None, None, None
+            if w > 0:
+                if stages.stage_of(w - 1) == stages.stage:
+                    prev_lat, prev_states, prev_mask = carry
+                else:
+                    prev_lat, prev_states, prev_mask = stages.recv_handoff(stages.stage_of(w - 1), lat_like,
+                                                                           state_shape, mask_shape, gen)
+            img = image_latents_for(w, wins[w], prev_lat)
+            lat, states, mask = run_window(j, w, wins[w], img, prev_states, prev_mask, w < n - 1)
+            if w < n - 1:
+                if stages.stage_of(w + 1) == stages.stage:
+                    carry = (lat, states, mask)
+                else:
+                    stages.send_handoff(stages.stage_of(w + 1), lat, states, mask, gen)
+            local[w] = lat
+        videos.append(assemble(stages.gather_windows(local, n, lat_like)))
+    return videos

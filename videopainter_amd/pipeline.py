@@ -44,13 +44,17 @@ class WindowState:
 
 class CogVideoXI2VDualInpaintAnyLHarness:
     def __init__(self, transformer, branch, scheduler, vae_scale_factor_spatial: int = 8,
-                 vae_scale_factor_temporal: int = 4):
+                 vae_scale_factor_temporal: int = 4, cfg_pair=None):
+        """cfg_pair: optional `distributed.CFGPair`.  The two CFG halves of every step then run on the pair's two
+        ranks at B=1 and their noise predictions are all-gathered (latency mode); both ranks apply the
+        same CFG combine + DPM step with the same generator stream, so their latents stay bit-identical."""
         self.transformer = transformer
         self.branch = branch
         self.scheduler = scheduler
         self.vae_scale_factor_spatial = vae_scale_factor_spatial
         self.vae_scale_factor_temporal = vae_scale_factor_temporal
         self.prev_resample_mask = None
+        self.cfg_pair = cfg_pair
 
     @property
     def device(self):
@@ -94,10 +98,17 @@ class CogVideoXI2VDualInpaintAnyLHarness:
         t_int = int(t)
         dev = self.device
         lat = st.latents
-        lvi = torch.cat([lat] * 2)
-        lmi = torch.cat([lvi, st.image_in], dim=2)
-        ts = torch.full((2,), t_int, device=dev, dtype=torch.int64)
-        bs = self.branch(hidden_states=lvi, encoder_hidden_states=prompt_embeds, branch_cond=st.branch_in,
+        # CFG batch (anyl.py:937-945); with a CFG pair this rank runs only its own half at B=1
+        if self.cfg_pair is None:
+            nb, sl = 2, slice(0, 2)
+        else:
+            c = self.cfg_pair.cfg_index
+            nb, sl = 1, slice(c, c + 1)
+        lvi = torch.cat([lat] * nb)
+        lmi = torch.cat([lvi, st.image_in[sl]], dim=2)
+        pe = prompt_embeds[sl]
+        ts = torch.full((nb,), t_int, device=dev, dtype=torch.int64)
+        bs = self.branch(hidden_states=lvi, encoder_hidden_states=pe, branch_cond=st.branch_in[sl],
                          conditioning_scale=conditioning_scale, timestep=ts, image_rotary_emb=rope,
                          attention_kwargs=attention_kwargs, return_dict=False)[0]
         akw = dict(attention_kwargs) if attention_kwargs else {}
@@ -106,13 +117,16 @@ class CogVideoXI2VDualInpaintAnyLHarness:
             akw["prev_clip_weight"] = prev_clip_weight
             akw["prev_resample_mask"] = self.prev_resample_mask
         noise_pred, hs_list, self.prev_resample_mask = self.transformer(
-            hidden_states=lmi, encoder_hidden_states=prompt_embeds, branch_block_samples=bs, timestep=ts,
+            hidden_states=lmi, encoder_hidden_states=pe, branch_block_samples=bs, timestep=ts,
             image_rotary_emb=rope, attention_kwargs=akw, add_first=add_first,
-            branch_block_masks=st.mask1 if mask_add else None, id_pool_resample_learnable=id_pool_resample_learnable,
+            branch_block_masks=st.mask1[sl] if mask_add else None,
+            id_pool_resample_learnable=id_pool_resample_learnable,
             return_hidden_states=True, return_resample_mask=True, return_dict=False)
         if capture_last_states and t_int == int(timesteps[-1]):
             st.last_states = {k: h for k, h in enumerate(hs_list)}
         del hs_list, bs
+        if self.cfg_pair is not None:
+            noise_pred = self.cfg_pair.allgather(noise_pred.contiguous())  # [2, F, C, h, w] = (uncond, text)
         n_steps = len(timesteps)
         g = guidance_scale
         if use_dynamic_cfg:
@@ -159,6 +173,81 @@ class CogVideoXI2VDualInpaintAnyLHarness:
         st.old_pred = pred
 
     # ------------------------------------------------------------------------------------------------------------
+    def frame_layout(self, n_windows: int, num_frames: int, stride: int, latent_frames: int):
+        """Latent-frame count of the whole clip and the first latent frame of each window (anyl.py:828-842,
+        1052-1064)."""
+        vt = self.vae_scale_factor_temporal
+        if stride < num_frames:
+            nfl = ((num_frames - 1) // vt + 1) * n_windows - (n_windows - 1) * ((num_frames - stride) // vt + 1)
+        elif stride == num_frames:
+            nfl = ((num_frames - 1) // vt) * n_windows + 1
+        else:
+            raise ValueError(f"stride: {stride}, num_frames: {num_frames}")
+        starts = []
+        for w in range(n_windows):
+            start = w * latent_frames
+            if w > 0 and stride < num_frames:
+                start -= (int((num_frames - stride) // vt) + 1) * w
+            elif w > 0 and stride == num_frames:
+                start -= w
+            starts.append(start)
+        return nfl, starts
+
+    def window_image_latents(self, w: int, win: dict, prev_latents: Optional[torch.Tensor], num_frames: int,
+                             stride: int) -> torch.Tensor:
+        """Window 0 conditions on the encoded first frame; window k>0 on the previous window's latent frame at the
+        overlap boundary (anyl.py:862-872)."""
+        if w == 0:
+            return win["image_latents"]
+        back = int((num_frames - stride) // self.vae_scale_factor_temporal)
+        img = prev_latents[:, -back - 1:-back + 1 - 1] if -back < 0 else prev_latents[:, -1:]
+        C, hh, ww = prev_latents.shape[2:]
+        pad = torch.zeros(1, prev_latents.shape[1] - 1, C, hh, ww, device=self.device, dtype=BF16)
+        return torch.cat([img, pad], dim=1)
+
+    @torch.no_grad()
+    def run_window(self, w: int, win: dict, image_latents: torch.Tensor, prompt_embeds_cfg: torch.Tensor,
+                   timesteps: torch.Tensor, *, prev_states=None, prev_mask=None, capture: bool = False,
+                   guidance_scale: float = 6.0, use_dynamic_cfg: bool = True, conditioning_scale: float = 1.0,
+                   replace_gt: bool = True, mask_add: bool = True, prev_clip_weight: float = 0.0,
+                   id_pool_resample_learnable: bool = False, add_first: bool = False,
+                   step_noise: Optional[Callable[[], torch.Tensor]] = None, generator=None):
+        """All denoising steps of one window (anyl.py:933-1050).  Returns (latents, last-step hidden states or
+        None, the transformer's last resample mask) — the hand-off the next window needs."""
+        st = self.make_window(win["latents"], image_latents, win["masked_video_latents"], win["mask"],
+                              win.get("video_latents"), win.get("noise"))
+        hh, ww = st.latents.shape[3], st.latents.shape[4]
+        rope = self.rope_for(st.latents.shape[1], hh, ww)
+        self.prev_resample_mask = prev_mask
+        for i in range(len(timesteps)):
+            self.step(st, i, timesteps, prompt_embeds_cfg, rope, guidance_scale=guidance_scale,
+                      use_dynamic_cfg=use_dynamic_cfg, conditioning_scale=conditioning_scale, replace_gt=replace_gt,
+                      mask_add=mask_add, add_first=add_first, id_pool_resample_learnable=id_pool_resample_learnable,
+                      prev_window_states=prev_states if w > 0 else None, prev_clip_weight=prev_clip_weight,
+                      capture_last_states=capture, step_noise=step_noise, generator=generator)
+        return st.latents, (st.last_states if capture else None), self.prev_resample_mask
+
+    def assemble(self, window_latents: List[torch.Tensor], num_frames: int, stride: int) -> torch.Tensor:
+        """Overlap-averaged latent video [1, F_total, C, h, w] (anyl.py:1052-1069)."""
+        lat0 = window_latents[0]
+        Fw, C, hh, ww = lat0.shape[1:]
+        nfl, starts = self.frame_layout(len(window_latents), num_frames, stride, Fw)
+        acc = torch.zeros(1, nfl, C, hh, ww, device=lat0.device, dtype=BF16)
+        counts = torch.zeros(nfl)
+        for latents, start in zip(window_latents, starts):
+            for i in range(Fw):
+                acc[:, start + i] += latents[:, i]
+                counts[start + i] += 1
+        for i in range(nfl):
+            if counts[i] > 0:
+                acc[:, i] /= counts[i]
+        return acc
+
+    def prepare_call(self, prompt_embeds, negative_prompt_embeds, num_inference_steps: int):
+        pe = torch.cat([negative_prompt_embeds, prompt_embeds], dim=0).to(self.device, BF16).contiguous()
+        self.scheduler.set_timesteps(num_inference_steps)
+        return pe, self.scheduler.timesteps.cpu()
+
     @torch.no_grad()
     def __call__(self, windows: List[dict], prompt_embeds: torch.Tensor, negative_prompt_embeds: torch.Tensor, *,
                  num_inference_steps: int = 50, num_frames: int = 49, stride: Optional[int] = None,
@@ -169,56 +258,53 @@ class CogVideoXI2VDualInpaintAnyLHarness:
         """Window loop (anyl.py:759-1069) with output_type="latent".  windows[k] holds what prepare_latents /
         prepare_mask_latents produced for window k: latents, noise, video_latents, mask, masked_video_latents, and
         (window 0 only) image_latents.  Returns the overlap-averaged latent video [1, F_total, C, h, w]."""
-        dev = self.device
         stride = num_frames if stride is None else stride
-        pe = torch.cat([negative_prompt_embeds, prompt_embeds], dim=0).to(dev, BF16).contiguous()
-        self.scheduler.set_timesteps(num_inference_steps)
-        timesteps = self.scheduler.timesteps.cpu()
+        pe, timesteps = self.prepare_call(prompt_embeds, negative_prompt_embeds, num_inference_steps)
         n_windows = len(windows)
-        vt = self.vae_scale_factor_temporal
-        if stride < num_frames:
-            nfl = ((num_frames - 1) // vt + 1) * n_windows - (n_windows - 1) * ((num_frames - stride) // vt + 1)
-        elif stride == num_frames:
-            nfl = ((num_frames - 1) // vt) * n_windows + 1
-        else:
-            raise ValueError(f"stride: {stride}, num_frames: {num_frames}")
-        lat0 = windows[0]["latents"]
-        C, hh, ww = lat0.shape[2], lat0.shape[3], lat0.shape[4]
-        acc = torch.zeros(1, nfl, C, hh, ww, device=dev, dtype=BF16)
-        counts = torch.zeros(nfl)
-        prev_states = None
-        latents = None
-        self.prev_resample_mask = None
+        self.frame_layout(n_windows, num_frames, stride, windows[0]["latents"].shape[1])  # validates stride
+        kw = dict(guidance_scale=guidance_scale, use_dynamic_cfg=use_dynamic_cfg, conditioning_scale=conditioning_scale,
+                  replace_gt=replace_gt, mask_add=mask_add, prev_clip_weight=prev_clip_weight,
+                  id_pool_resample_learnable=id_pool_resample_learnable, add_first=add_first, step_noise=step_noise,
+                  generator=generator)
+        outs = []
+        latents, states, mask = None, None, None
         for w, win in enumerate(windows):
-            if w == 0:
-                image_latents = win["image_latents"]
-            else:
-                back = int((num_frames - stride) // vt)
-                img = latents[:, -back - 1:-back + 1 - 1] if -back < 0 else latents[:, -1:]
-                pad = torch.zeros(1, latents.shape[1] - 1, C, hh, ww, device=dev, dtype=BF16)
-                image_latents = torch.cat([img, pad], dim=1)
-            st = self.make_window(win["latents"], image_latents, win["masked_video_latents"], win["mask"],
-                                  win.get("video_latents"), win.get("noise"))
-            rope = self.rope_for(st.latents.shape[1], hh, ww)
-            for i in range(len(timesteps)):
-                self.step(st, i, timesteps, pe, rope, guidance_scale=guidance_scale, use_dynamic_cfg=use_dynamic_cfg,
-                          conditioning_scale=conditioning_scale, replace_gt=replace_gt, mask_add=mask_add,
-                          add_first=add_first, id_pool_resample_learnable=id_pool_resample_learnable,
-                          prev_window_states=prev_states if w > 0 else None, prev_clip_weight=prev_clip_weight,
-                          capture_last_states=w < n_windows - 1, step_noise=step_noise, generator=generator)
-            latents = st.latents
-            if w < n_windows - 1:
-                prev_states = st.last_states
-            Fw = latents.shape[1]
-            for i in range(Fw):
-                start = w * Fw
-                if w > 0 and stride < num_frames:
-                    start -= (int((num_frames - stride) // vt) + 1) * w
-                elif w > 0 and stride == num_frames:
-                    start -= w
-                acc[:, start + i] += latents[:, i]
-                counts[start + i] += 1
-        for i in range(nfl):
-            if counts[i] > 0:
-                acc[:, i] /= counts[i]
-        return acc
+            img = self.window_image_latents(w, win, latents, num_frames, stride)
+            latents, states, mask = self.run_window(w, win, img, pe, timesteps, prev_states=states, prev_mask=mask,
+                                                    capture=w < n_windows - 1, **kw)
+            outs.append(latents)
+        return self.assemble(outs, num_frames, stride)
+
+
+@torch.no_grad()
+def run_any_length_pipelined(harness: CogVideoXI2VDualInpaintAnyLHarness, stages, clips: List[dict],
+                             prompt_embeds: torch.Tensor, negative_prompt_embeds: torch.Tensor, *,
+                             num_inference_steps: int = 50, num_frames: int = 49, stride: Optional[int] = None,
+                             **kw) -> List[torch.Tensor]:
+    """The any-length loop of `CogVideoXI2VDualInpaintAnyLHarness.__call__` for several clips on a multi-rank
+    stage pipeline (`distributed.WindowStages`, SURVEY.md §8e config 4): window w of every clip runs on stage w % S;
+    consecutive stages hand off (final latents, last-step hidden states, resample mask, generator state); with
+    `WindowStages(cfg_split=True)` each stage is a CFG pair exchanging one noise prediction per step.  Same result
+    as running the clips one after another through `harness(...)` with clip j's generator."""
+    from .distributed import run_window_chain
+    stride = num_frames if stride is None else stride
+    harness.cfg_pair = stages.pair
+    pe, timesteps = harness.prepare_call(prompt_embeds, negative_prompt_embeds, num_inference_steps)
+    first = clips[0]["windows"][0]["latents"]
+    cfg = harness.transformer.config
+    p = cfg.patch_size
+    _, F, C, hh, ww = first.shape
+    ntok = pe.shape[1] + F * (hh // p) * (ww // p)
+    rows = 1 if stages.pair is not None else 2
+    lat_like = torch.empty(tuple(first.shape), device=harness.device, dtype=BF16)
+    state_shape = (rows, ntok, cfg.num_attention_heads * cfg.attention_head_dim)
+    mask_shape = (rows, ntok)
+
+    def rw(j, w, win, img, prev_states, prev_mask, capture):
+        return harness.run_window(w, win, img, pe, timesteps, prev_states=prev_states, prev_mask=prev_mask,
+                                  capture=capture, generator=clips[j].get("generator"), **kw)
+
+    return run_window_chain(stages, clips, rw,
+                            lambda w, win, prev: harness.window_image_latents(w, win, prev, num_frames, stride),
+                            lambda lats: harness.assemble(lats, num_frames, stride), lat_like, state_shape,
+                            mask_shape)
