@@ -26,9 +26,9 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 1
+#define VP_ABI_VERSION 2
 int vp_abi_version(void);
-/* sizeof of the descriptor structs as compiled into the library: out[0..2] = gemm, attn, dpm (ABI self-check) */
+/* sizeof of the descriptor structs as compiled into the library: out[0..3] = gemm, attn, dpm, gemm_mx (ABI check) */
 void vp_struct_sizes(int64_t* out);
 
 /* ---------------------------------------------------------------------------------------------------------------
@@ -86,6 +86,48 @@ typedef struct vp_gemm_desc {
 int vp_gemm_bf16(const vp_gemm_desc* d, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
+ * MX-FP8 (OCP e4m3 elements, one E8M0 power-of-two scale per 32 consecutive K elements) — the fp8 path of
+ * BASELINE config 5.  The same projections as vp_gemm_bf16 (FeedForward net.0.proj / net.2,
+ * DF/models/attention.py:1177,1191), on gfx950's block-scaled MFMA (v_mfma_scale_f32_16x16x128_f8f6f4: 2x the
+ * bf16 MFMA rate; the hardware applies the scales, so the accumulator is the dequantised dot product).
+ *
+ * Data layout of an MX tensor with R rows and K columns (K % 128 == 0):
+ *   elements: uint8 e4m3 [R][K] at row stride ld (bytes);
+ *   scales:   uint8 E8M0 (value 2^(s-127)) in 256-row x 128-column tiles of 1 KiB, tile (R/256, K/128) at
+ *             byte ((r >> 8) * (K / 128) + (k >> 7)) * 1024, and inside it block b = (k >> 5) & 3 of row r at
+ *             b * 256 + (r & 15) * 16 + ((r >> 4) & 15) — one GEMM K-step's scales are one contiguous 1 KiB
+ *             LDS-DMA, and a lane's scales for 4 consecutive 16-row fragments are one aligned dword.
+ *             Size: ceil(R / 256) * (K / 128) * 1024 bytes.
+ * Quantisation of a 32-element block x: s = ceil(log2(amax|x| / 448)) (clamped to [-127, 127]),
+ * q = RNE_e4m3(x * 2^-s) (|q| <= 448, no clipping), scale byte s + 127 (0 for an all-zero block).
+ * ------------------------------------------------------------------------------------------------------------- */
+#define VP_MX_BLOCK 32
+int64_t vp_mx_scale_bytes(int64_t rows, int64_t K);
+
+/* rows x K bf16 (row stride ld_in elements) -> MX e4m3 (row stride ld_out bytes) + scales (layout above) */
+int vp_mx_quantize_bf16(const void* x, int64_t ld_in, void* q, int64_t ld_out, void* scales, int32_t rows, int32_t K,
+                        void* stream);
+
+/* out = epilogue(A · Wᵀ) with A and W in MX-FP8.  base: as vp_gemm_desc with A / W[] pointing at the e4m3
+ * elements (lda in BYTES; W rows are K bytes), epilogues VP_EPI_BIAS .. VP_EPI_BIAS_ADDROWS writing bf16 C, or
+ * VP_EPI_BIAS_GELU_MXFP8: C = MX-quantise(rnd(gelu_tanh(rnd(acc + bias)))) written as e4m3 [M][N] (ldc in bytes)
+ * plus c_scale (the FF1 -> FF2 hand-off stays in fp8).  K % 128 == 0, N % 256 == 0. */
+#define VP_EPI_BIAS_GELU_MXFP8 5
+typedef struct vp_gemm_mx_desc {
+  vp_gemm_desc base;
+  const void* a_scale;
+  const void* w_scale[3];
+  void* c_scale;
+} vp_gemm_mx_desc;
+
+int vp_gemm_mx_fp8(const vp_gemm_mx_desc* d, void* stream);
+
+/* layout self-test of one block-scaled MFMA (one wave): A, B e4m3 [16][128] row-major, per-lane scale bytes sa/sb
+ * [64]: lane l feeds K-chunks l/16 and l/16+4 (16 bytes each) of row l%16 and the scale of row l%16, K-block l/16;
+ * C fp32 [16][16] = Σ_k A[i][k]·2^(sa[i+16(k/32)]-127) · B[j][k]·2^(sb[j+16(k/32)]-127) */
+int vp_mx_mfma_probe(const void* A, const void* B, const void* sa, const void* sb, float* C, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
  * Flash attention forward, head_dim 64, non-causal, no mask — replaces F.scaled_dot_product_attention in
  * CogVideoXAttnProcessor2_0 (DF/models/attention_processor.py:2177-2197) and CogVideoXAttnProcessor2_0_resample
  * (:2283-2290; the doubled K/V is passed as two segments instead of being concatenated).
@@ -120,6 +162,11 @@ int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream);
 int vp_adaln_modulate_bf16(const void* x, void* y, int32_t B, int32_t Ntok, int32_t D, int32_t text_len,
                            const void* ln_w, const void* ln_b, float eps, const void* mod, int64_t mod_bstride,
                            void* stream);
+/* the same, writing the modulated rows as MX-FP8 (q: e4m3 [B*Ntok][D], scales: MX layout with R = B*Ntok, K = D)
+ * — the input of the fp8 FeedForward (BASELINE config 5).  D % 128 == 0. */
+int vp_adaln_modulate_mx_fp8(const void* x, void* q, void* scales, int32_t B, int32_t Ntok, int32_t D,
+                             int32_t text_len, const void* ln_w, const void* ln_b, float eps, const void* mod,
+                             int64_t mod_bstride, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * Per-head LayerNorm(64) + interleaved-pair RoPE — attn.norm_q / norm_k (attention_processor.py:2143-2146) and

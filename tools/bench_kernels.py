@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--gemm-variants", default="1,2")
     ap.add_argument("--variant", default="", help="attention kernel variant(s), e.g. 1 or 1,3")
-    ap.add_argument("--only", default="", help="attention | gemm: run just that kernel (for rocprofv3 --pmc passes)")
+    ap.add_argument("--only", default="", help="attention | gemm | mx: run just that kernel (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
     dev = "cuda"
     B, T, Nv, D, H = 2, 226, 17550, 3072, 48
@@ -46,6 +46,30 @@ def main():
     shapes = [("qkv", 3 * D, D), ("out", D, D), ("ff1", 4 * D, D), ("ff2", D, 4 * D)]
     if args.only == "attention":
         shapes = []
+    if args.only == "mx":
+        # MX-FP8 FeedForward GEMMs (BASELINE config 5 path) next to their bf16 versions, interleaved
+        from videopainter_amd import _native as NN
+        for rnd in range(2):
+            for name, Nn, Kk in (("ff1", 4 * D, D), ("ff2", D, 4 * D)):
+                a16 = torch.randn(M, Kk, device=dev).to(torch.bfloat16)
+                w16 = (torch.randn(Nn, Kk, device=dev) * Kk ** -0.5).to(torch.bfloat16)
+                b = torch.randn(Nn, device=dev).to(torch.bfloat16) * 0.1
+                A, W = K.mx_quantize(a16), K.mx_quantize(w16)
+                out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+                t = timeit(lambda: K.gemm_mx(A, [W], [b], out), args.iters)
+                res[f"mx_{name}_r{rnd}"] = dict(ms=t * 1e3, tflops=2 * M * Nn * Kk / t / 1e12)
+                print("gemm mxfp8", name, res[f"mx_{name}_r{rnd}"], flush=True)
+                if name == "ff1":
+                    H = K.MXTensor(M, Nn, dev)
+                    t = timeit(lambda: K.gemm_mx(A, [W], [b], H, epilogue=NN.EPI_BIAS_GELU_MXFP8), args.iters)
+                    res[f"mx_ff1_gelu_mx_r{rnd}"] = dict(ms=t * 1e3, tflops=2 * M * Nn * Kk / t / 1e12)
+                    print("gemm mxfp8 ff1+gelu->mx", res[f"mx_ff1_gelu_mx_r{rnd}"], flush=True)
+                t = timeit(lambda: K.gemm(a16, [w16], [b], out), args.iters)
+                res[f"bf16_{name}_r{rnd}"] = dict(ms=t * 1e3, tflops=2 * M * Nn * Kk / t / 1e12)
+                print("gemm bf16", name, res[f"bf16_{name}_r{rnd}"], flush=True)
+                del a16, w16, A, W, out
+        print(json.dumps(res))
+        return
     for name, Nn, Kk in shapes:
         w = (torch.randn(Nn, Kk, device=dev) * Kk ** -0.5).to(torch.bfloat16)
         b = torch.randn(Nn, device=dev).to(torch.bfloat16) * 0.1

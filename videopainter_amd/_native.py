@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -45,6 +45,10 @@ class AttnDesc(C.Structure):
                 ("scale", f32), ("out_scale", f32), ("accumulate", i32), ("pad", i32)]
 
 
+class GemmMxDesc(C.Structure):
+    _fields_ = [("base", GemmDesc), ("a_scale", vp), ("w_scale", vp * 3), ("c_scale", vp)]
+
+
 class DpmDesc(C.Structure):
     _fields_ = [("n", i64), ("noise_pred", vp), ("do_cfg", i32), ("guidance", f32), ("model_output", vp),
                 ("sample", vp), ("old_pred", vp), ("pred_out", vp), ("noise1", vp), ("noise2", vp),
@@ -55,13 +59,18 @@ class DpmDesc(C.Structure):
                 ("prev_out", vp)]
 
 
-EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS = range(5)
+EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS, EPI_BIAS_GELU_MXFP8 = range(6)
 
 # name -> (restype, argtypes)
 _SIGS = {
     "vp_abi_version": (i32, []),
     "vp_struct_sizes": (None, [C.POINTER(i64)]),
     "vp_gemm_bf16": (i32, [C.POINTER(GemmDesc), vp]),
+    "vp_gemm_mx_fp8": (i32, [C.POINTER(GemmMxDesc), vp]),
+    "vp_mx_scale_bytes": (i64, [i64, i64]),
+    "vp_mx_quantize_bf16": (i32, [vp, i64, vp, i64, vp, i32, i32, vp]),
+    "vp_mx_mfma_probe": (i32, [vp, vp, vp, vp, vp, vp]),
+    "vp_adaln_modulate_mx_fp8": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, f32, vp, i64, vp]),
     "vp_attention_fwd_bf16": (i32, [C.POINTER(AttnDesc), vp]),
     "vp_adaln_modulate_bf16": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, f32, vp, i64, vp]),
     "vp_head_norm_rope_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, i64,
@@ -105,9 +114,9 @@ def lib():
             fn.argtypes = args
         if L.vp_abi_version() != ABI_VERSION:
             raise HipLibraryError(f"libvp_hip ABI {L.vp_abi_version()} != {ABI_VERSION}; rebuild")
-        sizes = (i64 * 3)()
+        sizes = (i64 * 4)()
         L.vp_struct_sizes(sizes)
-        want = (C.sizeof(GemmDesc), C.sizeof(AttnDesc), C.sizeof(DpmDesc))
+        want = (C.sizeof(GemmDesc), C.sizeof(AttnDesc), C.sizeof(DpmDesc), C.sizeof(GemmMxDesc))
         if tuple(sizes) != want:
             raise HipLibraryError(f"descriptor size mismatch lib={tuple(sizes)} python={want}; rebuild")
         _lib = L

@@ -90,8 +90,82 @@ VP_DEV bf16x8 lds_frag64(const char* tile, int row, int chunk) {
   return *(const bf16x8*)(tile + row * 64 + ((chunk ^ swz64(row)) << 4));
 }
 
-template <int VAR>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_desc d) {
+// MX-FP8 extension of the descriptor (zero for the bf16 path)
+struct MxExt {
+  const uint8_t* a_scale;
+  const uint8_t* w_scale[3];
+  uint8_t* c_scale;
+};
+
+// scale ring of the fp8 path: 4 K-tiles x (A, W) x 1 KiB after the two operand stages (the ring slot of tile t is
+// refilled 3 tiles after its last read, so the LDS-DMA never races a reader)
+constexpr int SCALE_OFF = 2 * STAGE_BYTES;
+constexpr int LDS_BYTES_FP8 = (SCALE_OFF + 8 * 1024 > LDS_BYTES) ? SCALE_OFF + 8 * 1024 : LDS_BYTES;
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+
+
+// One block-scaled e4m3 MFMA, D = C in place.  Inline asm because the builtin form makes hipcc (ROCm 7.2) allocate
+// a fresh destination tuple per accumulator (dst != srcC), which does not fit the 256-VGPR budget of this tile and
+// spills.  The scale of the first operand (W) is byte BW of sw, of the second (A) byte BA of sa (op_sel /
+// op_sel_hi = low / high bit of the byte index).  Hazards the compiler does not see inside asm: the operands come
+// from ds_read (the compiler's lgkmcnt waits cover asm inputs), the same accumulator is reused only >= 8 MFMAs
+// later, and the kernel pads with s_nop before the epilogue reads the accumulators.
+template <int BW, int BA>
+VP_DEV void mfma_mx(f32x4& acc, const i32x8& w, const i32x8& a, int sw, int sa) {
+  if constexpr (BW == 0 && BA == 0)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,0,0] op_sel_hi:[0,0,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 0 && BA == 1)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,1,0] op_sel_hi:[0,0,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 0 && BA == 2)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,0,0] op_sel_hi:[0,1,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 0 && BA == 3)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,1,0] op_sel_hi:[0,1,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 1 && BA == 0)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[1,0,0] op_sel_hi:[0,0,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 1 && BA == 1)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[1,1,0] op_sel_hi:[0,0,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 1 && BA == 2)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[1,0,0] op_sel_hi:[0,1,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 1 && BA == 3)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[1,1,0] op_sel_hi:[0,1,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 2 && BA == 0)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,0,0] op_sel_hi:[1,0,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 2 && BA == 1)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,1,0] op_sel_hi:[1,0,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 2 && BA == 2)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,0,0] op_sel_hi:[1,1,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 2 && BA == 3)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,1,0] op_sel_hi:[1,1,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 3 && BA == 0)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 3 && BA == 1)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[1,1,0] op_sel_hi:[1,0,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 3 && BA == 2)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[1,0,0] op_sel_hi:[1,1,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+  if constexpr (BW == 3 && BA == 3)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[1,1,0] op_sel_hi:[1,1,0]"
+                 : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
+}
+
+template <int VAR, bool FP8 = false>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_desc d, const MxExt mx) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -140,7 +214,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     // each slot a wave waits for the unit issued 7 slots earlier (vmcnt(12): 6 units stay in flight) and for its
     // own LDS reads, then ONE barrier both publishes that unit and retires the reads of the region the slot's DMA
     // overwrites (each unit's region is last read in the slot just before the one that refills it).
-    const int nk = (d.K + BK - 1) / BK;
+    // bf16: a K-tile is 64 elements; fp8: 128 (the same 128 bytes per row, so the LDS images are identical)
+    constexpr int EB = FP8 ? 1 : 2;                 // bytes per element
+    constexpr int TK = FP8 ? 128 : BK;              // K elements per tile
+    const int nk = (d.K + TK - 1) / TK;
     using Z = std::integral_constant<int, 0>;
     using O = std::integral_constant<int, 1>;
     // Per-lane 32-bit byte offsets of the 4 units' source rows (2 LDS-DMA instructions each) from a wave-uniform
@@ -148,23 +225,36 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     // n_seg % 8 == 0), so the DMA uses saddr + voffset addressing and the per-tile advance is a scalar add.
     int uoff[4][2];
     const char* ubase[4][2];
+    // fp8 (the caller pads A to whole 256-row tiles and N % 256 == 0, so no row is clamped): every unit's
+    // per-lane offset is one of two lane values (the swizzle depends only on row bits 1-3, which the unit and
+    // instruction offsets do not touch) plus a wave-uniform base — 2 VGPRs instead of 8
+    int uoffA = 0, uoffW = 0;
+    int sgW = 0;
+    if constexpr (FP8) {
+      const int ra = wave * 8 + (lane >> 3);
+      uoffA = ra * (int)d.lda + (((lane & 7) ^ swz(ra)) << 4);
+      const int rw = (wave >> 2) * 64 + (wave & 3) * 8 + (lane >> 3);
+      uoffW = rw * d.K + (((lane & 7) ^ swz(rw)) << 4);
+      sgW = __builtin_amdgcn_readfirstlane(n0 / d.n_seg);
+    } else {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int g = i * 8 + wave;
-        const int rb = (u < 2) ? (g >> 3) * 128 + u * 64 + (g & 7) * 8 : (g >> 2) * 64 + (u - 2) * 32 + (g & 3) * 8;
-        const int r = rb + (lane >> 3);
-        const int c = (lane & 7) ^ swz(r);
-        if (u < 2) {
-          ubase[u][i] = (const char*)d.A;
-          uoff[u][i] = (min(m0 + r, d.M - 1) * d.lda + c * 8) * 2;
-        } else {
-          const int sg = __builtin_amdgcn_readfirstlane(min(n0 + rb, d.N - 1) / d.n_seg);
-          ubase[u][i] = (const char*)d.W[sg];
-          uoff[u][i] = ((min(n0 + r, d.N - 1) - sg * d.n_seg) * d.K + c * 8) * 2;
+        for (int i = 0; i < 2; ++i) {
+          const int g = i * 8 + wave;
+          const int rb = (u < 2) ? (g >> 3) * 128 + u * 64 + (g & 7) * 8 : (g >> 2) * 64 + (u - 2) * 32 + (g & 3) * 8;
+          const int r = rb + (lane >> 3);
+          const int c = (lane & 7) ^ swz(r);
+          if (u < 2) {
+            ubase[u][i] = (const char*)d.A;
+            uoff[u][i] = (min(m0 + r, d.M - 1) * d.lda) * EB + c * 16;
+          } else {
+            const int sg = __builtin_amdgcn_readfirstlane(min(n0 + rb, d.N - 1) / d.n_seg);
+            ubase[u][i] = (const char*)d.W[sg];
+            uoff[u][i] = ((min(n0 + r, d.N - 1) - sg * d.n_seg) * d.K) * EB + c * 16;
+          }
         }
-      }
+    }
     // unit u: 0 = A quadrant-row 0, 1 = A quadrant-row 1, 2 = W quadrant-col 0, 3 = W quadrant-col 1
     // (this variant runs only for K % 64 == 0, so there is no K tail here)
     auto issue_unit = [&](int u, int tile) {
@@ -173,7 +263,38 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
       for (int i = 0; i < 2; ++i) {
         const int g = i * 8 + wave;
         const int rb = (u < 2) ? (g >> 3) * 128 + u * 64 + (g & 7) * 8 : (g >> 2) * 64 + (u - 2) * 32 + (g & 3) * 8;
-        glds16(ubase[u][i] + tile * (BK * 2), uoff[u][i], base + rb * 128);
+        if constexpr (FP8) {
+          if (u < 2)
+            glds16((const char*)d.A + (int64_t)(m0 + i * 128 + u * 64) * d.lda + tile * 128, uoffA, base + rb * 128);
+          else
+            glds16((const char*)d.W[sgW] + (int64_t)(n0 - sgW * d.n_seg + i * 128 + (u - 2) * 32) * d.K + tile * 128,
+                   uoffW, base + rb * 128);
+        } else {
+          glds16(ubase[u][i] + tile * 128, uoff[u][i], base + rb * 128);
+        }
+      }
+    };
+    // fp8: the scales of tile T (1 KiB per operand, MX tile layout) ride with tile T's first unit (slot 4T-9):
+    // wave 0 fetches the A scales, wave 1 the W scales, into ring slot T & 3 — issued before that unit's DMA, so
+    // the wait that publishes the unit publishes them too
+    const char* sA = nullptr;
+    const char* sW = nullptr;
+    if constexpr (FP8) {
+      const int sgw = __builtin_amdgcn_readfirstlane(min(n0, d.N - 1) / d.n_seg);
+      sA = (const char*)mx.a_scale + (int64_t)(m0 >> 8) * nk * 1024;
+      sW = (const char*)mx.w_scale[sgw] + (int64_t)((n0 - sgw * d.n_seg) >> 8) * nk * 1024;
+    }
+    auto issue_scales = [&](int tile) {
+      if constexpr (FP8) {
+        char* dst = smem + SCALE_OFF + (tile & 3) * 2048;
+        if (wave < 2) {
+          // lane * 16 materialised in place (a hoisted copy would be one more long-lived VGPR, and its spill reload
+          // would drain the DMA queue with vmcnt(0))
+          int off;
+          asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 4, %0"
+                       : "=v"(off));
+          glds16(wave == 0 ? sA + tile * 1024 : sW + tile * 1024, off, wave == 0 ? dst : dst + 1024);
+        }
       }
     };
     auto slot_tile = [&](int sl, int& u) -> int {  // unit and tile issued by slot sl (sl >= -9)
@@ -189,7 +310,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     auto issue_slot = [&](int sl) {
       int u;
       const int tile = slot_tile(sl, u);
-      if (tile < nk) issue_unit(u, tile);
+      if (tile < nk) {
+        if (u == 0) issue_scales(tile);
+        issue_unit(u, tile);
+      }
     };
     auto top = [&](int sl) {
       if (exists(sl - 1)) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
@@ -201,53 +325,109 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     const int lrow = lane & 15;
     int lbase[2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) lbase[ks] = lrow * 128 + (((ks * 4 + (lane >> 4)) ^ swz(lrow)) << 4);
-    auto readA = [&](bf16x8 (&a)[8], auto par_c, auto qm_c) {
+    for (int ks = 0; ks < 2; ++ks) {
+      // bf16: k-step ks of a 16x16x32 fragment is chunk ks*4 + lane/16.  fp8 (measured, tools/mx_probe.py): the
+      // 32 bytes lane l feeds a 16x16x128 MFMA are K-chunks lane/16 and lane/16 + 4 of its row — the same two
+      // chunks, so the same conflict-free reads; K-block b = chunks 2b, 2b+1 takes lane (row, b)'s scale
+      const int ch = ks * 4 + (lane >> 4);
+      lbase[ks] = lrow * 128 + ((ch ^ swz(lrow)) << 4);
+    }
+    // fp8 scales of one K-tile, read once per tile: this lane's (row lane%16, K-block lane/16) byte of the A
+    // fragments (8 rows-groups: byte i of word qm = quadrant-row qm, fragment i) and of the W fragments (byte
+    // qn*2 + j).  Tile k+1's scales are read in tile k's phase 2, next to its first A fragments.
+    struct TileScales {
+      int a0, a1, w;
+    };
+    const int sbase = (lane >> 4) * 256 + lrow * 16;
+    auto readS = [&](TileScales& ts, int tile) {
+      if constexpr (FP8) {
+        const char* sp = smem + SCALE_OFF + (tile & 3) * 2048 + sbase;
+        const u32x2 a = *(const u32x2*)(sp + wr * 8);
+        ts.a0 = (int)a[0];
+        ts.a1 = (int)a[1];
+        ts.w = *(const int*)(sp + 1024 + wc * 4);
+      }
+    };
+    // register fragments of one quadrant: bf16 = 4 (A) / 2 (W) 16x16x32 fragments x 2 k-steps; fp8 = 4 / 2
+    // 16x16x128 fragments of 8 VGPRs each (both halves read straight into one register tuple)
+    using FragA = std::conditional_t<FP8, i32x8[4], bf16x8[8]>;
+    using FragB = std::conditional_t<FP8, i32x8[2], bf16x8[4]>;
+    auto read8 = [&](const char* p) -> i32x8 {
+      i32x8 f;
+      u32x4* h = (u32x4*)&f;  // both 16-byte halves land in one 8-VGPR tuple (no copy into the MFMA operand)
+      h[0] = *(const u32x4*)(p + lbase[0]);
+      h[1] = *(const u32x4*)(p + lbase[1]);
+      return f;
+    };
+    auto readA = [&](FragA& a, auto par_c, auto qm_c) {
       constexpr int par = decltype(par_c)::value, qm = decltype(qm_c)::value;
       const char* As = smem + par * STAGE_BYTES + (wr * WM + qm * 64) * 128;
+      if constexpr (FP8) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+        for (int i = 0; i < 4; ++i) a[i] = read8(As + i * 16 * 128);
+      } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a[ks * 4 + i] = *(const bf16x8*)(As + lbase[ks] + i * 16 * 128);
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[ks * 4 + i] = *(const bf16x8*)(As + lbase[ks] + i * 16 * 128);
+      }
     };
-    auto readB = [&](bf16x8 (&bb)[4], auto par_c, auto qn_c) {
+    auto readB = [&](FragB& bb, auto par_c, auto qn_c) {
       constexpr int par = decltype(par_c)::value, qn = decltype(qn_c)::value;
       const char* Bs = smem + par * STAGE_BYTES + TILE_BYTES + (wc * WN + qn * 32) * 128;
+      if constexpr (FP8) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+        for (int j = 0; j < 2; ++j) bb[j] = read8(Bs + j * 16 * 128);
+      } else {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bb[ks * 2 + j] = *(const bf16x8*)(Bs + lbase[ks] + j * 16 * 128);
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) bb[ks * 2 + j] = *(const bf16x8*)(Bs + lbase[ks] + j * 16 * 128);
+      }
     };
-    auto mma = [&](const bf16x8 (&a)[8], const bf16x8 (&bb)[4], auto qm_c, auto qn_c) {
+    auto mma = [&](const FragA& a, const FragB& bb, auto qm_c, auto qn_c, int sa, int sb) {
       constexpr int qm = decltype(qm_c)::value, qn = decltype(qn_c)::value;
       __builtin_amdgcn_sched_barrier(0);  // keep the next subtile's reads above this phase's MFMAs
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (FP8) {
+        // 16x16x128 e4m3 x e4m3 with per-lane E8M0 scales, W (quadrant-col qn) as the first operand like the bf16
+        // path; the byte opsel picks each fragment's scale out of the tile's scale words
+#define VP_MX_MMA(J, I) mfma_mx<qn * 2 + J, I>(acc[qn * 2 + J][qm * 4 + I], bb[J], a[I], sb, sa)
+        VP_MX_MMA(0, 0); VP_MX_MMA(0, 1); VP_MX_MMA(0, 2); VP_MX_MMA(0, 3);
+        VP_MX_MMA(1, 0); VP_MX_MMA(1, 1); VP_MX_MMA(1, 2); VP_MX_MMA(1, 3);
+#undef VP_MX_MMA
+      } else {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+        for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[qn * 2 + j][qm * 4 + i] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[ks * 2 + j], a[ks * 4 + i], acc[qn * 2 + j][qm * 4 + i], 0, 0, 0);
+            for (int i = 0; i < 4; ++i)
+              acc[qn * 2 + j][qm * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  bb[ks * 2 + j], a[ks * 4 + i], acc[qn * 2 + j][qm * 4 + i], 0, 0, 0);
+      }
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     };
-    bf16x8 a0[8], a1[8], bx[4], by[4];
+    FragA a0, a1;
+    FragB bx, by;
     // prologue: slots -9..-2 (tiles 0 and 1, and nothing that overwrites tile 0's quadrant-row-0 A before it is
     // read), then the first subtiles, then slot -1 (A quadrant-row 0 of tile 2 into tile 0's region)
     for (int sl = -9; sl < -1; ++sl) issue_slot(sl);
     if (exists(-2)) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // units of slots -9, -8 landed
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    TileScales scx = {0, 0, 0}, scy = {0, 0, 0};
     readA(a0, Z{}, Z{});
     readB(bx, Z{}, Z{});
+    readS(scx, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     issue_slot(-1);
     // one K-tile; PAR = k & 1 selects the LDS buffer and which of bx/by holds quadrant-col 0.  STEADY: every slot
     // of this tile issues a unit and 6 later units exist (k + 3 < nk), so the waits are the fixed vmcnt(12).
-    auto tile_body = [&](int k, auto par_c, auto steady_c, bf16x8 (&b0)[4], bf16x8 (&b1)[4]) {
+    auto tile_body = [&](int k, auto par_c, auto steady_c, FragB& b0, FragB& b1, const TileScales& sc,
+                         TileScales& scn) {
       using P = decltype(par_c);
       using NP = std::integral_constant<int, 1 - P::value>;
       constexpr bool STEADY = decltype(steady_c)::value;
@@ -258,6 +438,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
           __builtin_amdgcn_s_barrier();
           int u;
           const int tile = slot_tile(sl, u);
+          if (u == 0) issue_scales(tile);
           issue_unit(u, tile);
         } else {
           top(sl);
@@ -267,30 +448,34 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
       const bool more = STEADY || k + 1 < nk;
       slot(s0);
       readB(b1, P{}, O{});
-      mma(a0, b0, Z{}, Z{});
+      mma(a0, b0, Z{}, Z{}, sc.a0, sc.w);
       slot(s0 + 1);
       readA(a1, P{}, O{});
-      mma(a0, b1, Z{}, O{});
+      mma(a0, b1, Z{}, O{}, sc.a0, sc.w);
       slot(s0 + 2);
-      if (more) readA(a0, NP{}, Z{});
-      mma(a1, b1, O{}, O{});
+      if (more) {
+        readA(a0, NP{}, Z{});
+        readS(scn, k + 1);
+      }
+      mma(a1, b1, O{}, O{}, sc.a1, sc.w);
       slot(s0 + 3);
       if (more) readB(b1, NP{}, Z{});  // b1's registers carry the next tile's quadrant-col 0
-      mma(a1, b0, O{}, Z{});
+      mma(a1, b0, O{}, Z{}, sc.a1, sc.w);
     };
     using T_ = std::integral_constant<bool, true>;
     using F_ = std::integral_constant<bool, false>;
     int k = 0;
     for (; k + 4 < nk; k += 2) {
-      tile_body(k, Z{}, T_{}, bx, by);
-      tile_body(k + 1, O{}, T_{}, by, bx);
+      tile_body(k, Z{}, T_{}, bx, by, scx, scy);
+      tile_body(k + 1, O{}, T_{}, by, bx, scy, scx);
     }
     // tail (at most 4 tiles; k is even here, so the parities are static)
-    if (k < nk) tile_body(k, Z{}, F_{}, bx, by);
-    if (k + 1 < nk) tile_body(k + 1, O{}, F_{}, by, bx);
-    if (k + 2 < nk) tile_body(k + 2, Z{}, F_{}, bx, by);
-    if (k + 3 < nk) tile_body(k + 3, O{}, F_{}, by, bx);
+    if (k < nk) tile_body(k, Z{}, F_{}, bx, by, scx, scy);
+    if (k + 1 < nk) tile_body(k + 1, O{}, F_{}, by, bx, scy, scx);
+    if (k + 2 < nk) tile_body(k + 2, Z{}, F_{}, bx, by, scx, scy);
+    if (k + 3 < nk) tile_body(k + 3, O{}, F_{}, by, bx, scy, scx);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if constexpr (FP8) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");  // asm MFMA results
     __syncthreads();
   } else if constexpr (VAR == 4) {
     // VAR 1 with both k-halves' fragments read right after the barrier (24 reads in flight, 96 VGPRs), so the
@@ -492,7 +677,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = rbf(acc[j][i][r] + bv[r]);
-        if (epi == VP_EPI_BIAS_GELU) v = gelu_tanh(v);
+        if (epi == VP_EPI_BIAS_GELU || epi == VP_EPI_BIAS_GELU_MXFP8) v = gelu_tanh(v);
         else if (epi == VP_EPI_BIAS_SCALE) v = v * d.alpha;
         o[r] = f2bf(v);
       }
@@ -512,6 +697,18 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     if (m >= d.M || ncol >= d.N) continue;
     bf16x8 v = *(const bf16x8*)(smem + mloc * CT_STRIDE + chunk * 16);
     const int64_t orow = (int64_t)(m / d.rows_per_group) * d.group_stride + d.row_offset + (m % d.rows_per_group);
+    if (FP8 && epi == VP_EPI_BIAS_GELU_MXFP8) {
+      // MX-quantise the GELU output: the 4 lanes holding one 32-column block agree on its scale (N % 256 == 0, so
+      // a block's lanes are all in or all out of range)
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = bf2f(v[e]);
+      uint8_t sb;
+      const u32x2 q = mx_quantize_quarter(f, sb);
+      *(u32x2*)((uint8_t*)d.C + orow * d.ldc + ncol) = q;
+      if ((tid & 3) == 0) mx.c_scale[mx_scale_off(orow, ncol >> 5, d.N)] = sb;
+      continue;
+    }
     if (epi == VP_EPI_GATED) {
       const int b = m / d.tokens_per_batch;
       const int tok = m - b * d.tokens_per_batch;
@@ -558,6 +755,7 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
     if (d->inject != nullptr && ((d->inject_ld % 8) != 0 || (d->inject_bstride % 8) != 0)) return VP_ERR_ARG;
   }
   if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
+  const MxExt mx = {};
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -579,15 +777,116 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
     variant = 1;  // the quadrant pipeline needs whole K-tiles and 32-bit source offsets
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
   if (variant == 5)
-    hipLaunchKernelGGL(gemm_bf16_kernel<5>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+    hipLaunchKernelGGL(gemm_bf16_kernel<5>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
   else if (variant == 4)
-    hipLaunchKernelGGL(gemm_bf16_kernel<4>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+    hipLaunchKernelGGL(gemm_bf16_kernel<4>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
   else if (variant == 3)
-    hipLaunchKernelGGL(gemm_bf16_kernel<3>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+    hipLaunchKernelGGL(gemm_bf16_kernel<3>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
   else if (variant == 2)
-    hipLaunchKernelGGL(gemm_bf16_kernel<2>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+    hipLaunchKernelGGL(gemm_bf16_kernel<2>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
   else
-    hipLaunchKernelGGL(gemm_bf16_kernel<1>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d);
+    hipLaunchKernelGGL(gemm_bf16_kernel<1>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_gemm_mx_fp8(const vp_gemm_mx_desc* x, void* stream) {
+  if (x == nullptr) return VP_ERR_ARG;
+  const vp_gemm_desc* d = &x->base;
+  if (d->A == nullptr || d->W[0] == nullptr || d->C == nullptr || x->a_scale == nullptr || x->w_scale[0] == nullptr)
+    return VP_ERR_ARG;
+  if (d->M <= 0 || d->N <= 0 || d->K <= 0 || (d->K % 128) != 0 || (d->N % 256) != 0) return VP_ERR_ARG;
+  if (d->lda < d->K || (d->lda % 16) != 0 || d->rows_per_group <= 0) return VP_ERR_ARG;
+  const int nsegs = d->W[2] ? 3 : (d->W[1] ? 2 : 1);
+  if (d->n_seg <= 0 || d->n_seg * nsegs != d->N || (d->n_seg % 256) != 0) return VP_ERR_ARG;
+  for (int s = 0; s < nsegs; ++s)
+    if (x->w_scale[s] == nullptr) return VP_ERR_ARG;
+  if (d->epilogue < VP_EPI_BIAS || d->epilogue > VP_EPI_BIAS_GELU_MXFP8) return VP_ERR_ARG;
+  if (d->epilogue == VP_EPI_BIAS_GELU_MXFP8) {
+    if (x->c_scale == nullptr || (d->ldc % 16) != 0 || d->ldc < d->N || d->rows_per_group != d->M) return VP_ERR_ARG;
+  } else if (d->ldc < d->N || (d->ldc % 8) != 0) {
+    return VP_ERR_ARG;
+  }
+  if (d->epilogue == VP_EPI_GATED) {
+    if (d->R == nullptr || d->gate == nullptr || d->gate_text == nullptr || d->tokens_per_batch <= 0) return VP_ERR_ARG;
+    if ((d->ldr % 8) != 0 || (d->gate_bstride % 8) != 0) return VP_ERR_ARG;
+    if (d->inject != nullptr && ((d->inject_ld % 8) != 0 || (d->inject_bstride % 8) != 0)) return VP_ERR_ARG;
+  }
+  if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
+  // 32-bit DMA source offsets
+  if ((int64_t)d->M * d->lda >= ((int64_t)1 << 31) || (int64_t)d->n_seg * d->K >= ((int64_t)1 << 31)) return VP_ERR_ARG;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES_FP8);
+    attr_set = true;
+  }
+  MxExt mx;
+  mx.a_scale = (const uint8_t*)x->a_scale;
+  for (int s = 0; s < 3; ++s) mx.w_scale[s] = (const uint8_t*)x->w_scale[s];
+  mx.c_scale = (uint8_t*)x->c_scale;
+  const int tiles = ((d->M + BM - 1) / BM) * (d->N / BN);
+  hipLaunchKernelGGL((gemm_bf16_kernel<5, true>), dim3(tiles), dim3(NTHREADS), LDS_BYTES_FP8, (hipStream_t)stream,
+                     *d, mx);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+// ---- MX quantiser: 8 elements per thread, 4 threads per 32-element block ----
+__global__ __launch_bounds__(256) void mx_quantize_kernel(const bf16* __restrict__ x, int64_t ld_in,
+                                                          uint8_t* __restrict__ q, int64_t ld_out,
+                                                          uint8_t* __restrict__ scales, int rows, int K) {
+  const int cpr = K / 8;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = i / cpr;
+  const int c = (int)(i - r * cpr);
+  if (r >= rows) return;  // whole 4-lane groups leave together (cpr % 4 == 0)
+  const bf16x8 v = *(const bf16x8*)(x + r * ld_in + c * 8);
+  float f[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = bf2f(v[e]);
+  uint8_t sb;
+  const u32x2 pk = mx_quantize_quarter(f, sb);
+  *(u32x2*)(q + r * ld_out + c * 8) = pk;
+  if ((c & 3) == 0) scales[mx_scale_off(r, c >> 2, K)] = sb;
+}
+
+extern "C" int64_t vp_mx_scale_bytes(int64_t rows, int64_t K) { return ((rows + 255) / 256) * (K / 128) * 1024; }
+
+extern "C" int vp_mx_quantize_bf16(const void* x, int64_t ld_in, void* q, int64_t ld_out, void* scales, int32_t rows,
+                                   int32_t K, void* stream) {
+  if (!x || !q || !scales || rows <= 0 || K <= 0 || (K % 128) || ld_in < K || ld_out < K || (ld_in % 8) ||
+      (ld_out % 8))
+    return VP_ERR_ARG;
+  const int64_t n = (int64_t)rows * (K / 8);
+  hipLaunchKernelGGL(mx_quantize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)x, ld_in, (uint8_t*)q, ld_out, (uint8_t*)scales, rows, K);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+// ---- layout self-test: one wave, one block-scaled MFMA ----
+__global__ __launch_bounds__(64) void mx_probe_kernel(const uint8_t* A, const uint8_t* B, const uint8_t* sa,
+                                                      const uint8_t* sb, float* C) {
+  const int l = threadIdx.x;
+  // lane l feeds K-chunks l/16 and l/16 + 4 (16 bytes each) of row l % 16
+  i32x8 a, b;
+  u32x4* ha = (u32x4*)&a;
+  u32x4* hb = (u32x4*)&b;
+  ha[0] = *(const u32x4*)(A + (l & 15) * 128 + (l >> 4) * 16);
+  ha[1] = *(const u32x4*)(A + (l & 15) * 128 + ((l >> 4) + 4) * 16);
+  hb[0] = *(const u32x4*)(B + (l & 15) * 128 + (l >> 4) * 16);
+  hb[1] = *(const u32x4*)(B + (l & 15) * 128 + ((l >> 4) + 4) * 16);
+  f32x4 c = {0.f, 0.f, 0.f, 0.f};
+  c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, (int)sa[l], 0, (int)sb[l]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) C[(4 * (l >> 4) + r) * 16 + (l & 15)] = c[r];
+}
+
+extern "C" int vp_mx_mfma_probe(const void* A, const void* B, const void* sa, const void* sb, float* C, void* stream) {
+  if (!A || !B || !sa || !sb || !C) return VP_ERR_ARG;
+  hipLaunchKernelGGL(mx_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const uint8_t*)A,
+                     (const uint8_t*)B, (const uint8_t*)sa, (const uint8_t*)sb, C);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }

@@ -46,7 +46,11 @@ VP_DEV void row_stats(const RowRegs& r, int nch, int lane, int D, float& mean, f
 }
 
 // ---- AdaLN-Zero modulate (DF/models/normalization.py:373-379) ----
-__global__ __launch_bounds__(ROW_THREADS) void adaln_modulate_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+// MX = true: the modulated row is written as MX-FP8 (e4m3 + E8M0 per 32 columns, include/vp_hip.h) for the fp8
+// FeedForward — a 32-column block is 4 consecutive 8-column chunks = 4 consecutive lanes of the row's wave.
+template <bool MX>
+__global__ __launch_bounds__(ROW_THREADS) void adaln_modulate_kernel(const bf16* __restrict__ x, void* __restrict__ y,
+                                                                     uint8_t* __restrict__ yscale,
                                                                      int rows, int Ntok, int D, int text_len,
                                                                      const bf16* __restrict__ lw,
                                                                      const bf16* __restrict__ lb, float eps,
@@ -72,14 +76,24 @@ __global__ __launch_bounds__(ROW_THREADS) void adaln_modulate_kernel(const bf16*
       const bf16x8 bb = *(const bf16x8*)(lb + c * 8);
       const bf16x8 sh = *(const bf16x8*)(shift + c * 8);
       const bf16x8 sc = *(const bf16x8*)(scale + c * 8);
-      bf16x8 o;
+      float f[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float n = rbf((r.v[i][e] - mean) * rstd * bf2f(w[e]) + bf2f(bb[e]));
         const float s1 = rbf(1.f + bf2f(sc[e]));
-        o[e] = f2bf(rbf(n * s1) + bf2f(sh[e]));
+        f[e] = rbf(rbf(n * s1) + bf2f(sh[e]));
       }
-      *(bf16x8*)(y + (int64_t)row * D + c * 8) = o;
+      if constexpr (MX) {
+        uint8_t sb;
+        const u32x2 q = mx_quantize_quarter(f, sb);
+        *(u32x2*)((uint8_t*)y + (int64_t)row * D + c * 8) = q;
+        if ((c & 3) == 0) yscale[mx_scale_off(row, c >> 2, D)] = sb;
+      } else {
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(f[e]);
+        *(bf16x8*)((bf16*)y + (int64_t)row * D + c * 8) = o;
+      }
     }
   }
 }
@@ -238,9 +252,24 @@ extern "C" int vp_adaln_modulate_bf16(const void* x, void* y, int32_t B, int32_t
   if (mod_bstride % 8) return VP_ERR_ARG;
   const int rows = B * Ntok;
   const int grid = (rows + 3) / 4;
-  hipLaunchKernelGGL(adaln_modulate_kernel, dim3(grid), dim3(ROW_THREADS), 0, (hipStream_t)stream, (const bf16*)x,
-                     (bf16*)y, rows, Ntok, D, text_len, (const bf16*)ln_w, (const bf16*)ln_b, eps, (const bf16*)mod,
-                     mod_bstride);
+  hipLaunchKernelGGL(adaln_modulate_kernel<false>, dim3(grid), dim3(ROW_THREADS), 0, (hipStream_t)stream,
+                     (const bf16*)x, y, nullptr, rows, Ntok, D, text_len, (const bf16*)ln_w, (const bf16*)ln_b, eps,
+                     (const bf16*)mod, mod_bstride);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_adaln_modulate_mx_fp8(const void* x, void* q, void* scales, int32_t B, int32_t Ntok, int32_t D,
+                                        int32_t text_len, const void* ln_w, const void* ln_b, float eps,
+                                        const void* mod, int64_t mod_bstride, void* stream) {
+  if (!x || !q || !scales || !ln_w || !ln_b || !mod || B <= 0 || Ntok <= 0 || D <= 0 || (D % 128) || D > MAXC * 512)
+    return VP_ERR_ARG;
+  if (mod_bstride % 8) return VP_ERR_ARG;
+  const int rows = B * Ntok;
+  const int grid = (rows + 3) / 4;
+  hipLaunchKernelGGL(adaln_modulate_kernel<true>, dim3(grid), dim3(ROW_THREADS), 0, (hipStream_t)stream,
+                     (const bf16*)x, q, (uint8_t*)scales, rows, Ntok, D, text_len, (const bf16*)ln_w,
+                     (const bf16*)ln_b, eps, (const bf16*)mod, mod_bstride);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }

@@ -62,7 +62,59 @@ VP_DEV int xcd_remap(int wg, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-#define VP_CHECK_LAUNCH()                                   \
+// ---- MX-FP8 (e4m3 + E8M0 per 32 elements; layout and rounding rule in include/vp_hip.h) ----
+// byte offset of the scale of (row r, K-block kb) in an MX scale array of a tensor with K columns
+VP_DEV int64_t mx_scale_off(int64_t r, int kb, int K) {
+  return ((r >> 8) * (K >> 7) + (kb >> 2)) * 1024 + (kb & 3) * 256 + (r & 15) * 16 + ((r >> 4) & 15);
+}
+
+// scale exponent s = ceil(log2(amax / 448)) in [-127, 127]; -127 (byte 0) for an all-zero block
+VP_DEV int mx_exponent(float amax) {
+  if (!(amax > 0.f)) return -127;
+  const uint32_t u = __float_as_uint(amax * (1.f / 448.f));
+  int e = (int)((u >> 23) & 0xff) - 127;  // floor(log2) for normal values
+  if ((u & 0x7fffff) != 0) ++e;           // not a power of two -> round up
+  if (((u >> 23) & 0xff) == 0) e = -126;  // subnormal ratio: below 2^-126
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+
+// 2^-s as a float, s in [-127, 127] (2^-127 is subnormal)
+VP_DEV float mx_inv_scale(int s) {
+  const int e = 127 - s;  // biased exponent of 2^-s, in [0, 254]
+  return e == 0 ? __uint_as_float(0x00400000u) : __uint_as_float((uint32_t)e << 23);
+}
+
+// 8 floats -> 8 e4m3 bytes (RNE, |x| clamped to 448 first)
+VP_DEV u32x2 mx_pack8(const float (&v)[8], float mul) {
+  u32x2 r;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    int w = 0;
+    const float a = __builtin_amdgcn_fmed3f(v[4 * h + 0] * mul, 448.f, -448.f);
+    const float b = __builtin_amdgcn_fmed3f(v[4 * h + 1] * mul, 448.f, -448.f);
+    const float c = __builtin_amdgcn_fmed3f(v[4 * h + 2] * mul, 448.f, -448.f);
+    const float d = __builtin_amdgcn_fmed3f(v[4 * h + 3] * mul, 448.f, -448.f);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, w, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+    r[h] = (uint32_t)w;
+  }
+  return r;
+}
+
+// one 32-element MX block held as 8 values by each of 4 consecutive lanes (lane & 3 = block quarter): block
+// exponent via two xor-shuffles; returns the 8 packed bytes of this lane and the block's scale byte
+VP_DEV u32x2 mx_quantize_quarter(const float (&v)[8], uint8_t& scale_byte) {
+  float am = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(v[e]));
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  const int s = mx_exponent(am);
+  scale_byte = (uint8_t)(s + 127);
+  return mx_pack8(v, mx_inv_scale(s));
+}
+
+#define VP_CHECK_LAUNCH()                                 \
   do {                                                      \
     hipError_t _e = hipGetLastError();                      \
     if (_e != hipSuccess) return (int)_e;                   \

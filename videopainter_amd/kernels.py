@@ -156,6 +156,117 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], 
 
 
 # ------------------------------------------------------------------------------------------------------------------
+# MX-FP8 (BASELINE config 5): e4m3 elements + one E8M0 scale per 32 K-elements, scale layout of include/vp_hip.h
+# ------------------------------------------------------------------------------------------------------------------
+
+class MXTensor:
+    """rows x K MX-FP8 matrix on the device: `q` uint8 e4m3 [rows padded to a multiple of 256, K] (the GEMM streams
+    whole 256-row tiles) and `scales` uint8 in the 1-KiB tile layout."""
+
+    def __init__(self, rows: int, K: int, device, q: Optional[torch.Tensor] = None,
+                 scales: Optional[torch.Tensor] = None):
+        if K % 128:
+            raise ValueError(f"MX-FP8 needs K % 128 == 0, got {K}")
+        self.rows, self.K = rows, K
+        pad = (rows + 255) // 256 * 256
+        self.q = torch.zeros(pad, K, device=device, dtype=torch.uint8) if q is None else q
+        nb = N.lib().vp_mx_scale_bytes(rows, K)
+        self.scales = torch.zeros(nb, device=device, dtype=torch.uint8) if scales is None else scales
+
+    def __repr__(self):
+        return f"MXTensor(rows={self.rows}, K={self.K})"
+
+
+def mx_quantize(x: torch.Tensor, out: Optional["MXTensor"] = None) -> "MXTensor":
+    """bf16 [..., K] (last dim contiguous) -> MXTensor [rows, K]."""
+    _chk(x, "x")
+    x2 = x.reshape(-1, x.shape[-1])
+    rows, Kk = x2.shape
+    out = MXTensor(rows, Kk, x.device) if out is None else out
+    N.check(N.lib().vp_mx_quantize_bf16(_p(x2), _rowmajor(x2, "x"), _p(out.q), out.q.stride(0), _p(out.scales), rows,
+                                        Kk, _stream()), "vp_mx_quantize_bf16")
+    return out
+
+
+def gemm_mx(a: "MXTensor", weights: Sequence["MXTensor"], biases: Sequence[Optional[torch.Tensor]], out, *,
+            epilogue: int = N.EPI_BIAS, alpha: float = 1.0, resid: Optional[torch.Tensor] = None,
+            mod: Optional[torch.Tensor] = None, gate_chunk: int = 2, gate_text_chunk: int = 5,
+            tokens_per_batch: int = 1, text_len: int = 0, inject: Optional[torch.Tensor] = None,
+            inject_mask: Optional[torch.Tensor] = None):
+    """out = epilogue(a @ cat(weights).T) on the block-scaled fp8 MFMA.  `out` is a bf16 [M, N] tensor, or an
+    MXTensor for EPI_BIAS_GELU_MXFP8 (the FF1 -> FF2 hand-off stays in fp8)."""
+    Kk = a.K
+    for w in weights:
+        if w.K != Kk or w.rows != weights[0].rows:
+            raise ValueError("weight segments must share K and rows")
+    nseg = weights[0].rows
+    Ntot = nseg * len(weights)
+    x = N.GemmMxDesc()
+    d = x.base
+    d.M, d.N, d.K, d.epilogue = a.rows, Ntot, Kk, epilogue
+    d.A, d.lda = _p(a.q), a.q.stride(0)
+    x.a_scale = _p(a.scales)
+    for i, w in enumerate(weights):
+        d.W[i] = _p(w.q)
+        x.w_scale[i] = _p(w.scales)
+        b = biases[i] if biases is not None and i < len(biases) else None
+        if b is not None:
+            _chk(b, "bias")
+        d.bias[i] = _p(b)
+    d.n_seg = nseg
+    d.rows_per_group = a.rows
+    d.alpha = alpha
+    if epilogue == N.EPI_BIAS_GELU_MXFP8:
+        if not isinstance(out, MXTensor) or out.K != Ntot or out.rows != a.rows:
+            raise ValueError("EPI_BIAS_GELU_MXFP8 writes an MXTensor [M, N]")
+        d.C, d.ldc = _p(out.q), out.q.stride(0)
+        x.c_scale = _p(out.scales)
+    else:
+        _chk(out, "out")
+        d.C, d.ldc = _p(out), _rowmajor(out, "out")
+    if epilogue == N.EPI_GATED:
+        _chk(resid, "resid")
+        _chk(mod, "mod")
+        d.R, d.ldr = _p(resid), _rowmajor(resid, "resid")
+        d.gate = mod.data_ptr() + gate_chunk * Ntot * mod.element_size()
+        d.gate_text = mod.data_ptr() + gate_text_chunk * Ntot * mod.element_size()
+        d.gate_bstride = mod.stride(0)
+        d.tokens_per_batch, d.text_len = tokens_per_batch, text_len
+        if inject is not None:
+            _chk(inject, "inject")
+            d.inject, d.inject_ld, d.inject_bstride = _p(inject), inject.stride(1), inject.stride(0)
+            if inject_mask is not None:
+                _chk(inject_mask, "inject_mask", torch.uint8)
+                d.inject_mask = _p(inject_mask)
+                d.inject_mask_bstride = inject_mask.stride(0)
+    ev = _t0("gemm_mx")
+    N.check(N.lib().vp_gemm_mx_fp8(C.byref(x), _stream()), "vp_gemm_mx_fp8")
+    _t1("gemm_mx", ev)
+    return out
+
+
+def adaln_modulate_mx(x: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, mod: torch.Tensor, text_len: int,
+                      eps: float, out: Optional["MXTensor"] = None) -> "MXTensor":
+    """AdaLN-Zero modulate writing MX-FP8 rows (the fp8 FeedForward's input)."""
+    _chk(x, "x")
+    if not x.is_contiguous():
+        raise ValueError("x must be contiguous [B, N, D]")
+    B, Ntok, D = x.shape
+    out = MXTensor(B * Ntok, D, x.device) if out is None else out
+    N.check(N.lib().vp_adaln_modulate_mx_fp8(_p(x), _p(out.q), _p(out.scales), B, Ntok, D, text_len, _p(ln_w),
+                                             _p(ln_b), eps, _p(mod), mod.stride(0), _stream()),
+            "vp_adaln_modulate_mx_fp8")
+    return out
+
+
+def mx_mfma_probe(A: torch.Tensor, B: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) -> torch.Tensor:
+    """One block-scaled MFMA (layout self-test): A, B uint8 e4m3 [16, 128]; sa, sb uint8 [64] (lane scales)."""
+    Cm = torch.empty(16, 16, device=A.device, dtype=torch.float32)
+    N.check(N.lib().vp_mx_mfma_probe(_p(A), _p(B), _p(sa), _p(sb), _p(Cm), _stream()), "vp_mx_mfma_probe")
+    return Cm
+
+
+# ------------------------------------------------------------------------------------------------------------------
 # attention
 # ------------------------------------------------------------------------------------------------------------------
 
