@@ -26,17 +26,29 @@ sys.path.insert(0, ROOT)
 
 METRIC = "denoising steps/sec, CogVideoX-5b+branch 49f 480×720, 1→8 MI355X; MFMA util%"
 PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA peak, MI355X_MICROARCH.md
-B, T, F, HL, WL, D, H, L, LB = 2, 226, 13, 60, 90, 3072, 48, 42, 2
+PEAK_FP8_TFLOPS = 5000.0   # dense fp8 (block-scaled MFMA) peak
+B, T, F, D, H, L, LB = 2, 226, 13, 3072, 48, 42, 2
+# BASELINE config 2 (the headline): 49f 480x720 -> latent 60x90; config 5: 49f 720x1280 -> latent 90x160, fp8 FFN
+HL, WL = 60, 90
 NV = F * (HL // 2) * (WL // 2)
 NTOK = T + NV
 
 
-def step_flops() -> float:
-    """Algorithmic FLOP per denoising step: transformer + branch at B=2."""
+def set_config(cfg: int) -> None:
+    global HL, WL, NV, NTOK
+    HL, WL = (60, 90) if cfg == 2 else (90, 160)
+    NV = F * (HL // 2) * (WL // 2)
+    NTOK = T + NV
+
+
+def step_flops(split: bool = False):
+    """Algorithmic FLOP per denoising step: transformer + branch at B=2.  split=True returns
+    (total, FeedForward part) — the FeedForward GEMMs are the fp8 part of config 5."""
     blk = 24 * NTOK * D * D + 4 * NTOK * NTOK * D
     tr = B * (L * blk + 2 * NV * 128 * D + 2 * T * 4096 * D + 2 * NV * D * 64)
     br = B * (LB * blk + 2 * NV * 132 * D + 2 * T * 4096 * D + LB * 2 * NTOK * D * D)
-    return float(tr + br)
+    ffn = B * (L + LB) * 16 * NTOK * D * D
+    return (float(tr + br), float(ffn)) if split else float(tr + br)
 
 
 def attn_flops_per_launch() -> float:
@@ -93,9 +105,12 @@ def cpu_baseline(seconds_budget: float = 30.0) -> dict:
 def build_models(device, seed: int, rank: int, world: int):
     from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, device_scope
     from videopainter_amd.config import COGVIDEOX_5B_I2V
+    # config 5 (720x1280): random-init 5b-shaped model whose learned positional embedding is sized for the latent
+    # 90x160 grid (SURVEY.md finding 2: the real 5b-I2V checkpoint is locked to 60x90)
+    cfg = dict(COGVIDEOX_5B_I2V, sample_height=HL, sample_width=WL)
     with device_scope(device):
-        tr = CogVideoXTransformer3DModel(**COGVIDEOX_5B_I2V)
-        br = CogvideoXBranchModel(**dict(COGVIDEOX_5B_I2V, num_layers=LB))
+        tr = CogVideoXTransformer3DModel(**cfg)
+        br = CogvideoXBranchModel(**dict(cfg, num_layers=LB))
     if rank == 0 or world == 1:
         tr.init_synthetic_weights_(seed)
         br.init_synthetic_weights_(seed + 1)
@@ -130,7 +145,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 5),
+                    help="BASELINE config: 2 = 49f 480x720 bf16 (headline), 5 = 49f 720x1280 with the fp8 FeedForward")
     args = ap.parse_args()
+    set_config(args.config)
 
     if args.cpu_baseline_only:
         print(json.dumps({"cpu_baseline": cpu_baseline()}))
@@ -163,6 +181,26 @@ def main():
     st, pe = make_state(harness, device, 42 + rank)
     rope = harness.rope_for(F, HL, WL)
     gen = torch.Generator().manual_seed(42 + rank)
+    fp8_drift = None
+    if args.config == 5:
+        # the fp8 FeedForward's drift from this same model in bf16, one full forward on the step's inputs
+        # (re-stated tolerance of config 5; block level vs the reference: tests/test_model_gpu.py)
+        with torch.no_grad():
+            lmi = torch.cat([torch.cat([st.latents] * 2), st.image_in], dim=2)
+            ts = torch.full((2,), 999, device=device, dtype=torch.int64)
+
+            def fwd():
+                bs = br(hidden_states=torch.cat([st.latents] * 2), encoder_hidden_states=pe, branch_cond=st.branch_in,
+                        timestep=ts, image_rotary_emb=rope, return_dict=False)[0]
+                return tr(hidden_states=lmi, encoder_hidden_states=pe, branch_block_samples=bs, timestep=ts,
+                          image_rotary_emb=rope, branch_block_masks=st.mask1, return_dict=False)[0].float()
+            ref16 = fwd()
+            tr.enable_fp8_ffn()
+            br.enable_fp8_ffn()
+            out8 = fwd()
+            fp8_drift = float((out8 - ref16).norm() / ref16.norm())
+            del ref16, out8, lmi
+        log(f"[bench] config 5: fp8-FFN noise_pred vs bf16 rel-L2 {fp8_drift:.3e}")
     log(f"[bench] setup {time.time() - t_setup:.1f}s; rank {rank}/{world}")
 
     def one(i):
@@ -179,7 +217,7 @@ def main():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
-        with K.timed_launches("attention", "gemm") as tl:
+        with K.timed_launches("attention", "gemm", "gemm_mx") as tl:
             t0 = time.perf_counter()
             for i in range(args.warmup, args.warmup + args.steps):
                 one(i)
@@ -195,27 +233,34 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     attn_ms = tl.mean_ms("attention")
     attn_tf = attn_flops_per_launch() / (attn_ms * 1e-3) / 1e12
-    gemm_ev = tl.events.get("gemm", [])
+    gemm_ev = tl.events.get("gemm", []) + tl.events.get("gemm_mx", [])
     torch.cuda.synchronize()
     gemm_ms_total = sum(s.elapsed_time(e) for s, e in gemm_ev)
-    traffic, traffic_src = profiled_traffic()
-    step_frac = step_flops() * (steps_per_s / world) / (PEAK_BF16_TFLOPS * 1e12)
+    traffic, traffic_src = profiled_traffic() if args.config == 2 else (None, None)  # PMC file is per config
+    total_fl, ffn_fl = step_flops(split=True)
+    if args.config == 5:  # time the step would take at the dense peaks of the dtypes its MFMAs use
+        t_ideal = (total_fl - ffn_fl) / (PEAK_BF16_TFLOPS * 1e12) + ffn_fl / (PEAK_FP8_TFLOPS * 1e12)
+    else:
+        t_ideal = total_fl / (PEAK_BF16_TFLOPS * 1e12)
+    step_frac = t_ideal * (steps_per_s / world)
     if not math.isfinite(steps_per_s):
         raise RuntimeError("non-finite timing")
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 2:
         del st
         cpu = cpu_baseline()
     if rank == 0:
         out = {
             "metric": METRIC, "value": steps_per_s, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic latents/prompt embeds of the 49f 480x720 shape; random-init CogVideoX-5b-I2V (42 "
-                    "layers) + 2-layer branch weights (no checkpoints offline)",
-            "config": {"workload": "BASELINE config 2: CogVideoX-5b-I2V + 2-layer branch, 49f 480x720 (latent "
-                                   "13x60x90), CFG batch 2, 226+17550=17776 tokens, 1 denoising step = branch + "
-                                   "transformer + CFG/DPM/replace-gt", "clips_per_gpu": 1, "cfg_batch": B,
+            "vs_baseline": None, "dtype": "bf16" if args.config == 2 else "bf16 + fp8 (MX e4m3) FeedForward",
+            "data": f"synthetic latents/prompt embeds of the 49f {HL * 8}x{WL * 8} shape; random-init "
+                    "CogVideoX-5b-I2V (42 layers) + 2-layer branch weights (no checkpoints offline)",
+            "config": {"workload": (f"BASELINE config {args.config}: CogVideoX-5b-I2V + 2-layer branch, 49f "
+                                    f"{HL * 8}x{WL * 8} (latent 13x{HL}x{WL}), CFG batch 2, {T}+{NV}={NTOK} tokens, "
+                                    "1 denoising step = branch + transformer + CFG/DPM/replace-gt"
+                                    + (", FeedForward in MX-FP8" if args.config == 5 else "")),
+                       "clips_per_gpu": 1, "cfg_batch": B,
                        "tokens": NTOK, "layers": L, "branch_layers": LB,
                        "parallelism": f"dp{world} (independent clips, weights broadcast over RCCL)"},
             "roofline": {"kernel": "attention (vp_attention_fwd_bf16, dominant by time)", "bound": "mfma",
@@ -225,6 +270,7 @@ def main():
                          "per_launch_ms": attn_ms, "launches": tl.count("attention"),
                          "algorithmic_flop_per_launch": attn_flops_per_launch()},
             "step_mfma_frac": step_frac,
+            "fp8_ffn_rel_l2_vs_bf16": fp8_drift,
             "step_flop": step_flops(),
             "gemm_ms_per_step": gemm_ms_total / args.steps,
             "attention_ms_per_step": attn_ms * tl.count("attention") / args.steps,

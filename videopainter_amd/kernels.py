@@ -164,14 +164,16 @@ class MXTensor:
     whole 256-row tiles) and `scales` uint8 in the 1-KiB tile layout."""
 
     def __init__(self, rows: int, K: int, device, q: Optional[torch.Tensor] = None,
-                 scales: Optional[torch.Tensor] = None):
+                 scales: Optional[torch.Tensor] = None, zero: bool = True):
+        """zero=False leaves the padding rows uninitialised (they only feed GEMM rows that are never stored)."""
         if K % 128:
             raise ValueError(f"MX-FP8 needs K % 128 == 0, got {K}")
         self.rows, self.K = rows, K
         pad = (rows + 255) // 256 * 256
-        self.q = torch.zeros(pad, K, device=device, dtype=torch.uint8) if q is None else q
+        alloc = torch.zeros if zero else torch.empty
+        self.q = alloc(pad, K, device=device, dtype=torch.uint8) if q is None else q
         nb = N.lib().vp_mx_scale_bytes(rows, K)
-        self.scales = torch.zeros(nb, device=device, dtype=torch.uint8) if scales is None else scales
+        self.scales = alloc(nb, device=device, dtype=torch.uint8) if scales is None else scales
 
     def __repr__(self):
         return f"MXTensor(rows={self.rows}, K={self.K})"
@@ -252,7 +254,7 @@ def adaln_modulate_mx(x: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, m
     if not x.is_contiguous():
         raise ValueError("x must be contiguous [B, N, D]")
     B, Ntok, D = x.shape
-    out = MXTensor(B * Ntok, D, x.device) if out is None else out
+    out = MXTensor(B * Ntok, D, x.device, zero=False) if out is None else out
     N.check(N.lib().vp_adaln_modulate_mx_fp8(_p(x), _p(out.q), _p(out.scales), B, Ntok, D, text_len, _p(ln_w),
                                              _p(ln_b), eps, _p(mod), mod.stride(0), _stream()),
             "vp_adaln_modulate_mx_fp8")

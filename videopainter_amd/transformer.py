@@ -205,6 +205,19 @@ class CogVideoXBlock(nn.Module):
         self.norm2 = CogVideoXLayerNormZero(time_embed_dim, dim, norm_elementwise_affine, norm_eps, bias=True)
         self.ff = FeedForward(dim, inner_dim=ff_inner_dim, bias=ff_bias, final_dropout=final_dropout)
         self.dim = dim
+        self.ff_mx = None  # (W1, W2) as MX-FP8 when the fp8 FeedForward is enabled (BASELINE config 5)
+
+    def enable_fp8_ffn(self, enabled: bool = True) -> None:
+        """Run the FeedForward on the block-scaled fp8 MFMA: both weights quantised once to MX-FP8 (e4m3 + one
+        E8M0 scale per 32 inputs), the norm2 AdaLN output written in MX-FP8, FF1's GELU output re-quantised in its
+        epilogue, FF2 accumulating in fp32 into the bf16 gated residual.  The state dict is unchanged."""
+        if not enabled:
+            self.ff_mx = None
+            return
+        w1, w2 = self.ff.net[0].proj.weight, self.ff.net[2].weight
+        if w1.shape[0] % 256 or w2.shape[0] % 256 or w1.shape[1] % 128 or w2.shape[1] % 128:
+            raise ValueError(f"fp8 FeedForward needs widths that are multiples of 256, got {tuple(w1.shape)}")
+        self.ff_mx = (K.mx_quantize(w1), K.mx_quantize(w2))
 
     # -- joint-buffer fast path used by the models --
     def forward_joint(self, x: torch.Tensor, text_len: int, temb: torch.Tensor, rope=None,
@@ -233,14 +246,25 @@ class CogVideoXBlock(nn.Module):
                resid=xf, mod=mod1, gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok, text_len=text_len)
         del o
         mod2 = self.norm2.modulation(temb)
-        xn2 = K.adaln_modulate(x_mid, self.norm2.norm.weight, self.norm2.norm.bias, mod2, text_len,
-                               self.norm2.norm.eps)
         ff0 = self.ff.net[0].proj
         ff2 = self.ff.net[2]
-        h1 = K.linear(xn2, ff0.weight, ff0.bias, gelu=True)
-        del xn2
         if out is None:
             out = torch.empty_like(x)
+        if self.ff_mx is not None:
+            w1, w2 = self.ff_mx
+            xq = K.adaln_modulate_mx(x_mid, self.norm2.norm.weight, self.norm2.norm.bias, mod2, text_len,
+                                     self.norm2.norm.eps)
+            h1 = K.MXTensor(B * Ntok, w1.rows, x.device, zero=False)
+            K.gemm_mx(xq, [w1], [ff0.bias], h1, epilogue=NAT.EPI_BIAS_GELU_MXFP8)
+            del xq
+            K.gemm_mx(h1, [w2], [ff2.bias], out.view(B * Ntok, D), epilogue=NAT.EPI_GATED,
+                      resid=x_mid.view(B * Ntok, D), mod=mod2, tokens_per_batch=Ntok, text_len=text_len,
+                      inject=inject, inject_mask=inject_mask)
+            return out
+        xn2 = K.adaln_modulate(x_mid, self.norm2.norm.weight, self.norm2.norm.bias, mod2, text_len,
+                               self.norm2.norm.eps)
+        h1 = K.linear(xn2, ff0.weight, ff0.bias, gelu=True)
+        del xn2
         kw = {}
         if inject is not None:
             kw = dict(inject=inject, inject_ld=inject.stride(1), inject_bstride=inject.stride(0),
@@ -306,6 +330,13 @@ class CogVideoXTransformer3DModel(ModelMixin):
             for _ in range(num_layers)])
         self.norm_final = LayerNorm(inner_dim, norm_eps, norm_elementwise_affine)
         self._build_head(inner_dim, time_embed_dim, norm_elementwise_affine, norm_eps, patch_size, out_channels)
+
+    def enable_fp8_ffn(self, enabled: bool = True):
+        """fp8 FeedForward in every block (BASELINE config 5; see CogVideoXBlock.enable_fp8_ffn).  Call after the
+        weights are loaded; re-call after changing them."""
+        for blk in self.transformer_blocks:
+            blk.enable_fp8_ffn(enabled)
+        return self
 
     def _patch_channels(self):
         return self.config.in_channels
