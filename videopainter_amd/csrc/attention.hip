@@ -36,7 +36,7 @@ constexpr int V_STRIDE = 192;       // bytes per V row in LDS (128 data + 64 pad
 constexpr int V_TILE_BYTES = KBLK * V_STRIDE;
 constexpr int STAGE_BYTES = K_TILE_BYTES + V_TILE_BYTES;
 constexpr int LDS_BYTES = 2 * STAGE_BYTES;
-constexpr int DEFAULT_VARIANT = 10;
+constexpr int DEFAULT_VARIANT = 22;
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
@@ -353,6 +353,45 @@ VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f
   l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
 }
 
+// QK^T half with the first MFMA in inline asm so its destination is a fresh tuple (early-clobber) while C = -m
+// stays in its own registers: with the builtin, the compiler coalesces the rescale path's phi of -m into the second
+// half's accumulator and pays 8 v_mov_b64 per half to refill it.  The following builtin MFMAs accumulate on the
+// asm result in place (same opcode, exactly overlapping srcC: no wait states); -m is written by VALU only in the
+// rescale branch, long before the next QK^T.
+VP_DEV void qk_half_ci2(const char* Kl, int kh, const bf16x8 (&qf)[4], const f32x16& negm, f32x16& s, int lane) {
+  const int hl = lane >> 5;
+  const int row = kh * 32 + (lane & 31);
+  const char* kr = Kl + row * 128;
+  const int sw = swz(row);
+  bf16x8 k0 = *(const bf16x8*)(kr + ((hl ^ sw) << 4));
+  bf16x8 k1 = *(const bf16x8*)(kr + (((2 + hl) ^ sw) << 4));
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(s) : "v"(k0), "v"(qf[0]), "v"(negm));
+  k0 = *(const bf16x8*)(kr + (((4 + hl) ^ sw) << 4));
+  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[1], s, 0, 0, 0);
+  k1 = *(const bf16x8*)(kr + (((6 + hl) ^ sw) << 4));
+  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[2], s, 0, 0, 0);
+  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[3], s, 0, 0, 0);
+}
+
+// Lazy-max softmax half: exp2 straight off the C-init accumulator and sum, no max.  Correct as long as every
+// exponent s - m stays small; the check is on the sum this lane just computed (it bounds each of its 16 terms):
+// if any lane's sum exceeds 16 * 2^RESCALE_THR the wave runs the max path (softmax_half_ci) on the same scores,
+// which then rescales.  Otherwise P <= 2^(RESCALE_THR + 4), exact in bf16's exponent range, and
+// O / l is unchanged.  Returns false when the caller must take the max path.
+VP_DEV bool softmax_half_lazy(const f32x16& s, float& l_run, bf16x8 (&pf)[2]) {
+  float ps[4];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float p = __builtin_amdgcn_exp2f(s[i]);
+    ps[i & 3] = i < 4 ? p : ps[i & 3] + p;
+    pf[i >> 3][i & 7] = f2bf(p);  // packed right away (discarded if the check fails)
+  }
+  const float ls = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+  if (__ballot(!(ls <= 16.f * (1 << (int)RESCALE_THR))) != 0ull) return false;  // NaN/inf included
+  l_run += ls;
+  return true;
+}
+
 // ---- LDS-DMA staging (global_load_lds_dwordx4, saddr + 32-bit voffset): the LDS destination is lane-linear, so
 // both images are unpadded [64 rows][128 B] and their bank swizzles are applied on the SOURCE address
 // (cdna_hip_programming.md §5.4 rule 21).  K: chunk ^ swz(row) (conflict-free ds_read_b128).  V: chunk ^
@@ -584,7 +623,7 @@ VP_DEV void pv_half_x(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)
 // tile t waits (counted vmcnt) for tile t+1 only, then one barrier.  PRIO: the second half of the workgroup's waves
 // runs at s_setprio 1 (the arbitration loser of each SIMD pair, MI355X_MICROARCH.md "Two waves per SIMD" item 4).
 // ------------------------------------------------------------------------------------------------------------
-template <int NW, int OCC, int KB = 64, int RING = 2, bool PRIO = false>
+template <int NW, int OCC, int KB = 64, int RING = 2, bool PRIO = false, bool LAZY = false>
 __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc d) {
   constexpr int QB = NW * 32;
   constexpr int KT = KB * 128;                  // bytes per K (or V) tile
@@ -631,7 +670,11 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
     kch[i] = (lane & 7) ^ swz(prow[i]);
     vch[i] = (lane & 7) ^ vswz(prow[i]);
   }
-  auto slot_of = [&](int ti) { return smem + (RING == 2 ? (ti & 1) : ti % 3) * ST; };
+  // (the ring-3 slot offset goes through readfirstlane: otherwise the compiler hoists one address VGPR per LDS read
+  // and slot out of the loop and spills them)
+  auto slot_of = [&](int ti) {
+    return smem + (RING == 2 ? (ti & 1) * ST : __builtin_amdgcn_readfirstlane((ti % 3) * ST));
+  };
   auto issue = [&](int ti) {
     const Seg sg = tile_seg<KB>(d, ti, tiles1, b, h);
     char* slot = slot_of(ti);
@@ -686,10 +729,18 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
     for (int kh = 0; kh < HALVES; ++kh) {
       if (!active) break;
       f32x16 sh;
-      qk_half_ci(Kl, kh, qf, negm, sh, lane);
-      if (lim < KB) mask_half(sh, lim, kh, hl);
       bf16x8 pf[2];
-      softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf);
+      if constexpr (LAZY) {
+        qk_half_ci2(Kl, kh, qf, negm, sh, lane);
+        if (lim < KB) mask_half(sh, lim, kh, hl);
+        // the first half sets m by the max path (thr = -inf); afterwards the lazy path, falling back when it must
+        // (the lazy path leaves the scores intact, so the fallback needs no recompute)
+        if (thr == -INFINITY || !softmax_half_lazy(sh, l_run, pf)) softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf);
+      } else {
+        qk_half_ci(Kl, kh, qf, negm, sh, lane);
+        if (lim < KB) mask_half(sh, lim, kh, hl);
+        softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf);
+      }
       pv_half_x(Kl + KT, kh, pf, o, vo);
     }
     // retire tile ti+1 (RING 3: tile ti+2's pieces, 2 per piece-row of this wave, may stay in flight)
@@ -741,6 +792,11 @@ extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
       {(const void*)attn_fwd_dma<8, 4, 128, 2>, 8, 4 * 128 * 128},           // 16: 128-key tiles
       {(const void*)attn_fwd_dma<8, 4, 64, 2, true>, 8, 4 * KBLK * 128},      // 17: 10 + static prio for waves 4-7
       {(const void*)attn_fwd_dma<8, 4, 64, 3, true>, 8, 6 * KBLK * 128},      // 18: 15 + prio
+      {(const void*)attn_fwd_dma<8, 4, 64, 2, false, true>, 8, 4 * KBLK * 128},  // 19: 10 + lazy max, no -m copies
+      {(const void*)attn_fwd_dma<8, 4, 64, 2, true, true>, 8, 4 * KBLK * 128},   // 20: 19 + prio
+      {(const void*)attn_fwd_dma<8, 4, 64, 3, false, true>, 8, 6 * KBLK * 128},  // 21: 19 + 3-slot ring
+      {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true>, 8, 4 * 128 * 128},  // 22: 19 + 128-key tiles
+      {(const void*)attn_fwd_dma<8, 4, 64, 3, true, true>, 8, 6 * KBLK * 128},   // 23: 21 + prio
   };
 
   constexpr int NVAR = sizeof(vars) / sizeof(vars[0]);
