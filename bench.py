@@ -146,7 +146,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true")
     ap.add_argument("--config", type=int, default=2, choices=(2, 5),
-                    help="BASELINE config: 2 = 49f 480x720 bf16 (headline), 5 = 49f 720x1280 with the fp8 FeedForward")
+                    help="BASELINE config: 2 = 49f 480x720 bf16 (headline), 5 = 49f 720x1280 with attention + "
+                         "FeedForward in fp8")
     args = ap.parse_args()
     set_config(args.config)
 
@@ -183,7 +184,7 @@ def main():
     gen = torch.Generator().manual_seed(42 + rank)
     fp8_drift = None
     if args.config == 5:
-        # the fp8 FeedForward's drift from this same model in bf16, one full forward on the step's inputs
+        # the fp8 path's drift from this same model in bf16, one full forward on the step's inputs
         # (re-stated tolerance of config 5; block level vs the reference: tests/test_model_gpu.py)
         with torch.no_grad():
             lmi = torch.cat([torch.cat([st.latents] * 2), st.image_in], dim=2)
@@ -195,12 +196,12 @@ def main():
                 return tr(hidden_states=lmi, encoder_hidden_states=pe, branch_block_samples=bs, timestep=ts,
                           image_rotary_emb=rope, branch_block_masks=st.mask1, return_dict=False)[0].float()
             ref16 = fwd()
-            tr.enable_fp8_ffn()
-            br.enable_fp8_ffn()
+            tr.enable_fp8()
+            br.enable_fp8()
             out8 = fwd()
             fp8_drift = float((out8 - ref16).norm() / ref16.norm())
             del ref16, out8, lmi
-        log(f"[bench] config 5: fp8-FFN noise_pred vs bf16 rel-L2 {fp8_drift:.3e}")
+        log(f"[bench] config 5: fp8 attention+FFN noise_pred vs bf16 rel-L2 {fp8_drift:.3e}")
     log(f"[bench] setup {time.time() - t_setup:.1f}s; rank {rank}/{world}")
 
     def one(i):
@@ -217,7 +218,7 @@ def main():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
-        with K.timed_launches("attention", "gemm", "gemm_mx") as tl:
+        with K.timed_launches("attention", "attention_fp8", "gemm", "gemm_mx") as tl:
             t0 = time.perf_counter()
             for i in range(args.warmup, args.warmup + args.steps):
                 one(i)
@@ -231,7 +232,9 @@ def main():
         elapsed = max_over_ranks(elapsed, device)
     steps_per_s = world * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    attn_ms = tl.mean_ms("attention")
+    attn_name = "attention_fp8" if args.config == 5 else "attention"
+    attn_ms = tl.mean_ms(attn_name)
+    attn_peak = PEAK_FP8_TFLOPS if args.config == 5 else PEAK_BF16_TFLOPS
     attn_tf = attn_flops_per_launch() / (attn_ms * 1e-3) / 1e12
     gemm_ev = tl.events.get("gemm", []) + tl.events.get("gemm_mx", [])
     torch.cuda.synchronize()
@@ -239,7 +242,8 @@ def main():
     traffic, traffic_src = profiled_traffic() if args.config == 2 else (None, None)  # PMC file is per config
     total_fl, ffn_fl = step_flops(split=True)
     if args.config == 5:  # time the step would take at the dense peaks of the dtypes its MFMAs use
-        t_ideal = (total_fl - ffn_fl) / (PEAK_BF16_TFLOPS * 1e12) + ffn_fl / (PEAK_FP8_TFLOPS * 1e12)
+        f8_fl = ffn_fl + (L + LB) * attn_flops_per_launch()  # one attention launch per block
+        t_ideal = (total_fl - f8_fl) / (PEAK_BF16_TFLOPS * 1e12) + f8_fl / (PEAK_FP8_TFLOPS * 1e12)
     else:
         t_ideal = total_fl / (PEAK_BF16_TFLOPS * 1e12)
     step_frac = t_ideal * (steps_per_s / world)
@@ -253,27 +257,29 @@ def main():
         out = {
             "metric": METRIC, "value": steps_per_s, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16" if args.config == 2 else "bf16 + fp8 (MX e4m3) FeedForward",
+            "vs_baseline": None,
+            "dtype": "bf16" if args.config == 2 else "bf16 + fp8 (e4m3, block-scaled MFMA) attention + FeedForward",
             "data": f"synthetic latents/prompt embeds of the 49f {HL * 8}x{WL * 8} shape; random-init "
                     "CogVideoX-5b-I2V (42 layers) + 2-layer branch weights (no checkpoints offline)",
             "config": {"workload": (f"BASELINE config {args.config}: CogVideoX-5b-I2V + 2-layer branch, 49f "
                                     f"{HL * 8}x{WL * 8} (latent 13x{HL}x{WL}), CFG batch 2, {T}+{NV}={NTOK} tokens, "
                                     "1 denoising step = branch + transformer + CFG/DPM/replace-gt"
-                                    + (", FeedForward in MX-FP8" if args.config == 5 else "")),
+                                    + (", attention + FeedForward in fp8" if args.config == 5 else "")),
                        "clips_per_gpu": 1, "cfg_batch": B,
                        "tokens": NTOK, "layers": L, "branch_layers": LB,
                        "parallelism": f"dp{world} (independent clips, weights broadcast over RCCL)"},
-            "roofline": {"kernel": "attention (vp_attention_fwd_bf16, dominant by time)", "bound": "mfma",
-                         "achieved": attn_tf, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": attn_tf / PEAK_BF16_TFLOPS, "traffic": traffic, "traffic_unit": "bytes/launch",
+            "roofline": {"kernel": "attention (vp_attention_fwd_%s, dominant by time)"
+                                   % ("fp8" if args.config == 5 else "bf16"),
+                         "bound": "mfma", "achieved": attn_tf, "peak": attn_peak, "unit": "TFLOP/s",
+                         "frac": attn_tf / attn_peak, "traffic": traffic, "traffic_unit": "bytes/launch",
                          "traffic_source": traffic_src,
-                         "per_launch_ms": attn_ms, "launches": tl.count("attention"),
+                         "per_launch_ms": attn_ms, "launches": tl.count(attn_name),
                          "algorithmic_flop_per_launch": attn_flops_per_launch()},
             "step_mfma_frac": step_frac,
-            "fp8_ffn_rel_l2_vs_bf16": fp8_drift,
+            "fp8_rel_l2_vs_bf16": fp8_drift,
             "step_flop": step_flops(),
             "gemm_ms_per_step": gemm_ms_total / args.steps,
-            "attention_ms_per_step": attn_ms * tl.count("attention") / args.steps,
+            "attention_ms_per_step": attn_ms * tl.count(attn_name) / args.steps,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

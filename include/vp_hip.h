@@ -26,9 +26,10 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 2
+#define VP_ABI_VERSION 3
 int vp_abi_version(void);
-/* sizeof of the descriptor structs as compiled into the library: out[0..3] = gemm, attn, dpm, gemm_mx (ABI check) */
+/* sizeof of the descriptor structs as compiled into the library: out[0..4] = gemm, attn, dpm, gemm_mx, attn_fp8
+ * (ABI check) */
 void vp_struct_sizes(int64_t* out);
 
 /* ---------------------------------------------------------------------------------------------------------------
@@ -153,6 +154,32 @@ typedef struct vp_attn_desc {
 
 int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream);
 
+/* fp8 attention (BASELINE config 5 "attn + FFN in fp8"; same math as vp_attention_fwd_bf16, single K/V segment).
+ * base.Q / base.K: e4m3 [B, N, H*64] written by vp_head_norm_rope_fp8 (strides in bytes, multiples of 16), each
+ * carrying one power-of-two factor undone by the E8M0 bytes in qk_scale (bits 0-7: Q, bits 8-15: K; Q's factor
+ * also includes scale * log2 e, so base.scale is ignored).  base.V: V^T e4m3 [B, H, 64, npad] and vs: its scales,
+ * both from vp_v_pack_fp8.  base.O / out_scale / accumulate as in the bf16 kernel. */
+typedef struct vp_attn_fp8_desc {
+  vp_attn_desc base;
+  const void* vs;
+  int32_t npad;     /* ceil(Nk / 64) * 64 */
+  int32_t qk_scale; /* E8M0 bytes: Q | K << 8 */
+} vp_attn_fp8_desc;
+
+int vp_attention_fwd_fp8(const vp_attn_fp8_desc* d, void* stream);
+
+/* V [B, N, H*64] bf16 (row stride v_sn, batch stride v_sb, elements) -> V^T e4m3 [B, H, 64, npad] with the keys of
+ * every 64-key tile in MFMA K-slot order, plus one E8M0 scale per (d, 32 keys) (MX rule of vp_mx_quantize_bf16).
+ * Padded keys are zero.  vp_v_pack_fp8_bytes returns the V^T bytes and reports npad and the scale bytes. */
+int64_t vp_v_pack_fp8_bytes(int32_t B, int32_t H, int32_t N, int64_t* npad, int64_t* scale_bytes);
+int vp_v_pack_fp8(const void* V, int64_t v_sb, int64_t v_sn, int32_t B, int32_t N, int32_t H, void* vt, void* vs,
+                  void* stream);
+
+/* One v_mfma_scale_f32_32x32x64_f8f6f4 with the layout the fp8 attention assumes (lane l: row l % 32, 16-byte
+ * K-chunks l/32 and l/32 + 2 of A[32][64] / B[32][64], scale bytes sa[l] / sb[l] for (row l % 32, K-block l/32));
+ * C[32][32] row-major fp32 = A_deq . B_deq^T.  Layout self-test. */
+int vp_mx_mfma_probe32(const void* A, const void* B, const void* sa, const void* sb, float* C, void* stream);
+
 /* ---------------------------------------------------------------------------------------------------------------
  * AdaLN-Zero modulate — CogVideoXLayerNormZero.forward (DF/models/normalization.py:373-379):
  * y = rnd(rnd(rnd(LN(x)) * rnd(1 + scale)) + shift) over rows of x [B, Ntok, D] (contiguous).  mod is the bf16
@@ -180,6 +207,13 @@ int vp_head_norm_rope_bf16(const void* x_in, int64_t ld_in, int64_t bs_in, void*
                            int64_t bs_out, int32_t B, int32_t Ntok, int32_t H, int32_t text_len, const void* ln_w,
                            const void* ln_b, float eps, const float* cos, const float* sin, const uint8_t* tok_mask,
                            int64_t mask_bstride, float pre_scale, void* stream);
+
+/* The same LN(64) + RoPE, output e4m3 (x_bf16 * out_mul, clamped to +-448, RNE) for the fp8 attention; ld_out /
+ * bs_out in bytes. */
+int vp_head_norm_rope_fp8(const void* x_in, int64_t ld_in, int64_t bs_in, void* q_out, int64_t ld_out,
+                          int64_t bs_out, int32_t B, int32_t Ntok, int32_t H, int32_t text_len, const void* ln_w,
+                          const void* ln_b, float eps, const float* cos, const float* sin, float out_mul,
+                          void* stream);
 
 /* y[b, n, :] = rnd(rnd(x[b, n, :] * tok_mask[b, n]) * scale) — the masked value copy of the resample processor. */
 int vp_mask_scale_rows_bf16(const void* x_in, int64_t ld_in, int64_t bs_in, void* y, int64_t ld_out, int64_t bs_out,

@@ -365,3 +365,73 @@ def test_full_width_block_fp8_ffn_tolerance():
     assert r8 <= 4 * ro + 1e-2, (r8, r16, ro)
     # the fp8 delta is confined to the FeedForward branch: compare to the bf16 path's own output
     assert rel(flat8, flat16) < 3e-2
+
+
+def test_full_width_block_fp8_attention_and_ffn_tolerance():
+    """BASELINE config 5 ("attn + FFN in fp8") on the 5B-width block against the reference fp32 block: the fp8
+    attention (e4m3 Q/K with static LN-bounded factors, V^T with per-(d, 32 keys) scales, P in e4m3) plus the MX-FP8
+    FeedForward.  Re-stated tolerance: at most 6x the reference's own bf16 drift from fp32, plus 2e-2."""
+    from videopainter_amd import device_scope
+    from videopainter_amd.transformer import CogVideoXBlock
+    from oracle import cogvideox_oracle as O
+    c = full_block_case()
+    g = load_file(os.path.join(GOLD, "block_full.safetensors"))
+    with device_scope(dev):
+        blk = CogVideoXBlock(dim=3072, num_attention_heads=48, attention_head_dim=64, time_embed_dim=512,
+                             attention_bias=True)
+    for k, p in blk.state_dict().items():
+        p.copy_(torch.from_numpy(c["weights"][k]))
+    run = lambda: blk(hidden_states=_d(c["h"]), encoder_hidden_states=_d(c["e"]), temb=_d(c["temb"]),  # noqa: E731
+                      image_rotary_emb=c["rope"])
+    h16, e16 = run()
+    blk.enable_fp8_attention()
+    ha, ea = run()
+    blk.enable_fp8_ffn()
+    h8, e8 = run()
+    flat16 = torch.cat([e16, h16], dim=1).reshape(-1).float().cpu()
+    flata = torch.cat([ea, ha], dim=1).reshape(-1).float().cpu()
+    flat8 = torch.cat([e8, h8], dim=1).reshape(-1).float().cpu()
+    sd16 = {"b." + k: torch.from_numpy(v).to(torch.bfloat16) for k, v in c["weights"].items()}
+    oh, oe = O.block_forward(sd16, "b", dict(num_attention_heads=48, norm_eps=1e-5), _b16(c["h"]), _b16(c["e"]),
+                             _b16(c["temb"]), c["rope"])
+    oflat = torch.cat([oe, oh], dim=1).reshape(-1).float()
+    r8, ra, ro = rel(flat8[::97], g["slice"]), rel(flata[::97], g["slice"]), rel(oflat[::97], g["slice"])
+    print(f"fp8 attn+FFN block vs fp32: {r8:.3e}; fp8 attn only {ra:.3e}; reference bf16 {ro:.3e}; "
+          f"vs bf16 HIP: attn {rel(flata, flat16):.3e}, attn+FFN {rel(flat8, flat16):.3e}")
+    assert r8 <= 6 * ro + 2e-2, (r8, ra, ro)
+    assert rel(flat8, flat16) < 5e-2
+
+
+@torch.no_grad()
+def test_fp8_attention_model_modes(env):
+    """The fp8 attention on the tiny model: std and prev-clip (blend epilogue) modes against the reference fp32
+    goldens within the fp8 band; the ID-resample processor (two K/V segments) keeps the bf16 kernel, bit for bit."""
+    i, g = env["inp"], env["g"]
+    bs = [_d(b) for b in (g["branch.0"], g["branch.1"])]
+    prev = {k: _d(g[f"std.hs.{k}"]) for k in range(4)}
+    rm = g["std.resample_mask"].bool().to(dev)
+
+    def run(model, mode):
+        kw = dict(branch_block_masks=_d(i["mask"]))
+        if mode == "prevclip":
+            kw["attention_kwargs"] = {"prev_hidden_states": prev, "prev_clip_weight": 0.5, "prev_resample_mask": rm}
+        if model is env["trr"]:
+            kw["id_pool_resample_learnable"] = True
+        return model(hidden_states=_d(i["hidden"]), encoder_hidden_states=_d(i["enc"]),
+                     timestep=i["timestep"].to(dev), image_rotary_emb=i["rope"], branch_block_samples=bs,
+                     return_dict=False, **kw)[0]
+
+    for model, mode, gold in ((env["tr"], "std", "std.out"), (env["tr"], "prevclip", "prevclip.out"),
+                              (env["trr"], "std", None)):
+        out16 = run(model, mode)
+        model.enable_fp8_attention()
+        try:
+            out8 = run(model, mode)
+        finally:
+            model.enable_fp8_attention(False)
+        if gold is None:
+            assert torch.equal(out8, out16)
+            continue
+        r8, r16 = rel(out8, g[gold]), rel(out16, g[gold])
+        print(f"fp8 attention {mode}: vs fp32 {r8:.3e} (bf16 HIP {r16:.3e}); vs bf16 {rel(out8, out16):.3e}")
+        assert r8 <= 4 * r16 + 3e-2, (mode, r8, r16)

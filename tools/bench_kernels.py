@@ -35,7 +35,8 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--gemm-variants", default="1,2")
     ap.add_argument("--variant", default="", help="attention kernel variant(s), e.g. 1 or 1,3")
-    ap.add_argument("--only", default="", help="attention | gemm | mx: run just that kernel (for rocprofv3 --pmc passes)")
+    ap.add_argument("--only", default="", help="attention | attn8 | gemm | mx: run just that kernel (for rocprofv3 "
+                    "--pmc passes; attn8 = the fp8 attention only)")
     args = ap.parse_args()
     dev = "cuda"
     B, T, Nv, D, H = 2, 226, 17550, 3072, 48
@@ -90,6 +91,8 @@ def main():
         print(json.dumps(res))
         return
     variants = ("vdefault",) if args.only == "attention" else ("vdefault", "v1", "v3")
+    if args.only == "attn8":
+        variants = ()
     if args.variant:
         variants = tuple("v" + v for v in args.variant.split(","))
     for rnd in range(1 if args.only else 2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
@@ -102,7 +105,19 @@ def main():
             res[f"attention_{var}_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
             print("attention", var, res[f"attention_{var}_r{rnd}"], flush=True)
     os.environ.pop("VP_ATTN_VARIANT", None)
-    if args.only == "attention":
+    if args.only in ("attention", "attn8"):
+        # fp8 attention (config 5 path) on the same operands: producers once, then the kernel, interleaved with bf16
+        q_exp, k_exp = 5, 4
+        q8 = (q.float() * 0.125 * K.LOG2E * 2.0 ** q_exp).to(torch.float8_e4m3fn).view(torch.uint8)
+        k8 = (k.float() * 2.0 ** k_exp).to(torch.float8_e4m3fn).view(torch.uint8)
+        t = timeit(lambda: K.v_pack_fp8(v, H), args.iters)
+        res["v_pack_fp8"] = dict(ms=t * 1e3, gbps=(B * Ntok * D * 3) / t / 1e9)
+        print("v_pack_fp8", res["v_pack_fp8"], flush=True)
+        vp = K.v_pack_fp8(v, H)
+        for rnd in range(2):
+            t = timeit(lambda: K.attention_fp8(q8, k8, vp, o, H, q_exp, k_exp), max(2, args.iters // 2))
+            res[f"attention_fp8_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
+            print("attention fp8", res[f"attention_fp8_r{rnd}"], flush=True)
         print(json.dumps(res))
         return
     xin = torch.randn(B, Ntok, D, device=dev).to(torch.bfloat16)

@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -49,6 +49,10 @@ class GemmMxDesc(C.Structure):
     _fields_ = [("base", GemmDesc), ("a_scale", vp), ("w_scale", vp * 3), ("c_scale", vp)]
 
 
+class AttnFp8Desc(C.Structure):
+    _fields_ = [("base", AttnDesc), ("vs", vp), ("npad", i32), ("qk_scale", i32)]
+
+
 class DpmDesc(C.Structure):
     _fields_ = [("n", i64), ("noise_pred", vp), ("do_cfg", i32), ("guidance", f32), ("model_output", vp),
                 ("sample", vp), ("old_pred", vp), ("pred_out", vp), ("noise1", vp), ("noise2", vp),
@@ -72,6 +76,11 @@ _SIGS = {
     "vp_mx_mfma_probe": (i32, [vp, vp, vp, vp, vp, vp]),
     "vp_adaln_modulate_mx_fp8": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, f32, vp, i64, vp]),
     "vp_attention_fwd_bf16": (i32, [C.POINTER(AttnDesc), vp]),
+    "vp_attention_fwd_fp8": (i32, [C.POINTER(AttnFp8Desc), vp]),
+    "vp_v_pack_fp8_bytes": (i64, [i32, i32, i32, C.POINTER(i64), C.POINTER(i64)]),
+    "vp_v_pack_fp8": (i32, [vp, i64, i64, i32, i32, i32, vp, vp, vp]),
+    "vp_mx_mfma_probe32": (i32, [vp, vp, vp, vp, vp, vp]),
+    "vp_head_norm_rope_fp8": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp, vp, f32, vp]),
     "vp_adaln_modulate_bf16": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, f32, vp, i64, vp]),
     "vp_head_norm_rope_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, i64,
                                      f32, vp]),
@@ -114,9 +123,10 @@ def lib():
             fn.argtypes = args
         if L.vp_abi_version() != ABI_VERSION:
             raise HipLibraryError(f"libvp_hip ABI {L.vp_abi_version()} != {ABI_VERSION}; rebuild")
-        sizes = (i64 * 4)()
+        sizes = (i64 * 5)()
         L.vp_struct_sizes(sizes)
-        want = (C.sizeof(GemmDesc), C.sizeof(AttnDesc), C.sizeof(DpmDesc), C.sizeof(GemmMxDesc))
+        want = (C.sizeof(GemmDesc), C.sizeof(AttnDesc), C.sizeof(DpmDesc), C.sizeof(GemmMxDesc),
+                C.sizeof(AttnFp8Desc))
         if tuple(sizes) != want:
             raise HipLibraryError(f"descriptor size mismatch lib={tuple(sizes)} python={want}; rebuild")
         _lib = L

@@ -105,6 +105,9 @@ class CogVideoXAttnProcessor2_0:
         qkv = _qkv(attn, x)
         q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
         eps_q, eps_k = attn.norm_q.eps, attn.norm_k.eps
+        fp8 = getattr(attn, "fp8_qk_exp", None)
+        if fp8 is not None:
+            return self._attend_fp8(attn, q, k, v, text_len, rope, fp8, prev_hidden_states, prev_clip_weight)
         K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, eps_q, rope)
         K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, eps_k, rope)
         o = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
@@ -117,6 +120,33 @@ class CogVideoXAttnProcessor2_0:
             K.attention(q, pk, pv, o, H, scale=attn.scale, out_scale=w, accumulate=True)
         else:
             K.attention(q, k, v, o, H, scale=attn.scale)
+        return o
+
+    @staticmethod
+    def _attend_fp8(attn, q, k, v, text_len, rope, exps, prev_hidden_states, prev_clip_weight) -> torch.Tensor:
+        """fp8 attention (BASELINE config 5): qk-norm + RoPE written as e4m3 with the static power-of-two factors
+        chosen by `CogVideoXBlock.enable_fp8_attention` (Q's includes scale * log2 e), V packed to e4m3 V^T with
+        per-(d, 32 keys) scales, the block-scaled MFMA kernel; the prev-clip blend as in the bf16 path."""
+        B, Ntok, D = q.shape
+        H = attn.heads
+        q_exp, k_exp = exps
+        qmul = attn.scale * K.LOG2E * 2.0 ** q_exp
+        q8 = K.head_norm_rope_fp8(q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, attn.norm_q.eps, rope, qmul)
+        k8 = K.head_norm_rope_fp8(k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope,
+                                  2.0 ** k_exp)
+        vp = K.v_pack_fp8(v, H)
+        o = torch.empty(B, Ntok, D, device=q.device, dtype=BF16)
+        if prev_hidden_states is not None and prev_clip_weight is not None and prev_clip_weight > 0.0:
+            pkv = _kv(attn, prev_hidden_states.to(BF16).contiguous())
+            pk8 = K.head_norm_rope_fp8(pkv[..., :D], H, text_len, attn.norm_k.weight, attn.norm_k.bias,
+                                       attn.norm_k.eps, rope, 2.0 ** k_exp)
+            pvp = K.v_pack_fp8(pkv[..., D:], H)
+            del pkv
+            w = float(prev_clip_weight)
+            K.attention_fp8(q8, k8, vp, o, H, q_exp, k_exp, out_scale=1.0 - w)
+            K.attention_fp8(q8, pk8, pvp, o, H, q_exp, k_exp, out_scale=w, accumulate=True)
+        else:
+            K.attention_fp8(q8, k8, vp, o, H, q_exp, k_exp)
         return o
 
     def __call__(self, attn, hidden_states: torch.Tensor, encoder_hidden_states: torch.Tensor,

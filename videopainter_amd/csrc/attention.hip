@@ -755,6 +755,264 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
   store_out(d, o, l_run, q, b, h, hl);
 }
 
+
+// ============================================================================================================
+// fp8 attention (BASELINE config 5: "attn + FFN in fp8").  Both products on the block-scaled e4m3 MFMA
+// v_mfma_scale_f32_32x32x64_f8f6f4 (K = 64 per instruction: QK^T over the whole head in ONE MFMA per 32 keys, PV
+// over a 64-key tile in one MFMA per 32 output dims).
+//
+// Operand layout of the 32x32x64 MFMA (measured by vp_mx_mfma_probe32, tests/test_attention_fp8_gpu.py): lane l
+// supplies row l % 32 and the 16-byte K-chunks g = l / 32 and g + 2 (VGPRs 0-3 and 4-7), and the E8M0 scale of
+// (row l % 32, K-block g), a K-block being 32 consecutive K-slots.  C/D as the bf16 32x32 MFMA.
+//
+// Data formats (written by vp_head_norm_rope_fp8 and vp_v_pack_fp8):
+//  * Q, K: e4m3 [B, N, H*64] with ONE power-of-two factor each (Q also carries scale * log2 e), undone by the
+//    MFMA's constant scale bytes.  Their magnitude is bounded by the LayerNorm (|x| <= sqrt(63)|gamma| + |beta|,
+//    RoPE at most sqrt 2 more), so a static factor leaves the whole e4m3 range to the data.
+//  * V^T: e4m3 [B, H, 64 (d), Npad] — keys contiguous per d so the PV A-operand is two 16-byte row reads — with
+//    the keys of every 64-key tile stored in MFMA K-slot order: slot k holds key tile_key(k), the key whose score
+//    the S^T accumulator gives the lane that feeds slot k of the P^T B-operand (so P needs no cross-lane move),
+//    and one E8M0 scale per (d, 32-slot K-block) = per (d, 32 keys): [B, H, Npad/64, 64 lanes][2 (d-half)].
+// ============================================================================================================
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// K-slot -> key within a 64-key tile: slot k = 32 hh + 16 g + e  <->  S^T accumulator element e of half hh held
+// by lane group g (row 8 (e/4) + 4 g + e % 4 of the 32x32 C layout)
+VP_DEV int tile_key(int k) {
+  const int hh = k >> 5, g = (k >> 4) & 1, e = k & 15;
+  return 32 * hh + 8 * (e >> 2) + 4 * g + (e & 3);
+}
+// 64-byte fp8 tile rows in LDS: physical 16-byte chunk = logical ^ swz8(row) (rows 4 apart land 16 banks apart)
+VP_DEV int swz8(int row) { return (row >> 2) & 3; }
+
+// probe: one 32x32x64 scaled MFMA with the layout above; C row-major [32][32] fp32
+__global__ void mx_probe32_kernel(const uint8_t* A, const uint8_t* B, const uint8_t* sa, const uint8_t* sb,
+                                  float* C) {
+  const int l = threadIdx.x;
+  const int r = l & 31, g = l >> 5;
+  i32x8 a, b;
+  u32x4* ah = (u32x4*)&a;
+  u32x4* bh = (u32x4*)&b;
+  ah[0] = *(const u32x4*)(A + r * 64 + g * 16);
+  ah[1] = *(const u32x4*)(A + r * 64 + (g + 2) * 16);
+  bh[0] = *(const u32x4*)(B + r * 64 + g * 16);
+  bh[1] = *(const u32x4*)(B + r * 64 + (g + 2) * 16);
+  f32x16 c;
+  for (int i = 0; i < 16; ++i) c[i] = 0.f;
+  c = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, (int)sa[l], 0, (int)sb[l]);
+  for (int i = 0; i < 16; ++i) C[(8 * (i >> 2) + 4 * g + (i & 3)) * 32 + r] = c[i];
+}
+
+// V [B, N, ld] bf16 (head h at column h*64) -> V^T fp8 in tile K-slot order + per-(d, 32 keys) E8M0 scales.
+// One 256-thread block per (b, h, 64-key tile); thread t: d = t / 4, slots 16 (t % 4) .. +15.
+__global__ __launch_bounds__(256) void v_pack_fp8_kernel(const bf16* __restrict__ V, int64_t v_sb, int64_t v_sn,
+                                                         int N, int H, int ntiles, uint8_t* __restrict__ vt,
+                                                         uint8_t* __restrict__ vs) {
+  __shared__ bf16 tile[64][64 + 8];
+  const int blk = blockIdx.x;
+  const int t = blk % ntiles;
+  const int bh = blk / ntiles;
+  const int h = bh % H, b = bh / H;
+  const int tid = threadIdx.x;
+  const bf16* src = V + (int64_t)b * v_sb + h * 64;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int key = pass * 32 + (tid >> 3);
+    const int n = t * 64 + key;
+    bf16x8 x = {};
+    if (n < N) x = *(const bf16x8*)(src + (int64_t)n * v_sn + (tid & 7) * 8);
+    *(bf16x8*)&tile[key][(tid & 7) * 8] = x;
+  }
+  __syncthreads();
+  const int d = tid >> 2, qq = tid & 3;
+  float v[16];
+  float am = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    v[e] = bf2f(tile[tile_key(16 * qq + e)][d]);
+    am = fmaxf(am, fabsf(v[e]));
+  }
+  am = fmaxf(am, __shfl_xor(am, 1, 64));  // the 32 slots of one K-block = two threads
+  const int sx = mx_exponent(am);
+  const float mul = mx_inv_scale(sx);
+  float lo[8], hi[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    lo[e] = v[e];
+    hi[e] = v[8 + e];
+  }
+  const u32x2 p0 = mx_pack8(lo, mul), p1 = mx_pack8(hi, mul);
+  const int64_t npad = (int64_t)ntiles * 64;
+  *(u32x4*)(vt + ((int64_t)bh * 64 + d) * npad + t * 64 + 16 * qq) = (u32x4){p0[0], p0[1], p1[0], p1[1]};
+  if ((qq & 1) == 0) {
+    const int lane = (d & 31) + 32 * (qq >> 1);  // the MFMA lane that supplies (row d % 32, K-block qq / 2)
+    vs[((int64_t)bh * ntiles + t) * 128 + lane * 2 + (d >> 5)] = (uint8_t)(sx + 127);
+  }
+}
+
+constexpr int F8_TILE = 64 * 64;                   // bytes of a K or V^T tile
+constexpr int F8_STAGE = 2 * F8_TILE + 128;        // + the V^T scales
+constexpr int F8_OFF = 7;                          // P is stored as p * 2^F8_OFF
+constexpr float F8_THR = 1.5f;                     // P <= 2^(F8_OFF + F8_THR) = 362 < 448
+
+// fp8 attention: NW waves x 32 queries per workgroup, 64-key tiles through a 2-slot LDS ring by LDS-DMA (waves
+// 0-3: the 4 K pieces, 4-7: the 4 V^T pieces, wave 0 lanes 0-7 also the V^T scales).  Per tile: S^T for the two
+// 32-key halves (C-init: S = s - m + F8_OFF), one max over both, thresholded rescale, exp2 -> P in e4m3 straight
+// into the PV B-operand registers, PV as two MFMAs over all 64 keys.
+template <int NW, int OCC>
+__global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_desc dd) {
+  static_assert(NW == 8, "the DMA split assumes 8 waves");
+  const vp_attn_desc& d = dd.base;
+  constexpr int QB = NW * 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 5;
+
+  const int nqb = (d.Nq + QB - 1) / QB;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb;
+  const int qb = t - bh * nqb;
+  const int b = bh / d.H;
+  const int h = bh - b * d.H;
+  const int ntiles = dd.npad >> 6;
+
+  const int q = qb * QB + wave * 32 + (lane & 31);
+  const int qc = q < d.Nq ? q : d.Nq - 1;
+  i32x8 qf;
+  {
+    const uint8_t* qrow = (const uint8_t*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+    u32x4* hq = (u32x4*)&qf;
+    hq[0] = *(const u32x4*)(qrow + g * 16);
+    hq[1] = *(const u32x4*)(qrow + (g + 2) * 16);
+  }
+  const int sq = dd.qk_scale & 0xff, sk = (dd.qk_scale >> 8) & 0xff;
+
+  // DMA: this lane's row of its wave's piece (16 rows x 64 B) and the logical source chunk of its physical chunk
+  const int prow = (wave & 3) * 16 + (lane >> 2);
+  const int pch = (lane & 3) ^ swz8(prow);
+  const char* kbase = (const char*)d.K + (int64_t)b * d.k_sb + h * 64;
+  const char* vtbase = (const char*)d.V + (int64_t)bh * 64 * dd.npad;
+  const char* vsbase = (const char*)dd.vs + (int64_t)bh * ntiles * 128;
+  const int ksn = (int)d.k_sn;
+  auto issue = [&](int ti) {
+    char* slot = smem + (ti & 1) * F8_STAGE;
+    if (wave < 4) {
+      const int r = min(ti * 64 + prow, d.Nk - 1);  // rows past the end re-read the last key (masked later)
+      glds16(kbase, r * ksn + pch * 16, slot + wave * 1024);
+    } else {
+      glds16(vtbase + ti * 64, prow * dd.npad + pch * 16, slot + F8_TILE + (wave - 4) * 1024);
+    }
+    if (wave == 0 && lane < 8) glds16(vsbase + ti * 128, lane * 16, slot + 2 * F8_TILE);
+  };
+
+  // LDS read offsets (within a stage) of this lane's two 16-byte chunks of row r: r*64 + ((c ^ swz8(r)) << 4)
+  const int r0 = lane & 31;
+  const int ca = (g ^ swz8(r0)) << 4, cb = ((g + 2) ^ swz8(r0)) << 4;  // swz8(r0 + 32) == swz8(r0)
+
+  float m_run = 0.f, l_run = 0.f, thr = -INFINITY;
+  f32x16 o[2], negm;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    o[0][i] = 0.f;
+    o[1][i] = 0.f;
+    negm[i] = (float)F8_OFF;
+  }
+  const bool active = qb * QB + wave * 32 < d.Nq;  // wave-uniform
+  issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int ti = 0; ti < ntiles; ++ti) {
+    if (ti + 1 < ntiles) issue(ti + 1);
+    const char* st = smem + (ti & 1) * F8_STAGE;
+    if (active) {
+      f32x16 s[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const char* kr = st + (hh * 32 + r0) * 64;
+        i32x8 kf;
+        u32x4* hk = (u32x4*)&kf;
+        hk[0] = *(const u32x4*)(kr + ca);
+        hk[1] = *(const u32x4*)(kr + cb);
+        if (hh == 0) {
+          s[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, negm, 0, 0, 0, sk, 0, sq);
+        } else {
+          // asm: a fresh (early-clobber) destination with C = -m + F8_OFF kept in its own registers (the builtin
+          // form makes the compiler refill a copy of it with 8 v_mov_b64 per tile), then the 19 wait states a VALU
+          // read of a 16-pass XDL result needs (the hazard recognizer cannot see into asm)
+          asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %3, %4, %5 op_sel_hi:[0,0,0]\n\t"
+                       "s_nop 15\n\ts_nop 2"
+                       : "=&v"(s[1])
+                       : "v"(kf), "v"(qf), "v"(negm), "v"(sk), "v"(sq));
+        }
+      }
+      const int lim = d.Nk - ti * 64;
+      if (lim < 64) {
+        mask_half(s[0], lim, 0, g);
+        mask_half(s[1], lim, 1, g);
+      }
+      float mx = s[0][0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[0][i]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) - (float)F8_OFF;
+      }
+      if (__ballot(mx > thr) != 0ull) {
+        const float dm = mx > thr ? mx : 0.f;
+        const float alpha = __builtin_amdgcn_exp2f(-dm);
+        l_run *= alpha;
+        m_run += dm;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          o[0][i] *= alpha;
+          o[1][i] *= alpha;
+          s[0][i] -= dm;
+          s[1][i] -= dm;
+          negm[i] = (float)F8_OFF - m_run;
+        }
+        thr = F8_THR;
+      }
+      // P = exp2(S) in e4m3, 4 per VGPR: VGPRs 0-3 = half 0 (K-slots 16g..), 4-7 = half 1 (32+16g..)
+      i32x8 pf;
+      float ps[4];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float p0 = __builtin_amdgcn_exp2f(s[hh][4 * w + 0]);
+          const float p1 = __builtin_amdgcn_exp2f(s[hh][4 * w + 1]);
+          const float p2 = __builtin_amdgcn_exp2f(s[hh][4 * w + 2]);
+          const float p3 = __builtin_amdgcn_exp2f(s[hh][4 * w + 3]);
+          int pk = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, 0, false);
+          pk = __builtin_amdgcn_cvt_pk_fp8_f32(p2, p3, pk, true);
+          pf[hh * 4 + w] = pk;
+          const float a = (p0 + p1) + (p2 + p3);
+          ps[w] = hh == 0 ? a : ps[w] + a;
+        }
+      l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+      const int vsw = *(const unsigned short*)(st + 2 * F8_TILE + lane * 2);
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const char* vr = st + F8_TILE + (dh * 32 + r0) * 64;
+        i32x8 vf;
+        u32x4* hv = (u32x4*)&vf;
+        hv[0] = *(const u32x4*)(vr + ca);
+        hv[1] = *(const u32x4*)(vr + cb);
+        if (dh == 0)
+          o[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[0], 0, 0, 0, vsw, 0, 127);
+        else
+          o[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[1], 0, 0, 1, vsw, 0, 127);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  store_out(d, o, l_run, q, b, h, g);
+}
 }  // namespace
 
 extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
@@ -816,6 +1074,63 @@ extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
   void* args[] = {(void*)d};
   const hipError_t le = hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(v.nw * 64), args, v.lds,
                                         (hipStream_t)stream);
+  if (le != hipSuccess) return (int)le;
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_mx_mfma_probe32(const void* A, const void* B, const void* sa, const void* sb, float* C,
+                                  void* stream) {
+  if (!A || !B || !sa || !sb || !C) return VP_ERR_ARG;
+  hipLaunchKernelGGL(mx_probe32_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const uint8_t*)A,
+                     (const uint8_t*)B, (const uint8_t*)sa, (const uint8_t*)sb, C);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int64_t vp_v_pack_fp8_bytes(int32_t B, int32_t H, int32_t N, int64_t* npad, int64_t* scale_bytes) {
+  if (B <= 0 || H <= 0 || N <= 0) return -1;
+  const int64_t np = ((int64_t)N + 63) / 64 * 64;
+  if (npad) *npad = np;
+  if (scale_bytes) *scale_bytes = (int64_t)B * H * (np / 64) * 128;
+  return (int64_t)B * H * 64 * np;
+}
+
+extern "C" int vp_v_pack_fp8(const void* V, int64_t v_sb, int64_t v_sn, int32_t B, int32_t N, int32_t H, void* vt,
+                             void* vs, void* stream) {
+  if (!V || !vt || !vs || B <= 0 || N <= 0 || H <= 0 || (v_sn % 8) || (v_sb % 8)) return VP_ERR_ARG;
+  const int ntiles = (N + 63) / 64;
+  const int64_t grid = (int64_t)B * H * ntiles;
+  if (grid > 0x7fffffff) return VP_ERR_ARG;
+  hipLaunchKernelGGL(v_pack_fp8_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, (const bf16*)V,
+                     v_sb, v_sn, N, H, ntiles, (uint8_t*)vt, (uint8_t*)vs);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
+  if (dd == nullptr) return VP_ERR_ARG;
+  const vp_attn_desc& d = dd->base;
+  if (!d.Q || !d.K || !d.V || !d.O || !dd->vs) return VP_ERR_ARG;
+  if (d.head_dim != 64 || d.Nk2 != 0) return VP_ERR_UNSUPPORTED;
+  if (d.B <= 0 || d.H <= 0 || d.Nq <= 0 || d.Nk <= 0) return VP_ERR_ARG;
+  if (dd->npad != (d.Nk + 63) / 64 * 64) return VP_ERR_ARG;
+  if ((d.q_sn % 16) || (d.k_sn % 16) || (d.q_sb % 16) || (d.k_sb % 16) || (d.o_sn % 4) || (d.o_sb % 4))
+    return VP_ERR_ARG;
+  if ((int64_t)d.Nk * d.k_sn > 0x7fffffff || (int64_t)64 * dd->npad > 0x7fffffff) return VP_ERR_ARG;
+  constexpr int NW = 8;
+  static bool attr_set = false;
+  if (!attr_set) {
+    attr_set = true;
+    (void)hipFuncSetAttribute((const void*)attn_fwd_fp8<NW, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * F8_STAGE);
+  }
+  const int nqb = (d.Nq + NW * 32 - 1) / (NW * 32);
+  const int64_t grid = (int64_t)d.B * d.H * nqb;
+  if (grid > 0x7fffffff) return VP_ERR_ARG;
+  void* args[] = {(void*)dd};
+  const hipError_t le = hipLaunchKernel((const void*)attn_fwd_fp8<NW, 4>, dim3((unsigned)grid), dim3(NW * 64), args,
+                                        2 * F8_STAGE, (hipStream_t)stream);
   if (le != hipSuccess) return (int)le;
   VP_CHECK_LAUNCH();
   return VP_OK;

@@ -149,16 +149,18 @@ __global__ __launch_bounds__(ROW_THREADS) void final_norm_kernel(const bf16* __r
 }
 
 // ---- per-head LN(64) + RoPE (attention_processor.py:2143-2154; embeddings.py:655-701) ----
-// 8 lanes per 64-wide head vector (8 elements each); 32 vectors per 256-thread block.
+// 8 lanes per 64-wide head vector (8 elements each); 32 vectors per 256-thread block.  FP8: the bf16 value the
+// bf16 kernel writes, times out_mul, as e4m3 (strides then in bytes)
+template <bool FP8>
 __global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restrict__ xin, int64_t ld_in,
-                                                            int64_t bs_in, bf16* __restrict__ xout, int64_t ld_out,
+                                                            int64_t bs_in, void* __restrict__ xout, int64_t ld_out,
                                                             int64_t bs_out, int64_t nvec, int Ntok, int H,
                                                             int text_len, const bf16* __restrict__ lw,
                                                             const bf16* __restrict__ lb, float eps,
                                                             const float* __restrict__ cosp,
                                                             const float* __restrict__ sinp,
                                                             const uint8_t* __restrict__ tok_mask, int64_t mask_bs,
-                                                            float pre_scale) {
+                                                            float pre_scale, float out_mul) {
   const int64_t vec = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
   const int sub = threadIdx.x & 7;
   const bool valid = vec < nvec;
@@ -215,10 +217,17 @@ __global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restr
     for (int e = 0; e < 8; ++e) x[e] = y[e];
   }
   if (valid) {
-    bf16x8 o;
+    if constexpr (FP8) {
+      float y[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = f2bf(x[e]);
-    *(bf16x8*)(xout + (int64_t)b * bs_out + (int64_t)n * ld_out + h * 64 + sub * 8) = o;
+      for (int e = 0; e < 8; ++e) y[e] = rbf(x[e]);
+      *(u32x2*)((uint8_t*)xout + (int64_t)b * bs_out + (int64_t)n * ld_out + h * 64 + sub * 8) = mx_pack8(y, out_mul);
+    } else {
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(x[e]);
+      *(bf16x8*)((bf16*)xout + (int64_t)b * bs_out + (int64_t)n * ld_out + h * 64 + sub * 8) = o;
+    }
   }
 }
 
@@ -298,9 +307,25 @@ extern "C" int vp_head_norm_rope_bf16(const void* x_in, int64_t ld_in, int64_t b
   if ((cos == nullptr) != (sin == nullptr)) return VP_ERR_ARG;
   const int64_t nvec = (int64_t)B * Ntok * H;
   const int64_t grid = (nvec + 31) / 32;
-  hipLaunchKernelGGL(head_norm_rope_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16*)x_in, ld_in, bs_in, (bf16*)x_out, ld_out, bs_out, nvec, Ntok, H, text_len,
-                     (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, tok_mask, mask_bstride, pre_scale);
+  hipLaunchKernelGGL(head_norm_rope_kernel<false>, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)x_in, ld_in, bs_in, x_out, ld_out, bs_out, nvec, Ntok, H, text_len,
+                     (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, tok_mask, mask_bstride, pre_scale, 1.f);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_head_norm_rope_fp8(const void* x_in, int64_t ld_in, int64_t bs_in, void* q_out, int64_t ld_out,
+                                     int64_t bs_out, int32_t B, int32_t Ntok, int32_t H, int32_t text_len,
+                                     const void* ln_w, const void* ln_b, float eps, const float* cos,
+                                     const float* sin, float out_mul, void* stream) {
+  if (!x_in || !q_out || !ln_w || !ln_b || B <= 0 || Ntok <= 0 || H <= 0) return VP_ERR_ARG;
+  if ((ld_in % 8) || (bs_in % 8) || (ld_out % 8) || (bs_out % 8)) return VP_ERR_ARG;
+  if ((cos == nullptr) != (sin == nullptr) || !(out_mul > 0.f)) return VP_ERR_ARG;
+  const int64_t nvec = (int64_t)B * Ntok * H;
+  const int64_t grid = (nvec + 31) / 32;
+  hipLaunchKernelGGL(head_norm_rope_kernel<true>, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)x_in, ld_in, bs_in, q_out, ld_out, bs_out, nvec, Ntok, H, text_len,
+                     (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, nullptr, 0, 1.f, out_mul);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }

@@ -302,6 +302,97 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
     return out
 
 
+# ---- fp8 attention (BASELINE config 5; formats in include/vp_hip.h) ----
+
+LOG2E = 1.4426950408889634
+
+
+def mx_mfma_probe32(A: torch.Tensor, B: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) -> torch.Tensor:
+    """One v_mfma_scale_f32_32x32x64_f8f6f4 (layout self-test): A, B uint8 e4m3 [32, 64]; sa, sb uint8 [64]."""
+    Cm = torch.empty(32, 32, device=A.device, dtype=torch.float32)
+    N.check(N.lib().vp_mx_mfma_probe32(_p(A), _p(B), _p(sa), _p(sb), _p(Cm), _stream()), "vp_mx_mfma_probe32")
+    return Cm
+
+
+def qk_fp8_exponent(ln_w: torch.Tensor, ln_b: torch.Tensor, mul: float = 1.0) -> int:
+    """Largest a with |x| * mul * 2^a <= 448 for every output x of LN(64) + RoPE with this affine: after the
+    LayerNorm |x_hat| <= sqrt(63), so |x| <= sqrt(63) max|gamma| + max|beta|, and RoPE mixes pairs (x sqrt 2)."""
+    import math
+    bound = math.sqrt(2.0) * (math.sqrt(63.0) * float(ln_w.float().abs().max()) + float(ln_b.float().abs().max()))
+    bound = max(bound * mul, 1e-30)
+    return int(math.floor(math.log2(448.0 / bound)))
+
+
+def head_norm_rope_fp8(x_in: torch.Tensor, heads: int, text_len: int, ln_w, ln_b, eps: float, rope, out_mul: float,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """LN(64) + RoPE as `head_norm_rope`, written as e4m3 (x * out_mul) into uint8 [B, N, heads*64]."""
+    _chk(x_in, "x_in")
+    B, Ntok, _ = x_in.shape
+    if out is None:
+        out = torch.empty(B, Ntok, heads * 64, device=x_in.device, dtype=torch.uint8)
+    cos = sin = None
+    if rope is not None:
+        cos, sin = rope
+        _chk(cos, "cos", torch.float32)
+        _chk(sin, "sin", torch.float32)
+        if cos.shape[0] != Ntok - text_len or cos.shape[1] != 64 or not cos.is_contiguous() or not sin.is_contiguous():
+            raise ValueError(f"rope tables must be fp32 [{Ntok - text_len}, 64], got {tuple(cos.shape)}")
+    N.check(N.lib().vp_head_norm_rope_fp8(_p(x_in), x_in.stride(1), x_in.stride(0), _p(out), out.stride(1),
+                                          out.stride(0), B, Ntok, heads, text_len, _p(ln_w), _p(ln_b), eps, _p(cos),
+                                          _p(sin), out_mul, _stream()), "vp_head_norm_rope_fp8")
+    return out
+
+
+class VPacked:
+    """V^T in e4m3 with the fp8 attention's tile K-slot order and per-(d, 32 keys) E8M0 scales."""
+
+    def __init__(self, vt: torch.Tensor, vs: torch.Tensor, npad: int, n: int):
+        self.vt, self.vs, self.npad, self.n = vt, vs, npad, n
+
+
+def v_pack_fp8(v: torch.Tensor, heads: int) -> VPacked:
+    _chk(v, "v")
+    B, Nk, _ = v.shape
+    npad, sbytes = C.c_int64(), C.c_int64()
+    nb = N.lib().vp_v_pack_fp8_bytes(B, heads, Nk, C.byref(npad), C.byref(sbytes))
+    if nb <= 0:
+        raise ValueError("bad V shape")
+    vt = torch.empty(nb, device=v.device, dtype=torch.uint8)
+    vs = torch.empty(sbytes.value, device=v.device, dtype=torch.uint8)
+    N.check(N.lib().vp_v_pack_fp8(_p(v), v.stride(0), v.stride(1), B, Nk, heads, _p(vt), _p(vs), _stream()),
+            "vp_v_pack_fp8")
+    return VPacked(vt, vs, npad.value, Nk)
+
+
+def attention_fp8(q8: torch.Tensor, k8: torch.Tensor, vp: VPacked, out: torch.Tensor, heads: int, q_exp: int,
+                  k_exp: int, out_scale: float = 1.0, accumulate: bool = False) -> torch.Tensor:
+    """q8 = e4m3(q * scale * log2 e * 2^q_exp), k8 = e4m3(k * 2^k_exp): uint8 [B, N, heads*64]; out bf16."""
+    for t, n in ((q8, "q8"), (k8, "k8")):
+        _chk(t, n, torch.uint8)
+        if t.dim() != 3 or t.stride(-1) != 1 or t.shape[-1] != heads * 64:
+            raise ValueError(f"{n} must be [B, N, heads*64] uint8")
+    _chk(out, "out")
+    if k8.shape[1] != vp.n:
+        raise ValueError("k and packed v lengths differ")
+    if not (-127 <= q_exp <= 127 and -127 <= k_exp <= 127):
+        raise ValueError("scale exponents out of the E8M0 range")
+    dd = N.AttnFp8Desc()
+    d = dd.base
+    d.B, d.H, d.Nq, d.head_dim = q8.shape[0], heads, q8.shape[1], 64
+    d.Q, d.q_sb, d.q_sn = _p(q8), q8.stride(0), q8.stride(1)
+    d.K, d.k_sb, d.k_sn = _p(k8), k8.stride(0), k8.stride(1)
+    d.V = _p(vp.vt)
+    d.Nk = k8.shape[1]
+    d.O, d.o_sb, d.o_sn = _p(out), out.stride(0), out.stride(1)
+    d.scale, d.out_scale, d.accumulate = 1.0, out_scale, int(accumulate)
+    dd.vs, dd.npad = _p(vp.vs), vp.npad
+    dd.qk_scale = (127 - q_exp) | ((127 - k_exp) << 8)
+    ev = _t0("attention_fp8")
+    N.check(N.lib().vp_attention_fwd_fp8(C.byref(dd), _stream()), "vp_attention_fwd_fp8")
+    _t1("attention_fp8", ev)
+    return out
+
+
 # ------------------------------------------------------------------------------------------------------------------
 # norms
 # ------------------------------------------------------------------------------------------------------------------

@@ -219,6 +219,18 @@ class CogVideoXBlock(nn.Module):
             raise ValueError(f"fp8 FeedForward needs widths that are multiples of 256, got {tuple(w1.shape)}")
         self.ff_mx = (K.mx_quantize(w1), K.mx_quantize(w2))
 
+    def enable_fp8_attention(self, enabled: bool = True) -> None:
+        """Run self-attention on the block-scaled fp8 MFMA (vp_attention_fwd_fp8): Q and K leave the qk-norm + RoPE
+        kernel as e4m3 with one static power-of-two factor each, chosen from the LayerNorm's bound on its outputs
+        (kernels.qk_fp8_exponent: nothing can saturate), V is packed to e4m3 with per-(channel, 32 keys) scales,
+        and P is rounded to e4m3 inside the kernel.  The resample processor (two K/V segments) stays bf16."""
+        attn = self.attn1
+        if not enabled:
+            attn.fp8_qk_exp = None
+            return
+        attn.fp8_qk_exp = (K.qk_fp8_exponent(attn.norm_q.weight, attn.norm_q.bias, attn.scale * K.LOG2E),
+                           K.qk_fp8_exponent(attn.norm_k.weight, attn.norm_k.bias))
+
     # -- joint-buffer fast path used by the models --
     def forward_joint(self, x: torch.Tensor, text_len: int, temb: torch.Tensor, rope=None,
                       resample_mask: Optional[torch.Tensor] = None, prev_joint: Optional[torch.Tensor] = None,
@@ -337,6 +349,18 @@ class CogVideoXTransformer3DModel(ModelMixin):
         for blk in self.transformer_blocks:
             blk.enable_fp8_ffn(enabled)
         return self
+
+    def enable_fp8_attention(self, enabled: bool = True):
+        """fp8 self-attention in every block (BASELINE config 5; see CogVideoXBlock.enable_fp8_attention).  Call
+        after the weights are loaded (the Q/K factors come from the qk-norm affine)."""
+        for blk in self.transformer_blocks:
+            blk.enable_fp8_attention(enabled)
+        return self
+
+    def enable_fp8(self, ffn: bool = True, attention: bool = True):
+        """BASELINE config 5: "attn + FFN in fp8"."""
+        self.enable_fp8_ffn(ffn)
+        return self.enable_fp8_attention(attention)
 
     def _patch_channels(self):
         return self.config.in_channels
