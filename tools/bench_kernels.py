@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--gemm-variants", default="1,2")
     ap.add_argument("--variant", default="", help="attention kernel variant(s), e.g. 1 or 1,3")
+    ap.add_argument("--variant8", default="", help="fp8 attention kernel variant(s) (VP_ATTN8_VARIANT), e.g. 1,2")
     ap.add_argument("--only", default="", help="attention | attn8 | gemm | mx: run just that kernel (for rocprofv3 "
                     "--pmc passes; attn8 = the fp8 attention only)")
     args = ap.parse_args()
@@ -115,9 +116,13 @@ def main():
         print("v_pack_fp8", res["v_pack_fp8"], flush=True)
         vp = K.v_pack_fp8(v, H)
         for rnd in range(2):
-            t = timeit(lambda: K.attention_fp8(q8, k8, vp, o, H, q_exp, k_exp), max(2, args.iters // 2))
-            res[f"attention_fp8_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
-            print("attention fp8", res[f"attention_fp8_r{rnd}"], flush=True)
+            for var in (args.variant8.split(",") if args.variant8 else [""]):
+                if var:
+                    os.environ["VP_ATTN8_VARIANT"] = var
+                t = timeit(lambda: K.attention_fp8(q8, k8, vp, o, H, q_exp, k_exp), max(2, args.iters // 2))
+                res[f"attention_fp8_v{var}_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
+                print("attention fp8", var, res[f"attention_fp8_v{var}_r{rnd}"], flush=True)
+        os.environ.pop("VP_ATTN8_VARIANT", None)
         print(json.dumps(res))
         return
     xin = torch.randn(B, Ntok, D, device=dev).to(torch.bfloat16)

@@ -235,11 +235,12 @@ VP_DEV void qk_half(const char* Kl, int kh, const bf16x8 (&qf)[4], f32x16& s, in
 }
 
 VP_DEV void mask_half(f32x16& s, int lim, int kh, int hl) {
+  // key = kh*32 + (i&3) + 8*(i>>2) + 4*hl >= lim, with the lane part moved to the limit so every compare is
+  // against an inline constant (otherwise the compiler hoists 16 per-lane key indices out of the tile loop)
+  const int l2 = lim - kh * 32 - 4 * hl;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int key = kh * 32 + (i & 3) + 8 * (i >> 2) + 4 * hl;
-    if (key >= lim) s[i] = -INFINITY;
-  }
+  for (int i = 0; i < 16; ++i)
+    if ((i & 3) + 8 * (i >> 2) >= l2) s[i] = -INFINITY;
 }
 
 VP_DEV void softmax_half(f32x16& s, float& m_run, float& l_run, f32x16 (&o)[2], bf16x8 (&pf)[2], float c) {
@@ -852,16 +853,39 @@ __global__ __launch_bounds__(256) void v_pack_fp8_kernel(const bf16* __restrict_
 
 constexpr int F8_TILE = 64 * 64;                   // bytes of a K or V^T tile
 constexpr int F8_STAGE = 2 * F8_TILE + 128;        // + the V^T scales
-constexpr int F8_OFF = 7;                          // P is stored as p * 2^F8_OFF
-constexpr float F8_THR = 1.5f;                     // P <= 2^(F8_OFF + F8_THR) = 362 < 448
 
 // fp8 attention: NW waves x 32 queries per workgroup, 64-key tiles through a 2-slot LDS ring by LDS-DMA (waves
 // 0-3: the 4 K pieces, 4-7: the 4 V^T pieces, wave 0 lanes 0-7 also the V^T scales).  Per tile: S^T for the two
 // 32-key halves (C-init: S = s - m + F8_OFF), one max over both, thresholded rescale, exp2 -> P in e4m3 straight
 // into the PV B-operand registers, PV as two MFMAs over all 64 keys.
-template <int NW, int OCC>
+// P = exp2(S) in e4m3, 4 per VGPR: VGPRs 0-3 = half 0 (K-slots 16g..), 4-7 = half 1 (32+16g..); returns this
+// lane's sum of the 32 values
+VP_DEV float f8_exp_pack(const f32x16 (&s)[2], i32x8& pf) {
+  float ps[4];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float p0 = __builtin_amdgcn_exp2f(s[hh][4 * w + 0]);
+      const float p1 = __builtin_amdgcn_exp2f(s[hh][4 * w + 1]);
+      const float p2 = __builtin_amdgcn_exp2f(s[hh][4 * w + 2]);
+      const float p3 = __builtin_amdgcn_exp2f(s[hh][4 * w + 3]);
+      int pk = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, 0, false);
+      pk = __builtin_amdgcn_cvt_pk_fp8_f32(p2, p3, pk, true);
+      pf[hh * 4 + w] = pk;
+      const float a = (p0 + p1) + (p2 + p3);
+      ps[w] = hh == 0 ? a : ps[w] + a;
+    }
+  return (ps[0] + ps[1]) + (ps[2] + ps[3]);
+}
+
+// LAZY (lazy-max, as softmax_half_lazy): P stored as p * 2^6, the max path only when a lane's 32 stored values
+// sum past 448; otherwise P = p * 2^7 with the max path every tile and rescale threshold 1.5 (P <= 2^8.5 < 448).
+template <int NW, int OCC, bool LAZY = false>
 __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_desc dd) {
   static_assert(NW == 8, "the DMA split assumes 8 waves");
+  constexpr int OFF = LAZY ? 6 : 7;              // P is stored as p * 2^OFF
+  constexpr float THR = LAZY ? 2.5f : 1.5f;      // max path: P <= 2^(OFF + THR) < 448
   const vp_attn_desc& d = dd.base;
   constexpr int QB = NW * 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -917,7 +941,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
   for (int i = 0; i < 16; ++i) {
     o[0][i] = 0.f;
     o[1][i] = 0.f;
-    negm[i] = (float)F8_OFF;
+    negm[i] = (float)OFF;
   }
   const bool active = qb * QB + wave * 32 < d.Nq;  // wave-uniform
   issue(0);
@@ -928,72 +952,80 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
     const char* st = smem + (ti & 1) * F8_STAGE;
     if (active) {
       f32x16 s[2];
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const char* kr = st + (hh * 32 + r0) * 64;
-        i32x8 kf;
-        u32x4* hk = (u32x4*)&kf;
-        hk[0] = *(const u32x4*)(kr + ca);
-        hk[1] = *(const u32x4*)(kr + cb);
-        if (hh == 0) {
-          s[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, negm, 0, 0, 0, sk, 0, sq);
-        } else {
-          // asm: a fresh (early-clobber) destination with C = -m + F8_OFF kept in its own registers (the builtin
-          // form makes the compiler refill a copy of it with 8 v_mov_b64 per tile), then the 19 wait states a VALU
-          // read of a 16-pass XDL result needs (the hazard recognizer cannot see into asm)
-          asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %3, %4, %5 op_sel_hi:[0,0,0]\n\t"
-                       "s_nop 15\n\ts_nop 2"
-                       : "=&v"(s[1])
-                       : "v"(kf), "v"(qf), "v"(negm), "v"(sk), "v"(sq));
-        }
-      }
       const int lim = d.Nk - ti * 64;
-      if (lim < 64) {
-        mask_half(s[0], lim, 0, g);
-        mask_half(s[1], lim, 1, g);
-      }
-      float mx = s[0][0];
+      auto scores = [&]() {
 #pragma unroll
-      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[0][i]);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
-      {
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) - (float)F8_OFF;
-      }
-      if (__ballot(mx > thr) != 0ull) {
-        const float dm = mx > thr ? mx : 0.f;
-        const float alpha = __builtin_amdgcn_exp2f(-dm);
-        l_run *= alpha;
-        m_run += dm;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          o[0][i] *= alpha;
-          o[1][i] *= alpha;
-          s[0][i] -= dm;
-          s[1][i] -= dm;
-          negm[i] = (float)F8_OFF - m_run;
+        for (int hh = 0; hh < 2; ++hh) {
+          const char* kr = st + (hh * 32 + r0) * 64;
+          i32x8 kf;
+          u32x4* hk = (u32x4*)&kf;
+          hk[0] = *(const u32x4*)(kr + ca);
+          hk[1] = *(const u32x4*)(kr + cb);
+          if (hh == 0) {
+            if constexpr (LAZY)  // opaque, so the fallback's recomputation is not merged with this one
+              asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %3, %4, %5 op_sel_hi:[0,0,0]"
+                           : "=&v"(s[0])
+                           : "v"(kf), "v"(qf), "v"(negm), "v"(sk), "v"(sq));
+            else
+              s[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, negm, 0, 0, 0, sk, 0, sq);
+          } else {
+            // asm: a fresh (early-clobber) destination with C = -m + OFF kept in its own registers (the builtin
+            // form makes the compiler refill a copy of it with 8 v_mov_b64 per tile), then the 19 wait states a
+            // VALU read of a 16-pass XDL result needs (the hazard recognizer cannot see into asm)
+            asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %3, %4, %5 op_sel_hi:[0,0,0]\n\t"
+                         "s_nop 15\n\ts_nop 2"
+                         : "=&v"(s[1])
+                         : "v"(kf), "v"(qf), "v"(negm), "v"(sk), "v"(sq));
+          }
         }
-        thr = F8_THR;
-      }
-      // P = exp2(S) in e4m3, 4 per VGPR: VGPRs 0-3 = half 0 (K-slots 16g..), 4-7 = half 1 (32+16g..)
+        if (lim < 64) {
+          mask_half(s[0], lim, 0, g);
+          mask_half(s[1], lim, 1, g);
+        }
+      };
+      scores();
+      // max path: the tile max over both halves and the lane pair, thresholded rescale of O, l, S and -m
+      auto max_path = [&]() {
+        float mx = s[0][0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[0][i]);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
+        {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+          mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) - (float)OFF;
+        }
+        if (__ballot(mx > thr) != 0ull) {
+          const float dm = mx > thr ? mx : 0.f;
+          const float alpha = __builtin_amdgcn_exp2f(-dm);
+          l_run *= alpha;
+          m_run += dm;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            o[0][i] *= alpha;
+            o[1][i] *= alpha;
+            s[0][i] -= dm;
+            s[1][i] -= dm;
+            negm[i] = (float)OFF - m_run;
+          }
+          thr = THR;
+        }
+      };
       i32x8 pf;
-      float ps[4];
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const float p0 = __builtin_amdgcn_exp2f(s[hh][4 * w + 0]);
-          const float p1 = __builtin_amdgcn_exp2f(s[hh][4 * w + 1]);
-          const float p2 = __builtin_amdgcn_exp2f(s[hh][4 * w + 2]);
-          const float p3 = __builtin_amdgcn_exp2f(s[hh][4 * w + 3]);
-          int pk = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, 0, false);
-          pk = __builtin_amdgcn_cvt_pk_fp8_f32(p2, p3, pk, true);
-          pf[hh * 4 + w] = pk;
-          const float a = (p0 + p1) + (p2 + p3);
-          ps[w] = hh == 0 ? a : ps[w] + a;
-        }
-      l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+      float ls;
+      // lazy: no max; a lane sum <= 448 bounds each of its 32 stored values (e4m3 max), else the scores are
+      // recomputed (rare; keeping all 32 live through the exp2 pass would not fit 128 VGPRs) for the max path
+      bool need_max = !LAZY || thr == -INFINITY;
+      if (!need_max) {
+        ls = f8_exp_pack(s, pf);
+        need_max = __ballot(!(ls <= 448.f)) != 0ull;
+        if (need_max) scores();
+      }
+      if (need_max) {
+        max_path();
+        ls = f8_exp_pack(s, pf);
+      }
+      l_run += ls;
       const int vsw = *(const unsigned short*)(st + 2 * F8_TILE + lane * 2);
 #pragma unroll
       for (int dh = 0; dh < 2; ++dh) {
@@ -1119,18 +1151,24 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
     return VP_ERR_ARG;
   if ((int64_t)d.Nk * d.k_sn > 0x7fffffff || (int64_t)64 * dd->npad > 0x7fffffff) return VP_ERR_ARG;
   constexpr int NW = 8;
+  // variants (A/B switch VP_ATTN8_VARIANT): 1 = max path every tile (default), 2 = lazy max (needs 159 VGPRs: spills at
+  // 128; 0.21 PF/s), 3 / 4 = 1 / 2 at 3 waves/SIMD (1.01 / 0.69 PF/s against 1.43)
+  static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, false>, (const void*)attn_fwd_fp8<NW, 4, true>,
+                                    (const void*)attn_fwd_fp8<NW, 3, false>, (const void*)attn_fwd_fp8<NW, 3, true>};
   static bool attr_set = false;
   if (!attr_set) {
     attr_set = true;
-    (void)hipFuncSetAttribute((const void*)attn_fwd_fp8<NW, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              2 * F8_STAGE);
+    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * F8_STAGE);
   }
+  const char* e = getenv("VP_ATTN8_VARIANT");
+  int variant = e != nullptr ? atoi(e) : 0;
+  if (variant < 1 || variant > 4) variant = 1;
   const int nqb = (d.Nq + NW * 32 - 1) / (NW * 32);
   const int64_t grid = (int64_t)d.B * d.H * nqb;
   if (grid > 0x7fffffff) return VP_ERR_ARG;
   void* args[] = {(void*)dd};
-  const hipError_t le = hipLaunchKernel((const void*)attn_fwd_fp8<NW, 4>, dim3((unsigned)grid), dim3(NW * 64), args,
-                                        2 * F8_STAGE, (hipStream_t)stream);
+  const hipError_t le = hipLaunchKernel(fns[variant - 1], dim3((unsigned)grid), dim3(NW * 64), args, 2 * F8_STAGE,
+                                        (hipStream_t)stream);
   if (le != hipSuccess) return (int)le;
   VP_CHECK_LAUNCH();
   return VP_OK;
