@@ -164,6 +164,96 @@ VP_DEV void mfma_mx(f32x4& acc, const i32x8& w, const i32x8& a, int sw, int sa) 
                  : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
 }
 
+// ---- fused epilogue shared by the GEMM kernels: acc[j][i] = the 16x16 fragment (W rows j, A rows i) of a wave
+// whose C block is rows wr*WM.., cols wc*WN.. of the BM x BN tile; NT threads stream the LDS C image out ----
+template <int NT, int FN_, int FM_, int WN_, int WM_, bool FP8>
+VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&acc)[FN_][FM_], char* smem, int m0,
+                          int n0, int wr, int wc, int lane, int tid) {
+  constexpr int FN = FN_, FM = FM_, WN = WN_, WM = WM_;
+  // ---- epilogue phase 1: per-fragment bias / activation, bf16 into the LDS C image ----
+  const int epi = d.epilogue;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nloc = wc * WN + j * 16 + (lane >> 4) * 4;  // 4 consecutive columns
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + nloc + r;
+      if (n < d.N) {
+        const int sg = n / d.n_seg;
+        const bf16* bp = (const bf16*)d.bias[sg];
+        if (bp != nullptr) bv[r] = bf2f(bp[n - sg * d.n_seg]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int mloc = wr * WM + i * 16 + (lane & 15);
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = rbf(acc[j][i][r] + bv[r]);
+        if (epi == VP_EPI_BIAS_GELU || epi == VP_EPI_BIAS_GELU_MXFP8) v = gelu_tanh(v);
+        else if (epi == VP_EPI_BIAS_SCALE) v = v * d.alpha;
+        o[r] = f2bf(v);
+      }
+      *(bf16x4*)(smem + mloc * CT_STRIDE + nloc * 2) = o;
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue phase 2: coalesced 16-byte row stores (+ residual / gate / injection / pos-emb) ----
+  bf16* C = (bf16*)d.C;
+  const int chunk = tid & 31;         // 16-byte chunk within the 512-byte tile row
+  const int ncol = n0 + chunk * 8;
+#pragma unroll 1
+  for (int it = 0; it < BM / (NT / 32); ++it) {
+    const int mloc = it * (NT / 32) + (tid >> 5);
+    const int m = m0 + mloc;
+    if (m >= d.M || ncol >= d.N) continue;
+    bf16x8 v = *(const bf16x8*)(smem + mloc * CT_STRIDE + chunk * 16);
+    const int64_t orow = (int64_t)(m / d.rows_per_group) * d.group_stride + d.row_offset + (m % d.rows_per_group);
+    if (FP8 && epi == VP_EPI_BIAS_GELU_MXFP8) {
+      // MX-quantise the GELU output: the 4 lanes holding one 32-column block agree on its scale (N % 256 == 0, so
+      // a block's lanes are all in or all out of range)
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = bf2f(v[e]);
+      uint8_t sb;
+      const u32x2 q = mx_quantize_quarter(f, sb);
+      *(u32x2*)((uint8_t*)d.C + orow * d.ldc + ncol) = q;
+      if ((tid & 3) == 0) mx.c_scale[mx_scale_off(orow, ncol >> 5, d.N)] = sb;
+      continue;
+    }
+    if (epi == VP_EPI_GATED) {
+      const int b = m / d.tokens_per_batch;
+      const int tok = m - b * d.tokens_per_batch;
+      const bf16* g = (const bf16*)(tok < d.text_len ? d.gate_text : d.gate) + (int64_t)b * d.gate_bstride + ncol;
+      const bf16x8 gv = *(const bf16x8*)g;
+      const bf16x8 rv = *(const bf16x8*)((const bf16*)d.R + orow * d.ldr + ncol);
+      bool inj = false;
+      bf16x8 iv;
+      if (d.inject != nullptr && tok >= d.text_len) {
+        const int vtok = tok - d.text_len;
+        inj = (d.inject_mask == nullptr) || (d.inject_mask[(int64_t)b * d.inject_mask_bstride + vtok] == 0);
+        if (inj) iv = *(const bf16x8*)((const bf16*)d.inject + (int64_t)b * d.inject_bstride +
+                                       (int64_t)vtok * d.inject_ld + ncol);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float o = rbf(bf2f(rv[e]) + rbf(bf2f(gv[e]) * bf2f(v[e])));
+        if (inj) o = rbf(o + bf2f(iv[e]));
+        v[e] = f2bf(o);
+      }
+    } else if (epi == VP_EPI_BIAS_ADDROWS) {
+      const bf16x8 pv = *(const bf16x8*)((const bf16*)d.addrows +
+                                         (int64_t)((m % d.rows_per_group) + d.addrows_offset) * d.addrows_ld + ncol);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(pv[e]));
+    }
+    *(bf16x8*)(C + orow * d.ldc + ncol) = v;
+  }
+}
+
 template <int VAR, bool FP8 = false>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_desc d, const MxExt mx) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -655,88 +745,119 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     __syncthreads();  // all waves done with the ring before the epilogue reuses the LDS
   }
 
-  // ---- epilogue phase 1: per-fragment bias / activation, bf16 into the LDS C image ----
-  const int epi = d.epilogue;
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int nloc = wc * WN + j * 16 + (lane >> 4) * 4;  // 4 consecutive columns
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + nloc + r;
-      if (n < d.N) {
-        const int sg = n / d.n_seg;
-        const bf16* bp = (const bf16*)d.bias[sg];
-        if (bp != nullptr) bv[r] = bf2f(bp[n - sg * d.n_seg]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int mloc = wr * WM + i * 16 + (lane & 15);
-      bf16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = rbf(acc[j][i][r] + bv[r]);
-        if (epi == VP_EPI_BIAS_GELU || epi == VP_EPI_BIAS_GELU_MXFP8) v = gelu_tanh(v);
-        else if (epi == VP_EPI_BIAS_SCALE) v = v * d.alpha;
-        o[r] = f2bf(v);
-      }
-      *(bf16x4*)(smem + mloc * CT_STRIDE + nloc * 2) = o;
-    }
-  }
-  __syncthreads();
+  gemm_epilogue<NTHREADS, FN, FM, WN, WM, FP8>(d, mx, acc, smem, m0, n0, wr, wc, lane, tid);
+}
 
-  // ---- epilogue phase 2: coalesced 16-byte row stores (+ residual / gate / injection / pos-emb) ----
-  bf16* C = (bf16*)d.C;
-  const int chunk = tid & 31;         // 16-byte chunk within the 512-byte tile row
-  const int ncol = n0 + chunk * 8;
-#pragma unroll 1
-  for (int it = 0; it < BM / 16; ++it) {
-    const int mloc = it * 16 + (tid >> 5);
-    const int m = m0 + mloc;
-    if (m >= d.M || ncol >= d.N) continue;
-    bf16x8 v = *(const bf16x8*)(smem + mloc * CT_STRIDE + chunk * 16);
-    const int64_t orow = (int64_t)(m / d.rows_per_group) * d.group_stride + d.row_offset + (m % d.rows_per_group);
-    if (FP8 && epi == VP_EPI_BIAS_GELU_MXFP8) {
-      // MX-quantise the GELU output: the 4 lanes holding one 32-column block agree on its scale (N % 256 == 0, so
-      // a block's lanes are all in or all out of range)
-      float f[8];
+
+// ------------------------------------------------------------------------------------------------------------
+// Variant 6: 4 waves, ONE per SIMD, 128x128 C block per wave (8x8 16x16x32 fragments = 256 accumulator registers,
+// in the AGPR half of the 512-register file a single wave per SIMD owns).  Same 256x256 tile, BK = 32 half-steps
+// through a 4-slot LDS ring filled by LDS-DMA two half-steps ahead; the next half-step's 16 fragments (64 VGPRs) are
+// read while the current one's 64 MFMAs run, so one barrier per 1024 MFMA-cycles (the 8-wave kernels pay one per
+// 256-512).  Needs K % 32 == 0 and 32-bit source offsets.
+// ------------------------------------------------------------------------------------------------------------
+constexpr int W4_THREADS = 256;
+constexpr int W4_WM = 128, W4_WN = 128, W4_FM = 8, W4_FN = 8;
+
+__global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const vp_gemm_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1;  // 0..1 (M)
+  const int wc = wave & 1;   // 0..1 (N)
+
+  const int tiles_m = (d.M + BM - 1) / BM;
+  const int tiles_n = (d.N + BN - 1) / BN;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int group_id = t / per_group;
+  const int first_m = group_id * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + ((t % per_group) % gsz);
+  const int tn = (t % per_group) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // LDS-DMA pieces: a half-step slot holds A [256 rows][64 B] then W [256][64 B]; piece pc = 16 rows (1 KiB) ->
+  // wave-instruction i (0..7): operand i / 4, piece (i % 4) * 4 + wave; lane l -> row pc*16 + l/4, physical chunk
+  // l % 4 = logical chunk ^ swz64(row).  Per-lane 32-bit byte offsets from wave-uniform bases (row clamped).
+  int off[8];
+  const char* base[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = bf2f(v[e]);
-      uint8_t sb;
-      const u32x2 q = mx_quantize_quarter(f, sb);
-      *(u32x2*)((uint8_t*)d.C + orow * d.ldc + ncol) = q;
-      if ((tid & 3) == 0) mx.c_scale[mx_scale_off(orow, ncol >> 5, d.N)] = sb;
-      continue;
+  for (int i = 0; i < 8; ++i) {
+    const int pc = (i & 3) * 4 + wave;
+    const int r = pc * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ swz64(r);
+    if (i < 4) {
+      base[i] = (const char*)d.A;
+      off[i] = min(m0 + r, d.M - 1) * (int)d.lda * 2 + c * 16;
+    } else {
+      const int sg = __builtin_amdgcn_readfirstlane(min(n0 + pc * 16, d.N - 1) / d.n_seg);
+      base[i] = (const char*)d.W[sg];
+      off[i] = (min(n0 + r, d.N - 1) - sg * d.n_seg) * d.K * 2 + c * 16;
     }
-    if (epi == VP_EPI_GATED) {
-      const int b = m / d.tokens_per_batch;
-      const int tok = m - b * d.tokens_per_batch;
-      const bf16* g = (const bf16*)(tok < d.text_len ? d.gate_text : d.gate) + (int64_t)b * d.gate_bstride + ncol;
-      const bf16x8 gv = *(const bf16x8*)g;
-      const bf16x8 rv = *(const bf16x8*)((const bf16*)d.R + orow * d.ldr + ncol);
-      bool inj = false;
-      bf16x8 iv;
-      if (d.inject != nullptr && tok >= d.text_len) {
-        const int vtok = tok - d.text_len;
-        inj = (d.inject_mask == nullptr) || (d.inject_mask[(int64_t)b * d.inject_mask_bstride + vtok] == 0);
-        if (inj) iv = *(const bf16x8*)((const bf16*)d.inject + (int64_t)b * d.inject_bstride +
-                                       (int64_t)vtok * d.inject_ld + ncol);
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float o = rbf(bf2f(rv[e]) + rbf(bf2f(gv[e]) * bf2f(v[e])));
-        if (inj) o = rbf(o + bf2f(iv[e]));
-        v[e] = f2bf(o);
-      }
-    } else if (epi == VP_EPI_BIAS_ADDROWS) {
-      const bf16x8 pv = *(const bf16x8*)((const bf16*)d.addrows +
-                                         (int64_t)((m % d.rows_per_group) + d.addrows_offset) * d.addrows_ld + ncol);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(pv[e]));
-    }
-    *(bf16x8*)(C + orow * d.ldc + ncol) = v;
   }
+  const int nh = d.K / HK;
+  auto issue = [&](int h) {
+    char* slot = smem + (h & 3) * HSLOT;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) glds16(base[i] + h * 64, off[i], slot + (i >> 2) * HTILE + ((i & 3) * 4 + wave) * 1024);
+  };
+  const int ch = lane >> 4;
+  auto read = [&](int h, bf16x8 (&af)[W4_FM], bf16x8 (&wf)[W4_FN]) {
+    const char* As = smem + (h & 3) * HSLOT;
+    const char* Bs = As + HTILE;
+#pragma unroll
+    for (int i = 0; i < W4_FM; ++i) af[i] = lds_frag64(As, wr * W4_WM + i * 16 + (lane & 15), ch);
+#pragma unroll
+    for (int j = 0; j < W4_FN; ++j) wf[j] = lds_frag64(Bs, wc * W4_WN + j * 16 + (lane & 15), ch);
+  };
+  f32x4 acc[W4_FN][W4_FM];
+#pragma unroll
+  for (int j = 0; j < W4_FN; ++j)
+#pragma unroll
+    for (int i = 0; i < W4_FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const bf16x8 (&af)[W4_FM], const bf16x8 (&wf)[W4_FN]) {
+#pragma unroll
+    for (int j = 0; j < W4_FN; ++j)
+#pragma unroll
+      for (int i = 0; i < W4_FM; ++i)
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+  };
+  issue(0);
+  if (nh > 1) issue(1);
+  if (nh > 2) issue(2);
+  if (nh > 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // half-step 0 landed (1, 2 in flight)
+  else if (nh > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  bf16x8 afA[W4_FM], wfA[W4_FN], afB[W4_FM], wfB[W4_FN];
+  read(0, afA, wfA);
+  // half-step h: wait for h+1 (only h+2 may stay in flight), one barrier publishes it (and every wave has long
+  // finished reading slot (h-1)&3: its fragments fed the previous half-step's MFMAs), DMA h+3 into that slot, read
+  // h+1's fragments, then the 64 MFMAs of h
+  auto step = [&](int h, const bf16x8 (&afc)[W4_FM], const bf16x8 (&wfc)[W4_FN], bf16x8 (&afn)[W4_FM],
+                  bf16x8 (&wfn)[W4_FN]) {
+    if (h + 1 < nh) {
+      if (h + 2 < nh) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (h + 3 < nh) issue(h + 3);
+      read(h + 1, afn, wfn);
+    }
+    mma(afc, wfc);
+  };
+  int h = 0;
+  for (; h + 1 < nh; h += 2) {
+    step(h, afA, wfA, afB, wfB);
+    step(h + 1, afB, wfB, afA, wfA);
+  }
+  if (h < nh) step(h, afA, wfA, afB, wfB);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // all waves done with the ring before the epilogue reuses the LDS
+  const MxExt mx = {};
+  gemm_epilogue<W4_THREADS, W4_FN, W4_FM, W4_WN, W4_WM, false>(d, mx, acc, smem, m0, n0, wr, wc, lane, tid);
 }
 
 }  // namespace
@@ -768,15 +889,19 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_w4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr_set = true;
   }
   const char* e = getenv("VP_GEMM_VARIANT");  // A/B switch for benchmarking main-loop variants
-  int variant = (e != nullptr && e[0] >= '1' && e[0] <= '5') ? e[0] - '0' : 5;
-  if (variant == 5 && ((d->K % BK) != 0 || (int64_t)d->M * d->lda * 2 >= (int64_t)1 << 31 ||
-                       (int64_t)d->n_seg * d->K * 2 >= (int64_t)1 << 31))
+  int variant = (e != nullptr && e[0] >= '1' && e[0] <= '6') ? e[0] - '0' : 5;
+  const bool off32 = (int64_t)d->M * d->lda * 2 < ((int64_t)1 << 31) && (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
+  if (variant == 5 && ((d->K % BK) != 0 || !off32))
     variant = 1;  // the quadrant pipeline needs whole K-tiles and 32-bit source offsets
+  if (variant == 6 && ((d->K % HK) != 0 || !off32 || (d->n_seg % 16) != 0)) variant = 1;
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
-  if (variant == 5)
+  if (variant == 6)
+    hipLaunchKernelGGL(gemm_w4_kernel, dim3(tiles), dim3(W4_THREADS), LDS_BYTES, (hipStream_t)stream, *d);
+  else if (variant == 5)
     hipLaunchKernelGGL(gemm_bf16_kernel<5>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
   else if (variant == 4)
     hipLaunchKernelGGL(gemm_bf16_kernel<4>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
