@@ -201,7 +201,7 @@ def main():
             out8 = fwd()
             fp8_drift = float((out8 - ref16).norm() / ref16.norm())
             del ref16, out8, lmi
-        log(f"[bench] config 5: fp8 attention+FFN noise_pred vs bf16 rel-L2 {fp8_drift:.3e}")
+        log(f"[bench] config 5: fp8 QKV+attention+FFN noise_pred vs bf16 rel-L2 {fp8_drift:.3e}")
     log(f"[bench] setup {time.time() - t_setup:.1f}s; rank {rank}/{world}")
 
     def one(i):
@@ -242,7 +242,7 @@ def main():
     traffic, traffic_src = profiled_traffic() if args.config == 2 else (None, None)  # PMC file is per config
     total_fl, ffn_fl = step_flops(split=True)
     if args.config == 5:  # time the step would take at the dense peaks of the dtypes its MFMAs use
-        f8_fl = ffn_fl + (L + LB) * attn_flops_per_launch()  # one attention launch per block
+        f8_fl = ffn_fl + (L + LB) * (attn_flops_per_launch() + B * 6 * NTOK * D * D)  # + attention, QKV per block
         t_ideal = (total_fl - f8_fl) / (PEAK_BF16_TFLOPS * 1e12) + f8_fl / (PEAK_FP8_TFLOPS * 1e12)
     else:
         t_ideal = total_fl / (PEAK_BF16_TFLOPS * 1e12)
@@ -258,13 +258,14 @@ def main():
             "metric": METRIC, "value": steps_per_s, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if args.config == 2 else "bf16 + fp8 (e4m3, block-scaled MFMA) attention + FeedForward",
+            "dtype": "bf16" if args.config == 2 else "bf16 + fp8 (e4m3, block-scaled MFMA) QKV, attention, FeedForward",
             "data": f"synthetic latents/prompt embeds of the 49f {HL * 8}x{WL * 8} shape; random-init "
                     "CogVideoX-5b-I2V (42 layers) + 2-layer branch weights (no checkpoints offline)",
             "config": {"workload": (f"BASELINE config {args.config}: CogVideoX-5b-I2V + 2-layer branch, 49f "
                                     f"{HL * 8}x{WL * 8} (latent 13x{HL}x{WL}), CFG batch 2, {T}+{NV}={NTOK} tokens, "
                                     "1 denoising step = branch + transformer + CFG/DPM/replace-gt"
-                                    + (", attention + FeedForward in fp8" if args.config == 5 else "")),
+                                    + (", QKV projection + attention + FeedForward in fp8" if args.config == 5
+                                       else "")),
                        "clips_per_gpu": 1, "cfg_batch": B,
                        "tokens": NTOK, "layers": L, "branch_layers": LB,
                        "parallelism": f"dp{world} (independent clips, weights broadcast over RCCL)"},

@@ -369,8 +369,8 @@ def test_full_width_block_fp8_ffn_tolerance():
 
 def test_full_width_block_fp8_attention_and_ffn_tolerance():
     """BASELINE config 5 ("attn + FFN in fp8") on the 5B-width block against the reference fp32 block: the fp8
-    attention (e4m3 Q/K with static LN-bounded factors, V^T with per-(d, 32 keys) scales, P in e4m3) plus the MX-FP8
-    FeedForward.  Re-stated tolerance: at most 6x the reference's own bf16 drift from fp32, plus 2e-2."""
+    attention (e4m3 Q/K with static LN-bounded factors, V^T with per-(d, 32 keys) scales, P in e4m3), the MX-FP8
+    FeedForward, then the MX-FP8 QKV projection too.  Re-stated tolerance: at most 6x the reference's own bf16 drift from fp32, plus 2e-2."""
     from videopainter_amd import device_scope
     from videopainter_amd.transformer import CogVideoXBlock
     from oracle import cogvideox_oracle as O
@@ -388,6 +388,9 @@ def test_full_width_block_fp8_attention_and_ffn_tolerance():
     ha, ea = run()
     blk.enable_fp8_ffn()
     h8, e8 = run()
+    blk.enable_fp8_qkv()
+    hq, eq = run()
+    flatq = torch.cat([eq, hq], dim=1).reshape(-1).float().cpu()
     flat16 = torch.cat([e16, h16], dim=1).reshape(-1).float().cpu()
     flata = torch.cat([ea, ha], dim=1).reshape(-1).float().cpu()
     flat8 = torch.cat([e8, h8], dim=1).reshape(-1).float().cpu()
@@ -398,8 +401,11 @@ def test_full_width_block_fp8_attention_and_ffn_tolerance():
     r8, ra, ro = rel(flat8[::97], g["slice"]), rel(flata[::97], g["slice"]), rel(oflat[::97], g["slice"])
     print(f"fp8 attn+FFN block vs fp32: {r8:.3e}; fp8 attn only {ra:.3e}; reference bf16 {ro:.3e}; "
           f"vs bf16 HIP: attn {rel(flata, flat16):.3e}, attn+FFN {rel(flat8, flat16):.3e}")
+    rq = rel(flatq[::97], g["slice"])
+    print(f"+ fp8 QKV projection: vs fp32 {rq:.3e}, vs bf16 HIP {rel(flatq, flat16):.3e}")
     assert r8 <= 6 * ro + 2e-2, (r8, ra, ro)
-    assert rel(flat8, flat16) < 5e-2
+    assert rq <= 6 * ro + 2e-2, (rq, ro)
+    assert rel(flat8, flat16) < 5e-2 and rel(flatq, flat16) < 5e-2
 
 
 @torch.no_grad()

@@ -98,11 +98,12 @@ class CogVideoXAttnProcessor2_0:
     """HIP restatement of `CogVideoXAttnProcessor2_0.__call__` (attention_processor.py:2107-2209)."""
 
     def attend(self, attn, x: torch.Tensor, text_len: int, image_rotary_emb=None, prev_hidden_states=None,
-               prev_clip_weight=None, resample_mask=None, prev_resample_mask=None) -> torch.Tensor:
+               prev_clip_weight=None, resample_mask=None, prev_resample_mask=None,
+               qkv: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, Ntok, D = x.shape
         H = attn.heads
         rope = _rope_dev(image_rotary_emb, x.device)
-        qkv = _qkv(attn, x)
+        qkv = _qkv(attn, x) if qkv is None else qkv  # (the block may hand over an fp8 projection)
         q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
         eps_q, eps_k = attn.norm_q.eps, attn.norm_k.eps
         fp8 = getattr(attn, "fp8_qk_exp", None)
@@ -172,11 +173,12 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
     second K/V segment."""
 
     def attend(self, attn, x: torch.Tensor, text_len: int, image_rotary_emb=None, prev_hidden_states=None,
-               prev_clip_weight=None, resample_mask=None, prev_resample_mask=None) -> torch.Tensor:
+               prev_clip_weight=None, resample_mask=None, prev_resample_mask=None,
+               qkv: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, Ntok, D = x.shape
         H = attn.heads
         rope = _rope_dev(image_rotary_emb, x.device)
-        qkv = _qkv(attn, x)
+        qkv = _qkv(attn, x) if qkv is None else qkv  # (the block may hand over an fp8 projection)
         q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
         k2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
         v2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)

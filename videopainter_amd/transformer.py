@@ -206,6 +206,7 @@ class CogVideoXBlock(nn.Module):
         self.ff = FeedForward(dim, inner_dim=ff_inner_dim, bias=ff_bias, final_dropout=final_dropout)
         self.dim = dim
         self.ff_mx = None  # (W1, W2) as MX-FP8 when the fp8 FeedForward is enabled (BASELINE config 5)
+        self.qkv_mx = None  # (Wq, Wk, Wv) as MX-FP8 when the fp8 QKV projection is enabled
 
     def enable_fp8_ffn(self, enabled: bool = True) -> None:
         """Run the FeedForward on the block-scaled fp8 MFMA: both weights quantised once to MX-FP8 (e4m3 + one
@@ -218,6 +219,18 @@ class CogVideoXBlock(nn.Module):
         if w1.shape[0] % 256 or w2.shape[0] % 256 or w1.shape[1] % 128 or w2.shape[1] % 128:
             raise ValueError(f"fp8 FeedForward needs widths that are multiples of 256, got {tuple(w1.shape)}")
         self.ff_mx = (K.mx_quantize(w1), K.mx_quantize(w2))
+
+    def enable_fp8_qkv(self, enabled: bool = True) -> None:
+        """Fused QKV projection on the block-scaled fp8 MFMA: the three weights quantised once to MX-FP8, the norm1
+        AdaLN writing MX-FP8 directly, bf16 q/k/v out (the prev-clip K/V projection stays bf16)."""
+        if not enabled:
+            self.qkv_mx = None
+            return
+        a = self.attn1
+        ws = (a.to_q.weight, a.to_k.weight, a.to_v.weight)
+        if any(w.shape[0] % 256 or w.shape[1] % 128 for w in ws):
+            raise ValueError("fp8 QKV needs widths that are multiples of 256")
+        self.qkv_mx = tuple(K.mx_quantize(w) for w in ws)
 
     def enable_fp8_attention(self, enabled: bool = True) -> None:
         """Run self-attention on the block-scaled fp8 MFMA (vp_attention_fwd_fp8): Q and K leave the qk-norm + RoPE
@@ -243,14 +256,26 @@ class CogVideoXBlock(nn.Module):
         if not isinstance(processor, CogVideoXAttnProcessor2_0):
             raise ValueError(f"Unsupported processor type: {type(processor)}")
         mod1 = self.norm1.modulation(temb)
-        xn = K.adaln_modulate(x, self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len, self.norm1.norm.eps)
+        qkv = None
+        if self.qkv_mx is not None:
+            a = self.attn1
+            xq = K.adaln_modulate_mx(x, self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len,
+                                     self.norm1.norm.eps)
+            qkv = torch.empty(B, Ntok, 3 * D, device=x.device, dtype=x.dtype)
+            K.gemm_mx(xq, list(self.qkv_mx), [a.to_q.bias, a.to_k.bias, a.to_v.bias], qkv.view(B * Ntok, 3 * D))
+            del xq
+            xn = None
+        else:
+            xn = K.adaln_modulate(x, self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len,
+                                  self.norm1.norm.eps)
         pn = None
         if prev_joint is not None:
             # the block normalises the previous window's states with its own norm1 (reference :141-146)
             pn = K.adaln_modulate(_bf(prev_joint), self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len,
                                   self.norm1.norm.eps)
-        o = processor.attend(self.attn1, xn, text_len, rope, pn, prev_clip_weight, resample_mask,
-                             prev_resample_mask)
+        o = processor.attend(self.attn1, xn if xn is not None else x, text_len, rope, pn, prev_clip_weight,
+                             resample_mask, prev_resample_mask, qkv=qkv)
+        del qkv
         del xn, pn
         x_mid = torch.empty_like(x)
         to_out = self.attn1.to_out[0]
@@ -357,9 +382,16 @@ class CogVideoXTransformer3DModel(ModelMixin):
             blk.enable_fp8_attention(enabled)
         return self
 
-    def enable_fp8(self, ffn: bool = True, attention: bool = True):
-        """BASELINE config 5: "attn + FFN in fp8"."""
+    def enable_fp8_qkv(self, enabled: bool = True):
+        """fp8 fused QKV projection in every block (see CogVideoXBlock.enable_fp8_qkv)."""
+        for blk in self.transformer_blocks:
+            blk.enable_fp8_qkv(enabled)
+        return self
+
+    def enable_fp8(self, ffn: bool = True, attention: bool = True, qkv: bool = True):
+        """BASELINE config 5: "attn + FFN in fp8" (the QKV projection, the attention products, the FeedForward)."""
         self.enable_fp8_ffn(ffn)
+        self.enable_fp8_qkv(qkv)
         return self.enable_fp8_attention(attention)
 
     def _patch_channels(self):
