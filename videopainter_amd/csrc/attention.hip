@@ -235,12 +235,11 @@ VP_DEV void qk_half(const char* Kl, int kh, const bf16x8 (&qf)[4], f32x16& s, in
 }
 
 VP_DEV void mask_half(f32x16& s, int lim, int kh, int hl) {
-  // key = kh*32 + (i&3) + 8*(i>>2) + 4*hl >= lim, with the lane part moved to the limit so every compare is
-  // against an inline constant (otherwise the compiler hoists 16 per-lane key indices out of the tile loop)
-  const int l2 = lim - kh * 32 - 4 * hl;
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if ((i & 3) + 8 * (i >> 2) >= l2) s[i] = -INFINITY;
+  for (int i = 0; i < 16; ++i) {
+    const int key = kh * 32 + (i & 3) + 8 * (i >> 2) + 4 * hl;
+    if (key >= lim) s[i] = -INFINITY;
+  }
 }
 
 VP_DEV void softmax_half(f32x16& s, float& m_run, float& l_run, f32x16 (&o)[2], bf16x8 (&pf)[2], float c) {
@@ -881,7 +880,7 @@ VP_DEV float f8_exp_pack(const f32x16 (&s)[2], i32x8& pf) {
 
 // LAZY (lazy-max, as softmax_half_lazy): P stored as p * 2^6, the max path only when a lane's 32 stored values
 // sum past 448; otherwise P = p * 2^7 with the max path every tile and rescale threshold 1.5 (P <= 2^8.5 < 448).
-template <int NW, int OCC, bool LAZY = false>
+template <int NW, int OCC, bool LAZY = false, int SUB = 1>
 __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_desc dd) {
   static_assert(NW == 8, "the DMA split assumes 8 waves");
   constexpr int OFF = LAZY ? 6 : 7;              // P is stored as p * 2^OFF
@@ -920,15 +919,22 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
   const char* vtbase = (const char*)d.V + (int64_t)bh * 64 * dd.npad;
   const char* vsbase = (const char*)dd.vs + (int64_t)bh * ntiles * 128;
   const int ksn = (int)d.k_sn;
+  // ring slot ti holds SUB consecutive 64-key tiles (one barrier per SUB tiles)
+  const int nsup = (ntiles + SUB - 1) / SUB;
   auto issue = [&](int ti) {
-    char* slot = smem + (ti & 1) * F8_STAGE;
-    if (wave < 4) {
-      const int r = min(ti * 64 + prow, d.Nk - 1);  // rows past the end re-read the last key (masked later)
-      glds16(kbase, r * ksn + pch * 16, slot + wave * 1024);
-    } else {
-      glds16(vtbase + ti * 64, prow * dd.npad + pch * 16, slot + F8_TILE + (wave - 4) * 1024);
+#pragma unroll
+    for (int sb = 0; sb < SUB; ++sb) {
+      const int kt = ti * SUB + sb;
+      if (SUB > 1 && kt >= ntiles) break;  // wave-uniform
+      char* slot = smem + ((ti & 1) * SUB + sb) * F8_STAGE;
+      if (wave < 4) {
+        const int r = min(kt * 64 + prow, d.Nk - 1);  // rows past the end re-read the last key (masked later)
+        glds16(kbase, r * ksn + pch * 16, slot + wave * 1024);
+      } else {
+        glds16(vtbase + kt * 64, prow * dd.npad + pch * 16, slot + F8_TILE + (wave - 4) * 1024);
+      }
+      if (wave == 0 && lane < 8) glds16(vsbase + kt * 128, lane * 16, slot + 2 * F8_TILE);
     }
-    if (wave == 0 && lane < 8) glds16(vsbase + ti * 128, lane * 16, slot + 2 * F8_TILE);
   };
 
   // LDS read offsets (within a stage) of this lane's two 16-byte chunks of row r: r*64 + ((c ^ swz8(r)) << 4)
@@ -947,12 +953,16 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
   issue(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  for (int ti = 0; ti < ntiles; ++ti) {
-    if (ti + 1 < ntiles) issue(ti + 1);
-    const char* st = smem + (ti & 1) * F8_STAGE;
+  for (int ti = 0; ti < nsup; ++ti) {
+    if (ti + 1 < nsup) issue(ti + 1);
+#pragma unroll
+   for (int sb = 0; sb < SUB; ++sb) {
+    const int kt = ti * SUB + sb;
+    if (SUB > 1 && kt >= ntiles) break;
+    const char* st = smem + ((ti & 1) * SUB + sb) * F8_STAGE;
     if (active) {
       f32x16 s[2];
-      const int lim = d.Nk - ti * 64;
+      const int lim = d.Nk - kt * 64;
       auto scores = [&]() {
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
@@ -1040,6 +1050,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
           o[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[1], 0, 0, 1, vsw, 0, 127);
       }
     }
+   }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
@@ -1151,24 +1162,28 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
     return VP_ERR_ARG;
   if ((int64_t)d.Nk * d.k_sn > 0x7fffffff || (int64_t)64 * dd->npad > 0x7fffffff) return VP_ERR_ARG;
   constexpr int NW = 8;
-  // variants (A/B switch VP_ATTN8_VARIANT): 1 = max path every tile (default), 2 = lazy max (needs 159 VGPRs: spills at
-  // 128; 0.21 PF/s), 3 / 4 = 1 / 2 at 3 waves/SIMD (1.01 / 0.69 PF/s against 1.43)
+  // variants (A/B switch VP_ATTN8_VARIANT): 1 = max path every tile, 2 = lazy max (needs 159 VGPRs: spills at
+  // 128; 0.21 PF/s), 3 / 4 = 1 / 2 at 3 waves/SIMD (1.01 / 0.69 PF/s against 1.43), 5 = 1 with 128 keys per barrier
+  // (default, 1.46)
   static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, false>, (const void*)attn_fwd_fp8<NW, 4, true>,
-                                    (const void*)attn_fwd_fp8<NW, 3, false>, (const void*)attn_fwd_fp8<NW, 3, true>};
+                                    (const void*)attn_fwd_fp8<NW, 3, false>, (const void*)attn_fwd_fp8<NW, 3, true>,
+                                    (const void*)attn_fwd_fp8<NW, 4, false, 2>};
+  static const int subs[] = {1, 1, 1, 1, 2};
   static bool attr_set = false;
   if (!attr_set) {
     attr_set = true;
-    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * F8_STAGE);
+    for (int i = 0; i < 5; ++i)
+      (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, 2 * subs[i] * F8_STAGE);
   }
   const char* e = getenv("VP_ATTN8_VARIANT");
   int variant = e != nullptr ? atoi(e) : 0;
-  if (variant < 1 || variant > 4) variant = 1;
+  if (variant < 1 || variant > 5) variant = 5;
   const int nqb = (d.Nq + NW * 32 - 1) / (NW * 32);
   const int64_t grid = (int64_t)d.B * d.H * nqb;
   if (grid > 0x7fffffff) return VP_ERR_ARG;
   void* args[] = {(void*)dd};
-  const hipError_t le = hipLaunchKernel(fns[variant - 1], dim3((unsigned)grid), dim3(NW * 64), args, 2 * F8_STAGE,
-                                        (hipStream_t)stream);
+  const hipError_t le = hipLaunchKernel(fns[variant - 1], dim3((unsigned)grid), dim3(NW * 64), args,
+                                        2 * subs[variant - 1] * F8_STAGE, (hipStream_t)stream);
   if (le != hipSuccess) return (int)le;
   VP_CHECK_LAUNCH();
   return VP_OK;
