@@ -1,0 +1,86 @@
+"""Load-time LoRA folding (videopainter_amd/lora.py), CPU only.
+
+The reference applies the VideoPainterID adapter unfused through PEFT (not installed here, so its forward cannot be
+run: parity against PEFT itself is unpinned).  What is checked: the fold equals the LoRA forward it replaces,
+W x + s B (A x) with s = lora_scale (the CogVideoX loader's alpha = r) or alpha / r * lora_scale for kohya files;
+keys in the pipeline-level format ("transformer." prefix, PEFT "lora_A"/"lora_B"); unknown modules are rejected;
+fold + unfold restores the weights up to bf16 rounding."""
+import os
+
+import pytest
+import torch
+from safetensors.torch import save_file
+
+from tests.golden.cases import TINY_CFG
+
+
+def _model():
+    from videopainter_amd import CogVideoXTransformer3DModel
+    m = CogVideoXTransformer3DModel(**TINY_CFG)
+    g = torch.Generator().manual_seed(0)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_((torch.randn(p.shape, generator=g) * 0.05).to(p.dtype))
+    return m
+
+
+def _adapter(m, r=8, kohya_alpha=None, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for i in range(len(m.transformer_blocks)):
+        for t in ("to_q", "to_k", "to_v", "to_out.0"):
+            lin = dict(m.named_modules())[f"transformer_blocks.{i}.attn1.{t}"]
+            out_f, in_f = lin.weight.shape
+            A = torch.randn(r, in_f, generator=g) * 0.1
+            B = torch.randn(out_f, r, generator=g) * 0.1
+            base = f"transformer.transformer_blocks.{i}.attn1.{t}"
+            if kohya_alpha is None:
+                sd[f"{base}.lora_A.weight"], sd[f"{base}.lora_B.weight"] = A, B
+            else:
+                sd[f"{base}.lora_down.weight"], sd[f"{base}.lora_up.weight"] = A, B
+                sd[f"{base}.alpha"] = torch.tensor(float(kohya_alpha))
+    return sd
+
+
+@pytest.mark.parametrize("fmt", ["peft", "kohya"])
+def test_fold_matches_lora_forward(tmp_path, fmt):
+    from videopainter_amd.lora import load_lora_into_transformer
+    m = _model()
+    r, alpha, scale = 8, (4.0 if fmt == "kohya" else None), 0.7
+    sd = _adapter(m, r, alpha)
+    save_file(sd, os.path.join(tmp_path, "pytorch_lora_weights.safetensors"))
+    lin = dict(m.named_modules())["transformer_blocks.1.attn1.to_k"]
+    W0 = lin.weight.detach().float().clone()
+    x = torch.randn(5, W0.shape[1])
+    base = "transformer.transformer_blocks.1.attn1.to_k"
+    A = sd[f"{base}.lora_A.weight" if fmt == "peft" else f"{base}.lora_down.weight"]
+    B = sd[f"{base}.lora_B.weight" if fmt == "peft" else f"{base}.lora_up.weight"]
+    s = scale * (alpha / r if alpha is not None else 1.0)
+    want = x @ W0.T + s * (x @ A.T) @ B.T      # the unfused LoRA forward (PEFT: base + scaling * B(A x))
+    n = load_lora_into_transformer(m, str(tmp_path), lora_scale=scale)
+    assert n == 4 * len(m.transformer_blocks)
+    got = x @ lin.weight.float().T
+    assert torch.allclose(got, want, rtol=0, atol=2e-2 * float(want.abs().max()))  # bf16 weight rounding
+    # every other parameter is untouched
+    m2 = _model()
+    for (k, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        if not any(t in k for t in ("to_q", "to_k", "to_v", "to_out")) or k.endswith("bias"):
+            assert torch.equal(a, b), k
+
+
+def test_fold_unfold_roundtrip_and_rejects_unknown_modules():
+    from videopainter_amd.lora import fold_lora_, unfold_lora_
+    m = _model()
+    W0 = {k: v.float().clone() for k, v in m.state_dict().items()}
+    sd = _adapter(m)
+    fold_lora_(m, sd)
+    unfold_lora_(m, sd)
+    for k, v in m.state_dict().items():
+        assert torch.allclose(v.float(), W0[k], atol=2e-3), k
+    bad = {"transformer.nope.lora_A.weight": torch.zeros(2, 4), "transformer.nope.lora_B.weight": torch.zeros(4, 2)}
+    with pytest.raises(KeyError):
+        fold_lora_(m, bad)
+    assert fold_lora_(m, bad, strict=False) == 0
+    half = {"transformer.transformer_blocks.0.attn1.to_q.lora_A.weight": torch.zeros(2, 128)}
+    with pytest.raises(ValueError):
+        fold_lora_(m, half)

@@ -1,0 +1,103 @@
+"""VideoPainterID LoRA adapters, folded into the base weights at load time.
+
+The reference loads the ID-resample adapter unfused through PEFT (`pipe.load_lora_weights(path,
+weight_name="pytorch_lora_weights.safetensors", adapter_name=..., target_modules=["transformer"])`,
+infer/inpaint.py:310-315; `CogVideoXLoraLoaderMixin.load_lora_into_transformer`,
+diffusers/loaders/lora_pipeline.py:2632-2705).  Its forward is `W x + s * B (A x)` on to_q / to_k / to_v /
+to_out.0 (the training script's `LoraConfig(target_modules=["to_q", "to_k", "to_v", "to_out.0"])`,
+train/train_cogvideox_inpainting_i2v_video_resample.py:1520-1525) with
+
+    s = lora_alpha / r * lora_scale
+
+where the loader passes no network alphas, so `get_peft_kwargs` sets lora_alpha = r (utils/peft_utils.py:153) —
+s = lora_scale (attention_kwargs["scale"], default 1.0) whatever alpha the adapter was trained with.  Folding that
+product into W once (`W + s B A`, accumulated in fp32, rounded to the weight dtype) gives every kernel of the HIP
+path the adapted weights with no per-step cost.  Kohya-style files (`lora_down` / `lora_up` + `.alpha`) are
+accepted too; their alpha is honoured (alpha / r), as the generic diffusers conversion does.
+
+Parity: PEFT is not installed here, so the reference's unfused LoRA forward cannot run; `tests/test_lora_cpu.py`
+checks the fold against the LoRA formula on the module level and the round trip (fold, unfold) — "parity unpinned"
+against PEFT itself.
+"""
+from __future__ import annotations
+
+import os
+import re
+from typing import Dict, Optional
+
+import torch
+
+TARGETS = ("to_q", "to_k", "to_v", "to_out.0")
+_PEFT = re.compile(r"^(?:(?P<prefix>transformer)\.)?(?P<mod>.+)\.lora_(?P<ab>[AB])(?:\.[^.]+)?\.weight$")
+_KOHYA = re.compile(r"^(?:(?P<prefix>transformer)\.)?(?P<mod>.+)\.lora_(?P<ab>down|up)\.weight$")
+
+
+def load_lora_state_dict(path: str, weight_name: str = "pytorch_lora_weights.safetensors") -> Dict[str, torch.Tensor]:
+    """The adapter file (safetensors only: nothing in it is executed)."""
+    from safetensors.torch import load_file
+    f = os.path.join(path, weight_name) if os.path.isdir(path) else path
+    return load_file(f)
+
+
+def lora_pairs(sd: Dict[str, torch.Tensor]) -> Dict[str, dict]:
+    """{module path: {"A": [r, in], "B": [out, r], "alpha": float or None}} from a PEFT or kohya state dict."""
+    pairs: Dict[str, dict] = {}
+    for k, v in sd.items():
+        m = _PEFT.match(k) or _KOHYA.match(k)
+        if m is None:
+            if k.endswith(".alpha"):
+                mod = k[:-len(".alpha")]
+                mod = mod[len("transformer."):] if mod.startswith("transformer.") else mod
+                pairs.setdefault(mod, {})["alpha"] = float(v)
+            continue
+        ab = {"A": "A", "down": "A", "B": "B", "up": "B"}[m.group("ab")]
+        pairs.setdefault(m.group("mod"), {})[ab] = v
+    for mod, p in pairs.items():
+        if "A" not in p or "B" not in p:
+            raise ValueError(f"LoRA module {mod} has only {sorted(k for k in p if k in 'AB')}")
+        if p["B"].shape[1] != p["A"].shape[0]:
+            raise ValueError(f"LoRA module {mod}: B {tuple(p['B'].shape)} and A {tuple(p['A'].shape)} disagree")
+    return pairs
+
+
+@torch.no_grad()
+def fold_lora_(model: torch.nn.Module, sd: Dict[str, torch.Tensor], lora_scale: float = 1.0,
+               strict: bool = True) -> int:
+    """W += s * B @ A for every adapted Linear of `model` (in place); returns the number of folded layers.
+    s = lora_scale for PEFT-format adapters (the reference loader's alpha = r), alpha / r * lora_scale for kohya
+    files that carry an alpha.  Fold BEFORE `enable_fp8*` (those quantise the weights they find)."""
+    mods = dict(model.named_modules())
+    n = 0
+    for mod, p in lora_pairs(sd).items():
+        lin = mods.get(mod)
+        if lin is None or not hasattr(lin, "weight"):
+            if strict:
+                raise KeyError(f"LoRA targets {mod}, which the model does not have")
+            continue
+        A, B = p["A"], p["B"]
+        r = A.shape[0]
+        s = lora_scale * (p["alpha"] / r if p.get("alpha") is not None else 1.0)
+        W = lin.weight
+        if tuple(W.shape) != (B.shape[0], A.shape[1]):
+            raise ValueError(f"LoRA {mod}: B@A is {(B.shape[0], A.shape[1])}, weight is {tuple(W.shape)}")
+        delta = B.to(W.device, torch.float32) @ A.to(W.device, torch.float32)
+        W.copy_((W.float() + s * delta).to(W.dtype))
+        n += 1
+    return n
+
+
+def load_lora_into_transformer(transformer: torch.nn.Module, path: str,
+                               weight_name: str = "pytorch_lora_weights.safetensors", lora_scale: float = 1.0,
+                               strict: bool = True) -> int:
+    """What `pipe.load_lora_weights(path, weight_name=...)` + `attention_kwargs={"scale": lora_scale}` do to the
+    transformer's forward, as a one-time weight fold."""
+    sd = load_lora_state_dict(path, weight_name)
+    keys = [k for k in sd if k.startswith("transformer.")]
+    if keys:  # the pipeline-level file: only the transformer's entries (lora_pipeline.py:2653-2656)
+        sd = {k: v for k, v in sd.items() if k.startswith("transformer.")}
+    return fold_lora_(transformer, sd, lora_scale, strict)
+
+
+def unfold_lora_(model: torch.nn.Module, sd: Dict[str, torch.Tensor], lora_scale: float = 1.0) -> int:
+    """Remove a folded adapter (W -= s B A; exact only up to the weight dtype's rounding)."""
+    return fold_lora_(model, sd, -lora_scale)

@@ -368,6 +368,14 @@ class CogVideoXTransformer3DModel(ModelMixin):
         self.norm_final = LayerNorm(inner_dim, norm_eps, norm_elementwise_affine)
         self._build_head(inner_dim, time_embed_dim, norm_elementwise_affine, norm_eps, patch_size, out_channels)
 
+    def load_lora_weights(self, path: str, weight_name: str = "pytorch_lora_weights.safetensors",
+                          adapter_name: Optional[str] = None, lora_scale: float = 1.0, **_):
+        """The VideoPainterID adapter (PEFT safetensors) folded into to_q/to_k/to_v/to_out.0 at load time
+        (videopainter_amd/lora.py; the reference applies it unfused through PEFT, infer/inpaint.py:310-315)."""
+        from .lora import load_lora_into_transformer
+        load_lora_into_transformer(self, path, weight_name, lora_scale)
+        return self
+
     def enable_fp8_ffn(self, enabled: bool = True):
         """fp8 FeedForward in every block (BASELINE config 5; see CogVideoXBlock.enable_fp8_ffn).  Call after the
         weights are loaded; re-call after changing them."""
