@@ -18,7 +18,7 @@ def _lib():
     _native.lib()
 
 
-@pytest.fixture(params=["5", "6", "1"], ids=["gemm_v5", "gemm_v6", "gemm_v1"])
+@pytest.fixture(params=["5", "6", "7", "1"], ids=["gemm_v5", "gemm_v6", "gemm_v7", "gemm_v1"])
 def gemm_variant(request, monkeypatch):
     monkeypatch.setenv("VP_GEMM_VARIANT", request.param)
     return request.param

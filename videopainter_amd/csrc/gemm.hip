@@ -294,7 +294,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (VAR == 5) {
+  if constexpr (VAR == 5 || VAR == 7) {
     // Quadrant-phase pipeline.  Each wave's 128x64 C block is split into 4 quadrants (64 rows x 32 cols); a K-tile
     // (BK = 64) runs as 4 phases of 16 MFMAs, in the quadrant order (A0,B0) (A0,B1) (A1,B1) (A1,B0) so each phase
     // needs ONE new operand subtile, which is read from LDS into registers during the previous phase.  The LDS
@@ -539,18 +539,22 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
       slot(s0);
       readB(b1, P{}, O{});
       mma(a0, b0, Z{}, Z{}, sc.a0, sc.w);
+      if constexpr (VAR == 7) __builtin_amdgcn_s_barrier();  // phase-aligned waves (A/B)
       slot(s0 + 1);
       readA(a1, P{}, O{});
       mma(a0, b1, Z{}, O{}, sc.a0, sc.w);
+      if constexpr (VAR == 7) __builtin_amdgcn_s_barrier();  // phase-aligned waves (A/B)
       slot(s0 + 2);
       if (more) {
         readA(a0, NP{}, Z{});
         readS(scn, k + 1);
       }
       mma(a1, b1, O{}, O{}, sc.a1, sc.w);
+      if constexpr (VAR == 7) __builtin_amdgcn_s_barrier();  // phase-aligned waves (A/B)
       slot(s0 + 3);
       if (more) readB(b1, NP{}, Z{});  // b1's registers carry the next tile's quadrant-col 0
       mma(a1, b0, O{}, Z{}, sc.a1, sc.w);
+      if constexpr (VAR == 7) __builtin_amdgcn_s_barrier();  // phase-aligned waves (A/B)
     };
     using T_ = std::integral_constant<bool, true>;
     using F_ = std::integral_constant<bool, false>;
@@ -890,16 +894,20 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_w4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<7>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
     attr_set = true;
   }
   const char* e = getenv("VP_GEMM_VARIANT");  // A/B switch for benchmarking main-loop variants
-  int variant = (e != nullptr && e[0] >= '1' && e[0] <= '6') ? e[0] - '0' : 5;
+  int variant = (e != nullptr && e[0] >= '1' && e[0] <= '7') ? e[0] - '0' : 5;
   const bool off32 = (int64_t)d->M * d->lda * 2 < ((int64_t)1 << 31) && (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
-  if (variant == 5 && ((d->K % BK) != 0 || !off32))
+  if ((variant == 5 || variant == 7) && ((d->K % BK) != 0 || !off32))
     variant = 1;  // the quadrant pipeline needs whole K-tiles and 32-bit source offsets
   if (variant == 6 && ((d->K % HK) != 0 || !off32 || (d->n_seg % 16) != 0)) variant = 1;
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
-  if (variant == 6)
+  if (variant == 7)
+    hipLaunchKernelGGL(gemm_bf16_kernel<7>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
+  else if (variant == 6)
     hipLaunchKernelGGL(gemm_w4_kernel, dim3(tiles), dim3(W4_THREADS), LDS_BYTES, (hipStream_t)stream, *d);
   else if (variant == 5)
     hipLaunchKernelGGL(gemm_bf16_kernel<5>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
