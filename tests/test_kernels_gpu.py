@@ -71,6 +71,23 @@ def test_gemm_bias_random(M, Nn, Kk, gemm_variant):
     assert rel(out, ref) < 4e-3
 
 
+def test_gemm_large_row_stride():
+    """A whose rows span more than 2^31 bytes (M * lda * 2: FF2's input at config 5 is 94052 x 12288): the default
+    pipeline addresses A from a 64-bit tile base, so it must stay correct (and not fall back)."""
+    from videopainter_amd import kernels as K
+    M, Kk, Nn, lda = 33000, 128, 256, 33024
+    big = torch.empty(M, lda, device=dev, dtype=torch.bfloat16)
+    a = bf(rnd(M, Kk, seed=11))
+    big[:, :Kk] = a.to(dev)
+    w, b = bf(rnd(Nn, Kk, std=Kk ** -0.5, seed=12)), bf(rnd(Nn, std=0.1, seed=13))
+    out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    K.gemm(big[:, :Kk], [w.to(dev)], [b.to(dev)], out, lda=lda)
+    del big
+    ref = a.float() @ w.float().T + b.float()
+    assert rel(out, ref) < 4e-3
+    assert rel(out[-300:], ref[-300:]) < 4e-3  # the rows past 2^31 bytes
+
+
 @pytest.mark.parametrize("D,Kk", [(256, 256), (128, 96)])
 def test_gemm_segments_gelu_scale(D, Kk, gemm_variant):
     from videopainter_amd import kernels as K

@@ -336,8 +336,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
           const int r = rb + (lane >> 3);
           const int c = (lane & 7) ^ swz(r);
           if (u < 2) {
-            ubase[u][i] = (const char*)d.A;
-            uoff[u][i] = (min(m0 + r, d.M - 1) * d.lda) * EB + c * 16;
+            // 64-bit tile base + 32-bit in-tile offset (M * lda can pass 2^31 bytes: FF2 at config 5)
+            ubase[u][i] = (const char*)d.A + (int64_t)m0 * d.lda * EB;
+            uoff[u][i] = (min(m0 + r, d.M - 1) - m0) * (int)d.lda * EB + c * 16;
           } else {
             const int sg = __builtin_amdgcn_readfirstlane(min(n0 + rb, d.N - 1) / d.n_seg);
             ubase[u][i] = (const char*)d.W[sg];
@@ -900,9 +901,13 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   }
   const char* e = getenv("VP_GEMM_VARIANT");  // A/B switch for benchmarking main-loop variants
   int variant = (e != nullptr && e[0] >= '1' && e[0] <= '7') ? e[0] - '0' : 5;
-  const bool off32 = (int64_t)d->M * d->lda * 2 < ((int64_t)1 << 31) && (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
-  if ((variant == 5 || variant == 7) && ((d->K % BK) != 0 || !off32))
-    variant = 1;  // the quadrant pipeline needs whole K-tiles and 32-bit source offsets
+  // 32-bit in-tile source offsets: the quadrant pipeline adds them to a 64-bit tile base (A) / segment base (W);
+  // variant 6 still offsets A from the matrix base
+  const bool w32 = (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
+  const bool tile32 = (int64_t)BM * d->lda * 2 < ((int64_t)1 << 31) && w32;
+  const bool off32 = (int64_t)d->M * d->lda * 2 < ((int64_t)1 << 31) && w32;
+  if ((variant == 5 || variant == 7) && ((d->K % BK) != 0 || !tile32))
+    variant = 1;  // the quadrant pipeline needs whole K-tiles
   if (variant == 6 && ((d->K % HK) != 0 || !off32 || (d->n_seg % 16) != 0)) variant = 1;
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
   if (variant == 7)
