@@ -24,7 +24,7 @@ def gemm_variant(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["22", "10", "4", "1", "3", "6", "8", "11", "12", "13", "14", "15", "16", "17", "18", "19", "20", "21", "23"], ids=lambda v: f"attn_v{v}")
+@pytest.fixture(params=["22", "10", "4", "1", "3", "6", "8", "11", "12", "13", "14", "15", "16", "17", "18", "19", "20", "21", "23", "24", "25", "26"], ids=lambda v: f"attn_v{v}")
 def attn_variant(request, monkeypatch):
     monkeypatch.setenv("VP_ATTN_VARIANT", request.param)
     return request.param

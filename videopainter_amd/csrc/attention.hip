@@ -316,7 +316,7 @@ VP_DEV void qk_half_ci(const char* Kl, int kh, const bf16x8 (&qf)[4], const f32x
 }
 
 VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f32x16& negm, f32x16 (&o)[2],
-                            bf16x8 (&pf)[2]) {
+                            bf16x8 (&pf)[2], f32x16* s_next = nullptr) {
   float m2[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -340,6 +340,7 @@ VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f
       o[1][i] *= alpha;
       s[i] -= dm;
       negm[i] = -m_run;
+      if (s_next != nullptr) (*s_next)[i] -= dm;  // a next half already computed against the old -m
     }
     thr = RESCALE_THR;
   }
@@ -623,7 +624,7 @@ VP_DEV void pv_half_x(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)
 // tile t waits (counted vmcnt) for tile t+1 only, then one barrier.  PRIO: the second half of the workgroup's waves
 // runs at s_setprio 1 (the arbitration loser of each SIMD pair, MI355X_MICROARCH.md "Two waves per SIMD" item 4).
 // ------------------------------------------------------------------------------------------------------------
-template <int NW, int OCC, int KB = 64, int RING = 2, bool PRIO = false, bool LAZY = false>
+template <int NW, int OCC, int KB = 64, int RING = 2, bool PRIO = false, bool LAZY = false, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc d) {
   constexpr int QB = NW * 32;
   constexpr int KT = KB * 128;                  // bytes per K (or V) tile
@@ -725,6 +726,27 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
     const char* Kl = slot_of(ti);
     const Seg sg = tile_seg<KB>(d, ti, tiles1, b, h);
     const int lim = sg.n - sg.key0;
+    if constexpr (PIPE) {
+      // software-pipelined halves: the QK^T MFMAs of half kh+1 are issued before the softmax of half kh, so one
+      // wave keeps the matrix pipe busy through its own VALU work (a rescale in half kh shifts the early S too)
+      if (active) {
+        f32x16 sn;
+        qk_half_ci2(Kl, 0, qf, negm, sn, lane);
+        if (lim < KB) mask_half(sn, lim, 0, hl);
+#pragma unroll
+        for (int kh = 0; kh < HALVES; ++kh) {
+          f32x16 sh = sn;
+          if (kh + 1 < HALVES) {
+            qk_half_ci2(Kl, kh + 1, qf, negm, sn, lane);
+            if (lim < KB) mask_half(sn, lim, kh + 1, hl);
+          }
+          bf16x8 pf[2];
+          if (thr == -INFINITY || !softmax_half_lazy(sh, l_run, pf))
+            softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf, kh + 1 < HALVES ? &sn : nullptr);
+          pv_half_x(Kl + KT, kh, pf, o, vo);
+        }
+      }
+    } else
 #pragma unroll
     for (int kh = 0; kh < HALVES; ++kh) {
       if (!active) break;
@@ -1098,6 +1120,9 @@ extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
       {(const void*)attn_fwd_dma<8, 4, 64, 3, false, true>, 8, 6 * KBLK * 128},  // 21: 19 + 3-slot ring
       {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true>, 8, 4 * 128 * 128},  // 22: 19 + 128-key tiles
       {(const void*)attn_fwd_dma<8, 4, 64, 3, true, true>, 8, 6 * KBLK * 128},   // 23: 21 + prio
+      {(const void*)attn_fwd_dma<8, 3, 128, 2, false, true, true>, 8, 4 * 128 * 128},  // 24: 22 + pipelined halves, 3/SIMD
+      {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true, true>, 8, 4 * 128 * 128},  // 25: 24 at 4 waves/SIMD
+      {(const void*)attn_fwd_dma<8, 3, 128, 2, false, true>, 8, 4 * 128 * 128},        // 26: 22 at 3 waves/SIMD
   };
 
   constexpr int NVAR = sizeof(vars) / sizeof(vars[0]);
