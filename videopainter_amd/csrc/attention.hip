@@ -315,8 +315,9 @@ VP_DEV void qk_half_ci(const char* Kl, int kh, const bf16x8 (&qf)[4], const f32x
   s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[3], s, 0, 0, 0);
 }
 
+template <bool NEXT = false>
 VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f32x16& negm, f32x16 (&o)[2],
-                            bf16x8 (&pf)[2], f32x16* s_next = nullptr) {
+                            bf16x8 (&pf)[2], f32x16& s_next) {
   float m2[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -340,7 +341,7 @@ VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f
       o[1][i] *= alpha;
       s[i] -= dm;
       negm[i] = -m_run;
-      if (s_next != nullptr) (*s_next)[i] -= dm;  // a next half already computed against the old -m
+      if constexpr (NEXT) s_next[i] -= dm;  // a next half already computed against the old -m
     }
     thr = RESCALE_THR;
   }
@@ -352,6 +353,11 @@ VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f
     pf[i >> 3][i & 7] = f2bf(p);
   }
   l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+}
+
+VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f32x16& negm, f32x16 (&o)[2],
+                            bf16x8 (&pf)[2]) {
+  softmax_half_ci<false>(s, m_run, thr, l_run, negm, o, pf, s);
 }
 
 // QK^T half with the first MFMA in inline asm so its destination is a fresh tuple (early-clobber) while C = -m
@@ -741,8 +747,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
             if (lim < KB) mask_half(sn, lim, kh + 1, hl);
           }
           bf16x8 pf[2];
-          if (thr == -INFINITY || !softmax_half_lazy(sh, l_run, pf))
-            softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf, kh + 1 < HALVES ? &sn : nullptr);
+          if (thr == -INFINITY || !softmax_half_lazy(sh, l_run, pf)) {
+            if (kh + 1 < HALVES) softmax_half_ci<true>(sh, m_run, thr, l_run, negm, o, pf, sn);
+            else softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf);
+          }
           pv_half_x(Kl + KT, kh, pf, o, vo);
         }
       }
