@@ -441,3 +441,40 @@ def test_fp8_attention_model_modes(env):
         r8, r16 = rel(out8, g[gold]), rel(out16, g[gold])
         print(f"fp8 attention {mode}: vs fp32 {r8:.3e} (bf16 HIP {r16:.3e}); vs bf16 {rel(out8, out16):.3e}")
         assert r8 <= 4 * r16 + 3e-2, (mode, r8, r16)
+
+
+@torch.no_grad()
+def test_lora_folded_model_matches_oracle(env, tmp_path):
+    """A VideoPainterID-style adapter (PEFT keys on to_q/to_k/to_v/to_out.0) folded at load time: the HIP model
+    with the folded weights against the oracle run on the same folded state dict (the reference's unfused PEFT
+    forward cannot run here: parity against PEFT itself is unpinned, tests/test_lora_cpu.py checks the fold)."""
+    from safetensors.torch import save_file
+    from oracle import cogvideox_oracle as O
+    from videopainter_amd import CogVideoXTransformer3DModel, device_scope
+    i, g = env["inp"], env["g"]
+    tsd, _ = tiny_weights()
+    with device_scope(dev):
+        m = CogVideoXTransformer3DModel(**TINY_CFG)
+    m.load_diffusers_state_dict({k: torch.from_numpy(v) for k, v in tsd.items()})
+    gen = torch.Generator().manual_seed(5)
+    sd = {}
+    for b in range(TINY_CFG["num_layers"]):
+        for t in ("to_q", "to_k", "to_v", "to_out.0"):
+            w = tsd[f"transformer_blocks.{b}.attn1.{t}.weight"]
+            sd[f"transformer.transformer_blocks.{b}.attn1.{t}.lora_A.weight"] = torch.randn(16, w.shape[1], generator=gen) * 0.05
+            sd[f"transformer.transformer_blocks.{b}.attn1.{t}.lora_B.weight"] = torch.randn(w.shape[0], 16, generator=gen) * 0.05
+    save_file(sd, os.path.join(tmp_path, "pytorch_lora_weights.safetensors"))
+    m.load_lora_weights(str(tmp_path), lora_scale=0.5)
+    folded = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    assert not torch.equal(folded["transformer_blocks.0.attn1.to_q.weight"],
+                           torch.from_numpy(tsd["transformer_blocks.0.attn1.to_q.weight"]).to(torch.bfloat16))
+    bs = [g["branch.0"], g["branch.1"]]
+    out = m(hidden_states=_d(i["hidden"]), encoder_hidden_states=_d(i["enc"]), timestep=i["timestep"].to(dev),
+            image_rotary_emb=i["rope"], branch_block_samples=[_d(b) for b in bs], branch_block_masks=_d(i["mask"]),
+            return_dict=False)[0]
+    f32 = {k: v.float() for k, v in folded.items()}
+    ref = O.transformer_forward(f32, env["tcfg"], i["hidden"], i["enc"], i["timestep"], i["rope"],
+                                branch_block_samples=bs, branch_block_masks=i["mask"])[0]
+    o16 = O.transformer_forward(folded, env["tcfg"], _b16(i["hidden"]), _b16(i["enc"]), i["timestep"], i["rope"],
+                                branch_block_samples=[_b16(b) for b in bs], branch_block_masks=i["mask"])[0]
+    assert rel(out, ref) <= bound(o16, ref), (rel(out, ref), rel(o16, ref))
