@@ -36,7 +36,7 @@ NTOK = T + NV
 
 def set_config(cfg: int) -> None:
     global HL, WL, NV, NTOK
-    HL, WL = (60, 90) if cfg == 2 else (90, 160)
+    HL, WL = (90, 160) if cfg == 5 else (60, 90)
     NV = F * (HL // 2) * (WL // 2)
     NTOK = T + NV
 
@@ -138,6 +138,99 @@ def make_state(harness, device, seed: int):
     return st, pe
 
 
+def config4_step_flops(window: int) -> float:
+    """Algorithmic FLOP of one config-4 denoising step (1.024e15 window 0, 1.080e15 windows 1-3):
+    the ID-resample processor doubles every transformer attention's keys (the masked / previous-window K/V
+    segment, Nk = 2N); windows > 0 also project the previous window's states to K/V (4 N D^2 per block)."""
+    attn = 4 * NTOK * (2 * NTOK) * D
+    kv = 4 * NTOK * D * D if window > 0 else 0
+    blk = 24 * NTOK * D * D + attn + kv
+    tr = B * (L * blk + 2 * NV * 128 * D + 2 * T * 4096 * D + 2 * NV * D * 64)
+    br_blk = 24 * NTOK * D * D + 4 * NTOK * NTOK * D
+    br = B * (LB * br_blk + 2 * NV * 132 * D + 2 * T * 4096 * D + LB * 2 * NTOK * D * D)
+    return float(tr + br)
+
+
+def run_config4(args, world: int, local: int) -> None:
+    """BASELINE config 4 on one GPU: the VideoPainterID any-length chain — 196 frames as 4 windows of 49 at
+    stride 49, ID-resample processor, prev_clip_weight 0.5, each window conditioned on the previous one's last
+    latent and last-step hidden states — with --steps denoising steps per window (the reference runs 50; the
+    per-step work is the same).  value = denoising steps/s over the whole chain.  The chain is serial; its
+    multi-GPU form is the window-stage pipeline (distributed.run_window_chain, tests/test_distributed_cpu.py)."""
+    if world != 1:
+        raise SystemExit("bench --config 4 runs the serial chain on one GPU (multi-GPU: window-stage pipeline tests)")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, device_scope
+    from videopainter_amd import kernels as K
+    from videopainter_amd.config import COGVIDEOX_5B_I2V
+    from videopainter_amd.pipeline import CogVideoXI2VDualInpaintAnyLHarness
+    from videopainter_amd.scheduler import CogVideoXDPMScheduler
+    t_setup = time.time()
+    cfg = dict(COGVIDEOX_5B_I2V, sample_height=HL, sample_width=WL)
+    with device_scope(device):
+        tr = CogVideoXTransformer3DModel(**dict(cfg, id_pool_resample_learnable=True))
+        br = CogvideoXBranchModel(**dict(cfg, num_layers=LB))
+    tr.init_synthetic_weights_(1234)
+    br.init_synthetic_weights_(1235)
+    sch = CogVideoXDPMScheduler(snr_shift_scale=1.0, prediction_type="v_prediction", rescale_betas_zero_snr=True,
+                                clip_sample=False, set_alpha_to_one=True, timestep_spacing="trailing")
+    harness = CogVideoXI2VDualInpaintAnyLHarness(tr, br, sch)
+    n_windows = 4
+    g = torch.Generator().manual_seed(42)
+    windows = []
+    for w in range(n_windows):
+        lat = torch.randn(1, F, 16, HL, WL, generator=g)
+        vid = torch.randn(1, F, 16, HL, WL, generator=g)
+        mask = torch.zeros(1, 1, F, HL, WL)
+        mask[:, :, 1:, HL // 4:HL // 4 + HL // 2, WL // 4:WL // 4 + WL // 2] = 1.0
+        masked = vid * (1 - mask.permute(0, 2, 1, 3, 4))
+        win = dict(latents=lat, noise=lat.clone(), video_latents=vid, mask=torch.cat([mask] * 2),
+                   masked_video_latents=torch.cat([masked] * 2))
+        if w == 0:
+            img = torch.zeros(1, F, 16, HL, WL)
+            img[:, 0] = torch.randn(1, 16, HL, WL, generator=g) * 0.7
+            win["image_latents"] = img
+        windows.append({k: v.to(device, torch.bfloat16) for k, v in win.items()})
+    pe = torch.randn(1, T, 4096, generator=g).to(device, torch.bfloat16)
+    npe = torch.randn(1, T, 4096, generator=g).to(device, torch.bfloat16)
+    kw = dict(num_frames=49, stride=49, guidance_scale=6.0, use_dynamic_cfg=True, replace_gt=True, mask_add=True,
+              prev_clip_weight=0.5, id_pool_resample_learnable=True)
+    log(f"[bench] config 4 setup {time.time() - t_setup:.1f}s")
+    with torch.no_grad():
+        harness(windows[:2], pe, npe, num_inference_steps=max(1, args.warmup), generator=torch.Generator().manual_seed(0),
+                **kw)  # warm-up: both window kinds (resample w0, prev-clip w>0)
+        torch.cuda.synchronize()
+        with K.timed_launches("attention", "gemm") as tl:
+            t0 = time.perf_counter()
+            out = harness(windows, pe, npe, num_inference_steps=args.steps,
+                          generator=torch.Generator().manual_seed(0), **kw)
+            torch.cuda.synchronize()
+            elapsed = time.perf_counter() - t0
+    n_steps = n_windows * args.steps
+    steps_per_s = n_steps / elapsed
+    fl = sum(config4_step_flops(w) for w in range(n_windows)) * args.steps
+    attn_ms = tl.mean_ms("attention")
+    line = {
+        "metric": METRIC, "value": steps_per_s, "unit": "steps/s", "n_gpus": 1, "steps": n_steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / n_steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic latents/prompt embeds of the 4 x 49f 480x720 windows; random-init CogVideoX-5b-I2V "
+                "(ID-resample processor) + 2-layer branch weights (no checkpoints offline)",
+        "config": {"workload": f"BASELINE config 4: any-length 196 frames = 4 windows x 49f 480x720 at stride 49, "
+                               f"ID-resample + prev_clip_weight 0.5, {args.steps} denoising steps per window "
+                               "(value = denoising steps/s over the chain)",
+                   "windows": n_windows, "tokens": NTOK, "keys_per_attention": 2 * NTOK, "layers": L,
+                   "branch_layers": LB, "parallelism": "serial window chain on 1 GPU"},
+        "step_flop_mean": fl / n_steps,
+        "step_mfma_frac": fl / elapsed / (PEAK_BF16_TFLOPS * 1e12),
+        "attention_ms_per_launch": attn_ms, "attention_launches": tl.count("attention"),
+        "attention_ms_per_step": attn_ms * tl.count("attention") / n_steps,
+        "output_latents": list(out.shape),
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -145,9 +238,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-only", action="store_true")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 5),
-                    help="BASELINE config: 2 = 49f 480x720 bf16 (headline), 5 = 49f 720x1280 with attention + "
-                         "FeedForward in fp8")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
+                    help="BASELINE config: 2 = 49f 480x720 bf16 (headline), 4 = the any-length ID-resample chain "
+                         "(4 windows, --steps denoising steps each), 5 = 49f 720x1280 with attention + FeedForward in fp8")
     args = ap.parse_args()
     set_config(args.config)
 
@@ -158,6 +251,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config == 4:
+        run_config4(args, world, local)
+        return
     if world != args.gpus:
         log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
