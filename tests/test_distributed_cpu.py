@@ -162,3 +162,39 @@ def test_window_chain_pipeline_matches_serial_gloo(world, cfg_split, n_windows):
         assert len(vids) == 2
         for v, r in zip(vids, ref):
             assert torch.equal(v, r), f"rank {rank}: pipelined window chain differs from the serial loop"
+
+
+def _concurrent_worker(rank, world, port, n_windows, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from videopainter_amd.distributed import init, run_windows_concurrent
+    init("gloo")
+    wins = [dict(x=torch.full(SHAPE, float(w + 1))) for w in range(n_windows)]
+    ran = []
+
+    def rw(w, win):
+        ran.append(w)
+        return win["x"] * 2 + w
+
+    out = run_windows_concurrent(wins, rw, _assemble, torch.empty(SHAPE))
+    q.put((rank, out.clone(), ran))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_concurrent_windows_allgather_gloo():
+    """The labelled non-parity mode: windows round-robin over the ranks, one all-gather, every rank assembles the
+    same clip as a single process running all windows."""
+    n_windows, world = 5, 2
+    ref = _assemble([torch.full(SHAPE, float(w + 1)) * 2 + w for w in range(n_windows)])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_concurrent_worker, args=(r, world, port, n_windows, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=100) for _ in ps]
+    for p in ps:
+        p.join(60)
+    for rank, out, ran in res:
+        assert ran == list(range(rank, n_windows, world))
+        assert torch.equal(out, ref)

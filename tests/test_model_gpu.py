@@ -478,3 +478,32 @@ def test_lora_folded_model_matches_oracle(env, tmp_path):
     o16 = O.transformer_forward(folded, env["tcfg"], _b16(i["hidden"]), _b16(i["enc"]), i["timestep"], i["rope"],
                                 branch_block_samples=[_b16(b) for b in bs], branch_block_masks=i["mask"])[0]
     assert rel(out, ref) <= bound(o16, ref), (rel(out, ref), rel(o16, ref))
+
+
+@torch.no_grad()
+def test_concurrent_windows_mode_runs_windows_independently(env):
+    """The labelled non-parity any-length mode on one process: identical to running every window on its own first
+    frame (no hand-off) and assembling — and different from the reference's chained result."""
+    from videopainter_amd.pipeline import CogVideoXI2VDualInpaintAnyLHarness, run_any_length_concurrent
+    from videopainter_amd.scheduler import CogVideoXDPMScheduler
+    from tests.golden.cases import pipe_inputs
+    g = load_file(os.path.join(GOLD, "pipe_tiny.safetensors"))
+    c = PIPE_CASE
+    sch = CogVideoXDPMScheduler(snr_shift_scale=1.0, prediction_type="v_prediction", rescale_betas_zero_snr=True,
+                                clip_sample=False, set_alpha_to_one=True, timestep_spacing="trailing",
+                                beta_start=0.00085, beta_end=0.012)
+    h = CogVideoXI2VDualInpaintAnyLHarness(env["trr"], env["br"], sch)
+    windows = [dict(latents=g[f"w{w}.latents"], image_latents=g["w0.image_latents"], noise=g[f"w{w}.noise"],
+                    video_latents=g[f"w{w}.video_latents"], mask=g[f"w{w}.mask"],
+                    masked_video_latents=g[f"w{w}.masked_video_latents"]) for w in range(2)]
+    windows = [{k: v.to(dev) for k, v in win.items()} for win in windows]
+    inp = pipe_inputs()
+    kw = dict(num_inference_steps=c["steps"], num_frames=c["num_frames"], stride=c["stride"],
+              id_pool_resample_learnable=c["id_pool_resample_learnable"])
+    out = run_any_length_concurrent(h, windows, inp["prompt_embeds"], inp["negative_prompt_embeds"], seed=3, **kw)
+    pe, ts = h.prepare_call(inp["prompt_embeds"], inp["negative_prompt_embeds"], c["steps"])
+    lats = [h.run_window(w, win, win["image_latents"], pe, ts, id_pool_resample_learnable=True,
+                         generator=torch.Generator().manual_seed(3 + w))[0] for w, win in enumerate(windows)]
+    ref = h.assemble(lats, c["num_frames"], c["stride"])
+    assert torch.equal(out, ref)
+    assert out.shape == g["final"].shape

@@ -255,3 +255,41 @@ def run_window_chain(stages: WindowStages, clips: List[dict], run_window: Callab
             local[w] = lat
         videos.append(assemble(stages.gather_windows(local, n, lat_like)))
     return videos
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# concurrent windows: the north-star's literal "segments sharded across GPUs + all-gather of the overlap latents".
+# NOT the reference's semantics: the reference chains windows (window k conditions on window k-1's
+# final latents and, with prev_clip_weight > 0, its last-step hidden states, anyl.py:862-872, 962-988).  Here every
+# window conditions on its own first frame and no previous-window states, so all windows run at once; only the
+# overlap averaging of the assembled clip couples them.  Opt-in, labelled, and never used by the parity tests.
+# ----------------------------------------------------------------------------------------------------------------
+
+def allgather_windows(local: Dict[int, torch.Tensor], n_windows: int, like: torch.Tensor) -> List[torch.Tensor]:
+    """Window w lives on rank w % world; returns every window's latents on every rank (one all-gather over xGMI)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [local[w] for w in range(n_windows)]
+    world, rank = dist.get_world_size(), dist.get_rank()
+    per = (n_windows + world - 1) // world
+    buf = torch.zeros((per,) + tuple(like.shape), dtype=like.dtype, device=like.device)
+    for w, t in local.items():
+        if w % world != rank:
+            raise ValueError(f"window {w} is not placed on rank {rank}")
+        buf[w // world] = t
+    allb = torch.empty((world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
+    if dist.get_backend() == "nccl":
+        dist.all_gather_into_tensor(allb, buf)
+    else:
+        dist.all_gather(list(allb.unbind(0)), buf)
+    return [allb[w % world][w // world] for w in range(n_windows)]
+
+
+def run_windows_concurrent(windows: List[dict], run_window: Callable, assemble: Callable,
+                           lat_like: torch.Tensor) -> torch.Tensor:
+    """NON-PARITY any-length mode: rank r runs windows r, r + world, ... independently (each window's own
+    `image_latents`, no previous-window hand-off), then one all-gather of the window latents and the reference's
+    overlap averaging.  run_window(w, win) -> latents.  Returns the assembled clip on every rank."""
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    local = {w: run_window(w, windows[w]) for w in range(rank, len(windows), world)}
+    return assemble(allgather_windows(local, len(windows), lat_like))

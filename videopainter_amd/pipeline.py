@@ -308,3 +308,31 @@ def run_any_length_pipelined(harness: CogVideoXI2VDualInpaintAnyLHarness, stages
                             lambda w, win, prev: harness.window_image_latents(w, win, prev, num_frames, stride),
                             lambda lats: harness.assemble(lats, num_frames, stride), lat_like, state_shape,
                             mask_shape)
+
+
+@torch.no_grad()
+def run_any_length_concurrent(harness: CogVideoXI2VDualInpaintAnyLHarness, windows: List[dict],
+                              prompt_embeds: torch.Tensor, negative_prompt_embeds: torch.Tensor, *,
+                              num_inference_steps: int = 50, num_frames: int = 49, stride: Optional[int] = None,
+                              seed: int = 0, **kw) -> torch.Tensor:
+    """NON-PARITY multi-GPU any-length mode (the north-star's "clip segments sharded across the GPUs with an
+    all-gather of the overlapping-region latents"; distributed.run_windows_concurrent): every window needs its own
+    `image_latents` (its first frame, encoded) and runs without the previous window's conditioning latent or
+    hidden states (prev_clip_weight is forced to 0); window w draws its scheduler noise from a generator seeded
+    seed + w.  The reference's chained semantics are `harness(...)` / `run_any_length_pipelined`."""
+    from .distributed import run_windows_concurrent
+    stride = num_frames if stride is None else stride
+    pe, timesteps = harness.prepare_call(prompt_embeds, negative_prompt_embeds, num_inference_steps)
+    kw = dict(kw, prev_clip_weight=0.0)
+    for w, win in enumerate(windows):
+        if "image_latents" not in win:
+            raise ValueError(f"window {w} has no image_latents (the concurrent mode conditions every window on its "
+                             "own first frame)")
+
+    def rw(w, win):
+        lat, _, _ = harness.run_window(w, win, win["image_latents"], pe, timesteps, prev_states=None, prev_mask=None,
+                                       capture=False, generator=torch.Generator().manual_seed(seed + w), **kw)
+        return lat
+
+    like = torch.empty(tuple(windows[0]["latents"].shape), device=harness.device, dtype=BF16)
+    return run_windows_concurrent(windows, rw, lambda outs: harness.assemble(outs, num_frames, stride), like)
