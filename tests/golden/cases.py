@@ -96,3 +96,32 @@ def pipe_inputs():
     pe = torch.from_numpy(synth_tensor("pipe.prompt", (1, TINY_T, 32)))
     ne = torch.from_numpy(synth_tensor("pipe.neg", (1, TINY_T, 32)))
     return dict(frames=frames, masks=masks, prompt_embeds=pe, negative_prompt_embeds=ne)
+
+
+# BASELINE config 1 at full model width/depth: 5b-I2V-shaped (42 layers, 48 x 64 heads, text 4096) with
+# sample 32 x 48 x 9 -> latent 3 x 32 x 48 (Nv = 1152, N = 1378), B = 2 (CFG); weights from the counter generator
+# under plain state-dict names, seeds 1234 (transformer) / 1235 (branch) — what `init_synthetic_weights_` and
+# bench.py use
+CONFIG1_SEEDS = (1234, 1235)
+
+
+def config1_cfg():
+    from videopainter_amd.config import COGVIDEOX_5B_I2V
+    cfg = dict(COGVIDEOX_5B_I2V, sample_height=32, sample_width=48, sample_frames=9)
+    return cfg, dict(cfg, num_layers=2)
+
+
+def config1_inputs(dtype=torch.float32):
+    b, f, h, w, t = 2, 3, 32, 48, 226
+    video = synth_tensor("c1.video", (b, f, 16, h, w))
+    image = synth_tensor("c1.image", (b, f, 16, h, w)) * np.float32(0.7)
+    image[:, 1:] = 0.0
+    hidden = np.concatenate([video, image], axis=2)
+    mask = make_mask(b, f, h, w, "c1.mask")
+    masked = synth_tensor("c1.masked", (b, f, 16, h, w)) * (1.0 - mask)
+    branch_cond = np.concatenate([masked, mask], axis=2)
+    enc = synth_tensor("c1.enc", (b, t, 4096))
+    cos, sin = prepare_rotary_positional_embeddings(h * 8, w * 8, f, 64)
+    cv = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dtype)  # noqa: E731
+    return dict(hidden=cv(hidden), video=cv(video), mask=cv(mask), branch_cond=cv(branch_cond), enc=cv(enc),
+                timestep=torch.tensor([999, 999], dtype=torch.int64), rope=(cos, sin))

@@ -17,6 +17,10 @@ Fixtures (all fp32):
                           it drew (captured) and the final latents.
   block_full.safetensors— one full-width CogVideoXBlock (3072 = 48 x 64) at N = 226 + 1152 (config-1 shape), B=1:
                           strided slice + digest of the output.
+  config1.safetensors   — the WHOLE 5b-I2V-shaped transformer (42 layers) + 2-layer branch at config-1 shape, B=2:
+                          noise prediction in fp32 (strided slice + digest) and the reference's own bf16 run's
+                          rel-L2 from it (the tolerance band); weights from the counter generator (plain names,
+                          seeds 1234 / 1235), filled into meta-initialised reference modules.
 """
 from __future__ import annotations
 
@@ -226,8 +230,77 @@ def make_full_block():
                                                             dtype=torch.float64)})
 
 
+def _fill_synthetic(model, seed):
+    """Materialise a meta-initialised reference module on the CPU with the counter-generator weights (threads:
+    numpy releases the GIL in the generator's array ops)."""
+    import concurrent.futures as cf
+    from videopainter_amd.weights import synth_param
+    model = model.to_empty(device="cpu")
+    sd = model.state_dict(keep_vars=True)
+    names = set(sd)
+    for n, _ in model.named_buffers():
+        if n not in names:
+            raise RuntimeError(f"non-persistent buffer {n} would stay uninitialised")
+
+    def one(item):
+        name, t = item
+        with torch.no_grad():
+            t.data.copy_(torch.from_numpy(synth_param(name, tuple(t.shape), seed)))
+        return name
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        for _ in ex.map(one, list(sd.items())):
+            pass
+    return model
+
+
+@torch.no_grad()
+def make_config1():
+    import time
+    from diffusers.models.transformers.cogvideox_transformer_3d import CogVideoXTransformer3DModel
+    from diffusers.models.branch_cogvideox import CogvideoXBranchModel
+    from tests.golden.cases import config1_cfg, config1_inputs, CONFIG1_SEEDS
+    tcfg, bcfg = config1_cfg()
+    t0 = time.time()
+    with torch.device("meta"):
+        tr = CogVideoXTransformer3DModel(**tcfg).eval()
+        br = CogvideoXBranchModel(**bcfg).eval()
+    tr = _fill_synthetic(tr, CONFIG1_SEEDS[0])
+    br = _fill_synthetic(br, CONFIG1_SEEDS[1])
+    print(f"weights {time.time() - t0:.0f}s", flush=True)
+    inp = config1_inputs()
+
+    def fwd(dt):
+        c = lambda x: x.to(dt)  # noqa: E731
+        bs = br(hidden_states=c(inp["video"]), encoder_hidden_states=c(inp["enc"]), branch_cond=c(inp["branch_cond"]),
+                timestep=inp["timestep"], image_rotary_emb=inp["rope"], return_dict=False)[0]
+        o = tr(hidden_states=c(inp["hidden"]), encoder_hidden_states=c(inp["enc"]), timestep=inp["timestep"],
+               image_rotary_emb=inp["rope"], branch_block_samples=bs, branch_block_masks=c(inp["mask"]),
+               return_dict=False)[0]
+        return o.float(), [b.float() for b in bs]
+
+    t0 = time.time()
+    o32, bs32 = fwd(torch.float32)
+    print(f"fp32 forward {time.time() - t0:.0f}s", flush=True)
+    tr.to(torch.bfloat16)
+    br.to(torch.bfloat16)
+    t0 = time.time()
+    o16, bs16 = fwd(torch.bfloat16)
+    print(f"bf16 forward {time.time() - t0:.0f}s", flush=True)
+    rel = lambda a, b: float((a.double() - b.double()).norm() / b.double().norm())  # noqa: E731
+    flat = o32.reshape(-1)
+    out = {"slice": flat[::37].clone(),
+           "digest": torch.tensor([flat.sum(), flat.abs().sum(), flat.norm()], dtype=torch.float64),
+           "branch.0.slice": bs32[0].reshape(-1)[::997].clone(), "branch.1.slice": bs32[1].reshape(-1)[::997].clone(),
+           "ref_bf16_rel": torch.tensor([rel(o16, o32), rel(bs16[0], bs32[0]), rel(bs16[1], bs32[1])])}
+    print("reference bf16 vs fp32 rel-L2: noise_pred %.3e, branch %.3e / %.3e" % tuple(out["ref_bf16_rel"].tolist()))
+    _save("config1.safetensors", out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["tiny", "sched", "pipe", "block"]
+    if "config1" in which:
+        make_config1()
     if "tiny" in which:
         make_tiny()
     if "sched" in which:

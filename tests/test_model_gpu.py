@@ -507,3 +507,45 @@ def test_concurrent_windows_mode_runs_windows_independently(env):
     ref = h.assemble(lats, c["num_frames"], c["stride"])
     assert torch.equal(out, ref)
     assert out.shape == g["final"].shape
+
+
+@torch.no_grad()
+def test_config1_full_model_matches_reference():
+    """BASELINE config 1 at full depth and width: the 42-layer 5b-I2V-shaped transformer + 2-layer branch at
+    N = 226 + 1152, B = 2 (CFG), weights from the counter generator (device fill), against the REFERENCE's fp32
+    forward of the same weights and inputs (tests/golden/config1.safetensors, made by make_golden.py config1).
+    Bound: 2x the reference's own bf16 drift from its fp32 result, + 2e-3."""
+    from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, device_scope
+    from videopainter_amd.weights import synth_param
+    from tests.golden.cases import config1_cfg, config1_inputs, CONFIG1_SEEDS
+    path = os.path.join(GOLD, "config1.safetensors")
+    if not os.path.exists(path):
+        pytest.skip("config1 fixture not generated")
+    g = load_file(path)
+    tcfg, bcfg = config1_cfg()
+    with device_scope(dev):
+        tr = CogVideoXTransformer3DModel(**tcfg)
+        br = CogvideoXBranchModel(**bcfg)
+    tr.init_synthetic_weights_(CONFIG1_SEEDS[0])
+    br.init_synthetic_weights_(CONFIG1_SEEDS[1])
+    # the device generator reproduces the host one the fixture used (up to rare bf16 rounding-boundary ties)
+    for name in ("norm_final.weight", "transformer_blocks.7.attn1.to_v.weight"):
+        p = tr.state_dict()[name].float().cpu()
+        h = torch.from_numpy(synth_param(name, tuple(p.shape), CONFIG1_SEEDS[0]))
+        assert float((p != h).float().mean()) < 1e-3, name
+    inp = config1_inputs()
+    bs = br(hidden_states=_d(inp["video"]), encoder_hidden_states=_d(inp["enc"]), branch_cond=_d(inp["branch_cond"]),
+            timestep=inp["timestep"].to(dev), image_rotary_emb=inp["rope"], return_dict=False)[0]
+    o = tr(hidden_states=_d(inp["hidden"]), encoder_hidden_states=_d(inp["enc"]), timestep=inp["timestep"].to(dev),
+           image_rotary_emb=inp["rope"], branch_block_samples=bs, branch_block_masks=_d(inp["mask"]),
+           return_dict=False)[0]
+    rb = g["ref_bf16_rel"].double()
+    r = rel(o.float().reshape(-1)[::37], g["slice"])
+    r0 = rel(bs[0].float().reshape(-1)[::997], g["branch.0.slice"])
+    r1 = rel(bs[1].float().reshape(-1)[::997], g["branch.1.slice"])
+    print(f"config 1 full model vs reference fp32: noise_pred {r:.3e} (reference bf16 {float(rb[0]):.3e}), "
+          f"branch {r0:.3e} / {r1:.3e} (reference bf16 {float(rb[1]):.3e} / {float(rb[2]):.3e})")
+    assert r <= 2 * float(rb[0]) + 2e-3
+    assert r0 <= 2 * float(rb[1]) + 2e-3 and r1 <= 2 * float(rb[2]) + 2e-3
+    del tr, br, bs, o
+    torch.cuda.empty_cache()
