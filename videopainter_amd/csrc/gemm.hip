@@ -254,7 +254,7 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
   }
 }
 
-template <int VAR, bool FP8 = false>
+template <int VAR, bool FP8 = false, int GROUP = 4>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_desc d, const MxExt mx) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -266,7 +266,6 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
   const int tiles_m = (d.M + BM - 1) / BM;
   const int tiles_n = (d.N + BN - 1) / BN;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GROUP = 8;
   const int per_group = GROUP * tiles_n;
   const int group_id = t / per_group;
   const int first_m = group_id * GROUP;
@@ -897,20 +896,30 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
     (void)hipFuncSetAttribute((const void*)gemm_w4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<7>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5, false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5, false, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr_set = true;
   }
   const char* e = getenv("VP_GEMM_VARIANT");  // A/B switch for benchmarking main-loop variants
-  int variant = (e != nullptr && e[0] >= '1' && e[0] <= '7') ? e[0] - '0' : 5;
+  int variant = (e != nullptr && e[0] >= '1' && e[0] <= '9') ? e[0] - '0' : 5;
   // 32-bit in-tile source offsets: the quadrant pipeline adds them to a 64-bit tile base (A) / segment base (W);
   // variant 6 still offsets A from the matrix base
   const bool w32 = (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
   const bool tile32 = (int64_t)BM * d->lda * 2 < ((int64_t)1 << 31) && w32;
   const bool off32 = (int64_t)d->M * d->lda * 2 < ((int64_t)1 << 31) && w32;
-  if ((variant == 5 || variant == 7) && ((d->K % BK) != 0 || !tile32))
+  if ((variant == 5 || variant == 7 || variant == 8 || variant == 9) && ((d->K % BK) != 0 || !tile32))
     variant = 1;  // the quadrant pipeline needs whole K-tiles
   if (variant == 6 && ((d->K % HK) != 0 || !off32 || (d->n_seg % 16) != 0)) variant = 1;
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
-  if (variant == 7)
+  if (variant == 8)  // v5 with 8 / 2 M-tiles per L2 group instead of 4 (A/B: within noise, FF2 -2 %; 16: -4..7 %)
+    hipLaunchKernelGGL((gemm_bf16_kernel<5, false, 8>), dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream,
+                       *d, mx);
+  else if (variant == 9)
+    hipLaunchKernelGGL((gemm_bf16_kernel<5, false, 2>), dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream,
+                       *d, mx);
+  else if (variant == 7)
     hipLaunchKernelGGL(gemm_bf16_kernel<7>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
   else if (variant == 6)
     hipLaunchKernelGGL(gemm_w4_kernel, dim3(tiles), dim3(W4_THREADS), LDS_BYTES, (hipStream_t)stream, *d);
