@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 3
+#define VP_ABI_VERSION 4
 int vp_abi_version(void);
 /* sizeof of the descriptor structs as compiled into the library: out[0..4] = gemm, attn, dpm, gemm_mx, attn_fp8
  * (ABI check) */
@@ -153,6 +153,13 @@ typedef struct vp_attn_desc {
 } vp_attn_desc;
 
 int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream);
+
+/* The same with a caller-provided workspace for the grid-tail split: when the last round of workgroups would run
+ * on a mostly idle chip (blocks mod resident slots <= half the slots), those blocks run as several key-range
+ * workgroups each plus a merge pass.  vp_attention_workspace_bytes: bytes needed for this descriptor (0: no split;
+ * -1: invalid descriptor).  A null or too small workspace runs the unsplit grid. */
+int64_t vp_attention_workspace_bytes(const vp_attn_desc* d);
+int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* fp8 attention (BASELINE config 5 "attn + FFN in fp8"; same math as vp_attention_fwd_bf16, single K/V segment).
  * base.Q / base.K: e4m3 [B, N, H*64] written by vp_head_norm_rope_fp8 (strides in bytes, multiples of 16), each

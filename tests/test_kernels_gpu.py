@@ -304,3 +304,43 @@ def test_linear_small_timestep_patchify_unpatchify_mask():
     tm = K.patch_mask(m.to(dev), 2)
     ref = (F.avg_pool2d(m.reshape(-1, 1, H, W), 2) > 0).view(B, Fr, -1).reshape(B, -1)
     assert torch.equal(tm.cpu().bool(), ref)
+
+
+@pytest.mark.parametrize("Nq,Nk2", [(333, 0), (1500, 700), (17776, 0)])
+def test_attention_tail_split_matches_unsplit(Nq, Nk2, monkeypatch):
+    """The grid-tail split (last partial round of workgroups run as key-range workgroups + a merge pass) against the
+    unsplit launch of the default kernel: the same attention up to the merge's rounding; at config-2 length the
+    split is exactly what the step runs (6720 blocks on 512 slots)."""
+    from videopainter_amd import kernels as K
+    from videopainter_amd import _native as N
+    import ctypes as C
+    B, H = 2, 2 if Nq < 17776 else 48
+    D = H * 64
+    q, k, v = (bf(rnd(B, Nq, D, seed=s)).to(dev) for s in (70, 71, 72))
+    kw = {}
+    if Nk2:
+        kw = dict(k2=bf(rnd(B, Nk2, D, seed=73)).to(dev), v2=bf(rnd(B, Nk2, D, seed=74)).to(dev))
+    d = N.AttnDesc()
+    d.B, d.H, d.Nq, d.head_dim, d.Nk, d.Nk2 = B, H, Nq, 64, Nq, Nk2
+    d.Q = d.K = d.V = d.O = q.data_ptr()
+    d.q_sn = d.k_sn = d.v_sn = d.o_sn = D
+    d.q_sb = d.k_sb = d.v_sb = d.o_sb = Nq * D
+    if Nk2:
+        d.K2 = d.V2 = q.data_ptr()
+        d.k2_sn = d.v2_sn = D
+        d.k2_sb = d.v2_sb = Nk2 * D
+    assert N.lib().vp_attention_workspace_bytes(C.byref(d)) > 0  # the split is active for this shape
+    out_s = torch.empty(B, Nq, D, device=dev, dtype=torch.bfloat16)
+    K.attention(q, k, v, out_s, H, **kw)
+    monkeypatch.setenv("VP_ATTN_NO_SPLIT", "1")
+    out_u = torch.empty_like(out_s)
+    K.attention(q, k, v, out_u, H, **kw)
+    # bf16 P is rounded against each range's own running max, so the two differ at bf16 noise level
+    assert rel(out_s, out_u) < 5e-3
+    if Nq < 17776:
+        hd = lambda x: x.float().cpu().reshape(B, -1, H, 64).transpose(1, 2)  # noqa: E731
+        kk, vv = hd(k), hd(v)
+        if Nk2:
+            kk, vv = torch.cat([kk, hd(kw["k2"])], 2), torch.cat([vv, hd(kw["v2"])], 2)
+        ref = _sdpa(hd(q), kk, vv).transpose(1, 2).reshape(B, Nq, D)
+        assert rel(out_s, ref) < 1e-2 and rel(out_u, ref) < 1e-2

@@ -623,6 +623,83 @@ VP_DEV void pv_half_x(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)
   }
 }
 
+// ---- grid-tail split: the last partial round of workgroups (nblk mod resident slots) is re-launched as
+// nsplit workgroups per block, each over a contiguous range of key tiles, writing an unnormalised partial
+// (O relative to its own running max, row sum, max) to a workspace; attn_combine_kernel merges them.  Without it the
+// last round runs a few workgroups on an otherwise idle chip (at config 2: 6720 blocks on 512 slots -> 64 blocks
+// alone for a whole block time). ----
+struct AttnSplit {
+  int t_base;   // first block index of this launch
+  int nsplit;   // 1: normal launch; > 1: key-range split of blocks t_base + blockIdx.x / nsplit
+  float* ws;    // partials: [block - t_base][split][query in block (QB)][66] = O[64], m, l
+};
+
+// O^T accumulator layout of one lane (store_out): dim d = dh*32 + 8*gq + 4*hl + r  <->  o[dh][4*gq + r]
+VP_DEV void store_partial(float* rec, const f32x16 (&o)[2], float m_run, float l_run, int hl) {
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int dd = dh * 32 + 8 * gq + 4 * hl;
+      *(f32x4*)(rec + dd) = (f32x4){o[dh][4 * gq], o[dh][4 * gq + 1], o[dh][4 * gq + 2], o[dh][4 * gq + 3]};
+    }
+  if (hl == 0) {
+    rec[64] = m_run;
+    rec[65] = l_tot;
+  }
+}
+
+// one thread per (tail block, query): merge the nsplit partials and store like store_out
+__global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d, int t_base, int ntail, int nsplit,
+                                                           int QB, const float* __restrict__ ws) {
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  if (gid >= ntail * QB) return;
+  const int j = gid / QB, qi = gid - j * QB;
+  const int t = t_base + j;
+  const int nqb = (d.Nq + QB - 1) / QB;
+  const int bh = t / nqb, qb = t - bh * nqb;
+  const int b = bh / d.H, h = bh - b * d.H;
+  const int q = qb * QB + qi;
+  if (q >= d.Nq) return;
+  const float* rec0 = ws + ((int64_t)j * nsplit * QB + qi) * 66;
+  float mx = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, rec0[(int64_t)s * QB * 66 + 64]);
+  float acc[64];
+#pragma unroll
+  for (int e = 0; e < 64; ++e) acc[e] = 0.f;
+  float l = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float* rec = rec0 + (int64_t)s * QB * 66;
+    const float w = __builtin_amdgcn_exp2f(rec[64] - mx);
+    l += rec[65] * w;
+#pragma unroll
+    for (int e = 0; e < 64; e += 4) {
+      const f32x4 v = *(const f32x4*)(rec + e);
+      acc[e] += v[0] * w;
+      acc[e + 1] += v[1] * w;
+      acc[e + 2] += v[2] * w;
+      acc[e + 3] += v[3] * w;
+    }
+  }
+  const float inv = 1.f / l;
+  bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
+#pragma unroll
+  for (int e = 0; e < 64; e += 4) {
+    bf16x4 ov;
+    bf16x4 old;
+    if (d.accumulate) old = *(const bf16x4*)(orow + e);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = rbf(acc[e + r] * inv);
+      if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
+      if (d.accumulate) v = bf2f(old[r]) + v;
+      ov[r] = f2bf(v);
+    }
+    *(bf16x4*)(orow + e) = ov;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // LDS-DMA kernel: NW waves x 32 queries, KB-key tiles (KB = 64 or 128) in a RING-slot LDS ring filled by
 // global_load_lds (no staging registers, no LDS write pass), C-init 32-key halves (see softmax_half_ci).  Tile t +
@@ -631,7 +708,7 @@ VP_DEV void pv_half_x(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)
 // runs at s_setprio 1 (the arbitration loser of each SIMD pair, MI355X_MICROARCH.md "Two waves per SIMD" item 4).
 // ------------------------------------------------------------------------------------------------------------
 template <int NW, int OCC, int KB = 64, int RING = 2, bool PRIO = false, bool LAZY = false, bool PIPE = false>
-__global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc d) {
+__global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc d, const AttnSplit sp) {
   constexpr int QB = NW * 32;
   constexpr int KT = KB * 128;                  // bytes per K (or V) tile
   constexpr int ST = 2 * KT;
@@ -646,14 +723,18 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
   const int hl = lane >> 5;
 
   const int nqb = (d.Nq + QB - 1) / QB;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
+  const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
   const int bh = t / nqb;
   const int qb = t - bh * nqb;
   const int b = bh / d.H;
   const int h = bh - b * d.H;
   const int tiles1 = (d.Nk + KB - 1) / KB;
   const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KB - 1) / KB : 0;
-  const int ntiles = tiles1 + tiles2;
+  const int ntiles_all = tiles1 + tiles2;
+  // key-tile range of this workgroup (the whole sequence unless this is a tail split)
+  const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
+  const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
 
   const int q = qb * QB + wave * 32 + (lane & 31);
   const int qc = q < d.Nq ? q : d.Nq - 1;
@@ -721,14 +802,14 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
   if constexpr (PRIO) {
     if (__builtin_amdgcn_readfirstlane(tid) >= NW * 32) __builtin_amdgcn_s_setprio(1);
   }
-  issue(0);
+  issue(tbeg);
   if constexpr (RING == 3) {
-    if (ntiles > 1) issue(1);
+    if (tbeg + 1 < tend) issue(tbeg + 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  for (int ti = 0; ti < ntiles; ++ti) {
-    if (ti + RING - 1 < ntiles) issue(ti + RING - 1);
+  for (int ti = tbeg; ti < tend; ++ti) {
+    if (ti + RING - 1 < tend) issue(ti + RING - 1);
     const char* Kl = slot_of(ti);
     const Seg sg = tile_seg<KB>(d, ti, tiles1, b, h);
     const int lim = sg.n - sg.key0;
@@ -774,7 +855,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
       pv_half_x(Kl + KT, kh, pf, o, vo);
     }
     // retire tile ti+1 (RING 3: tile ti+2's pieces, 2 per piece-row of this wave, may stay in flight)
-    if (RING == 3 && ti + 2 < ntiles) {
+    if (RING == 3 && ti + 2 < tend) {
       if constexpr (2 * PPW == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
     } else {
@@ -782,7 +863,12 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
     }
     __builtin_amdgcn_s_barrier();
   }
-  store_out(d, o, l_run, q, b, h, hl);
+  if (sp.nsplit > 1) {
+    const int qi = wave * 32 + (lane & 31);
+    store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qi) * 66, o, m_run, l_run, hl);
+  } else {
+    store_out(d, o, l_run, q, b, h, hl);
+  }
 }
 
 
@@ -1088,7 +1174,54 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
 }
 }  // namespace
 
-extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
+namespace {
+// kernel variants (A/B switch VP_ATTN_VARIANT for benchmarking): waves per workgroup, waves/SIMD occupancy target,
+// LDS bytes, key-tile size of the LDS-DMA kernels (0: the register-staged kernels, which take no tail split)
+struct AttnVar {
+  const void* fn;
+  int nw;
+  int lds;
+  int kb;
+};
+static const AttnVar attn_vars[] = {
+    {(const void*)attn_fwd_t<8, 2, 8>, 8, LDS_BYTES, 0},                      // 1: 8 waves x 32 queries, 2 waves/SIMD
+    {(const void*)attn_fwd_t<4, 2, 8>, 4, LDS_BYTES, 0},                      // 2: 4-wave workgroups, 2 per CU
+    {(const void*)attn_fwd_t<4, 3, 8>, 4, LDS_BYTES, 0},                      // 3: 4-wave workgroups, 3 per CU
+    {(const void*)attn_fwd_t<8, 4, 8, false, true>, 8, LDS_BYTES, 0},         // 4: half tiles, 4 waves/SIMD (default)
+    {(const void*)attn_fwd_t<4, 4, 8, false, true>, 4, LDS_BYTES, 0},         // 5: half tiles, 4-wave workgroups
+    {(const void*)attn_fwd_t<8, 2, 8, true>, 8, LDS_BYTES, 0},                // 6: row sums on the MFMA
+    {(const void*)attn_fwd_t<8, 4, 8, false, true, true>, 8, LDS_BYTES, 0},   // 7: C-init half tiles, 4 waves/SIMD
+    {(const void*)attn_fwd_t<4, 3, 8, false, true, true>, 4, LDS_BYTES, 0},   // 8: C-init half tiles, 4-wave WGs, 3/SIMD
+    {(const void*)attn_fwd_t<8, 2, 8, false, true, true>, 8, LDS_BYTES, 0},   // 9: C-init half tiles, 2 waves/SIMD
+    {(const void*)attn_fwd_dma<8, 4>, 8, 4 * KBLK * 128, 64},       // 10: LDS-DMA ring + C-init, 4 waves/SIMD
+    {(const void*)attn_fwd_dma<8, 2>, 8, 4 * KBLK * 128, 64},       // 11: LDS-DMA ring + C-init, 2 waves/SIMD
+    {(const void*)attn_fwd_dma<4, 4>, 4, 4 * KBLK * 128, 64},       // 12: LDS-DMA ring + C-init, 4-wave WGs
+    {(const void*)attn_fwd_dma<5, 4>, 5, 4 * KBLK * 128, 64},       // 13: 5-wave WGs (3 per CU: no grid tail at N=17776)
+    {(const void*)attn_fwd_dma<7, 4>, 7, 4 * KBLK * 128, 64},       // 14: 7-wave WGs (2 per CU)
+    {(const void*)attn_fwd_dma<8, 4, 64, 3>, 8, 6 * KBLK * 128, 64},            // 15: 3-slot ring (2 tiles ahead)
+    {(const void*)attn_fwd_dma<8, 4, 128, 2>, 8, 4 * 128 * 128, 128},           // 16: 128-key tiles
+    {(const void*)attn_fwd_dma<8, 4, 64, 2, true>, 8, 4 * KBLK * 128, 64},      // 17: 10 + static prio for waves 4-7
+    {(const void*)attn_fwd_dma<8, 4, 64, 3, true>, 8, 6 * KBLK * 128, 64},      // 18: 15 + prio
+    {(const void*)attn_fwd_dma<8, 4, 64, 2, false, true>, 8, 4 * KBLK * 128, 64},  // 19: 10 + lazy max, no -m copies
+    {(const void*)attn_fwd_dma<8, 4, 64, 2, true, true>, 8, 4 * KBLK * 128, 64},   // 20: 19 + prio
+    {(const void*)attn_fwd_dma<8, 4, 64, 3, false, true>, 8, 6 * KBLK * 128, 64},  // 21: 19 + 3-slot ring
+    {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true>, 8, 4 * 128 * 128, 128},  // 22: 19 + 128-key tiles
+    {(const void*)attn_fwd_dma<8, 4, 64, 3, true, true>, 8, 6 * KBLK * 128, 64},   // 23: 21 + prio
+    {(const void*)attn_fwd_dma<8, 3, 128, 2, false, true, true>, 8, 4 * 128 * 128, 128},  // 24: 22 + pipelined halves, 3/SIMD
+    {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true, true>, 8, 4 * 128 * 128, 128},  // 25: 24 at 4 waves/SIMD
+    {(const void*)attn_fwd_dma<8, 3, 128, 2, false, true>, 8, 4 * 128 * 128, 128},        // 26: 22 at 3 waves/SIMD
+};
+constexpr int ATTN_NVAR = sizeof(attn_vars) / sizeof(attn_vars[0]);
+
+struct AttnPlan {
+  const AttnVar* v;
+  int QB;
+  int64_t nblk;
+  int ntail = 0, nsplit = 1;  // tail split: the last ntail blocks as ntail * nsplit key-range workgroups
+  int64_t ws_bytes = 0;
+};
+
+int attn_check(const vp_attn_desc* d) {
   if (d == nullptr || d->Q == nullptr || d->K == nullptr || d->V == nullptr || d->O == nullptr) return VP_ERR_ARG;
   if (d->head_dim != 64) return VP_ERR_UNSUPPORTED;
   if (d->B <= 0 || d->H <= 0 || d->Nq <= 0 || d->Nk <= 0 || d->Nk2 < 0) return VP_ERR_ARG;
@@ -1097,62 +1230,92 @@ extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
       (d->v_sb % 8) || (d->o_sb % 4))
     return VP_ERR_ARG;
   if (d->Nk2 > 0 && ((d->k2_sn % 8) || (d->v2_sn % 8) || (d->k2_sb % 8) || (d->v2_sb % 8))) return VP_ERR_ARG;
-  // kernel variants (A/B switch VP_ATTN_VARIANT for benchmarking): waves per workgroup, waves/SIMD occupancy
-  // target, deferred-max softmax, K fragments read ahead
-  struct Var {
-    const void* fn;
-    int nw;
-    int lds = LDS_BYTES;
-  };
-  static const Var vars[] = {
-      {(const void*)attn_fwd_t<8, 2, 8>, 8},                      // 1: 8 waves x 32 queries, 2 waves/SIMD
-      {(const void*)attn_fwd_t<4, 2, 8>, 4},                      // 2: 4-wave workgroups, 2 per CU
-      {(const void*)attn_fwd_t<4, 3, 8>, 4},                      // 3: 4-wave workgroups, 3 per CU
-      {(const void*)attn_fwd_t<8, 4, 8, false, true>, 8},         // 4: half tiles, 4 waves/SIMD (default)
-      {(const void*)attn_fwd_t<4, 4, 8, false, true>, 4},         // 5: half tiles, 4-wave workgroups
-      {(const void*)attn_fwd_t<8, 2, 8, true>, 8},                // 6: row sums on the MFMA
-      {(const void*)attn_fwd_t<8, 4, 8, false, true, true>, 8},   // 7: C-init half tiles, 4 waves/SIMD
-      {(const void*)attn_fwd_t<4, 3, 8, false, true, true>, 4},   // 8: C-init half tiles, 4-wave WGs, 3/SIMD
-      {(const void*)attn_fwd_t<8, 2, 8, false, true, true>, 8},   // 9: C-init half tiles, 2 waves/SIMD
-      {(const void*)attn_fwd_dma<8, 4>, 8, 4 * KBLK * 128},       // 10: LDS-DMA ring + C-init, 4 waves/SIMD
-      {(const void*)attn_fwd_dma<8, 2>, 8, 4 * KBLK * 128},       // 11: LDS-DMA ring + C-init, 2 waves/SIMD
-      {(const void*)attn_fwd_dma<4, 4>, 4, 4 * KBLK * 128},       // 12: LDS-DMA ring + C-init, 4-wave WGs
-      {(const void*)attn_fwd_dma<5, 4>, 5, 4 * KBLK * 128},       // 13: 5-wave WGs (3 per CU: no grid tail at N=17776)
-      {(const void*)attn_fwd_dma<7, 4>, 7, 4 * KBLK * 128},       // 14: 7-wave WGs (2 per CU)
-      {(const void*)attn_fwd_dma<8, 4, 64, 3>, 8, 6 * KBLK * 128},            // 15: 3-slot ring (2 tiles ahead)
-      {(const void*)attn_fwd_dma<8, 4, 128, 2>, 8, 4 * 128 * 128},           // 16: 128-key tiles
-      {(const void*)attn_fwd_dma<8, 4, 64, 2, true>, 8, 4 * KBLK * 128},      // 17: 10 + static prio for waves 4-7
-      {(const void*)attn_fwd_dma<8, 4, 64, 3, true>, 8, 6 * KBLK * 128},      // 18: 15 + prio
-      {(const void*)attn_fwd_dma<8, 4, 64, 2, false, true>, 8, 4 * KBLK * 128},  // 19: 10 + lazy max, no -m copies
-      {(const void*)attn_fwd_dma<8, 4, 64, 2, true, true>, 8, 4 * KBLK * 128},   // 20: 19 + prio
-      {(const void*)attn_fwd_dma<8, 4, 64, 3, false, true>, 8, 6 * KBLK * 128},  // 21: 19 + 3-slot ring
-      {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true>, 8, 4 * 128 * 128},  // 22: 19 + 128-key tiles
-      {(const void*)attn_fwd_dma<8, 4, 64, 3, true, true>, 8, 6 * KBLK * 128},   // 23: 21 + prio
-      {(const void*)attn_fwd_dma<8, 3, 128, 2, false, true, true>, 8, 4 * 128 * 128},  // 24: 22 + pipelined halves, 3/SIMD
-      {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true, true>, 8, 4 * 128 * 128},  // 25: 24 at 4 waves/SIMD
-      {(const void*)attn_fwd_dma<8, 3, 128, 2, false, true>, 8, 4 * 128 * 128},        // 26: 22 at 3 waves/SIMD
-  };
+  return VP_OK;
+}
 
-  constexpr int NVAR = sizeof(vars) / sizeof(vars[0]);
+int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   static bool attr_set = false;
+  static int slots[ATTN_NVAR] = {};
   if (!attr_set) {
     attr_set = true;
-    for (int i = 0; i < NVAR; ++i)
-      (void)hipFuncSetAttribute(vars[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize, vars[i].lds);
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    for (int i = 0; i < ATTN_NVAR; ++i) {
+      (void)hipFuncSetAttribute(attn_vars[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize, attn_vars[i].lds);
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, attn_vars[i].fn, attn_vars[i].nw * 64,
+                                                       attn_vars[i].lds) != hipSuccess)
+        per_cu = 0;
+      slots[i] = per_cu * cus;
+    }
   }
   const char* e = getenv("VP_ATTN_VARIANT");
   int variant = e != nullptr ? atoi(e) : 0;
-  if (variant < 1 || variant > NVAR) variant = DEFAULT_VARIANT;
-  const Var& v = vars[variant - 1];
-  const int nqb = (d->Nq + v.nw * 32 - 1) / (v.nw * 32);
-  const int64_t grid = (int64_t)d->B * d->H * nqb;
-  if (grid > 0x7fffffff) return VP_ERR_ARG;
-  void* args[] = {(void*)d};
-  const hipError_t le = hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(v.nw * 64), args, v.lds,
-                                        (hipStream_t)stream);
-  if (le != hipSuccess) return (int)le;
+  if (variant < 1 || variant > ATTN_NVAR) variant = DEFAULT_VARIANT;
+  pl.v = &attn_vars[variant - 1];
+  pl.QB = pl.v->nw * 32;
+  const int nqb = (d->Nq + pl.QB - 1) / pl.QB;
+  pl.nblk = (int64_t)d->B * d->H * nqb;
+  if (pl.nblk > 0x7fffffff) return VP_ERR_ARG;
+  const int sl = slots[variant - 1];
+  const char* ns = getenv("VP_ATTN_NO_SPLIT");
+  if (pl.v->kb > 0 && sl > 0 && (ns == nullptr || ns[0] == '0')) {
+    const int tail = (int)(pl.nblk % sl);
+    const int ntile = (d->Nk + pl.v->kb - 1) / pl.v->kb + (d->Nk2 > 0 ? (d->Nk2 + pl.v->kb - 1) / pl.v->kb : 0);
+    if (tail > 0 && 2 * tail <= sl) {
+      const int S = min(min(8, sl / tail), ntile);
+      if (S >= 2) {
+        pl.ntail = tail;
+        pl.nsplit = S;
+        pl.ws_bytes = (int64_t)tail * S * pl.QB * 66 * 4;
+      }
+    }
+  }
+  return VP_OK;
+}
+}  // namespace
+
+extern "C" int64_t vp_attention_workspace_bytes(const vp_attn_desc* d) {
+  if (attn_check(d) != VP_OK) return -1;
+  AttnPlan pl;
+  if (attn_plan(d, pl) != VP_OK) return -1;
+  return pl.ws_bytes;
+}
+
+extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, int64_t workspace_bytes,
+                                        void* stream) {
+  int rc = attn_check(d);
+  if (rc != VP_OK) return rc;
+  AttnPlan pl;
+  rc = attn_plan(d, pl);
+  if (rc != VP_OK) return rc;
+  const AttnVar& v = *pl.v;
+  const bool split = pl.ntail > 0 && workspace != nullptr && workspace_bytes >= pl.ws_bytes;
+  const int64_t main_blocks = split ? pl.nblk - pl.ntail : pl.nblk;
+  hipError_t le = hipSuccess;
+  if (main_blocks > 0) {
+    const AttnSplit none = {0, 1, nullptr};
+    void* args[] = {(void*)d, (void*)&none};
+    le = hipLaunchKernel(v.fn, dim3((unsigned)main_blocks), dim3(v.nw * 64), args, v.lds, (hipStream_t)stream);
+    if (le != hipSuccess) return (int)le;
+  }
+  if (split) {
+    const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace};
+    void* args[] = {(void*)d, (void*)&sp};
+    le = hipLaunchKernel(v.fn, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.nw * 64), args, v.lds,
+                         (hipStream_t)stream);
+    if (le != hipSuccess) return (int)le;
+    const int nthreads = pl.ntail * pl.QB;
+    hipLaunchKernelGGL(attn_combine_kernel, dim3((nthreads + 255) / 256), dim3(256), 0, (hipStream_t)stream, *d,
+                       (int)main_blocks, pl.ntail, pl.nsplit, pl.QB, (const float*)workspace);
+  }
   VP_CHECK_LAUNCH();
   return VP_OK;
+}
+
+extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
+  return vp_attention_fwd_bf16_ws(d, nullptr, 0, stream);
 }
 
 extern "C" int vp_mx_mfma_probe32(const void* A, const void* B, const void* sa, const void* sb, float* C,

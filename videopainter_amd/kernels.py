@@ -296,10 +296,28 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
         d.Nk2 = k2.shape[1]
     d.O, d.o_sb, d.o_sn = _p(out), out.stride(0), out.stride(1)
     d.scale, d.out_scale, d.accumulate = scale, out_scale, int(accumulate)
+    L = N.lib()
+    nb = L.vp_attention_workspace_bytes(C.byref(d))
+    if nb < 0:
+        raise ValueError("invalid attention descriptor")
+    ws = _workspace(q.device, nb) if nb > 0 else None
     ev = _t0("attention")
-    N.check(N.lib().vp_attention_fwd_bf16(C.byref(d), _stream()), "vp_attention_fwd_bf16")
+    N.check(L.vp_attention_fwd_bf16_ws(C.byref(d), _p(ws), nb, _stream()), "vp_attention_fwd_bf16_ws")
     _t1("attention", ev)
     return out
+
+
+_WS: dict = {}
+
+
+def _workspace(device, nbytes: int) -> torch.Tensor:
+    """A per-device scratch buffer reused across launches (stream-ordered: every user runs on the current stream)."""
+    key = (device.type, device.index)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1 << 20), device=device, dtype=torch.uint8)
+        _WS[key] = ws
+    return ws
 
 
 # ---- fp8 attention (BASELINE config 5; formats in include/vp_hip.h) ----
