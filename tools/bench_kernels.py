@@ -106,7 +106,10 @@ def main():
             res[f"attention_{var}_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
             print("attention", var, res[f"attention_{var}_r{rnd}"], flush=True)
     os.environ.pop("VP_ATTN_VARIANT", None)
-    if args.only in ("attention", "attn8"):
+    if args.only == "attention":  # bf16 attention only (rocprofv3 --pmc passes filter on the kernel name)
+        print(json.dumps(res))
+        return
+    if args.only == "attn8":
         # fp8 attention (config 5 path) on the same operands: producers once, then the kernel, interleaved with bf16
         q_exp, k_exp = 5, 4
         q8 = (q.float() * 0.125 * K.LOG2E * 2.0 ** q_exp).to(torch.float8_e4m3fn).view(torch.uint8)
