@@ -707,7 +707,8 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d,
 // tile t waits (counted vmcnt) for tile t+1 only, then one barrier.  PRIO: the second half of the workgroup's waves
 // runs at s_setprio 1 (the arbitration loser of each SIMD pair, MI355X_MICROARCH.md "Two waves per SIMD" item 4).
 // ------------------------------------------------------------------------------------------------------------
-template <int NW, int OCC, int KB = 64, int RING = 2, bool PRIO = false, bool LAZY = false, bool PIPE = false>
+template <int NW, int OCC, int KB = 64, int RING = 2, bool PRIO = false, bool LAZY = false, bool PIPE = false,
+          bool TAIL = false>  // TAIL: the grid-tail split instance (a separate symbol, so profiles list it apart)
 __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc d, const AttnSplit sp) {
   constexpr int QB = NW * 32;
   constexpr int KT = KB * 128;                  // bytes per K (or V) tile
@@ -1176,12 +1177,13 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
 
 namespace {
 // kernel variants (A/B switch VP_ATTN_VARIANT for benchmarking): waves per workgroup, waves/SIMD occupancy target,
-// LDS bytes, key-tile size of the LDS-DMA kernels (0: the register-staged kernels, which take no tail split)
+// LDS bytes, key-tile size of the LDS-DMA kernels (0: the register-staged kernels), the grid-tail split instance
 struct AttnVar {
   const void* fn;
   int nw;
   int lds;
   int kb;
+  const void* fn_tail = nullptr;  // the TAIL instance (variants that take the grid-tail split)
 };
 static const AttnVar attn_vars[] = {
     {(const void*)attn_fwd_t<8, 2, 8>, 8, LDS_BYTES, 0},                      // 1: 8 waves x 32 queries, 2 waves/SIMD
@@ -1205,7 +1207,8 @@ static const AttnVar attn_vars[] = {
     {(const void*)attn_fwd_dma<8, 4, 64, 2, false, true>, 8, 4 * KBLK * 128, 64},  // 19: 10 + lazy max, no -m copies
     {(const void*)attn_fwd_dma<8, 4, 64, 2, true, true>, 8, 4 * KBLK * 128, 64},   // 20: 19 + prio
     {(const void*)attn_fwd_dma<8, 4, 64, 3, false, true>, 8, 6 * KBLK * 128, 64},  // 21: 19 + 3-slot ring
-    {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true>, 8, 4 * 128 * 128, 128},  // 22: 19 + 128-key tiles
+    {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true>, 8, 4 * 128 * 128, 128,
+     (const void*)attn_fwd_dma<8, 4, 128, 2, false, true, false, true>},  // 22: 19 + 128-key tiles
     {(const void*)attn_fwd_dma<8, 4, 64, 3, true, true>, 8, 6 * KBLK * 128, 64},   // 23: 21 + prio
     {(const void*)attn_fwd_dma<8, 3, 128, 2, false, true, true>, 8, 4 * 128 * 128, 128},  // 24: 22 + pipelined halves, 3/SIMD
     {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true, true>, 8, 4 * 128 * 128, 128},  // 25: 24 at 4 waves/SIMD
@@ -1243,6 +1246,9 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     for (int i = 0; i < ATTN_NVAR; ++i) {
       (void)hipFuncSetAttribute(attn_vars[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize, attn_vars[i].lds);
+      if (attn_vars[i].fn_tail != nullptr)
+        (void)hipFuncSetAttribute(attn_vars[i].fn_tail, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  attn_vars[i].lds);
       int per_cu = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, attn_vars[i].fn, attn_vars[i].nw * 64,
                                                        attn_vars[i].lds) != hipSuccess)
@@ -1260,7 +1266,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   if (pl.nblk > 0x7fffffff) return VP_ERR_ARG;
   const int sl = slots[variant - 1];
   const char* ns = getenv("VP_ATTN_NO_SPLIT");
-  if (pl.v->kb > 0 && sl > 0 && (ns == nullptr || ns[0] == '0')) {
+  if (pl.v->fn_tail != nullptr && sl > 0 && (ns == nullptr || ns[0] == '0')) {
     const int tail = (int)(pl.nblk % sl);
     const int ntile = (d->Nk + pl.v->kb - 1) / pl.v->kb + (d->Nk2 > 0 ? (d->Nk2 + pl.v->kb - 1) / pl.v->kb : 0);
     if (tail > 0 && 2 * tail <= sl) {
@@ -1303,7 +1309,7 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   if (split) {
     const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace};
     void* args[] = {(void*)d, (void*)&sp};
-    le = hipLaunchKernel(v.fn, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.nw * 64), args, v.lds,
+    le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.nw * 64), args, v.lds,
                          (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
     const int nthreads = pl.ntail * pl.QB;
