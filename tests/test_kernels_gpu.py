@@ -1,5 +1,4 @@
 """Numerics of each HIP kernel against a plain-PyTorch fp32 reference of the same op (GPU only)."""
-import math
 
 import pytest
 import torch

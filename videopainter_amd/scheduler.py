@@ -10,7 +10,7 @@ so seeded runs match.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Tuple, Union
+from typing import Optional, Tuple, Union
 
 import numpy as np
 import torch
