@@ -25,12 +25,13 @@ VP_DEV float rbf(float x) { return (float)(bf16)x; }
 
 VP_DEV float gelu_tanh(float x) {
   // torch F.gelu(approximate="tanh"): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  // tanh(u) = 1 - 2 / (exp(2u) + 1), stable for large |u|
-  float e = __expf(2.f * u);
-  float t = 1.f - 2.f / (e + 1.f);
-  return 0.5f * x * (1.f + t);
+  // = x / (1 + exp(-2u)) = x / (1 + 2^(x (c0 + c1 x^2))) with c0 = -2 k0 log2(e), c1 = c0 k1: 5 VALU + v_exp_f32 +
+  // v_rcp_f32 (1 ulp).  The IEEE division of the textbook form costs ~10 VALU per element, and in the FF1 GEMM's
+  // epilogue (256 x 256 outputs per workgroup, not overlapped with MFMA) that was ~20 % of the tile time.  Large
+  // |x| saturates correctly: 2^(+big) = inf -> rcp = 0 -> -0; 2^(-big) = 0 -> x.
+  const float c0 = -2.f * 0.7978845608028654f * 1.4426950408889634f, c1 = c0 * 0.044715f;
+  const float a = x * __builtin_fmaf(c1, x * x, c0);
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(a));
 }
 
 VP_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
