@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 4
+#define VP_ABI_VERSION 5
 int vp_abi_version(void);
 /* sizeof of the descriptor structs as compiled into the library: out[0..4] = gemm, attn, dpm, gemm_mx, attn_fp8
  * (ABI check) */
@@ -49,7 +49,13 @@ enum {
   VP_EPI_BIAS_GELU = 1,   /* C = rnd(gelu_tanh(rnd(acc + bias)))                                             */
   VP_EPI_BIAS_SCALE = 2,  /* C = rnd(rnd(acc + bias) * alpha)            (branch conditioning_scale)         */
   VP_EPI_GATED = 3,       /* C = rnd(R + rnd(gate * rnd(acc + bias))) [then rnd(C + inject) on video rows]   */
-  VP_EPI_BIAS_ADDROWS = 4 /* C = rnd(rnd(acc + bias) + addrows[(m % rows_per_group) + addrows_offset, n])   */
+  VP_EPI_BIAS_ADDROWS = 4, /* C = rnd(rnd(acc + bias) + addrows[(m % rows_per_group) + addrows_offset, n])  */
+  /* 5 = VP_EPI_BIAS_GELU_MXFP8 (vp_gemm_mx_fp8 only, below) */
+  VP_EPI_BIAS_QKNORM_ROPE = 6 /* fused QKV projection: segments 0 / 1 (q / k): every 64-column head of
+                               * y = rnd(acc + bias) -> rnd(LayerNorm64(y; qk_ln_w[s], qk_ln_b[s], qk_eps[s])), then on
+                               * video rows (m % tokens_per_batch >= text_len) the interleaved-pair RoPE from
+                               * rope_cos / rope_sin (fp32 [tokens_per_batch - text_len][64]) -> rnd; segment 2 (v) as
+                               * VP_EPI_BIAS.  = vp_gemm_bf16 + vp_head_norm_rope_bf16 on q and k, bit for bit. */
 };
 
 typedef struct vp_gemm_desc {
@@ -82,6 +88,12 @@ typedef struct vp_gemm_desc {
   /* VP_EPI_BIAS_ADDROWS */
   const void* addrows;
   int64_t addrows_ld, addrows_offset;
+  /* VP_EPI_BIAS_QKNORM_ROPE (norm_q / norm_k are LayerNorm(64) with affine bf16 weights; rows_per_group == M) */
+  const void* qk_ln_w[2];
+  const void* qk_ln_b[2];
+  float qk_eps[2];
+  const float* rope_cos; /* NULL: no RoPE (image_rotary_emb None) */
+  const float* rope_sin;
 } vp_gemm_desc;
 
 int vp_gemm_bf16(const vp_gemm_desc* d, void* stream);

@@ -273,6 +273,45 @@ def test_head_norm_rope_and_masked_null_key():
     assert torch.equal(k2[0, 0, :64].cpu(), lb)
 
 
+@pytest.mark.parametrize("H,T,rope", [(2, 8, True), (4, 5, True), (2, 0, False)])
+def test_gemm_qknorm_rope_epilogue_matches_separate_kernels(H, T, rope, gemm_variant):
+    """EPI_BIAS_QKNORM_ROPE (the fused QKV projection) == GEMM + vp_head_norm_rope_bf16 on q and k, bit for bit
+    (one shared device routine); v untouched; ragged M (not a multiple of the 256-row tile)."""
+    from types import SimpleNamespace
+
+    from videopainter_amd import _native as NAT
+    from videopainter_amd import kernels as K
+    from oracle.cogvideox_oracle import apply_rotary_emb, prepare_rotary_positional_embeddings
+    B, D = 2, H * 64
+    cos, sin = prepare_rotary_positional_embeddings(128, 192, 3, 64)
+    Nv = cos.shape[0]
+    Ntok = T + Nv
+    x = bf(rnd(B * Ntok, 128, seed=101)).to(dev)
+    ws = [bf(rnd(D, 128, std=0.1, seed=102 + i)).to(dev) for i in range(3)]
+    bs = [bf(rnd(D, std=0.1, seed=105 + i)).to(dev) for i in range(3)]
+    lns = [SimpleNamespace(weight=bf(1 + 0.1 * rnd(64, seed=108 + i)).to(dev),
+                           bias=bf(0.1 * rnd(64, seed=110 + i)).to(dev), eps=(1e-6, 1e-5)[i]) for i in range(2)]
+    rp = (cos.to(dev), sin.to(dev)) if rope else None
+    want = torch.empty(B * Ntok, 3 * D, device=dev, dtype=torch.bfloat16)
+    K.gemm(x, ws, bs, want)
+    w3 = want.view(B, Ntok, 3 * D)
+    for s in range(2):
+        K.head_norm_rope(w3[..., s * D:(s + 1) * D], w3[..., s * D:(s + 1) * D], H, T, lns[s].weight, lns[s].bias,
+                         lns[s].eps, rp)
+    got = torch.full((B * Ntok, 3 * D), float("nan"), device=dev, dtype=torch.bfloat16)
+    K.gemm(x, ws, bs, got, epilogue=NAT.EPI_BIAS_QKNORM_ROPE, qk_norm=tuple(lns), rope=rp, tokens_per_batch=Ntok,
+           text_len=T)
+    assert torch.equal(got, want)
+    # and against plain torch fp32 (LN over each head, rotary on video tokens)
+    y = bf(x.float().cpu() @ torch.cat(ws).float().cpu().T + torch.cat(bs).float().cpu()).view(B, Ntok, 3 * D)
+    for s in range(2):
+        h = y[..., s * D:(s + 1) * D].view(B, Ntok, H, 64).transpose(1, 2)
+        n = F.layer_norm(h, (64,), lns[s].weight.float().cpu(), lns[s].bias.float().cpu(), lns[s].eps)
+        if rope:
+            n[:, :, T:] = apply_rotary_emb(n[:, :, T:], cos, sin)
+        assert rel(got.view(B, Ntok, 3 * D)[..., s * D:(s + 1) * D], n.transpose(1, 2).reshape(B, Ntok, D)) < 8e-3
+
+
 def test_linear_small_timestep_patchify_unpatchify_mask():
     from videopainter_amd import kernels as K
     from oracle.cogvideox_oracle import timestep_embedding

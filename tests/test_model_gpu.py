@@ -108,6 +108,25 @@ def test_transformer_matches_reference(env, mode):
 
 
 @torch.no_grad()
+def test_fused_qkv_norm_rope_bit_exact_vs_separate_launches(env, monkeypatch):
+    """The QKV GEMM with the qk-norm + RoPE epilogue (default) gives the model output of the separate
+    vp_head_norm_rope_bf16 launches (VP_NO_QKV_FUSION=1) bit for bit, incl. the returned hidden states."""
+    i, g = env["inp"], env["g"]
+    bs = [_d(g["branch.0"]), _d(g["branch.1"])]
+
+    def run():
+        return env["tr"](hidden_states=_d(i["hidden"]), encoder_hidden_states=_d(i["enc"]),
+                         timestep=i["timestep"].to(dev), image_rotary_emb=i["rope"], branch_block_samples=bs,
+                         branch_block_masks=i["mask"], return_hidden_states=True, return_dict=False)
+    fused = run()
+    monkeypatch.setenv("VP_NO_QKV_FUSION", "1")
+    sep = run()
+    assert torch.equal(fused[0], sep[0])
+    for k in range(4):
+        assert torch.equal(fused[1][k], sep[1][k]), k
+
+
+@torch.no_grad()
 def test_resample_processor_matches_reference(env):
     from oracle import cogvideox_oracle as O
     i, g = env["inp"], env["g"]

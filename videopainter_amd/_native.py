@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -32,7 +32,8 @@ class GemmDesc(C.Structure):
                 ("tokens_per_batch", i32), ("text_len", i32),
                 ("inject", vp), ("inject_ld", i64), ("inject_bstride", i64), ("inject_mask", vp),
                 ("inject_mask_bstride", i64),
-                ("addrows", vp), ("addrows_ld", i64), ("addrows_offset", i64)]
+                ("addrows", vp), ("addrows_ld", i64), ("addrows_offset", i64),
+                ("qk_ln_w", vp * 2), ("qk_ln_b", vp * 2), ("qk_eps", f32 * 2), ("rope_cos", vp), ("rope_sin", vp)]
 
 
 class AttnDesc(C.Structure):
@@ -63,7 +64,7 @@ class DpmDesc(C.Structure):
                 ("prev_out", vp)]
 
 
-EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS, EPI_BIAS_GELU_MXFP8 = range(6)
+EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS, EPI_BIAS_GELU_MXFP8, EPI_BIAS_QKNORM_ROPE = range(7)
 
 # name -> (restype, argtypes)
 _SIGS = {

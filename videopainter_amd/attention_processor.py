@@ -13,11 +13,13 @@ block calls it directly so that to_out runs as one GEMM with the gated residual 
 from __future__ import annotations
 
 import inspect
+import os
 from typing import Optional, Tuple
 
 import torch
 import torch.nn as nn
 
+from . import _native as NAT
 from . import kernels as K
 from .modules import Dropout, LayerNorm, Linear
 
@@ -77,12 +79,20 @@ class Attention(nn.Module):
                               attention_mask=attention_mask, **kw)
 
 
-def _qkv(attn, x: torch.Tensor) -> torch.Tensor:
+def _qkv(attn, x: torch.Tensor, norm_rope=None) -> torch.Tensor:
+    """The fused QKV projection; with norm_rope = (text_len, rope) q and k leave the GEMM already through norm_q /
+    norm_k and RoPE (the epilogue EPI_BIAS_QKNORM_ROPE: bit-equal to the GEMM + vp_head_norm_rope_bf16 on each)."""
     B, Ntok, D = x.shape
     out = torch.empty(B, Ntok, 3 * attn.inner_dim if hasattr(attn, "inner_dim") else 3 * D, device=x.device,
                       dtype=BF16)
-    K.gemm(x.reshape(-1, D), [attn.to_q.weight, attn.to_k.weight, attn.to_v.weight],
-           [attn.to_q.bias, attn.to_k.bias, attn.to_v.bias], out.view(B * Ntok, -1))
+    ws = [attn.to_q.weight, attn.to_k.weight, attn.to_v.weight]
+    bs = [attn.to_q.bias, attn.to_k.bias, attn.to_v.bias]
+    if norm_rope is None:
+        K.gemm(x.reshape(-1, D), ws, bs, out.view(B * Ntok, -1))
+    else:
+        text_len, rope = norm_rope
+        K.gemm(x.reshape(-1, D), ws, bs, out.view(B * Ntok, -1), epilogue=NAT.EPI_BIAS_QKNORM_ROPE,
+               qk_norm=(attn.norm_q, attn.norm_k), rope=rope, tokens_per_batch=Ntok, text_len=text_len)
     return out
 
 
@@ -94,6 +104,19 @@ def _kv(attn, x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _fusable_norms(attn) -> bool:
+    """norm_q / norm_k are LayerNorm(64) with bf16 affine parameters (CogVideoX's qk_norm, the fused epilogue's
+    contract); env VP_NO_QKV_FUSION=1 keeps the separate vp_head_norm_rope_bf16 launches (A/B)."""
+    if os.environ.get("VP_NO_QKV_FUSION", "0") == "1":
+        return False
+    for ln in (getattr(attn, "norm_q", None), getattr(attn, "norm_k", None)):
+        if ln is None or getattr(ln, "weight", None) is None or getattr(ln, "bias", None) is None:
+            return False
+        if ln.weight.numel() != 64 or ln.weight.dtype != BF16 or ln.bias.dtype != BF16:
+            return False
+    return True
+
+
 class CogVideoXAttnProcessor2_0:
     """HIP restatement of `CogVideoXAttnProcessor2_0.__call__` (attention_processor.py:2107-2209)."""
 
@@ -103,14 +126,17 @@ class CogVideoXAttnProcessor2_0:
         B, Ntok, D = x.shape
         H = attn.heads
         rope = _rope_dev(image_rotary_emb, x.device)
-        qkv = _qkv(attn, x) if qkv is None else qkv  # (the block may hand over an fp8 projection)
-        q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
-        eps_q, eps_k = attn.norm_q.eps, attn.norm_k.eps
         fp8 = getattr(attn, "fp8_qk_exp", None)
+        fused = qkv is None and fp8 is None and _fusable_norms(attn)
+        if qkv is None:  # (the block may hand over an fp8 projection)
+            qkv = _qkv(attn, x, (text_len, rope) if fused else None)
+        q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
+        eps_k = attn.norm_k.eps
         if fp8 is not None:
             return self._attend_fp8(attn, q, k, v, text_len, rope, fp8, prev_hidden_states, prev_clip_weight)
-        K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, eps_q, rope)
-        K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, eps_k, rope)
+        if not fused:
+            K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, attn.norm_q.eps, rope)
+            K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, eps_k, rope)
         o = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
         if prev_hidden_states is not None and prev_clip_weight is not None and prev_clip_weight > 0.0:
             pkv = _kv(attn, prev_hidden_states.to(BF16).contiguous())

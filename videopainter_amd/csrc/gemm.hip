@@ -244,6 +244,21 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
         if (inj) o = rbf(o + bf2f(iv[e]));
         v[e] = f2bf(o);
       }
+    } else if (epi == VP_EPI_BIAS_QKNORM_ROPE) {
+      // the 8 lanes of a 64-column head are consecutive (chunk & 7) and row-uniform; n0 and n_seg are multiples of 64
+      const int sg = ncol / d.n_seg;
+      if (sg < 2) {
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = bf2f(v[e]);
+        const int tok = m % d.tokens_per_batch;
+        const bool rot = d.rope_cos != nullptr && tok >= d.text_len;
+        const int64_t ro = (int64_t)(tok - d.text_len) * 64;
+        ln64_rope8(f, chunk & 7, (const bf16*)d.qk_ln_w[sg], (const bf16*)d.qk_ln_b[sg], d.qk_eps[sg],
+                   rot ? d.rope_cos + ro : nullptr, rot ? d.rope_sin + ro : nullptr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(f[e]);
+      }
     } else if (epi == VP_EPI_BIAS_ADDROWS) {
       const bf16x8 pv = *(const bf16x8*)((const bf16*)d.addrows +
                                          (int64_t)((m % d.rows_per_group) + d.addrows_offset) * d.addrows_ld + ncol);
@@ -873,7 +888,14 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   if (d->rows_per_group <= 0) return VP_ERR_ARG;
   const int nsegs = d->W[2] ? 3 : (d->W[1] ? 2 : 1);
   if (d->n_seg <= 0 || d->n_seg * nsegs != d->N) return VP_ERR_ARG;
-  if (d->epilogue < VP_EPI_BIAS || d->epilogue > VP_EPI_BIAS_ADDROWS) return VP_ERR_ARG;
+  if (d->epilogue < VP_EPI_BIAS || d->epilogue > VP_EPI_BIAS_QKNORM_ROPE || d->epilogue == VP_EPI_BIAS_GELU_MXFP8)
+    return VP_ERR_ARG;
+  if (d->epilogue == VP_EPI_BIAS_QKNORM_ROPE) {
+    if (nsegs != 3 || (d->n_seg % 64) != 0 || d->rows_per_group != d->M || d->tokens_per_batch <= 0) return VP_ERR_ARG;
+    for (int s = 0; s < 2; ++s)
+      if (d->qk_ln_w[s] == nullptr || d->qk_ln_b[s] == nullptr) return VP_ERR_ARG;
+    if ((d->rope_cos == nullptr) != (d->rope_sin == nullptr)) return VP_ERR_ARG;
+  }
   if (d->epilogue == VP_EPI_GATED) {
     if (d->R == nullptr || d->gate == nullptr || d->gate_text == nullptr || d->tokens_per_batch <= 0) return VP_ERR_ARG;
     if ((d->ldr % 8) != 0 || (d->gate_bstride % 8) != 0) return VP_ERR_ARG;

@@ -179,43 +179,9 @@ __global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restr
     if (tok_mask != nullptr) t = rbf(rbf(t * m) * pre_scale);
     x[e] = t;
   }
-  float s = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) s += x[e];
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  s += __shfl_xor(s, 4, 64);
-  const float mean = s * (1.f / 64.f);
-  float q = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float t = x[e] - mean;
-    q += t * t;
-  }
-  q += __shfl_xor(q, 1, 64);
-  q += __shfl_xor(q, 2, 64);
-  q += __shfl_xor(q, 4, 64);
-  const float rstd = rsqrtf(q * (1.f / 64.f) + eps);
-  const bf16x8 w = *(const bf16x8*)(lw + sub * 8);
-  const bf16x8 bb = *(const bf16x8*)(lb + sub * 8);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) x[e] = rbf((x[e] - mean) * rstd * bf2f(w[e]) + bf2f(bb[e]));
-  if (cosp != nullptr && n >= text_len) {
-    const float* cr = cosp + (int64_t)(n - text_len) * 64 + sub * 8;
-    const float* sr = sinp + (int64_t)(n - text_len) * 64 + sub * 8;
-    const f32x4 c0 = *(const f32x4*)cr, c1 = *(const f32x4*)(cr + 4);
-    const f32x4 s0 = *(const f32x4*)sr, s1 = *(const f32x4*)(sr + 4);
-    const float cs[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-    const float sn[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-    float y[8];
-#pragma unroll
-    for (int e = 0; e < 8; e += 2) {
-      y[e] = x[e] * cs[e] + (-x[e + 1]) * sn[e];
-      y[e + 1] = x[e + 1] * cs[e + 1] + x[e] * sn[e + 1];
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) x[e] = y[e];
-  }
+  const bool rot = cosp != nullptr && n >= text_len;
+  ln64_rope8(x, sub, lw, lb, eps, rot ? cosp + (int64_t)(n - text_len) * 64 : nullptr,
+             rot ? sinp + (int64_t)(n - text_len) * 64 : nullptr);
   if (valid) {
     if constexpr (FP8) {
       float y[8];

@@ -36,6 +36,51 @@ VP_DEV float gelu_tanh(float x) {
 
 VP_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
 
+// norm_q / norm_k + apply_rotary_emb on one 64-wide head held as 8 consecutive values by each of 8 consecutive lanes
+// (sub = the lane's eighth; the 8 lanes are active together): LayerNorm(64) in fp32 from the bf16 inputs (two-pass
+// mean / centred variance, rstd = rsqrt(var + eps)), bf16 output (torch LayerNorm on bf16,
+// attention_processor.py:2143-2154), then when cr / sr are given (video tokens) the interleaved-pair rotation in
+// fp32 of the bf16 values, x * cos + rot(x) * sin (embeddings.py:655-701, apply_rotary_emb).  Shared by
+// vp_head_norm_rope_* and the QKV GEMM's fused epilogue so the two are bit-equal.
+VP_DEV void ln64_rope8(float (&x)[8], int sub, const bf16* __restrict__ lw, const bf16* __restrict__ lb, float eps,
+                       const float* __restrict__ cr, const float* __restrict__ sr) {
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s += x[e];
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  const float mean = s * (1.f / 64.f);
+  float q = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float t = x[e] - mean;
+    q += t * t;
+  }
+  q += __shfl_xor(q, 1, 64);
+  q += __shfl_xor(q, 2, 64);
+  q += __shfl_xor(q, 4, 64);
+  const float rstd = rsqrtf(q * (1.f / 64.f) + eps);
+  const bf16x8 w = *(const bf16x8*)(lw + sub * 8);
+  const bf16x8 bb = *(const bf16x8*)(lb + sub * 8);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = rbf((x[e] - mean) * rstd * bf2f(w[e]) + bf2f(bb[e]));
+  if (cr != nullptr) {
+    const f32x4 c0 = *(const f32x4*)(cr + sub * 8), c1 = *(const f32x4*)(cr + sub * 8 + 4);
+    const f32x4 s0 = *(const f32x4*)(sr + sub * 8), s1 = *(const f32x4*)(sr + sub * 8 + 4);
+    const float cs[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+    const float sn[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    float y[8];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      y[e] = x[e] * cs[e] + (-x[e + 1]) * sn[e];
+      y[e + 1] = x[e + 1] * cs[e + 1] + x[e] * sn[e + 1];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = y[e];
+  }
+}
+
 VP_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

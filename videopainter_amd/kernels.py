@@ -88,8 +88,10 @@ def gemm(a: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[Opti
          mod: Optional[torch.Tensor] = None, gate_chunk: int = 2, gate_text_chunk: int = 5,
          tokens_per_batch: int = 1, text_len: int = 0, inject: Optional[torch.Tensor] = None,
          inject_ld: int = 0, inject_bstride: int = 0, inject_mask: Optional[torch.Tensor] = None,
-         addrows: Optional[torch.Tensor] = None, addrows_offset: int = 0) -> torch.Tensor:
-    """out = epilogue(a @ cat(weights).T).  `a` rows: M rows of length K at stride lda."""
+         addrows: Optional[torch.Tensor] = None, addrows_offset: int = 0, qk_norm=None, rope=None) -> torch.Tensor:
+    """out = epilogue(a @ cat(weights).T).  `a` rows: M rows of length K at stride lda.
+    EPI_BIAS_QKNORM_ROPE: qk_norm = (norm_q, norm_k) LayerNorm(64) modules, rope = (cos, sin) fp32 [N - text_len, 64]
+    or None; rows are (batch, token) with `tokens_per_batch` / `text_len`."""
     _chk(a, "a")
     _chk(out, "out")
     K = weights[0].shape[1]
@@ -135,6 +137,23 @@ def gemm(a: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[Opti
                 _chk(inject_mask, "inject_mask", torch.uint8)
                 d.inject_mask = _p(inject_mask)
                 d.inject_mask_bstride = inject_mask.stride(0)
+    if epilogue == N.EPI_BIAS_QKNORM_ROPE:
+        for i, ln in enumerate(qk_norm):
+            _chk(ln.weight, "ln weight")
+            _chk(ln.bias, "ln bias")
+            if ln.weight.numel() != 64:
+                raise ValueError("the fused qk-norm epilogue is LayerNorm over head_dim 64")
+            d.qk_ln_w[i], d.qk_ln_b[i], d.qk_eps[i] = _p(ln.weight), _p(ln.bias), float(ln.eps)
+        d.tokens_per_batch, d.text_len = tokens_per_batch, text_len
+        if rope is not None:
+            cos, sin = rope
+            _chk(cos, "cos", torch.float32)
+            _chk(sin, "sin", torch.float32)
+            if (cos.shape != (tokens_per_batch - text_len, 64) or sin.shape != cos.shape or not cos.is_contiguous()
+                    or not sin.is_contiguous()):
+                raise ValueError(f"rope tables must be fp32 [{tokens_per_batch - text_len}, 64], "
+                                 f"got {tuple(cos.shape)}")
+            d.rope_cos, d.rope_sin = _p(cos), _p(sin)
     if epilogue == N.EPI_BIAS_ADDROWS:
         _chk(addrows, "addrows")
         d.addrows, d.addrows_ld, d.addrows_offset = _p(addrows), _rowmajor(addrows, "addrows"), addrows_offset
