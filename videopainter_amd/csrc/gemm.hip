@@ -172,8 +172,52 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
   constexpr int FN = FN_, FM = FM_, WN = WN_, WM = WM_;
   // ---- epilogue phase 1: per-fragment bias / activation, bf16 into the LDS C image ----
   const int epi = d.epilogue;
+  // fused QKV (VP_EPI_BIAS_QKNORM_ROPE): a wave's 64-column block (WN % 64 == 0, n0 % 256 == 0) is whole heads, 4
+  // fragments each; q / k heads go through norm + RoPE here in registers (ln64_rope16: lane xor 16 / 32 are the
+  // other column quarters of the same row), v heads take the plain path below
+  static_assert(FN % 4 == 0 && WN % 64 == 0, "whole heads per wave");
+  bool head_done[FN / 4] = {};
+  if (epi == VP_EPI_BIAS_QKNORM_ROPE) {
+#pragma unroll
+    for (int hh = 0; hh < FN / 4; ++hh) {
+      const int nh = n0 + wc * WN + hh * 64;  // first column of the head
+      const int sg = nh / d.n_seg;
+      if (nh >= d.N || sg >= 2) continue;
+      head_done[hh] = true;
+      const int g = lane >> 4;
+      const bf16* bp = (const bf16*)d.bias[sg];
+      const int hc = nh - sg * d.n_seg;  // column within the segment
+      float bv[16];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[4 * jj + r] = bp != nullptr ? bf2f(bp[hc + 16 * jj + 4 * g + r]) : 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int mloc = wr * WM + i * 16 + (lane & 15);
+        const int tok = (m0 + mloc) % d.tokens_per_batch;
+        const bool rot = d.rope_cos != nullptr && tok >= d.text_len;
+        const int64_t ro = (int64_t)(tok - d.text_len) * 64;
+        float x[16];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x[4 * jj + r] = rbf(acc[hh * 4 + jj][i][r] + bv[4 * jj + r]);
+        ln64_rope16<16, 32>(x, g, (const bf16*)d.qk_ln_w[sg], (const bf16*)d.qk_ln_b[sg], d.qk_eps[sg],
+                            rot ? d.rope_cos + ro : nullptr, rot ? d.rope_sin + ro : nullptr);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = f2bf(x[4 * jj + r]);
+          *(bf16x4*)(smem + mloc * CT_STRIDE + (wc * WN + (hh * 4 + jj) * 16 + g * 4) * 2) = o;
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
+    if (head_done[j / 4]) continue;
     const int nloc = wc * WN + j * 16 + (lane >> 4) * 4;  // 4 consecutive columns
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -243,21 +287,6 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
         float o = rbf(bf2f(rv[e]) + rbf(bf2f(gv[e]) * bf2f(v[e])));
         if (inj) o = rbf(o + bf2f(iv[e]));
         v[e] = f2bf(o);
-      }
-    } else if (epi == VP_EPI_BIAS_QKNORM_ROPE) {
-      // the 8 lanes of a 64-column head are consecutive (chunk & 7) and row-uniform; n0 and n_seg are multiples of 64
-      const int sg = ncol / d.n_seg;
-      if (sg < 2) {
-        float f[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = bf2f(v[e]);
-        const int tok = m % d.tokens_per_batch;
-        const bool rot = d.rope_cos != nullptr && tok >= d.text_len;
-        const int64_t ro = (int64_t)(tok - d.text_len) * 64;
-        ln64_rope8(f, chunk & 7, (const bf16*)d.qk_ln_w[sg], (const bf16*)d.qk_ln_b[sg], d.qk_eps[sg],
-                   rot ? d.rope_cos + ro : nullptr, rot ? d.rope_sin + ro : nullptr);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = f2bf(f[e]);
       }
     } else if (epi == VP_EPI_BIAS_ADDROWS) {
       const bf16x8 pv = *(const bf16x8*)((const bf16*)d.addrows +

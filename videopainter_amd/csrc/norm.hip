@@ -149,8 +149,9 @@ __global__ __launch_bounds__(ROW_THREADS) void final_norm_kernel(const bf16* __r
 }
 
 // ---- per-head LN(64) + RoPE (attention_processor.py:2143-2154; embeddings.py:655-701) ----
-// 8 lanes per 64-wide head vector (8 elements each); 32 vectors per 256-thread block.  FP8: the bf16 value the
-// bf16 kernel writes, times out_mul, as e4m3 (strides then in bytes)
+// 4 lanes per 64-wide head vector, 16 elements each in the MFMA-accumulator column order of ln64_rope16 (lane g
+// holds columns 16 j + 4 g + r: four 8-byte pieces), 64 vectors per 256-thread block — the arithmetic of the QKV
+// GEMM's fused epilogue.  FP8: the bf16 value the bf16 kernel writes, times out_mul, as e4m3 (strides then in bytes)
 template <bool FP8>
 __global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restrict__ xin, int64_t ld_in,
                                                             int64_t bs_in, void* __restrict__ xout, int64_t ld_out,
@@ -161,38 +162,49 @@ __global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restr
                                                             const float* __restrict__ sinp,
                                                             const uint8_t* __restrict__ tok_mask, int64_t mask_bs,
                                                             float pre_scale, float out_mul) {
-  const int64_t vec = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
-  const int sub = threadIdx.x & 7;
+  const int64_t vec = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+  const int g = threadIdx.x & 3;
   const bool valid = vec < nvec;
   const int64_t vv = valid ? vec : nvec - 1;
   const int h = (int)(vv % H);
   const int64_t bn = vv / H;
   const int n = (int)(bn % Ntok);
   const int b = (int)(bn / Ntok);
-  const bf16x8 xr = *(const bf16x8*)(xin + (int64_t)b * bs_in + (int64_t)n * ld_in + h * 64 + sub * 8);
-  float x[8];
+  const bf16* src = xin + (int64_t)b * bs_in + (int64_t)n * ld_in + h * 64 + g * 4;
   float m = 1.f;
   if (tok_mask != nullptr) m = tok_mask[(int64_t)b * mask_bs + n] ? 1.f : 0.f;
+  float x[16];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    float t = bf2f(xr[e]);
-    if (tok_mask != nullptr) t = rbf(rbf(t * m) * pre_scale);
-    x[e] = t;
+  for (int j = 0; j < 4; ++j) {
+    const bf16x4 xr = *(const bf16x4*)(src + 16 * j);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float t = bf2f(xr[r]);
+      if (tok_mask != nullptr) t = rbf(rbf(t * m) * pre_scale);
+      x[4 * j + r] = t;
+    }
   }
   const bool rot = cosp != nullptr && n >= text_len;
-  ln64_rope8(x, sub, lw, lb, eps, rot ? cosp + (int64_t)(n - text_len) * 64 : nullptr,
-             rot ? sinp + (int64_t)(n - text_len) * 64 : nullptr);
+  ln64_rope16<1, 2>(x, g, lw, lb, eps, rot ? cosp + (int64_t)(n - text_len) * 64 : nullptr,
+                    rot ? sinp + (int64_t)(n - text_len) * 64 : nullptr);
   if (valid) {
-    if constexpr (FP8) {
-      float y[8];
+    const int64_t o = (int64_t)b * bs_out + (int64_t)n * ld_out + h * 64 + g * 4;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) y[e] = rbf(x[e]);
-      *(u32x2*)((uint8_t*)xout + (int64_t)b * bs_out + (int64_t)n * ld_out + h * 64 + sub * 8) = mx_pack8(y, out_mul);
-    } else {
-      bf16x8 o;
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (FP8) {
+        int w = 0;
+        float y[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(x[e]);
-      *(bf16x8*)((bf16*)xout + (int64_t)b * bs_out + (int64_t)n * ld_out + h * 64 + sub * 8) = o;
+        for (int r = 0; r < 4; ++r) y[r] = __builtin_amdgcn_fmed3f(rbf(x[4 * j + r]) * out_mul, 448.f, -448.f);
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(y[0], y[1], w, false);
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(y[2], y[3], w, true);
+        *(uint32_t*)((uint8_t*)xout + o + 16 * j) = (uint32_t)w;
+      } else {
+        bf16x4 ov;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ov[r] = f2bf(x[4 * j + r]);
+        *(bf16x4*)((bf16*)xout + o + 16 * j) = ov;
+      }
     }
   }
 }
@@ -272,7 +284,7 @@ extern "C" int vp_head_norm_rope_bf16(const void* x_in, int64_t ld_in, int64_t b
   if ((ld_in % 8) || (ld_out % 8) || (bs_in % 8) || (bs_out % 8)) return VP_ERR_ARG;
   if ((cos == nullptr) != (sin == nullptr)) return VP_ERR_ARG;
   const int64_t nvec = (int64_t)B * Ntok * H;
-  const int64_t grid = (nvec + 31) / 32;
+  const int64_t grid = (nvec + 63) / 64;
   hipLaunchKernelGGL(head_norm_rope_kernel<false>, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
                      (const bf16*)x_in, ld_in, bs_in, x_out, ld_out, bs_out, nvec, Ntok, H, text_len,
                      (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, tok_mask, mask_bstride, pre_scale, 1.f);
@@ -288,7 +300,7 @@ extern "C" int vp_head_norm_rope_fp8(const void* x_in, int64_t ld_in, int64_t bs
   if ((ld_in % 8) || (bs_in % 8) || (ld_out % 8) || (bs_out % 8)) return VP_ERR_ARG;
   if ((cos == nullptr) != (sin == nullptr) || !(out_mul > 0.f)) return VP_ERR_ARG;
   const int64_t nvec = (int64_t)B * Ntok * H;
-  const int64_t grid = (nvec + 31) / 32;
+  const int64_t grid = (nvec + 63) / 64;
   hipLaunchKernelGGL(head_norm_rope_kernel<true>, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
                      (const bf16*)x_in, ld_in, bs_in, q_out, ld_out, bs_out, nvec, Ntok, H, text_len,
                      (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, nullptr, 0, 1.f, out_mul);

@@ -36,48 +36,51 @@ VP_DEV float gelu_tanh(float x) {
 
 VP_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
 
-// norm_q / norm_k + apply_rotary_emb on one 64-wide head held as 8 consecutive values by each of 8 consecutive lanes
-// (sub = the lane's eighth; the 8 lanes are active together): LayerNorm(64) in fp32 from the bf16 inputs (two-pass
-// mean / centred variance, rstd = rsqrt(var + eps)), bf16 output (torch LayerNorm on bf16,
+// norm_q / norm_k + apply_rotary_emb on one 64-wide head spread over 4 lanes (g = the lane's quarter, partners at
+// lane xor X1 and xor X2; the 4 lanes are active together), 16 values each: x[4 j + r] is column 16 j + 4 g + r —
+// the layout of a 16x16 MFMA accumulator row (4 consecutive columns per lane, 4 fragments per head), so the QKV
+// GEMM applies it to its accumulators (X1, X2 = 16, 32) and vp_head_norm_rope_* to loaded rows (X1, X2 = 1, 2)
+// with the same arithmetic in the same order: bit-equal.  LayerNorm(64) in fp32 from the bf16 inputs (two-pass mean
+// / centred variance, rstd = rsqrt(var + eps)), bf16 output (torch LayerNorm on bf16,
 // attention_processor.py:2143-2154), then when cr / sr are given (video tokens) the interleaved-pair rotation in
-// fp32 of the bf16 values, x * cos + rot(x) * sin (embeddings.py:655-701, apply_rotary_emb).  Shared by
-// vp_head_norm_rope_* and the QKV GEMM's fused epilogue so the two are bit-equal.
-VP_DEV void ln64_rope8(float (&x)[8], int sub, const bf16* __restrict__ lw, const bf16* __restrict__ lb, float eps,
-                       const float* __restrict__ cr, const float* __restrict__ sr) {
+// fp32 of the bf16 values, x * cos + rot(x) * sin (embeddings.py:655-701, apply_rotary_emb).
+template <int X1, int X2>
+VP_DEV void ln64_rope16(float (&x)[16], int g, const bf16* __restrict__ lw, const bf16* __restrict__ lb, float eps,
+                        const float* __restrict__ cr, const float* __restrict__ sr) {
+  // every multiply-add spelled out (fma or not) and no contraction: otherwise hipcc fuses differently in different
+  // surroundings (SLP-packed v_pk_mul + v_add in one kernel, v_fmac in another) and the two users drift by an ulp
+#pragma clang fp contract(off)
   float s = 0.f;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) s += x[e];
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  s += __shfl_xor(s, 4, 64);
+  for (int e = 0; e < 16; ++e) s += x[e];
+  s += __shfl_xor(s, X1, 64);
+  s += __shfl_xor(s, X2, 64);
   const float mean = s * (1.f / 64.f);
   float q = 0.f;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
+  for (int e = 0; e < 16; ++e) {
     const float t = x[e] - mean;
-    q += t * t;
+    q = __builtin_fmaf(t, t, q);
   }
-  q += __shfl_xor(q, 1, 64);
-  q += __shfl_xor(q, 2, 64);
-  q += __shfl_xor(q, 4, 64);
-  const float rstd = rsqrtf(q * (1.f / 64.f) + eps);
-  const bf16x8 w = *(const bf16x8*)(lw + sub * 8);
-  const bf16x8 bb = *(const bf16x8*)(lb + sub * 8);
+  q += __shfl_xor(q, X1, 64);
+  q += __shfl_xor(q, X2, 64);
+  const float rstd = rsqrtf(__builtin_fmaf(q, 1.f / 64.f, eps));
 #pragma unroll
-  for (int e = 0; e < 8; ++e) x[e] = rbf((x[e] - mean) * rstd * bf2f(w[e]) + bf2f(bb[e]));
-  if (cr != nullptr) {
-    const f32x4 c0 = *(const f32x4*)(cr + sub * 8), c1 = *(const f32x4*)(cr + sub * 8 + 4);
-    const f32x4 s0 = *(const f32x4*)(sr + sub * 8), s1 = *(const f32x4*)(sr + sub * 8 + 4);
-    const float cs[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-    const float sn[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-    float y[8];
+  for (int j = 0; j < 4; ++j) {
+    const int c = 16 * j + 4 * g;
+    const bf16x4 w = *(const bf16x4*)(lw + c);
+    const bf16x4 bb = *(const bf16x4*)(lb + c);
 #pragma unroll
-    for (int e = 0; e < 8; e += 2) {
-      y[e] = x[e] * cs[e] + (-x[e + 1]) * sn[e];
-      y[e + 1] = x[e + 1] * cs[e + 1] + x[e] * sn[e + 1];
+    for (int r = 0; r < 4; ++r)
+      x[4 * j + r] = rbf(__builtin_fmaf((x[4 * j + r] - mean) * rstd, bf2f(w[r]), bf2f(bb[r])));
+    if (cr != nullptr) {
+      const f32x4 cs = *(const f32x4*)(cr + c), sn = *(const f32x4*)(sr + c);
+      const float x0 = x[4 * j], x1 = x[4 * j + 1], x2 = x[4 * j + 2], x3 = x[4 * j + 3];
+      x[4 * j] = __builtin_fmaf(x0, cs[0], -(x1 * sn[0]));
+      x[4 * j + 1] = __builtin_fmaf(x1, cs[1], x0 * sn[1]);
+      x[4 * j + 2] = __builtin_fmaf(x2, cs[2], -(x3 * sn[2]));
+      x[4 * j + 3] = __builtin_fmaf(x3, cs[3], x2 * sn[3]);
     }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) x[e] = y[e];
   }
 }
 
