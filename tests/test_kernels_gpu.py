@@ -17,7 +17,7 @@ def _lib():
     _native.lib()
 
 
-@pytest.fixture(params=["5", "6", "7", "1"], ids=["gemm_v5", "gemm_v6", "gemm_v7", "gemm_v1"])
+@pytest.fixture(params=["10", "5", "6", "7", "1"], ids=["gemm_v10", "gemm_v5", "gemm_v6", "gemm_v7", "gemm_v1"])
 def gemm_variant(request, monkeypatch):
     monkeypatch.setenv("VP_GEMM_VARIANT", request.param)
     return request.param
@@ -310,6 +310,55 @@ def test_gemm_qknorm_rope_epilogue_matches_separate_kernels(H, T, rope, gemm_var
         if rope:
             n[:, :, T:] = apply_rotary_emb(n[:, :, T:], cos, sin)
         assert rel(got.view(B, Ntok, 3 * D)[..., s * D:(s + 1) * D], n.transpose(1, 2).reshape(B, Ntok, D)) < 8e-3
+
+
+@pytest.mark.parametrize("Kk", [64, 192, 320, 3072])
+def test_gemm_persistent_matches_per_tile_kernel(Kk, monkeypatch):
+    """Variant 10 (persistent workgroups, the next tile's first K-tile loading during the split epilogue) gives the
+    per-tile quadrant pipeline's (variant 5) result bit for bit for every epilogue kind — same MFMA order — with
+    several tiles per workgroup, ragged M, nk = 1 / 3 / 5 / 48 K-tiles, the row remap and the injection."""
+    from types import SimpleNamespace
+
+    from videopainter_amd import _native as N
+    from videopainter_amd import kernels as K
+    B, T, Nv, H = 2, 37, 1263, 4
+    Ntok, D = T + Nv, H * 64  # M = 2600: 11 row tiles (ragged); 3 segments of 256 -> 33 tiles, nwg 32
+    a = bf(rnd(B * Ntok, Kk, seed=120)).to(dev)
+    ws = [bf(rnd(D, Kk, std=Kk ** -0.5, seed=121 + i)).to(dev) for i in range(3)]
+    bs = [bf(rnd(D, std=0.1, seed=124 + i)).to(dev) for i in range(3)]
+    resid = bf(rnd(B, Ntok, D, seed=127)).to(dev)
+    mod = bf(rnd(B, 6 * D, seed=128)).to(dev)
+    inj = bf(rnd(B, Nv, D, seed=129)).to(dev)
+    tm = (torch.rand(B, Nv, generator=torch.Generator().manual_seed(5)) > 0.5).to(torch.uint8).to(dev)
+    pos = bf(rnd(Ntok, D, seed=130)).to(dev)
+    lns = tuple(SimpleNamespace(weight=bf(1 + 0.1 * rnd(64, seed=131 + i)).to(dev),
+                                bias=bf(0.1 * rnd(64, seed=133 + i)).to(dev), eps=1e-6) for i in range(2))
+    cos, sin = rnd(Nv, 64, seed=135).to(dev), rnd(Nv, 64, seed=136).to(dev)
+    cases = {
+        "bias3": lambda out: K.gemm(a, ws, bs, out.view(-1, 3 * D)),
+        "qknorm": lambda out: K.gemm(a, ws, bs, out.view(-1, 3 * D), epilogue=N.EPI_BIAS_QKNORM_ROPE, qk_norm=lns,
+                                     rope=(cos, sin), tokens_per_batch=Ntok, text_len=T),
+        "gelu": lambda out: K.gemm(a, ws[:1], bs[:1], out.view(-1, D), epilogue=N.EPI_BIAS_GELU),
+        "scale": lambda out: K.gemm(a, ws[:1], bs[:1], out.view(-1, D), epilogue=N.EPI_BIAS_SCALE, alpha=0.37),
+        "gated": lambda out: K.gemm(a, ws[:1], bs[:1], out.view(-1, D), epilogue=N.EPI_GATED, resid=resid, mod=mod,
+                                    tokens_per_batch=Ntok, text_len=T, inject=inj, inject_ld=D,
+                                    inject_bstride=Nv * D, inject_mask=tm),
+        "addrows": lambda out: K.gemm(a[:B * Nv], ws[:1], bs[:1], out.view(-1, D), epilogue=N.EPI_BIAS_ADDROWS,
+                                      rows_per_group=Nv, group_stride=Ntok, row_offset=T, addrows=pos,
+                                      addrows_offset=T),
+    }
+    for name, fn in cases.items():
+        width = 3 * D if name in ("bias3", "qknorm") else D
+        outs = []
+        for v in ("5", "10"):
+            monkeypatch.setenv("VP_GEMM_VARIANT", v)
+            o = torch.full((B, Ntok, width), float("nan"), device=dev, dtype=torch.bfloat16)
+            if name == "addrows":
+                o.zero_()
+            fn(o)
+            outs.append(o)
+        assert torch.equal(outs[0], outs[1]), name
+        assert not torch.isnan(outs[1].float()).any(), name
 
 
 def test_linear_small_timestep_patchify_unpatchify_mask():

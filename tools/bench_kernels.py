@@ -33,7 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
-    ap.add_argument("--gemm-variants", default="1,2")
+    ap.add_argument("--gemm-variants", default="10,5")
     ap.add_argument("--variant", default="", help="attention kernel variant(s), e.g. 1 or 1,3")
     ap.add_argument("--variant8", default="", help="fp8 attention kernel variant(s) (VP_ATTN8_VARIANT), e.g. 1,2")
     ap.add_argument("--only", default="", help="attention | attn8 | gemm | mx: run just that kernel (for rocprofv3 "

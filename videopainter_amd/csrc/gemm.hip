@@ -165,28 +165,29 @@ VP_DEV void mfma_mx(f32x4& acc, const i32x8& w, const i32x8& a, int sw, int sa) 
 }
 
 // ---- fused epilogue shared by the GEMM kernels: acc[j][i] = the 16x16 fragment (W rows j, A rows i) of a wave
-// whose C block is rows wr*WM.., cols wc*WN.. of the BM x BN tile; NT threads stream the LDS C image out ----
-template <int NT, int FN_, int FM_, int WN_, int WM_, bool FP8>
-VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&acc)[FN_][FM_], char* smem, int m0,
-                          int n0, int wr, int wc, int lane, int tid) {
-  constexpr int FN = FN_, FM = FM_, WN = WN_, WM = WM_;
-  // ---- epilogue phase 1: per-fragment bias / activation, bf16 into the LDS C image ----
-  const int epi = d.epilogue;
-  // fused QKV (VP_EPI_BIAS_QKNORM_ROPE): a wave's 64-column block (WN % 64 == 0, n0 % 256 == 0) is whole heads, 4
-  // fragments each; q / k heads go through norm + RoPE here in registers (ln64_rope16: lane xor 16 / 32 are the
-  // other column quarters of the same row), v heads take the plain path below
+// whose C block is rows wr*WM.., cols wc*WN.. of the BM x BN tile.  Three pieces: epi_values (per-fragment bias /
+// activation / qk-norm in registers -> bf16), epi_to_lds (a wave's values into the LDS C image), epi_rows_out (NT
+// threads stream image rows out as 16-byte row stores, with the row-wise epilogues: residual / gate / injection /
+// pos-emb / MX).  The persistent kernel runs the last two per half tile so the next tile's first K-tile can load
+// into the other half of the LDS meanwhile. ----
+// EPI >= 0: the epilogue kind as a compile-time constant (the persistent kernel is instantiated per kind; with the
+// runtime switch its register allocation spills), FULL_N: N % 256 == 0 (no column guard)
+template <int FN, int FM, int WN, int WM, int EPI = -1, bool FULL_N = false, class Sink>
+VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&& sink, int m0, int n0, int wr, int wc,
+                       int lane) {
+  const int epi = EPI >= 0 ? EPI : d.epilogue;
+  // head by head (4 fragments = 64 columns; WN % 64 == 0 and n0 % 256 == 0), so a head's accumulators die as its
+  // values go to the sink.  Fused QKV (VP_EPI_BIAS_QKNORM_ROPE): q / k heads go through norm + RoPE in registers
+  // (ln64_rope16: lane xor 16 / 32 are the other column quarters of the same row); v heads take the plain path.
   static_assert(FN % 4 == 0 && WN % 64 == 0, "whole heads per wave");
-  bool head_done[FN / 4] = {};
-  if (epi == VP_EPI_BIAS_QKNORM_ROPE) {
+  const int g = lane >> 4;
 #pragma unroll
-    for (int hh = 0; hh < FN / 4; ++hh) {
-      const int nh = n0 + wc * WN + hh * 64;  // first column of the head
-      const int sg = nh / d.n_seg;
-      if (nh >= d.N || sg >= 2) continue;
-      head_done[hh] = true;
-      const int g = lane >> 4;
-      const bf16* bp = (const bf16*)d.bias[sg];
-      const int hc = nh - sg * d.n_seg;  // column within the segment
+  for (int hh = 0; hh < FN / 4; ++hh) {
+    const int nh = n0 + wc * WN + hh * 64;  // first column of the head
+    const int sgh = nh / d.n_seg;
+    if (epi == VP_EPI_BIAS_QKNORM_ROPE && nh < d.N && sgh < 2) {
+      const bf16* bp = (const bf16*)d.bias[sgh];
+      const int hc = nh - sgh * d.n_seg;  // column within the segment
       float bv[16];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
@@ -194,8 +195,7 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
         for (int r = 0; r < 4; ++r) bv[4 * jj + r] = bp != nullptr ? bf2f(bp[hc + 16 * jj + 4 * g + r]) : 0.f;
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int mloc = wr * WM + i * 16 + (lane & 15);
-        const int tok = (m0 + mloc) % d.tokens_per_batch;
+        const int tok = (m0 + wr * WM + i * 16 + (lane & 15)) % d.tokens_per_batch;
         const bool rot = d.rope_cos != nullptr && tok >= d.text_len;
         const int64_t ro = (int64_t)(tok - d.text_len) * 64;
         float x[16];
@@ -203,56 +203,66 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
         for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
           for (int r = 0; r < 4; ++r) x[4 * jj + r] = rbf(acc[hh * 4 + jj][i][r] + bv[4 * jj + r]);
-        ln64_rope16<16, 32>(x, g, (const bf16*)d.qk_ln_w[sg], (const bf16*)d.qk_ln_b[sg], d.qk_eps[sg],
+        ln64_rope16<16, 32>(x, g, (const bf16*)d.qk_ln_w[sgh], (const bf16*)d.qk_ln_b[sgh], d.qk_eps[sgh],
                             rot ? d.rope_cos + ro : nullptr, rot ? d.rope_sin + ro : nullptr);
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           bf16x4 o;
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = f2bf(x[4 * jj + r]);
-          *(bf16x4*)(smem + mloc * CT_STRIDE + (wc * WN + (hh * 4 + jj) * 16 + g * 4) * 2) = o;
+          sink(hh * 4 + jj, i, o);
         }
       }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    if (head_done[j / 4]) continue;
-    const int nloc = wc * WN + j * 16 + (lane >> 4) * 4;  // 4 consecutive columns
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + nloc + r;
-      if (n < d.N) {
-        const int sg = n / d.n_seg;
-        const bf16* bp = (const bf16*)d.bias[sg];
-        if (bp != nullptr) bv[r] = bf2f(bp[n - sg * d.n_seg]);
-      }
+      continue;
     }
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int mloc = wr * WM + i * 16 + (lane & 15);
-      bf16x4 o;
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = hh * 4 + jj;
+      const int nloc = wc * WN + j * 16 + g * 4;  // 4 consecutive columns
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = rbf(acc[j][i][r] + bv[r]);
-        if (epi == VP_EPI_BIAS_GELU || epi == VP_EPI_BIAS_GELU_MXFP8) v = gelu_tanh(v);
-        else if (epi == VP_EPI_BIAS_SCALE) v = v * d.alpha;
-        o[r] = f2bf(v);
+        const int n = n0 + nloc + r;
+        if (FULL_N || n < d.N) {
+          const int sg = n / d.n_seg;
+          const bf16* bp = (const bf16*)d.bias[sg];
+          if (bp != nullptr) bv[r] = bf2f(bp[n - sg * d.n_seg]);
+        }
       }
-      *(bf16x4*)(smem + mloc * CT_STRIDE + nloc * 2) = o;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = rbf(acc[j][i][r] + bv[r]);
+          if (epi == VP_EPI_BIAS_GELU || epi == VP_EPI_BIAS_GELU_MXFP8) v = gelu_tanh(v);
+          else if (epi == VP_EPI_BIAS_SCALE) v = v * d.alpha;
+          o[r] = f2bf(v);
+        }
+        sink(j, i, o);
+      }
     }
   }
-  __syncthreads();
+}
 
-  // ---- epilogue phase 2: coalesced 16-byte row stores (+ residual / gate / injection / pos-emb) ----
+// the LDS C image address of fragment (j, i)'s 4 values for this lane (image row = tile row - row0)
+template <int WN, int WM>
+VP_DEV char* epi_lds_addr(char* img, int j, int i, int row0, int wr, int wc, int lane) {
+  return img + (wr * WM + i * 16 + (lane & 15) - row0) * CT_STRIDE + (wc * WN + j * 16 + (lane >> 4) * 4) * 2;
+}
+
+// image rows [0, nrows) = tile rows row0.. out to C (coalesced 16-byte row stores + the row-wise epilogues)
+template <int NT, bool FP8, int EPI = -1>
+VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* smem, int row0, int nrows, int m0,
+                         int n0, int tid) {
+  const int epi = EPI >= 0 ? EPI : d.epilogue;
   bf16* C = (bf16*)d.C;
   const int chunk = tid & 31;         // 16-byte chunk within the 512-byte tile row
   const int ncol = n0 + chunk * 8;
 #pragma unroll 1
-  for (int it = 0; it < BM / (NT / 32); ++it) {
+  for (int it = 0; it < nrows / (NT / 32); ++it) {
     const int mloc = it * (NT / 32) + (tid >> 5);
-    const int m = m0 + mloc;
+    const int m = m0 + row0 + mloc;
     if (m >= d.M || ncol >= d.N) continue;
     bf16x8 v = *(const bf16x8*)(smem + mloc * CT_STRIDE + chunk * 16);
     const int64_t orow = (int64_t)(m / d.rows_per_group) * d.group_stride + d.row_offset + (m % d.rows_per_group);
@@ -296,6 +306,18 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
     }
     *(bf16x8*)(C + orow * d.ldc + ncol) = v;
   }
+}
+
+
+template <int NT, int FN, int FM, int WN, int WM, bool FP8>
+VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&acc)[FN][FM], char* smem, int m0,
+                          int n0, int wr, int wc, int lane, int tid) {
+  epi_values<FN, FM, WN, WM>(
+      d, acc,
+      [&](int j, int i, const bf16x4& o) { *(bf16x4*)epi_lds_addr<WN, WM>(smem, j, i, 0, wr, wc, lane) = o; }, m0,
+      n0, wr, wc, lane);
+  __syncthreads();
+  epi_rows_out<NT, FP8>(d, mx, smem, 0, BM, m0, n0, tid);
 }
 
 template <int VAR, bool FP8 = false, int GROUP = 4>
@@ -797,6 +819,228 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 }
 
 
+// ---- variant 10: the quadrant-phase pipeline (variant 5, bf16) as a PERSISTENT kernel ----
+// One workgroup per CU walks the tiles of its XCD's contiguous range (the grouped order of variant 5, so the 32
+// CUs of an XCD work on neighbouring tiles in lock step and share A / W panels in their L2).  What it removes is
+// the per-tile fixed cost of a one-tile workgroup (measured: ~13.6 us per 256x256 tile = 16 % at K = 3072 — every
+// CU stores its C tile and then loads the next tile's first K-tiles at the same moment, HBM-bound bursts, plus the
+// workgroup launch): here the next tile's first K-tile (4 units = LDS stage 0) is issued BEFORE the epilogue, whose
+// C image then goes through the other half of the LDS one 128-row half at a time; the next tile's second K-tile
+// follows the epilogue.  Waits: the first wait of a tile is vmcnt(8) (only the second K-tile's 8 LDS-DMAs may still
+// be in flight: loads complete in order, so this also holds if the epilogue's stores retire out of order).
+// A/B (tools/blas_calibration.py, interleaved): no gain over variant 5 (QKV / out / FF2 within +-2 %, FF1 with its
+// GELU epilogue -5 %): the per-tile cost it overlaps is small; kept as VP_GEMM_VARIANT=10, bit-equal to variant 5.
+template <int EPI>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_persist_kernel(const vp_gemm_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2;  // 0..1  (M)
+  const int wc = wave & 3;   // 0..3  (N)
+  constexpr int GROUP = 4;
+  const int tiles_m = (d.M + BM - 1) / BM;
+  const int tiles_n = (d.N + BN - 1) / BN;
+  const int T = tiles_m * tiles_n;
+  // this workgroup's tiles: XCD x (= blockIdx % 8) owns the contiguous logical range [xs, xs + xn); its
+  // nwg / 8 workgroups take every (nwg / 8)-th tile of it (the launcher makes nwg a multiple of 8)
+  const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8, per_xcd = gridDim.x / 8;
+  const int q8 = T / 8, r8 = T % 8;
+  const int xs = xcd * q8 + min(xcd, r8), xn = q8 + (xcd < r8 ? 1 : 0);
+  auto tile_mn = [&](int it, int& m0, int& n0) {
+    const int t = xs + it;
+    const int per_group = GROUP * tiles_n;
+    const int first_m = (t / per_group) * GROUP;
+    const int gsz = min(tiles_m - first_m, GROUP);
+    m0 = (first_m + ((t % per_group) % gsz)) * BM;
+    n0 = ((t % per_group) / gsz) * BN;
+  };
+  const int nk = d.K / BK;  // the launcher guarantees K % 64 == 0
+  // per-lane 32-bit source offsets of the 4 units (2 LDS-DMA instructions each) from wave-uniform bases
+  int uoff[4][2];
+  const char* ubase[4][2];
+  auto setup = [&](int m0, int n0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int g = i * 8 + wave;
+        const int rb = (u < 2) ? (g >> 3) * 128 + u * 64 + (g & 7) * 8 : (g >> 2) * 64 + (u - 2) * 32 + (g & 3) * 8;
+        const int r = rb + (lane >> 3);
+        const int c = (lane & 7) ^ swz(r);
+        if (u < 2) {
+          ubase[u][i] = (const char*)d.A + (int64_t)m0 * d.lda * 2;
+          uoff[u][i] = (min(m0 + r, d.M - 1) - m0) * (int)d.lda * 2 + c * 16;
+        } else {
+          const int sg = __builtin_amdgcn_readfirstlane(min(n0 + rb, d.N - 1) / d.n_seg);
+          ubase[u][i] = (const char*)d.W[sg];
+          uoff[u][i] = ((min(n0 + r, d.N - 1) - sg * d.n_seg) * d.K) * 2 + c * 16;
+        }
+      }
+  };
+  auto issue_unit = [&](int u, int tile) {
+    char* base = smem + (tile & 1) * STAGE_BYTES + (u >= 2 ? TILE_BYTES : 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int g = i * 8 + wave;
+      const int rb = (u < 2) ? (g >> 3) * 128 + u * 64 + (g & 7) * 8 : (g >> 2) * 64 + (u - 2) * 32 + (g & 3) * 8;
+      glds16(ubase[u][i] + tile * 128, uoff[u][i], base + rb * 128);
+    }
+  };
+  auto slot_tile = [&](int sl, int& u) -> int {  // unit and K-tile issued by slot sl (sl >= -9)
+    const int k = (sl + 12) / 4 - 3;
+    const int p = sl - 4 * k;
+    u = p == 0 ? 2 : p == 1 ? 3 : p == 2 ? 1 : 0;
+    return p < 3 ? k + 2 : k + 3;
+  };
+  auto exists = [&](int sl) {
+    int u;
+    return slot_tile(sl, u) < nk;
+  };
+  auto issue_slot = [&](int sl) {
+    int u;
+    const int tile = slot_tile(sl, u);
+    if (tile < nk) issue_unit(u, tile);
+  };
+  const int lrow = lane & 15;
+  int lbase[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) lbase[ks] = lrow * 128 + (((ks * 4 + (lane >> 4)) ^ swz(lrow)) << 4);
+  auto readA = [&](bf16x8 (&a)[8], auto par_c, auto qm_c) {
+    constexpr int par = decltype(par_c)::value, qm = decltype(qm_c)::value;
+    const char* As = smem + par * STAGE_BYTES + (wr * WM + qm * 64) * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[ks * 4 + i] = *(const bf16x8*)(As + lbase[ks] + i * 16 * 128);
+  };
+  auto readB = [&](bf16x8 (&bb)[4], auto par_c, auto qn_c) {
+    constexpr int par = decltype(par_c)::value, qn = decltype(qn_c)::value;
+    const char* Bs = smem + par * STAGE_BYTES + TILE_BYTES + (wc * WN + qn * 32) * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bb[ks * 2 + j] = *(const bf16x8*)(Bs + lbase[ks] + j * 16 * 128);
+  };
+  f32x4 acc[FN][FM];
+  auto mma = [&](const bf16x8 (&a)[8], const bf16x8 (&bb)[4], auto qm_c, auto qn_c) {
+    constexpr int qm = decltype(qm_c)::value, qn = decltype(qn_c)::value;
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[qn * 2 + j][qm * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[ks * 2 + j], a[ks * 4 + i],
+                                                                               acc[qn * 2 + j][qm * 4 + i], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using Z = std::integral_constant<int, 0>;
+  using O = std::integral_constant<int, 1>;
+  using T_ = std::integral_constant<bool, true>;
+  using F_ = std::integral_constant<bool, false>;
+  bf16x8 a0[8], a1[8], bx[4], by[4];
+
+  int m0 = 0, n0 = 0;
+  if (slot < xn) {
+    tile_mn(slot, m0, n0);
+    setup(m0, n0);
+    for (int sl = -9; sl < -1; ++sl) issue_slot(sl);
+  }
+#pragma unroll 1
+  for (int it = slot; it < xn; it += per_xcd) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (exists(-2)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // the first K-tile (4 units) landed
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    readA(a0, Z{}, Z{});
+    readB(bx, Z{}, Z{});
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_slot(-1);
+    auto tile_body = [&](int k, auto par_c, auto steady_c, bf16x8 (&b0)[4], bf16x8 (&b1)[4]) {
+      using P = decltype(par_c);
+      using NP = std::integral_constant<int, 1 - P::value>;
+      constexpr bool STEADY = decltype(steady_c)::value;
+      const int s0 = 4 * k;
+      auto slotf = [&](int sl) {
+        if (STEADY || exists(sl - 1)) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if constexpr (STEADY) {
+          int u;
+          const int tile = slot_tile(sl, u);
+          issue_unit(u, tile);
+        } else {
+          issue_slot(sl);
+        }
+      };
+      const bool more = STEADY || k + 1 < nk;
+      slotf(s0);
+      readB(b1, P{}, O{});
+      mma(a0, b0, Z{}, Z{});
+      slotf(s0 + 1);
+      readA(a1, P{}, O{});
+      mma(a0, b1, Z{}, O{});
+      slotf(s0 + 2);
+      if (more) readA(a0, NP{}, Z{});
+      mma(a1, b1, O{}, O{});
+      slotf(s0 + 3);
+      if (more) readB(b1, NP{}, Z{});
+      mma(a1, b0, O{}, Z{});
+    };
+    int k = 0;
+    for (; k + 4 < nk; k += 2) {
+      tile_body(k, Z{}, T_{}, bx, by);
+      tile_body(k + 1, O{}, T_{}, by, bx);
+    }
+    if (k < nk) tile_body(k, Z{}, F_{}, bx, by);
+    if (k + 1 < nk) tile_body(k + 1, O{}, F_{}, by, bx);
+    if (k + 2 < nk) tile_body(k + 2, Z{}, F_{}, bx, by);
+    if (k + 3 < nk) tile_body(k + 3, O{}, F_{}, by, bx);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // the ring is free
+
+    // epilogue values in registers, then the next tile's first K-tile into stage 0 while the C image streams out
+    // through [STAGE_BYTES, STAGE_BYTES + 128 * CT_STRIDE) in two 128-row halves
+    bf16x4 pk[FN][FM];
+    epi_values<FN, FM, WN, WM, EPI, true>(d, acc, [&](int j, int i, const bf16x4& o) { pk[j][i] = o; }, m0, n0, wr,
+                                          wc, lane);
+    const int cm0 = m0, cn0 = n0;
+    const bool next = it + per_xcd < xn;
+    if (next) {
+      tile_mn(it + per_xcd, m0, n0);
+      setup(m0, n0);
+      for (int sl = -9; sl < -5; ++sl) issue_slot(sl);
+    }
+    char* img = smem + STAGE_BYTES;
+    const MxExt mx = {};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (wr == h) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < FM; ++i) *(bf16x4*)epi_lds_addr<WN, WM>(img, j, i, h * WM, wr, wc, lane) = pk[j][i];
+      }
+      // LDS-only ordering: __syncthreads() would also wait for the in-flight LDS-DMA (vmcnt(0))
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      epi_rows_out<NTHREADS, false, EPI>(d, mx, img, h * WM, WM, cm0, cn0, tid);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    if (next)
+      for (int sl = -5; sl < -1; ++sl) issue_slot(sl);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Variant 6: 4 waves, ONE per SIMD, 128x128 C block per wave (8x8 16x16x32 fragments = 256 accumulator registers,
 // in the AGPR half of the 512-register file a single wave per SIMD owns).  Same 256x256 tile, BK = 32 half-steps
@@ -910,6 +1154,19 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const vp_gemm_de
 
 }  // namespace
 
+// compute units of the current device (cached per device id)
+static int cu_count() {
+  static int cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   if (d == nullptr || d->A == nullptr || d->W[0] == nullptr || d->C == nullptr) return VP_ERR_ARG;
   if (d->M <= 0 || d->N <= 0 || d->K <= 0 || (d->K % 8) != 0 || (d->N % 8) != 0) return VP_ERR_ARG;
@@ -954,7 +1211,8 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
     attr_set = true;
   }
   const char* e = getenv("VP_GEMM_VARIANT");  // A/B switch for benchmarking main-loop variants
-  int variant = (e != nullptr && e[0] >= '1' && e[0] <= '9') ? e[0] - '0' : 5;
+  int variant = e != nullptr ? atoi(e) : 5;
+  if (variant < 1 || variant > 10) variant = 5;
   // 32-bit in-tile source offsets: the quadrant pipeline adds them to a 64-bit tile base (A) / segment base (W);
   // variant 6 still offsets A from the matrix base
   const bool w32 = (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
@@ -964,6 +1222,55 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
     variant = 1;  // the quadrant pipeline needs whole K-tiles
   if (variant == 6 && ((d->K % HK) != 0 || !off32 || (d->n_seg % 16) != 0)) variant = 1;
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
+  if (variant == 10) {
+    // persistent: one workgroup per CU (a multiple of 8, so every XCD gets the same count), whole 256-column tiles
+    const int ncu = cu_count();
+    const int nwg = (tiles < ncu ? tiles : ncu) & ~7;
+    if ((d->K % BK) != 0 || !tile32 || (d->N % BN) != 0 || nwg < 8) {
+      variant = (d->K % BK) == 0 && tile32 ? 5 : 1;
+    } else {
+      static bool pattr = false;
+      if (!pattr) {
+        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_BIAS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_BIAS_GELU>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_BIAS_SCALE>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_GATED>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_BIAS_ADDROWS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_BIAS_QKNORM_ROPE>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        pattr = true;
+      }
+      const hipStream_t st = (hipStream_t)stream;
+      switch (d->epilogue) {
+        case VP_EPI_BIAS:
+          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_BIAS>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st, *d);
+          break;
+        case VP_EPI_BIAS_GELU:
+          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_BIAS_GELU>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st, *d);
+          break;
+        case VP_EPI_BIAS_SCALE:
+          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_BIAS_SCALE>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st, *d);
+          break;
+        case VP_EPI_GATED:
+          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_GATED>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st, *d);
+          break;
+        case VP_EPI_BIAS_ADDROWS:
+          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_BIAS_ADDROWS>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st, *d);
+          break;
+        default:
+          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_BIAS_QKNORM_ROPE>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st,
+                             *d);
+          break;
+      }
+      VP_CHECK_LAUNCH();
+      return VP_OK;
+    }
+  }
   if (variant == 8)  // v5 with 8 / 2 M-tiles per L2 group instead of 4 (A/B: within noise, FF2 -2 %; 16: -4..7 %)
     hipLaunchKernelGGL((gemm_bf16_kernel<5, false, 8>), dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream,
                        *d, mx);
