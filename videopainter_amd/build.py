@@ -20,7 +20,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # attention: no NaN semantics needed (masked scores are -inf, never NaN); without this hipcc inserts a
 # canonicalising v_max before every fmaxf of an MFMA result (cdna_hip_programming.md, attention pitfalls)
-PER_FILE_FLAGS = {"attention.hip": ["-fno-honor-nans", "-Wno-inline-asm"], "gemm.hip": ["-Wno-inline-asm"]}
+# attention: -fno-slp-vectorize keeps the softmax row sums as single f32 adds — the SLP pass packs them into
+# v_pk_add_f32, which costs more issue cycles beside MFMAs (MI355X_MICROARCH.md cycle constants): measured
+# 1.07 -> 1.13 PF/s at config 2 (tools/ab_run.sh).  The GEMM keeps SLP (no gain there: the epilogue is not under MFMA).
+PER_FILE_FLAGS = {"attention.hip": ["-fno-honor-nans", "-Wno-inline-asm", "-fno-slp-vectorize"],
+                  "gemm.hip": ["-Wno-inline-asm"]}
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-result",
           "-Wno-unused-function", "-munsafe-fp-atomics"]
 
@@ -40,17 +44,19 @@ def _digest() -> str:
     return h.hexdigest()
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    os.makedirs(LIBDIR, exist_ok=True)
-    stamp = os.path.join(LIBDIR, "libvp_hip.sha256")
-    dg = _digest()
-    if not force and os.path.exists(LIB) and os.path.exists(stamp) and open(stamp).read().strip() == dg:
-        return LIB
+def build(force: bool = False, verbose: bool = True, out: str = LIB, extra_flags=None) -> str:
+    """out / extra_flags ({file: [flags]}) build an A/B copy of the library (VP_HIP_LIB selects it at load time)."""
+    libdir = os.path.dirname(out)
+    os.makedirs(libdir, exist_ok=True)
+    stamp = os.path.join(libdir, os.path.basename(out).replace(".so", ".sha256"))
+    dg = _digest() + repr(sorted((extra_flags or {}).items()))
+    if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read().strip() == dg:
+        return out
     objs = []
 
     def cc(src):
-        obj = os.path.join(LIBDIR, os.path.basename(src).replace(".hip", ".o"))
-        extra = PER_FILE_FLAGS.get(os.path.basename(src), [])
+        obj = os.path.join(libdir, os.path.basename(src).replace(".hip", ".o"))
+        extra = PER_FILE_FLAGS.get(os.path.basename(src), []) + (extra_flags or {}).get(os.path.basename(src), [])
         cmd = [HIPCC, *CFLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
@@ -60,20 +66,29 @@ def build(force: bool = False, verbose: bool = True) -> str:
     jobs = max(1, min(len(_sources()), int(os.environ.get("MAX_JOBS", "8"))))
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(cc, _sources()))
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], capture_output=True,
                        text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, LIB)
+    os.replace(tmp, out)
     for o in objs:
         os.remove(o)
     with open(stamp, "w") as f:
         f.write(dg)
     if verbose:
-        print(f"[videopainter_amd] built {LIB}")
-    return LIB
+        print(f"[videopainter_amd] built {out}")
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    # python -m videopainter_amd.build [--force] [--out PATH] [--extra FILE:FLAG ...]
+    args = sys.argv[1:]
+    o, ex = LIB, {}
+    for i, a in enumerate(args):
+        if a == "--out":
+            o = os.path.abspath(args[i + 1])
+        if a == "--extra":
+            f, fl = args[i + 1].split(":", 1)
+            ex.setdefault(f, []).append(fl)
+    build(force="--force" in args, out=o, extra_flags=ex)
