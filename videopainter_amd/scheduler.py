@@ -31,7 +31,14 @@ def randn_tensor(shape, generator=None, device=None, dtype=None):
     """DF/utils/torch_utils.py:38-83 for a single (CPU) generator: draw on the generator's device, then move."""
     rand_device = generator.device if generator is not None else (device or "cpu")
     out = torch.randn(shape, generator=generator, device=rand_device, dtype=dtype)
-    return out.to(device) if device is not None else out
+    if device is None or torch.device(device) == out.device:
+        return out
+    if out.device.type == "cpu" and torch.device(device).type == "cuda":
+        # same values, but the host->device copy is queued on the stream from pinned memory instead of a pageable
+        # copy that blocks the host until the GPU has drained the step's forward (the CPU draw then ran while the GPU
+        # idled: ~15 ms per second-order step at config 2, profiles/r01_bench_kernel_trace gap analysis)
+        return out.pin_memory().to(device, non_blocking=True)
+    return out.to(device)
 
 
 def _rbf(x: float) -> float:
