@@ -37,7 +37,7 @@ def _digest() -> str:
     h = hashlib.sha256()
     for p in _sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "vp_hip.h")]:
         with open(p, "rb") as f:
-            h.update(p.encode())
+            h.update(os.path.relpath(p, ROOT).encode())  # relative: the GPU box's checkout path differs
             h.update(f.read())
     h.update(" ".join(CFLAGS).encode())
     h.update(repr(sorted(PER_FILE_FLAGS.items())).encode())
