@@ -26,8 +26,10 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 5
+#define VP_ABI_VERSION 6
 int vp_abi_version(void);
+/* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
+const char* vp_build_digest(void);
 /* sizeof of the descriptor structs as compiled into the library: out[0..4] = gemm, attn, dpm, gemm_mx, attn_fp8
  * (ABI check) */
 void vp_struct_sizes(int64_t* out);
@@ -161,8 +163,14 @@ typedef struct vp_attn_desc {
   void* O;
   int64_t o_sb, o_sn;
   float scale, out_scale;
-  int32_t accumulate, pad;
+  int32_t accumulate;
+  int32_t flags; /* VP_ATTN_BOUNDED_SCORES: the caller guarantees |scale * q.k| * log2(e) <= VP_ATTN_SCORE_BOUND for
+                    every (query, key) pair, so the kernel runs without a running max (exact: bf16/fp32 hold
+                    2^+-60 and O / l is invariant to the reference point).  CogVideoX's qk-LayerNorm gives the bound
+                    from the norm weights: videopainter_amd.kernels.score_bound_log2. */
 } vp_attn_desc;
+#define VP_ATTN_BOUNDED_SCORES 1
+#define VP_ATTN_SCORE_BOUND 60.0f
 
 int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream);
 

@@ -63,8 +63,12 @@ def tiny_inputs(dtype=torch.float32):
                 enc=cv(enc), timestep=torch.tensor([999, 377], dtype=torch.int64), rope=(cos, sin))
 
 
-def full_block_case(seed: int = 0, dtype=torch.float32):
-    """One full-width block (D=3072, 48 heads x 64, temb 512) at config-1 shape: T=226, video 3x16x24 = 1152."""
+def full_block_case(seed: int = 0, dtype=torch.float32, latent=(3, 32, 48), key="fb"):
+    """One full-width block (D=3072, 48 heads x 64, temb 512), B=1, T=226 text rows.  Default: config-1 shape (latent
+    3x32x48 -> video 3x16x24 = 1152 tokens).  `latent=(13, 90, 160), key="fb5"` is config 5 (720x1280: 13x45x80 =
+    46 800 video tokens, N = 47 026)."""
+    f, lh, lw = latent
+    nv = f * (lh // 2) * (lw // 2)
     from videopainter_amd.config import block_shapes
     shapes = block_shapes(3072, 512)
     s2 = {}
@@ -76,10 +80,10 @@ def full_block_case(seed: int = 0, dtype=torch.float32):
         s2[k] = v
     w = synth_state_dict({"FB." + k: v for k, v in s2.items()}, seed)
     w = {k[3:]: v for k, v in w.items()}
-    h = torch.from_numpy(synth_tensor("fb.h", (1, 1152, 3072))).to(dtype)
-    e = torch.from_numpy(synth_tensor("fb.e", (1, 226, 3072))).to(dtype)
-    temb = torch.from_numpy(synth_tensor("fb.temb", (1, 512))).to(dtype)
-    rope = prepare_rotary_positional_embeddings(256, 384, 3, 64)
+    h = torch.from_numpy(synth_tensor(f"{key}.h", (1, nv, 3072))).to(dtype)
+    e = torch.from_numpy(synth_tensor(f"{key}.e", (1, 226, 3072))).to(dtype)
+    temb = torch.from_numpy(synth_tensor(f"{key}.temb", (1, 512))).to(dtype)
+    rope = prepare_rotary_positional_embeddings(lh * 8, lw * 8, f, 64)
     return dict(weights=w, h=h, e=e, temb=temb, rope=rope)
 
 
@@ -125,3 +129,31 @@ def config1_inputs(dtype=torch.float32):
     cv = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dtype)  # noqa: E731
     return dict(hidden=cv(hidden), video=cv(video), mask=cv(mask), branch_cond=cv(branch_cond), enc=cv(enc),
                 timestep=torch.tensor([999, 999], dtype=torch.int64), rope=(cos, sin))
+
+
+# BASELINE config 2 (the headline bench shape) at full size: 49f 480x720 -> latent 13x60x90 (Nv = 17 550,
+# N = 17 776), B = 2 (CFG), the real 5b-I2V config (sample 60x90x49, so the learned pos-emb buffer is used as is);
+# same weight seeds as config 1 / bench.py.  SURVEY.md 8(c)(iv).
+CONFIG2_SEEDS = CONFIG1_SEEDS
+
+
+def config2_cfg():
+    from videopainter_amd.config import COGVIDEOX_5B_I2V
+    cfg = dict(COGVIDEOX_5B_I2V)
+    return cfg, dict(cfg, num_layers=2)
+
+
+def config2_inputs(dtype=torch.float32):
+    b, f, h, w, t = 2, 13, 60, 90, 226
+    video = synth_tensor("c2.video", (b, f, 16, h, w))
+    image = synth_tensor("c2.image", (b, f, 16, h, w)) * np.float32(0.7)
+    image[:, 1:] = 0.0
+    hidden = np.concatenate([video, image], axis=2)
+    mask = make_mask(b, f, h, w, "c2.mask")
+    masked = synth_tensor("c2.masked", (b, f, 16, h, w)) * (1.0 - mask)
+    branch_cond = np.concatenate([masked, mask], axis=2)
+    enc = synth_tensor("c2.enc", (b, t, 4096))
+    cos, sin = prepare_rotary_positional_embeddings(h * 8, w * 8, f, 64)
+    cv = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dtype)  # noqa: E731
+    return dict(hidden=cv(hidden), video=cv(video), mask=cv(mask), branch_cond=cv(branch_cond), enc=cv(enc),
+                timestep=torch.tensor([499, 499], dtype=torch.int64), rope=(cos, sin))

@@ -17,6 +17,10 @@ Fixtures (all fp32):
                           it drew (captured) and the final latents.
   block_full.safetensors— one full-width CogVideoXBlock (3072 = 48 x 64) at N = 226 + 1152 (config-1 shape), B=1:
                           strided slice + digest of the output.
+  config2.safetensors   — the same at the HEADLINE shape (BASELINE config 2: 49f 480x720, N = 17 776, B = 2), SURVEY
+                          8(c)(iv): noise-prediction slice in fp32 and in the reference's own bf16 run, digest, branch
+                          slices, bf16 drift.
+  block5.safetensors    — one full-width block at config-5 length (720x1280: N = 47 026), fp32 + bf16 slices.
   config1.safetensors   — the WHOLE 5b-I2V-shaped transformer (42 layers) + 2-layer branch at config-1 shape, B=2:
                           noise prediction in fp32 (strided slice + digest) and the reference's own bf16 run's
                           rel-L2 from it (the tolerance band); weights from the counter generator (plain names,
@@ -255,20 +259,20 @@ def _fill_synthetic(model, seed):
 
 
 @torch.no_grad()
-def make_config1():
+def _make_full_model(tag, cfg_fn, inputs_fn, seeds, out_stride):
+    """The reference's whole 42-layer transformer + 2-layer branch, fp32 then bf16, on the counter weights."""
     import time
     from diffusers.models.transformers.cogvideox_transformer_3d import CogVideoXTransformer3DModel
     from diffusers.models.branch_cogvideox import CogvideoXBranchModel
-    from tests.golden.cases import config1_cfg, config1_inputs, CONFIG1_SEEDS
-    tcfg, bcfg = config1_cfg()
+    tcfg, bcfg = cfg_fn()
     t0 = time.time()
     with torch.device("meta"):
         tr = CogVideoXTransformer3DModel(**tcfg).eval()
         br = CogvideoXBranchModel(**bcfg).eval()
-    tr = _fill_synthetic(tr, CONFIG1_SEEDS[0])
-    br = _fill_synthetic(br, CONFIG1_SEEDS[1])
-    print(f"weights {time.time() - t0:.0f}s", flush=True)
-    inp = config1_inputs()
+    tr = _fill_synthetic(tr, seeds[0])
+    br = _fill_synthetic(br, seeds[1])
+    print(f"{tag}: weights {time.time() - t0:.0f}s", flush=True)
+    inp = inputs_fn()
 
     def fwd(dt):
         c = lambda x: x.to(dt)  # noqa: E731
@@ -281,26 +285,75 @@ def make_config1():
 
     t0 = time.time()
     o32, bs32 = fwd(torch.float32)
-    print(f"fp32 forward {time.time() - t0:.0f}s", flush=True)
+    t32 = time.time() - t0
+    print(f"{tag}: fp32 forward {t32:.0f}s", flush=True)
     tr.to(torch.bfloat16)
     br.to(torch.bfloat16)
     t0 = time.time()
     o16, bs16 = fwd(torch.bfloat16)
-    print(f"bf16 forward {time.time() - t0:.0f}s", flush=True)
+    t16 = time.time() - t0
+    print(f"{tag}: bf16 forward {t16:.0f}s", flush=True)
     rel = lambda a, b: float((a.double() - b.double()).norm() / b.double().norm())  # noqa: E731
     flat = o32.reshape(-1)
-    out = {"slice": flat[::37].clone(),
+    out = {"slice": flat[::out_stride].clone(),
            "digest": torch.tensor([flat.sum(), flat.abs().sum(), flat.norm()], dtype=torch.float64),
            "branch.0.slice": bs32[0].reshape(-1)[::997].clone(), "branch.1.slice": bs32[1].reshape(-1)[::997].clone(),
            "ref_bf16_rel": torch.tensor([rel(o16, o32), rel(bs16[0], bs32[0]), rel(bs16[1], bs32[1])])}
-    print("reference bf16 vs fp32 rel-L2: noise_pred %.3e, branch %.3e / %.3e" % tuple(out["ref_bf16_rel"].tolist()))
-    _save("config1.safetensors", out)
+    if tag != "config1":
+        out["bf16.slice"] = o16.reshape(-1)[::out_stride].clone()
+    print("%s: reference bf16 vs fp32 rel-L2: noise_pred %.3e, branch %.3e / %.3e"
+          % ((tag,) + tuple(out["ref_bf16_rel"].tolist())))
+    _save(f"{tag}.safetensors", out, {"cpu_seconds": {"fp32": t32, "bf16": t16}} if tag != "config1" else None)
+
+
+def make_config1():
+    from tests.golden.cases import config1_cfg, config1_inputs, CONFIG1_SEEDS
+    _make_full_model("config1", config1_cfg, config1_inputs, CONFIG1_SEEDS, 37)
+
+
+def make_config2():
+    """the headline shape (49f 480x720, N = 17 776, B = 2) through the reference, whole model.
+    noise_pred [2,13,16,60,90]: strided slice (every 7th element, fp32 and the reference's own bf16 run) + digest."""
+    from tests.golden.cases import config2_cfg, config2_inputs, CONFIG2_SEEDS
+    _make_full_model("config2", config2_cfg, config2_inputs, CONFIG2_SEEDS, 7)
+
+
+@torch.no_grad()
+def make_block5():
+    """Config 5 (720x1280: N = 226 + 46 800 = 47 026): one full-width block, B = 1, fp32 and bf16."""
+    import time
+    from diffusers.models.transformers.cogvideox_transformer_3d import CogVideoXBlock
+    case = full_block_case(latent=(13, 90, 160), key="fb5")
+    blk = CogVideoXBlock(dim=3072, num_attention_heads=48, attention_head_dim=64, time_embed_dim=512,
+                         attention_bias=True).eval()
+    blk.load_state_dict({k: torch.from_numpy(v) for k, v in case["weights"].items()}, strict=True)
+
+    def run(dt):
+        h, e = blk.to(dt)(hidden_states=case["h"].to(dt), encoder_hidden_states=case["e"].to(dt),
+                          temb=case["temb"].to(dt), image_rotary_emb=case["rope"])
+        return torch.cat([e, h], dim=1).float()
+
+    t0 = time.time()
+    o32 = run(torch.float32)
+    print(f"block5 fp32 {time.time() - t0:.0f}s", flush=True)
+    o16 = run(torch.bfloat16)
+    rel = float((o16.double() - o32.double()).norm() / o32.double().norm())
+    print(f"block5 reference bf16 vs fp32 rel-L2 {rel:.3e}", flush=True)
+    flat = o32.reshape(-1)
+    _save("block5.safetensors", {"slice": flat[::1999].clone(), "bf16.slice": o16.reshape(-1)[::1999].clone(),
+                                 "digest": torch.tensor([flat.sum(), flat.abs().sum(), flat.norm()],
+                                                        dtype=torch.float64),
+                                 "ref_bf16_rel": torch.tensor([rel])})
 
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["tiny", "sched", "pipe", "block"]
     if "config1" in which:
         make_config1()
+    if "config2" in which:
+        make_config2()
+    if "block5" in which:
+        make_block5()
     if "tiny" in which:
         make_tiny()
     if "sched" in which:

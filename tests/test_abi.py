@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_functions():
     src = open(os.path.join(ROOT, "include", "vp_hip.h")).read()
-    return sorted(set(re.findall(r"^(?:int|void|int64_t)\s+(vp_\w+)\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|void|int64_t|const char\*)\s+(vp_\w+)\(", src, flags=re.M)))
 
 
 def test_header_and_binding_agree():

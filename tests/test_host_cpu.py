@@ -48,6 +48,28 @@ def test_checkpoint_round_trip_and_config_overrides(tmp_path):
         CogVideoXTransformer3DModel(**dict(TINY_CFG, use_rotary_positional_embeddings=False))
 
 
+def test_from_transformer_initialises_uncopied_parameters_and_rejects_shape_mismatch():
+    """branch_cogvideox.py:255-293: parameters the reference never copies (text_proj, norms, head) keep PyTorch's
+    default init (finite, Linear U(+-1/sqrt(fan_in)), LayerNorm 1/0), and load_state_dict(strict=False) raises on a
+    size mismatch (the default attention_head_dim=128 against a 64-dim transformer)."""
+    from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel
+    tsd, _ = tiny_weights()
+    tr = CogVideoXTransformer3DModel(**TINY_CFG)
+    tr.load_diffusers_state_dict({k: torch.from_numpy(v) for k, v in tsd.items()})
+    br = CogvideoXBranchModel.from_transformer(tr, num_layers=2, attention_head_dim=64, num_attention_heads=2)
+    for k, v in br.state_dict().items():
+        assert torch.isfinite(v.float()).all(), k
+    tp = br.patch_embed.text_proj.weight.float()
+    bound = 1.0 / tp.shape[1] ** 0.5
+    assert 0.0 < float(tp.abs().max()) <= bound * 1.01
+    assert float(tp.std()) > 0.3 * bound
+    assert torch.equal(br.norm_final.weight.float(), torch.ones_like(br.norm_final.weight.float()))
+    assert float(br.branch_x_embedder.weight.abs().max()) == 0.0
+    assert torch.equal(br.transformer_blocks[1].attn1.to_q.weight, tr.transformer_blocks[1].attn1.to_q.weight)
+    with pytest.raises(RuntimeError, match="size mismatch"):
+        CogvideoXBranchModel.from_transformer(tr, num_layers=2, attention_head_dim=128, num_attention_heads=1)
+
+
 def test_rope_and_sincos_tables_match_oracle():
     from videopainter_amd.embeddings import prepare_rotary_positional_embeddings, joint_sincos_pos_embedding
     for (h, w, f) in ((480, 720, 13), (256, 384, 3), (720, 1280, 13)):

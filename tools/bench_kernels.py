@@ -33,8 +33,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
-    ap.add_argument("--gemm-variants", default="10,5")
-    ap.add_argument("--variant", default="", help="attention kernel variant(s), e.g. 1 or 1,3")
+    ap.add_argument("--gemm-variants", default="5,11", help="VP_GEMM_VARIANT values, interleaved over 2 rounds")
+    ap.add_argument("--variant", default="", help="attention kernel(s): lazy, bounded (default: both)")
     ap.add_argument("--variant8", default="", help="fp8 attention kernel variant(s) (VP_ATTN8_VARIANT), e.g. 1,2")
     ap.add_argument("--only", default="", help="attention | attn8 | gemm | mx: run just that kernel (for rocprofv3 "
                     "--pmc passes; attn8 = the fp8 attention only)")
@@ -72,16 +72,18 @@ def main():
                 del a16, w16, A, W, out
         print(json.dumps(res))
         return
-    for name, Nn, Kk in shapes:
-        w = (torch.randn(Nn, Kk, device=dev) * Kk ** -0.5).to(torch.bfloat16)
-        b = torch.randn(Nn, device=dev).to(torch.bfloat16) * 0.1
-        out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
-        a = x[:, :Kk]
-        for gv in args.gemm_variants.split(","):
-            os.environ["VP_GEMM_VARIANT"] = gv
-            t = timeit(lambda: K.gemm(a, [w], [b], out, lda=x.stride(0)), args.iters)
-            res[f"gemm{gv}_{name}_{M}x{Nn}x{Kk}"] = dict(ms=t * 1e3, tflops=2 * M * Nn * Kk / t / 1e12)
-            print(f"gemm v{gv}", name, res[f"gemm{gv}_{name}_{M}x{Nn}x{Kk}"], flush=True)
+    for rnd in range(2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
+        for name, Nn, Kk in shapes:
+            w = (torch.randn(Nn, Kk, device=dev) * Kk ** -0.5).to(torch.bfloat16)
+            b = torch.randn(Nn, device=dev).to(torch.bfloat16) * 0.1
+            out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+            a = x[:, :Kk]
+            for gv in args.gemm_variants.split(","):
+                os.environ["VP_GEMM_VARIANT"] = gv
+                t = timeit(lambda: K.gemm(a, [w], [b], out, lda=x.stride(0)), args.iters)
+                res[f"gemm{gv}_{name}_r{rnd}"] = dict(ms=t * 1e3, tflops=2 * M * Nn * Kk / t / 1e12)
+                print(f"gemm v{gv}", name, res[f"gemm{gv}_{name}_r{rnd}"], flush=True)
+            del w, b, out
         os.environ.pop("VP_GEMM_VARIANT", None)
     del x
     qkv = torch.randn(B, Ntok, 3 * D, device=dev).to(torch.bfloat16)
@@ -91,21 +93,16 @@ def main():
     if args.only == "gemm":
         print(json.dumps(res))
         return
-    variants = ("vdefault",) if args.only == "attention" else ("vdefault", "v1", "v3")
+    # lazy = the running-max kernel; bounded = the no-max kernel the processors pick when the qk-norm
+    # bounds every score (these random q, k: |q.k| * 0.125 * log2 e stays far below the bound of 60)
+    variants = tuple(args.variant.split(",")) if args.variant else ("lazy", "bounded")
     if args.only == "attn8":
         variants = ()
-    if args.variant:
-        variants = tuple("v" + v for v in args.variant.split(","))
     for rnd in range(1 if args.only else 2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
         for var in variants:
-            if var == "vdefault":
-                os.environ.pop("VP_ATTN_VARIANT", None)
-            else:
-                os.environ["VP_ATTN_VARIANT"] = var[1:]
-            t = timeit(lambda: K.attention(q, k, v, o, H), max(2, args.iters // 2))
+            t = timeit(lambda: K.attention(q, k, v, o, H, bounded_scores=var != "lazy"), max(2, args.iters // 2))
             res[f"attention_{var}_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
             print("attention", var, res[f"attention_{var}_r{rnd}"], flush=True)
-    os.environ.pop("VP_ATTN_VARIANT", None)
     if args.only == "attention":  # bf16 attention only (rocprofv3 --pmc passes filter on the kernel name)
         print(json.dumps(res))
         return

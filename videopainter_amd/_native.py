@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -43,7 +43,7 @@ class AttnDesc(C.Structure):
                 ("Nk", i32), ("Nk2", i32),
                 ("K2", vp), ("V2", vp), ("k2_sb", i64), ("k2_sn", i64), ("v2_sb", i64), ("v2_sn", i64),
                 ("O", vp), ("o_sb", i64), ("o_sn", i64),
-                ("scale", f32), ("out_scale", f32), ("accumulate", i32), ("pad", i32)]
+                ("scale", f32), ("out_scale", f32), ("accumulate", i32), ("flags", i32)]
 
 
 class GemmMxDesc(C.Structure):
@@ -69,6 +69,7 @@ EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS, EPI_BIAS_G
 # name -> (restype, argtypes)
 _SIGS = {
     "vp_abi_version": (i32, []),
+    "vp_build_digest": (C.c_char_p, []),
     "vp_struct_sizes": (None, [C.POINTER(i64)]),
     "vp_gemm_bf16": (i32, [C.POINTER(GemmDesc), vp]),
     "vp_gemm_mx_fp8": (i32, [C.POINTER(GemmMxDesc), vp]),
@@ -126,6 +127,11 @@ def lib():
             fn.argtypes = args
         if L.vp_abi_version() != ABI_VERSION:
             raise HipLibraryError(f"libvp_hip ABI {L.vp_abi_version()} != {ABI_VERSION}; rebuild")
+        built = (L.vp_build_digest() or b"").decode()
+        src = _source_digest()
+        if src is not None and built.split(":")[0] != src:
+            raise HipLibraryError(f"{LIB_PATH} was built from other sources (digest {built[:12]}.. != "
+                                  f"{src[:12]}..); rebuild with `python -m videopainter_amd.build`")
         sizes = (i64 * 5)()
         L.vp_struct_sizes(sizes)
         want = (C.sizeof(GemmDesc), C.sizeof(AttnDesc), C.sizeof(DpmDesc), C.sizeof(GemmMxDesc),
@@ -134,6 +140,14 @@ def lib():
             raise HipLibraryError(f"descriptor size mismatch lib={tuple(sizes)} python={want}; rebuild")
         _lib = L
         return L
+
+
+def _source_digest():
+    """Digest of the csrc/ sources next to this package (None when they are absent, e.g. a binary-only install)."""
+    from . import build as _b
+    if not _b._sources():
+        return None
+    return _b.source_digest()
 
 
 _ERRS = {1000: "VP_ERR_ARG (invalid size/stride/pointer)", 1001: "VP_ERR_UNSUPPORTED"}

@@ -117,6 +117,21 @@ def _fusable_norms(attn) -> bool:
     return True
 
 
+def bounded_scores(attn) -> bool:
+    """True when the qk-LayerNorm weights bound every attention score of `attn` within the kernel's exact
+    no-running-max range (kernels.score_bound_log2 <= SCORE_BOUND_LOG2).  Cached per layer on the weights' storage and
+    version (one host sync per weight update); env VP_ATTN_BOUNDED=0 forces the running-max kernel (A/B)."""
+    if os.environ.get("VP_ATTN_BOUNDED", "1") == "0":
+        return False
+    nq, nk = attn.norm_q, attn.norm_k
+    key = tuple((t.data_ptr(), t._version) for t in (nq.weight, nq.bias, nk.weight, nk.bias)) + (float(attn.scale),)
+    cached = getattr(attn, "_vp_score_bound", None)
+    if cached is None or cached[0] != key:
+        cached = (key, K.score_bound_log2(nq, nk, float(attn.scale)) <= K.SCORE_BOUND_LOG2)
+        attn._vp_score_bound = cached
+    return cached[1]
+
+
 class CogVideoXAttnProcessor2_0:
     """HIP restatement of `CogVideoXAttnProcessor2_0.__call__` (attention_processor.py:2107-2209)."""
 
@@ -143,10 +158,11 @@ class CogVideoXAttnProcessor2_0:
             pk, pv = pkv[..., :D], pkv[..., D:]
             K.head_norm_rope(pk, pk, H, text_len, attn.norm_k.weight, attn.norm_k.bias, eps_k, rope)
             w = float(prev_clip_weight)
-            K.attention(q, k, v, o, H, scale=attn.scale, out_scale=1.0 - w)
-            K.attention(q, pk, pv, o, H, scale=attn.scale, out_scale=w, accumulate=True)
+            bs = bounded_scores(attn)
+            K.attention(q, k, v, o, H, scale=attn.scale, out_scale=1.0 - w, bounded_scores=bs)
+            K.attention(q, pk, pv, o, H, scale=attn.scale, out_scale=w, accumulate=True, bounded_scores=bs)
         else:
-            K.attention(q, k, v, o, H, scale=attn.scale)
+            K.attention(q, k, v, o, H, scale=attn.scale, bounded_scores=bounded_scores(attn))
         return o
 
     @staticmethod
@@ -225,5 +241,5 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
         K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, attn.norm_q.eps, rope)
         K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope)
         o = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
-        K.attention(q, k, v, o, H, k2=k2, v2=v2, scale=attn.scale)
+        K.attention(q, k, v, o, H, k2=k2, v2=v2, scale=attn.scale, bounded_scores=bounded_scores(attn))
         return o

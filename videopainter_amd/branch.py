@@ -62,12 +62,20 @@ class CogvideoXBranchModel(CogVideoXTransformer3DModel):
     @classmethod
     def from_transformer(cls, transformer, num_layers: int = 4, attention_head_dim: int = 128,
                          num_attention_heads: int = 24, load_weights_from_transformer=True, wo_text: bool = False):
-        """branch_cogvideox.py:255-293."""
+        """branch_cogvideox.py:255-293.  Parameters the reference does not copy keep its constructor's
+        initialisation (PyTorch defaults; `branch_blocks` / `branch_x_embedder` zero, :143-145); the block copy is
+        `load_state_dict(strict=False)`, which skips missing keys but raises on a shape mismatch (e.g. the default
+        attention_head_dim=128 against a 64-dim transformer)."""
         cfg = {k: v for k, v in dict(transformer.config).items() if not k.startswith("_")}
         cfg.update(num_layers=num_layers, attention_head_dim=attention_head_dim,
                    num_attention_heads=num_attention_heads, wo_text=wo_text)
         dev = transformer.proj_out.weight.device
         branch = cls.from_config(cfg, device=dev, dtype=transformer.proj_out.weight.dtype)
+        branch.reset_parameters_()
+        with torch.no_grad():
+            for lin in list(branch.branch_blocks) + [branch.branch_x_embedder]:  # zero_module (:143-145)
+                lin.weight.zero_()
+                lin.bias.zero_()
         if load_weights_from_transformer:
             with torch.no_grad():
                 w = torch.zeros_like(branch.patch_embed.proj.weight)
@@ -89,12 +97,14 @@ class CogvideoXBranchModel(CogVideoXTransformer3DModel):
                     a.bias.copy_(b.bias)
                 tsd = transformer.transformer_blocks.state_dict()
                 bsd = branch.transformer_blocks.state_dict()
+                bad = [f"{k}: {tuple(tsd[k].shape)} vs {tuple(v.shape)}" for k, v in bsd.items()
+                       if k in tsd and tsd[k].shape != v.shape]
+                if bad:
+                    raise RuntimeError("Error(s) in loading state_dict for ModuleList: size mismatch for "
+                                       + "; ".join(bad[:4]))
                 for k, v in bsd.items():  # strict=False: the first `num_layers` blocks
-                    if k in tsd and tsd[k].shape == v.shape:
+                    if k in tsd:
                         v.copy_(tsd[k])
-                for lin in list(branch.branch_blocks) + [branch.branch_x_embedder]:  # zero_module
-                    lin.weight.zero_()
-                    lin.bias.zero_()
         return branch
 
     def forward(self, hidden_states: torch.Tensor, encoder_hidden_states: torch.Tensor = None,

@@ -33,7 +33,8 @@ def _sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
 
-def _digest() -> str:
+def source_digest() -> str:
+    """sha256 of the sources, headers and flags (repo-relative paths: the GPU box's checkout path differs)."""
     h = hashlib.sha256()
     for p in _sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "vp_hip.h")]:
         with open(p, "rb") as f:
@@ -44,12 +45,25 @@ def _digest() -> str:
     return h.hexdigest()
 
 
+def compiler_digest() -> str:
+    r = subprocess.run([HIPCC, "--version"], capture_output=True, text=True)
+    return hashlib.sha256((r.stdout + r.stderr).encode()).hexdigest()[:16]
+
+
+def _digest() -> str:
+    return source_digest() + ":" + compiler_digest()
+
+
 def build(force: bool = False, verbose: bool = True, out: str = LIB, extra_flags=None) -> str:
     """out / extra_flags ({file: [flags]}) build an A/B copy of the library (VP_HIP_LIB selects it at load time)."""
     libdir = os.path.dirname(out)
     os.makedirs(libdir, exist_ok=True)
+    # the stamp is a local cache (git-ignored): a checkout that changes csrc/ changes source_digest() and rebuilds;
+    # _native.lib() also compares the digest compiled INTO the library with the sources at load time
     stamp = os.path.join(libdir, os.path.basename(out).replace(".so", ".sha256"))
-    dg = _digest() + repr(sorted((extra_flags or {}).items()))
+    dg = _digest()
+    if extra_flags:
+        dg += ":" + hashlib.sha256(repr(sorted(extra_flags.items())).encode()).hexdigest()[:16]
     if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read().strip() == dg:
         return out
     objs = []
@@ -57,7 +71,8 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, extra_flags
     def cc(src):
         obj = os.path.join(libdir, os.path.basename(src).replace(".hip", ".o"))
         extra = PER_FILE_FLAGS.get(os.path.basename(src), []) + (extra_flags or {}).get(os.path.basename(src), [])
-        cmd = [HIPCC, *CFLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+        cmd = [HIPCC, *CFLAGS, *extra, f'-DVP_BUILD_DIGEST="{dg}"', "-I", os.path.join(ROOT, "include"), "-c", src,
+               "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")

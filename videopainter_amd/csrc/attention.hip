@@ -4,39 +4,47 @@
 //
 // Layout of the math (one wave = 32 queries, one workgroup = 8 waves = 256 queries of one (batch, head)):
 //   S^T[key][q] = K · Q^T        v_mfma_f32_32x32x16_bf16, A = K rows from LDS (ds_read_b128, XOR-swizzled),
-//                                B = Q^T held in registers for the whole key loop.
-//   The accumulator has the query on the lane, so the online-softmax state (running max m, sum l) is per lane and
-//   the row max is 31 in-register fmax + one cross-half shuffle.
-//   O^T[d][q] += V^T · P^T      A = V^T read with ds_read_b64_tr_b16 (hardware transpose) from a padded V image,
+//                                B = Q^T held in registers for the whole key loop (pre-scaled by scale·log2 e, so
+//                                the scores leave the matrix pipe in log2 units and the softmax is a bare v_exp_f32).
+//   The accumulator has the query on the lane, so the online-softmax state (running max m, sum l) is per lane.
+//   O^T[d][q] += V^T · P^T      A = V^T read with ds_read_b64_tr_b16 (hardware transpose) from the V tile,
 //                                B = P^T taken straight from the S^T accumulator registers (bf16-packed, with the
 //                                k-order permutation of cdna_hip_programming.md §3 "accumulator tile as operand").
-//   O^T keeps the query on the lane too, so the rescale by exp(m_old - m_new) is a per-lane scalar.
-// K/V tiles of 64 keys are double-buffered in LDS with register staging (global loads issued before the tile's
-// MFMAs, LDS writes after them; one barrier per tile).
-// Roofline: MFMA-bound in principle (4·N²·64 flop per (b,h)); at d=64 the softmax VALU (one exp per 256 MFMA
-// flops) is the co-bottleneck, so the lever is latency hiding across waves: the default variant consumes each
-// 64-key tile in two 32-key halves (16 score + 8 packed-P registers live), which fits 128 VGPRs and runs 4 waves
-// per SIMD (two 8-wave workgroups per CU).  Measured at config 2 (B=2, H=48, N=17776): 2 waves/SIMD 773-800
-// TFLOP/s, 3 waves/SIMD 835-863, 4 waves/SIMD half tiles 888.  Tried and dropped (slower at this shape):
-// an 8-wave ping-pong schedule (two wave groups alternating MFMA and softmax phases between barriers: 735, the
-// softmax phase is twice the MFMA phase at d=64 so the MFMA group idles), deferred-max softmax (register cost
-// outweighs the skipped max), software-pipelined S tiles (spills).
+// 128-key K/V tiles stream into a 2-slot LDS ring by LDS-DMA (global_load_lds_dwordx4) and are consumed as 32-key
+// halves (16 score + 8 packed-P registers live: 128 VGPRs, 4 waves per SIMD = two 8-wave workgroups per CU).
+// Roofline: MFMA-bound in principle (4·N²·64 flop per (b,h)); at d = 64 every score costs one v_exp_f32, a bf16 pack
+// and a row-sum add against 256 MFMA flops, so the softmax VALU issue is the co-bottleneck.
+//
+// Softmax modes (template MODE):
+//   LAZY   (default for unbounded scores): C-init QK^T (the running max enters the first MFMA as C = -m, so S - m
+//          leaves the matrix pipe), then exp2 straight off the accumulator; the max path runs only when a lane's
+//          half-sum shows an exponent above the threshold.
+//   BOUNDED (the host proves |score| <= VP_ATTN_SCORE_BOUND in log2 units, flag VP_ATTN_BOUNDED_SCORES): no
+//          running max at all — p = exp2(s) is exact in bf16 and fp32 over [2^-60, 2^60] and O / l is invariant to
+//          the reference point.  CogVideoX's qk-LayerNorm bounds every score: |q|, |k| <= 8 max|gamma| + |beta|_2
+//          (attention_processor.py:2143-2146), so the processors set the flag per layer from the norm weights.
+//          The row sums run on the matrix pipe: one v_mfma_f32_16x16x32_bf16 per 16 keys with a 0/1 selector as A
+//          and the P^T operand as B gives all 32 queries' sums, so the VALU does only exp2 + pack per score.
+//          (Measured at config 2: 1.15 PF/s against 1.13 for LAZY; the same no-max kernel with the sums on the VALU
+//          needs a second score tile live and spills at 128 VGPRs: 0.97.)
 #include <stdlib.h>
 
 #include "vp_common.h"
 
 namespace {
 
-constexpr int NWAVES = 8;
-constexpr int NTHREADS = NWAVES * 64;
-constexpr int QBLK = NWAVES * 32;   // 256 queries per workgroup
-constexpr int KBLK = 64;            // keys per tile
-constexpr int K_TILE_BYTES = KBLK * 128;
-constexpr int V_STRIDE = 192;       // bytes per V row in LDS (128 data + 64 pad: conflict-free transposed reads)
-constexpr int V_TILE_BYTES = KBLK * V_STRIDE;
-constexpr int STAGE_BYTES = K_TILE_BYTES + V_TILE_BYTES;
-constexpr int LDS_BYTES = 2 * STAGE_BYTES;
-constexpr int DEFAULT_VARIANT = 22;
+constexpr int NW = 8;               // waves per workgroup
+constexpr int QB = NW * 32;         // 256 queries per workgroup
+constexpr int KB = 128;             // keys per LDS tile
+constexpr int KT = KB * 128;        // bytes per K (or V) tile
+constexpr int ST = 2 * KT;          // one ring slot = K + V
+constexpr int LDS_BYTES = 2 * ST;   // 2-slot ring
+constexpr int NP = KB / 8;          // 1-KiB DMA pieces (8 rows) per operand per tile
+constexpr int PPW = NP / NW;        // pieces per wave
+constexpr int HALVES = KB / 32;
+static_assert(NP % NW == 0, "pieces per wave");
+
+enum { MODE_LAZY = 0, MODE_BOUNDED = 1 };
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
@@ -50,7 +58,6 @@ struct Seg {
   int key0;
 };
 
-template <int KB = KBLK>
 VP_DEV Seg tile_seg(const vp_attn_desc& d, int ti, int tiles1, int b, int h) {
   Seg s;
   if (ti < tiles1) {
@@ -71,169 +78,7 @@ VP_DEV Seg tile_seg(const vp_attn_desc& d, int ti, int tiles1, int b, int h) {
   return s;
 }
 
-// S^T = K Q^T for one 64-key tile; PRE = K fragments read ahead of the first MFMA (8: all, 4: one key half at a
-// time, 16 fewer VGPRs)
-template <int PRE>
-VP_DEV void qk_tile(const char* Kl, const bf16x8 (&qf)[4], f32x16 (&s)[2], int lane) {
-  const int hl = lane >> 5;
-  static_assert(PRE == 8 || PRE == 4, "PRE");
-  constexpr int KH_PER = PRE / 4;
-#pragma unroll
-  for (int kh0 = 0; kh0 < 2; kh0 += KH_PER) {
-    bf16x8 kf[KH_PER][4];
-#pragma unroll
-    for (int j = 0; j < KH_PER; ++j) {
-      const int row = (kh0 + j) * 32 + (lane & 31);
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) {
-        const int ch = ds * 2 + hl;
-        kf[j][ds] = *(const bf16x8*)(Kl + row * 128 + ((ch ^ swz(row)) << 4));
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < KH_PER; ++j) {
-      const int kh = kh0 + j;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[kh][i] = 0.f;
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds)
-        s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[j][ds], qf[ds], s[kh], 0, 0, 0);
-    }
-  }
-}
-
-VP_DEV void mask_tail(f32x16 (&s)[2], int lim, int hl) {
-#pragma unroll
-  for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key = kh * 32 + (i & 3) + 8 * (i >> 2) + 4 * hl;
-      if (key >= lim) s[kh][i] = -INFINITY;
-    }
-}
-
-VP_DEV void softmax_tile(f32x16 (&s)[2], float& m_run, float& l_run, f32x16 (&o)[2], bf16x8 (&pf)[4], float c) {
-  // max over the lane's 32 scores as 4 independent v_max3_f32 chains (short dependency chains: the wave has
-  // little other work to hide latency behind); the file is built with -fno-honor-nans so no canonicalising v_max
-  // is inserted on the MFMA results
-  float m4[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const f32x16& v = s[j >> 1];
-    const int o = (j & 1) * 8;
-    m4[j] = fmaxf(fmaxf(fmaxf(v[o], v[o + 1]), v[o + 2]), fmaxf(fmaxf(v[o + 3], v[o + 4]), v[o + 5]));
-    m4[j] = fmaxf(fmaxf(m4[j], v[o + 6]), v[o + 7]);
-  }
-  float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  const float m_new = fmaxf(m_run, mx);
-  if (__ballot(m_new > m_run) != 0ull) {  // wave-uniform: some query's max moved -> rescale O and l
-    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
-    l_run *= alpha;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o[0][i] *= alpha;
-      o[1][i] *= alpha;
-    }
-    m_run = m_new;
-  }
-  const float mc = m_run * c;
-  float ps[4] = {0.f, 0.f, 0.f, 0.f};  // 4 independent partial sums (8-deep chains instead of one 32-deep)
-#pragma unroll
-  for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float p = __builtin_amdgcn_exp2f(fmaf(s[kh][i], c, -mc));
-      ps[i & 3] += p;
-      pf[kh * 2 + (i >> 3)][i & 7] = f2bf(p);
-    }
-  l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
-}
-
-VP_DEV void pv_tile(const char* Vl, const bf16x8 (&pf)[4], f32x16 (&o)[2], int trow, int tcol) {
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh) {
-      const char* base = Vl + (ks * 16 + trow) * V_STRIDE + (dh * 32 + tcol) * 2;
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * V_STRIDE));
-      const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[ks], o[dh], 0, 0, 0);
-    }
-  }
-}
-
-// Row-sum-on-MFMA softmax: the tile's row sums come out of 4 extra MFMAs (ones^T x P^T, accumulated in lsum where
-// every entry of a lane holds its query's running sum), so the VALU does only max, exp, scale and bf16 packing — at
-// head_dim 64 the VALU, not the matrix pipe, is the bottleneck.  The sum is then over the bf16-rounded P that also
-// feeds O (numerator and denominator see the same P).
-VP_DEV void softmax_tile_rs(f32x16 (&s)[2], float& m_run, f32x16 (&o)[2], f32x16& lsum, bf16x8 (&pf)[4], float c) {
-  float m4[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const f32x16& v = s[j >> 1];
-    const int o8 = (j & 1) * 8;
-    m4[j] = fmaxf(fmaxf(fmaxf(v[o8], v[o8 + 1]), v[o8 + 2]), fmaxf(fmaxf(v[o8 + 3], v[o8 + 4]), v[o8 + 5]));
-    m4[j] = fmaxf(fmaxf(m4[j], v[o8 + 6]), v[o8 + 7]);
-  }
-  float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
-  {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-    mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-  }
-  const float m_new = fmaxf(m_run, mx);
-  if (__ballot(m_new > m_run) != 0ull) {
-    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o[0][i] *= alpha;
-      o[1][i] *= alpha;
-      lsum[i] *= alpha;
-    }
-    m_run = m_new;
-  }
-  const float mc = m_run * c;
-#pragma unroll
-  for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) pf[kh * 2 + (i >> 3)][i & 7] = f2bf(__builtin_amdgcn_exp2f(fmaf(s[kh][i], c, -mc)));
-}
-
-VP_DEV void pv_tile_rs(const char* Vl, const bf16x8 (&pf)[4], f32x16 (&o)[2], f32x16& lsum, int trow, int tcol) {
-  const bf16 one = f2bf(1.f);
-  const bf16x8 ones = {one, one, one, one, one, one, one, one};
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh) {
-      const char* base = Vl + (ks * 16 + trow) * V_STRIDE + (dh * 32 + tcol) * 2;
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * V_STRIDE));
-      const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[ks], o[dh], 0, 0, 0);
-    }
-    lsum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[ks], lsum, 0, 0, 0);
-  }
-}
-
-// ---- half-tile (32-key) helpers: the 64-key LDS tile is consumed in two 32-key halves so only 16 score
-// registers, 8 packed-P registers and 16 K-fragment registers are live (the register budget of 4 waves/SIMD) ----
-VP_DEV void qk_half(const char* Kl, int kh, const bf16x8 (&qf)[4], f32x16& s, int lane) {
-  const int hl = lane >> 5;
-  const int row = kh * 32 + (lane & 31);
-  bf16x8 kf[4];
-#pragma unroll
-  for (int ds = 0; ds < 4; ++ds) {
-    const int ch = ds * 2 + hl;
-    kf[ds] = *(const bf16x8*)(Kl + row * 128 + ((ch ^ swz(row)) << 4));
-  }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) s[i] = 0.f;
-#pragma unroll
-  for (int ds = 0; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ds], qf[ds], s, 0, 0, 0);
-}
-
+// keys past the segment end (the DMA re-read the last key there) get score -inf
 VP_DEV void mask_half(f32x16& s, int lim, int kh, int hl) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -242,82 +87,13 @@ VP_DEV void mask_half(f32x16& s, int lim, int kh, int hl) {
   }
 }
 
-VP_DEV void softmax_half(f32x16& s, float& m_run, float& l_run, f32x16 (&o)[2], bf16x8 (&pf)[2], float c) {
-  float m2[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int o8 = j * 8;
-    m2[j] = fmaxf(fmaxf(fmaxf(s[o8], s[o8 + 1]), s[o8 + 2]), fmaxf(fmaxf(s[o8 + 3], s[o8 + 4]), s[o8 + 5]));
-    m2[j] = fmaxf(fmaxf(m2[j], s[o8 + 6]), s[o8 + 7]);
-  }
-  float mx = fmaxf(m2[0], m2[1]);
-  {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-    mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-  }
-  const float m_new = fmaxf(m_run, mx);
-  if (__ballot(m_new > m_run) != 0ull) {
-    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * c);
-    l_run *= alpha;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o[0][i] *= alpha;
-      o[1][i] *= alpha;
-    }
-    m_run = m_new;
-  }
-  const float mc = m_run * c;
-  float ps[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float p = __builtin_amdgcn_exp2f(fmaf(s[i], c, -mc));
-    ps[i & 3] += p;
-    pf[i >> 3][i & 7] = f2bf(p);
-  }
-  l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
-}
-
-VP_DEV void pv_half(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)[2], int trow, int tcol) {
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int ks = kh * 2 + j;
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh) {
-      const char* base = Vl + (ks * 16 + trow) * V_STRIDE + (dh * 32 + tcol) * 2;
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * V_STRIDE));
-      const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[j], o[dh], 0, 0, 0);
-    }
-  }
-}
-
-// ---- C-init half tiles: the QK^T MFMA chain starts from C = -m_run (per lane = per query; Q pre-multiplied by
-// scale*log2e when loaded), so the accumulator already holds the exponent s - m and the softmax is exp2 + sum +
-// pack per score — no per-score scale/subtract FMA.  A lane rescales only when its tile max exceeds its running
-// max by more than `thr` (thr = -inf before the first tile, so the first tile always sets m; afterwards RESCALE_THR:
-// P stays <= 2^RESCALE_THR, exact in bf16's exponent range, and the ratio O / l is unchanged). ----
+// ---- LAZY mode: C-init half tiles.  A lane rescales only when its tile max exceeds its running max by more than
+// `thr` (thr = -inf before the first tile, so the first tile always sets m; afterwards RESCALE_THR: P stays
+// <= 2^RESCALE_THR, exact in bf16's exponent range, and the ratio O / l is unchanged). ----
 constexpr float RESCALE_THR = 8.f;
 
-VP_DEV void qk_half_ci(const char* Kl, int kh, const bf16x8 (&qf)[4], const f32x16& negm, f32x16& s, int lane) {
-  const int hl = lane >> 5;
-  const int row = kh * 32 + (lane & 31);
-  const char* kr = Kl + row * 128;
-  const int sw = swz(row);
-  // two K fragments in flight at a time (8 VGPRs instead of 16: the 4-waves/SIMD budget is 128)
-  bf16x8 k0 = *(const bf16x8*)(kr + ((hl ^ sw) << 4));
-  bf16x8 k1 = *(const bf16x8*)(kr + (((2 + hl) ^ sw) << 4));
-  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[0], negm, 0, 0, 0);
-  k0 = *(const bf16x8*)(kr + (((4 + hl) ^ sw) << 4));
-  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[1], s, 0, 0, 0);
-  k1 = *(const bf16x8*)(kr + (((6 + hl) ^ sw) << 4));
-  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[2], s, 0, 0, 0);
-  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[3], s, 0, 0, 0);
-}
-
-template <bool NEXT = false>
 VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f32x16& negm, f32x16 (&o)[2],
-                            bf16x8 (&pf)[2], f32x16& s_next) {
+                            bf16x8 (&pf)[2]) {
   float m2[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -341,7 +117,6 @@ VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f
       o[1][i] *= alpha;
       s[i] -= dm;
       negm[i] = -m_run;
-      if constexpr (NEXT) s_next[i] -= dm;  // a next half already computed against the old -m
     }
     thr = RESCALE_THR;
   }
@@ -355,17 +130,12 @@ VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f
   l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
 }
 
-VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f32x16& negm, f32x16 (&o)[2],
-                            bf16x8 (&pf)[2]) {
-  softmax_half_ci<false>(s, m_run, thr, l_run, negm, o, pf, s);
-}
-
 // QK^T half with the first MFMA in inline asm so its destination is a fresh tuple (early-clobber) while C = -m
 // stays in its own registers: with the builtin, the compiler coalesces the rescale path's phi of -m into the second
 // half's accumulator and pays 8 v_mov_b64 per half to refill it.  The following builtin MFMAs accumulate on the
 // asm result in place (same opcode, exactly overlapping srcC: no wait states); -m is written by VALU only in the
 // rescale branch, long before the next QK^T.
-VP_DEV void qk_half_ci2(const char* Kl, int kh, const bf16x8 (&qf)[4], const f32x16& negm, f32x16& s, int lane) {
+VP_DEV void qk_half_ci(const char* Kl, int kh, const bf16x8 (&qf)[4], const f32x16& negm, f32x16& s, int lane) {
   const int hl = lane >> 5;
   const int row = kh * 32 + (lane & 31);
   const char* kr = Kl + row * 128;
@@ -373,6 +143,23 @@ VP_DEV void qk_half_ci2(const char* Kl, int kh, const bf16x8 (&qf)[4], const f32
   bf16x8 k0 = *(const bf16x8*)(kr + ((hl ^ sw) << 4));
   bf16x8 k1 = *(const bf16x8*)(kr + (((2 + hl) ^ sw) << 4));
   asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(s) : "v"(k0), "v"(qf[0]), "v"(negm));
+  k0 = *(const bf16x8*)(kr + (((4 + hl) ^ sw) << 4));
+  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[1], s, 0, 0, 0);
+  k1 = *(const bf16x8*)(kr + (((6 + hl) ^ sw) << 4));
+  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[2], s, 0, 0, 0);
+  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[3], s, 0, 0, 0);
+}
+
+// BOUNDED modes: QK^T from C = 0 (the raw log2-unit scores)
+VP_DEV void qk_half_zero(const char* Kl, int kh, const bf16x8 (&qf)[4], f32x16& s, int lane) {
+  const int hl = lane >> 5;
+  const int row = kh * 32 + (lane & 31);
+  const char* kr = Kl + row * 128;
+  const int sw = swz(row);
+  bf16x8 k0 = *(const bf16x8*)(kr + ((hl ^ sw) << 4));
+  bf16x8 k1 = *(const bf16x8*)(kr + (((2 + hl) ^ sw) << 4));
+  const f32x16 z = {};
+  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[0], z, 0, 0, 0);
   k0 = *(const bf16x8*)(kr + (((4 + hl) ^ sw) << 4));
   s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[1], s, 0, 0, 0);
   k1 = *(const bf16x8*)(kr + (((6 + hl) ^ sw) << 4));
@@ -399,8 +186,14 @@ VP_DEV bool softmax_half_lazy(const f32x16& s, float& l_run, bf16x8 (&pf)[2]) {
   return true;
 }
 
+// BOUNDED: p = exp2(s), s the raw score (the row sums come from the caller's MFMAs over the packed P)
+VP_DEV void softmax_half_bounded(const f32x16& s, bf16x8 (&pf)[2]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) pf[i >> 3][i & 7] = f2bf(__builtin_amdgcn_exp2f(s[i]));
+}
+
 // ---- LDS-DMA staging (global_load_lds_dwordx4, saddr + 32-bit voffset): the LDS destination is lane-linear, so
-// both images are unpadded [64 rows][128 B] and their bank swizzles are applied on the SOURCE address
+// both images are unpadded [rows][128 B] and their bank swizzles are applied on the SOURCE address
 // (cdna_hip_programming.md §5.4 rule 21).  K: chunk ^ swz(row) (conflict-free ds_read_b128).  V: chunk ^
 // vswz(row) with vswz(r) = 4*((r>>1)&1): the 4-row x 16-column blocks a 32-lane half reads with
 // ds_read_b64_tr_b16 (rows r..r+3, 64 contiguous bytes) then land on 4 disjoint 16-bank groups. ----
@@ -414,7 +207,8 @@ VP_DEV void glds16(const char* sbase, int voff, char* lds) {
                : "memory", "m0");
 }
 
-// O = O^T accumulator / l, rounded to bf16 like the reference's SDPA output, then the optional prev-clip blend
+// O = O^T accumulator / l, rounded to bf16 like the reference's SDPA output, then the optional prev-clip blend.
+// split_sum: l_run holds this lane's half of the row sum (the partner lane l ^ 32 has the other half).
 VP_DEV void store_out(const vp_attn_desc& d, const f32x16 (&o)[2], float l_run, int q, int b, int h, int hl,
                       bool split_sum = true) {
   const float l_tot = split_sum ? l_run + __shfl_xor(l_run, 32, 64) : l_run;
@@ -440,175 +234,12 @@ VP_DEV void store_out(const vp_attn_desc& d, const f32x16 (&o)[2], float l_run, 
     }
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// Main kernel: NW waves x 32 queries per workgroup, one barrier per 64-key tile, 2-slot LDS ring with register
-// staging (global loads for tile t+1 issued before tile t's MFMAs, written to LDS after them).  With NW = 4 two
-// workgroups share a CU, so their waves are not barrier-locked to each other and one workgroup's softmax VALU runs
-// beside the other's MFMAs.
-// ------------------------------------------------------------------------------------------------------------
-template <int NW, int OCC, int PRE, bool RS = false, bool HALF = false, bool CINIT = false>
-__global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_t(const vp_attn_desc d) {
-  constexpr int NT = NW * 64;
-  constexpr int QB = NW * 32;
-  constexpr int CH_PER_THREAD = (KBLK * 8) / NT;  // 16-byte chunks of a K (and of a V) tile per thread
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hl = lane >> 5;
-
-  const int nqb = (d.Nq + QB - 1) / QB;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = t / nqb;
-  const int qb = t - bh * nqb;
-  const int b = bh / d.H;
-  const int h = bh - b * d.H;
-  const int tiles1 = (d.Nk + KBLK - 1) / KBLK;
-  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KBLK - 1) / KBLK : 0;
-  const int ntiles = tiles1 + tiles2;
-
-  const int q = qb * QB + wave * 32 + (lane & 31);
-  const int qc = q < d.Nq ? q : d.Nq - 1;
-  const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
-  if constexpr (CINIT) {  // scores come out of the MFMA in log2 units
-    const float cq = d.scale * 1.4426950408889634f;
-#pragma unroll
-    for (int ds = 0; ds < 4; ++ds)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[ds][j] = f2bf(bf2f(qf[ds][j]) * cq);
-  }
-
-  int k_off[CH_PER_THREAD], v_off[CH_PER_THREAD], srow[CH_PER_THREAD], sch[CH_PER_THREAD];
-#pragma unroll
-  for (int i = 0; i < CH_PER_THREAD; ++i) {
-    const int cidx = tid + i * NT;
-    srow[i] = cidx >> 3;
-    sch[i] = cidx & 7;
-    k_off[i] = srow[i] * 128 + ((sch[i] ^ swz(srow[i])) << 4);
-    v_off[i] = K_TILE_BYTES + srow[i] * V_STRIDE + sch[i] * 16;
-  }
-  bf16x8 kreg[CH_PER_THREAD], vreg[CH_PER_THREAD];
-  // Per-chunk source pointers advance by one tile per call; recomputed (with the row clamp) only at a segment start
-  // or for a segment's partial last tile, so the steady-state address math is one 64-bit add per chunk.
-  const bf16* kp[CH_PER_THREAD];
-  const bf16* vp[CH_PER_THREAD];
-  auto gload = [&](int ti) {
-    Seg sg = tile_seg(d, ti, tiles1, b, h);
-    const bool fresh = (ti == 0) || (ti == tiles1) || (sg.key0 + KBLK > sg.n);
-#pragma unroll
-    for (int i = 0; i < CH_PER_THREAD; ++i) {
-      if (fresh) {
-        const int key = min(sg.key0 + srow[i], sg.n - 1);
-        kp[i] = sg.k + (int64_t)key * sg.k_sn + sch[i] * 8;
-        vp[i] = sg.v + (int64_t)key * sg.v_sn + sch[i] * 8;
-      } else {
-        kp[i] += KBLK * sg.k_sn;
-        vp[i] += KBLK * sg.v_sn;
-      }
-      kreg[i] = *(const bf16x8*)kp[i];
-      vreg[i] = *(const bf16x8*)vp[i];
-    }
-  };
-  auto lstore = [&](char* slotp) {
-#pragma unroll
-    for (int i = 0; i < CH_PER_THREAD; ++i) {
-      *(bf16x8*)(slotp + k_off[i]) = kreg[i];
-      *(bf16x8*)(slotp + v_off[i]) = vreg[i];
-    }
-  };
-
-  gload(0);
-  lstore(smem);
-  __syncthreads();
-
-  const float c = d.scale * 1.4426950408889634f;
-  float m_run = -1e30f, l_run = 0.f;
-  f32x16 o[2], lsum;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    o[0][i] = 0.f;
-    o[1][i] = 0.f;
-    lsum[i] = 0.f;
-  }
-  const int g = lane >> 4;
-  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
-  const int tcol = 16 * (g & 1) + 4 * (lane & 3);
-  f32x16 negm;
-  float thr = -INFINITY;
-  if constexpr (CINIT) {
-    m_run = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) negm[i] = 0.f;
-  }
-
-  for (int ti = 0; ti < ntiles; ++ti) {
-    const char* Kl = smem + (ti & 1) * STAGE_BYTES;
-    const bool has_next = ti + 1 < ntiles;
-    if (has_next) gload(ti + 1);
-    if constexpr (CINIT) {
-      Seg sg = tile_seg(d, ti, tiles1, b, h);
-      const int lim = sg.n - sg.key0;
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        f32x16 sh;
-        qk_half_ci(Kl, kh, qf, negm, sh, lane);
-        if (lim < KBLK) mask_half(sh, lim, kh, hl);
-        bf16x8 pf[2];
-        softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf);
-        pv_half(Kl + K_TILE_BYTES, kh, pf, o, trow, tcol);
-      }
-      if (has_next) lstore(smem + ((ti + 1) & 1) * STAGE_BYTES);
-      __syncthreads();
-      continue;
-    }
-    if constexpr (HALF) {
-      Seg sg = tile_seg(d, ti, tiles1, b, h);
-      const int lim = sg.n - sg.key0;
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        f32x16 sh;
-        qk_half(Kl, kh, qf, sh, lane);
-        if (lim < KBLK) mask_half(sh, lim, kh, hl);
-        bf16x8 pf[2];
-        softmax_half(sh, m_run, l_run, o, pf, c);
-        pv_half(Kl + K_TILE_BYTES, kh, pf, o, trow, tcol);
-      }
-      if (has_next) lstore(smem + ((ti + 1) & 1) * STAGE_BYTES);
-      __syncthreads();
-      continue;
-    }
-    f32x16 s[2];
-    qk_tile<PRE>(Kl, qf, s, lane);
-    {
-      Seg sg = tile_seg(d, ti, tiles1, b, h);
-      const int lim = sg.n - sg.key0;
-      if (lim < KBLK) mask_tail(s, lim, hl);
-    }
-    bf16x8 pf[4];
-    if constexpr (RS) {
-      softmax_tile_rs(s, m_run, o, lsum, pf, c);
-      pv_tile_rs(Kl + K_TILE_BYTES, pf, o, lsum, trow, tcol);
-    } else {
-      softmax_tile(s, m_run, l_run, o, pf, c);
-      pv_tile(Kl + K_TILE_BYTES, pf, o, trow, tcol);
-    }
-    if (has_next) lstore(smem + ((ti + 1) & 1) * STAGE_BYTES);
-    __syncthreads();
-  }
-
-  if constexpr (RS)
-    store_out(d, o, lsum[0], q, b, h, hl, false);
-  else
-    store_out(d, o, l_run, q, b, h, hl);
-}
-
-
 // V^T fragments for one 32-key half from the swizzled V image (vo[dh]: this lane's byte offset of its first
-// 4-row block in the 16-key slab, constant over the slabs because vswz depends only on row bit 1)
-VP_DEV void pv_half_x(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)[2], const int (&vo)[2]) {
+// 4-row block in the 16-key slab, constant over the slabs because vswz depends only on row bit 1); RS: the row-sum
+// MFMA per 16-key slab (sel = the 0/1 selector operand, lsum its accumulator)
+template <bool RS>
+VP_DEV void pv_half(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)[2], const int (&vo)[2],
+                    const bf16x8& sel, f32x4& lsum) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int ks = kh * 2 + j;
@@ -620,6 +251,10 @@ VP_DEV void pv_half_x(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)
       const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[j], o[dh], 0, 0, 0);
     }
+    // row sums: the P^T operand read as the B operand of a 16x16x32 MFMA (lane l: column l % 16, K-block l / 16),
+    // whose column n then holds query n's 16 keys in K-blocks 0 / 2 and query n + 16's in blocks 1 / 3; the
+    // selector keeps blocks 0 / 2 in rows 0-7 and blocks 1 / 3 in rows 8-15 (see the kernel's `sel`)
+    if constexpr (RS) lsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf[j], lsum, 0, 0, 0);
   }
 }
 
@@ -635,8 +270,7 @@ struct AttnSplit {
 };
 
 // O^T accumulator layout of one lane (store_out): dim d = dh*32 + 8*gq + 4*hl + r  <->  o[dh][4*gq + r]
-VP_DEV void store_partial(float* rec, const f32x16 (&o)[2], float m_run, float l_run, int hl) {
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+VP_DEV void store_partial(float* rec, const f32x16 (&o)[2], float m_run, float l_tot, int hl) {
 #pragma unroll
   for (int dh = 0; dh < 2; ++dh)
 #pragma unroll
@@ -652,25 +286,25 @@ VP_DEV void store_partial(float* rec, const f32x16 (&o)[2], float m_run, float l
 
 // one thread per (tail block, query): merge the nsplit partials and store like store_out
 __global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d, int t_base, int ntail, int nsplit,
-                                                           int QB, const float* __restrict__ ws) {
+                                                           int qb_size, const float* __restrict__ ws) {
   const int gid = blockIdx.x * 256 + threadIdx.x;
-  if (gid >= ntail * QB) return;
-  const int j = gid / QB, qi = gid - j * QB;
+  if (gid >= ntail * qb_size) return;
+  const int j = gid / qb_size, qi = gid - j * qb_size;
   const int t = t_base + j;
-  const int nqb = (d.Nq + QB - 1) / QB;
+  const int nqb = (d.Nq + qb_size - 1) / qb_size;
   const int bh = t / nqb, qb = t - bh * nqb;
   const int b = bh / d.H, h = bh - b * d.H;
-  const int q = qb * QB + qi;
+  const int q = qb * qb_size + qi;
   if (q >= d.Nq) return;
-  const float* rec0 = ws + ((int64_t)j * nsplit * QB + qi) * 66;
+  const float* rec0 = ws + ((int64_t)j * nsplit * qb_size + qi) * 66;
   float mx = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, rec0[(int64_t)s * QB * 66 + 64]);
+  for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, rec0[(int64_t)s * qb_size * 66 + 64]);
   float acc[64];
 #pragma unroll
   for (int e = 0; e < 64; ++e) acc[e] = 0.f;
   float l = 0.f;
   for (int s = 0; s < nsplit; ++s) {
-    const float* rec = rec0 + (int64_t)s * QB * 66;
+    const float* rec = rec0 + (int64_t)s * qb_size * 66;
     const float w = __builtin_amdgcn_exp2f(rec[64] - mx);
     l += rec[65] * w;
 #pragma unroll
@@ -701,22 +335,15 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d,
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// LDS-DMA kernel: NW waves x 32 queries, KB-key tiles (KB = 64 or 128) in a RING-slot LDS ring filled by
-// global_load_lds (no staging registers, no LDS write pass), C-init 32-key halves (see softmax_half_ci).  Tile t +
-// RING - 1 is issued at the top of tile t (its slot was released by the barrier that closed tile t-1); the bottom of
-// tile t waits (counted vmcnt) for tile t+1 only, then one barrier.  PRIO: the second half of the workgroup's waves
-// runs at s_setprio 1 (the arbitration loser of each SIMD pair, MI355X_MICROARCH.md "Two waves per SIMD" item 4).
+// The kernel: 8 waves x 32 queries, 128-key tiles in a 2-slot LDS ring filled by global_load_lds (no staging
+// registers, no LDS write pass), consumed as 32-key halves.  Tile t + 1 is issued at the top of tile t (its slot was
+// released by the barrier that closed tile t-1); the bottom of tile t waits for tile t+1, then one barrier.
+// TAIL: the grid-tail split instance (a separate symbol, so profiles list it apart).
 // ------------------------------------------------------------------------------------------------------------
-template <int NW, int OCC, int KB = 64, int RING = 2, bool PRIO = false, bool LAZY = false, bool PIPE = false,
-          bool TAIL = false>  // TAIL: the grid-tail split instance (a separate symbol, so profiles list it apart)
-__global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc d, const AttnSplit sp) {
-  constexpr int QB = NW * 32;
-  constexpr int KT = KB * 128;                  // bytes per K (or V) tile
-  constexpr int ST = 2 * KT;
-  constexpr int NP = KB / 8;                    // 1-KB DMA pieces (8 rows) per operand per tile
-  constexpr int PPW = (NP + NW - 1) / NW;       // pieces per wave (piece p -> wave p % NW)
-  constexpr int HALVES = KB / 32;
-  static_assert(RING == 2 || (RING == 3 && NP % NW == 0 && PPW <= 2), "RING");
+template <int MODE, bool TAIL = false>
+__global__ __launch_bounds__(NW * 64, 4) void attn_fwd(const vp_attn_desc d, const AttnSplit sp) {
+  constexpr bool BOUNDED = MODE == MODE_BOUNDED;
+  constexpr bool RS = BOUNDED;  // row sums on the matrix pipe
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -759,13 +386,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
     kch[i] = (lane & 7) ^ swz(prow[i]);
     vch[i] = (lane & 7) ^ vswz(prow[i]);
   }
-  // (the ring-3 slot offset goes through readfirstlane: otherwise the compiler hoists one address VGPR per LDS read
-  // and slot out of the loop and spills them)
-  auto slot_of = [&](int ti) {
-    return smem + (RING == 2 ? (ti & 1) * ST : __builtin_amdgcn_readfirstlane((ti % 3) * ST));
-  };
+  auto slot_of = [&](int ti) { return smem + (ti & 1) * ST; };
   auto issue = [&](int ti) {
-    const Seg sg = tile_seg<KB>(d, ti, tiles1, b, h);
+    const Seg sg = tile_seg(d, ti, tiles1, b, h);
     char* slot = slot_of(ti);
     const int last = sg.n - 1 - sg.key0;  // rows past the segment end re-read its last key (masked later)
     const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
@@ -774,7 +397,6 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int pc = wave + i * NW;
-      if (NP % NW != 0 && pc >= NP) break;  // wave-uniform
       const int r = min(prow[i], last);
       glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + pc * 1024);
       glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
@@ -796,79 +418,62 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_dma(const vp_attn_desc 
     o[1][i] = 0.f;
     negm[i] = 0.f;
   }
+  // row-sum selector of the 16x16x32 MFMA: lane l supplies A-row l % 16, K-block l / 16; rows 0-7 take K-blocks
+  // 0 / 2 (query n), rows 8-15 blocks 1 / 3 (query n + 16)
+  f32x4 lsum = {0.f, 0.f, 0.f, 0.f};
+  bf16x8 sel;
+  {
+    const bf16 one = f2bf((((lane >> 4) & 1) == 0) == ((lane & 15) < 8) ? 1.f : 0.f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sel[e] = one;
+  }
 
   // a wave whose 32 queries all lie past Nq (the last query block of a head) only helps with the DMA and the
   // barriers, leaving its SIMD to the co-resident workgroups
   const bool active = qb * QB + wave * 32 < d.Nq;  // wave-uniform
-  if constexpr (PRIO) {
-    if (__builtin_amdgcn_readfirstlane(tid) >= NW * 32) __builtin_amdgcn_s_setprio(1);
-  }
   issue(tbeg);
-  if constexpr (RING == 3) {
-    if (tbeg + 1 < tend) issue(tbeg + 1);
-  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   for (int ti = tbeg; ti < tend; ++ti) {
-    if (ti + RING - 1 < tend) issue(ti + RING - 1);
+    if (ti + 1 < tend) issue(ti + 1);
     const char* Kl = slot_of(ti);
-    const Seg sg = tile_seg<KB>(d, ti, tiles1, b, h);
+    const Seg sg = tile_seg(d, ti, tiles1, b, h);
     const int lim = sg.n - sg.key0;
-    if constexpr (PIPE) {
-      // software-pipelined halves: the QK^T MFMAs of half kh+1 are issued before the softmax of half kh, so one
-      // wave keeps the matrix pipe busy through its own VALU work (a rescale in half kh shifts the early S too)
-      if (active) {
-        f32x16 sn;
-        qk_half_ci2(Kl, 0, qf, negm, sn, lane);
-        if (lim < KB) mask_half(sn, lim, 0, hl);
-#pragma unroll
-        for (int kh = 0; kh < HALVES; ++kh) {
-          f32x16 sh = sn;
-          if (kh + 1 < HALVES) {
-            qk_half_ci2(Kl, kh + 1, qf, negm, sn, lane);
-            if (lim < KB) mask_half(sn, lim, kh + 1, hl);
-          }
-          bf16x8 pf[2];
-          if (thr == -INFINITY || !softmax_half_lazy(sh, l_run, pf)) {
-            if (kh + 1 < HALVES) softmax_half_ci<true>(sh, m_run, thr, l_run, negm, o, pf, sn);
-            else softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf);
-          }
-          pv_half_x(Kl + KT, kh, pf, o, vo);
-        }
-      }
-    } else
 #pragma unroll
     for (int kh = 0; kh < HALVES; ++kh) {
       if (!active) break;
       f32x16 sh;
       bf16x8 pf[2];
-      if constexpr (LAZY) {
-        qk_half_ci2(Kl, kh, qf, negm, sh, lane);
+      if constexpr (BOUNDED) {
+        qk_half_zero(Kl, kh, qf, sh, lane);
+        if (lim < KB) mask_half(sh, lim, kh, hl);
+        softmax_half_bounded(sh, pf);
+      } else {
+        qk_half_ci(Kl, kh, qf, negm, sh, lane);
         if (lim < KB) mask_half(sh, lim, kh, hl);
         // the first half sets m by the max path (thr = -inf); afterwards the lazy path, falling back when it must
         // (the lazy path leaves the scores intact, so the fallback needs no recompute)
         if (thr == -INFINITY || !softmax_half_lazy(sh, l_run, pf)) softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf);
-      } else {
-        qk_half_ci(Kl, kh, qf, negm, sh, lane);
-        if (lim < KB) mask_half(sh, lim, kh, hl);
-        softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf);
       }
-      pv_half_x(Kl + KT, kh, pf, o, vo);
+      pv_half<RS>(Kl + KT, kh, pf, o, vo, sel, lsum);
     }
-    // retire tile ti+1 (RING 3: tile ti+2's pieces, 2 per piece-row of this wave, may stay in flight)
-    if (RING == 3 && ti + 2 < tend) {
-      if constexpr (2 * PPW == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // retire tile ti+1
     __builtin_amdgcn_s_barrier();
+  }
+  // the row sum of this lane's query: split over the lane pair (l, l ^ 32) on the VALU; on the matrix pipe, query
+  // n < 16 sits in lane n, query n >= 16 in lane n + 16
+  float l_tot;
+  if constexpr (RS) {
+    const int qq = lane & 31;
+    l_tot = __shfl(lsum[0], qq < 16 ? qq : qq + 16, 64);
+  } else {
+    l_tot = l_run + __shfl_xor(l_run, 32, 64);
   }
   if (sp.nsplit > 1) {
     const int qi = wave * 32 + (lane & 31);
-    store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qi) * 66, o, m_run, l_run, hl);
+    store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qi) * 66, o, m_run, l_tot, hl);
   } else {
-    store_out(d, o, l_run, q, b, h, hl);
+    store_out(d, o, l_tot, q, b, h, hl, false);
   }
 }
 
@@ -1176,49 +781,20 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
 }  // namespace
 
 namespace {
-// kernel variants (A/B switch VP_ATTN_VARIANT for benchmarking): waves per workgroup, waves/SIMD occupancy target,
-// LDS bytes, key-tile size of the LDS-DMA kernels (0: the register-staged kernels), the grid-tail split instance
+// kernels: LAZY for unbounded scores, BOUNDED for VP_ATTN_BOUNDED_SCORES (env VP_ATTN_BOUNDED_MODE=lazy runs the
+// LAZY kernel there too: A/B)
 struct AttnVar {
   const void* fn;
-  int nw;
-  int lds;
-  int kb;
-  const void* fn_tail = nullptr;  // the TAIL instance (variants that take the grid-tail split)
+  const void* fn_tail;  // the grid-tail split instance
 };
 static const AttnVar attn_vars[] = {
-    {(const void*)attn_fwd_t<8, 2, 8>, 8, LDS_BYTES, 0},                      // 1: 8 waves x 32 queries, 2 waves/SIMD
-    {(const void*)attn_fwd_t<4, 2, 8>, 4, LDS_BYTES, 0},                      // 2: 4-wave workgroups, 2 per CU
-    {(const void*)attn_fwd_t<4, 3, 8>, 4, LDS_BYTES, 0},                      // 3: 4-wave workgroups, 3 per CU
-    {(const void*)attn_fwd_t<8, 4, 8, false, true>, 8, LDS_BYTES, 0},         // 4: half tiles, 4 waves/SIMD (default)
-    {(const void*)attn_fwd_t<4, 4, 8, false, true>, 4, LDS_BYTES, 0},         // 5: half tiles, 4-wave workgroups
-    {(const void*)attn_fwd_t<8, 2, 8, true>, 8, LDS_BYTES, 0},                // 6: row sums on the MFMA
-    {(const void*)attn_fwd_t<8, 4, 8, false, true, true>, 8, LDS_BYTES, 0},   // 7: C-init half tiles, 4 waves/SIMD
-    {(const void*)attn_fwd_t<4, 3, 8, false, true, true>, 4, LDS_BYTES, 0},   // 8: C-init half tiles, 4-wave WGs, 3/SIMD
-    {(const void*)attn_fwd_t<8, 2, 8, false, true, true>, 8, LDS_BYTES, 0},   // 9: C-init half tiles, 2 waves/SIMD
-    {(const void*)attn_fwd_dma<8, 4>, 8, 4 * KBLK * 128, 64},       // 10: LDS-DMA ring + C-init, 4 waves/SIMD
-    {(const void*)attn_fwd_dma<8, 2>, 8, 4 * KBLK * 128, 64},       // 11: LDS-DMA ring + C-init, 2 waves/SIMD
-    {(const void*)attn_fwd_dma<4, 4>, 4, 4 * KBLK * 128, 64},       // 12: LDS-DMA ring + C-init, 4-wave WGs
-    {(const void*)attn_fwd_dma<5, 4>, 5, 4 * KBLK * 128, 64},       // 13: 5-wave WGs (3 per CU: no grid tail at N=17776)
-    {(const void*)attn_fwd_dma<7, 4>, 7, 4 * KBLK * 128, 64},       // 14: 7-wave WGs (2 per CU)
-    {(const void*)attn_fwd_dma<8, 4, 64, 3>, 8, 6 * KBLK * 128, 64},            // 15: 3-slot ring (2 tiles ahead)
-    {(const void*)attn_fwd_dma<8, 4, 128, 2>, 8, 4 * 128 * 128, 128},           // 16: 128-key tiles
-    {(const void*)attn_fwd_dma<8, 4, 64, 2, true>, 8, 4 * KBLK * 128, 64},      // 17: 10 + static prio for waves 4-7
-    {(const void*)attn_fwd_dma<8, 4, 64, 3, true>, 8, 6 * KBLK * 128, 64},      // 18: 15 + prio
-    {(const void*)attn_fwd_dma<8, 4, 64, 2, false, true>, 8, 4 * KBLK * 128, 64},  // 19: 10 + lazy max, no -m copies
-    {(const void*)attn_fwd_dma<8, 4, 64, 2, true, true>, 8, 4 * KBLK * 128, 64},   // 20: 19 + prio
-    {(const void*)attn_fwd_dma<8, 4, 64, 3, false, true>, 8, 6 * KBLK * 128, 64},  // 21: 19 + 3-slot ring
-    {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true>, 8, 4 * 128 * 128, 128,
-     (const void*)attn_fwd_dma<8, 4, 128, 2, false, true, false, true>},  // 22: 19 + 128-key tiles
-    {(const void*)attn_fwd_dma<8, 4, 64, 3, true, true>, 8, 6 * KBLK * 128, 64},   // 23: 21 + prio
-    {(const void*)attn_fwd_dma<8, 3, 128, 2, false, true, true>, 8, 4 * 128 * 128, 128},  // 24: 22 + pipelined halves, 3/SIMD
-    {(const void*)attn_fwd_dma<8, 4, 128, 2, false, true, true>, 8, 4 * 128 * 128, 128},  // 25: 24 at 4 waves/SIMD
-    {(const void*)attn_fwd_dma<8, 3, 128, 2, false, true>, 8, 4 * 128 * 128, 128},        // 26: 22 at 3 waves/SIMD
+    {(const void*)attn_fwd<MODE_LAZY>, (const void*)attn_fwd<MODE_LAZY, true>},
+    {(const void*)attn_fwd<MODE_BOUNDED>, (const void*)attn_fwd<MODE_BOUNDED, true>},
 };
 constexpr int ATTN_NVAR = sizeof(attn_vars) / sizeof(attn_vars[0]);
 
 struct AttnPlan {
   const AttnVar* v;
-  int QB;
   int64_t nblk;
   int ntail = 0, nsplit = 1;  // tail split: the last ntail blocks as ntail * nsplit key-range workgroups
   int64_t ws_bytes = 0;
@@ -1233,48 +809,49 @@ int attn_check(const vp_attn_desc* d) {
       (d->v_sb % 8) || (d->o_sb % 4))
     return VP_ERR_ARG;
   if (d->Nk2 > 0 && ((d->k2_sn % 8) || (d->v2_sn % 8) || (d->k2_sb % 8) || (d->v2_sb % 8))) return VP_ERR_ARG;
+  if (d->flags & ~VP_ATTN_BOUNDED_SCORES) return VP_ERR_ARG;
+  // the LDS-DMA source offsets are 32-bit: a tile's rows must lie within 2^31 bytes of its first row
+  if ((int64_t)KB * d->k_sn * 2 >= ((int64_t)1 << 31) || (int64_t)KB * d->v_sn * 2 >= ((int64_t)1 << 31))
+    return VP_ERR_ARG;
   return VP_OK;
 }
 
 int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   static bool attr_set = false;
-  static int slots[ATTN_NVAR] = {};
+  static int slots = 0;  // resident workgroups chip-wide (the same for every variant: 128 VGPRs, LDS_BYTES)
   if (!attr_set) {
     attr_set = true;
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     for (int i = 0; i < ATTN_NVAR; ++i) {
-      (void)hipFuncSetAttribute(attn_vars[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize, attn_vars[i].lds);
-      if (attn_vars[i].fn_tail != nullptr)
-        (void)hipFuncSetAttribute(attn_vars[i].fn_tail, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  attn_vars[i].lds);
-      int per_cu = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, attn_vars[i].fn, attn_vars[i].nw * 64,
-                                                       attn_vars[i].lds) != hipSuccess)
-        per_cu = 0;
-      slots[i] = per_cu * cus;
+      (void)hipFuncSetAttribute(attn_vars[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      (void)hipFuncSetAttribute(attn_vars[i].fn_tail, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, attn_vars[0].fn, NW * 64, LDS_BYTES) != hipSuccess)
+      per_cu = 0;
+    slots = per_cu * cus;
   }
-  const char* e = getenv("VP_ATTN_VARIANT");
-  int variant = e != nullptr ? atoi(e) : 0;
-  if (variant < 1 || variant > ATTN_NVAR) variant = DEFAULT_VARIANT;
-  pl.v = &attn_vars[variant - 1];
-  pl.QB = pl.v->nw * 32;
-  const int nqb = (d->Nq + pl.QB - 1) / pl.QB;
+  int variant = 0;
+  if (d->flags & VP_ATTN_BOUNDED_SCORES) {
+    const char* e = getenv("VP_ATTN_BOUNDED_MODE");
+    variant = (e != nullptr && e[0] == 'l') ? 0 : 1;
+  }
+  pl.v = &attn_vars[variant];
+  const int nqb = (d->Nq + QB - 1) / QB;
   pl.nblk = (int64_t)d->B * d->H * nqb;
   if (pl.nblk > 0x7fffffff) return VP_ERR_ARG;
-  const int sl = slots[variant - 1];
   const char* ns = getenv("VP_ATTN_NO_SPLIT");
-  if (pl.v->fn_tail != nullptr && sl > 0 && (ns == nullptr || ns[0] == '0')) {
-    const int tail = (int)(pl.nblk % sl);
-    const int ntile = (d->Nk + pl.v->kb - 1) / pl.v->kb + (d->Nk2 > 0 ? (d->Nk2 + pl.v->kb - 1) / pl.v->kb : 0);
-    if (tail > 0 && 2 * tail <= sl) {
-      const int S = min(min(8, sl / tail), ntile);
+  if (slots > 0 && (ns == nullptr || ns[0] == '0')) {
+    const int tail = (int)(pl.nblk % slots);
+    const int ntile = (d->Nk + KB - 1) / KB + (d->Nk2 > 0 ? (d->Nk2 + KB - 1) / KB : 0);
+    if (tail > 0 && 2 * tail <= slots) {
+      const int S = min(min(8, slots / tail), ntile);
       if (S >= 2) {
         pl.ntail = tail;
         pl.nsplit = S;
-        pl.ws_bytes = (int64_t)tail * S * pl.QB * 66 * 4;
+        pl.ws_bytes = (int64_t)tail * S * QB * 66 * 4;
       }
     }
   }
@@ -1303,18 +880,18 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   if (main_blocks > 0) {
     const AttnSplit none = {0, 1, nullptr};
     void* args[] = {(void*)d, (void*)&none};
-    le = hipLaunchKernel(v.fn, dim3((unsigned)main_blocks), dim3(v.nw * 64), args, v.lds, (hipStream_t)stream);
+    le = hipLaunchKernel(v.fn, dim3((unsigned)main_blocks), dim3(NW * 64), args, LDS_BYTES, (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
   }
   if (split) {
     const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace};
     void* args[] = {(void*)d, (void*)&sp};
-    le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.nw * 64), args, v.lds,
+    le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(NW * 64), args, LDS_BYTES,
                          (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
-    const int nthreads = pl.ntail * pl.QB;
+    const int nthreads = pl.ntail * QB;
     hipLaunchKernelGGL(attn_combine_kernel, dim3((nthreads + 255) / 256), dim3(256), 0, (hipStream_t)stream, *d,
-                       (int)main_blocks, pl.ntail, pl.nsplit, pl.QB, (const float*)workspace);
+                       (int)main_blocks, pl.ntail, pl.nsplit, QB, (const float*)workspace);
   }
   VP_CHECK_LAUNCH();
   return VP_OK;

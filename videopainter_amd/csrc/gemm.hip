@@ -66,30 +66,6 @@ VP_DEV bf16x8 lds_frag(const char* tile, int row, int chunk) {
   return *(const bf16x8*)(tile + row * 128 + ((chunk ^ swz(row)) << 4));
 }
 
-// ---- variant 2 main-loop pieces: BK = 32 half-steps, 4-slot LDS ring (128 KB), 3 half-steps of LDS-DMA in flight
-// across raw barriers (counted vmcnt, never 0 in the loop: cdna_hip_programming.md §5 "Pipelining across barriers").
-constexpr int HK = 32;                      // k per half-step
-constexpr int HTILE = BM * HK * 2;          // 16 KB per operand half-tile
-constexpr int HSLOT = 2 * HTILE;            // A + B
-VP_DEV int swz64(int row) { return ((row >> 2) & 1) << 1; }  // conflict-free ds_read_b128 on 64-byte rows
-
-VP_DEV void stage_half(const bf16* const (&rows)[2], int K, int k0, char* tile, int wave, int lane) {
-  // wave-instruction i covers 16 rows x 64 B: lane l -> row (i*8 + wave)*16 + l/4, physical chunk l%4
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int rb = i * 8 + wave;
-    const int r = rb * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ swz64(r);
-    const int kc = k0 + c * 8;
-    const bf16* src = kc < K ? rows[i] + kc : g_zero_chunk;
-    __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(tile + rb * 1024), 16, 0, 0);
-  }
-}
-
-VP_DEV bf16x8 lds_frag64(const char* tile, int row, int chunk) {
-  return *(const bf16x8*)(tile + row * 64 + ((chunk ^ swz64(row)) << 4));
-}
-
 // MX-FP8 extension of the descriptor (zero for the bf16 path)
 struct MxExt {
   const uint8_t* a_scale;
@@ -359,7 +335,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (VAR == 5 || VAR == 7) {
+  if constexpr (VAR == 5 || VAR == 11) {
     // Quadrant-phase pipeline.  Each wave's 128x64 C block is split into 4 quadrants (64 rows x 32 cols); a K-tile
     // (BK = 64) runs as 4 phases of 16 MFMAs, in the quadrant order (A0,B0) (A0,B1) (A1,B1) (A1,B0) so each phase
     // needs ONE new operand subtile, which is read from LDS into registers during the previous phase.  The LDS
@@ -565,12 +541,22 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     };
+    // VAR 11 = VAR 5 with the two wave groups STAGGERED (cdna_hip_programming.md §5 "256² 8-phase template",
+    // MI355X_MICROARCH.md "Two waves per SIMD" item 9): every slot is [memory part] barrier [16 MFMAs] barrier and
+    // waves 4-7 (quadrant-row 1, one wave on each SIMD) run one barrier behind waves 0-3, so on every SIMD one
+    // wave's MFMA cluster overlaps its partner's LDS-DMA issue + ds_reads instead of both contending for the matrix
+    // pipe and then both stalling at the same barrier.  With the stagger a staged unit must be waited for one slot
+    // BEFORE the slot that reads it (the reader group may be a barrier ahead of the issuer group), so a slot waits
+    // for the unit issued 6 slots earlier (vmcnt(10)) and reads the one issued 7 earlier; a slot's own reads retire
+    // (lgkmcnt(0)) before its first barrier, so the v5 refill distance (one slot after the last read) still holds.
+    constexpr bool STAGGER = VAR == 11;
     FragA a0, a1;
     FragB bx, by;
     // prologue: slots -9..-2 (tiles 0 and 1, and nothing that overwrites tile 0's quadrant-row-0 A before it is
     // read), then the first subtiles, then slot -1 (A quadrant-row 0 of tile 2 into tile 0's region)
     for (int sl = -9; sl < -1; ++sl) issue_slot(sl);
-    if (exists(-2)) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // units of slots -9, -8 landed
+    if constexpr (STAGGER) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // slots -9..-7 landed (nk >= 8)
+    else if (exists(-2)) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // units of slots -9, -8 landed
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     TileScales scx = {0, 0, 0}, scy = {0, 0, 0};
@@ -580,6 +566,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     issue_slot(-1);
+    if constexpr (STAGGER) {
+      if (wr == 1) __builtin_amdgcn_s_barrier();  // wave-uniform: waves 4-7 start one barrier behind
+    }
     // one K-tile; PAR = k & 1 selects the LDS buffer and which of bx/by holds quadrant-col 0.  STEADY: every slot
     // of this tile issues a unit and 6 later units exist (k + 3 < nk), so the waits are the fixed vmcnt(12).
     auto tile_body = [&](int k, auto par_c, auto steady_c, FragB& b0, FragB& b1, const TileScales& sc,
@@ -589,7 +578,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
       constexpr bool STEADY = decltype(steady_c)::value;
       const int s0 = 4 * k;
       auto slot = [&](int sl) {
-        if constexpr (STEADY) {
+        if constexpr (STAGGER) {
+          // memory part, first half: wait for the unit the NEXT slot reads, then issue this slot's unit
+          if (STEADY || exists(sl - 1)) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          issue_slot(sl);
+        } else if constexpr (STEADY) {
           asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           int u;
@@ -602,25 +596,38 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
         }
       };
       const bool more = STEADY || k + 1 < nk;
+      auto cluster = [&]() {  // stagger: this slot's reads retire, then the MFMA cluster between two barriers
+        if constexpr (STAGGER) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+      };
+      auto cluster_end = [&]() {
+        if constexpr (STAGGER) __builtin_amdgcn_s_barrier();
+      };
       slot(s0);
       readB(b1, P{}, O{});
+      cluster();
       mma(a0, b0, Z{}, Z{}, sc.a0, sc.w);
-      if constexpr (VAR == 7) __builtin_amdgcn_s_barrier();  // phase-aligned waves (A/B)
+      cluster_end();
       slot(s0 + 1);
       readA(a1, P{}, O{});
+      cluster();
       mma(a0, b1, Z{}, O{}, sc.a0, sc.w);
-      if constexpr (VAR == 7) __builtin_amdgcn_s_barrier();  // phase-aligned waves (A/B)
+      cluster_end();
       slot(s0 + 2);
       if (more) {
         readA(a0, NP{}, Z{});
         readS(scn, k + 1);
       }
+      cluster();
       mma(a1, b1, O{}, O{}, sc.a1, sc.w);
-      if constexpr (VAR == 7) __builtin_amdgcn_s_barrier();  // phase-aligned waves (A/B)
+      cluster_end();
       slot(s0 + 3);
       if (more) readB(b1, NP{}, Z{});  // b1's registers carry the next tile's quadrant-col 0
+      cluster();
       mma(a1, b0, O{}, Z{}, sc.a1, sc.w);
-      if constexpr (VAR == 7) __builtin_amdgcn_s_barrier();  // phase-aligned waves (A/B)
+      cluster_end();
     };
     using T_ = std::integral_constant<bool, true>;
     using F_ = std::integral_constant<bool, false>;
@@ -634,45 +641,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     if (k + 1 < nk) tile_body(k + 1, O{}, F_{}, by, bx, scy, scx);
     if (k + 2 < nk) tile_body(k + 2, Z{}, F_{}, bx, by, scx, scy);
     if (k + 3 < nk) tile_body(k + 3, O{}, F_{}, by, bx, scy, scx);
+    if constexpr (STAGGER) {
+      if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the groups (equal barrier counts)
+    }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if constexpr (FP8) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");  // asm MFMA results
     __syncthreads();
-  } else if constexpr (VAR == 4) {
-    // VAR 1 with both k-halves' fragments read right after the barrier (24 reads in flight, 96 VGPRs), so the
-    // second half's LDS latency hides under the first half's 32 MFMAs
-    const int nk = (d.K + BK - 1) / BK;
-    stage_tile(arow, d.K, 0, smem, wave, lane);
-    stage_tile(wrow, d.K, 0, smem + TILE_BYTES, wave, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      char* cur = smem + (kt & 1) * STAGE_BYTES;
-      const char* As = cur;
-      const char* Bs = cur + TILE_BYTES;
-      bf16x8 af[2][FM], wf[2][FN];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int ch = ks * 4 + (lane >> 4);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) wf[ks][j] = lds_frag(Bs, wc * WN + j * 16 + (lane & 15), ch);
-#pragma unroll
-        for (int i = 0; i < FM; ++i) af[ks][i] = lds_frag(As, wr * WM + i * 16 + (lane & 15), ch);
-      }
-      if (kt + 1 < nk) {
-        char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
-        stage_tile(arow, d.K, (kt + 1) * BK, nxt, wave, lane);
-        stage_tile(wrow, d.K, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][j], af[ks][i], acc[j][i], 0, 0, 0);
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
   } else if constexpr (VAR == 1) {
     const int nk = (d.K + BK - 1) / BK;
     stage_tile(arow, d.K, 0, smem, wave, lane);
@@ -706,466 +680,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
-  } else if constexpr (VAR == 3) {
-    // BK = 32 half-steps through the 4-slot ring with the NEXT half-step's fragments read into registers while the
-    // current half-step's 32 MFMAs run, so no LDS latency sits between a barrier and the matrix pipe.  At the top of
-    // half-step t the wave waits for its own loads of t+1 (vmcnt(4): only t+2 still in flight), one barrier makes
-    // t+1 visible and retires every wave's reads of t-1, then the LDS-DMA for t+3 goes into t-1's slot.
-    const bf16* ah[2];
-    const bf16* wh[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = (i * 8 + wave) * 16 + (lane >> 2);
-      ah[i] = (const bf16*)d.A + (int64_t)min(m0 + r, d.M - 1) * d.lda;
-      const int n = min(n0 + r, d.N - 1);
-      const int sg = n / d.n_seg;
-      wh[i] = (const bf16*)d.W[sg] + (int64_t)(n - sg * d.n_seg) * d.K;
-    }
-    const int nh = (d.K + HK - 1) / HK;
-    auto issue = [&](int t) {
-      char* slot = smem + (t & 3) * HSLOT;
-      stage_half(ah, d.K, t * HK, slot, wave, lane);
-      stage_half(wh, d.K, t * HK, slot + HTILE, wave, lane);
-    };
-    const int ch = lane >> 4;
-    auto read = [&](int t, bf16x8 (&af)[FM], bf16x8 (&wf)[FN]) {
-      const char* As = smem + (t & 3) * HSLOT;
-      const char* Bs = As + HTILE;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = lds_frag64(As, wr * WM + i * 16 + (lane & 15), ch);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) wf[j] = lds_frag64(Bs, wc * WN + j * 16 + (lane & 15), ch);
-    };
-    auto mma = [&](const bf16x8 (&af)[FM], const bf16x8 (&wf)[FN]) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
-    };
-    issue(0);
-    if (nh > 1) issue(1);
-    if (nh > 2) issue(2);
-    if (nh > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // half-step 0 landed (1, 2 in flight)
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    bf16x8 afA[FM], wfA[FN], afB[FM], wfB[FN];
-    read(0, afA, wfA);
-    auto step = [&](int t, const bf16x8 (&afc)[FM], const bf16x8 (&wfc)[FN], bf16x8 (&afn)[FM],
-                    bf16x8 (&wfn)[FN]) {
-      // make t+1 visible, free slot (t-1)&3
-      if (t + 2 < nh) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (t + 3 < nh) issue(t + 3);
-      if (t + 1 < nh) read(t + 1, afn, wfn);
-      mma(afc, wfc);
-    };
-    int t = 0;
-    for (; t + 1 < nh; t += 2) {
-      step(t, afA, wfA, afB, wfB);
-      step(t + 1, afB, wfB, afA, wfA);
-    }
-    if (t < nh) step(t, afA, wfA, afB, wfB);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-  } else {
-    // per-lane half-tile source rows (2 LDS-DMA instructions per operand per half-step)
-    const bf16* ah[2];
-    const bf16* wh[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = (i * 8 + wave) * 16 + (lane >> 2);
-      ah[i] = (const bf16*)d.A + (int64_t)min(m0 + r, d.M - 1) * d.lda;
-      const int n = min(n0 + r, d.N - 1);
-      const int sg = n / d.n_seg;
-      wh[i] = (const bf16*)d.W[sg] + (int64_t)(n - sg * d.n_seg) * d.K;
-    }
-    const int nh = (d.K + HK - 1) / HK;
-    auto issue = [&](int t) {
-      char* slot = smem + (t & 3) * HSLOT;
-      stage_half(ah, d.K, t * HK, slot, wave, lane);
-      stage_half(wh, d.K, t * HK, slot + HTILE, wave, lane);
-    };
-    issue(0);
-    if (nh > 1) issue(1);
-    if (nh > 2) issue(2);
-    for (int t = 0; t < nh; ++t) {
-      // retire half-step t (4 LDS-DMA per half-step per lane); keep the later ones in flight
-      if (t + 2 < nh) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (t + 1 < nh) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (t + 3 < nh) issue(t + 3);
-      const char* As = smem + (t & 3) * HSLOT;
-      const char* Bs = As + HTILE;
-      bf16x8 af[FM], wf[FN];
-      const int ch = lane >> 4;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = lds_frag64(As, wr * WM + i * 16 + (lane & 15), ch);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) wf[j] = lds_frag64(Bs, wc * WN + j * 16 + (lane & 15), ch);
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();  // all waves done with the ring before the epilogue reuses the LDS
   }
 
   gemm_epilogue<NTHREADS, FN, FM, WN, WM, FP8>(d, mx, acc, smem, m0, n0, wr, wc, lane, tid);
 }
 
 
-// ---- variant 10: the quadrant-phase pipeline (variant 5, bf16) as a PERSISTENT kernel ----
-// One workgroup per CU walks the tiles of its XCD's contiguous range (the grouped order of variant 5, so the 32
-// CUs of an XCD work on neighbouring tiles in lock step and share A / W panels in their L2).  What it removes is
-// the per-tile fixed cost of a one-tile workgroup (measured: ~13.6 us per 256x256 tile = 16 % at K = 3072 — every
-// CU stores its C tile and then loads the next tile's first K-tiles at the same moment, HBM-bound bursts, plus the
-// workgroup launch): here the next tile's first K-tile (4 units = LDS stage 0) is issued BEFORE the epilogue, whose
-// C image then goes through the other half of the LDS one 128-row half at a time; the next tile's second K-tile
-// follows the epilogue.  Waits: the first wait of a tile is vmcnt(8) (only the second K-tile's 8 LDS-DMAs may still
-// be in flight: loads complete in order, so this also holds if the epilogue's stores retire out of order).
-// A/B (tools/blas_calibration.py, interleaved): no gain over variant 5 (QKV / out / FF2 within +-2 %, FF1 with its
-// GELU epilogue -5 %): the per-tile cost it overlaps is small; kept as VP_GEMM_VARIANT=10, bit-equal to variant 5.
-template <int EPI>
-__global__ __launch_bounds__(NTHREADS, 2) void gemm_persist_kernel(const vp_gemm_desc d) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2;  // 0..1  (M)
-  const int wc = wave & 3;   // 0..3  (N)
-  constexpr int GROUP = 4;
-  const int tiles_m = (d.M + BM - 1) / BM;
-  const int tiles_n = (d.N + BN - 1) / BN;
-  const int T = tiles_m * tiles_n;
-  // this workgroup's tiles: XCD x (= blockIdx % 8) owns the contiguous logical range [xs, xs + xn); its
-  // nwg / 8 workgroups take every (nwg / 8)-th tile of it (the launcher makes nwg a multiple of 8)
-  const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8, per_xcd = gridDim.x / 8;
-  const int q8 = T / 8, r8 = T % 8;
-  const int xs = xcd * q8 + min(xcd, r8), xn = q8 + (xcd < r8 ? 1 : 0);
-  auto tile_mn = [&](int it, int& m0, int& n0) {
-    const int t = xs + it;
-    const int per_group = GROUP * tiles_n;
-    const int first_m = (t / per_group) * GROUP;
-    const int gsz = min(tiles_m - first_m, GROUP);
-    m0 = (first_m + ((t % per_group) % gsz)) * BM;
-    n0 = ((t % per_group) / gsz) * BN;
-  };
-  const int nk = d.K / BK;  // the launcher guarantees K % 64 == 0
-  // per-lane 32-bit source offsets of the 4 units (2 LDS-DMA instructions each) from wave-uniform bases
-  int uoff[4][2];
-  const char* ubase[4][2];
-  auto setup = [&](int m0, int n0) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int g = i * 8 + wave;
-        const int rb = (u < 2) ? (g >> 3) * 128 + u * 64 + (g & 7) * 8 : (g >> 2) * 64 + (u - 2) * 32 + (g & 3) * 8;
-        const int r = rb + (lane >> 3);
-        const int c = (lane & 7) ^ swz(r);
-        if (u < 2) {
-          ubase[u][i] = (const char*)d.A + (int64_t)m0 * d.lda * 2;
-          uoff[u][i] = (min(m0 + r, d.M - 1) - m0) * (int)d.lda * 2 + c * 16;
-        } else {
-          const int sg = __builtin_amdgcn_readfirstlane(min(n0 + rb, d.N - 1) / d.n_seg);
-          ubase[u][i] = (const char*)d.W[sg];
-          uoff[u][i] = ((min(n0 + r, d.N - 1) - sg * d.n_seg) * d.K) * 2 + c * 16;
-        }
-      }
-  };
-  auto issue_unit = [&](int u, int tile) {
-    char* base = smem + (tile & 1) * STAGE_BYTES + (u >= 2 ? TILE_BYTES : 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int g = i * 8 + wave;
-      const int rb = (u < 2) ? (g >> 3) * 128 + u * 64 + (g & 7) * 8 : (g >> 2) * 64 + (u - 2) * 32 + (g & 3) * 8;
-      glds16(ubase[u][i] + tile * 128, uoff[u][i], base + rb * 128);
-    }
-  };
-  auto slot_tile = [&](int sl, int& u) -> int {  // unit and K-tile issued by slot sl (sl >= -9)
-    const int k = (sl + 12) / 4 - 3;
-    const int p = sl - 4 * k;
-    u = p == 0 ? 2 : p == 1 ? 3 : p == 2 ? 1 : 0;
-    return p < 3 ? k + 2 : k + 3;
-  };
-  auto exists = [&](int sl) {
-    int u;
-    return slot_tile(sl, u) < nk;
-  };
-  auto issue_slot = [&](int sl) {
-    int u;
-    const int tile = slot_tile(sl, u);
-    if (tile < nk) issue_unit(u, tile);
-  };
-  const int lrow = lane & 15;
-  int lbase[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) lbase[ks] = lrow * 128 + (((ks * 4 + (lane >> 4)) ^ swz(lrow)) << 4);
-  auto readA = [&](bf16x8 (&a)[8], auto par_c, auto qm_c) {
-    constexpr int par = decltype(par_c)::value, qm = decltype(qm_c)::value;
-    const char* As = smem + par * STAGE_BYTES + (wr * WM + qm * 64) * 128;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[ks * 4 + i] = *(const bf16x8*)(As + lbase[ks] + i * 16 * 128);
-  };
-  auto readB = [&](bf16x8 (&bb)[4], auto par_c, auto qn_c) {
-    constexpr int par = decltype(par_c)::value, qn = decltype(qn_c)::value;
-    const char* Bs = smem + par * STAGE_BYTES + TILE_BYTES + (wc * WN + qn * 32) * 128;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bb[ks * 2 + j] = *(const bf16x8*)(Bs + lbase[ks] + j * 16 * 128);
-  };
-  f32x4 acc[FN][FM];
-  auto mma = [&](const bf16x8 (&a)[8], const bf16x8 (&bb)[4], auto qm_c, auto qn_c) {
-    constexpr int qm = decltype(qm_c)::value, qn = decltype(qn_c)::value;
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[qn * 2 + j][qm * 4 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[ks * 2 + j], a[ks * 4 + i],
-                                                                               acc[qn * 2 + j][qm * 4 + i], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  using Z = std::integral_constant<int, 0>;
-  using O = std::integral_constant<int, 1>;
-  using T_ = std::integral_constant<bool, true>;
-  using F_ = std::integral_constant<bool, false>;
-  bf16x8 a0[8], a1[8], bx[4], by[4];
-
-  int m0 = 0, n0 = 0;
-  if (slot < xn) {
-    tile_mn(slot, m0, n0);
-    setup(m0, n0);
-    for (int sl = -9; sl < -1; ++sl) issue_slot(sl);
-  }
-#pragma unroll 1
-  for (int it = slot; it < xn; it += per_xcd) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int i = 0; i < FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (exists(-2)) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // the first K-tile (4 units) landed
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    readA(a0, Z{}, Z{});
-    readB(bx, Z{}, Z{});
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    issue_slot(-1);
-    auto tile_body = [&](int k, auto par_c, auto steady_c, bf16x8 (&b0)[4], bf16x8 (&b1)[4]) {
-      using P = decltype(par_c);
-      using NP = std::integral_constant<int, 1 - P::value>;
-      constexpr bool STEADY = decltype(steady_c)::value;
-      const int s0 = 4 * k;
-      auto slotf = [&](int sl) {
-        if (STEADY || exists(sl - 1)) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if constexpr (STEADY) {
-          int u;
-          const int tile = slot_tile(sl, u);
-          issue_unit(u, tile);
-        } else {
-          issue_slot(sl);
-        }
-      };
-      const bool more = STEADY || k + 1 < nk;
-      slotf(s0);
-      readB(b1, P{}, O{});
-      mma(a0, b0, Z{}, Z{});
-      slotf(s0 + 1);
-      readA(a1, P{}, O{});
-      mma(a0, b1, Z{}, O{});
-      slotf(s0 + 2);
-      if (more) readA(a0, NP{}, Z{});
-      mma(a1, b1, O{}, O{});
-      slotf(s0 + 3);
-      if (more) readB(b1, NP{}, Z{});
-      mma(a1, b0, O{}, Z{});
-    };
-    int k = 0;
-    for (; k + 4 < nk; k += 2) {
-      tile_body(k, Z{}, T_{}, bx, by);
-      tile_body(k + 1, O{}, T_{}, by, bx);
-    }
-    if (k < nk) tile_body(k, Z{}, F_{}, bx, by);
-    if (k + 1 < nk) tile_body(k + 1, O{}, F_{}, by, bx);
-    if (k + 2 < nk) tile_body(k + 2, Z{}, F_{}, bx, by);
-    if (k + 3 < nk) tile_body(k + 3, O{}, F_{}, by, bx);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();  // the ring is free
-
-    // epilogue values in registers, then the next tile's first K-tile into stage 0 while the C image streams out
-    // through [STAGE_BYTES, STAGE_BYTES + 128 * CT_STRIDE) in two 128-row halves
-    bf16x4 pk[FN][FM];
-    epi_values<FN, FM, WN, WM, EPI, true>(d, acc, [&](int j, int i, const bf16x4& o) { pk[j][i] = o; }, m0, n0, wr,
-                                          wc, lane);
-    const int cm0 = m0, cn0 = n0;
-    const bool next = it + per_xcd < xn;
-    if (next) {
-      tile_mn(it + per_xcd, m0, n0);
-      setup(m0, n0);
-      for (int sl = -9; sl < -5; ++sl) issue_slot(sl);
-    }
-    char* img = smem + STAGE_BYTES;
-    const MxExt mx = {};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (wr == h) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int i = 0; i < FM; ++i) *(bf16x4*)epi_lds_addr<WN, WM>(img, j, i, h * WM, wr, wc, lane) = pk[j][i];
-      }
-      // LDS-only ordering: __syncthreads() would also wait for the in-flight LDS-DMA (vmcnt(0))
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      epi_rows_out<NTHREADS, false, EPI>(d, mx, img, h * WM, WM, cm0, cn0, tid);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-    if (next)
-      for (int sl = -5; sl < -1; ++sl) issue_slot(sl);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------------------
-// Variant 6: 4 waves, ONE per SIMD, 128x128 C block per wave (8x8 16x16x32 fragments = 256 accumulator registers,
-// in the AGPR half of the 512-register file a single wave per SIMD owns).  Same 256x256 tile, BK = 32 half-steps
-// through a 4-slot LDS ring filled by LDS-DMA two half-steps ahead; the next half-step's 16 fragments (64 VGPRs) are
-// read while the current one's 64 MFMAs run, so one barrier per 1024 MFMA-cycles (the 8-wave kernels pay one per
-// 256-512).  Needs K % 32 == 0 and 32-bit source offsets.
-// ------------------------------------------------------------------------------------------------------------
-constexpr int W4_THREADS = 256;
-constexpr int W4_WM = 128, W4_WN = 128, W4_FM = 8, W4_FN = 8;
-
-__global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const vp_gemm_desc d) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1;  // 0..1 (M)
-  const int wc = wave & 1;   // 0..1 (N)
-
-  const int tiles_m = (d.M + BM - 1) / BM;
-  const int tiles_n = (d.N + BN - 1) / BN;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GROUP = 8;
-  const int per_group = GROUP * tiles_n;
-  const int group_id = t / per_group;
-  const int first_m = group_id * GROUP;
-  const int gsz = min(tiles_m - first_m, GROUP);
-  const int tm = first_m + ((t % per_group) % gsz);
-  const int tn = (t % per_group) / gsz;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  // LDS-DMA pieces: a half-step slot holds A [256 rows][64 B] then W [256][64 B]; piece pc = 16 rows (1 KiB) ->
-  // wave-instruction i (0..7): operand i / 4, piece (i % 4) * 4 + wave; lane l -> row pc*16 + l/4, physical chunk
-  // l % 4 = logical chunk ^ swz64(row).  Per-lane 32-bit byte offsets from wave-uniform bases (row clamped).
-  int off[8];
-  const char* base[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int pc = (i & 3) * 4 + wave;
-    const int r = pc * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ swz64(r);
-    if (i < 4) {
-      base[i] = (const char*)d.A;
-      off[i] = min(m0 + r, d.M - 1) * (int)d.lda * 2 + c * 16;
-    } else {
-      const int sg = __builtin_amdgcn_readfirstlane(min(n0 + pc * 16, d.N - 1) / d.n_seg);
-      base[i] = (const char*)d.W[sg];
-      off[i] = (min(n0 + r, d.N - 1) - sg * d.n_seg) * d.K * 2 + c * 16;
-    }
-  }
-  const int nh = d.K / HK;
-  auto issue = [&](int h) {
-    char* slot = smem + (h & 3) * HSLOT;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) glds16(base[i] + h * 64, off[i], slot + (i >> 2) * HTILE + ((i & 3) * 4 + wave) * 1024);
-  };
-  const int ch = lane >> 4;
-  auto read = [&](int h, bf16x8 (&af)[W4_FM], bf16x8 (&wf)[W4_FN]) {
-    const char* As = smem + (h & 3) * HSLOT;
-    const char* Bs = As + HTILE;
-#pragma unroll
-    for (int i = 0; i < W4_FM; ++i) af[i] = lds_frag64(As, wr * W4_WM + i * 16 + (lane & 15), ch);
-#pragma unroll
-    for (int j = 0; j < W4_FN; ++j) wf[j] = lds_frag64(Bs, wc * W4_WN + j * 16 + (lane & 15), ch);
-  };
-  f32x4 acc[W4_FN][W4_FM];
-#pragma unroll
-  for (int j = 0; j < W4_FN; ++j)
-#pragma unroll
-    for (int i = 0; i < W4_FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const bf16x8 (&af)[W4_FM], const bf16x8 (&wf)[W4_FN]) {
-#pragma unroll
-    for (int j = 0; j < W4_FN; ++j)
-#pragma unroll
-      for (int i = 0; i < W4_FM; ++i)
-        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
-  };
-  issue(0);
-  if (nh > 1) issue(1);
-  if (nh > 2) issue(2);
-  if (nh > 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // half-step 0 landed (1, 2 in flight)
-  else if (nh > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  bf16x8 afA[W4_FM], wfA[W4_FN], afB[W4_FM], wfB[W4_FN];
-  read(0, afA, wfA);
-  // half-step h: wait for h+1 (only h+2 may stay in flight), one barrier publishes it (and every wave has long
-  // finished reading slot (h-1)&3: its fragments fed the previous half-step's MFMAs), DMA h+3 into that slot, read
-  // h+1's fragments, then the 64 MFMAs of h
-  auto step = [&](int h, const bf16x8 (&afc)[W4_FM], const bf16x8 (&wfc)[W4_FN], bf16x8 (&afn)[W4_FM],
-                  bf16x8 (&wfn)[W4_FN]) {
-    if (h + 1 < nh) {
-      if (h + 2 < nh) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (h + 3 < nh) issue(h + 3);
-      read(h + 1, afn, wfn);
-    }
-    mma(afc, wfc);
-  };
-  int h = 0;
-  for (; h + 1 < nh; h += 2) {
-    step(h, afA, wfA, afB, wfB);
-    step(h + 1, afB, wfB, afA, wfA);
-  }
-  if (h < nh) step(h, afA, wfA, afB, wfB);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();  // all waves done with the ring before the epilogue reuses the LDS
-  const MxExt mx = {};
-  gemm_epilogue<W4_THREADS, W4_FN, W4_FM, W4_WN, W4_WM, false>(d, mx, acc, smem, m0, n0, wr, wc, lane, tid);
-}
-
 }  // namespace
-
-// compute units of the current device (cached per device id)
-static int cu_count() {
-  static int cache[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cache[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cache[dev] = n;
-  }
-  return cache[dev];
-}
 
 extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   if (d == nullptr || d->A == nullptr || d->W[0] == nullptr || d->C == nullptr) return VP_ERR_ARG;
@@ -1193,102 +714,28 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_w4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<7>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<11>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5, false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5, false, 2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr_set = true;
   }
-  const char* e = getenv("VP_GEMM_VARIANT");  // A/B switch for benchmarking main-loop variants
-  int variant = e != nullptr ? atoi(e) : 5;
-  if (variant < 1 || variant > 10) variant = 5;
-  // 32-bit in-tile source offsets: the quadrant pipeline adds them to a 64-bit tile base (A) / segment base (W);
-  // variant 6 still offsets A from the matrix base
+  // main loops: 11 = the quadrant-phase pipeline with the two wave groups staggered (default: +5 % over 5 on every
+  // config-2 shape), 5 = the unstaggered pipeline (VP_GEMM_VARIANT=5, A/B), 1 = the 2-stage ring
+  // (K % 64 != 0, e.g. the patch-embed im2col K = 132)
+  const char* e = getenv("VP_GEMM_VARIANT");
+  int variant = e != nullptr ? atoi(e) : 11;
+  if (variant != 1 && variant != 5 && variant != 11) variant = 11;
+  // the quadrant pipeline adds 32-bit in-tile source offsets to a 64-bit tile base (A) / segment base (W)
   const bool w32 = (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
   const bool tile32 = (int64_t)BM * d->lda * 2 < ((int64_t)1 << 31) && w32;
-  const bool off32 = (int64_t)d->M * d->lda * 2 < ((int64_t)1 << 31) && w32;
-  if ((variant == 5 || variant == 7 || variant == 8 || variant == 9) && ((d->K % BK) != 0 || !tile32))
-    variant = 1;  // the quadrant pipeline needs whole K-tiles
-  if (variant == 6 && ((d->K % HK) != 0 || !off32 || (d->n_seg % 16) != 0)) variant = 1;
+  if (variant != 1 && ((d->K % BK) != 0 || !tile32)) variant = 1;  // needs whole K-tiles
+  if (variant == 11 && d->K < 8 * BK) variant = 5;                  // the staggered prologue assumes >= 8 K-tiles
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
-  if (variant == 10) {
-    // persistent: one workgroup per CU (a multiple of 8, so every XCD gets the same count), whole 256-column tiles
-    const int ncu = cu_count();
-    const int nwg = (tiles < ncu ? tiles : ncu) & ~7;
-    if ((d->K % BK) != 0 || !tile32 || (d->N % BN) != 0 || nwg < 8) {
-      variant = (d->K % BK) == 0 && tile32 ? 5 : 1;
-    } else {
-      static bool pattr = false;
-      if (!pattr) {
-        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_BIAS>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_BIAS_GELU>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_BIAS_SCALE>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_GATED>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_BIAS_ADDROWS>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)gemm_persist_kernel<VP_EPI_BIAS_QKNORM_ROPE>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        pattr = true;
-      }
-      const hipStream_t st = (hipStream_t)stream;
-      switch (d->epilogue) {
-        case VP_EPI_BIAS:
-          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_BIAS>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st, *d);
-          break;
-        case VP_EPI_BIAS_GELU:
-          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_BIAS_GELU>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st, *d);
-          break;
-        case VP_EPI_BIAS_SCALE:
-          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_BIAS_SCALE>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st, *d);
-          break;
-        case VP_EPI_GATED:
-          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_GATED>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st, *d);
-          break;
-        case VP_EPI_BIAS_ADDROWS:
-          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_BIAS_ADDROWS>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st, *d);
-          break;
-        default:
-          hipLaunchKernelGGL(gemm_persist_kernel<VP_EPI_BIAS_QKNORM_ROPE>, dim3(nwg), dim3(NTHREADS), LDS_BYTES, st,
-                             *d);
-          break;
-      }
-      VP_CHECK_LAUNCH();
-      return VP_OK;
-    }
-  }
-  if (variant == 8)  // v5 with 8 / 2 M-tiles per L2 group instead of 4 (A/B: within noise, FF2 -2 %; 16: -4..7 %)
-    hipLaunchKernelGGL((gemm_bf16_kernel<5, false, 8>), dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream,
-                       *d, mx);
-  else if (variant == 9)
-    hipLaunchKernelGGL((gemm_bf16_kernel<5, false, 2>), dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream,
-                       *d, mx);
-  else if (variant == 7)
-    hipLaunchKernelGGL(gemm_bf16_kernel<7>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
-  else if (variant == 6)
-    hipLaunchKernelGGL(gemm_w4_kernel, dim3(tiles), dim3(W4_THREADS), LDS_BYTES, (hipStream_t)stream, *d);
+  if (variant == 11)
+    hipLaunchKernelGGL(gemm_bf16_kernel<11>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
   else if (variant == 5)
     hipLaunchKernelGGL(gemm_bf16_kernel<5>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
-  else if (variant == 4)
-    hipLaunchKernelGGL(gemm_bf16_kernel<4>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
-  else if (variant == 3)
-    hipLaunchKernelGGL(gemm_bf16_kernel<3>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
-  else if (variant == 2)
-    hipLaunchKernelGGL(gemm_bf16_kernel<2>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
   else
     hipLaunchKernelGGL(gemm_bf16_kernel<1>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
   VP_CHECK_LAUNCH();

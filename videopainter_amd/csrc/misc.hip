@@ -194,6 +194,13 @@ __global__ void fill_normal_kernel(bf16* __restrict__ out, int64_t n, uint64_t s
 
 extern "C" int vp_abi_version(void) { return VP_ABI_VERSION; }
 
+// digest of the sources + flags this library was compiled from (set by videopainter_amd/build.py), checked at load
+// time against the sources next to it so a stale library never runs silently
+#ifndef VP_BUILD_DIGEST
+#define VP_BUILD_DIGEST "unknown"
+#endif
+extern "C" const char* vp_build_digest(void) { return VP_BUILD_DIGEST; }
+
 extern "C" void vp_struct_sizes(int64_t* out) {
   out[0] = (int64_t)sizeof(vp_gemm_desc);
   out[1] = (int64_t)sizeof(vp_attn_desc);

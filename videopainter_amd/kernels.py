@@ -293,55 +293,73 @@ def mx_mfma_probe(A: torch.Tensor, B: torch.Tensor, sa: torch.Tensor, sb: torch.
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, heads: int, *,
               k2: Optional[torch.Tensor] = None, v2: Optional[torch.Tensor] = None, scale: float = 0.125,
-              out_scale: float = 1.0, accumulate: bool = False) -> torch.Tensor:
-    """q, k, v, out: [B, N, heads*64] views (last dim contiguous, any row/batch stride)."""
-    for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
+              out_scale: float = 1.0, accumulate: bool = False, bounded_scores: bool = False) -> torch.Tensor:
+    """q, k, v, out: [B, N, heads*64] views (last dim contiguous, any row/batch stride); k2 / v2: an optional second
+    K/V segment of the same form.  The native side sees only pointers and strides, so every extent is checked here."""
+    segs = [(q, "q"), (k, "k"), (v, "v"), (out, "out")]
+    if (k2 is None) != (v2 is None):
+        raise ValueError("k2 and v2 must be given together")
+    if k2 is not None:
+        segs += [(k2, "k2"), (v2, "v2")]
+    for t, n in segs:
         _chk(t, n)
         if t.dim() != 3 or t.stride(-1) != 1 or t.shape[-1] != heads * 64:
             raise ValueError(f"{n} must be [B, N, heads*64] with a contiguous last dim, got {tuple(t.shape)}")
+        if t.shape[0] != q.shape[0]:
+            raise ValueError(f"{n} batch {t.shape[0]} != q batch {q.shape[0]}")
+    if out.shape[1] != q.shape[1]:
+        raise ValueError(f"out length {out.shape[1]} != q length {q.shape[1]}")
+    if k.shape[1] != v.shape[1] or k.shape[1] == 0:
+        raise ValueError("k and v lengths differ (or are empty)")
+    if k2 is not None and (k2.shape[1] != v2.shape[1] or k2.shape[1] == 0):
+        raise ValueError("k2 and v2 lengths differ (or are empty)")
     d = N.AttnDesc()
     d.B, d.H, d.Nq, d.head_dim = q.shape[0], heads, q.shape[1], 64
     d.Q, d.q_sb, d.q_sn = _p(q), q.stride(0), q.stride(1)
     d.K, d.V = _p(k), _p(v)
     d.k_sb, d.k_sn, d.v_sb, d.v_sn = k.stride(0), k.stride(1), v.stride(0), v.stride(1)
     d.Nk = k.shape[1]
-    if v.shape[1] != k.shape[1]:
-        raise ValueError("k and v lengths differ")
     if k2 is not None:
-        _chk(k2, "k2")
-        _chk(v2, "v2")
         d.K2, d.V2 = _p(k2), _p(v2)
         d.k2_sb, d.k2_sn, d.v2_sb, d.v2_sn = k2.stride(0), k2.stride(1), v2.stride(0), v2.stride(1)
         d.Nk2 = k2.shape[1]
     d.O, d.o_sb, d.o_sn = _p(out), out.stride(0), out.stride(1)
     d.scale, d.out_scale, d.accumulate = scale, out_scale, int(accumulate)
+    # bounded_scores: the caller guarantees |scale * q.k| * log2 e <= SCORE_BOUND_LOG2 (score_bound_log2)
+    d.flags = ATTN_BOUNDED_SCORES if bounded_scores else 0
     L = N.lib()
     nb = L.vp_attention_workspace_bytes(C.byref(d))
     if nb < 0:
         raise ValueError("invalid attention descriptor")
-    ws = _workspace(q.device, nb) if nb > 0 else None
+    # tail-split partials: taken from the caching allocator per call, so they are ordered on the launch stream
+    # (a caller may run attention on several streams at once)
+    ws = torch.empty(nb, device=q.device, dtype=torch.uint8) if nb > 0 else None
     ev = _t0("attention")
     N.check(L.vp_attention_fwd_bf16_ws(C.byref(d), _p(ws), nb, _stream()), "vp_attention_fwd_bf16_ws")
     _t1("attention", ev)
     return out
 
 
-_WS: dict = {}
-
-
-def _workspace(device, nbytes: int) -> torch.Tensor:
-    """A per-device scratch buffer reused across launches (stream-ordered: every user runs on the current stream)."""
-    key = (device.type, device.index)
-    ws = _WS.get(key)
-    if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(max(nbytes, 1 << 20), device=device, dtype=torch.uint8)
-        _WS[key] = ws
-    return ws
-
-
 # ---- fp8 attention (BASELINE config 5; formats in include/vp_hip.h) ----
 
 LOG2E = 1.4426950408889634
+ATTN_BOUNDED_SCORES = 1      # include/vp_hip.h VP_ATTN_BOUNDED_SCORES
+SCORE_BOUND_LOG2 = 60.0      # include/vp_hip.h VP_ATTN_SCORE_BOUND
+
+
+def ln_output_norm_bound(ln) -> float:
+    """Upper bound of the L2 norm of any output row of LayerNorm(64) `ln` (then rotated by RoPE, which preserves
+    it): x_hat has sum(x_hat^2) = 64 var / (var + eps) < 64, so |gamma * x_hat + beta| <= 8 max|gamma| + |beta|_2."""
+    w = ln.weight.detach().float()
+    b = ln.bias.detach().float()
+    return float(8.0 * w.abs().max() + b.norm())
+
+
+def score_bound_log2(norm_q, norm_k, scale: float) -> float:
+    """Bound of |scale * q.k| * log2 e over every query / key pair of a CogVideoX attention (q, k the outputs of
+    norm_q / norm_k + RoPE, attention_processor.py:2143-2154), with 3 % for the bf16 roundings of q, k and of the
+    pre-scaled Q fragments."""
+    return ln_output_norm_bound(norm_q) * ln_output_norm_bound(norm_k) * scale * LOG2E * 1.03
 
 
 def mx_mfma_probe32(A: torch.Tensor, B: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) -> torch.Tensor:

@@ -166,6 +166,25 @@ class ModelMixin(nn.Module):
     def expected_state_dict_shapes(self):
         return state_dict_shapes(dict(self.config), branch=self._is_branch)
 
+    def reset_parameters_(self, seed: int = 0):
+        """PyTorch's default module initialisation, as the reference modules get it in `__init__`: nn.Linear /
+        nn.Conv2d weight and bias U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (kaiming_uniform with a = sqrt 5), LayerNorm
+        weight 1 / bias 0; the positional-embedding buffer keeps its sin-cos initialisation.  Drawn on the host from a
+        seeded torch.Generator (the reference draws from the global RNG), then copied to the parameters' device."""
+        g = torch.Generator().manual_seed(seed)
+        with torch.no_grad():
+            for mod in self.modules():
+                if isinstance(mod, (Linear, Conv2dPatch)):
+                    fan_in = mod.weight[0].numel()
+                    bound = 1.0 / fan_in ** 0.5
+                    for t in (mod.weight, mod.bias):
+                        if t is not None:
+                            t.copy_((torch.rand(t.shape, generator=g) * 2 - 1) * bound)
+                elif isinstance(mod, LayerNorm):
+                    mod.weight.fill_(1.0)
+                    mod.bias.zero_()
+        return self
+
     def init_synthetic_weights_(self, seed: int = 0, host_exact: bool = False):
         """Fill every parameter with the deterministic synthetic distribution of `weights.param_std`.
 
