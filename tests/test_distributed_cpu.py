@@ -17,7 +17,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, method="scatter_allgather"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     from videopainter_amd.distributed import init, broadcast_module, max_over_ranks
     from videopainter_amd import CogVideoXTransformer3DModel
@@ -28,27 +28,96 @@ def _worker(rank, world, port, q):
     with torch.no_grad():
         for p in m.state_dict().values():
             p.copy_(torch.randn(p.shape) * (rank + 1))
-    broadcast_module(m, src=0, bucket_bytes=1 << 16)  # small buckets: exercises the multi-tensor flatten path
+    if rank == 0:
+        want = [p.clone() for p in m.state_dict().values()]
+    broadcast_module(m, src=0, bucket_bytes=1 << 16, method=method)  # small buckets: the multi-tensor path
     digest = float(sum(p.double().sum() for p in m.state_dict().values()))
+    if rank == 0:
+        assert all(torch.equal(a, b) for a, b in zip(want, m.state_dict().values()))
     t = max_over_ranks(1.0 + rank)
     q.put((rank, digest, t))
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_broadcast_and_max_over_ranks_gloo():
+@pytest.mark.parametrize("world,method", [(2, "scatter_allgather"), (3, "scatter_allgather"), (2, "broadcast")])
+def test_broadcast_and_max_over_ranks_gloo(world, method):
+    """Weight replication (both methods; world 3 exercises the padded shards) is an exact copy of rank 0's
+    weights on every rank, and the bench's timing rule takes the max over ranks."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, method)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in ps]
     for p in ps:
         p.join(60)
     res.sort()
-    assert res[0][1] == res[1][1], "ranks disagree after broadcast"
-    assert res[0][2] == res[1][2] == 2.0
+    assert all(r[1] == res[0][1] for r in res), "ranks disagree after replication"
+    assert all(r[2] == float(world) for r in res)
+
+
+def _bench_worker(rank, world, port, mode, q):
+    """bench.py's rank logic (clip assignment, warm-up + barrier-bracketed timed steps, max over ranks, whole-job
+    value) with the toy window step instead of the HIP model (GPU-free)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import bench
+    from videopainter_amd.distributed import init, barrier, max_over_ranks, CFGPair
+    init("gloo")
+    pair = CFGPair() if mode == "cfgpair" else None
+    clip = bench.clip_of(rank, mode)
+    clips = _toy_clips(max(1, world), 1)
+    g = torch.Generator().manual_seed(5 + clip)
+    x = clips[clip]["windows"][0]["latents"].clone()
+    halves = [0, 1] if pair is None else [pair.cfg_index]
+    state = {"x": x}
+
+    def one(i):
+        preds = torch.cat([torch.tanh(state["x"] * (1.0 + 0.1 * c) + i) for c in halves])
+        if pair is not None:
+            preds = pair.allgather(preds)
+        state["x"] = state["x"] + 0.1 * (preds[0:1] + 6.0 * (preds[1:2] - preds[0:1])) + 0.01 * torch.randn(
+            SHAPE, generator=g)
+
+    elapsed = bench.timed_steps(one, lambda: barrier(), warmup=2, steps=3)
+    emax = max_over_ranks(elapsed)
+    n_clips, value = bench.job_value(emax, 3, world, mode)
+    q.put((rank, clip, state["x"].clone(), elapsed, emax, n_clips, value))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["dp", "cfgpair"])
+def test_bench_rank_logic_gloo(mode):
+    """World size 2: dp gives each rank its own clip (2 clips), cfgpair puts both CFG halves of ONE clip on the pair
+    (latents bit-identical on both ranks, equal to the single-process B=2 run); value = clips x steps / max time."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bench_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in ps], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+    emax = max(r[3] for r in res)
+    for rank, clip, x, el, em, n_clips, value in res:
+        assert em == emax
+        assert n_clips == (1 if mode == "cfgpair" else 2)
+        assert abs(value - n_clips * 3 / emax) < 1e-12
+    if mode == "cfgpair":
+        assert res[0][1] == res[1][1] == 0 and torch.equal(res[0][2], res[1][2])
+        # the same clip stepped by one process at B=2
+        g = torch.Generator().manual_seed(5)
+        x = _toy_clips(world, 1)[0]["windows"][0]["latents"].clone()
+        for i in range(5):
+            preds = torch.cat([torch.tanh(x * (1.0 + 0.1 * c) + i) for c in (0, 1)])
+            x = x + 0.1 * (preds[0:1] + 6.0 * (preds[1:2] - preds[0:1])) + 0.01 * torch.randn(SHAPE, generator=g)
+        assert torch.equal(res[0][2], x)
+    else:
+        assert [r[1] for r in res] == [0, 1]
 
 
 # ------------------------------------------------------------------------------------------------------------------

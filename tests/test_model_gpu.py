@@ -1,9 +1,11 @@
 """Model-level parity of the HIP path against the reference's golden vectors (GPU only).
 
 Tolerance rule: the HIP path computes in bf16 (fp32 accumulation), the golden vectors are the
-reference in fp32.  For every case we run the CPU oracle in bf16 on the same inputs and require
-    rel_L2(HIP, golden_fp32) <= 2 * rel_L2(oracle_bf16, golden_fp32) + 2e-3
-i.e. the HIP path may not drift more than twice as far from fp32 as the reference itself does in bf16.
+reference in fp32.  For every case the reference's own bf16 drift is measured on the same inputs (the CPU oracle in
+bf16 for the small cases, the reference's own bf16 run for the full-size fixtures) and we require
+    rel_L2(HIP, golden_fp32) <= 1.25 * rel_L2(reference_bf16, golden_fp32) + 1e-3
+i.e. the HIP path may drift from fp32 at most a quarter further than the reference itself does in bf16 (measured:
+1.0-1.05x at full depth).  The fp8 path (config 5) has its own re-stated band, written at each test.
 """
 import os
 
@@ -25,8 +27,15 @@ def rel(a, b):
     return float((a - b).norm() / (b.norm() + 1e-30))
 
 
+GATE_MUL, GATE_ADD = 1.25, 1e-3
+
+
 def bound(oracle_bf16, gold):
-    return 2.0 * rel(oracle_bf16, gold) + 2e-3
+    return GATE_MUL * rel(oracle_bf16, gold) + GATE_ADD
+
+
+def gate(ref_drift: float) -> float:
+    return GATE_MUL * ref_drift + GATE_ADD
 
 
 @pytest.fixture(scope="module")
@@ -533,7 +542,7 @@ def test_config1_full_model_matches_reference():
     """BASELINE config 1 at full depth and width: the 42-layer 5b-I2V-shaped transformer + 2-layer branch at
     N = 226 + 1152, B = 2 (CFG), weights from the counter generator (device fill), against the REFERENCE's fp32
     forward of the same weights and inputs (tests/golden/config1.safetensors, made by make_golden.py config1).
-    Bound: 2x the reference's own bf16 drift from its fp32 result, + 2e-3."""
+    Bound: gate() of the reference's own bf16 drift from its fp32 result."""
     from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, device_scope
     from videopainter_amd.weights import synth_param
     from tests.golden.cases import config1_cfg, config1_inputs, CONFIG1_SEEDS
@@ -564,8 +573,8 @@ def test_config1_full_model_matches_reference():
     r1 = rel(bs[1].float().reshape(-1)[::997], g["branch.1.slice"])
     print(f"config 1 full model vs reference fp32: noise_pred {r:.3e} (reference bf16 {float(rb[0]):.3e}), "
           f"branch {r0:.3e} / {r1:.3e} (reference bf16 {float(rb[1]):.3e} / {float(rb[2]):.3e})")
-    assert r <= 2 * float(rb[0]) + 2e-3
-    assert r0 <= 2 * float(rb[1]) + 2e-3 and r1 <= 2 * float(rb[2]) + 2e-3
+    assert r <= gate(float(rb[0]))
+    assert r0 <= gate(float(rb[1])) and r1 <= gate(float(rb[2]))
     # config 5's fp8 path (QKV projection, attention, FeedForward in e4m3) at full depth, same reference:
     # re-stated tolerance 3x the reference's bf16 drift + 2e-2
     tr.enable_fp8()
@@ -582,3 +591,122 @@ def test_config1_full_model_matches_reference():
     assert r8 <= 3 * float(rb[0]) + 2e-2
     del tr, br, bs, o, bs8, o8
     torch.cuda.empty_cache()
+
+
+@torch.no_grad()
+def test_config2_full_model_matches_reference():
+    """BASELINE config 2 — the shape bench.py times — at full size: the real 5b-I2V config (sample 60x90x49, learned
+    pos-emb), 42 layers + 2-layer branch, 49f 480x720 -> N = 226 + 17 550, B = 2 (CFG), against the REFERENCE's
+    fp32 forward of the same counter weights and inputs (tests/golden/config2.safetensors, SURVEY.md 8(c)(iv);
+    reference: pipeline_cogvideox_inpainting_i2v_branch_anyl.py:947-980, cogvideox_transformer_3d.py:472-646)."""
+    from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, device_scope
+    from tests.golden.cases import config2_cfg, config2_inputs, CONFIG2_SEEDS
+    g = load_file(os.path.join(GOLD, "config2.safetensors"))
+    tcfg, bcfg = config2_cfg()
+    with device_scope(dev):
+        tr = CogVideoXTransformer3DModel(**tcfg)
+        br = CogvideoXBranchModel(**bcfg)
+    tr.init_synthetic_weights_(CONFIG2_SEEDS[0])
+    br.init_synthetic_weights_(CONFIG2_SEEDS[1])
+    inp = config2_inputs()
+    bs = br(hidden_states=_d(inp["video"]), encoder_hidden_states=_d(inp["enc"]), branch_cond=_d(inp["branch_cond"]),
+            timestep=inp["timestep"].to(dev), image_rotary_emb=inp["rope"], return_dict=False)[0]
+    o = tr(hidden_states=_d(inp["hidden"]), encoder_hidden_states=_d(inp["enc"]), timestep=inp["timestep"].to(dev),
+           image_rotary_emb=inp["rope"], branch_block_samples=bs, branch_block_masks=_d(inp["mask"]),
+           return_dict=False)[0]
+    assert o.shape == (2, 13, 16, 60, 90)
+    rb = g["ref_bf16_rel"].double()
+    of = o.float().reshape(-1)
+    assert torch.isfinite(of).all()
+    r = rel(of[::7], g["slice"])
+    r_vs16 = rel(of[::7], g["bf16.slice"])
+    d = g["digest"].double()
+    r0 = rel(bs[0].float().reshape(-1)[::997], g["branch.0.slice"])
+    r1 = rel(bs[1].float().reshape(-1)[::997], g["branch.1.slice"])
+    print(f"config 2 full model vs reference fp32: noise_pred {r:.3e} (reference bf16 {float(rb[0]):.3e}; HIP vs "
+          f"reference bf16 {r_vs16:.3e}; |x| sum {float(of.double().abs().sum()):.6e} vs {float(d[1]):.6e}), "
+          f"branch {r0:.3e} / {r1:.3e} (reference bf16 {float(rb[1]):.3e} / {float(rb[2]):.3e})")
+    assert r <= gate(float(rb[0]))
+    assert r0 <= gate(float(rb[1])) and r1 <= gate(float(rb[2]))
+    assert abs(float(of.double().abs().sum()) / float(d[1]) - 1.0) < 2 * float(rb[0])
+    del tr, br, bs, o
+    torch.cuda.empty_cache()
+
+
+@torch.no_grad()
+def test_config5_length_block_matches_reference():
+    """BASELINE config 5's sequence length (720x1280: N = 226 + 46 800 = 47 026): one full-width block against the
+    reference's fp32 block (tests/golden/block5.safetensors), in bf16 (gate of the reference's own bf16 drift) and
+    with the config-5 fp8 path (QKV, attention, FeedForward in e4m3; re-stated band 6x the reference's bf16 drift
+    + 2e-2, as at N = 1378)."""
+    from videopainter_amd import device_scope
+    from videopainter_amd.transformer import CogVideoXBlock
+    c = full_block_case(latent=(13, 90, 160), key="fb5")
+    g = load_file(os.path.join(GOLD, "block5.safetensors"))
+    with device_scope(dev):
+        blk = CogVideoXBlock(dim=3072, num_attention_heads=48, attention_head_dim=64, time_embed_dim=512,
+                             attention_bias=True)
+    for k, p in blk.state_dict().items():
+        p.copy_(torch.from_numpy(c["weights"][k]))
+    run = lambda: blk(hidden_states=_d(c["h"]), encoder_hidden_states=_d(c["e"]), temb=_d(c["temb"]),  # noqa: E731
+                      image_rotary_emb=c["rope"])
+    h16, e16 = run()
+    flat16 = torch.cat([e16, h16], dim=1).reshape(-1).float().cpu()
+    rb = float(g["ref_bf16_rel"][0])
+    r16 = rel(flat16[::1999], g["slice"])
+    blk.enable_fp8_attention()
+    blk.enable_fp8_ffn()
+    blk.enable_fp8_qkv()
+    h8, e8 = run()
+    flat8 = torch.cat([e8, h8], dim=1).reshape(-1).float().cpu()
+    r8 = rel(flat8[::1999], g["slice"])
+    print(f"config-5 length block vs reference fp32: bf16 HIP {r16:.3e}, fp8 QKV+attention+FFN {r8:.3e} "
+          f"(reference bf16 {rb:.3e}); fp8 vs bf16 HIP {rel(flat8, flat16):.3e}")
+    assert r16 <= gate(rb)
+    assert r8 <= 6 * rb + 2e-2
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("mode", ["std", "prevclip", "resample0", "resample1"])
+def test_processor_call_path_matches_oracle(env, mode):
+    """The secondary drop-in boundary: `Attention.forward` -> `processor.__call__` exactly as
+    CogVideoXBlock calls it (attention_processor.py:452-496: kwargs the processor does not declare are dropped;
+    :2107-2209 standard incl. prev-clip, :2223-2304 ID-resample window 0 and prev-window), on block 0 of the tiny
+    model, against the oracle's attn_standard / attn_resample in fp32 (gate: the oracle's own bf16 drift)."""
+    from oracle import cogvideox_oracle as O
+    i = env["inp"]
+    resample = mode.startswith("resample")
+    attn = (env["trr"] if resample else env["tr"]).transformer_blocks[0].attn1
+    tsd, _ = tiny_weights()
+    sd32 = {k: torch.from_numpy(v) for k, v in tsd.items() if k.startswith("transformer_blocks.0.attn1.")}
+    sd16 = {k: v.to(torch.bfloat16) for k, v in sd32.items()}
+    B, T, D = 2, TINY_T, 128
+    Nv = i["rope"][0].shape[0]
+    gen = torch.Generator().manual_seed(17)
+    h = torch.randn(B, Nv, D, generator=gen)
+    e = torch.randn(B, T, D, generator=gen)
+    prev = torch.randn(B, T + Nv, D, generator=gen)
+    rmask = torch.zeros(B, T + Nv, dtype=torch.bool)
+    rmask[:, T:] = torch.rand(B, Nv, generator=gen) > 0.5
+    kw, okw = {}, {}
+    if mode in ("prevclip", "resample1"):
+        kw = dict(prev_hidden_states=_d(prev), prev_clip_weight=0.5, prev_resample_mask=rmask.to(dev))
+        okw = dict(prev_hidden_states=prev, prev_clip_weight=0.5, prev_resample_mask=rmask.float())
+    if resample:
+        kw["resample_mask"] = rmask.to(dev)
+    out_h, out_e = attn(hidden_states=_d(h), encoder_hidden_states=_d(e), image_rotary_emb=i["rope"],
+                        not_a_processor_kwarg=123, **kw)  # dropped by the signature filter, as in the reference
+    assert out_h.shape == (B, Nv, D) and out_e.shape == (B, T, D)
+    p = "transformer_blocks.0.attn1"
+    if resample:
+        ref = O.attn_resample(sd32, p, 2, h, e, i["rope"], rmask.float(), **okw)
+        o16 = O.attn_resample(sd16, p, 2, _b16(h), _b16(e), i["rope"], rmask.to(torch.bfloat16),
+                              **{k: (_b16(v) if torch.is_tensor(v) else v) for k, v in okw.items()})
+    else:
+        ref = O.attn_standard(sd32, p, 2, h, e, i["rope"], okw.get("prev_hidden_states"), okw.get("prev_clip_weight"))
+        o16 = O.attn_standard(sd16, p, 2, _b16(h), _b16(e), i["rope"],
+                              _b16(prev) if okw else None, okw.get("prev_clip_weight"))
+    for got, want, w16, name in ((out_h, ref[0], o16[0], "video"), (out_e, ref[1], o16[1], "text")):
+        r, r16 = rel(got, want), rel(w16, want)
+        print(f"processor {mode} {name}: HIP {r:.3e}, oracle bf16 {r16:.3e}")
+        assert r <= bound(w16, want), (mode, name, r, r16)

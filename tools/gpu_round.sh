@@ -15,6 +15,7 @@ for step in "$@"; do
     ktests) run ktests 600 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread -rA ;;
     mtests) run mtests 900 python -u -m pytest tests/test_model_gpu.py -v --timeout 300 --timeout-method thread -rA ;;
     gtests) run gtests 1150 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -rA ;;
+    ftests) run ftests 600 python -u -m pytest tests/test_attention_fp8_gpu.py tests/test_mx_gpu.py -v --timeout 300 --timeout-method thread -rA ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 900 python bench.py --steps 5 --warmup 2 ;;
     benchq) run bench 900 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;

@@ -52,25 +52,65 @@ def _buckets(tensors: List[torch.Tensor], limit: int):
 
 
 @torch.no_grad()
-def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0, bucket_bytes: int = BUCKET_BYTES) -> None:
-    """Broadcast tensors from `src` in flat buckets (one collective per <= bucket_bytes of same-dtype tensors)."""
+def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0, bucket_bytes: int = BUCKET_BYTES,
+                      method: str = "scatter_allgather") -> None:
+    """Replicate tensors from `src` in flat buckets (one exchange per <= bucket_bytes of same-dtype tensors).
+
+    method "broadcast": one RCCL broadcast per bucket (a pipelined ring: every byte crosses every hop, so a bucket
+    costs ~bytes / one link's bandwidth).  method "scatter_allgather" (default): the bucket is split into world
+    shards; the source sends shard r straight to rank r (point-to-point, all of the source's xGMI links at once) and
+    an all-gather then circulates the shards (each rank forwards (world-1)/world of the bucket) — on a fully
+    connected 8-GPU node the source no longer serialises the whole payload through one link.  Both are exact copies."""
     ts = [t for t in tensors if t.numel() > 0]
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
     for b in _buckets(ts, bucket_bytes):
-        if len(b) == 1:
+        if world == 1:
+            continue
+        if method == "broadcast" and len(b) == 1:
             dist.broadcast(b[0], src=src)
             continue
-        flat = torch.cat([t.reshape(-1) for t in b])
-        dist.broadcast(flat, src=src)
-        off = 0
-        for t in b:
-            n = t.numel()
-            t.copy_(flat[off:off + n].view_as(t))
-            off += n
+        n = sum(t.numel() for t in b)
+        per = (n + world - 1) // world
+        flat = torch.empty(per * world, dtype=b[0].dtype, device=b[0].device)
+        if rank == src:
+            off = 0
+            for t in b:
+                flat[off:off + t.numel()].copy_(t.reshape(-1))
+                off += t.numel()
+        if method == "broadcast":
+            dist.broadcast(flat, src=src)
+        elif method == "scatter_allgather":
+            shard = torch.empty(per, dtype=flat.dtype, device=flat.device)
+            if dist.get_backend() == "nccl":
+                # point-to-point scatter (RCCL has no native scatter): batched sends from the source
+                ops = []
+                if rank == src:
+                    for r in range(world):
+                        if r != src:
+                            ops.append(dist.P2POp(dist.isend, flat[r * per:(r + 1) * per], r))
+                    shard.copy_(flat[src * per:(src + 1) * per])
+                else:
+                    ops.append(dist.P2POp(dist.irecv, shard, src))
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+                dist.all_gather_into_tensor(flat, shard)
+            else:
+                dist.scatter(shard, list(flat.chunk(world)) if rank == src else None, src=src)
+                dist.all_gather(list(flat.chunk(world)), shard)
+        else:
+            raise ValueError(f"unknown replication method {method!r}")
+        if rank != src:
+            off = 0
+            for t in b:
+                t.copy_(flat[off:off + t.numel()].view_as(t))
+                off += t.numel()
 
 
-def broadcast_module(module: torch.nn.Module, src: int = 0, bucket_bytes: int = BUCKET_BYTES) -> None:
+def broadcast_module(module: torch.nn.Module, src: int = 0, bucket_bytes: int = BUCKET_BYTES,
+                     method: str = "scatter_allgather") -> None:
     """Replicate a model's parameters and buffers from rank `src` (config 3: weights over RCCL/xGMI)."""
-    broadcast_tensors(list(module.state_dict().values()), src=src, bucket_bytes=bucket_bytes)
+    broadcast_tensors(list(module.state_dict().values()), src=src, bucket_bytes=bucket_bytes, method=method)
 
 
 def max_over_ranks(value: float, device=None) -> float:
