@@ -157,3 +157,33 @@ def config2_inputs(dtype=torch.float32):
     cv = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dtype)  # noqa: E731
     return dict(hidden=cv(hidden), video=cv(video), mask=cv(mask), branch_cond=cv(branch_cond), enc=cv(enc),
                 timestep=torch.tensor([499, 499], dtype=torch.int64), rope=(cos, sin))
+
+
+# CogVideoX 3D causal VAE (reference autoencoder_kl_cogvideox.py:922-1376).  Tiny: 32 channels at every
+# level, 1 resnet per block; 5b-shaped: the real CogVideoX-5b VAE config (128/256/256/512, 3 resnets per block, 16
+# latent channels, scaling 0.7).  Weights from the counter generator under the diffusers state-dict names.
+VAE_TINY_CFG = dict(block_out_channels=(32, 32, 32, 32), layers_per_block=1, latent_channels=16, norm_num_groups=32,
+                    temporal_compression_ratio=4)
+VAE_5B_CFG = dict(block_out_channels=(128, 256, 256, 512), layers_per_block=3, latent_channels=16,
+                  norm_num_groups=32, temporal_compression_ratio=4, scaling_factor=0.7)
+VAE_SEEDS = (2001, 2002)
+
+
+def vae_inputs(frames: int = 17, height: int = 64, width: int = 96, latent_frames: int = 5, key: str = "vae"):
+    """Pixel video in [-1, 1] [1, 3, frames, H, W] (smooth + noise, like a normalised frame) and a latent
+    [1, 16, latent_frames, H/8, W/8] ~ N(0, 1)."""
+    n = 3 * frames * height * width
+    u = counter_uniform(f"{key}.video", n).reshape(1, 3, frames, height, width)
+    yy = np.linspace(-1, 1, height, dtype=np.float32)[None, None, None, :, None]
+    xx = np.linspace(-1, 1, width, dtype=np.float32)[None, None, None, None, :]
+    tt = np.linspace(0, 1, frames, dtype=np.float32)[None, None, :, None, None]
+    video = np.clip(0.6 * np.sin(3 * xx + 2 * yy + 4 * tt + np.arange(3, dtype=np.float32)[None, :, None, None, None])
+                    + 0.4 * (2 * u - 1), -1, 1).astype(np.float32)
+    z = synth_tensor(f"{key}.latent", (1, 16, latent_frames, height // 8, width // 8), bf16=False)
+    return torch.from_numpy(video), torch.from_numpy(z)
+
+
+def vae_weights(cfg: dict, seed: int):
+    """The counter-generator VAE state dict (bf16-valued fp32 numpy) the golden generator filled into the reference."""
+    from videopainter_amd.config import full_vae_config, vae_state_dict_shapes
+    return synth_state_dict(vae_state_dict_shapes(full_vae_config(cfg)), seed)

@@ -20,6 +20,7 @@ Fixtures (all fp32):
   config2.safetensors   — the same at the HEADLINE shape (BASELINE config 2: 49f 480x720, N = 17 776, B = 2), SURVEY
                           8(c)(iv): noise-prediction slice in fp32 and in the reference's own bf16 run, digest, branch
                           slices, bf16 drift.
+  vae.safetensors       — the reference 3D causal VAE (tiny and 5b-shaped), encode / decode at 17 and 9 frames.
   block5.safetensors    — one full-width block at config-5 length (720x1280: N = 47 026), fp32 + bf16 slices.
   config1.safetensors   — the WHOLE 5b-I2V-shaped transformer (42 layers) + 2-layer branch at config-1 shape, B=2:
                           noise prediction in fp32 (strided slice + digest) and the reference's own bf16 run's
@@ -345,6 +346,44 @@ def make_block5():
                                                         dtype=torch.float64),
                                  "ref_bf16_rel": torch.tensor([rel])})
 
+@torch.no_grad()
+def make_vae():
+    """The reference AutoencoderKLCogVideoX (tiny and 5b-shaped configs, counter weights): encode -> latent_dist
+    mean / logvar and decode of a fixed latent, at 17 frames 64x96 (two encoder frame batches: 9 + 8, so the causal
+    conv caches carry across) and 5 latent frames (two decoder batches: 3 + 2); plus the 9-frame / 3-latent-frame
+    single-batch case; fp32, and the 5b-shaped model's own bf16 drift.  vae.safetensors."""
+    import time
+    from diffusers import AutoencoderKLCogVideoX
+    from tests.golden.cases import VAE_TINY_CFG, VAE_5B_CFG, VAE_SEEDS, vae_inputs
+    out = {}
+    meta = {}
+    for tag, cfg, seed in (("tiny", VAE_TINY_CFG, VAE_SEEDS[0]), ("5b", VAE_5B_CFG, VAE_SEEDS[1])):
+        with torch.device("meta"):
+            vae = AutoencoderKLCogVideoX(**cfg).eval()
+        vae = _fill_synthetic(vae, seed)
+        for frames, lf in ((17, 5), (9, 3)):
+            x, z = vae_inputs(frames, 64, 96, lf, key=f"vae{frames}")
+            t0 = time.time()
+            dist = vae.encode(x).latent_dist
+            dec = vae.decode(z).sample
+            meta[f"{tag}.f{frames}.seconds_fp32"] = time.time() - t0
+            out[f"{tag}.f{frames}.mean"] = dist.mean
+            out[f"{tag}.f{frames}.logvar"] = dist.logvar
+            out[f"{tag}.f{frames}.decode"] = dec
+            print(f"vae {tag} f{frames}: mean {tuple(dist.mean.shape)} decode {tuple(dec.shape)} "
+                  f"{time.time() - t0:.0f}s", flush=True)
+            if tag == "5b":
+                vae16 = vae.to(torch.bfloat16)
+                d16 = vae16.encode(x.to(torch.bfloat16)).latent_dist
+                dec16 = vae16.decode(z.to(torch.bfloat16)).sample
+                rel = lambda a, b: float((a.double() - b.double()).norm() / b.double().norm())  # noqa: E731
+                out[f"{tag}.f{frames}.ref_bf16_rel"] = torch.tensor([rel(d16.mean.float(), dist.mean),
+                                                                    rel(dec16.float(), dec)])
+                print(f"  reference bf16 drift: mean {rel(d16.mean.float(), dist.mean):.3e} decode "
+                      f"{rel(dec16.float(), dec):.3e}", flush=True)
+                vae = vae16.float()
+    _save("vae.safetensors", out, meta)
+
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["tiny", "sched", "pipe", "block"]
@@ -354,6 +393,8 @@ if __name__ == "__main__":
         make_config2()
     if "block5" in which:
         make_block5()
+    if "vae" in which:
+        make_vae()
     if "tiny" in which:
         make_tiny()
     if "sched" in which:

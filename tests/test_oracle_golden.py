@@ -137,3 +137,26 @@ def test_full_width_block():
     d = g["digest"]
     # digest was reduced in fp32 by the generator; compare like with like
     assert abs(float(flat.norm()) - float(d[2])) / float(d[2]) < 1e-5
+
+
+@pytest.mark.parametrize("tag", ["tiny", "5b"])
+def test_vae_oracle_matches_reference(tag):
+    """oracle/vae_oracle.py against the reference AutoencoderKLCogVideoX run (tests/golden/vae.safetensors): encode
+    (two frame batches 9 + 8 with the causal caches carried across, and one batch of 9) and decode (latent batches
+    3 + 2, and 3), fp32."""
+    from oracle import vae_oracle as V
+    from tests.golden.cases import VAE_TINY_CFG, VAE_5B_CFG, VAE_SEEDS, vae_inputs, vae_weights
+    from videopainter_amd.config import full_vae_config
+    cfg, seed = (VAE_TINY_CFG, VAE_SEEDS[0]) if tag == "tiny" else (VAE_5B_CFG, VAE_SEEDS[1])
+    sd = {k: torch.from_numpy(v) for k, v in vae_weights(cfg, seed).items()}
+    cfg = full_vae_config(cfg)
+    g = load_file(os.path.join(GOLD, "vae.safetensors"))
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    for frames, lf in ((17, 5), (9, 3)):
+        x, z = vae_inputs(frames, 64, 96, lf, key=f"vae{frames}")
+        with torch.no_grad():
+            mean, logvar, _ = V.latent_dist(V.encode(sd, cfg, x))
+            dec = V.decode(sd, cfg, z)
+        assert rel(mean, g[f"{tag}.f{frames}.mean"]) < 1e-5
+        assert rel(logvar, g[f"{tag}.f{frames}.logvar"]) < 1e-5
+        assert rel(dec, g[f"{tag}.f{frames}.decode"]) < 1e-5

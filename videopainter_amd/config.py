@@ -119,6 +119,95 @@ def state_dict_shapes(cfg: dict, branch: bool = False) -> Dict[str, Tuple[int, .
     return s
 
 
+# `AutoencoderKLCogVideoX.__init__` DF/models/autoencoders/autoencoder_kl_cogvideox.py:921-954 (CogVideoX-5b's
+# checkpoint overrides scaling_factor = 0.7)
+VAE_DEFAULTS = dict(
+    in_channels=3, out_channels=3,
+    down_block_types=("CogVideoXDownBlock3D",) * 4, up_block_types=("CogVideoXUpBlock3D",) * 4,
+    block_out_channels=(128, 256, 256, 512), latent_channels=16, layers_per_block=3, act_fn="silu", norm_eps=1e-6,
+    norm_num_groups=32, temporal_compression_ratio=4, sample_height=480, sample_width=720, scaling_factor=1.15258426,
+    shift_factor=None, latents_mean=None, latents_std=None, force_upcast=True, use_quant_conv=False,
+    use_post_quant_conv=False,
+)
+
+
+def full_vae_config(kwargs: dict) -> dict:
+    base = dict(VAE_DEFAULTS)
+    unknown = set(kwargs) - set(base) - {"_class_name", "_diffusers_version", "_name_or_path"}
+    if unknown:
+        raise TypeError(f"unexpected VAE config keys: {sorted(unknown)}")
+    base.update({k: v for k, v in kwargs.items() if not k.startswith("_")})
+    base["block_out_channels"] = tuple(base["block_out_channels"])
+    return base
+
+
+def _vae_resnet_shapes(s: dict, p: str, cin: int, cout: int, zq: int = 0) -> None:
+    """`CogVideoXResnetBlock3D` :218-275 with temb_channels = 0 (no temb_proj) and the 1x1x1 SafeConv3d shortcut."""
+    def norm(n, c):
+        if zq:  # CogVideoXSpatialNorm3D :164-173
+            s[f"{p}.{n}.norm_layer.weight"] = (c,)
+            s[f"{p}.{n}.norm_layer.bias"] = (c,)
+            for cv in ("conv_y", "conv_b"):
+                s[f"{p}.{n}.{cv}.conv.weight"] = (c, zq, 1, 1, 1)
+                s[f"{p}.{n}.{cv}.conv.bias"] = (c,)
+        else:
+            s[f"{p}.{n}.weight"] = (c,)
+            s[f"{p}.{n}.bias"] = (c,)
+    norm("norm1", cin)
+    norm("norm2", cout)
+    s[f"{p}.conv1.conv.weight"] = (cout, cin, 3, 3, 3)
+    s[f"{p}.conv1.conv.bias"] = (cout,)
+    s[f"{p}.conv2.conv.weight"] = (cout, cout, 3, 3, 3)
+    s[f"{p}.conv2.conv.bias"] = (cout,)
+    if cin != cout:
+        s[f"{p}.conv_shortcut.weight"] = (cout, cin, 1, 1, 1)
+        s[f"{p}.conv_shortcut.bias"] = (cout,)
+
+
+def vae_state_dict_shapes(cfg: dict) -> Dict[str, Tuple[int, ...]]:
+    """State-dict keys / shapes of `AutoencoderKLCogVideoX` (encoder :635-704, decoder :769-845), registration order."""
+    ch = list(cfg["block_out_channels"])
+    nb, L, lpb = len(ch), cfg["latent_channels"], cfg["layers_per_block"]
+    s: Dict[str, Tuple[int, ...]] = {}
+    s["encoder.conv_in.conv.weight"] = (ch[0], cfg["in_channels"], 3, 3, 3)
+    s["encoder.conv_in.conv.bias"] = (ch[0],)
+    cout = ch[0]
+    for i in range(nb):
+        cin, cout = cout, ch[i]
+        for j in range(lpb):
+            _vae_resnet_shapes(s, f"encoder.down_blocks.{i}.resnets.{j}", cin if j == 0 else cout, cout)
+        if i < nb - 1:
+            s[f"encoder.down_blocks.{i}.downsamplers.0.conv.weight"] = (cout, cout, 3, 3)
+            s[f"encoder.down_blocks.{i}.downsamplers.0.conv.bias"] = (cout,)
+    for j in range(2):
+        _vae_resnet_shapes(s, f"encoder.mid_block.resnets.{j}", ch[-1], ch[-1])
+    s["encoder.norm_out.weight"] = (ch[-1],)
+    s["encoder.norm_out.bias"] = (ch[-1],)
+    s["encoder.conv_out.conv.weight"] = (2 * L, ch[-1], 3, 3, 3)
+    s["encoder.conv_out.conv.bias"] = (2 * L,)
+    rch = ch[::-1]
+    s["decoder.conv_in.conv.weight"] = (rch[0], L, 3, 3, 3)
+    s["decoder.conv_in.conv.bias"] = (rch[0],)
+    for j in range(2):
+        _vae_resnet_shapes(s, f"decoder.mid_block.resnets.{j}", rch[0], rch[0], zq=L)
+    cout = rch[0]
+    for i in range(nb):
+        cin, cout = cout, rch[i]
+        for j in range(lpb + 1):
+            _vae_resnet_shapes(s, f"decoder.up_blocks.{i}.resnets.{j}", cin if j == 0 else cout, cout, zq=L)
+        if i < nb - 1:
+            s[f"decoder.up_blocks.{i}.upsamplers.0.conv.weight"] = (cout, cout, 3, 3)
+            s[f"decoder.up_blocks.{i}.upsamplers.0.conv.bias"] = (cout,)
+    s["decoder.norm_out.norm_layer.weight"] = (rch[-1],)
+    s["decoder.norm_out.norm_layer.bias"] = (rch[-1],)
+    for cv in ("conv_y", "conv_b"):
+        s[f"decoder.norm_out.{cv}.conv.weight"] = (rch[-1], L, 1, 1, 1)
+        s[f"decoder.norm_out.{cv}.conv.bias"] = (rch[-1],)
+    s["decoder.conv_out.conv.weight"] = (cfg["out_channels"], rch[-1], 3, 3, 3)
+    s["decoder.conv_out.conv.bias"] = (cfg["out_channels"],)
+    return s
+
+
 def config_signature_check(cls, cfg: dict) -> None:
     sig = inspect.signature(cls.__init__)
     for k in cfg:
