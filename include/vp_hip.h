@@ -26,12 +26,12 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 6
+#define VP_ABI_VERSION 7
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
-/* sizeof of the descriptor structs as compiled into the library: out[0..4] = gemm, attn, dpm, gemm_mx, attn_fp8
- * (ABI check) */
+/* sizeof of the descriptor structs as compiled into the library: out[0..5] = gemm, attn, dpm, gemm_mx, attn_fp8,
+ * conv3d (ABI check) */
 void vp_struct_sizes(int64_t* out);
 
 /* ---------------------------------------------------------------------------------------------------------------
@@ -319,6 +319,79 @@ int vp_dpm_step_bf16(const vp_dpm_desc* d, void* stream);
 
 /* deterministic N(mean, std²) fill (splitmix64 + Box-Muller) for synthetic weights on the device */
 int vp_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float mean, float std, void* stream);
+
+/* ---- CogVideoX 3D causal VAE (DF/models/autoencoders/autoencoder_kl_cogvideox.py) ----
+ * Activations are channels-last bf16 [B, T, H, W, C] ("NDHWC"); a channel count that is not a power of two >= 8
+ * (the 3 pixel channels, ...) is zero-padded to one.  Conv weights are re-laid-out once at load time as
+ * [Cout, kt, kh, kw, Cin] (Cin padded like the activation) so every conv is an implicit GEMM whose K runs over
+ * (tap, channel) with channels contiguous. */
+#define VP_CONV_MAX_T 128
+typedef struct vp_conv3d_desc {
+  int32_t B, Cin, Cout;            /* Cin = the (padded, power of two >= 8) channel count of x / hist / weight rows */
+  int32_t Tout, Hout, Wout;        /* output grid */
+  int32_t Hin, Win;                /* physical input grid (before the nearest upsampling below) */
+  int32_t kt, kh, kw;              /* kernel (each 1 or 3); temporal stride 1 */
+  int32_t sh, sw;                  /* spatial stride (1 or 2) */
+  int32_t ph, pw;                  /* top / left zero padding in the upsampled grid (bottom / right: the bounds) */
+  int32_t uh, uw;                  /* nearest upsampling of the input grid (1 or 2), folded into the gather */
+  int32_t x_frames, hist_frames;   /* frames per batch element of x / hist */
+  int32_t ldy, ldr;                /* row (pixel) strides of y / resid in elements: multiples of 8, >= Cout */
+  int32_t tmap[VP_CONV_MAX_T];     /* virtual input frame v = t + dt (t: output frame, dt: temporal tap) ->
+                                      >= 0: frame of x, < 0: frame (-1 - value) of hist (the causal cache) */
+  const void* x;                   /* bf16 [B, x_frames, Hin, Win, Cin] */
+  const void* hist;                /* bf16 [B, hist_frames, Hin, Win, Cin] or NULL */
+  const void* w;                   /* bf16 [Cout, kt, kh, kw, Cin] */
+  const void* bias;                /* bf16 [Cout] or NULL */
+  const void* resid;               /* bf16 [B, Tout, Hout, Wout] rows of stride ldr, added after the bias, or NULL */
+  void* y;                         /* bf16 [B, Tout, Hout, Wout] rows of stride ldy; channels [Cout, ldy) get 0 */
+} vp_conv3d_desc;
+
+/* CogVideoXCausalConv3d.forward (:133-145; kt = 3, 1x1x1), the resnet conv_shortcut (:273), CogVideoXDownsample3D's
+ * stride-2 conv2d (DF/models/downsampling.py:344-353) and CogVideoXUpsample3D's nearest-upsample + conv2d
+ * (DF/models/upsampling.py:384-412) as one implicit-GEMM MFMA kernel. */
+int vp_conv3d_bf16(const vp_conv3d_desc* d, void* stream);
+
+/* nn.GroupNorm over [B, P, C] channels-last (groups of C / G consecutive channels), fp32 statistics (per-thread sums
+ * shifted by the group's first element, combined in fp64): stats = float [B, G, 2] (mean, rstd); partials: float
+ * workspace of vp_group_norm_workspace_floats(B, G) floats. */
+int64_t vp_group_norm_workspace_floats(int32_t B, int32_t G);
+int vp_group_norm_stats(const void* x, int32_t B, int64_t P, int32_t C, int32_t G, float eps, float* partials,
+                        float* stats, void* stream);
+
+/* y = act(GroupNorm(x) [* Ymod + Bmod]) over [B, T, H, W, C]: GroupNorm affine (gamma, beta bf16 [C]); with
+ * mod != NULL the CogVideoXSpatialNorm3D modulation (:175-188): mod = bf16 [B, Tz, Hz, Wz, 2C] holding
+ * conv_y(z) | conv_b(z) at the LATENT resolution (a 1x1x1 conv commutes with nearest resizing), gathered at the
+ * nearest source position: frame tzmap[t] (host array of T entries), row floor(h * (Hz / H)), column
+ * floor(w * (Wz / W)) (torch's nearest rule, float scale); act = SiLU if silu. */
+int vp_group_norm_apply_bf16(const void* x, void* y, int32_t B, int32_t T, int32_t H, int32_t W, int32_t C,
+                             int32_t G, const float* stats, const void* gamma, const void* beta, const void* mod,
+                             int32_t Tz, int32_t Hz, int32_t Wz, const int32_t* tzmap_host, int32_t silu,
+                             void* stream);
+
+/* CogVideoXDownsample3D's temporal compression (DF/models/downsampling.py:323-342): x [B, T, P, C] ->
+ * [B, T', P, C] with frame 0 kept when T is odd and every following pair averaged. */
+int vp_time_pool2_bf16(const void* x, void* y, int32_t B, int32_t T, int64_t P, int32_t C, void* stream);
+
+/* layout: NCDHW (fp32 or bf16) [B, C, T, H, W] <-> channels-last bf16 [B, T, H, W, Cpad] (zero padding channels);
+ * the reverse takes channels [c0, c0 + C) of rows of stride ldx and writes bf16 NCDHW */
+int vp_ncdhw_to_ndhwc_bf16(const void* x, int32_t x_is_f32, void* y, int32_t B, int32_t C, int32_t T, int32_t H,
+                           int32_t W, int32_t Cpad, void* stream);
+int vp_ndhwc_to_ncdhw_bf16(const void* x, int32_t ldx, void* y, int32_t B, int32_t C, int32_t T, int32_t H,
+                           int32_t W, int32_t c0, void* stream);
+
+/* DiagonalGaussianDistribution (DF/models/autoencoders/vae.py:768-789) on the encoder output [B, T, H, W] rows of
+ * stride ldp holding mean | logvar (2L channels): mean, logvar clamped to [-30, 20] as bf16 NCDHW [B, L, T, H, W];
+ * with noise != NULL (bf16 NCDHW) sample = mean + exp(0.5 logvar) * noise is written to `sample`. */
+int vp_latent_dist_bf16(const void* params, int32_t ldp, void* mean, void* logvar, const void* noise, void* sample,
+                        int32_t B, int32_t L, int32_t T, int32_t H, int32_t W, void* stream);
+
+/* AutoencoderKLCogVideoX.blend_v / blend_h (:1192-1206) on channels-last tiles, in place on b: with e = min(Ha, Hb,
+ * extent) (axis 0) rows y < e of b become a[row Ha - e + y] * (1 - y / e) + b[row y] * (y / e); axis 1 the same over
+ * columns (e = min(Wa, Wb, extent)).  a [B, T, Ha, Wa, C], b [B, T, Hb, Wb, C], both contiguous; axis 0 needs
+ * Wa == Wb, axis 1 Ha == Hb. */
+int vp_tile_blend_bf16(const void* a, void* b, int32_t B, int32_t T, int32_t Ha, int32_t Wa, int32_t Hb, int32_t Wb,
+                       int32_t C, int32_t axis, int32_t extent, void* stream);
+
 
 #ifdef __cplusplus
 }

@@ -190,3 +190,41 @@ def full_vae_config(kw: Optional[dict] = None) -> dict:
     c = dict(VAE_DEFAULTS)
     c.update(kw or {})
     return c
+
+
+def _blend(a, b, extent, dim):
+    """`blend_v` (dim 3) / `blend_h` (dim 4) :1192-1206, in place on b."""
+    e = min(a.shape[dim], b.shape[dim], extent)
+    for y in range(e):
+        if dim == 3:
+            b[:, :, :, y, :] = a[:, :, :, -e + y, :] * (1 - y / e) + b[:, :, :, y, :] * (y / e)
+        else:
+            b[:, :, :, :, y] = a[:, :, :, :, -e + y] * (1 - y / e) + b[:, :, :, :, y] * (y / e)
+    return b
+
+
+def tiled(sd: SD, cfg: dict, x, encode_: bool):
+    """`tiled_encode` :1208-1277 / `tiled_decode` :1279-1358 with the default tile sizes of the config
+    (sample_height // 2 x sample_width // 2, latent / 2^(levels - 1), overlap factors 1/6, 1/5)."""
+    nb = len(cfg["block_out_channels"])
+    ts_h, ts_w = cfg["sample_height"] // 2, cfg["sample_width"] // 2
+    tl_h, tl_w = int(ts_h / (2 ** (nb - 1))), int(ts_w / (2 ** (nb - 1)))
+    fh, fw = 1 / 6, 1 / 5
+    tin_h, tin_w, tout_h, tout_w = (ts_h, ts_w, tl_h, tl_w) if encode_ else (tl_h, tl_w, ts_h, ts_w)
+    ov_h, ov_w = int(tin_h * (1 - fh)), int(tin_w * (1 - fw))
+    be_h, be_w = int(tout_h * fh), int(tout_w * fw)
+    lim_h, lim_w = tout_h - be_h, tout_w - be_w
+    run = (lambda t: encode(sd, cfg, t)) if encode_ else (lambda t: decode(sd, cfg, t))
+    rows = [[run(x[:, :, :, i:i + tin_h, j:j + tin_w]) for j in range(0, x.shape[4], ov_w)]
+            for i in range(0, x.shape[3], ov_h)]
+    out = []
+    for i, row in enumerate(rows):
+        res = []
+        for j, tile in enumerate(row):
+            if i > 0:
+                tile = _blend(rows[i - 1][j], tile, be_h, 3)
+            if j > 0:
+                tile = _blend(row[j - 1], tile, be_w, 4)
+            res.append(tile[:, :, :, :lim_h, :lim_w])
+        out.append(torch.cat(res, dim=4))
+    return torch.cat(out, dim=3)

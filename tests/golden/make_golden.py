@@ -385,6 +385,31 @@ def make_vae():
     _save("vae.safetensors", out, meta)
 
 
+@torch.no_grad()
+def make_vae_tiled():
+    """The reference tiny VAE with tiling and slicing enabled (sample 128x192 -> 64x96 sample tiles, 8x12 latent
+    tiles, so both blend_v and blend_h run with extents > 1) on a B = 2 batch: encode -> mean / logvar of a 9-frame
+    128x192 video, decode of a [2, 16, 3, 16, 24] latent.  vae_tiled.safetensors."""
+    from diffusers import AutoencoderKLCogVideoX
+    from tests.golden.cases import VAE_TINY_CFG, VAE_SEEDS, vae_inputs
+    cfg = dict(VAE_TINY_CFG, sample_height=128, sample_width=192)
+    with torch.device("meta"):
+        vae = AutoencoderKLCogVideoX(**cfg).eval()
+    vae = _fill_synthetic(vae, VAE_SEEDS[0])
+    vae.enable_tiling()
+    vae.enable_slicing()
+    x0, z0 = vae_inputs(9, 128, 192, 3, key="vaet0")
+    x1, z1 = vae_inputs(9, 128, 192, 3, key="vaet1")
+    x, z = torch.cat([x0, x1]), torch.cat([z0, z1])
+    dist = vae.encode(x).latent_dist
+    dec = vae.decode(z).sample
+    print(f"vae tiled: mean {tuple(dist.mean.shape)} decode {tuple(dec.shape)}", flush=True)
+    # decode kept at every second row / column (1.5 MB); the shape (2, 3, 9, 140, 202) is the reference's own tiled
+    # crop arithmetic at this size, not 128 x 192
+    _save("vae_tiled.safetensors", {"mean": dist.mean, "logvar": dist.logvar, "decode_s2": dec[..., ::2, ::2],
+                                    "decode_shape": torch.tensor(dec.shape, dtype=torch.float32)})
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["tiny", "sched", "pipe", "block"]
     if "config1" in which:
@@ -395,6 +420,8 @@ if __name__ == "__main__":
         make_block5()
     if "vae" in which:
         make_vae()
+    if "vae_tiled" in which:
+        make_vae_tiled()
     if "tiny" in which:
         make_tiny()
     if "sched" in which:

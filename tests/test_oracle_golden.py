@@ -160,3 +160,22 @@ def test_vae_oracle_matches_reference(tag):
         assert rel(mean, g[f"{tag}.f{frames}.mean"]) < 1e-5
         assert rel(logvar, g[f"{tag}.f{frames}.logvar"]) < 1e-5
         assert rel(dec, g[f"{tag}.f{frames}.decode"]) < 1e-5
+
+
+def test_vae_tiled_oracle_matches_reference():
+    """Tiled + sliced encode / decode (tests/golden/vae_tiled.safetensors: tiny VAE, sample 128x192, B = 2)."""
+    from oracle import vae_oracle as V
+    from tests.golden.cases import VAE_TINY_CFG, VAE_SEEDS, vae_inputs, vae_weights
+    from videopainter_amd.config import full_vae_config
+    cfg = full_vae_config(dict(VAE_TINY_CFG, sample_height=128, sample_width=192))
+    sd = {k: torch.from_numpy(v) for k, v in vae_weights(VAE_TINY_CFG, VAE_SEEDS[0]).items()}
+    g = load_file(os.path.join(GOLD, "vae_tiled.safetensors"))
+    x0, z0 = vae_inputs(9, 128, 192, 3, key="vaet0")
+    x1, z1 = vae_inputs(9, 128, 192, 3, key="vaet1")
+    with torch.no_grad():
+        p = torch.cat([V.tiled(sd, cfg, x, True) for x in (x0, x1)])
+        mean, logvar, _ = V.latent_dist(p)
+        dec = torch.cat([V.tiled(sd, cfg, z, False) for z in (z0, z1)])
+    assert rel(mean, g["mean"]) < 1e-5 and rel(logvar, g["logvar"]) < 1e-5
+    assert tuple(dec.shape) == tuple(int(v) for v in g["decode_shape"])
+    assert rel(dec[..., ::2, ::2], g["decode_s2"]) < 1e-5

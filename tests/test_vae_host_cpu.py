@@ -1,0 +1,154 @@
+"""Host logic of videopainter_amd/vae.py on the CPU: the frame batching, causal-cache hand-over, tmaps, spatial-norm
+frame maps, resize folding and tile blend order — with every kernel entry point of `videopainter_amd.kernels`
+replaced, INSIDE THIS TEST ONLY, by a torch restatement of the kernel's documented contract (include/vp_hip.h).
+The product path has no such substitute: without the HIP library its calls raise.  Compared against the
+reference's fp32 outputs (tests/golden/vae*.safetensors) at a bf16-level tolerance."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+from safetensors.torch import load_file
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm())
+
+
+def _r(t):
+    return t.to(torch.bfloat16)
+
+
+def conv3d(x, w, bias, *, Tout, Hout, Wout, tmap, hist=None, stride=1, pad=0, up=1, resid=None, out=None, ldy=None):
+    B, xf, Hin, Win, Cin = x.shape
+    Cout, kt, kh, kw, _ = w.shape
+    frames = [x[:, f] if f >= 0 else hist[:, -1 - f] for f in tmap]
+    v = torch.stack(frames, 1).float()                       # [B, Tv, H, W, C]
+    if up > 1:
+        v = v.repeat_interleave(up, 2).repeat_interleave(up, 3)
+    v = v.permute(0, 4, 1, 2, 3)                             # NCDHW
+    Hu, Wu = v.shape[3], v.shape[4]
+    v = F.pad(v, (pad, max(0, (Wout - 1) * stride + kw - pad - Wu), pad, max(0, (Hout - 1) * stride + kh - pad - Hu)))
+    y = F.conv3d(v, w.float().permute(0, 4, 1, 2, 3), bias.float() if bias is not None else None,
+                 stride=(1, stride, stride))[:, :, :Tout, :Hout, :Wout]
+    y = _r(y).float()
+    if resid is not None:
+        y = y + resid[..., :Cout].float().permute(0, 4, 1, 2, 3)
+    y = y.permute(0, 2, 3, 4, 1)
+    ldy = ldy or (Cout + 7) // 8 * 8
+    return _r(F.pad(y, (0, ldy - Cout))).contiguous()
+
+
+def group_norm(x, gamma, beta, groups, eps, *, silu=False, mod=None, tzmap=None, out=None):
+    B, T, H, W, C = x.shape
+    y = F.group_norm(x.float().permute(0, 4, 1, 2, 3), groups, gamma.float(), beta.float(), eps)
+    if mod is not None:
+        Tz, Hz, Wz = mod.shape[1:4]
+        m = mod.float()[:, tzmap]
+        hi = [min(int(h * (Hz / H)), Hz - 1) for h in range(H)]
+        wi = [min(int(w * (Wz / W)), Wz - 1) for w in range(W)]
+        m = m[:, :, hi][:, :, :, wi].permute(0, 4, 1, 2, 3)
+        y = y * m[:, :C] + m[:, C:]
+    if silu:
+        y = F.silu(y)
+    return _r(y.permute(0, 2, 3, 4, 1)).contiguous()
+
+
+def time_pool2(x):
+    xf = x.float()
+    if x.shape[1] % 2:
+        y = torch.cat([xf[:, :1], (xf[:, 1::2] + xf[:, 2::2]) / 2], 1)
+    else:
+        y = (xf[:, 0::2] + xf[:, 1::2]) / 2
+    return _r(y).contiguous()
+
+
+def ncdhw_to_ndhwc(x, cpad):
+    y = x.float().permute(0, 2, 3, 4, 1)
+    return _r(F.pad(y, (0, cpad - y.shape[-1]))).contiguous()
+
+
+def ndhwc_to_ncdhw(x, channels, c0=0):
+    return x[..., c0:c0 + channels].permute(0, 4, 1, 2, 3).contiguous().to(torch.bfloat16)
+
+
+def latent_dist(params, L, noise=None):
+    p = params.float().permute(0, 4, 1, 2, 3)
+    mean, lv = _r(p[:, :L]), _r(p[:, L:2 * L].clamp(-30, 20))
+    if noise is None:
+        return mean, lv
+    return mean, lv, _r(p[:, :L] + torch.exp(0.5 * lv.float()) * noise.float())
+
+
+def tile_blend_(a, b, axis, extent):
+    d = 2 + axis
+    e = min(a.shape[d], b.shape[d], extent)
+    af, bf = a.float(), b.float()
+    for y in range(e):
+        if axis == 0:
+            b[:, :, y] = _r(af[:, :, a.shape[2] - e + y] * (1 - y / e) + bf[:, :, y] * (y / e))
+        else:
+            b[:, :, :, y] = _r(af[:, :, :, a.shape[3] - e + y] * (1 - y / e) + bf[:, :, :, y] * (y / e))
+    return b
+
+
+@pytest.fixture
+def mocked(monkeypatch):
+    from videopainter_amd import vae as V
+    for n, f in dict(conv3d=conv3d, group_norm=group_norm, time_pool2=time_pool2, ncdhw_to_ndhwc=ncdhw_to_ndhwc,
+                     ndhwc_to_ncdhw=ndhwc_to_ncdhw, latent_dist=latent_dist, tile_blend_=tile_blend_).items():
+        monkeypatch.setattr(V.K, n, f)
+    monkeypatch.setattr(V.AutoencoderKLCogVideoX, "_check", lambda self, t, what: None)
+    return V
+
+
+def _model(V, cfg, seed, **over):
+    from tests.golden.cases import vae_weights
+    m = V.AutoencoderKLCogVideoX(**dict(cfg, **over))
+    m.load_diffusers_state_dict({k: torch.from_numpy(v) for k, v in vae_weights(cfg, seed).items()})
+    return m
+
+
+def test_vae_host_logic_frame_batches_and_caches(mocked):
+    from tests.golden.cases import VAE_TINY_CFG, VAE_SEEDS, vae_inputs
+    g = load_file(os.path.join(GOLD, "vae.safetensors"))
+    m = _model(mocked, VAE_TINY_CFG, VAE_SEEDS[0])
+    for frames, lf in ((17, 5), (9, 3)):
+        x, z = vae_inputs(frames, 64, 96, lf, key=f"vae{frames}")
+        with torch.no_grad():
+            post = m.encode(x).latent_dist
+            dec = m.decode(z).sample
+        assert rel(post.mean.float(), g[f"tiny.f{frames}.mean"]) < 2e-2
+        assert tuple(dec.shape) == tuple(g[f"tiny.f{frames}.decode"].shape)
+        assert rel(dec.float(), g[f"tiny.f{frames}.decode"]) < 2e-2
+        assert not m._caches  # cleared after every encode / decode
+
+
+def test_vae_host_logic_tiling(mocked):
+    from tests.golden.cases import VAE_TINY_CFG, VAE_SEEDS, vae_inputs
+    g = load_file(os.path.join(GOLD, "vae_tiled.safetensors"))
+    m = _model(mocked, VAE_TINY_CFG, VAE_SEEDS[0], sample_height=128, sample_width=192)
+    m.enable_tiling()
+    m.enable_slicing()
+    x0, z0 = vae_inputs(9, 128, 192, 3, key="vaet0")
+    x1, z1 = vae_inputs(9, 128, 192, 3, key="vaet1")
+    with torch.no_grad():
+        post = m.encode(torch.cat([x0, x1])).latent_dist
+        dec = m.decode(torch.cat([z0, z1])).sample
+    assert rel(post.mean.float(), g["mean"]) < 2e-2
+    assert tuple(dec.shape) == tuple(int(v) for v in g["decode_shape"])
+    assert rel(dec[..., ::2, ::2].float(), g["decode_s2"]) < 2e-2
+
+
+def test_vae_state_dict_and_config_contract():
+    from videopainter_amd.vae import AutoencoderKLCogVideoX
+    from videopainter_amd.config import VAE_DEFAULTS
+    m = AutoencoderKLCogVideoX(block_out_channels=(32, 32, 32, 32), layers_per_block=1)
+    assert m.config.scaling_factor == VAE_DEFAULTS["scaling_factor"]
+    assert "decoder.up_blocks.0.resnets.1.norm2.conv_b.conv.weight" in m.state_dict()
+    with pytest.raises(NotImplementedError):
+        AutoencoderKLCogVideoX(use_quant_conv=True)
+    with pytest.raises(TypeError):
+        AutoencoderKLCogVideoX(bogus=1)

@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -64,6 +64,17 @@ class DpmDesc(C.Structure):
                 ("prev_out", vp)]
 
 
+CONV_MAX_T = 128
+
+
+class Conv3dDesc(C.Structure):
+    _fields_ = [("B", i32), ("Cin", i32), ("Cout", i32), ("Tout", i32), ("Hout", i32), ("Wout", i32),
+                ("Hin", i32), ("Win", i32), ("kt", i32), ("kh", i32), ("kw", i32), ("sh", i32), ("sw", i32),
+                ("ph", i32), ("pw", i32), ("uh", i32), ("uw", i32), ("x_frames", i32), ("hist_frames", i32),
+                ("ldy", i32), ("ldr", i32), ("tmap", i32 * CONV_MAX_T),
+                ("x", vp), ("hist", vp), ("w", vp), ("bias", vp), ("resid", vp), ("y", vp)]
+
+
 EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS, EPI_BIAS_GELU_MXFP8, EPI_BIAS_QKNORM_ROPE = range(7)
 
 # name -> (restype, argtypes)
@@ -97,6 +108,16 @@ _SIGS = {
     "vp_unpatchify_bf16": (i32, [vp, i64, vp, i32, i32, i32, i32, i32, i32, vp]),
     "vp_dpm_step_bf16": (i32, [C.POINTER(DpmDesc), vp]),
     "vp_fill_normal_bf16": (i32, [vp, i64, C.c_uint64, f32, f32, vp]),
+    "vp_conv3d_bf16": (i32, [C.POINTER(Conv3dDesc), vp]),
+    "vp_group_norm_workspace_floats": (i64, [i32, i32]),
+    "vp_group_norm_stats": (i32, [vp, i32, i64, i32, i32, f32, vp, vp, vp]),
+    "vp_group_norm_apply_bf16": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, i32, i32,
+                                       C.POINTER(i32), i32, vp]),
+    "vp_time_pool2_bf16": (i32, [vp, vp, i32, i32, i64, i32, vp]),
+    "vp_ncdhw_to_ndhwc_bf16": (i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "vp_ndhwc_to_ncdhw_bf16": (i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "vp_latent_dist_bf16": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
+    "vp_tile_blend_bf16": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
 }
 
 EXPORTS = tuple(_SIGS)
@@ -132,10 +153,10 @@ def lib():
         if src is not None and built.split(":")[0] != src:
             raise HipLibraryError(f"{LIB_PATH} was built from other sources (digest {built[:12]}.. != "
                                   f"{src[:12]}..); rebuild with `python -m videopainter_amd.build`")
-        sizes = (i64 * 5)()
+        sizes = (i64 * 6)()
         L.vp_struct_sizes(sizes)
         want = (C.sizeof(GemmDesc), C.sizeof(AttnDesc), C.sizeof(DpmDesc), C.sizeof(GemmMxDesc),
-                C.sizeof(AttnFp8Desc))
+                C.sizeof(AttnFp8Desc), C.sizeof(Conv3dDesc))
         if tuple(sizes) != want:
             raise HipLibraryError(f"descriptor size mismatch lib={tuple(sizes)} python={want}; rebuild")
         _lib = L

@@ -207,6 +207,7 @@ extern "C" void vp_struct_sizes(int64_t* out) {
   out[2] = (int64_t)sizeof(vp_dpm_desc);
   out[3] = (int64_t)sizeof(vp_gemm_mx_desc);
   out[4] = (int64_t)sizeof(vp_attn_fp8_desc);
+  out[5] = (int64_t)sizeof(vp_conv3d_desc);
 }
 
 extern "C" int vp_linear_small_bf16(const void* x, int64_t ldx, const void* W, const void* bias, void* y,

@@ -582,3 +582,145 @@ def fill_normal_(t: torch.Tensor, seed: int, mean: float = 0.0, std: float = 1.0
     N.check(N.lib().vp_fill_normal_bf16(_p(t), t.numel(), seed & 0xFFFFFFFFFFFFFFFF, mean, std, _stream()),
             "vp_fill_normal_bf16")
     return t
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# CogVideoX 3D causal VAE (channels-last bf16 activations [B, T, H, W, C])
+# ------------------------------------------------------------------------------------------------------------------
+
+def conv3d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], *, Tout: int, Hout: int, Wout: int,
+           tmap: Sequence[int], hist: Optional[torch.Tensor] = None, stride: int = 1, pad: int = 0, up: int = 1,
+           resid: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+           ldy: Optional[int] = None) -> torch.Tensor:
+    """Implicit-GEMM conv (vp_conv3d_bf16): x / hist [B, T, Hin, Win, Cin] channels-last, w [Cout, kt, kh, kw, Cin];
+    tmap[t + dt] = x frame (>= 0) or -1 - hist frame for output frame t and temporal tap dt."""
+    _chk(x, "x")
+    _chk(w, "w")
+    if not x.is_contiguous() or not w.is_contiguous() or x.dim() != 5 or w.dim() != 5:
+        raise ValueError("conv3d: x [B,T,H,W,C] and w [Cout,kt,kh,kw,Cin] must be contiguous")
+    B, xf, Hin, Win, Cin = x.shape
+    Cout, kt, kh, kw, wc = w.shape
+    if wc != Cin:
+        raise ValueError(f"conv3d: weight Cin {wc} != activation channels {Cin}")
+    if len(tmap) != Tout + kt - 1 or len(tmap) > N.CONV_MAX_T:
+        raise ValueError("conv3d: tmap must have Tout + kt - 1 <= CONV_MAX_T entries")
+    ldy = ldy if ldy is not None else (Cout + 7) // 8 * 8
+    if out is None:
+        out = torch.empty(B, Tout, Hout, Wout, ldy, device=x.device, dtype=BF16)
+    elif out.shape != (B, Tout, Hout, Wout, ldy) or not out.is_contiguous():
+        raise ValueError("conv3d: out has the wrong shape")
+    d = N.Conv3dDesc()
+    d.B, d.Cin, d.Cout, d.Tout, d.Hout, d.Wout, d.Hin, d.Win = B, Cin, Cout, Tout, Hout, Wout, Hin, Win
+    d.kt, d.kh, d.kw, d.sh, d.sw, d.ph, d.pw, d.uh, d.uw = kt, kh, kw, stride, stride, pad, pad, up, up
+    d.x_frames = xf
+    if hist is not None:
+        _chk(hist, "hist")
+        if not hist.is_contiguous() or hist.shape[0] != B or hist.shape[2:] != x.shape[2:]:
+            raise ValueError("conv3d: hist must be [B, Th, Hin, Win, Cin] contiguous")
+        d.hist, d.hist_frames = _p(hist), hist.shape[1]
+    for i, v in enumerate(tmap):
+        d.tmap[i] = int(v)
+    d.x, d.w, d.y, d.ldy = _p(x), _p(w), _p(out), ldy
+    if bias is not None:
+        _chk(bias, "bias")
+        d.bias = _p(bias)
+    if resid is not None:
+        _chk(resid, "resid")
+        if resid.shape[:4] != out.shape[:4] or not resid.is_contiguous():
+            raise ValueError("conv3d: resid must be [B, Tout, Hout, Wout, ldr] contiguous")
+        d.resid, d.ldr = _p(resid), resid.shape[4]
+    N.check(N.lib().vp_conv3d_bf16(C.byref(d), _stream()), "vp_conv3d_bf16")
+    return out
+
+
+def group_norm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, eps: float, *,
+               silu: bool = False, mod: Optional[torch.Tensor] = None, tzmap: Optional[Sequence[int]] = None,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """act(GroupNorm(x) [* mod_y + mod_b]) over channels-last x [B, T, H, W, C] (vp_group_norm_stats + _apply);
+    mod [B, Tz, Hz, Wz, 2C] = conv_y(z) | conv_b(z) at latent resolution, tzmap[t] = its frame for frame t."""
+    _chk(x, "x")
+    _chk(gamma, "gamma")
+    _chk(beta, "beta")
+    if not x.is_contiguous() or x.dim() != 5:
+        raise ValueError("group_norm: x must be contiguous [B, T, H, W, C]")
+    B, T, H, W, Cc = x.shape
+    L = N.lib()
+    part = torch.empty(L.vp_group_norm_workspace_floats(B, groups), device=x.device, dtype=torch.float32)
+    stats = torch.empty(B, groups, 2, device=x.device, dtype=torch.float32)
+    N.check(L.vp_group_norm_stats(_p(x), B, T * H * W, Cc, groups, eps, _p(part), _p(stats), _stream()),
+            "vp_group_norm_stats")
+    out = torch.empty_like(x) if out is None else out
+    tz = None
+    Tz = Hz = Wz = 0
+    if mod is not None:
+        _chk(mod, "mod")
+        if not mod.is_contiguous() or mod.shape[0] != B or mod.shape[4] != 2 * Cc or tzmap is None or len(tzmap) != T:
+            raise ValueError("group_norm: mod must be [B, Tz, Hz, Wz, 2C] with a tzmap of T entries")
+        Tz, Hz, Wz = mod.shape[1:4]
+        tz = (N.i32 * T)(*[int(v) for v in tzmap])
+    N.check(L.vp_group_norm_apply_bf16(_p(x), _p(out), B, T, H, W, Cc, groups, _p(stats), _p(gamma), _p(beta),
+                                       _p(mod), Tz, Hz, Wz, tz, int(silu), _stream()), "vp_group_norm_apply_bf16")
+    return out
+
+
+def time_pool2(x: torch.Tensor) -> torch.Tensor:
+    _chk(x, "x")
+    B, T, H, W, Cc = x.shape
+    T2 = (T + 1) // 2 if T % 2 else T // 2
+    out = torch.empty(B, T2, H, W, Cc, device=x.device, dtype=BF16)
+    N.check(N.lib().vp_time_pool2_bf16(_p(x.contiguous()), _p(out), B, T, H * W, Cc, _stream()), "vp_time_pool2_bf16")
+    return out
+
+
+def ncdhw_to_ndhwc(x: torch.Tensor, cpad: int) -> torch.Tensor:
+    if not x.is_cuda or x.dtype not in (torch.float32, BF16):
+        raise TypeError("ncdhw_to_ndhwc: x must be a float32 / bfloat16 device tensor")
+    x = x.contiguous()
+    B, Cc, T, H, W = x.shape
+    out = torch.empty(B, T, H, W, cpad, device=x.device, dtype=BF16)
+    N.check(N.lib().vp_ncdhw_to_ndhwc_bf16(_p(x), int(x.dtype == torch.float32), _p(out), B, Cc, T, H, W, cpad,
+                                           _stream()), "vp_ncdhw_to_ndhwc_bf16")
+    return out
+
+
+def ndhwc_to_ncdhw(x: torch.Tensor, channels: int, c0: int = 0) -> torch.Tensor:
+    _chk(x, "x")
+    B, T, H, W, ld = x.shape
+    out = torch.empty(B, channels, T, H, W, device=x.device, dtype=BF16)
+    N.check(N.lib().vp_ndhwc_to_ncdhw_bf16(_p(x.contiguous()), ld, _p(out), B, channels, T, H, W, c0, _stream()),
+            "vp_ndhwc_to_ncdhw_bf16")
+    return out
+
+
+def latent_dist(params: torch.Tensor, latent_channels: int, noise: Optional[torch.Tensor] = None):
+    """(mean, logvar[, sample]) NCDHW bf16 from the encoder output rows [B, T, H, W, >= 2L]."""
+    _chk(params, "params")
+    B, T, H, W, ld = params.shape
+    L = latent_channels
+    mean = torch.empty(B, L, T, H, W, device=params.device, dtype=BF16)
+    logvar = torch.empty_like(mean)
+    sample = None
+    if noise is not None:
+        _chk(noise, "noise")
+        if tuple(noise.shape) != tuple(mean.shape):
+            raise ValueError("latent_dist: noise must be [B, L, T, H, W]")
+        noise = noise.contiguous()
+        sample = torch.empty_like(mean)
+    N.check(N.lib().vp_latent_dist_bf16(_p(params.contiguous()), ld, _p(mean), _p(logvar), _p(noise), _p(sample), B, L,
+                                        T, H, W, _stream()), "vp_latent_dist_bf16")
+    return (mean, logvar) if noise is None else (mean, logvar, sample)
+
+
+def tile_blend_(a: torch.Tensor, b: torch.Tensor, axis: int, extent: int) -> torch.Tensor:
+    """In place on b (channels-last [B, T, H, W, C]): the reference's blend_v (axis 0) / blend_h (axis 1)."""
+    _chk(a, "a")
+    _chk(b, "b")
+    if not a.is_contiguous() or not b.is_contiguous():
+        raise ValueError("tile_blend_: tiles must be contiguous")
+    B, T, Ha, Wa, Cc = a.shape
+    Hb, Wb = b.shape[2], b.shape[3]
+    if b.shape[0] != B or b.shape[1] != T or b.shape[4] != Cc:
+        raise ValueError("tile_blend_: tiles differ in batch / frames / channels")
+    N.check(N.lib().vp_tile_blend_bf16(_p(a), _p(b), B, T, Ha, Wa, Hb, Wb, Cc, axis, extent, _stream()),
+            "vp_tile_blend_bf16")
+    return b
