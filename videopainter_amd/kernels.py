@@ -629,7 +629,9 @@ def conv3d(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], *, To
         if resid.shape[:4] != out.shape[:4] or not resid.is_contiguous():
             raise ValueError("conv3d: resid must be [B, Tout, Hout, Wout, ldr] contiguous")
         d.resid, d.ldr = _p(resid), resid.shape[4]
+    ev = _t0("conv3d")
     N.check(N.lib().vp_conv3d_bf16(C.byref(d), _stream()), "vp_conv3d_bf16")
+    _t1("conv3d", ev)
     return out
 
 
