@@ -36,7 +36,7 @@ def main():
     ap.add_argument("--gemm-variants", default="5,11", help="VP_GEMM_VARIANT values, interleaved over 2 rounds")
     ap.add_argument("--variant", default="", help="attention kernel(s): lazy, bounded (default: both)")
     ap.add_argument("--variant8", default="", help="fp8 attention kernel variant(s) (VP_ATTN8_VARIANT), e.g. 1,2")
-    ap.add_argument("--only", default="", help="attention | attn8 | gemm | mx: run just that kernel (for rocprofv3 "
+    ap.add_argument("--only", default="", help="attention | attn8 | gemm | mx | norms: run just that kernel (for rocprofv3 "
                     "--pmc passes; attn8 = the fp8 attention only)")
     args = ap.parse_args()
     dev = "cuda"
@@ -46,7 +46,7 @@ def main():
     res = {}
     x = torch.randn(M, 4 * D, device=dev).to(torch.bfloat16)
     shapes = [("qkv", 3 * D, D), ("out", D, D), ("ff1", 4 * D, D), ("ff2", D, 4 * D)]
-    if args.only == "attention":
+    if args.only in ("attention", "norms"):
         shapes = []
     if args.only == "mx":
         # MX-FP8 FeedForward GEMMs (BASELINE config 5 path) next to their bf16 versions, interleaved
@@ -96,7 +96,7 @@ def main():
     # lazy = the running-max kernel; bounded = the no-max kernel the processors pick when the qk-norm
     # bounds every score (these random q, k: |q.k| * 0.125 * log2 e stays far below the bound of 60)
     variants = tuple(args.variant.split(",")) if args.variant else ("lazy", "bounded")
-    if args.only == "attn8":
+    if args.only in ("attn8", "norms"):
         variants = ()
     for rnd in range(1 if args.only else 2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
         for var in variants:

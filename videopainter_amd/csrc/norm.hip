@@ -45,31 +45,43 @@ VP_DEV void row_stats(const RowRegs& r, int nch, int lane, int D, float& mean, f
   rstd = rsqrtf(wave_sum(q) / (float)D + eps);
 }
 
-// ---- AdaLN-Zero modulate (DF/models/normalization.py:373-379) ----
-// MX = true: the modulated row is written as MX-FP8 (e4m3 + E8M0 per 32 columns, include/vp_hip.h) for the fp8
-// FeedForward — a 32-column block is 4 consecutive 8-column chunks = 4 consecutive lanes of the row's wave.
-template <bool MX>
-__global__ __launch_bounds__(ROW_THREADS) void adaln_modulate_kernel(const bf16* __restrict__ x, void* __restrict__ y,
-                                                                     uint8_t* __restrict__ yscale,
-                                                                     int rows, int Ntok, int D, int text_len,
-                                                                     const bf16* __restrict__ lw,
-                                                                     const bf16* __restrict__ lb, float eps,
-                                                                     const bf16* __restrict__ mod, int64_t mod_bs) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
-  if (row >= rows) return;
+// AdaLN row body: x (this wave's row as NCH bf16 chunks per lane) -> normalised, modulated row (same arithmetic,
+// in the same order, as the reference chain: LayerNorm in fp32 from bf16, bf16 rounding after the affine, after
+// (1 + scale), after the product and after + shift)
+template <bool MX, int NCH>
+VP_DEV void adaln_row(bf16x8 (&xr)[NCH], int row, int lane, int Ntok, int D, int text_len, const bf16* __restrict__ lw,
+                      const bf16* __restrict__ lb, float eps, const bf16* __restrict__ mod, int64_t mod_bs,
+                      void* __restrict__ y, uint8_t* __restrict__ yscale) {
   const int b = row / Ntok;
   const int tok = row - b * Ntok;
   const int nch = D / 8;
-  RowRegs r;
-  load_row(x + (int64_t)row * D, nch, lane, r);
-  float mean, rstd;
-  row_stats(r, nch, lane, D, mean, rstd, eps);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+    if (lane + i * 64 < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += bf2f(xr[i][e]);
+  const float mean = wave_sum(s) / (float)D;
+  // opaque: keep the row as bf16 (re-widened per use, 1 VALU) instead of 8 floats per chunk across the reductions
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) asm volatile("" : "+v"(xr[i]));
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+    if (lane + i * 64 < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float t = bf2f(xr[i][e]) - mean;
+        q += t * t;
+      }
+  const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) asm volatile("" : "+v"(xr[i]));
   const bool text = tok < text_len;
   const bf16* shift = mod + (int64_t)b * mod_bs + (text ? 3 : 0) * D;
   const bf16* scale = mod + (int64_t)b * mod_bs + (text ? 4 : 1) * D;
 #pragma unroll
-  for (int i = 0; i < MAXC; ++i) {
+  for (int i = 0; i < NCH; ++i) {
     const int c = lane + i * 64;
     if (c < nch) {
       const bf16x8 w = *(const bf16x8*)(lw + c * 8);
@@ -79,14 +91,14 @@ __global__ __launch_bounds__(ROW_THREADS) void adaln_modulate_kernel(const bf16*
       float f[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float n = rbf((r.v[i][e] - mean) * rstd * bf2f(w[e]) + bf2f(bb[e]));
+        const float n = rbf((bf2f(xr[i][e]) - mean) * rstd * bf2f(w[e]) + bf2f(bb[e]));
         const float s1 = rbf(1.f + bf2f(sc[e]));
         f[e] = rbf(rbf(n * s1) + bf2f(sh[e]));
       }
       if constexpr (MX) {
         uint8_t sb;
-        const u32x2 q = mx_quantize_quarter(f, sb);
-        *(u32x2*)((uint8_t*)y + (int64_t)row * D + c * 8) = q;
+        const u32x2 qq = mx_quantize_quarter(f, sb);
+        *(u32x2*)((uint8_t*)y + (int64_t)row * D + c * 8) = qq;
         if ((c & 3) == 0) yscale[mx_scale_off(row, c >> 2, D)] = sb;
       } else {
         bf16x8 o;
@@ -95,7 +107,58 @@ __global__ __launch_bounds__(ROW_THREADS) void adaln_modulate_kernel(const bf16*
         *(bf16x8*)((bf16*)y + (int64_t)row * D + c * 8) = o;
       }
     }
+    // one chunk's parameter loads live at a time (hoisting all 4 x NCH of them costs 96 VGPRs and half the
+    // occupancy; the other resident rows cover their L2 latency)
+    __builtin_amdgcn_sched_barrier(0);
   }
+}
+
+template <int NCH>
+VP_DEV void load_row_bf16(bf16x8 (&xr)[NCH], const bf16* __restrict__ xrow, int lane, int nch) {
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + i * 64;
+    if (c < nch) xr[i] = *(const bf16x8*)(xrow + c * 8);
+  }
+}
+
+// ---- AdaLN-Zero modulate (DF/models/normalization.py:373-379) ----
+// MX = true: the modulated row is written as MX-FP8 (e4m3 + E8M0 per 32 columns, include/vp_hip.h) for the fp8
+// FeedForward — a 32-column block is 4 consecutive 8-column chunks = 4 consecutive lanes of the row's wave.
+// HBM-latency bound: one row's load -> reduce -> store chain leaves the memory pipe idle unless many rows overlap.
+// The row stays in registers as bf16 (NCH 16-byte chunks per lane, 4 VGPRs each: 24 VGPRs at D = 3072).
+// One row per wave, 6-7 waves per SIMD (70-76 VGPRs): 4.4-4.5 TB/s at config 2 (3.8 with the row held as floats, 116
+// VGPRs).  Measured and dropped (tools/gpu_ab_norms.sh): persistent waves prefetching the next row (126 VGPRs,
+// 3.7 TB/s); 512-thread blocks staging the affine + shift / scale in LDS (3.4-3.5 TB/s); 8 waves/SIMD with 10
+// spilled VGPRs (3.1 TB/s).
+template <bool MX, int NCH>
+__global__ __launch_bounds__(ROW_THREADS) void adaln_modulate_kernel(const bf16* __restrict__ x, void* __restrict__ y,
+                                                                        uint8_t* __restrict__ yscale,
+                                                                        int rows, int Ntok, int D, int text_len,
+                                                                        const bf16* __restrict__ lw,
+                                                                        const bf16* __restrict__ lb, float eps,
+                                                                        const bf16* __restrict__ mod, int64_t mod_bs) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  bf16x8 xr[NCH];
+  load_row_bf16<NCH>(xr, x + (int64_t)row * D, lane, D / 8);
+  adaln_row<MX, NCH>(xr, row, lane, Ntok, D, text_len, lw, lb, eps, mod, mod_bs, y, yscale);
+}
+
+template <bool MX>
+void launch_adaln(int rows, hipStream_t s, const bf16* x, void* y, uint8_t* ys, int Ntok, int D,
+                  int text_len, const bf16* lw, const bf16* lb, float eps, const bf16* mod, int64_t mod_bs) {
+  const int nch = (D / 8 + 63) / 64;  // 16-byte chunks per lane
+  const int grid = (rows + 3) / 4;
+#define VP_ADALN(N) hipLaunchKernelGGL((adaln_modulate_kernel<MX, N>), dim3(grid), dim3(ROW_THREADS), 0, s, x, y, ys, \
+                                       rows, Ntok, D, text_len, lw, lb, eps, mod, mod_bs)
+  if (nch <= 1) VP_ADALN(1);
+  else if (nch <= 2) VP_ADALN(2);
+  else if (nch <= 4) VP_ADALN(4);
+  else if (nch <= 6) VP_ADALN(6);
+  else VP_ADALN(8);
+#undef VP_ADALN
 }
 
 // ---- final norm_final + norm_out (cogvideox_transformer_3d.py:617-624; normalization.py:73-85) ----
@@ -238,10 +301,8 @@ extern "C" int vp_adaln_modulate_bf16(const void* x, void* y, int32_t B, int32_t
     return VP_ERR_ARG;
   if (mod_bstride % 8) return VP_ERR_ARG;
   const int rows = B * Ntok;
-  const int grid = (rows + 3) / 4;
-  hipLaunchKernelGGL(adaln_modulate_kernel<false>, dim3(grid), dim3(ROW_THREADS), 0, (hipStream_t)stream,
-                     (const bf16*)x, y, nullptr, rows, Ntok, D, text_len, (const bf16*)ln_w, (const bf16*)ln_b, eps,
-                     (const bf16*)mod, mod_bstride);
+  launch_adaln<false>(rows, (hipStream_t)stream, (const bf16*)x, y, nullptr, Ntok, D, text_len,
+                      (const bf16*)ln_w, (const bf16*)ln_b, eps, (const bf16*)mod, mod_bstride);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
@@ -253,10 +314,8 @@ extern "C" int vp_adaln_modulate_mx_fp8(const void* x, void* q, void* scales, in
     return VP_ERR_ARG;
   if (mod_bstride % 8) return VP_ERR_ARG;
   const int rows = B * Ntok;
-  const int grid = (rows + 3) / 4;
-  hipLaunchKernelGGL(adaln_modulate_kernel<true>, dim3(grid), dim3(ROW_THREADS), 0, (hipStream_t)stream,
-                     (const bf16*)x, q, (uint8_t*)scales, rows, Ntok, D, text_len, (const bf16*)ln_w,
-                     (const bf16*)ln_b, eps, (const bf16*)mod, mod_bstride);
+  launch_adaln<true>(rows, (hipStream_t)stream, (const bf16*)x, q, (uint8_t*)scales, Ntok, D, text_len,
+                     (const bf16*)ln_w, (const bf16*)ln_b, eps, (const bf16*)mod, mod_bstride);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
