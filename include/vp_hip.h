@@ -393,6 +393,24 @@ int vp_tile_blend_bf16(const void* a, void* b, int32_t B, int32_t T, int32_t Ha,
                        int32_t C, int32_t axis, int32_t extent, void* stream);
 
 
+/* ---- T5 v1.1 encoder (transformers modeling_t5.py, pinned transformers==4.42.2) ----
+ * The projections (q|k|v fused, o, wi_0 + GELU-tanh, wi_1, wo) run on vp_gemm_bf16 (no bias; the residual adds are
+ * its VP_EPI_BIAS_ADDROWS epilogue).  T5Stack.embed_tokens: out[r] = table[ids[r]] (bf16 [vocab, D]). */
+int vp_embedding_gather_bf16(const void* table, const int64_t* ids, void* out, int32_t rows, int32_t D, int32_t vocab,
+                             void* stream);
+/* T5LayerNorm: y = w * bf16(x * rsqrt(mean(x^2) + eps)) over rows of D (bf16 in / out, fp32 statistics) */
+int vp_rms_norm_bf16(const void* x, const void* w, void* y, int32_t rows, int32_t D, float eps, void* stream);
+/* T5DenseGatedActDense's product: y = bf16(a * b) elementwise (n % 8 == 0) */
+int vp_mul_bf16(const void* a, const void* b, void* y, int64_t n, void* stream);
+/* T5Attention (encoder, bidirectional): qkv [B, L, ld] bf16 holding q | k | v (inner = H * 64 columns each);
+ * scores = bf16(q . k) + bias_table[buckets[q * L + k], h] (no 1/sqrt(d) scaling), masked keys (mask[b, k] == 0,
+ * int64 [B, L], or mask NULL) get the bf16 minimum added, softmax in fp32, out [B, L] rows of stride ldo, head h at
+ * column h * 64.  buckets: int32 [L, L] from T5Attention._relative_position_bucket (host-computed); L <= 512. */
+int vp_t5_attention_bf16(const void* qkv, int64_t ld, int32_t inner, int32_t B, int32_t L, int32_t H,
+                         const void* bias_table, const int32_t* buckets, const int64_t* mask, void* out, int64_t ldo,
+                         void* stream);
+
+
 #ifdef __cplusplus
 }
 #endif

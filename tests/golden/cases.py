@@ -187,3 +187,47 @@ def vae_weights(cfg: dict, seed: int):
     """The counter-generator VAE state dict (bf16-valued fp32 numpy) the golden generator filled into the reference."""
     from videopainter_amd.config import full_vae_config, vae_state_dict_shapes
     return synth_state_dict(vae_state_dict_shapes(full_vae_config(cfg)), seed)
+
+
+# T5 v1.1 encoder (SURVEY.md 8f #4).  Tiny: 3 layers, d_model 128, 2 heads; xxl2: the real T5-XXL widths (d_model 4096,
+# 64 heads x 64, d_ff 10240, vocab 32128) with 2 layers.  Weights from the counter generator: linears N(0, 1/fan_in),
+# RMS-norm weights 1 + N(0, 0.05^2), token embeddings N(0, 1), relative-position bias N(0, 0.5^2).  (xxl2 uses a
+# 4096-token vocabulary.)
+T5_TINY_CFG = dict(vocab_size=256, d_model=128, d_kv=64, d_ff=256, num_layers=3, num_heads=2,
+                   feed_forward_proj="gated-gelu")
+T5_XXL2_CFG = dict(num_layers=2, vocab_size=4096)  # vocab cut: the gather does not care, generation time does
+T5_SEEDS = (3001, 3002)
+T5_L = 226
+
+
+def t5_weights(cfg: dict, seed: int):
+    from videopainter_amd.config import full_t5_config, t5_state_dict_shapes
+    from videopainter_amd.weights import counter_normal, round_bf16
+    out = {}
+    for name, shape in t5_state_dict_shapes(full_t5_config(cfg)).items():
+        n = int(np.prod(shape))
+        key = "shared.weight" if name == "encoder.embed_tokens.weight" else name  # tied
+        z = counter_normal(key, n, seed).reshape(shape)
+        if name.endswith("layer_norm.weight"):
+            a = 1.0 + 0.05 * z
+        elif "relative_attention_bias" in name:
+            a = 0.5 * z
+        elif key == "shared.weight":
+            a = z
+        else:
+            a = z / np.sqrt(shape[1])
+        out[name] = round_bf16(a.astype(np.float32))
+    return out
+
+
+def t5_inputs(vocab: int, key: str = "t5"):
+    """ids [2, 226]: prompt tokens, then eos (1), then padding (0) — the tokenizer's padding="max_length" layout;
+    and the matching attention mask."""
+    u = counter_uniform(f"{key}.ids", 2 * T5_L).reshape(2, T5_L)
+    ids = (2 + (u * (vocab - 2)).astype(np.int64)).clip(2, vocab - 1)
+    mask = np.ones((2, T5_L), dtype=np.int64)
+    for b, n in enumerate((37, 180)):
+        ids[b, n] = 1
+        ids[b, n + 1:] = 0
+        mask[b, n + 1:] = 0
+    return torch.from_numpy(ids), torch.from_numpy(mask)

@@ -410,6 +410,46 @@ def make_vae_tiled():
                                     "decode_shape": torch.tensor(dec.shape, dtype=torch.float32)})
 
 
+@torch.no_grad()
+def make_t5():
+    """transformers' T5EncoderModel (installed 5.15.0; the reference pins 4.42.2 — same encoder math) on counter
+    weights: tiny (3 layers) and xxl2 (T5-XXL widths, 2 layers) at L = 226, B = 2, as the pipeline calls it (ids only),
+    plus the tiny model with an attention mask; fp32, and bf16 runs (all bf16, and bf16 with `wo` kept in fp32 as
+    from_pretrained(torch_dtype=bf16) does via _keep_in_fp32_modules) for the drift gates.  t5.safetensors."""
+    from transformers import T5Config, T5EncoderModel
+    from tests.golden.cases import T5_TINY_CFG, T5_XXL2_CFG, T5_SEEDS, t5_inputs, t5_weights
+    from videopainter_amd.config import full_t5_config
+    out = {}
+    rel = lambda a, b: float((a.double() - b.double()).norm() / b.double().norm())  # noqa: E731
+    for tag, cfg, seed in (("tiny", T5_TINY_CFG, T5_SEEDS[0]), ("xxl2", T5_XXL2_CFG, T5_SEEDS[1])):
+        fc = full_t5_config(cfg)
+        conf = T5Config(**{k: v for k, v in fc.items() if k not in ("dense_act_fn", "is_gated_act")})
+        m = T5EncoderModel(conf).eval()
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in t5_weights(cfg, seed).items()}, strict=True)
+        ids, mask = t5_inputs(fc["vocab_size"], key=f"t5{tag}")
+        y = m(ids)[0]
+        stride = 1 if tag == "tiny" else 8
+        out[f"{tag}.out"] = y[..., ::stride]
+        if tag == "tiny":
+            out["tiny.masked.out"] = m(ids, attention_mask=mask)[0]
+        m16 = m.to(torch.bfloat16)
+        d_all = rel(m16(ids)[0].float(), y)
+        for blk in m16.encoder.block:
+            blk.layer[1].DenseReluDense.wo.float()
+        d_keep = rel(m16(ids)[0].float(), y)
+        out[f"{tag}.ref_bf16_rel"] = torch.tensor([d_all, d_keep])
+        # transformers 5.x runs the attention through its sdpa interface (fp32 scores inside the fused kernel); the
+        # pinned 4.42.2 eager path rounds q.k to bf16 before the bias and the softmax, as the oracle restates — its
+        # bf16 run is the drift the HIP path is gated on
+        from oracle import t5_oracle as T
+        sd16 = {k: torch.from_numpy(v).bfloat16() for k, v in t5_weights(cfg, seed).items()}
+        d_or = rel(T.encoder_forward(sd16, fc, ids).float(), y)
+        out[f"{tag}.oracle_bf16_rel"] = torch.tensor([d_or])
+        print(f"t5 {tag}: out {tuple(y.shape)} bf16 drift {d_all:.3e} (wo fp32: {d_keep:.3e}; 4.42 eager-path "
+              f"oracle in bf16: {d_or:.3e})", flush=True)
+    _save("t5.safetensors", out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["tiny", "sched", "pipe", "block"]
     if "config1" in which:
@@ -422,6 +462,8 @@ if __name__ == "__main__":
         make_vae()
     if "vae_tiled" in which:
         make_vae_tiled()
+    if "t5" in which:
+        make_t5()
     if "tiny" in which:
         make_tiny()
     if "sched" in which:

@@ -179,3 +179,23 @@ def test_vae_tiled_oracle_matches_reference():
     assert rel(mean, g["mean"]) < 1e-5 and rel(logvar, g["logvar"]) < 1e-5
     assert tuple(dec.shape) == tuple(int(v) for v in g["decode_shape"])
     assert rel(dec[..., ::2, ::2], g["decode_s2"]) < 1e-5
+
+
+@pytest.mark.parametrize("tag", ["tiny", "xxl2"])
+def test_t5_oracle_matches_transformers(tag):
+    """oracle/t5_oracle.py against transformers' T5EncoderModel (tests/golden/t5.safetensors), fp32."""
+    from oracle import t5_oracle as T
+    from tests.golden.cases import T5_TINY_CFG, T5_XXL2_CFG, T5_SEEDS, t5_inputs, t5_weights
+    from videopainter_amd.config import full_t5_config
+    cfg, seed = (T5_TINY_CFG, T5_SEEDS[0]) if tag == "tiny" else (T5_XXL2_CFG, T5_SEEDS[1])
+    fc = full_t5_config(cfg)
+    sd = {k: torch.from_numpy(v) for k, v in t5_weights(cfg, seed).items()}
+    g = load_file(os.path.join(GOLD, "t5.safetensors"))
+    ids, mask = t5_inputs(fc["vocab_size"], key=f"t5{tag}")
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    with torch.no_grad():
+        y = T.encoder_forward(sd, fc, ids)
+        stride = 1 if tag == "tiny" else 8
+        assert rel(y[..., ::stride], g[f"{tag}.out"]) < 1e-5
+        if tag == "tiny":
+            assert rel(T.encoder_forward(sd, fc, ids, mask), g["tiny.masked.out"]) < 1e-5

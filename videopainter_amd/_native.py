@@ -118,6 +118,10 @@ _SIGS = {
     "vp_ndhwc_to_ncdhw_bf16": (i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp]),
     "vp_latent_dist_bf16": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "vp_tile_blend_bf16": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "vp_embedding_gather_bf16": (i32, [vp, vp, vp, i32, i32, i32, vp]),
+    "vp_rms_norm_bf16": (i32, [vp, vp, vp, i32, i32, f32, vp]),
+    "vp_mul_bf16": (i32, [vp, vp, vp, i64, vp]),
+    "vp_t5_attention_bf16": (i32, [vp, i64, i32, i32, i32, i32, vp, vp, vp, vp, i64, vp]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -213,3 +213,47 @@ def config_signature_check(cls, cfg: dict) -> None:
     for k in cfg:
         if k not in sig.parameters:
             raise TypeError(f"{cls.__name__} got unexpected config key {k}")
+
+
+# T5 v1.1 encoder config fields (transformers T5Config) — defaults = CogVideoX's text encoder, google t5-v1_1-xxl
+T5_DEFAULTS = dict(
+    vocab_size=32128, d_model=4096, d_kv=64, d_ff=10240, num_layers=24, num_decoder_layers=24, num_heads=64,
+    relative_attention_num_buckets=32, relative_attention_max_distance=128, dropout_rate=0.1,
+    layer_norm_epsilon=1e-6, initializer_factor=1.0, feed_forward_proj="gated-gelu", is_encoder_decoder=True,
+    use_cache=True, pad_token_id=0, eos_token_id=1, decoder_start_token_id=0, tie_word_embeddings=False,
+    classifier_dropout=0.0, dense_act_fn="gelu_new", is_gated_act=True,
+)
+
+
+def full_t5_config(kwargs: dict) -> dict:
+    base = dict(T5_DEFAULTS)
+    base.update({k: v for k, v in kwargs.items() if not k.startswith("_")})
+    ff = base["feed_forward_proj"].split("-")
+    base["is_gated_act"] = ff[0] == "gated"
+    base["dense_act_fn"] = "gelu_new" if ff[-1] == "gelu" else ff[-1]
+    return base
+
+
+def t5_state_dict_shapes(cfg: dict) -> Dict[str, Tuple[int, ...]]:
+    """`T5EncoderModel.state_dict()` keys / shapes (gated FF: wi_0 / wi_1; the relative bias lives in block 0)."""
+    D, inner, F = cfg["d_model"], cfg["num_heads"] * cfg["d_kv"], cfg["d_ff"]
+    s: Dict[str, Tuple[int, ...]] = {"shared.weight": (cfg["vocab_size"], D),
+                                     "encoder.embed_tokens.weight": (cfg["vocab_size"], D)}
+    for i in range(cfg["num_layers"]):
+        p = f"encoder.block.{i}.layer"
+        for n in ("q", "k", "v"):
+            s[f"{p}.0.SelfAttention.{n}.weight"] = (inner, D)
+        s[f"{p}.0.SelfAttention.o.weight"] = (D, inner)
+        if i == 0:
+            s[f"{p}.0.SelfAttention.relative_attention_bias.weight"] = (cfg["relative_attention_num_buckets"],
+                                                                         cfg["num_heads"])
+        s[f"{p}.0.layer_norm.weight"] = (D,)
+        if cfg["is_gated_act"]:
+            s[f"{p}.1.DenseReluDense.wi_0.weight"] = (F, D)
+            s[f"{p}.1.DenseReluDense.wi_1.weight"] = (F, D)
+        else:
+            s[f"{p}.1.DenseReluDense.wi.weight"] = (F, D)
+        s[f"{p}.1.DenseReluDense.wo.weight"] = (D, F)
+        s[f"{p}.1.layer_norm.weight"] = (D,)
+    s["encoder.final_layer_norm.weight"] = (D,)
+    return s

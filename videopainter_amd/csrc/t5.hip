@@ -1,0 +1,192 @@
+// T5 v1.1 encoder pieces for gfx950 (CogVideoX's text encoder, T5-XXL, 226 tokens, once per
+// prompt).  The projections run on vp_gemm_bf16; this file holds what is T5-specific: the token-embedding gather,
+// T5LayerNorm (RMS norm, no mean, no bias), the gated-GELU product and the self-attention with the bucketed
+// relative-position bias and no 1/sqrt(d) scaling.
+// Reference algorithm: transformers `modeling_t5.py` (pinned transformers==4.42.2 in the reference's
+// requirements.txt): T5LayerNorm, T5DenseGatedActDense, T5Attention (compute_bias / _relative_position_bucket),
+// called by the pipeline's `_get_t5_prompt_embeds` (…_anyl.py:216-256).
+#include "vp_common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void embed_gather_kernel(const bf16* __restrict__ table, const int64_t* __restrict__ ids,
+                                                           bf16* __restrict__ out, int rows, int D, int vocab) {
+  const int C8 = D >> 3;
+  const int64_t total = (int64_t)rows * C8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int r = (int)(i / C8), c = (int)(i - (int64_t)r * C8);
+    int64_t id = ids[r];
+    id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);  // the host checks the range; never read out of bounds
+    *(bf16x8*)(out + (int64_t)r * D + c * 8) = *(const bf16x8*)(table + id * D + c * 8);
+  }
+}
+
+// T5LayerNorm: y = w * bf16(x * rsqrt(mean(x^2) + eps)) — fp32 statistics from the bf16 row, bf16 rounding of the
+// normalised row before the weight, like the reference module on bf16 weights.  One wave per row.
+__global__ __launch_bounds__(256) void rms_norm_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                       bf16* __restrict__ y, int rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bf16* xr = x + (int64_t)row * D;
+  const int C8 = D >> 3;
+  float ss = 0.f;
+  for (int c = lane; c < C8; c += 64) {
+    const bf16x8 v = *(const bf16x8*)(xr + c * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ss = __builtin_fmaf(bf2f(v[e]), bf2f(v[e]), ss);
+  }
+  const float r = rsqrtf(wave_sum(ss) / (float)D + eps);
+  for (int c = lane; c < C8; c += 64) {
+    const bf16x8 v = *(const bf16x8*)(xr + c * 8);
+    const bf16x8 wv = *(const bf16x8*)(w + c * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(wv[e]) * rbf(bf2f(v[e]) * r));
+    *(bf16x8*)(y + (int64_t)row * D + c * 8) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void mul_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b,
+                                                  bf16* __restrict__ y, int64_t n8) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const bf16x8 u = *(const bf16x8*)(a + i * 8), v = *(const bf16x8*)(b + i * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(u[e]) * bf2f(v[e]));
+    *(bf16x8*)(y + i * 8) = o;
+  }
+}
+
+// Self-attention of one (batch, head) over L <= T5_MAX_L tokens (d_kv = 64): K and V of the head in LDS (K rows
+// padded to 66 elements: the score pass reads one key row per lane), 4 waves x QW queries per block.
+// scores = bf16(q.k) (the reference's bf16 matmul output) + bias (bf16 add), softmax in fp32 -> bf16 weights,
+// out = bf16(sum_j w_j v_j) with fp32 accumulation; masked keys (mask[b, j] == 0) get the dtype minimum added.
+constexpr int T5_MAX_L = 512;
+constexpr int QW = 8;  // queries per wave
+constexpr int KROW = 66;
+
+__global__ __launch_bounds__(256) void t5_attention_kernel(const bf16* __restrict__ qkv, int64_t ld, int inner,
+                                                           int L, int H, const bf16* __restrict__ bias_table,
+                                                           const int32_t* __restrict__ buckets,
+                                                           const int64_t* __restrict__ mask, bf16* __restrict__ out,
+                                                           int64_t ldo) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int Lp = (L + 7) & ~7;                 // 16-byte aligned sub-arrays
+  bf16* Ks = (bf16*)smem;                       // [Lp][KROW]
+  bf16* Vs = Ks + Lp * KROW;                    // [Lp][64]
+  float* Ps = (float*)(Vs + Lp * 64);           // [4 waves][Lp]
+  const int nqb = (L + 4 * QW - 1) / (4 * QW);
+  const int bh = blockIdx.x / nqb, qb = blockIdx.x - bh * nqb;
+  const int b = bh / H, h = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16* base = qkv + (int64_t)b * L * ld;
+  for (int i = tid; i < L * 8; i += 256) {
+    const int j = i >> 3, c = i & 7;
+    const bf16x8 kv = *(const bf16x8*)(base + (int64_t)j * ld + inner + h * 64 + c * 8);
+    const bf16x8 vv = *(const bf16x8*)(base + (int64_t)j * ld + 2 * inner + h * 64 + c * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) Ks[j * KROW + c * 8 + e] = kv[e];
+    *(bf16x8*)(Vs + j * 64 + c * 8) = vv;
+  }
+  __syncthreads();
+  float* P = Ps + wave * Lp;
+  for (int qi = 0; qi < QW; ++qi) {
+    const int q = (qb * 4 + wave) * QW + qi;
+    if (q >= L) break;  // wave-uniform
+    const bf16* qrow = base + (int64_t)q * ld + h * 64;
+    float qv[64];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const bf16x8 v = *(const bf16x8*)(qrow + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qv[c * 8 + e] = bf2f(v[e]);
+    }
+    float mx = -INFINITY;
+    for (int j = lane; j < L; j += 64) {
+      float s = 0.f;
+      const bf16* kr = Ks + j * KROW;
+#pragma unroll
+      for (int e = 0; e < 64; e += 2) {
+        const bf16x2 k2 = *(const bf16x2*)(kr + e);
+        s = __builtin_fmaf(qv[e], bf2f(k2[0]), s);
+        s = __builtin_fmaf(qv[e + 1], bf2f(k2[1]), s);
+      }
+      float sc = rbf(rbf(s) + bf2f(bias_table[buckets[q * L + j] * H + h]));
+      if (mask != nullptr && mask[(int64_t)b * L + j] == 0) sc = rbf(sc + -3.3895313892515355e38f);
+      P[j] = sc;
+      mx = fmaxf(mx, sc);
+    }
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int j = lane; j < L; j += 64) {
+      const float e = __expf(P[j] - mx);
+      P[j] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    const float inv = 1.f / sum;
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    // out[d = lane] = sum_j bf16(p_j / sum) v_j[d]
+    float acc = 0.f;
+    for (int j = 0; j < L; ++j) acc = __builtin_fmaf(rbf(P[j] * inv), bf2f(Vs[j * 64 + lane]), acc);
+    out[(int64_t)(b * L + q) * ldo + h * 64 + lane] = f2bf(acc);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+int grid_for(int64_t work) {
+  const int64_t g = (work + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > (1 << 20) ? (1 << 20) : g));
+}
+
+}  // namespace
+
+extern "C" int vp_embedding_gather_bf16(const void* table, const int64_t* ids, void* out, int32_t rows, int32_t D,
+                                        int32_t vocab, void* stream) {
+  if (table == nullptr || ids == nullptr || out == nullptr || rows <= 0 || D <= 0 || (D % 8) || vocab <= 0)
+    return VP_ERR_ARG;
+  hipLaunchKernelGGL(embed_gather_kernel, dim3(grid_for((int64_t)rows * (D / 8))), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)table, ids, (bf16*)out, rows, D, vocab);
+  VP_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vp_rms_norm_bf16(const void* x, const void* w, void* y, int32_t rows, int32_t D, float eps,
+                                void* stream) {
+  if (x == nullptr || w == nullptr || y == nullptr || rows <= 0 || D <= 0 || (D % 8)) return VP_ERR_ARG;
+  hipLaunchKernelGGL(rms_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, (const bf16*)x,
+                     (const bf16*)w, (bf16*)y, rows, D, eps);
+  VP_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vp_mul_bf16(const void* a, const void* b, void* y, int64_t n, void* stream) {
+  if (a == nullptr || b == nullptr || y == nullptr || n <= 0 || (n % 8)) return VP_ERR_ARG;
+  hipLaunchKernelGGL(mul_kernel, dim3(grid_for(n / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16*)a,
+                     (const bf16*)b, (bf16*)y, n / 8);
+  VP_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vp_t5_attention_bf16(const void* qkv, int64_t ld, int32_t inner, int32_t B, int32_t L, int32_t H,
+                                    const void* bias_table, const int32_t* buckets, const int64_t* mask, void* out,
+                                    int64_t ldo, void* stream) {
+  if (qkv == nullptr || bias_table == nullptr || buckets == nullptr || out == nullptr) return VP_ERR_ARG;
+  if (B <= 0 || L <= 0 || H <= 0 || inner != H * 64 || ld < 3 * inner || (ld % 8) || ldo < inner) return VP_ERR_ARG;
+  if (L > T5_MAX_L) return VP_ERR_UNSUPPORTED;
+  const size_t Lp = (size_t)((L + 7) & ~7);
+  const size_t lds = Lp * KROW * 2 + Lp * 64 * 2 + 4 * Lp * 4;
+  static bool attr = false;
+  if (!attr) {
+    const size_t mx = (size_t)T5_MAX_L * (KROW * 2 + 64 * 2 + 16);
+    (void)hipFuncSetAttribute((const void*)t5_attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mx);
+    attr = true;
+  }
+  const int nqb = (L + 4 * QW - 1) / (4 * QW);
+  hipLaunchKernelGGL(t5_attention_kernel, dim3(B * H * nqb), dim3(256), lds, (hipStream_t)stream,
+                     (const bf16*)qkv, ld, inner, L, H, (const bf16*)bias_table, buckets, mask, (bf16*)out, ldo);
+  VP_CHECK_LAUNCH();
+  return 0;
+}

@@ -726,3 +726,61 @@ def tile_blend_(a: torch.Tensor, b: torch.Tensor, axis: int, extent: int) -> tor
     N.check(N.lib().vp_tile_blend_bf16(_p(a), _p(b), B, T, Ha, Wa, Hb, Wb, Cc, axis, extent, _stream()),
             "vp_tile_blend_bf16")
     return b
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# T5 encoder pieces
+# ------------------------------------------------------------------------------------------------------------------
+
+def embedding_gather(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    _chk(table, "table")
+    if not ids.is_cuda or ids.dtype != torch.int64:
+        raise TypeError("ids must be an int64 device tensor")
+    ids = ids.contiguous()
+    vocab, D = table.shape
+    out = torch.empty(ids.numel(), D, device=table.device, dtype=BF16)
+    N.check(N.lib().vp_embedding_gather_bf16(_p(table), _p(ids), _p(out), ids.numel(), D, vocab, _stream()),
+            "vp_embedding_gather_bf16")
+    return out
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _chk(x, "x")
+    _chk(w, "w")
+    D = x.shape[-1]
+    if not x.is_contiguous() or w.numel() != D:
+        raise ValueError("rms_norm: x must be contiguous with the weight's width")
+    out = torch.empty_like(x) if out is None else out
+    N.check(N.lib().vp_rms_norm_bf16(_p(x), _p(w), _p(out), x.numel() // D, D, eps, _stream()), "vp_rms_norm_bf16")
+    return out
+
+
+def mul(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _chk(a, "a")
+    _chk(b, "b")
+    if a.shape != b.shape or not a.is_contiguous() or not b.is_contiguous():
+        raise ValueError("mul: contiguous operands of one shape")
+    out = torch.empty_like(a) if out is None else out
+    N.check(N.lib().vp_mul_bf16(_p(a), _p(b), _p(out), a.numel(), _stream()), "vp_mul_bf16")
+    return out
+
+
+def t5_attention(qkv: torch.Tensor, B: int, L: int, H: int, bias_table: torch.Tensor, buckets: torch.Tensor,
+                 mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """qkv [B * L, 3 * H * 64] (q | k | v) -> [B * L, H * 64]."""
+    _chk(qkv, "qkv")
+    _chk(bias_table, "bias_table")
+    _chk(buckets, "buckets", torch.int32)
+    inner = H * 64
+    if qkv.shape != (B * L, 3 * inner) or buckets.shape != (L, L) or bias_table.shape[1] != H:
+        raise ValueError("t5_attention: shape mismatch")
+    if mask is not None:
+        _chk(mask, "mask", torch.int64)
+        if mask.shape != (B, L):
+            raise ValueError("t5_attention: mask must be [B, L]")
+        mask = mask.contiguous()
+    out = torch.empty(B * L, inner, device=qkv.device, dtype=BF16)
+    N.check(N.lib().vp_t5_attention_bf16(_p(qkv), qkv.stride(0), inner, B, L, H, _p(bias_table.contiguous()),
+                                         _p(buckets.contiguous()), _p(mask), _p(out), out.stride(0), _stream()),
+            "vp_t5_attention_bf16")
+    return out
