@@ -411,6 +411,20 @@ int vp_t5_attention_bf16(const void* qkv, int64_t ld, int32_t inner, int32_t B, 
                          void* stream);
 
 
+/* ---- pixel-space glue of the any-length pipeline's VAE stage (…_anyl.py:339-484) ---- */
+/* y = bf16(x * s) (the latents' scaling_factor and its inverse, :372 / :430 / :481) */
+int vp_scale_bf16(const void* x, void* y, int64_t n, float s, void* stream);
+/* out = video * (mask < 0.5) (keep_above: >= 0.5, mask_background) over [B, C, P] with mask [B, 1, P] fp32
+ * (:890-893); video fp32 or bf16, out bf16 */
+int vp_mask_video_bf16(const void* video, int32_t video_is_f32, const float* mask, int32_t keep_above, void* out,
+                       int32_t B, int32_t C, int64_t P, void* stream);
+/* F.interpolate(mode="nearest", size=(t, h, w)) of fp32 [BC, T, H, W] -> bf16 (:437-439) */
+int vp_nearest_resize3d_bf16(const float* x, void* y, int32_t BC, int32_t T, int32_t H, int32_t W, int32_t t,
+                             int32_t h, int32_t w, void* stream);
+/* VaeImageProcessor.denormalize on bf16: (x / 2 + 0.5).clamp(0, 1) */
+int vp_denormalize_bf16(const void* x, void* y, int64_t n, void* stream);
+
+
 #ifdef __cplusplus
 }
 #endif

@@ -231,3 +231,15 @@ def t5_inputs(vocab: int, key: str = "t5"):
         ids[b, n + 1:] = 0
         mask[b, n + 1:] = 0
     return torch.from_numpy(ids), torch.from_numpy(mask)
+
+
+def pipe_pixel_inputs():
+    """The video / masked-video / first-frame processors' outputs for pipe_inputs() (no resize at 128x192):
+    video [1, 3, T, H, W] = frames / 255 * 2 - 1, masks [1, 1, T, H, W] = the (binary) mask / 255, image = frame 0
+    [1, 3, H, W]; pinned to the reference's own tensors by the digests in pipe_pixels.safetensors."""
+    inp = pipe_inputs()
+    fr = torch.from_numpy(inp["frames"]).float()
+    video = (fr / 255.0 * 2 - 1).permute(3, 0, 1, 2)[None].contiguous()
+    masks = (torch.from_numpy(inp["masks"]).float()[..., 0] / 255.0)[None, None].contiguous()
+    return dict(video=video, masks=masks, image=video[:, :, 0].contiguous(), prompt_embeds=inp["prompt_embeds"],
+                negative_prompt_embeds=inp["negative_prompt_embeds"])

@@ -220,6 +220,76 @@ def make_pipe():
 
 
 @torch.no_grad()
+def make_pipe_pixels():
+    """The same any-length run as make_pipe (2 windows x 2 steps, ID-resample + prev-clip) from PIXELS with the
+    counter-weight tiny VAE (VAE_TINY_CFG / VAE_SEEDS[0], so the HIP side can rebuild it) and output_type="pt":
+    records the video / mask / first-frame processors' outputs (the HIP harness's inputs), every window's
+    prepare_latents / prepare_mask_latents outputs, the overlap-averaged latents and the decoded frames.
+    pipe_pixels.safetensors."""
+    from diffusers import AutoencoderKLCogVideoX, CogVideoXDPMScheduler
+    from diffusers.pipelines.cogvideo.pipeline_cogvideox_inpainting_i2v_branch_anyl import (
+        CogVideoXI2VDualInpaintAnyLPipeline)
+    from PIL import Image
+    from tests.golden.cases import VAE_TINY_CFG, VAE_SEEDS
+    c = PIPE_CASE
+    tr, br = build_models(resample=c["id_pool_resample_learnable"])
+    with torch.device("meta"):
+        vae = AutoencoderKLCogVideoX(**VAE_TINY_CFG).eval()
+    vae = _fill_synthetic(vae, VAE_SEEDS[0])
+    sch = CogVideoXDPMScheduler(snr_shift_scale=1.0, prediction_type="v_prediction", rescale_betas_zero_snr=True,
+                                clip_sample=False, set_alpha_to_one=True, timestep_spacing="trailing",
+                                beta_start=0.00085, beta_end=0.012)
+    pipe = CogVideoXI2VDualInpaintAnyLPipeline(tokenizer=None, text_encoder=None, vae=vae, transformer=tr,
+                                               scheduler=sch, branch=br)
+    rec = {"latents": [], "mask": [], "video": [], "maskc": [], "image": [], "acc": []}
+
+    def wrap(obj, name, key):
+        orig = getattr(obj, name)
+
+        def f(*a, **k):
+            o = orig(*a, **k)
+            rec[key].append(o.clone() if torch.is_tensor(o) else [x.clone() for x in o])
+            return o
+        setattr(obj, name, f)
+    wrap(pipe, "prepare_latents", "latents")
+    wrap(pipe, "prepare_mask_latents", "mask")
+    wrap(pipe.video_processor, "preprocess_video", "video")
+    wrap(pipe.masked_video_processor, "preprocess_video", "maskc")
+    wrap(pipe.video_processor, "preprocess", "image")
+    orig_dec = pipe.decode_latents
+
+    def dec(latents):
+        rec["acc"].append(latents.clone())
+        return orig_dec(latents)
+    pipe.decode_latents = dec
+    inp = pipe_inputs()
+    frames = [Image.fromarray(f) for f in inp["frames"]]
+    masks = [Image.fromarray(m) for m in inp["masks"]]
+    res = pipe(prompt_embeds=inp["prompt_embeds"], negative_prompt_embeds=inp["negative_prompt_embeds"],
+               image=frames[0], video=frames, masks=masks, num_frames=c["num_frames"], height=c["height"],
+               width=c["width"], num_inference_steps=c["steps"], use_dynamic_cfg=True, guidance_scale=6.0,
+               generator=torch.Generator().manual_seed(42), strength=1.0, replace_gt=True, mask_add=True,
+               stride=c["stride"], prev_clip_weight=c["prev_clip_weight"],
+               id_pool_resample_learnable=c["id_pool_resample_learnable"], output_type="pt", return_dict=False)[0]
+    # decoded frames kept at every second row / column; the processors' outputs are NOT stored (they are exactly
+    # frames / 255 * 2 - 1 and mask / 255: tests/golden/cases.pipe_pixel_inputs rebuilds them) — their fp64 digests
+    # pin that reconstruction
+    dig = lambda t: torch.tensor([t.double().sum(), t.double().abs().sum(), t.double().norm()], dtype=torch.float64)  # noqa: E731
+    image = [t for t in rec["image"] if t.shape[0] == 1][0]
+    out = {"frames_s2": res[..., ::2, ::2], "frames_shape": torch.tensor(res.shape, dtype=torch.float32),
+           "latents": rec["acc"][0], "image_digest": dig(image),
+           "video_digest": dig(torch.cat(rec["video"], dim=2)), "masks_digest": dig(torch.cat(rec["maskc"], dim=2))}
+    for w, (lat, img, noise, vid) in enumerate(rec["latents"]):
+        out[f"w{w}.latents"], out[f"w{w}.image_latents"], out[f"w{w}.video_latents"] = lat, img, vid
+    for w, (m, mv) in enumerate(rec["mask"]):
+        out[f"w{w}.mask"], out[f"w{w}.masked_video_latents"] = m, mv
+    print("pipe pixels:", {k: tuple(v.shape) for k, v in out.items()}, flush=True)
+    save_file({k: (v.contiguous() if v.dtype == torch.float64 else v.detach().float().contiguous())
+               for k, v in out.items()}, os.path.join(HERE, "pipe_pixels.safetensors"),
+              metadata={"case": json.dumps(c)})
+
+
+@torch.no_grad()
 def make_full_block():
     from diffusers.models.transformers.cogvideox_transformer_3d import CogVideoXBlock
     case = full_block_case()
@@ -464,6 +534,8 @@ if __name__ == "__main__":
         make_vae_tiled()
     if "t5" in which:
         make_t5()
+    if "pipe_pixels" in which:
+        make_pipe_pixels()
     if "tiny" in which:
         make_tiny()
     if "sched" in which:

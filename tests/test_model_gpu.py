@@ -285,6 +285,48 @@ def test_anyl_harness_matches_reference_pipeline(env):
 
 
 @torch.no_grad()
+def test_pixel_pipeline_matches_reference(env):
+    """The whole any-length call from pixels (tests/golden/pipe_pixels.safetensors: the reference pipeline with the
+    counter-weight tiny VAE, output_type="pt", fp32): the HIP VAE encodes every window (first frame, video, masked
+    video; posterior and initial noise drawn from the same generator in the reference's order), the step loop runs as
+    in the latent harness, and the HIP VAE decodes the overlap-averaged latents.  The reference ran in fp32 with fp32
+    draws (noise_dtype=float32 here); the HIP path computes in bf16."""
+    from videopainter_amd.pipeline import CogVideoXI2VDualInpaintAnyLHarness
+    from videopainter_amd.scheduler import CogVideoXDPMScheduler
+    from videopainter_amd.vae import AutoencoderKLCogVideoX
+    from tests.golden.cases import VAE_TINY_CFG, VAE_SEEDS, pipe_pixel_inputs, vae_weights
+    g = load_file(os.path.join(GOLD, "pipe_pixels.safetensors"))
+    c = PIPE_CASE
+    vae = AutoencoderKLCogVideoX.from_config(VAE_TINY_CFG, device=dev)
+    vae.load_diffusers_state_dict({k: torch.from_numpy(v) for k, v in vae_weights(VAE_TINY_CFG, VAE_SEEDS[0]).items()})
+    sch = CogVideoXDPMScheduler(snr_shift_scale=1.0, prediction_type="v_prediction", rescale_betas_zero_snr=True,
+                                clip_sample=False, set_alpha_to_one=True, timestep_spacing="trailing",
+                                beta_start=0.00085, beta_end=0.012)
+    h = CogVideoXI2VDualInpaintAnyLHarness(env["trr"], env["br"], sch, vae=vae, noise_dtype=torch.float32)
+    inp = pipe_pixel_inputs()
+    # window 0's VAE stage alone, against the reference's prepare_latents / prepare_mask_latents outputs
+    gen = torch.Generator().manual_seed(42)
+    win = h.encode_window(0, inp["video"][:, :, :c["num_frames"]], inp["masks"][:, :, :c["num_frames"]],
+                          inp["image"], gen, None, c["num_frames"], c["stride"])
+    for k in ("latents", "mask"):  # the same generator draw / the same nearest pick, rounded to bf16
+        assert torch.equal(win[k].float().cpu(), g[f"w0.{k}"].bfloat16().float()), k
+    for k in ("image_latents", "video_latents", "masked_video_latents"):
+        r = rel(win[k], g[f"w0.{k}"])
+        print(f"pixel pipeline w0.{k}: rel {r:.3e}")
+        assert r < 3e-2, k
+    frames = h.generate(inp["video"], inp["masks"], inp["image"], inp["prompt_embeds"],
+                        inp["negative_prompt_embeds"], generator=torch.Generator().manual_seed(42),
+                        num_inference_steps=c["steps"], num_frames=c["num_frames"], stride=c["stride"],
+                        guidance_scale=6.0, use_dynamic_cfg=True, replace_gt=True, mask_add=True,
+                        prev_clip_weight=c["prev_clip_weight"], id_pool_resample_learnable=c["id_pool_resample_learnable"],
+                        output_type="pt")
+    assert tuple(frames.shape) == tuple(int(v) for v in g["frames_shape"])
+    rf = rel(frames[..., ::2, ::2], g["frames_s2"])
+    print(f"pixel pipeline frames: rel {rf:.3e}")
+    assert rf < 3e-2
+
+
+@torch.no_grad()
 def test_cfg_split_halves_bit_exact(env):
     """CFG split (SURVEY.md §8e latency mode) is exact: each CFG half run alone at B=1 — what one rank of a
     `CFGPair` computes — reproduces its half of the B=2 forward bit for bit (branch, noise prediction, hidden-state

@@ -199,3 +199,14 @@ def test_t5_oracle_matches_transformers(tag):
         assert rel(y[..., ::stride], g[f"{tag}.out"]) < 1e-5
         if tag == "tiny":
             assert rel(T.encoder_forward(sd, fc, ids, mask), g["tiny.masked.out"]) < 1e-5
+
+
+def test_pipe_pixel_inputs_are_the_reference_processor_outputs():
+    """tests/golden/cases.pipe_pixel_inputs rebuilds the video / mask / first-frame processors' outputs the reference
+    pipeline produced (pipe_pixels.safetensors holds their fp64 digests, not the tensors)."""
+    from tests.golden.cases import pipe_pixel_inputs
+    g = load_file(os.path.join(GOLD, "pipe_pixels.safetensors"))
+    inp = pipe_pixel_inputs()
+    for k, t in (("video", inp["video"]), ("masks", inp["masks"]), ("image", inp["image"])):
+        d = torch.tensor([t.double().sum(), t.double().abs().sum(), t.double().norm()], dtype=torch.float64)
+        assert torch.allclose(d, g[f"{k}_digest"], rtol=1e-12, atol=1e-9), k

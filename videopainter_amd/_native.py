@@ -122,6 +122,10 @@ _SIGS = {
     "vp_rms_norm_bf16": (i32, [vp, vp, vp, i32, i32, f32, vp]),
     "vp_mul_bf16": (i32, [vp, vp, vp, i64, vp]),
     "vp_t5_attention_bf16": (i32, [vp, i64, i32, i32, i32, i32, vp, vp, vp, vp, i64, vp]),
+    "vp_scale_bf16": (i32, [vp, vp, i64, f32, vp]),
+    "vp_mask_video_bf16": (i32, [vp, i32, vp, i32, vp, i32, i32, i64, vp]),
+    "vp_nearest_resize3d_bf16": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "vp_denormalize_bf16": (i32, [vp, vp, i64, vp]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -784,3 +784,51 @@ def t5_attention(qkv: torch.Tensor, B: int, L: int, H: int, bias_table: torch.Te
                                          _p(buckets.contiguous()), _p(mask), _p(out), out.stride(0), _stream()),
             "vp_t5_attention_bf16")
     return out
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# pixel-space glue of the pipeline's VAE stage
+# ------------------------------------------------------------------------------------------------------------------
+
+def scale_bf16(x: torch.Tensor, s: float) -> torch.Tensor:
+    _chk(x, "x")
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    N.check(N.lib().vp_scale_bf16(_p(x), _p(out), x.numel(), s, _stream()), "vp_scale_bf16")
+    return out
+
+
+def mask_video(video: torch.Tensor, mask: torch.Tensor, keep_above: bool = False) -> torch.Tensor:
+    """bf16(video * (mask < 0.5)) — or (mask >= 0.5) for keep_above — video [B, C, F, H, W] fp32/bf16, mask
+    [B, 1, F, H, W] fp32."""
+    if not video.is_cuda or video.dtype not in (torch.float32, BF16):
+        raise TypeError("mask_video: video must be a float32 / bfloat16 device tensor")
+    _chk(mask, "mask", torch.float32)
+    video, mask = video.contiguous(), mask.contiguous()
+    B, Cc = video.shape[:2]
+    P = video[0, 0].numel()
+    if mask.shape[0] != B or mask.shape[1] != 1 or mask[0, 0].numel() != P:
+        raise ValueError("mask_video: mask must be [B, 1, F, H, W] matching the video")
+    out = torch.empty(video.shape, device=video.device, dtype=BF16)
+    N.check(N.lib().vp_mask_video_bf16(_p(video), int(video.dtype == torch.float32), _p(mask), int(keep_above),
+                                       _p(out), B, Cc, P, _stream()), "vp_mask_video_bf16")
+    return out
+
+
+def nearest_resize_3d(x: torch.Tensor, size) -> torch.Tensor:
+    _chk(x, "x", torch.float32)
+    x = x.contiguous()
+    B, Cc, T, H, W = x.shape
+    t, h, w = size
+    out = torch.empty(B, Cc, t, h, w, device=x.device, dtype=BF16)
+    N.check(N.lib().vp_nearest_resize3d_bf16(_p(x), _p(out), B * Cc, T, H, W, t, h, w, _stream()),
+            "vp_nearest_resize3d_bf16")
+    return out
+
+
+def denormalize_bf16(x: torch.Tensor) -> torch.Tensor:
+    _chk(x, "x")
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    N.check(N.lib().vp_denormalize_bf16(_p(x), _p(out), x.numel(), _stream()), "vp_denormalize_bf16")
+    return out

@@ -1,10 +1,13 @@
-"""Latent-space harness of the any-length VideoPainter pipeline's hot loop.
+"""Harness of the any-length VideoPainter pipeline on the HIP models.
 
 Restates the step loop of `CogVideoXI2VDualInpaintAnyLPipeline.__call__`
 (DF/pipelines/cogvideo/pipeline_cogvideox_inpainting_i2v_branch_anyl.py:932-1050) and its window loop
-(:759, 828-872, 962-988, 1052-1069) on the HIP models, starting from the latents the VAE / T5 stages would have
-produced (those stages run once per window and are out of scope this round).  One denoising step =
-branch forward + transformer forward at B=2 (CFG) + one fused CFG/DPM/replace-gt kernel.
+(:759, 828-872, 962-988, 1052-1069).  `__call__` starts from the per-window latents the VAE stage produced;
+`generate` starts from the preprocessed pixels (the video / mask processors' outputs) and runs the VAE stage on the HIP
+VAE too — per window prepare_latents (:339-412: first-frame encode, video encode, initial noise) and
+prepare_mask_latents (:434-477: nearest mask resize, masked-video encode), drawing from the caller's generator in
+the reference's order — then decodes the overlap-averaged latents (decode_latents :479-484, :1071-1073).  One
+denoising step = branch forward + transformer forward at B=2 (CFG) + one fused CFG/DPM/replace-gt kernel.
 
 Reference quirks reproduced on purpose:
   * dynamic CFG uses the raw timestep t (anyl.py:991-994);
@@ -44,7 +47,7 @@ class WindowState:
 
 class CogVideoXI2VDualInpaintAnyLHarness:
     def __init__(self, transformer, branch, scheduler, vae_scale_factor_spatial: int = 8,
-                 vae_scale_factor_temporal: int = 4, cfg_pair=None):
+                 vae_scale_factor_temporal: int = 4, cfg_pair=None, vae=None, noise_dtype=BF16):
         """cfg_pair: optional `distributed.CFGPair`.  The two CFG halves of every step then run on the pair's two
         ranks at B=1 and their noise predictions are all-gathered (latency mode); both ranks apply the
         same CFG combine + DPM step with the same generator stream, so their latents stay bit-identical."""
@@ -55,6 +58,11 @@ class CogVideoXI2VDualInpaintAnyLHarness:
         self.vae_scale_factor_temporal = vae_scale_factor_temporal
         self.prev_resample_mask = None
         self.cfg_pair = cfg_pair
+        self.vae = vae
+        # dtype of every generator draw (posterior samples, initial noise, scheduler noise): the reference draws in the
+        # pipeline's dtype (bf16 in the inference scripts); torch's CPU generator gives different values for a bf16
+        # and an fp32 draw of the same shape, so replaying an fp32 reference run needs float32 here
+        self.noise_dtype = noise_dtype
 
     @property
     def device(self):
@@ -137,7 +145,8 @@ class CogVideoXI2VDualInpaintAnyLHarness:
         def draw():
             if step_noise is not None:
                 return step_noise().to(dev, BF16).contiguous()
-            return randn_tensor(lat.shape, generator=generator, device=dev, dtype=BF16).contiguous()
+            n = randn_tensor(lat.shape, generator=generator, device=dev, dtype=self.noise_dtype)
+            return n.to(BF16).contiguous()
 
         noise1 = draw()
         noise2 = draw() if second else None
@@ -274,6 +283,82 @@ class CogVideoXI2VDualInpaintAnyLHarness:
                                                     capture=w < n_windows - 1, **kw)
             outs.append(latents)
         return self.assemble(outs, num_frames, stride)
+
+
+    # ------------------------------------------------------------------------------------------------------------
+    # pixel-space entry: the VAE stage of each window on the HIP VAE
+    # ------------------------------------------------------------------------------------------------------------
+    def _vae_sample(self, x: torch.Tensor, generator) -> torch.Tensor:
+        """retrieve_latents(vae.encode(x), generator) * scaling_factor, as [B, F, C, h, w] (anyl.py:145-152,
+        412-423); the posterior noise is drawn from the caller's generator in `noise_dtype`."""
+        post = self.vae.encode(x).latent_dist
+        noise = randn_tensor(post.mean.shape, generator=generator, dtype=self.noise_dtype)
+        z = post.sample_from(noise)
+        return K.scale_bf16(z, float(self.vae.config.scaling_factor)).permute(0, 2, 1, 3, 4)
+
+    def encode_window(self, w: int, window_video: torch.Tensor, mask_condition: torch.Tensor,
+                      image: Optional[torch.Tensor], generator, prev_latents: Optional[torch.Tensor], num_frames: int,
+                      stride: int, mask_background: bool = False) -> dict:
+        """prepare_latents + prepare_mask_latents of window w (anyl.py:339-477, 852-908) from the preprocessed window
+        video [1, 3, F, H, W] in [-1, 1], mask [1, 1, F, H, W] in [0, 1] and (window 0) the first frame [1, 3, H, W].
+        Generator order as the reference: first-frame posterior (window 0), video posterior, initial noise,
+        masked-video posterior."""
+        dev = self.device
+        vt = self.vae_scale_factor_temporal
+        F, H, W = window_video.shape[2:]
+        lf, hh, ww = (F - 1) // vt + 1, H // self.vae_scale_factor_spatial, W // self.vae_scale_factor_spatial
+        C = self.transformer.config.in_channels // 2
+        video = window_video.to(dev)
+        if w == 0:
+            img_lat = self._vae_sample(image.to(dev).unsqueeze(2), generator)  # [1, 1, C, h, w]
+            image_latents = torch.cat([img_lat, torch.zeros(1, lf - 1, C, hh, ww, device=dev, dtype=BF16)], dim=1)
+        else:
+            image_latents = self.window_image_latents(w, {}, prev_latents, num_frames, stride)
+        video_latents = self._vae_sample(video, generator)
+        noise = randn_tensor((1, lf, C, hh, ww), generator=generator, device=dev, dtype=self.noise_dtype).to(BF16)
+        mcond = mask_condition.to(dev, torch.float32)
+        masked = K.mask_video(video, mcond, keep_above=mask_background)
+        mask = K.nearest_resize_3d(mcond, (lf, hh, ww))
+        masked_latents = self._vae_sample(masked, generator)
+        return dict(latents=noise, noise=noise, image_latents=image_latents, video_latents=video_latents,
+                    mask=torch.cat([mask] * 2), masked_video_latents=torch.cat([masked_latents] * 2))
+
+    def decode(self, latents: torch.Tensor, output_type: str = "pt") -> torch.Tensor:
+        """decode_latents (anyl.py:479-484) + the video processor's denormalisation for output_type "pt"
+        ([B, F, 3, H, W] in [0, 1]); "raw" returns the VAE output [B, 3, F, H, W] in [-1, 1]."""
+        z = K.scale_bf16(latents.permute(0, 2, 1, 3, 4).contiguous(), 1.0 / float(self.vae.config.scaling_factor))
+        video = self.vae.decode(z).sample
+        if output_type == "raw":
+            return video
+        return K.denormalize_bf16(video).permute(0, 2, 1, 3, 4)
+
+    @torch.no_grad()
+    def generate(self, video: torch.Tensor, masks: torch.Tensor, image: torch.Tensor, prompt_embeds: torch.Tensor,
+                 negative_prompt_embeds: torch.Tensor, *, generator=None, num_inference_steps: int = 50,
+                 num_frames: int = 49, stride: Optional[int] = None, output_type: str = "pt",
+                 mask_background: bool = False, **kw) -> torch.Tensor:
+        """The whole any-length call from preprocessed pixels: video [1, 3, T, H, W] in [-1, 1] (preprocess_video),
+        masks [1, 1, T, H, W] in [0, 1] (the masked-video processor), image [1, 3, H, W] (the first frame, window 0).
+        Returns the latent video ("latent") or the decoded frames ("pt": [1, F, 3, H, W] in [0, 1])."""
+        if self.vae is None:
+            raise ValueError("generate() needs the harness built with vae=")
+        stride = num_frames if stride is None else stride
+        pe, timesteps = self.prepare_call(prompt_embeds, negative_prompt_embeds, num_inference_steps)
+        total = video.shape[2]
+        n_windows = (total - num_frames) // stride + 1
+        outs = []
+        latents, states, mask = None, None, None
+        for w in range(n_windows):
+            s0 = w * stride
+            win = self.encode_window(w, video[:, :, s0:s0 + num_frames], masks[:, :, s0:s0 + num_frames],
+                                     image if w == 0 else None, generator, latents, num_frames, stride,
+                                     mask_background=mask_background)
+            latents, states, mask = self.run_window(w, win, win["image_latents"], pe, timesteps, prev_states=states,
+                                                    prev_mask=mask, capture=w < n_windows - 1, generator=generator,
+                                                    **kw)
+            outs.append(latents)
+        lat = self.assemble(outs, num_frames, stride)
+        return lat if output_type == "latent" else self.decode(lat, output_type)
 
 
 @torch.no_grad()
