@@ -21,6 +21,12 @@ def __getattr__(name):
     if name in ("CogVideoXDPMScheduler",):
         from . import scheduler
         return getattr(scheduler, name)
+    if name in ("AutoencoderKLCogVideoX",):
+        from . import vae
+        return getattr(vae, name)
+    if name in ("T5EncoderModel",):
+        from . import t5
+        return getattr(t5, name)
     if name in ("CogVideoXI2VDualInpaintAnyLHarness",):
         from . import pipeline
         return getattr(pipeline, name)
