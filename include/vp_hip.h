@@ -26,12 +26,12 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 7
+#define VP_ABI_VERSION 8
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
-/* sizeof of the descriptor structs as compiled into the library: out[0..5] = gemm, attn, dpm, gemm_mx, attn_fp8,
- * conv3d (ABI check) */
+/* sizeof of the descriptor structs as compiled into the library: out[0..6] = gemm, attn, dpm, gemm_mx, attn_fp8,
+ * conv3d, attn_bwd (ABI check) */
 void vp_struct_sizes(int64_t* out);
 
 /* ---------------------------------------------------------------------------------------------------------------
@@ -168,6 +168,8 @@ typedef struct vp_attn_desc {
                     every (query, key) pair, so the kernel runs without a running max (exact: bf16/fp32 hold
                     2^+-60 and O / l is invariant to the reference point).  CogVideoX's qk-LayerNorm gives the bound
                     from the norm weights: videopainter_amd.kernels.score_bound_log2. */
+  float* lse;     /* optional fp32 [B, H, Nq]: per query log2-sum-exp2 of the scaled log2-unit scores (m + log2 l), the
+                     softmax statistics vp_attention_bwd_bf16 recomputes P from (bf16 kernel only; NULL: not written) */
 } vp_attn_desc;
 #define VP_ATTN_BOUNDED_SCORES 1
 #define VP_ATTN_SCORE_BOUND 60.0f
@@ -423,6 +425,36 @@ int vp_nearest_resize3d_bf16(const float* x, void* y, int32_t BC, int32_t T, int
                              int32_t h, int32_t w, void* stream);
 /* VaeImageProcessor.denormalize on bf16: (x / 2 + 0.5).clamp(0, 1) */
 int vp_denormalize_bf16(const void* x, void* y, int64_t n, void* stream);
+
+
+/* ---- backward (train/train_cogvideox_inpainting_i2v_video.py:1892 accelerator.backward) ---- */
+/* Flash-attention backward of vp_attention_fwd_bf16 (one K/V segment, no blend): with P = exp2(c q.k - lse),
+ * c = scale * log2 e, lse from the forward's vp_attn_desc.lse: dQ = scale dS K, dK = scale dS^T Q, dV = P^T dO with
+ * dS = P (dO V^T - rowsum(dO O)).  delta: fp32 workspace [B, H, Nq].  All tensors [B, N, H*64]-strided bf16. */
+typedef struct vp_attn_bwd_desc {
+  int32_t B, H, Nq, Nk, head_dim, pad0;
+  const void* Q;
+  int64_t q_sb, q_sn;
+  const void* K;
+  int64_t k_sb, k_sn;
+  const void* V;
+  int64_t v_sb, v_sn;
+  const void* O;
+  int64_t o_sb, o_sn;
+  const void* dO;
+  int64_t do_sb, do_sn;
+  const float* lse;
+  float* delta;
+  void* dQ;
+  int64_t dq_sb, dq_sn;
+  void* dK;
+  int64_t dk_sb, dk_sn;
+  void* dV;
+  int64_t dv_sb, dv_sn;
+  float scale;
+  int32_t pad1;
+} vp_attn_bwd_desc;
+int vp_attention_bwd_bf16(const vp_attn_bwd_desc* d, void* stream);
 
 
 #ifdef __cplusplus

@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -43,7 +43,7 @@ class AttnDesc(C.Structure):
                 ("Nk", i32), ("Nk2", i32),
                 ("K2", vp), ("V2", vp), ("k2_sb", i64), ("k2_sn", i64), ("v2_sb", i64), ("v2_sn", i64),
                 ("O", vp), ("o_sb", i64), ("o_sn", i64),
-                ("scale", f32), ("out_scale", f32), ("accumulate", i32), ("flags", i32)]
+                ("scale", f32), ("out_scale", f32), ("accumulate", i32), ("flags", i32), ("lse", vp)]
 
 
 class GemmMxDesc(C.Structure):
@@ -73,6 +73,15 @@ class Conv3dDesc(C.Structure):
                 ("ph", i32), ("pw", i32), ("uh", i32), ("uw", i32), ("x_frames", i32), ("hist_frames", i32),
                 ("ldy", i32), ("ldr", i32), ("tmap", i32 * CONV_MAX_T),
                 ("x", vp), ("hist", vp), ("w", vp), ("bias", vp), ("resid", vp), ("y", vp)]
+
+
+class AttnBwdDesc(C.Structure):
+    _fields_ = [("B", i32), ("H", i32), ("Nq", i32), ("Nk", i32), ("head_dim", i32), ("pad0", i32),
+                ("Q", vp), ("q_sb", i64), ("q_sn", i64), ("K", vp), ("k_sb", i64), ("k_sn", i64),
+                ("V", vp), ("v_sb", i64), ("v_sn", i64), ("O", vp), ("o_sb", i64), ("o_sn", i64),
+                ("dO", vp), ("do_sb", i64), ("do_sn", i64), ("lse", vp), ("delta", vp),
+                ("dQ", vp), ("dq_sb", i64), ("dq_sn", i64), ("dK", vp), ("dk_sb", i64), ("dk_sn", i64),
+                ("dV", vp), ("dv_sb", i64), ("dv_sn", i64), ("scale", f32), ("pad1", i32)]
 
 
 EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS, EPI_BIAS_GELU_MXFP8, EPI_BIAS_QKNORM_ROPE = range(7)
@@ -126,6 +135,7 @@ _SIGS = {
     "vp_mask_video_bf16": (i32, [vp, i32, vp, i32, vp, i32, i32, i64, vp]),
     "vp_nearest_resize3d_bf16": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
     "vp_denormalize_bf16": (i32, [vp, vp, i64, vp]),
+    "vp_attention_bwd_bf16": (i32, [C.POINTER(AttnBwdDesc), vp]),
 }
 
 EXPORTS = tuple(_SIGS)
@@ -161,10 +171,10 @@ def lib():
         if src is not None and built.split(":")[0] != src:
             raise HipLibraryError(f"{LIB_PATH} was built from other sources (digest {built[:12]}.. != "
                                   f"{src[:12]}..); rebuild with `python -m videopainter_amd.build`")
-        sizes = (i64 * 6)()
+        sizes = (i64 * 7)()
         L.vp_struct_sizes(sizes)
         want = (C.sizeof(GemmDesc), C.sizeof(AttnDesc), C.sizeof(DpmDesc), C.sizeof(GemmMxDesc),
-                C.sizeof(AttnFp8Desc), C.sizeof(Conv3dDesc))
+                C.sizeof(AttnFp8Desc), C.sizeof(Conv3dDesc), C.sizeof(AttnBwdDesc))
         if tuple(sizes) != want:
             raise HipLibraryError(f"descriptor size mismatch lib={tuple(sizes)} python={want}; rebuild")
         _lib = L

@@ -210,10 +210,13 @@ VP_DEV void glds16(const char* sbase, int voff, char* lds) {
 // O = O^T accumulator / l, rounded to bf16 like the reference's SDPA output, then the optional prev-clip blend.
 // split_sum: l_run holds this lane's half of the row sum (the partner lane l ^ 32 has the other half).
 VP_DEV void store_out(const vp_attn_desc& d, const f32x16 (&o)[2], float l_run, int q, int b, int h, int hl,
-                      bool split_sum = true) {
+                      bool split_sum = true, float m_lse = NAN) {
   const float l_tot = split_sum ? l_run + __shfl_xor(l_run, 32, 64) : l_run;
   const float inv = 1.f / l_tot;
   if (q >= d.Nq) return;
+  // softmax statistics for the backward (both lanes of a pair hold the same query, m and l: one writes)
+  if (d.lse != nullptr && hl == 0 && !__builtin_isnan(m_lse))
+    d.lse[((int64_t)b * d.H + h) * d.Nq + q] = m_lse + __log2f(l_tot);
   bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
 #pragma unroll
   for (int dh = 0; dh < 2; ++dh)
@@ -317,6 +320,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d,
     }
   }
   const float inv = 1.f / l;
+  if (d.lse != nullptr) d.lse[((int64_t)b * d.H + h) * d.Nq + q] = mx + __log2f(l);
   bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
 #pragma unroll
   for (int e = 0; e < 64; e += 4) {
@@ -473,7 +477,7 @@ __global__ __launch_bounds__(NW * 64, 4) void attn_fwd(const vp_attn_desc d, con
     const int qi = wave * 32 + (lane & 31);
     store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qi) * 66, o, m_run, l_tot, hl);
   } else {
-    store_out(d, o, l_tot, q, b, h, hl, false);
+    store_out(d, o, l_tot, q, b, h, hl, false, m_run);
   }
 }
 

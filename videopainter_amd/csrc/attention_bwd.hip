@@ -1,0 +1,346 @@
+// Flash-attention backward for CogVideoX joint attention on gfx950 (the training caller's
+// `accelerator.backward(loss)`, train/train_cogvideox_inpainting_i2v_video.py:1892, through
+// F.scaled_dot_product_attention at DF/models/attention_processor.py:2192).  head_dim 64, non-causal, no mask.
+//
+// Given Q, K, V, the forward output O, the output gradient dO and the forward's softmax statistics
+// lse = m + log2(l) (vp_attn_desc.lse, log2 units of c * q.k with c = scale * log2 e):
+//   P = exp2(c q.k - lse),  dP = dO . V^T,  D = rowsum(dO * O),  dS = P * (dP - D)
+//   dQ = scale * dS . K,   dK = scale * dS^T . Q,   dV = P^T . dO
+// Three launches: the D rows; dQ with a workgroup per 128 queries looping over 64-key tiles (S^T = K Q^T with Q^T in
+// registers, exactly the forward's layout, so P^T and dS^T leave the accumulator as the B operand of
+// dQ^T += K^T dS^T, K^T read with ds_read_b64_tr_b16); dK / dV with a workgroup per 128 keys looping over 64-query
+// tiles (S = Q K^T with K^T in registers: P and dS are the B operands of dV^T += dO^T P and dK^T += Q^T dS).  Every
+// product on v_mfma_f32_32x32x16_bf16; tiles stream through a 2-slot LDS ring by LDS-DMA (global_load_lds_dwordx4,
+// bank swizzle on the source address).  Roofline: MFMA (2.5 x the forward's 4 N^2 d FLOP per head: S twice, dP
+// twice, dQ, dK, dV), VALU exp2 per score twice.
+#include "vp_common.h"
+
+namespace {
+
+constexpr int BW = 4;                 // waves per workgroup
+constexpr int BT = 64;                // rows per streamed tile
+constexpr int TILE = BT * 128;        // bytes of one 64 x 64 bf16 tile
+constexpr int STAGE = 2 * TILE + 512; // two tiles + 64 fp32 lse + 64 fp32 D (dK/dV kernel)
+constexpr int LDS_BWD = 2 * STAGE;
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+VP_DEV int swz(int row) { return (row >> 1) & 7; }
+
+VP_DEV void glds16(const char* sbase, int voff, char* lds) {
+  const unsigned la = (unsigned)(uintptr_t)(lds_void_t*)lds;
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(la), "v"(voff), "s"(sbase)
+               : "memory", "m0");
+}
+
+// stage 64 rows of a [N, ld] bf16 head slice (64 columns from `base`) into a swizzled [64][128 B] LDS tile: 2 DMA
+// pieces of 8 rows per wave (rows past `nrows` re-read the last row; the caller masks them)
+VP_DEV void stage_tile(const bf16* base, int64_t ld, int row0, int nrows, char* tile, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pc = wave + i * BW;               // piece: tile rows pc*8 .. pc*8+7
+    const int r = pc * 8 + (lane >> 3);
+    const int rs = min(row0 + r, nrows - 1) - row0;
+    const int ch = (lane & 7) ^ swz(r);
+    glds16((const char*)(base + (int64_t)row0 * ld), (int)((rs * ld + ch * 8) * 2), tile + pc * 1024);
+  }
+}
+
+// A-operand rows (ds_read_b128) of a 32-row half of a swizzled tile: chunk (2c + hl) ^ swz(row) = dims 16c + 8hl
+VP_DEV void read_rows(const char* tile, int half, int lane, bf16x8 (&f)[4]) {
+  const int hl = lane >> 5;
+  const int row = half * 32 + (lane & 31);
+  const char* rp = tile + row * 128;
+  const int sw = swz(row);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) f[c] = *(const bf16x8*)(rp + (((2 * c + hl) ^ sw) << 4));
+}
+
+// A-operand of X^T (rows = the 64 columns in two 32-halves dh, k = 16 tile rows of slab `slab`) by transposing
+// reads of the swizzled tile, in the k order of a 32x32 accumulator used as the B operand (lane group hl supplies
+// rows {4hl..4hl+3, 8+4hl..8+4hl+3} of the slab): the forward's V^T read (attention.hip pv_half)
+struct TrAddr {
+  int lo[2], hi[2];
+};
+VP_DEV TrAddr tr_addr(int lane) {
+  const int g = lane >> 4;
+  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
+  const int tcol = 16 * (g & 1) + 4 * (lane & 3);
+  TrAddr a;
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh) {
+    const int chunk = dh * 4 + (tcol >> 3);
+    a.lo[dh] = trow * 128 + ((chunk ^ swz(trow)) << 4) + (tcol & 7) * 2;
+    a.hi[dh] = (trow + 8) * 128 + ((chunk ^ swz(trow + 8)) << 4) + (tcol & 7) * 2;
+  }
+  return a;
+}
+VP_DEV bf16x8 read_tr(const char* tile, int slab, const TrAddr& a, int dh) {
+  const char* base = tile + slab * 16 * 128;  // swz depends on row bits 1-3: the same for every 16-row slab
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + a.lo[dh]));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + a.hi[dh]));
+  return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+VP_DEV f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// 32x32 accumulator element i of lane group hl sits in row 8 (i / 4) + 4 hl + i % 4
+VP_DEV int acc_row(int i, int hl) { return 8 * (i >> 2) + 4 * hl + (i & 3); }
+
+// store a transposed accumulator pair X^T (rows = 64 columns in halves dh, col = lane % 32 = this lane's row) as
+// bf16 row `row` of a [N, ld] tensor, times `mul`
+VP_DEV void store_rowT(bf16* rowp, const f32x16 (&x)[2], int hl, float mul) {
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(x[dh][4 * j + r] * mul);
+      *(bf16x4*)(rowp + dh * 32 + 8 * j + 4 * hl) = v;
+    }
+}
+
+// ---- D = rowsum(dO * O): one thread per (b, q, h), fp32 ----
+__global__ __launch_bounds__(256) void bwd_delta_kernel(const vp_attn_bwd_desc d) {
+  const int64_t total = (int64_t)d.B * d.Nq * d.H;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int h = (int)(i % d.H);
+    const int64_t bq = i / d.H;
+    const int q = (int)(bq % d.Nq), b = (int)(bq / d.Nq);
+    const bf16* o = (const bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
+    const bf16* g = (const bf16*)d.dO + (int64_t)b * d.do_sb + (int64_t)q * d.do_sn + h * 64;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const bf16x8 a = *(const bf16x8*)(o + c * 8), bb = *(const bf16x8*)(g + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s = __builtin_fmaf(bf2f(a[e]), bf2f(bb[e]), s);
+    }
+    d.delta[((int64_t)b * d.H + h) * d.Nq + q] = s;
+  }
+}
+
+// ---- dQ: a workgroup per (b, h, 128 queries), 64-key tiles ----
+__global__ __launch_bounds__(BW * 64, 2) void bwd_dq_kernel(const vp_attn_bwd_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqb = (d.Nq + BW * 32 - 1) / (BW * 32);
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb, qb = t - bh * nqb;
+  const int b = bh / d.H, h = bh - b * d.H;
+  const int q = qb * BW * 32 + wave * 32 + (lane & 31);
+  const int qc = min(q, d.Nq - 1);
+  const float c = d.scale * 1.4426950408889634f;
+  // B operands: Q^T pre-scaled by c (the forward's rounding) and dO^T, from this lane's query row
+  bf16x8 qf[4], gf[4];
+  {
+    const bf16* qr = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+    const bf16* gr = (const bf16*)d.dO + (int64_t)b * d.do_sb + (int64_t)qc * d.do_sn + h * 64;
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) {
+      qf[ds] = *(const bf16x8*)(qr + ds * 16 + hl * 8);
+      gf[ds] = *(const bf16x8*)(gr + ds * 16 + hl * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qf[ds][e] = f2bf(bf2f(qf[ds][e]) * c);
+    }
+  }
+  const int64_t so = ((int64_t)b * d.H + h) * d.Nq + qc;
+  const float lse = d.lse[so], Dq = d.delta[so];
+  const bf16* kb = (const bf16*)d.K + (int64_t)b * d.k_sb + h * 64;
+  const bf16* vb = (const bf16*)d.V + (int64_t)b * d.v_sb + h * 64;
+  const TrAddr ta = tr_addr(lane);
+  f32x16 dqt[2] = {zero16(), zero16()};
+  const bool active = qb * BW * 32 + wave * 32 < d.Nq;  // wave-uniform
+  const int ntiles = (d.Nk + BT - 1) / BT;
+  auto issue = [&](int ti) {
+    char* st = smem + (ti & 1) * STAGE;
+    stage_tile(kb, d.k_sn, ti * BT, d.Nk, st, wave, lane);
+    stage_tile(vb, d.v_sn, ti * BT, d.Nk, st + TILE, wave, lane);
+  };
+  issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ti = 0; ti < ntiles; ++ti) {
+    if (ti + 1 < ntiles) issue(ti + 1);
+    const char* Kt = smem + (ti & 1) * STAGE;
+    const char* Vt = Kt + TILE;
+    const int lim = d.Nk - ti * BT;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      if (!active) break;
+      bf16x8 a[4];
+      read_rows(Kt, kh, lane, a);
+      f32x16 s = zero16();
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], qf[ds], s, 0, 0, 0);
+      read_rows(Vt, kh, lane, a);
+      f32x16 dp = zero16();
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], gf[ds], dp, 0, 0, 0);
+      bf16x8 pf[2];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kh * 32 + acc_row(i, hl);
+        const float p = key < lim ? __builtin_amdgcn_exp2f(s[i] - lse) : 0.f;
+        pf[i >> 3][i & 7] = f2bf(p * (dp[i] - Dq));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh)
+          dqt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Kt, kh * 2 + j, ta, dh), pf[j], dqt[dh], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (q < d.Nq) store_rowT((bf16*)d.dQ + (int64_t)b * d.dq_sb + (int64_t)q * d.dq_sn + h * 64, dqt, hl, d.scale);
+}
+
+// ---- dK, dV: a workgroup per (b, h, 128 keys), 64-query tiles ----
+__global__ __launch_bounds__(BW * 64, 2) void bwd_dkdv_kernel(const vp_attn_bwd_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nkb = (d.Nk + BW * 32 - 1) / (BW * 32);
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nkb, kb = t - bh * nkb;
+  const int b = bh / d.H, h = bh - b * d.H;
+  const int key = kb * BW * 32 + wave * 32 + (lane & 31);
+  const int kc = min(key, d.Nk - 1);
+  const float c = d.scale * 1.4426950408889634f;
+  // B operands: K^T and V^T from this lane's key row
+  bf16x8 kf[4], vf[4];
+  {
+    const bf16* kr = (const bf16*)d.K + (int64_t)b * d.k_sb + (int64_t)kc * d.k_sn + h * 64;
+    const bf16* vr = (const bf16*)d.V + (int64_t)b * d.v_sb + (int64_t)kc * d.v_sn + h * 64;
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) {
+      kf[ds] = *(const bf16x8*)(kr + ds * 16 + hl * 8);
+      vf[ds] = *(const bf16x8*)(vr + ds * 16 + hl * 8);
+    }
+  }
+  const bf16* qb = (const bf16*)d.Q + (int64_t)b * d.q_sb + h * 64;
+  const bf16* gb = (const bf16*)d.dO + (int64_t)b * d.do_sb + h * 64;
+  const float* lse_row = d.lse + ((int64_t)b * d.H + h) * d.Nq;
+  const float* d_row = d.delta + ((int64_t)b * d.H + h) * d.Nq;
+  const TrAddr ta = tr_addr(lane);
+  f32x16 dkt[2] = {zero16(), zero16()}, dvt[2] = {zero16(), zero16()};
+  const bool active = kb * BW * 32 + wave * 32 < d.Nk;  // wave-uniform
+  const int ntiles = (d.Nq + BT - 1) / BT;
+  // per-query statistics of a tile: thread tid < 64 holds lse, 64 <= tid < 128 D (plain loads, written to LDS after
+  // the tile's compute, before the barrier that publishes the stage)
+  float stat = 0.f;
+  auto load_stat = [&](int ti) {
+    const int qq = ti * BT + (tid & 63);
+    if (tid < 2 * BT) stat = qq < d.Nq ? (tid < BT ? lse_row[qq] : d_row[qq]) : 0.f;
+  };
+  auto put_stat = [&](int ti) {
+    if (tid < 2 * BT) ((float*)(smem + (ti & 1) * STAGE + 2 * TILE))[tid] = stat;
+  };
+  auto issue = [&](int ti) {
+    char* st = smem + (ti & 1) * STAGE;
+    stage_tile(qb, d.q_sn, ti * BT, d.Nq, st, wave, lane);
+    stage_tile(gb, d.do_sn, ti * BT, d.Nq, st + TILE, wave, lane);
+  };
+  issue(0);
+  load_stat(0);
+  put_stat(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ti = 0; ti < ntiles; ++ti) {
+    if (ti + 1 < ntiles) {
+      issue(ti + 1);
+      load_stat(ti + 1);
+    }
+    const char* Qt = smem + (ti & 1) * STAGE;
+    const char* Gt = Qt + TILE;
+    const float* st = (const float*)(Qt + 2 * TILE);
+    const int lim = d.Nq - ti * BT;
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      if (!active) break;
+      bf16x8 a[4];
+      read_rows(Qt, qh, lane, a);
+      f32x16 s = zero16();
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], kf[ds], s, 0, 0, 0);
+      read_rows(Gt, qh, lane, a);
+      f32x16 dp = zero16();
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], vf[ds], dp, 0, 0, 0);
+      bf16x8 pp[2], pd[2];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r0 = qh * 32 + 8 * j + 4 * hl;
+        const f32x4 l4 = *(const f32x4*)(st + r0), d4 = *(const f32x4*)(st + BT + r0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 4 * j + r;
+          // s is q.K in natural units here (Q from memory, K unscaled): c * s - lse in log2 units
+          const float p = r0 + r < lim ? __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], c, -l4[r])) : 0.f;
+          pp[i >> 3][i & 7] = f2bf(p);
+          pd[i >> 3][i & 7] = f2bf(p * (dp[i] - d4[r]));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          dvt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Gt, qh * 2 + j, ta, dh), pp[j], dvt[dh], 0, 0, 0);
+          dkt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Qt, qh * 2 + j, ta, dh), pd[j], dkt[dh], 0, 0, 0);
+        }
+    }
+    if (ti + 1 < ntiles) put_stat(ti + 1);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (key < d.Nk) {
+    store_rowT((bf16*)d.dK + (int64_t)b * d.dk_sb + (int64_t)key * d.dk_sn + h * 64, dkt, hl, d.scale);
+    store_rowT((bf16*)d.dV + (int64_t)b * d.dv_sb + (int64_t)key * d.dv_sn + h * 64, dvt, hl, 1.f);
+  }
+}
+
+}  // namespace
+
+extern "C" int vp_attention_bwd_bf16(const vp_attn_bwd_desc* d, void* stream) {
+  if (d == nullptr || !d->Q || !d->K || !d->V || !d->O || !d->dO || !d->lse || !d->delta || !d->dQ || !d->dK ||
+      !d->dV)
+    return VP_ERR_ARG;
+  if (d->head_dim != 64) return VP_ERR_UNSUPPORTED;
+  if (d->B <= 0 || d->H <= 0 || d->Nq <= 0 || d->Nk <= 0) return VP_ERR_ARG;
+  const int64_t strides[] = {d->q_sn, d->k_sn, d->v_sn, d->o_sn, d->do_sn, d->dq_sn, d->dk_sn, d->dv_sn,
+                             d->q_sb, d->k_sb, d->v_sb, d->o_sb, d->do_sb, d->dq_sb, d->dk_sb, d->dv_sb};
+  for (int64_t s : strides)
+    if (s % 8) return VP_ERR_ARG;
+  // the LDS-DMA source offsets are 32-bit: a tile's rows lie within 2^31 bytes of its first row
+  if ((int64_t)BT * d->q_sn * 2 >= ((int64_t)1 << 31) || (int64_t)BT * d->k_sn * 2 >= ((int64_t)1 << 31) ||
+      (int64_t)BT * d->v_sn * 2 >= ((int64_t)1 << 31) || (int64_t)BT * d->do_sn * 2 >= ((int64_t)1 << 31))
+    return VP_ERR_ARG;
+  static bool attr = false;
+  if (!attr) {
+    attr = true;
+    (void)hipFuncSetAttribute((const void*)bwd_dq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BWD);
+    (void)hipFuncSetAttribute((const void*)bwd_dkdv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BWD);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nd = (int64_t)d->B * d->Nq * d->H;
+  const int64_t gd = (nd + 255) / 256;
+  hipLaunchKernelGGL(bwd_delta_kernel, dim3((unsigned)(gd < (1 << 20) ? gd : (1 << 20))), dim3(256), 0, s, *d);
+  VP_CHECK_LAUNCH();
+  const int64_t gq = (int64_t)d->B * d->H * ((d->Nq + BW * 32 - 1) / (BW * 32));
+  const int64_t gk = (int64_t)d->B * d->H * ((d->Nk + BW * 32 - 1) / (BW * 32));
+  if (gq > 0x7fffffff || gk > 0x7fffffff) return VP_ERR_ARG;
+  hipLaunchKernelGGL(bwd_dq_kernel, dim3((unsigned)gq), dim3(BW * 64), LDS_BWD, s, *d);
+  VP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bwd_dkdv_kernel, dim3((unsigned)gk), dim3(BW * 64), LDS_BWD, s, *d);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}

@@ -208,6 +208,7 @@ extern "C" void vp_struct_sizes(int64_t* out) {
   out[3] = (int64_t)sizeof(vp_gemm_mx_desc);
   out[4] = (int64_t)sizeof(vp_attn_fp8_desc);
   out[5] = (int64_t)sizeof(vp_conv3d_desc);
+  out[6] = (int64_t)sizeof(vp_attn_bwd_desc);
 }
 
 extern "C" int vp_linear_small_bf16(const void* x, int64_t ldx, const void* W, const void* bias, void* y,

@@ -293,9 +293,11 @@ def mx_mfma_probe(A: torch.Tensor, B: torch.Tensor, sa: torch.Tensor, sb: torch.
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, heads: int, *,
               k2: Optional[torch.Tensor] = None, v2: Optional[torch.Tensor] = None, scale: float = 0.125,
-              out_scale: float = 1.0, accumulate: bool = False, bounded_scores: bool = False) -> torch.Tensor:
+              out_scale: float = 1.0, accumulate: bool = False, bounded_scores: bool = False,
+              lse: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q, k, v, out: [B, N, heads*64] views (last dim contiguous, any row/batch stride); k2 / v2: an optional second
-    K/V segment of the same form.  The native side sees only pointers and strides, so every extent is checked here."""
+    K/V segment of the same form.  The native side sees only pointers and strides, so every extent is checked here.
+    lse: optional fp32 [B, heads, Nq] receiving the softmax statistics the backward needs."""
     segs = [(q, "q"), (k, "k"), (v, "v"), (out, "out")]
     if (k2 is None) != (v2 is None):
         raise ValueError("k2 and v2 must be given together")
@@ -325,6 +327,11 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
         d.Nk2 = k2.shape[1]
     d.O, d.o_sb, d.o_sn = _p(out), out.stride(0), out.stride(1)
     d.scale, d.out_scale, d.accumulate = scale, out_scale, int(accumulate)
+    if lse is not None:
+        _chk(lse, "lse", torch.float32)
+        if lse.shape != (q.shape[0], heads, q.shape[1]) or not lse.is_contiguous():
+            raise ValueError("lse must be contiguous fp32 [B, heads, Nq]")
+        d.lse = _p(lse)
     # bounded_scores: the caller guarantees |scale * q.k| * log2 e <= SCORE_BOUND_LOG2 (score_bound_log2)
     d.flags = ATTN_BOUNDED_SCORES if bounded_scores else 0
     L = N.lib()
@@ -338,6 +345,43 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
     N.check(L.vp_attention_fwd_bf16_ws(C.byref(d), _p(ws), nb, _stream()), "vp_attention_fwd_bf16_ws")
     _t1("attention", ev)
     return out
+
+
+def attention_bwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor, do: torch.Tensor,
+                  lse: torch.Tensor, heads: int, scale: float = 0.125, dq: Optional[torch.Tensor] = None,
+                  dk: Optional[torch.Tensor] = None, dv: Optional[torch.Tensor] = None):
+    """Flash-attention backward (vp_attention_bwd_bf16) of `attention(q, k, v, o, heads, lse=lse)`: returns
+    (dq, dk, dv), each [B, N, heads*64] bf16 (new contiguous tensors unless given)."""
+    for t, n in ((q, "q"), (k, "k"), (v, "v"), (o, "o"), (do, "do")):
+        _chk(t, n)
+        if t.dim() != 3 or t.stride(-1) != 1 or t.shape[-1] != heads * 64 or t.shape[0] != q.shape[0]:
+            raise ValueError(f"{n} must be [B, N, heads*64] with a contiguous last dim")
+    if o.shape[1] != q.shape[1] or do.shape[1] != q.shape[1] or k.shape[1] != v.shape[1]:
+        raise ValueError("attention_bwd: length mismatch")
+    _chk(lse, "lse", torch.float32)
+    B, Nq, Nk = q.shape[0], q.shape[1], k.shape[1]
+    if lse.shape != (B, heads, Nq) or not lse.is_contiguous():
+        raise ValueError("lse must be contiguous fp32 [B, heads, Nq]")
+    dq = torch.empty(B, Nq, heads * 64, device=q.device, dtype=BF16) if dq is None else dq
+    dk = torch.empty(B, Nk, heads * 64, device=q.device, dtype=BF16) if dk is None else dk
+    dv = torch.empty(B, Nk, heads * 64, device=q.device, dtype=BF16) if dv is None else dv
+    for t, n, L in ((dq, "dq", Nq), (dk, "dk", Nk), (dv, "dv", Nk)):
+        _chk(t, n)
+        if t.shape != (B, L, heads * 64) or t.stride(-1) != 1:
+            raise ValueError(f"{n} must be [B, {L}, heads*64]")
+    delta = torch.empty(B, heads, Nq, device=q.device, dtype=torch.float32)
+    d = N.AttnBwdDesc()
+    d.B, d.H, d.Nq, d.Nk, d.head_dim = B, heads, Nq, Nk, 64
+    for name, t in (("q", q), ("k", k), ("v", v), ("o", o), ("do", do), ("dq", dq), ("dk", dk), ("dv", dv)):
+        setattr(d, {"q": "Q", "k": "K", "v": "V", "o": "O", "do": "dO", "dq": "dQ", "dk": "dK", "dv": "dV"}[name],
+                _p(t))
+        setattr(d, f"{name}_sb", t.stride(0))
+        setattr(d, f"{name}_sn", t.stride(1))
+    d.lse, d.delta, d.scale = _p(lse), _p(delta), scale
+    ev = _t0("attention_bwd")
+    N.check(N.lib().vp_attention_bwd_bf16(C.byref(d), _stream()), "vp_attention_bwd_bf16")
+    _t1("attention_bwd", ev)
+    return dq, dk, dv
 
 
 # ---- fp8 attention (BASELINE config 5; formats in include/vp_hip.h) ----
