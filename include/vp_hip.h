@@ -457,6 +457,44 @@ typedef struct vp_attn_bwd_desc {
 int vp_attention_bwd_bf16(const vp_attn_bwd_desc* d, void* stream);
 
 
+/* The other backward passes (row / elementwise / column reductions; the backward's matrix products run on
+ * vp_gemm_bf16 against transposed operands).  y[c][r] = x[r][c] for nbatch R x C bf16 matrices: */
+int vp_transpose_bf16(const void* x, int64_t ldx, int64_t x_bs, void* y, int64_t ldy, int64_t y_bs, int32_t R,
+                      int32_t Cc, int32_t nbatch, void* stream);
+/* out[(batch * 2 + type) * cols + n] += sum over rows m of that (batch = m / Ntok, type = text (1) if m % Ntok <
+ * text_len) of a[m, n] (* b[m, n] when b != NULL): bias / gate / shift / scale / LayerNorm-affine gradients (fp32
+ * atomics; cols % 8 == 0) */
+int vp_colsum_bf16(const void* a, int64_t lda, const void* b, int64_t ldb, int32_t rows, int32_t cols, int32_t Ntok,
+                   int32_t text_len, float* out, void* stream);
+/* CogVideoXLayerNormZero backward (normalization.py:373-379): with n = bf16(LN(x) w + b) and the forward's
+ * y = bf16(bf16(n (1 + scale)) + shift) (scale / shift = chunks scale_v / shift_v of mod for video rows, _t for
+ * text rows), dx += LN'(dy (1 + scale) w) (bf16 in place); optionally writes n, dn = dy (1 + scale) and LN(x) (bf16
+ * [rows, D]) for the parameter column sums. */
+int vp_adaln_bwd_bf16(const void* x, const void* dy, void* dx, int32_t B, int32_t Ntok, int32_t D, int32_t text_len,
+                      const void* ln_w, const void* ln_b, float eps, const void* mod, int64_t mod_bstride,
+                      int32_t shift_v, int32_t scale_v, int32_t shift_t, int32_t scale_t, void* n_out, void* dn_out,
+                      void* xhat_out, void* stream);
+/* y = bf16(x * gate) with gate = chunk chunk_v (video rows) / chunk_t (text rows) of mod [B, *] (the gated
+ * residual's gradient into its branch, cogvideox_transformer_3d.py:161-162, 179-180) */
+int vp_rowscale_bf16(const void* x, int64_t ldx, void* y, int64_t ldy, int32_t rows, int32_t Ntok, int32_t D,
+                     int32_t text_len, const void* mod, int64_t mod_bstride, int32_t chunk_v, int32_t chunk_t,
+                     void* stream);
+/* GELU(tanh) forward h = gelu(z) and backward dz = dh * gelu'(z) (activations.py:65-90), elementwise bf16 */
+int vp_gelu_bf16(const void* z, void* h, int64_t n, void* stream);
+int vp_gelu_bwd_bf16(const void* dh, const void* z, void* dz, int64_t n, void* stream);
+/* y = bf16(a + alpha b) (gradient accumulation), n % 8 == 0 */
+int vp_axpy_bf16(const void* a, const void* b, float alpha, void* y, int64_t n, void* stream);
+/* y = dy * silu'(x) (the AdaLN / time-embedding SiLU) */
+int vp_silu_bwd_bf16(const void* dy, const void* x, void* y, int64_t n, void* stream);
+/* backward of vp_head_norm_rope_bf16 (LayerNorm(64) + RoPE on rows >= text_len; no token mask): x_in = the
+ * pre-norm q or k, dy = the gradient of the normed + rotated output, dx = the gradient of x_in; dln_w / dln_b: fp32
+ * [64] accumulated (atomics) or both NULL */
+int vp_head_norm_rope_bwd_bf16(const void* x_in, int64_t ld_in, int64_t bs_in, const void* dy, int64_t ld_dy,
+                               int64_t bs_dy, void* dx, int64_t ld_dx, int64_t bs_dx, int32_t B, int32_t Ntok,
+                               int32_t H, int32_t text_len, const void* ln_w, const void* ln_b, float eps,
+                               const float* cos, const float* sin, float* dln_w, float* dln_b, void* stream);
+
+
 #ifdef __cplusplus
 }
 #endif

@@ -136,6 +136,17 @@ _SIGS = {
     "vp_nearest_resize3d_bf16": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
     "vp_denormalize_bf16": (i32, [vp, vp, i64, vp]),
     "vp_attention_bwd_bf16": (i32, [C.POINTER(AttnBwdDesc), vp]),
+    "vp_transpose_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, vp]),
+    "vp_colsum_bf16": (i32, [vp, i64, vp, i64, i32, i32, i32, i32, vp, vp]),
+    "vp_adaln_bwd_bf16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, f32, vp, i64, i32, i32, i32, i32, vp, vp, vp,
+                                vp]),
+    "vp_rowscale_bf16": (i32, [vp, i64, vp, i64, i32, i32, i32, i32, vp, i64, i32, i32, vp]),
+    "vp_gelu_bf16": (i32, [vp, vp, i64, vp]),
+    "vp_gelu_bwd_bf16": (i32, [vp, vp, vp, i64, vp]),
+    "vp_axpy_bf16": (i32, [vp, vp, f32, vp, i64, vp]),
+    "vp_silu_bwd_bf16": (i32, [vp, vp, vp, i64, vp]),
+    "vp_head_norm_rope_bwd_bf16": (i32, [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp,
+                                         vp, vp, vp, vp]),
 }
 
 EXPORTS = tuple(_SIGS)
