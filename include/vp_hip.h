@@ -484,7 +484,8 @@ int vp_gelu_bf16(const void* z, void* h, int64_t n, void* stream);
 int vp_gelu_bwd_bf16(const void* dh, const void* z, void* dz, int64_t n, void* stream);
 /* y = bf16(a + alpha b) (gradient accumulation), n % 8 == 0 */
 int vp_axpy_bf16(const void* a, const void* b, float alpha, void* y, int64_t n, void* stream);
-/* y = dy * silu'(x) (the AdaLN / time-embedding SiLU) */
+/* y = silu(x) and y = dy * silu'(x) (the AdaLN / time-embedding SiLU) */
+int vp_silu_bf16(const void* x, void* y, int64_t n, void* stream);
 int vp_silu_bwd_bf16(const void* dy, const void* x, void* y, int64_t n, void* stream);
 /* backward of vp_head_norm_rope_bf16 (LayerNorm(64) + RoPE on rows >= text_len; no token mask): x_in = the
  * pre-norm q or k, dy = the gradient of the normed + rotated output, dx = the gradient of x_in; dln_w / dln_b: fp32

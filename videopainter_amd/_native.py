@@ -144,6 +144,7 @@ _SIGS = {
     "vp_gelu_bf16": (i32, [vp, vp, i64, vp]),
     "vp_gelu_bwd_bf16": (i32, [vp, vp, vp, i64, vp]),
     "vp_axpy_bf16": (i32, [vp, vp, f32, vp, i64, vp]),
+    "vp_silu_bf16": (i32, [vp, vp, i64, vp]),
     "vp_silu_bwd_bf16": (i32, [vp, vp, vp, i64, vp]),
     "vp_head_norm_rope_bwd_bf16": (i32, [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp,
                                          vp, vp, vp, vp]),

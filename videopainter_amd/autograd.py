@@ -1,0 +1,472 @@
+"""Training backward of the CogVideoX transformer + VideoPainter branch on the HIP kernels.
+
+The caller is the reference's training step (train/train_cogvideox_inpainting_i2v_video.py:1857-1892): the branch
+(trainable) runs on the noisy latents + masked-video condition, its per-block samples are injected into the frozen
+42-layer transformer, the v-prediction loss is backpropagated (`accelerator.backward(loss)`) through the frozen
+transformer into the branch's parameters.  Each piece is a `torch.autograd.Function` whose forward is the inference
+path itself (same launches, same rounding points) and whose backward runs only native kernels:
+
+  * `_BlockFn` — one CogVideoXBlock (cogvideox_transformer_3d.py:125-184), gradient-checkpointed: only the block
+    input is saved; the backward recomputes mod1/mod2, the AdaLN outputs, the pre-norm q/k/v, the normed q/k, the
+    attention output + softmax statistics, the gated residual and the FF1 pre-activation, then runs
+      FF2 dgrad -> GELU' -> FF1 dgrad -> AdaLN2' (+ residual) -> gate1 row-scale -> to_out dgrad
+      -> flash-attention backward -> (LayerNorm(64) + RoPE)' for q, k -> fused QKV dgrad -> AdaLN1' (+ residual)
+    with the dgrad GEMMs against cached transposed weights.  Trainable blocks add the weight gradients (one GEMM over
+    the token dimension per weight, `kernels.wgrad`), bias / LayerNorm-affine / modulation sums (`kernels.colsum`)
+    and the modulation linear's backward into the time embedding.
+  * `_HeadFn` — norm_final + norm_out (AdaLN, shift|scale) + proj_out + unpatchify (:613-637), input gradient only
+    (the transformer is frozen in the reference's training; trainable head parameters raise).
+  * `_PatchEmbedFn` (embeddings.py:400-454), `_TimeEmbedFn` (embeddings.py:729-774), `_RowLinearFn` (the branch's
+    zero-initialised output linears, branch_cogvideox.py:418-426): parameter gradients (inputs are data).
+
+Grad tensors are bf16 like the parameters (fp32 accumulation inside every kernel; the per-column sums are fp32 until
+the final cast).  Out of scope for the backward (NotImplementedError): the fp8 modes, the resample processor, the
+previous-clip blend and `return_hidden_states` — inference-only features of the reference.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from . import _native as NAT
+from . import kernels as K
+from .attention_processor import bounded_scores
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# transposed weights for the dgrad GEMMs (cached on the parameter, keyed on storage + version)
+# ------------------------------------------------------------------------------------------------------------------
+
+def _wt(w: torch.Tensor) -> torch.Tensor:
+    key = (w.data_ptr(), w._version, tuple(w.shape))
+    c = getattr(w, "_vp_wt", None)
+    if c is None or c[0] != key:
+        c = (key, K.transpose(w.detach()))
+        w._vp_wt = c
+    return c[1]
+
+
+def _qkv_t(attn) -> torch.Tensor:
+    """[D, 3D] = cat(W_q, W_k, W_v)^T: the fused QKV dgrad's weight."""
+    ws = (attn.to_q.weight, attn.to_k.weight, attn.to_v.weight)
+    key = tuple((w.data_ptr(), w._version) for w in ws)
+    c = getattr(attn, "_vp_qkv_t", None)
+    if c is None or c[0] != key:
+        D = ws[0].shape[1]
+        n = ws[0].shape[0]
+        wt = torch.empty(D, 3 * n, device=ws[0].device, dtype=BF16)
+        for s, w in enumerate(ws):
+            K.transpose(w.detach(), out=wt[:, s * n:(s + 1) * n])
+        c = (key, wt)
+        attn._vp_qkv_t = c
+    return c[1]
+
+
+def _dgrad(dy2: torch.Tensor, w: torch.Tensor, out2: torch.Tensor) -> torch.Tensor:
+    """out = dy W for y = x W^T: the GEMM C = A B^T with B = W^T."""
+    return K.gemm(dy2, [_wt(w)], [None], out2)
+
+
+def _total(a: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 column sum over every row of a 2-D view (of a * b)."""
+    return K.colsum(a, b)[0, 0]
+
+
+class _Grads:
+    """Collects parameter gradients (bf16, the parameter's shape) for parameters that require them."""
+
+    def __init__(self):
+        self.g: Dict[int, torch.Tensor] = {}
+
+    def put(self, p: Optional[torch.Tensor], g: torch.Tensor) -> None:
+        if p is None or not p.requires_grad:
+            return
+        g = g.reshape(p.shape).to(p.dtype)
+        if id(p) in self.g:
+            self.g[id(p)] = self.g[id(p)] + g
+        else:
+            self.g[id(p)] = g
+
+    def out(self, params: Sequence[torch.Tensor]) -> List[Optional[torch.Tensor]]:
+        return [self.g.get(id(p)) for p in params]
+
+
+def _mod_grad(shift: torch.Tensor, scale: torch.Tensor, gate: torch.Tensor) -> torch.Tensor:
+    """[B, 6D] bf16 gradient of the CogVideoXLayerNormZero modulation (shift|scale|gate|enc_shift|enc_scale|enc_gate)
+    from the per-(batch, video/text) column sums [B, 2, D]."""
+    B, _, D = shift.shape
+    return torch.stack((shift[:, 0], scale[:, 0], gate[:, 0], shift[:, 1], scale[:, 1], gate[:, 1]), 1) \
+        .reshape(B, 6 * D).to(BF16)
+
+
+def _small_linear_bwd(G: _Grads, lin, x_in: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+    """Backward of y = x_in W^T + b on a few rows (the modulation / time-embedding linears): parameter grads into G,
+    returns d x_in (bf16 [rows, in])."""
+    G.put(lin.weight, K.wgrad(dy, x_in))
+    if lin.bias is not None:
+        G.put(lin.bias, _total(dy))
+    return K.linear_small(dy, _wt(lin.weight), None)
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# the block
+# ------------------------------------------------------------------------------------------------------------------
+
+def _check_block_trainable_path(block) -> None:
+    a = block.attn1
+    if block.ff_mx is not None or block.qkv_mx is not None or getattr(a, "fp8_qk_exp", None) is not None:
+        raise NotImplementedError("the backward runs the bf16 path: disable the fp8 modes for training")
+    from .attention_processor import CogVideoXAttnProcessor2_0_resample
+    if isinstance(a.processor, CogVideoXAttnProcessor2_0_resample):
+        raise NotImplementedError("the resample processor (VideoPainterID inference) has no backward")
+
+
+def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inject_mask: Optional[torch.Tensor],
+                   dout: torch.Tensor, want_dtemb: bool, want_dinject: bool, train: bool):
+    """Gradient-checkpointed backward of `block.forward_joint(x, T, temb, rope, inject=.., inject_mask=..)`.
+    Returns (dx [B, Ntok, D], dtemb or None, dinject [B, Nv, D] or None, _Grads)."""
+    B, Ntok, D = x.shape
+    M = B * Ntok
+    a = block.attn1
+    H = a.heads
+    n1, n2 = block.norm1, block.norm2
+    ff0, ff2, to_out = block.ff.net[0].proj, block.ff.net[2], a.to_out[0]
+    F4 = ff0.weight.shape[0]
+    dev = x.device
+    need_dmod = train or want_dtemb
+    G = _Grads()
+
+    # ---- recompute (forward_joint's launches and rounding points; the fused QKV + qk-norm epilogue is bit-exact
+    # to the separate launches used here, tests/test_model_gpu.py) ----
+    mod1 = n1.modulation(temb)
+    mod2 = n2.modulation(temb)
+    xn = K.adaln_modulate(x, n1.norm.weight, n1.norm.bias, mod1, T, n1.norm.eps)
+    qkv = torch.empty(B, Ntok, 3 * D, device=dev, dtype=BF16)
+    K.gemm(xn.view(M, D), [a.to_q.weight, a.to_k.weight, a.to_v.weight], [a.to_q.bias, a.to_k.bias, a.to_v.bias],
+           qkv.view(M, 3 * D))
+    qk = torch.empty(B, Ntok, 2 * D, device=dev, dtype=BF16)
+    qn, kn, v = qk[..., :D], qk[..., D:], qkv[..., 2 * D:]
+    K.head_norm_rope(qkv[..., :D], qn, H, T, a.norm_q.weight, a.norm_q.bias, a.norm_q.eps, rope)
+    K.head_norm_rope(qkv[..., D:2 * D], kn, H, T, a.norm_k.weight, a.norm_k.bias, a.norm_k.eps, rope)
+    o = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
+    lse = torch.empty(B, H, Ntok, device=dev, dtype=F32)
+    K.attention(qn, kn, v, o, H, scale=a.scale, bounded_scores=bounded_scores(a), lse=lse)
+    x_mid = torch.empty_like(x)
+    K.gemm(o.view(M, D), [to_out.weight], [to_out.bias], x_mid.view(M, D), epilogue=NAT.EPI_GATED,
+           resid=x.view(M, D), mod=mod1, gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok, text_len=T)
+    xn2 = K.adaln_modulate(x_mid, n2.norm.weight, n2.norm.bias, mod2, T, n2.norm.eps)
+    z = torch.empty(M, F4, device=dev, dtype=BF16)
+    K.gemm(xn2.view(M, D), [ff0.weight], [ff0.bias], z)
+
+    dout = dout.contiguous()
+    dout2 = dout.view(M, D)
+    dinj = None
+    if want_dinject:
+        if inject_mask is None:
+            dinj = dout[:, T:].clone()
+        else:
+            dinj = torch.empty(B, Ntok - T, D, device=dev, dtype=BF16)
+            K.mask_scale_rows(dout[:, T:], dinj, (inject_mask == 0).to(torch.uint8), 1.0)
+
+    # ---- FeedForward + gated residual 2 ----
+    g = dout.clone()  # d x_mid, then d x
+    df = torch.empty(M, D, device=dev, dtype=BF16)
+    K.rowscale(dout2, df, Ntok, T, mod2, 2, 5)
+    dz = torch.empty(M, F4, device=dev, dtype=BF16)
+    _dgrad(df, ff2.weight, dz)
+    K.gelu_bwd(dz, z, out=dz)
+    dxn2 = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
+    _dgrad(dz, ff0.weight, dxn2.view(M, D))
+    n2o = dn2 = xh2 = None
+    if need_dmod:
+        n2o, dn2, xh2 = (torch.empty_like(x) for _ in range(3))
+    K.adaln_bwd(x_mid, dxn2, g, T, n2.norm.weight, n2.norm.bias, n2.norm.eps, mod2, n_out=n2o, dn_out=dn2,
+                xhat_out=xh2)
+    if need_dmod:
+        h = K.gelu(z)
+        f = torch.empty(M, D, device=dev, dtype=BF16)
+        K.gemm(h, [ff2.weight], [ff2.bias], f)
+        dmod2 = _mod_grad(K.colsum(dxn2.view(M, D), tokens_per_batch=Ntok, text_len=T),
+                          K.colsum(dxn2.view(M, D), n2o.view(M, D), tokens_per_batch=Ntok, text_len=T),
+                          K.colsum(dout2, f, tokens_per_batch=Ntok, text_len=T))
+        del f
+        if train:
+            G.put(ff2.weight, K.wgrad(df, h))
+            G.put(ff2.bias, _total(df))
+            G.put(ff0.weight, K.wgrad(dz, xn2.view(M, D)))
+            G.put(ff0.bias, _total(dz))
+            G.put(n2.norm.weight, _total(dn2.view(M, D), xh2.view(M, D)))
+            G.put(n2.norm.bias, _total(dn2.view(M, D)))
+        del h
+    del z, dz, df, xn2, n2o, dn2, xh2, dxn2
+
+    # ---- attention + gated residual 1 ----
+    dao = torch.empty(M, D, device=dev, dtype=BF16)
+    K.rowscale(g.view(M, D), dao, Ntok, T, mod1, 2, 5)
+    if need_dmod:
+        ao = torch.empty(M, D, device=dev, dtype=BF16)
+        K.gemm(o.view(M, D), [to_out.weight], [to_out.bias], ao)
+        gate1 = K.colsum(g.view(M, D), ao, tokens_per_batch=Ntok, text_len=T)
+        del ao
+        if train:
+            G.put(to_out.weight, K.wgrad(dao, o.view(M, D)))
+            G.put(to_out.bias, _total(dao))
+    do = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
+    _dgrad(dao, to_out.weight, do.view(M, D))
+    del dao
+    dqkv = torch.empty(B, Ntok, 3 * D, device=dev, dtype=BF16)
+    K.attention_bwd(qn, kn, v, o, do, lse, H, scale=a.scale, dq=dqkv[..., :D], dk=dqkv[..., D:2 * D],
+                    dv=dqkv[..., 2 * D:])
+    del do, o, lse, qk
+    dlnq = dlnk = None
+    if train and (a.norm_q.weight.requires_grad or a.norm_k.weight.requires_grad):
+        dlnq = (torch.zeros(64, device=dev, dtype=F32), torch.zeros(64, device=dev, dtype=F32))
+        dlnk = (torch.zeros(64, device=dev, dtype=F32), torch.zeros(64, device=dev, dtype=F32))
+    K.head_norm_rope_bwd(qkv[..., :D], dqkv[..., :D], dqkv[..., :D], H, T, a.norm_q, rope, dlnq)
+    K.head_norm_rope_bwd(qkv[..., D:2 * D], dqkv[..., D:2 * D], dqkv[..., D:2 * D], H, T, a.norm_k, rope, dlnk)
+    del qkv
+    if dlnq is not None:
+        G.put(a.norm_q.weight, dlnq[0])
+        G.put(a.norm_q.bias, dlnq[1])
+        G.put(a.norm_k.weight, dlnk[0])
+        G.put(a.norm_k.bias, dlnk[1])
+    dxn = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
+    K.gemm(dqkv.view(M, 3 * D), [_qkv_t(a)], [None], dxn.view(M, D))
+    if train:
+        dw = K.wgrad(dqkv.view(M, 3 * D), xn.view(M, D))
+        db = _total(dqkv.view(M, 3 * D))
+        for s, lin in enumerate((a.to_q, a.to_k, a.to_v)):
+            G.put(lin.weight, dw[s * D:(s + 1) * D])
+            G.put(lin.bias, db[s * D:(s + 1) * D])
+        del dw
+    del dqkv, xn
+    n1o = dn1 = xh1 = None
+    if need_dmod:
+        n1o, dn1, xh1 = (torch.empty_like(x) for _ in range(3))
+    K.adaln_bwd(x, dxn, g, T, n1.norm.weight, n1.norm.bias, n1.norm.eps, mod1, n_out=n1o, dn_out=dn1, xhat_out=xh1)
+
+    dtemb = None
+    if need_dmod:
+        dmod1 = _mod_grad(K.colsum(dxn.view(M, D), tokens_per_batch=Ntok, text_len=T),
+                          K.colsum(dxn.view(M, D), n1o.view(M, D), tokens_per_batch=Ntok, text_len=T), gate1)
+        if train:
+            G.put(n1.norm.weight, _total(dn1.view(M, D), xh1.view(M, D)))
+            G.put(n1.norm.bias, _total(dn1.view(M, D)))
+        s = K.silu(temb.contiguous())
+        ds = K.axpy(_small_linear_bwd(G, n1.linear, s, dmod1), _small_linear_bwd(G, n2.linear, s, dmod2))
+        if want_dtemb:
+            dtemb = K.silu_bwd(ds, temb.contiguous())
+    return g, dtemb, dinj, G
+
+
+class _BlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, block, T, rope, inject_mask, x, temb, inject, *params):
+        out = block.forward_joint(x, T, temb, rope, inject=inject,
+                                  inject_mask=inject_mask if inject is not None else None)
+        ctx.block, ctx.T, ctx.rope, ctx.inject_mask = block, T, rope, inject_mask
+        ctx.has_inject = inject is not None
+        ctx.params = params
+        ctx.save_for_backward(x, temb)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, temb = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        train = any(need[7:])
+        dx, dtemb, dinj, G = block_backward(ctx.block, x, ctx.T, temb, ctx.rope,
+                                            ctx.inject_mask if ctx.has_inject else None, dout, need[5],
+                                            need[6] and ctx.has_inject, train)
+        return (None, None, None, None, dx if need[4] else None, dtemb, dinj, *G.out(ctx.params))
+
+
+def block_apply(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inject: Optional[torch.Tensor] = None,
+                inject_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Differentiable `block.forward_joint` (gradient-checkpointed)."""
+    _check_block_trainable_path(block)
+    params = [p for p in block.parameters()]
+    return _BlockFn.apply(block, T, rope, inject_mask, x, temb, inject, *params)
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# head, embeddings, branch output linears
+# ------------------------------------------------------------------------------------------------------------------
+
+class _HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, dims, x, emb):
+        B, F, H, W, T = dims
+        cfg = model.config
+        p = cfg.patch_size
+        D = x.shape[-1]
+        Nv = x.shape[1] - T
+        mod = K.linear_small(emb, model.norm_out.linear.weight, model.norm_out.linear.bias, act_in=K.ACT_SILU)
+        y = K.final_norm(x, T, model.norm_final.weight, model.norm_final.bias, model.norm_out.norm.weight,
+                         model.norm_out.norm.bias, model.norm_out.norm.eps, mod)
+        proj = K.linear(y.view(B * Nv, D), model.proj_out.weight, model.proj_out.bias)
+        ctx.model, ctx.dims = model, dims
+        ctx.save_for_backward(x, emb)
+        return K.unpatchify(proj, B, F, cfg.out_channels, H, W, p)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, emb = ctx.saved_tensors
+        m = ctx.model
+        B, F, H, W, T = ctx.dims
+        cfg = m.config
+        p = cfg.patch_size
+        _, Ntok, D = x.shape
+        Nv = Ntok - T
+        if ctx.needs_input_grad[3]:
+            raise NotImplementedError("the head's time-embedding gradient (a trainable transformer time embedding) "
+                                      "is not implemented: the reference trains the branch only")
+        mod = K.linear_small(emb, m.norm_out.linear.weight, m.norm_out.linear.bias, act_in=K.ACT_SILU)
+        dproj = K.patchify(dout.to(BF16).contiguous(), None, p, p * p * cfg.out_channels)
+        dy = torch.empty(B * Nv, D, device=x.device, dtype=BF16)
+        _dgrad(dproj, m.proj_out.weight, dy)
+        zero_mod = torch.zeros(B, 6 * D, device=x.device, dtype=BF16)
+        n1 = K.adaln_modulate(x, m.norm_final.weight, m.norm_final.bias, zero_mod, T, m.norm_final.eps)
+        dx = torch.zeros_like(x)
+        dn1 = torch.empty(1, Nv, D, device=x.device, dtype=BF16)
+        for b in range(B):
+            dn1.zero_()
+            K.adaln_bwd(n1[b:b + 1, T:], dy[b * Nv:(b + 1) * Nv].view(1, Nv, D), dn1, 0, m.norm_out.norm.weight,
+                        m.norm_out.norm.bias, m.norm_out.norm.eps, mod[b:b + 1], chunks=(0, 1, 0, 1))
+            K.adaln_bwd(x[b:b + 1, T:], dn1, dx[b:b + 1, T:], 0, m.norm_final.weight, m.norm_final.bias,
+                        m.norm_final.eps, zero_mod[b:b + 1], chunks=(0, 1, 0, 1))
+        return None, None, dx, None
+
+
+def head_apply(model, x: torch.Tensor, emb: torch.Tensor, dims) -> torch.Tensor:
+    head = [model.norm_final.weight, model.norm_final.bias, model.norm_out.linear.weight, model.norm_out.linear.bias,
+            model.norm_out.norm.weight, model.norm_out.norm.bias, model.proj_out.weight, model.proj_out.bias]
+    if any(t is not None and t.requires_grad for t in head):
+        raise NotImplementedError("trainable transformer head parameters: the reference trains the branch only")
+    return _HeadFn.apply(model, dims, x, emb)
+
+
+class _PatchEmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pe, text, video, video2, *params):
+        ctx.pe = pe
+        ctx.params = params
+        ctx.save_for_backward(text, video, video2)
+        return pe.embed(text, video, video2)
+
+    @staticmethod
+    def backward(ctx, dx):
+        text, video, video2 = ctx.saved_tensors
+        pe = ctx.pe
+        G = _Grads()
+        dx = dx.contiguous()
+        B, Ntok, D = dx.shape
+        T = text.shape[1]
+        G.put(pe.text_proj.weight, K.wgrad(dx[:, :T], text))
+        wp, kpad = pe._padded_conv_weight()
+        cols = K.patchify(video, video2, pe.patch_size, kpad)
+        w = pe.proj.weight
+        kk = w.shape[1] * w.shape[2] * w.shape[3]
+        dwp = K.wgrad(dx[:, T:], cols)
+        G.put(w, dwp[:, :kk].contiguous())
+        if pe.text_proj.bias is not None or pe.proj.bias is not None:
+            st = torch.zeros(1, 2, D, device=dx.device, dtype=F32)
+            sv = torch.zeros(1, 2, D, device=dx.device, dtype=F32)
+            for b in range(B):
+                K.colsum(dx[b, :T], out=st)
+                K.colsum(dx[b, T:], out=sv)
+            G.put(pe.text_proj.bias, st[0, 0])
+            G.put(pe.proj.bias, sv[0, 0])
+        return (None, None, None, None, *G.out(ctx.params))
+
+
+def patch_embed_apply(pe, text: torch.Tensor, video: torch.Tensor, video2: Optional[torch.Tensor] = None):
+    if any(t is not None and t.requires_grad for t in (text, video, video2)):
+        raise NotImplementedError("gradients w.r.t. the latents / prompt embeddings are not implemented (the "
+                                  "reference's training feeds them as data)")
+    params = [pe.text_proj.weight, pe.text_proj.bias, pe.proj.weight, pe.proj.bias]
+    if not any(p is not None and p.requires_grad for p in params):
+        return pe.embed(text, video, video2)
+    return _PatchEmbedFn.apply(pe, text, video, video2, *[p for p in params if p is not None])
+
+
+class _TimeEmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, te, t0, *params):
+        h = K.linear_small(t0, te.linear_1.weight, te.linear_1.bias, act_out=K.ACT_SILU)
+        ctx.te, ctx.params = te, params
+        ctx.save_for_backward(t0)
+        return K.linear_small(h, te.linear_2.weight, te.linear_2.bias)
+
+    @staticmethod
+    def backward(ctx, demb):
+        (t0,) = ctx.saved_tensors
+        te = ctx.te
+        G = _Grads()
+        a1 = K.linear_small(t0, te.linear_1.weight, te.linear_1.bias)
+        h = K.silu(a1)
+        dh = _small_linear_bwd(G, te.linear_2, h, demb.to(BF16).contiguous())
+        _small_linear_bwd(G, te.linear_1, t0, K.silu_bwd(dh, a1))
+        return (None, None, *G.out(ctx.params))
+
+
+def time_embed_apply(te, t0: torch.Tensor) -> torch.Tensor:
+    params = [p for p in te.parameters()]
+    if not any(p.requires_grad for p in params):
+        h = K.linear_small(t0, te.linear_1.weight, te.linear_1.bias, act_out=K.ACT_SILU)
+        return K.linear_small(h, te.linear_2.weight, te.linear_2.bias)
+    return _TimeEmbedFn.apply(te, t0, *params)
+
+
+class _RowLinearFn(torch.autograd.Function):
+    """y = (x W^T + b) * scale over every row of the joint buffer (the branch's output linears)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, scale):
+        B, Ntok, D = x.shape
+        o = torch.empty(B, Ntok, w.shape[0], device=x.device, dtype=BF16)
+        epi = NAT.EPI_BIAS if scale == 1.0 else NAT.EPI_BIAS_SCALE
+        K.gemm(x.reshape(B * Ntok, D), [w], [b], o.view(B * Ntok, -1), epilogue=epi, alpha=scale)
+        ctx.scale = scale
+        ctx.save_for_backward(x, w, b)
+        return o
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b = ctx.saved_tensors
+        B, Ntok, D = x.shape
+        dy = dy.to(BF16).contiguous()
+        if ctx.scale != 1.0:
+            dy = K.scale_bf16(dy, ctx.scale)
+        dy2 = dy.view(B * Ntok, -1)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _dgrad(dy2, w, dx.view(B * Ntok, D))
+        if ctx.needs_input_grad[1]:
+            dw = K.wgrad(dy2, x.reshape(B * Ntok, D)).to(w.dtype)
+        if b is not None and ctx.needs_input_grad[2]:
+            db = _total(dy2).to(b.dtype)
+        return dx, dw, db, None
+
+
+def row_linear_apply(x: torch.Tensor, lin, scale: float) -> torch.Tensor:
+    return _RowLinearFn.apply(x, lin.weight, lin.bias, float(scale))
+
+
+def needs_grad(module, *tensors) -> bool:
+    """The training path is taken when autograd is on and a parameter or an input requires grad."""
+    if not torch.is_grad_enabled():
+        return False
+    if any(p.requires_grad for p in module.parameters()):
+        return True
+    for t in tensors:
+        if isinstance(t, torch.Tensor) and t.requires_grad:
+            return True
+        if isinstance(t, (list, tuple)) and any(isinstance(s, torch.Tensor) and s.requires_grad for s in t):
+            return True
+    return False

@@ -115,7 +115,8 @@ class CogvideoXBranchModel(CogVideoXTransformer3DModel):
                 wo_text: Optional[bool] = False, return_dict: bool = True):
         """branch_cogvideox.py:295-434.  Returns a list of [B, Nv, D] bf16 injection tensors (views of one
         [B, T + Nv, D] buffer per block; the text rows of that buffer are scratch)."""
-        self._check_inference(hidden_states, encoder_hidden_states, branch_cond)
+        from . import autograd as AG
+        train = AG.needs_grad(self, hidden_states, encoder_hidden_states, branch_cond)
         if wo_text:
             raise NotImplementedError("wo_text branches are not used by the VideoPainter inference scripts")
         if timestep_cond is not None:
@@ -129,14 +130,23 @@ class CogvideoXBranchModel(CogVideoXTransformer3DModel):
         T = enc.shape[1]
         D = cfg.num_attention_heads * cfg.attention_head_dim
         emb = self._time_embed(timestep, B, dev)
+        rope = _rope_dev(image_rotary_emb, dev)
+        scale = float(conditioning_scale)
+        if train:
+            # the training step's branch call (train_cogvideox_inpainting_i2v_video.py:1856-1865): differentiable
+            x = AG.patch_embed_apply(self.patch_embed, enc, hs, bc)
+            outs = []
+            for block, lin in zip(self.transformer_blocks, self.branch_blocks):
+                x = AG.block_apply(block, x, T, emb, rope)
+                outs.append(AG.row_linear_apply(x, lin, scale)[:, T:])
+            outs = None if len(outs) == 0 else outs
+            return (outs,) if not return_dict else CogvideoxBranchOutput(branch_block_samples=outs)
         x = self.patch_embed.embed(enc, hs, bc)
         Ntok = x.shape[1]
-        rope = _rope_dev(image_rotary_emb, dev)
         samples = []
         for i, block in enumerate(self.transformer_blocks):
             x = block.forward_joint(x, T, emb, rope)
             samples.append(x)
-        scale = float(conditioning_scale)
         outs = []
         for s, lin in zip(samples, self.branch_blocks):
             o = torch.empty(B, Ntok, D, device=dev, dtype=BF16)

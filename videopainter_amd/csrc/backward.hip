@@ -229,6 +229,14 @@ __global__ __launch_bounds__(256) void axpy_kernel(const bf16* __restrict__ a, c
   }
 }
 
+// y = silu(x) (the input of the AdaLN / time-embedding linears, for their weight gradients)
+__global__ __launch_bounds__(256) void silu_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float v = bf2f(x[i]);
+    y[i] = f2bf(v / (1.f + __expf(-v)));
+  }
+}
+
 // y = dy * silu'(x) = dy * sigmoid(x) (1 + x (1 - sigmoid(x)))  (the AdaLN / time-embedding SiLU)
 __global__ __launch_bounds__(256) void silu_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                        bf16* __restrict__ y, int64_t n) {
@@ -422,6 +430,13 @@ extern "C" int vp_axpy_bf16(const void* a, const void* b, float alpha, void* y, 
   if (!a || !b || !y || n <= 0 || (n % 8)) return VP_ERR_ARG;
   hipLaunchKernelGGL(axpy_kernel, dim3(grid_for(n / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16*)a,
                      (const bf16*)b, alpha, (bf16*)y, n / 8);
+  VP_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int vp_silu_bf16(const void* x, void* y, int64_t n, void* stream) {
+  if (!x || !y || n <= 0) return VP_ERR_ARG;
+  hipLaunchKernelGGL(silu_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (bf16*)y, n);
   VP_CHECK_LAUNCH();
   return 0;
 }

@@ -5,7 +5,7 @@ Tensors are plumbing here — device memory and streams.  Every arithmetic op on
 from __future__ import annotations
 
 import ctypes as C
-from typing import Optional, Sequence
+from typing import Optional, Sequence, Tuple
 
 import torch
 
@@ -875,4 +875,182 @@ def denormalize_bf16(x: torch.Tensor) -> torch.Tensor:
     x = x.contiguous()
     out = torch.empty_like(x)
     N.check(N.lib().vp_denormalize_bf16(_p(x), _p(out), x.numel(), _stream()), "vp_denormalize_bf16")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# training backward (csrc/backward.hip)
+# ------------------------------------------------------------------------------------------------------------------
+
+def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None, pad_to: int = 1) -> torch.Tensor:
+    """x: [R, C] or [nb, R, C] (contiguous last dim, any row / batch stride) -> [C, nb*R rounded up to pad_to]
+    (batch b in columns b*R ..); the pad columns are zero."""
+    _chk(x, "x")
+    x3 = x if x.dim() == 3 else x.unsqueeze(0)
+    nb, R, Cc = x3.shape
+    if x3.stride(-1) != 1:
+        raise ValueError("x must have a contiguous last dimension")
+    cols = nb * R
+    colp = (cols + pad_to - 1) // pad_to * pad_to
+    if out is None:
+        out = torch.empty(Cc, colp, device=x.device, dtype=BF16)
+    _chk(out, "out")
+    if out.shape[0] != Cc or out.shape[1] < cols or out.stride(1) != 1:
+        raise ValueError(f"transpose out must be [{Cc}, >= {cols}]")
+    if out.shape[1] > cols:
+        out[:, cols:].zero_()
+    N.check(N.lib().vp_transpose_bf16(_p(x3), x3.stride(1), x3.stride(0) if nb > 1 else 0, _p(out), out.stride(0), R,
+                                      R, Cc, nb, _stream()), "vp_transpose_bf16")
+    return out
+
+
+def colsum(a: torch.Tensor, b: Optional[torch.Tensor] = None, *, tokens_per_batch: Optional[int] = None,
+           text_len: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Column sums of a (* b) over rows, split per (batch, text/video): fp32 [rows / tokens_per_batch, 2, cols]
+    (index 1 = the text rows).  tokens_per_batch=None sums every row into [1, 2, cols][0, 0]."""
+    _chk(a, "a")
+    rows, cols = a.shape[0], a.shape[-1]
+    if a.dim() != 2:
+        a = a.reshape(-1, cols)
+        rows = a.shape[0]
+    ntok = rows if tokens_per_batch is None else tokens_per_batch
+    nb = rows // ntok
+    if out is None:
+        out = torch.zeros(nb, 2, cols, device=a.device, dtype=torch.float32)
+    _chk(out, "out", torch.float32)
+    ldb = 0
+    if b is not None:
+        _chk(b, "b")
+        b = b.reshape(-1, cols) if b.dim() != 2 else b
+        if b.shape[0] != rows:
+            raise ValueError("colsum: a and b row counts differ")
+        ldb = _rowmajor(b, "b")
+    N.check(N.lib().vp_colsum_bf16(_p(a), _rowmajor(a, "a"), _p(b), ldb, rows, cols, ntok, text_len, _p(out),
+                                   _stream()), "vp_colsum_bf16")
+    return out
+
+
+def adaln_bwd(x: torch.Tensor, dy: torch.Tensor, dx: torch.Tensor, text_len: int, ln_w, ln_b, eps: float,
+              mod: torch.Tensor, chunks=(0, 1, 3, 4), n_out=None, dn_out=None, xhat_out=None) -> torch.Tensor:
+    """dx += LN'(dy (1 + scale) w) for y = bf16(bf16(LN(x) w + b) (1 + scale) + shift); x, dy, dx contiguous
+    [B, Ntok, D]; chunks = (shift_v, scale_v, shift_t, scale_t) of mod [B, *]."""
+    for t, n in ((x, "x"), (dy, "dy"), (dx, "dx")):
+        _chk(t, n)
+        if not t.is_contiguous() or t.shape != x.shape:
+            raise ValueError(f"{n} must be contiguous {tuple(x.shape)}")
+    B, Ntok, D = x.shape
+    for t in (n_out, dn_out, xhat_out):
+        if t is not None and (t.shape != x.shape or not t.is_contiguous()):
+            raise ValueError("adaln_bwd outputs must be contiguous like x")
+    if mod.shape[0] != B or mod.stride(-1) != 1:
+        raise ValueError("mod must be [B, *] with a contiguous last dim")
+    N.check(N.lib().vp_adaln_bwd_bf16(_p(x), _p(dy), _p(dx), B, Ntok, D, text_len, _p(ln_w), _p(ln_b), eps, _p(mod),
+                                      mod.stride(0), *chunks, _p(n_out), _p(dn_out), _p(xhat_out), _stream()),
+            "vp_adaln_bwd_bf16")
+    return dx
+
+
+def rowscale(x: torch.Tensor, out: torch.Tensor, tokens_per_batch: int, text_len: int, mod: torch.Tensor,
+             chunk_v: int, chunk_t: int) -> torch.Tensor:
+    """out = bf16(x * mod[b, chunk]) per row (video / text chunk); x, out 2-D [rows, D] row-major views."""
+    _chk(x, "x")
+    _chk(out, "out")
+    rows, D = x.shape
+    if out.shape != x.shape:
+        raise ValueError("rowscale: shape mismatch")
+    N.check(N.lib().vp_rowscale_bf16(_p(x), _rowmajor(x, "x"), _p(out), _rowmajor(out, "out"), rows,
+                                     tokens_per_batch, D, text_len, _p(mod), mod.stride(0), chunk_v, chunk_t,
+                                     _stream()), "vp_rowscale_bf16")
+    return out
+
+
+def _flat(t: torch.Tensor, name: str) -> None:
+    _chk(t, name)
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def gelu(z: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _flat(z, "z")
+    out = torch.empty_like(z) if out is None else out
+    _flat(out, "out")
+    N.check(N.lib().vp_gelu_bf16(_p(z), _p(out), z.numel(), _stream()), "vp_gelu_bf16")
+    return out
+
+
+def gelu_bwd(dh: torch.Tensor, z: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _flat(dh, "dh")
+    _flat(z, "z")
+    out = torch.empty_like(z) if out is None else out
+    _flat(out, "out")
+    if dh.numel() != z.numel() or out.numel() != z.numel():
+        raise ValueError("gelu_bwd: size mismatch")
+    N.check(N.lib().vp_gelu_bwd_bf16(_p(dh), _p(z), _p(out), z.numel(), _stream()), "vp_gelu_bwd_bf16")
+    return out
+
+
+def axpy(a: torch.Tensor, b: torch.Tensor, alpha: float = 1.0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _flat(a, "a")
+    _flat(b, "b")
+    out = torch.empty_like(a) if out is None else out
+    _flat(out, "out")
+    if a.numel() != b.numel() or out.numel() != a.numel():
+        raise ValueError("axpy: size mismatch")
+    N.check(N.lib().vp_axpy_bf16(_p(a), _p(b), alpha, _p(out), a.numel(), _stream()), "vp_axpy_bf16")
+    return out
+
+
+def silu(x: torch.Tensor) -> torch.Tensor:
+    _flat(x, "x")
+    out = torch.empty_like(x)
+    N.check(N.lib().vp_silu_bf16(_p(x), _p(out), x.numel(), _stream()), "vp_silu_bf16")
+    return out
+
+
+def silu_bwd(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    _flat(dy, "dy")
+    _flat(x, "x")
+    if dy.numel() != x.numel():
+        raise ValueError("silu_bwd: size mismatch")
+    out = torch.empty_like(x)
+    N.check(N.lib().vp_silu_bwd_bf16(_p(dy), _p(x), _p(out), x.numel(), _stream()), "vp_silu_bwd_bf16")
+    return out
+
+
+def head_norm_rope_bwd(x_in: torch.Tensor, dy: torch.Tensor, dx: torch.Tensor, heads: int, text_len: int, ln,
+                       rope=None, dln: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+    """Backward of head_norm_rope (LayerNorm(64) module `ln`, RoPE on rows >= text_len): [B, N, heads*64] views with
+    contiguous last dim (dx may alias dy); dln = fp32 ([64], [64]) accumulators for the affine grads, or None."""
+    for t, n in ((x_in, "x_in"), (dy, "dy"), (dx, "dx")):
+        _chk(t, n)
+        if t.dim() != 3 or t.stride(-1) != 1 or t.shape != x_in.shape or t.shape[-1] != heads * 64:
+            raise ValueError(f"{n} must be [B, N, heads*64] with a contiguous last dim")
+    B, Ntok, _ = x_in.shape
+    cos = sin = None
+    if rope is not None:
+        cos, sin = rope
+        if cos.shape != (Ntok - text_len, 64) or not cos.is_contiguous() or not sin.is_contiguous():
+            raise ValueError(f"rope tables must be fp32 [{Ntok - text_len}, 64]")
+    dw = db = None
+    if dln is not None:
+        dw, db = dln
+        _chk(dw, "dln_w", torch.float32)
+        _chk(db, "dln_b", torch.float32)
+    N.check(N.lib().vp_head_norm_rope_bwd_bf16(_p(x_in), x_in.stride(1), x_in.stride(0), _p(dy), dy.stride(1),
+                                               dy.stride(0), _p(dx), dx.stride(1), dx.stride(0), B, Ntok, heads,
+                                               text_len, _p(ln.weight), _p(ln.bias), float(ln.eps), _p(cos), _p(sin),
+                                               _p(dw), _p(db), _stream()), "vp_head_norm_rope_bwd_bf16")
+    return dx
+
+
+WGRAD_PAD = 64  # the GEMM's fast path wants whole 64-wide K tiles
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW = dy^T x for a linear y = x W^T (+ b): dy [M, N], x [M, K] (or [nb, R, *] batched row views) -> bf16 [N, K]
+    by one GEMM over the token dimension (both operands transposed, M zero-padded to whole K tiles)."""
+    dyt = transpose(dy, pad_to=WGRAD_PAD)
+    xt = transpose(x, pad_to=WGRAD_PAD)
+    out = torch.empty(dyt.shape[0], xt.shape[0], device=dy.device, dtype=BF16)
+    gemm(dyt, [xt], [None], out)
     return out

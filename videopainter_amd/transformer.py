@@ -440,9 +440,8 @@ class CogVideoXTransformer3DModel(ModelMixin):
             timestep = timestep.expand(batch)
         temb0 = K.timestep_embedding(timestep, self.config.num_attention_heads * self.config.attention_head_dim,
                                      float(self.config.freq_shift))
-        te = self.time_embedding
-        h = K.linear_small(temb0, te.linear_1.weight, te.linear_1.bias, act_out=K.ACT_SILU)
-        return K.linear_small(h, te.linear_2.weight, te.linear_2.bias)
+        from .autograd import time_embed_apply
+        return time_embed_apply(self.time_embedding, temb0)
 
     def forward(self, hidden_states: torch.Tensor, encoder_hidden_states: torch.Tensor,
                 timestep: Union[int, float, torch.LongTensor], timestep_cond: Optional[torch.Tensor] = None,
@@ -452,8 +451,14 @@ class CogVideoXTransformer3DModel(ModelMixin):
                 self_guidance_hidden_states=None, self_guidance_masks=None,
                 return_hidden_states: Optional[bool] = False, return_resample_mask: Optional[bool] = False,
                 id_pool_resample_learnable: Optional[bool] = False, return_dict: bool = True):
-        """Reference :472-646."""
-        self._check_inference(hidden_states, encoder_hidden_states)
+        """Reference :472-646.  With autograd on and a parameter or input requiring grad, the differentiable path
+        (videopainter_amd/autograd.py: gradient-checkpointed blocks on the HIP backward kernels) runs instead."""
+        from . import autograd as AG
+        if AG.needs_grad(self, hidden_states, encoder_hidden_states, branch_block_samples):
+            return self._forward_train(hidden_states, encoder_hidden_states, timestep, image_rotary_emb,
+                                       attention_kwargs, branch_block_samples, branch_block_masks, add_first,
+                                       self_guidance_hidden_states, return_hidden_states, return_resample_mask,
+                                       id_pool_resample_learnable, timestep_cond, return_dict)
         if timestep_cond is not None:
             raise ValueError("timestep_cond requires a cond_proj, which CogVideoX's TimestepEmbedding does not have")
         if self_guidance_hidden_states is not None or self_guidance_masks is not None:
@@ -536,6 +541,53 @@ class CogVideoXTransformer3DModel(ModelMixin):
                 if return_resample_mask:
                     return (output, hidden_states_list, resample_mask)
                 return (output, hidden_states_list)
+            return (output,)
+        return Transformer2DModelOutput(sample=output)
+
+
+    def _forward_train(self, hidden_states, encoder_hidden_states, timestep, image_rotary_emb, attention_kwargs,
+                       branch_block_samples, branch_block_masks, add_first, self_guidance_hidden_states,
+                       return_hidden_states, return_resample_mask, id_pool_resample_learnable, timestep_cond,
+                       return_dict):
+        """The training step's transformer call (train_cogvideox_inpainting_i2v_video.py:1867-1876): the same
+        forward launches, every block a gradient-checkpointed autograd node."""
+        from . import autograd as AG
+        if timestep_cond is not None or self_guidance_hidden_states is not None:
+            raise NotImplementedError("timestep_cond / self-guidance are not on the training path")
+        if attention_kwargs and attention_kwargs.get("prev_hidden_states") is not None:
+            raise NotImplementedError("the previous-clip blend is inference-only (no backward)")
+        if return_hidden_states or return_resample_mask or id_pool_resample_learnable:
+            raise NotImplementedError("return_hidden_states / resample masks are inference-only (no backward)")
+        dev = self.proj_out.weight.device
+        B, F, C, H, W = hidden_states.shape
+        cfg = self.config
+        p = cfg.patch_size
+        if not cfg.use_rotary_positional_embeddings:
+            raise NotImplementedError("CogVideoX-2B head (norm_final on video rows only) is not on the 5B-I2V path")
+        hs = _bf(hidden_states.to(dev))
+        enc = _bf(encoder_hidden_states.to(dev))
+        T = enc.shape[1]
+        emb = self._time_embed(timestep, B, dev)
+        x = AG.patch_embed_apply(self.patch_embed, enc, hs)
+        tok_mask = None
+        if branch_block_masks is not None:
+            tok_mask = K.patch_mask(branch_block_masks.detach().to(dev), p)
+        rope = _rope_dev(image_rotary_emb, dev)
+        bs = None
+        if branch_block_samples is not None:
+            bs = [s.to(dev, BF16) for s in branch_block_samples]
+        nl = len(self.transformer_blocks)
+        interval = int(np.ceil(nl / len(bs))) if bs else 1
+        for i, block in enumerate(self.transformer_blocks):
+            inj = None
+            if bs is not None:
+                if not add_first:
+                    inj = bs[i // interval]
+                elif i < len(bs):
+                    inj = bs[i]
+            x = AG.block_apply(block, x, T, emb, rope, inj, tok_mask if inj is not None else None)
+        output = AG.head_apply(self, x, emb, (B, F, H, W, T))
+        if not return_dict:
             return (output,)
         return Transformer2DModelOutput(sample=output)
 
