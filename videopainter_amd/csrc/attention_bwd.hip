@@ -83,6 +83,13 @@ VP_DEV bf16x8 read_tr(const char* tile, int slab, const TrAddr& a, int dh) {
   return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+VP_DEV f32x16 splat16(float v) {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = v;
+  return z;
+}
+
 VP_DEV f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -128,7 +135,10 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const vp_attn_bwd_desc d
 }
 
 // ---- dQ: a workgroup per (b, h, 128 queries), 64-key tiles ----
-__global__ __launch_bounds__(BW * 64, 2) void bwd_dq_kernel(const vp_attn_bwd_desc d) {
+#ifndef VP_DQ_WAVES
+#define VP_DQ_WAVES 2  // waves per SIMD the dQ kernel is register-budgeted for (A/B: -DVP_DQ_WAVES=3)
+#endif
+__global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_attn_bwd_desc d) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -153,7 +163,7 @@ __global__ __launch_bounds__(BW * 64, 2) void bwd_dq_kernel(const vp_attn_bwd_de
     }
   }
   const int64_t so = ((int64_t)b * d.H + h) * d.Nq + qc;
-  const float lse = d.lse[so], Dq = d.delta[so];
+  const f32x16 negl = splat16(-d.lse[so]), negd = splat16(-d.delta[so]);
   const bf16* kb = (const bf16*)d.K + (int64_t)b * d.k_sb + h * 64;
   const bf16* vb = (const bf16*)d.V + (int64_t)b * d.v_sb + h * 64;
   const TrAddr ta = tr_addr(lane);
@@ -173,25 +183,35 @@ __global__ __launch_bounds__(BW * 64, 2) void bwd_dq_kernel(const vp_attn_bwd_de
     const char* Kt = smem + (ti & 1) * STAGE;
     const char* Vt = Kt + TILE;
     const int lim = d.Nk - ti * BT;
+    // the accumulators start at -lse / -D (C-init), so P = exp2(S) and dS = P * dP come straight off the matrix
+    // pipe: one exp and one multiply per score; keys past Nk (last tile only) start at -inf instead
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
       if (!active) break;
       bf16x8 a[4];
       read_rows(Kt, kh, lane, a);
-      f32x16 s = zero16();
+      // first MFMA of each chain in asm with the loop-invariant C (dst != srcC: the -lse / -D registers are
+      // never copied)
+      f32x16 s, dp;
+      if (lim >= BT) {  // wave-uniform
+        asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(s) : "v"(a[0]), "v"(qf[0]), "v"(negl));
+      } else {
+        f32x16 cm = negl;
 #pragma unroll
-      for (int ds = 0; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], qf[ds], s, 0, 0, 0);
+        for (int i = 0; i < 16; ++i)
+          if (kh * 32 + acc_row(i, hl) >= lim) cm[i] = -INFINITY;
+        // (builtin here: the compiler places the VALU-write -> MFMA-srcC wait states, which it does not for asm)
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], qf[0], cm, 0, 0, 0);
+      }
+#pragma unroll
+      for (int ds = 1; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], qf[ds], s, 0, 0, 0);
       read_rows(Vt, kh, lane, a);
-      f32x16 dp = zero16();
+      asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(dp) : "v"(a[0]), "v"(gf[0]), "v"(negd));
 #pragma unroll
-      for (int ds = 0; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], gf[ds], dp, 0, 0, 0);
+      for (int ds = 1; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], gf[ds], dp, 0, 0, 0);
       bf16x8 pf[2];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = kh * 32 + acc_row(i, hl);
-        const float p = key < lim ? __builtin_amdgcn_exp2f(s[i] - lse) : 0.f;
-        pf[i >> 3][i & 7] = f2bf(p * (dp[i] - Dq));
-      }
+      for (int i = 0; i < 16; ++i) pf[i >> 3][i & 7] = f2bf(__builtin_amdgcn_exp2f(s[i]) * dp[i]);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -216,7 +236,7 @@ __global__ __launch_bounds__(BW * 64, 2) void bwd_dkdv_kernel(const vp_attn_bwd_
   const int key = kb * BW * 32 + wave * 32 + (lane & 31);
   const int kc = min(key, d.Nk - 1);
   const float c = d.scale * 1.4426950408889634f;
-  // B operands: K^T and V^T from this lane's key row
+  // B operands: K^T pre-scaled by c (so S comes out in log2 units) and V^T, from this lane's key row
   bf16x8 kf[4], vf[4];
   {
     const bf16* kr = (const bf16*)d.K + (int64_t)b * d.k_sb + (int64_t)kc * d.k_sn + h * 64;
@@ -225,6 +245,8 @@ __global__ __launch_bounds__(BW * 64, 2) void bwd_dkdv_kernel(const vp_attn_bwd_
     for (int ds = 0; ds < 4; ++ds) {
       kf[ds] = *(const bf16x8*)(kr + ds * 16 + hl * 8);
       vf[ds] = *(const bf16x8*)(vr + ds * 16 + hl * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) kf[ds][e] = f2bf(bf2f(kf[ds][e]) * c);
     }
   }
   const bf16* qb = (const bf16*)d.Q + (int64_t)b * d.q_sb + h * 64;
@@ -240,7 +262,9 @@ __global__ __launch_bounds__(BW * 64, 2) void bwd_dkdv_kernel(const vp_attn_bwd_
   float stat = 0.f;
   auto load_stat = [&](int ti) {
     const int qq = ti * BT + (tid & 63);
-    if (tid < 2 * BT) stat = qq < d.Nq ? (tid < BT ? lse_row[qq] : d_row[qq]) : 0.f;
+    // rows past Nq: lse = +inf, so their S accumulators start at -inf and P = 0 there (no per-score mask)
+    // (stored negated: they are the C-init of the S / dP accumulators)
+    if (tid < 2 * BT) stat = qq < d.Nq ? -(tid < BT ? lse_row[qq] : d_row[qq]) : (tid < BT ? -INFINITY : 0.f);
   };
   auto put_stat = [&](int ti) {
     if (tid < 2 * BT) ((float*)(smem + (ti & 1) * STAGE + 2 * TILE))[tid] = stat;
@@ -263,32 +287,35 @@ __global__ __launch_bounds__(BW * 64, 2) void bwd_dkdv_kernel(const vp_attn_bwd_
     const char* Qt = smem + (ti & 1) * STAGE;
     const char* Gt = Qt + TILE;
     const float* st = (const float*)(Qt + 2 * TILE);
-    const int lim = d.Nq - ti * BT;
+    // S and dP accumulators start at -lse / -D of their query rows (C-init from the staged, negated statistics): P =
+    // exp2(S), dS = P * dP, one exp and one multiply per score
 #pragma unroll
     for (int qh = 0; qh < 2; ++qh) {
       if (!active) break;
-      bf16x8 a[4];
-      read_rows(Qt, qh, lane, a);
-      f32x16 s = zero16();
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], kf[ds], s, 0, 0, 0);
-      read_rows(Gt, qh, lane, a);
-      f32x16 dp = zero16();
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], vf[ds], dp, 0, 0, 0);
-      bf16x8 pp[2], pd[2];
+      f32x16 s, dp;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r0 = qh * 32 + 8 * j + 4 * hl;
         const f32x4 l4 = *(const f32x4*)(st + r0), d4 = *(const f32x4*)(st + BT + r0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int i = 4 * j + r;
-          // s is q.K in natural units here (Q from memory, K unscaled): c * s - lse in log2 units
-          const float p = r0 + r < lim ? __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], c, -l4[r])) : 0.f;
-          pp[i >> 3][i & 7] = f2bf(p);
-          pd[i >> 3][i & 7] = f2bf(p * (dp[i] - d4[r]));
+          s[4 * j + r] = l4[r];
+          dp[4 * j + r] = d4[r];
         }
+      }
+      bf16x8 a[4];
+      read_rows(Qt, qh, lane, a);
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], kf[ds], s, 0, 0, 0);
+      read_rows(Gt, qh, lane, a);
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], vf[ds], dp, 0, 0, 0);
+      bf16x8 pp[2], pd[2];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(s[i]);
+        pp[i >> 3][i & 7] = f2bf(p);
+        pd[i >> 3][i & 7] = f2bf(p * dp[i]);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j)
