@@ -359,7 +359,7 @@ def run_config4(args, world: int, rank: int, local: int) -> None:
         line = {
             "metric": METRIC, "value": steps_per_s, "unit": "steps/s", "n_gpus": world, "steps": n_steps,
             "warmup": args.warmup, "ms_per_step": elapsed / n_steps * 1e3 * world, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "scaling": "strong" if args.mode == "ulysses" else "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic latents/prompt embeds of the 4 x 49f 480x720 windows; random-init CogVideoX-5b-I2V "
                     "(ID-resample processor) + 2-layer branch weights (no checkpoints offline)",
             "config": {"workload": f"BASELINE config 4: any-length 196 frames = 4 windows x 49f 480x720 at stride 49, "
@@ -380,7 +380,7 @@ def run_config4(args, world: int, rank: int, local: int) -> None:
 
 def clip_of(rank: int, mode: str) -> int:
     """The clip a rank works on: its own (dp) or its CFG pair's (cfgpair: ranks 2p, 2p + 1 share clip p)."""
-    return rank // 2 if mode == "cfgpair" else rank
+    return rank // 2 if mode == "cfgpair" else (0 if mode == "ulysses" else rank)
 
 
 def timed_steps(one, sync_all, warmup: int, steps: int) -> float:
@@ -398,23 +398,24 @@ def timed_steps(one, sync_all, warmup: int, steps: int) -> float:
 
 def job_value(elapsed_max: float, steps: int, world: int, mode: str):
     """Whole-job denoising steps/s from the slowest rank's time: every clip advances `steps` steps."""
-    clips = world // 2 if mode == "cfgpair" else world
+    clips = world // 2 if mode == "cfgpair" else (1 if mode == "ulysses" else world)
     return clips, clips * steps / elapsed_max
 
 
-def kernel_classes(tl, n_steps: int, fp8: bool):
+def kernel_classes(tl, n_steps: int, fp8: bool, share: float = 1.0):
     """Per-kernel-class roofline from the instrumented pass: algorithmic FLOP per step of the class / its summed
     launch time per step.  attention: 4 B H N^2 64 per launch (one call = main grid + tail split + merge); gemm: every
-    projection GEMM of the step (step FLOP - attention FLOP), bf16 (and the MX-FP8 FeedForward GEMMs for config 5)."""
+    projection GEMM of the step (step FLOP - attention FLOP), bf16 (and the MX-FP8 FeedForward GEMMs for config 5).
+    share: the fraction of the step's work one rank does (1/P under the head-parallel split)."""
     torch.cuda.synchronize()
     attn_name = "attention_fp8" if fp8 else "attention"
     attn_ev = tl.events.get(attn_name, [])
     attn_ms_total = sum(a.elapsed_time(b) for a, b in attn_ev)
     gemm_ev = tl.events.get("gemm", []) + tl.events.get("gemm_mx", [])
     gemm_ms_total = sum(a.elapsed_time(b) for a, b in gemm_ev)
-    attn_fl_step = (L + LB) * attn_flops_per_launch()
+    attn_fl_step = (L + LB) * attn_flops_per_launch() * share
     total_fl, ffn_fl = step_flops(split=True)
-    gemm_fl_step = total_fl - attn_fl_step
+    gemm_fl_step = total_fl * share - attn_fl_step
     attn_ms = attn_ms_total / n_steps
     gemm_ms = gemm_ms_total / n_steps
     out = {}
@@ -425,7 +426,7 @@ def kernel_classes(tl, n_steps: int, fp8: bool):
                         "achieved": a_tf, "peak": peak_a, "unit": "TFLOP/s", "frac": a_tf / peak_a,
                         "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": src,
                         "per_launch_ms": attn_ms_total / max(1, len(attn_ev)), "launches_per_step": len(attn_ev) / n_steps,
-                        "ms_per_step": attn_ms, "algorithmic_flop_per_launch": attn_flops_per_launch()}
+                        "ms_per_step": attn_ms, "algorithmic_flop_per_launch": attn_flops_per_launch() * share}
     if fp8:  # FeedForward GEMMs in MX-FP8 (5 PF peak), the rest bf16: the peak of the class is the FLOP-weighted mix
         f8 = ffn_fl + (L + LB) * B * 6 * NTOK * D * D
         t_ideal = (gemm_fl_step - f8) / (PEAK_BF16_TFLOPS * 1e12) + f8 / (PEAK_FP8_TFLOPS * 1e12)
@@ -455,9 +456,10 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
                     help="BASELINE config: 2 = 49f 480x720 bf16 (headline), 4 = the any-length ID-resample chain "
                          "(4 windows, --steps denoising steps each), 5 = 49f 720x1280 with attention + FeedForward in fp8")
-    ap.add_argument("--mode", default="dp", choices=("dp", "cfgpair"),
+    ap.add_argument("--mode", default="dp", choices=("dp", "cfgpair", "ulysses"),
                     help="multi-GPU layout of configs 2/5: dp = one clip per rank, cfgpair = one clip per rank pair "
-                         "(CFG halves, one all-gather per step)")
+                         "(CFG halves, one all-gather per step), ulysses = ONE clip split head-parallel over all "
+                         "ranks (two all-to-alls per block; strong scaling)")
     ap.add_argument("--bcast", default="scatter_allgather", choices=("scatter_allgather", "broadcast"),
                     help="weight replication for N > 1 (distributed.broadcast_module)")
     args = ap.parse_args()
@@ -500,7 +502,12 @@ def main():
                                 clip_sample=False, set_alpha_to_one=True, timestep_spacing="trailing")
     sch.set_timesteps(50)
     timesteps = sch.timesteps.cpu()
-    harness = CogVideoXI2VDualInpaintAnyLHarness(tr, br, sch, cfg_pair=pair)
+    if args.mode == "ulysses":
+        from videopainter_amd import ulysses as U
+        views = U.UlyssesModels(tr, br, U.DistComm() if world > 1 else U.ThreadComm(1), rank=rank)
+        harness = CogVideoXI2VDualInpaintAnyLHarness(views.transformer, views.branch, sch)
+    else:
+        harness = CogVideoXI2VDualInpaintAnyLHarness(tr, br, sch, cfg_pair=pair)
     clip = clip_of(rank, args.mode)
     st, pe = make_state(harness, device, 42 + clip)
     rope = harness.rope_for(F, HL, WL)
@@ -555,7 +562,7 @@ def main():
         elapsed = max_over_ranks(elapsed, device)
     clips, steps_per_s = job_value(elapsed, args.steps, world, args.mode)
     ms_per_step = elapsed / args.steps * 1e3
-    classes, dominant = kernel_classes(tl, n_prof, args.config == 5)
+    classes, dominant = kernel_classes(tl, n_prof, args.config == 5, 1.0 / world if args.mode == "ulysses" else 1.0)
     total_fl, ffn_fl = step_flops(split=True)
     if args.config == 5:  # time the step would take at the dense peaks of the dtypes its MFMAs use
         f8_fl = ffn_fl + (L + LB) * (attn_flops_per_launch() + B * 6 * NTOK * D * D)  # + attention, QKV per block
@@ -573,12 +580,13 @@ def main():
     if rank == 0:
         rf = dict(classes[dominant])
         rf["kernel"] = f"{rf['kernel']} ({dominant}: dominant by time in this run)"
-        par = (f"dp{world} (independent clips, weights replicated over RCCL: {args.bcast})" if pair is None else
-               f"cfgpair x{clips} (CFG halves on rank pairs, one noise-prediction all-gather per step)")
+        par = (f"cfgpair x{clips} (CFG halves on rank pairs, one noise-prediction all-gather per step)" if pair
+               else f"ulysses{world} (one clip, head-parallel: 2 all-to-alls per block)" if args.mode == "ulysses"
+               else f"dp{world} (independent clips, weights replicated over RCCL: {args.bcast})")
         out = {
             "metric": METRIC, "value": steps_per_s, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.mode == "ulysses" else "weak",
             "vs_baseline": None,
             "dtype": "bf16" if args.config == 2 else "bf16 + fp8 (e4m3, block-scaled MFMA) QKV, attention, FeedForward",
             "data": f"synthetic latents/prompt embeds of the 49f {HL * 8}x{WL * 8} shape; random-init "

@@ -249,7 +249,9 @@ class CogVideoXBlock(nn.Module):
                       resample_mask: Optional[torch.Tensor] = None, prev_joint: Optional[torch.Tensor] = None,
                       prev_clip_weight: Optional[float] = None, prev_resample_mask: Optional[torch.Tensor] = None,
                       inject: Optional[torch.Tensor] = None, inject_mask: Optional[torch.Tensor] = None,
-                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      out: Optional[torch.Tensor] = None, attend=None) -> torch.Tensor:
+        """attend: optional replacement of the processor's attention, `attend(attn, xn, text_len, rope) -> o`
+        [B, N, D] (the Ulysses head-parallel split, videopainter_amd/ulysses.py)."""
         B, Ntok, D = x.shape
         xf = x.view(B * Ntok, D)
         processor = self.attn1.processor
@@ -257,6 +259,8 @@ class CogVideoXBlock(nn.Module):
             raise ValueError(f"Unsupported processor type: {type(processor)}")
         mod1 = self.norm1.modulation(temb)
         qkv = None
+        if attend is not None and (self.qkv_mx is not None or prev_joint is not None):
+            raise NotImplementedError("the head-parallel split runs the bf16 standard processor only")
         if self.qkv_mx is not None:
             a = self.attn1
             xq = K.adaln_modulate_mx(x, self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len,
@@ -273,8 +277,11 @@ class CogVideoXBlock(nn.Module):
             # the block normalises the previous window's states with its own norm1 (reference :141-146)
             pn = K.adaln_modulate(_bf(prev_joint), self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len,
                                   self.norm1.norm.eps)
-        o = processor.attend(self.attn1, xn if xn is not None else x, text_len, rope, pn, prev_clip_weight,
-                             resample_mask, prev_resample_mask, qkv=qkv)
+        if attend is not None:
+            o = attend(self.attn1, xn, text_len, rope)
+        else:
+            o = processor.attend(self.attn1, xn if xn is not None else x, text_len, rope, pn, prev_clip_weight,
+                                 resample_mask, prev_resample_mask, qkv=qkv)
         del qkv
         del xn, pn
         x_mid = torch.empty_like(x)
