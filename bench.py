@@ -1,6 +1,6 @@
 """Denoising steps/s of the VideoPainter hot path on MI355X (BASELINE.json config 2, data-parallel clips for N>1).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|4|5] [--mode dp|cfgpair]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|4|5] [--mode dp|cfgpair|ulysses|stages]
                     [--no-cpu-baseline] [--cpu-baseline-only [--cpu-full-step]]
     (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
 
@@ -456,10 +456,11 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
                     help="BASELINE config: 2 = 49f 480x720 bf16 (headline), 4 = the any-length ID-resample chain "
                          "(4 windows, --steps denoising steps each), 5 = 49f 720x1280 with attention + FeedForward in fp8")
-    ap.add_argument("--mode", default="dp", choices=("dp", "cfgpair", "ulysses"),
+    ap.add_argument("--mode", default="dp", choices=("dp", "cfgpair", "ulysses", "stages"),
                     help="multi-GPU layout of configs 2/5: dp = one clip per rank, cfgpair = one clip per rank pair "
                          "(CFG halves, one all-gather per step), ulysses = ONE clip split head-parallel over all "
-                         "ranks (two all-to-alls per block; strong scaling)")
+                         "ranks (two all-to-alls per block; strong scaling); stages = the any-length window chain "
+                         "as a window-stage pipeline (point-to-point hand-offs; = --config 4)")
     ap.add_argument("--bcast", default="scatter_allgather", choices=("scatter_allgather", "broadcast"),
                     help="weight replication for N > 1 (distributed.broadcast_module)")
     args = ap.parse_args()
@@ -473,7 +474,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.config == 4:
+    if args.config == 4 or args.mode == "stages":
+        set_config(2)  # the any-length chain runs 49f 480x720 windows
         run_config4(args, world, rank, local)
         return
     if world != args.gpus:

@@ -1,0 +1,12 @@
+#!/bin/bash
+# FETCH_SIZE / WRITE_SIZE passes (one counter block per run) on the GEMM and the bf16 attention at config-2 shapes
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for K in gemm attention; do
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/pmc_${K}_$C -o k --output-format csv -- python tools/bench_kernels.py --only $K --iters 2 --gemm-variants 11 --variant bounded > gpurun_out/pmc_${K}_$C.log 2>&1
+    rc=$?; echo "pmc $K $C rc=$rc"; [ $rc -ne 0 ] && exit $rc
+  done
+done
+exit 0

@@ -9,6 +9,8 @@
 // accumulator = 4 consecutive output channels of one pixel), operand tiles staged by LDS-DMA
 // (global_load_lds_dwordx4: per-lane gather source, lane-linear LDS destination, bank swizzle on the source address
 // and undone on the read), 2-stage ring.  Roofline: MFMA-bound for Cin >= 64 (AI = 2*128*BN*64 / 16+BN/8 KB).
+#include <stdlib.h>
+
 #include "vp_common.h"
 
 namespace {
@@ -39,7 +41,12 @@ VP_DEV void glds16(const bf16* src, char* lds) {
   __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)lds, 16, 0, 0);
 }
 
-template <int BN>
+// HOIST (Cin >= 64): a 64-channel K-tile never straddles a tap, so the tap of K-tile kt is wave-uniform and each of
+// this lane's 4 A rows needs its gather address only once per tap (then + the tile's channel offset): 3 VALU per
+// row and K-tile instead of the full tap decode + bounds + 64-bit pixel arithmetic (~25 VALU), which on the
+// 128-channel high-resolution convs issued as many VALU cycles as the tile's 32 MFMAs.  The weight rows are one
+// 64-bit pointer per instruction plus a uniform K offset.
+template <int BN, bool HOIST>
 __global__ __launch_bounds__(CNT, 2) void conv3d_kernel(const vp_conv3d_desc d, int c8s) {
   using G = ConvGeom<BN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -90,7 +97,54 @@ __global__ __launch_bounds__(CNT, 2) void conv3d_kernel(const vp_conv3d_desc d, 
   const bf16* Hs = (const bf16*)d.hist;
   const bf16* Wt = (const bf16*)d.w;
 
+  // source pixel (element offset of its channel 0, from X or the history) of row i at tap (dt, dy, dx), or null
+  auto row_src = [&](int i, int dt, int dy, int dx) -> const bf16* {
+    const int yu = ry[i] + dy, xu = rx[i] + dx;
+    if (!rv[i] || yu < 0 || yu >= Hu || xu < 0 || xu >= Wu) return nullptr;
+    const int f = tmapl[rt[i] + dt];
+    const int64_t pix = (f >= 0 ? (int64_t)rb[i] * d.x_frames + f : (int64_t)rb[i] * d.hist_frames + (-1 - f)) *
+                            HWi + (int64_t)(yu >> ush) * d.Win + (xu >> usw);
+    return (f >= 0 ? X : Hs) + pix * d.Cin;
+  };
+
+  // HOIST state: per row the tap's source address (+ this lane's swizzled chunk) and a keep-offset mask
+  const char* abase[4];
+  int amask[4];
+  const char* wbase[G::B_INSTR];
+  const int tpt = HOIST ? (C8 >> 3) : 1;  // K-tiles per tap (power of two)
+  if constexpr (HOIST) {
+#pragma unroll
+    for (int j = 0; j < G::B_INSTR; ++j) {
+      const int r = (j * 4 + wave) * 8 + (lane >> 3);
+      const int n = min(n0 + r, d.Cout - 1);
+      wbase[j] = (const char*)(Wt + (int64_t)n * Ktot + (((lane & 7) ^ cswz(r)) << 3));
+    }
+  }
+  auto set_tap = [&](int tap) {  // HOIST: wave-uniform tap
+    const int dt = khw == 1 ? tap : tap / khw;
+    const int rem = tap - dt * khw;
+    const int dy = d.kw == 1 ? rem : rem / 3;
+    const int dx = rem - dy * d.kw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (i * 4 + wave) * 8 + (lane >> 3);
+      const bf16* p = row_src(i, dt, dy, dx);
+      amask[i] = p != nullptr ? -1 : 0;
+      abase[i] = p != nullptr ? (const char*)(p + (((lane & 7) ^ cswz(r)) << 3)) : (const char*)g_zero16;
+    }
+  };
+
   auto stage = [&](int kt, char* buf) {
+    if constexpr (HOIST) {
+      if ((kt & (tpt - 1)) == 0) set_tap(kt / tpt);
+      const int cb = (kt & (tpt - 1)) * 128;  // byte offset of the tile's 64 channels within the tap
+#pragma unroll
+      for (int i = 0; i < 4; ++i) glds16((const bf16*)(abase[i] + (cb & amask[i])), buf + (i * 4 + wave) * 1024);
+#pragma unroll
+      for (int j = 0; j < G::B_INSTR; ++j)
+        glds16((const bf16*)(wbase[j] + (int64_t)kt * 128), buf + G::A_BYTES + (j * 4 + wave) * 1024);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rbase = (i * 4 + wave) * 8;
@@ -104,13 +158,8 @@ __global__ __launch_bounds__(CNT, 2) void conv3d_kernel(const vp_conv3d_desc d, 
         const int rem = tap - dt * khw;
         const int dy = d.kw == 1 ? rem : (rem * 11) >> 5;  // rem / 3 for rem < 9
         const int dx = rem - dy * d.kw;
-        const int yu = ry[i] + dy, xu = rx[i] + dx;
-        if (yu >= 0 && yu < Hu && xu >= 0 && xu < Wu) {
-          const int f = tmapl[rt[i] + dt];
-          const int64_t pix = (f >= 0 ? (int64_t)rb[i] * d.x_frames + f : (int64_t)rb[i] * d.hist_frames + (-1 - f)) *
-                                  HWi + (int64_t)(yu >> ush) * d.Win + (xu >> usw);
-          src = (f >= 0 ? X : Hs) + pix * d.Cin + cin;
-        }
+        const bf16* p = row_src(i, dt, dy, dx);
+        if (p != nullptr) src = p + cin;
       }
       glds16(src, buf + rbase * 128);
     }
@@ -482,10 +531,20 @@ int launch_conv(const vp_conv3d_desc& d, int c8s, int64_t tiles, hipStream_t s) 
   using G = ConvGeom<BN>;
   static bool attr = false;  // > 64 KB of dynamic LDS needs the opt-in (once per instance)
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv3d_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    (void)hipFuncSetAttribute((const void*)conv3d_kernel<BN, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              G::LDS);
+    (void)hipFuncSetAttribute((const void*)conv3d_kernel<BN, true>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL(conv3d_kernel<BN>, dim3((unsigned)tiles), dim3(CNT), G::LDS, s, d, c8s);
+  // VP_CONV_HOIST=0 keeps the per-K-tile tap decode (A/B)
+  static const int hoist_env = [] {
+    const char* e = getenv("VP_CONV_HOIST");
+    return e != nullptr ? atoi(e) : 1;
+  }();
+  if (d.Cin >= 64 && hoist_env != 0)
+    hipLaunchKernelGGL((conv3d_kernel<BN, true>), dim3((unsigned)tiles), dim3(CNT), G::LDS, s, d, c8s);
+  else
+    hipLaunchKernelGGL((conv3d_kernel<BN, false>), dim3((unsigned)tiles), dim3(CNT), G::LDS, s, d, c8s);
   VP_CHECK_LAUNCH();
   return 0;
 }
