@@ -201,6 +201,13 @@ VP_DEV int vswz(int row) { return ((row >> 1) & 1) << 2; }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+// the lane id computed in place (a hoisted copy would be one more long-lived VGPR)
+VP_DEV int lane_id_opaque() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 VP_DEV void glds16(const char* sbase, int voff, char* lds) {
   const unsigned la = (unsigned)(uintptr_t)(lds_void_t*)lds;
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(la), "v"(voff), "s"(sbase)
@@ -584,7 +591,7 @@ constexpr int F8_STAGE = 2 * F8_TILE + 128;        // + the V^T scales
 // 32-key halves (C-init: S = s - m + F8_OFF), one max over both, thresholded rescale, exp2 -> P in e4m3 straight
 // into the PV B-operand registers, PV as two MFMAs over all 64 keys.
 // P = exp2(S) in e4m3, 4 per VGPR: VGPRs 0-3 = half 0 (K-slots 16g..), 4-7 = half 1 (32+16g..); returns this
-// lane's sum of the 32 values
+// lane's sum of the 32 values (dead code, removed by the compiler, when the sums run on the matrix pipe)
 VP_DEV float f8_exp_pack(const f32x16 (&s)[2], i32x8& pf) {
   float ps[4];
 #pragma unroll
@@ -604,13 +611,19 @@ VP_DEV float f8_exp_pack(const f32x16 (&s)[2], i32x8& pf) {
   return (ps[0] + ps[1]) + (ps[2] + ps[3]);
 }
 
-// LAZY (lazy-max, as softmax_half_lazy): P stored as p * 2^6, the max path only when a lane's 32 stored values
-// sum past 448; otherwise P = p * 2^7 with the max path every tile and rescale threshold 1.5 (P <= 2^8.5 < 448).
-template <int NW, int OCC, bool LAZY = false, int SUB = 1>
+// The kernel.  P is stored as p * 2^7 with the max path every tile and rescale threshold 1.5 (P <= 2^8.5 < 448).
+// RS: the row sums on the matrix pipe instead of 28 VALU adds per lane and tile — the packed P^T operand read as the
+// B operand of ONE v_mfma_scale_f32_16x16x128_f8f6f4 (lane l: column l % 16, K-chunks l / 16 and l / 16 + 4), whose
+// column n then holds query n's 64 keys in K-chunks {0, 2, 4, 6} and query n + 16's in {1, 3, 5, 7}; a 0/1 e4m3
+// selector as A (row 0 = the first set, row 1 = the second) leaves sum(query n) in accumulator row 0 and
+// sum(query n + 16) in row 1, i.e. in lane n's registers 0 and 1.  (The sum is then over the e4m3-ROUNDED P the PV
+// product uses, in fp32.)  At d = 64 the softmax VALU (32 exp2 at 8 cycles + max + pack) outweighs the tile's 4
+// MFMAs (256 cycles), so moving 112 VALU cycles onto a 32-cycle MFMA is the lever.
+template <int NW, int OCC, int SUB, bool RS>
 __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_desc dd) {
   static_assert(NW == 8, "the DMA split assumes 8 waves");
-  constexpr int OFF = LAZY ? 6 : 7;              // P is stored as p * 2^OFF
-  constexpr float THR = LAZY ? 2.5f : 1.5f;      // max path: P <= 2^(OFF + THR) < 448
+  constexpr int OFF = 7;        // P is stored as p * 2^OFF
+  constexpr float THR = 1.5f;   // max path: P <= 2^(OFF + THR) < 448
   const vp_attn_desc& d = dd.base;
   constexpr int QB = NW * 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -638,13 +651,19 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
   }
   const int sq = dd.qk_scale & 0xff, sk = (dd.qk_scale >> 8) & 0xff;
 
-  // DMA: this lane's row of its wave's piece (16 rows x 64 B) and the logical source chunk of its physical chunk
-  const int prow = (wave & 3) * 16 + (lane >> 2);
-  const int pch = (lane & 3) ^ swz8(prow);
+  // DMA: this lane's row of its wave's piece (16 rows x 64 B) and the logical source chunk of its physical chunk,
+  // held as ONE byte offset per lane (waves 0-3 stage K, 4-7 stage V^T) from a wave-uniform base that advances by
+  // whole tiles; only the last K tile (rows past Nk re-read the last key) recomputes the row from the lane id.  More
+  // long-lived address VGPRs get spilled at 128, and the spill reload's vmcnt(0) sits in front of the DMA issue.
+  const int ksn = (int)d.k_sn;
+  const int dma = [&] {
+    const int prow = (wave & 3) * 16 + (lane >> 2);
+    const int pch = (lane & 3) ^ swz8(prow);
+    return wave < 4 ? prow * ksn + pch * 16 : prow * dd.npad + pch * 16;
+  }();
   const char* kbase = (const char*)d.K + (int64_t)b * d.k_sb + h * 64;
   const char* vtbase = (const char*)d.V + (int64_t)bh * 64 * dd.npad;
   const char* vsbase = (const char*)dd.vs + (int64_t)bh * ntiles * 128;
-  const int ksn = (int)d.k_sn;
   // ring slot ti holds SUB consecutive 64-key tiles (one barrier per SUB tiles)
   const int nsup = (ntiles + SUB - 1) / SUB;
   auto issue = [&](int ti) {
@@ -654,10 +673,16 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
       if (SUB > 1 && kt >= ntiles) break;  // wave-uniform
       char* slot = smem + ((ti & 1) * SUB + sb) * F8_STAGE;
       if (wave < 4) {
-        const int r = min(kt * 64 + prow, d.Nk - 1);  // rows past the end re-read the last key (masked later)
-        glds16(kbase, r * ksn + pch * 16, slot + wave * 1024);
+        if (kt * 64 + 64 <= d.Nk) {
+          glds16(kbase + (int64_t)kt * 64 * ksn, dma, slot + wave * 1024);
+        } else {  // rows past the end re-read the last key (masked later)
+          const int ln = lane_id_opaque();
+          const int prow = (wave & 3) * 16 + (ln >> 2);
+          const int r = min(kt * 64 + prow, d.Nk - 1);
+          glds16(kbase, r * ksn + (((ln & 3) ^ swz8(prow)) << 4), slot + wave * 1024);
+        }
       } else {
-        glds16(vtbase + kt * 64, prow * dd.npad + pch * 16, slot + F8_TILE + (wave - 4) * 1024);
+        glds16(vtbase + kt * 64, dma, slot + F8_TILE + (wave - 4) * 1024);
       }
       if (wave == 0 && lane < 8) glds16(vsbase + kt * 128, lane * 16, slot + 2 * F8_TILE);
     }
@@ -675,6 +700,15 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
     o[1][i] = 0.f;
     negm[i] = (float)OFF;
   }
+  // RS: this lane's selector word (e4m3 1.0 = 0x38) and the 16x16 accumulator of the row sums.  The 8-VGPR
+  // selector tuple is re-materialised from the word next to each row-sum MFMA (after the scores died), not kept
+  // live through the softmax: at 128 VGPRs that is the difference between 13 spilled registers and none.
+  int selw = 0;
+  f32x4 lsum = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (RS) {
+    const int col = lane & 15, c = lane >> 4;
+    selw = ((col == 0 && (c & 1) == 0) || (col == 1 && (c & 1) == 1)) ? 0x38383838 : 0;
+  }
   const bool active = qb * QB + wave * 32 < d.Nq;  // wave-uniform
   issue(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -682,14 +716,13 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
   for (int ti = 0; ti < nsup; ++ti) {
     if (ti + 1 < nsup) issue(ti + 1);
 #pragma unroll
-   for (int sb = 0; sb < SUB; ++sb) {
-    const int kt = ti * SUB + sb;
-    if (SUB > 1 && kt >= ntiles) break;
-    const char* st = smem + ((ti & 1) * SUB + sb) * F8_STAGE;
-    if (active) {
-      f32x16 s[2];
-      const int lim = d.Nk - kt * 64;
-      auto scores = [&]() {
+    for (int sb = 0; sb < SUB; ++sb) {
+      const int kt = ti * SUB + sb;
+      if (SUB > 1 && kt >= ntiles) break;
+      const char* st = smem + ((ti & 1) * SUB + sb) * F8_STAGE;
+      if (active) {
+        f32x16 s[2];
+        const int lim = d.Nk - kt * 64;
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const char* kr = st + (hh * 32 + r0) * 64;
@@ -698,12 +731,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
           hk[0] = *(const u32x4*)(kr + ca);
           hk[1] = *(const u32x4*)(kr + cb);
           if (hh == 0) {
-            if constexpr (LAZY)  // opaque, so the fallback's recomputation is not merged with this one
-              asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %3, %4, %5 op_sel_hi:[0,0,0]"
-                           : "=&v"(s[0])
-                           : "v"(kf), "v"(qf), "v"(negm), "v"(sk), "v"(sq));
-            else
-              s[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, negm, 0, 0, 0, sk, 0, sq);
+            s[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, negm, 0, 0, 0, sk, 0, sq);
           } else {
             // asm: a fresh (early-clobber) destination with C = -m + OFF kept in its own registers (the builtin
             // form makes the compiler refill a copy of it with 8 v_mov_b64 per tile), then the 19 wait states a
@@ -718,10 +746,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
           mask_half(s[0], lim, 0, g);
           mask_half(s[1], lim, 1, g);
         }
-      };
-      scores();
-      // max path: the tile max over both halves and the lane pair, thresholded rescale of O, l, S and -m
-      auto max_path = [&]() {
+        // the tile max over both halves and the lane pair, thresholded rescale of O, l, S and -m
         float mx = s[0][0];
 #pragma unroll
         for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[0][i]);
@@ -734,7 +759,14 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
         if (__ballot(mx > thr) != 0ull) {
           const float dm = mx > thr ? mx : 0.f;
           const float alpha = __builtin_amdgcn_exp2f(-dm);
-          l_run *= alpha;
+          if constexpr (RS) {
+            // lane n < 16 holds the sums of queries n (this lane's) and n + 16 (lane n + 16's)
+            const float a16 = __shfl(alpha, (lane_id_opaque() + 16) & 63, 64);
+            lsum[0] *= alpha;
+            lsum[1] *= a16;
+          } else {
+            l_run *= alpha;
+          }
           m_run += dm;
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
@@ -746,41 +778,41 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
           }
           thr = THR;
         }
-      };
-      i32x8 pf;
-      float ls;
-      // lazy: no max; a lane sum <= 448 bounds each of its 32 stored values (e4m3 max), else the scores are
-      // recomputed (rare; keeping all 32 live through the exp2 pass would not fit 128 VGPRs) for the max path
-      bool need_max = !LAZY || thr == -INFINITY;
-      if (!need_max) {
-        ls = f8_exp_pack(s, pf);
-        need_max = __ballot(!(ls <= 448.f)) != 0ull;
-        if (need_max) scores();
-      }
-      if (need_max) {
-        max_path();
-        ls = f8_exp_pack(s, pf);
-      }
-      l_run += ls;
-      const int vsw = *(const unsigned short*)(st + 2 * F8_TILE + lane * 2);
-#pragma unroll
-      for (int dh = 0; dh < 2; ++dh) {
-        const char* vr = st + F8_TILE + (dh * 32 + r0) * 64;
-        i32x8 vf;
-        u32x4* hv = (u32x4*)&vf;
-        hv[0] = *(const u32x4*)(vr + ca);
-        hv[1] = *(const u32x4*)(vr + cb);
-        if (dh == 0)
-          o[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[0], 0, 0, 0, vsw, 0, 127);
+        i32x8 pf;
+        const float ls = f8_exp_pack(s, pf);
+        if constexpr (RS) {
+          int w;
+          asm volatile("v_mov_b32 %0, %1" : "=v"(w) : "v"(selw));  // opaque: keeps the tuple inside the loop
+          const i32x8 sel = {w, w, w, w, w, w, w, w};
+          lsum = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(sel, pf, lsum, 0, 0, 0, 127, 0, 127);
+        }
         else
-          o[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[1], 0, 0, 1, vsw, 0, 127);
+          l_run += ls;
+        const int vsw = *(const unsigned short*)(st + 2 * F8_TILE + lane * 2);
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          const char* vr = st + F8_TILE + (dh * 32 + r0) * 64;
+          i32x8 vf;
+          u32x4* hv = (u32x4*)&vf;
+          hv[0] = *(const u32x4*)(vr + ca);
+          hv[1] = *(const u32x4*)(vr + cb);
+          if (dh == 0)
+            o[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[0], 0, 0, 0, vsw, 0, 127);
+          else
+            o[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[1], 0, 0, 1, vsw, 0, 127);
+        }
       }
     }
-   }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
-  store_out(d, o, l_run, q, b, h, g);
+  if constexpr (RS) {
+    const int qq = lane & 31;
+    const float v0 = __shfl(lsum[0], qq & 15, 64), v1 = __shfl(lsum[1], qq & 15, 64);
+    store_out(d, o, qq < 16 ? v0 : v1, q, b, h, g, false);
+  } else {
+    store_out(d, o, l_run, q, b, h, g);
+  }
 }
 }  // namespace
 
@@ -945,28 +977,25 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
     return VP_ERR_ARG;
   if ((int64_t)d.Nk * d.k_sn > 0x7fffffff || (int64_t)64 * dd->npad > 0x7fffffff) return VP_ERR_ARG;
   constexpr int NW = 8;
-  // variants (A/B switch VP_ATTN8_VARIANT): 1 = max path every tile, 2 = lazy max (needs 159 VGPRs: spills at
-  // 128; 0.21 PF/s), 3 / 4 = 1 / 2 at 3 waves/SIMD (1.01 / 0.69 PF/s against 1.43), 5 = 1 with 128 keys per barrier
-  // (default, 1.46)
-  static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, false>, (const void*)attn_fwd_fp8<NW, 4, true>,
-                                    (const void*)attn_fwd_fp8<NW, 3, false>, (const void*)attn_fwd_fp8<NW, 3, true>,
-                                    (const void*)attn_fwd_fp8<NW, 4, false, 2>};
-  static const int subs[] = {1, 1, 1, 1, 2};
+  // VP_ATTN8_VARIANT (A/B): 1 = row sums on the VALU, 2 = row sums on the matrix pipe (default); both 128 keys per
+  // barrier at 4 waves/SIMD.  Dropped after round-1 A/B: lazy max (159 VGPRs, spills: 0.21 PF/s), 3 waves/SIMD
+  // (1.01), 64 keys per barrier (1.43 against 1.46).
+  static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, 2, false>, (const void*)attn_fwd_fp8<NW, 4, 2, true>};
   static bool attr_set = false;
   if (!attr_set) {
     attr_set = true;
-    for (int i = 0; i < 5; ++i)
-      (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, 2 * subs[i] * F8_STAGE);
+    for (int i = 0; i < 2; ++i)
+      (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * F8_STAGE);
   }
   const char* e = getenv("VP_ATTN8_VARIANT");
   int variant = e != nullptr ? atoi(e) : 0;
-  if (variant < 1 || variant > 5) variant = 5;
+  if (variant < 1 || variant > 2) variant = 2;
   const int nqb = (d.Nq + NW * 32 - 1) / (NW * 32);
   const int64_t grid = (int64_t)d.B * d.H * nqb;
   if (grid > 0x7fffffff) return VP_ERR_ARG;
   void* args[] = {(void*)dd};
-  const hipError_t le = hipLaunchKernel(fns[variant - 1], dim3((unsigned)grid), dim3(NW * 64), args,
-                                        2 * subs[variant - 1] * F8_STAGE, (hipStream_t)stream);
+  const hipError_t le = hipLaunchKernel(fns[variant - 1], dim3((unsigned)grid), dim3(NW * 64), args, 2 * 2 * F8_STAGE,
+                                        (hipStream_t)stream);
   if (le != hipSuccess) return (int)le;
   VP_CHECK_LAUNCH();
   return VP_OK;
