@@ -157,10 +157,14 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
   // (ln64_rope16: lane xor 16 / 32 are the other column quarters of the same row); v heads take the plain path.
   static_assert(FN % 4 == 0 && WN % 64 == 0, "whole heads per wave");
   const int g = lane >> 4;
+  // no integer division per element: the segment of a column by compares (at most 3 segments), the token of a row
+  // from the tile's first token (one division per tile)
+  auto seg_of = [&](int c) { return (int)(c >= d.n_seg) + (int)(c >= 2 * d.n_seg); };
+  const int tok0 = epi == VP_EPI_BIAS_QKNORM_ROPE ? m0 % d.tokens_per_batch : 0;
 #pragma unroll
   for (int hh = 0; hh < FN / 4; ++hh) {
     const int nh = n0 + wc * WN + hh * 64;  // first column of the head
-    const int sgh = nh / d.n_seg;
+    const int sgh = seg_of(nh);
     if (epi == VP_EPI_BIAS_QKNORM_ROPE && nh < d.N && sgh < 2) {
       const bf16* bp = (const bf16*)d.bias[sgh];
       const int hc = nh - sgh * d.n_seg;  // column within the segment
@@ -171,7 +175,8 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
         for (int r = 0; r < 4; ++r) bv[4 * jj + r] = bp != nullptr ? bf2f(bp[hc + 16 * jj + 4 * g + r]) : 0.f;
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int tok = (m0 + wr * WM + i * 16 + (lane & 15)) % d.tokens_per_batch;
+        int tok = tok0 + wr * WM + i * 16 + (lane & 15);
+        while (tok >= d.tokens_per_batch) tok -= d.tokens_per_batch;
         const bool rot = d.rope_cos != nullptr && tok >= d.text_len;
         const int64_t ro = (int64_t)(tok - d.text_len) * 64;
         float x[16];
@@ -196,13 +201,16 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
       const int j = hh * 4 + jj;
       const int nloc = wc * WN + j * 16 + g * 4;  // 4 consecutive columns
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      {
+        // the 4 columns share a segment (n_seg % 8 == 0)
+        const int sg = seg_of(n0 + nloc);
+        const bf16* bp = (const bf16*)d.bias[sg];
+        if (bp != nullptr) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + nloc + r;
-        if (FULL_N || n < d.N) {
-          const int sg = n / d.n_seg;
-          const bf16* bp = (const bf16*)d.bias[sg];
-          if (bp != nullptr) bv[r] = bf2f(bp[n - sg * d.n_seg]);
+          for (int r = 0; r < 4; ++r) {
+            const int n = n0 + nloc + r;
+            if (FULL_N || n < d.N) bv[r] = bf2f(bp[n - sg * d.n_seg]);
+          }
         }
       }
 #pragma unroll
@@ -235,13 +243,27 @@ VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* sme
   bf16* C = (bf16*)d.C;
   const int chunk = tid & 31;         // 16-byte chunk within the 512-byte tile row
   const int ncol = n0 + chunk * 8;
+  // row bookkeeping without an integer division per row: the image rows are consecutive matrix rows, so the output
+  // group (rows_per_group) and the batch (tokens_per_batch) of the image's first row are computed once and the
+  // rows of this thread step forward from there (at most one boundary per few rows unless a group is tiny)
+  const int mbase = m0 + row0;
+  const int rpg = d.rows_per_group;
+  const int grp0 = mbase / rpg, gin0 = mbase - grp0 * rpg;
+  const int tpb = d.tokens_per_batch;
+  const bool need_b = epi == VP_EPI_GATED;
+  const int b0 = need_b ? mbase / tpb : 0, tk0 = need_b ? mbase - b0 * tpb : 0;
 #pragma unroll 1
   for (int it = 0; it < nrows / (NT / 32); ++it) {
     const int mloc = it * (NT / 32) + (tid >> 5);
-    const int m = m0 + row0 + mloc;
+    const int m = mbase + mloc;
     if (m >= d.M || ncol >= d.N) continue;
     bf16x8 v = *(const bf16x8*)(smem + mloc * CT_STRIDE + chunk * 16);
-    const int64_t orow = (int64_t)(m / d.rows_per_group) * d.group_stride + d.row_offset + (m % d.rows_per_group);
+    int grp = grp0, gin = gin0 + mloc;
+    while (gin >= rpg) {
+      gin -= rpg;
+      ++grp;
+    }
+    const int64_t orow = (int64_t)grp * d.group_stride + d.row_offset + gin;
     if (FP8 && epi == VP_EPI_BIAS_GELU_MXFP8) {
       // MX-quantise the GELU output: the 4 lanes holding one 32-column block agree on its scale (N % 256 == 0, so
       // a block's lanes are all in or all out of range)
@@ -255,8 +277,11 @@ VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* sme
       continue;
     }
     if (epi == VP_EPI_GATED) {
-      const int b = m / d.tokens_per_batch;
-      const int tok = m - b * d.tokens_per_batch;
+      int b = b0, tok = tk0 + mloc;
+      while (tok >= tpb) {
+        tok -= tpb;
+        ++b;
+      }
       const bf16* g = (const bf16*)(tok < d.text_len ? d.gate_text : d.gate) + (int64_t)b * d.gate_bstride + ncol;
       const bf16x8 gv = *(const bf16x8*)g;
       const bf16x8 rv = *(const bf16x8*)((const bf16*)d.R + orow * d.ldr + ncol);
@@ -275,28 +300,33 @@ VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* sme
         v[e] = f2bf(o);
       }
     } else if (epi == VP_EPI_BIAS_ADDROWS) {
-      const bf16x8 pv = *(const bf16x8*)((const bf16*)d.addrows +
-                                         (int64_t)((m % d.rows_per_group) + d.addrows_offset) * d.addrows_ld + ncol);
+      const bf16x8 pv = *(const bf16x8*)((const bf16*)d.addrows + (int64_t)(gin + d.addrows_offset) * d.addrows_ld + ncol);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(pv[e]));
     }
+#ifdef VP_GEMM_ABL_NOSTORE  // ablation build (tools/gemm_kscan.py): everything but the global store
+    asm volatile("" ::"v"(v));
+#else
     *(bf16x8*)(C + orow * d.ldc + ncol) = v;
+#endif
   }
 }
 
 
-template <int NT, int FN, int FM, int WN, int WM, bool FP8>
+template <int NT, int FN, int FM, int WN, int WM, bool FP8, int EPI = -1>
 VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&acc)[FN][FM], char* smem, int m0,
                           int n0, int wr, int wc, int lane, int tid) {
-  epi_values<FN, FM, WN, WM>(
+  epi_values<FN, FM, WN, WM, EPI>(
       d, acc,
       [&](int j, int i, const bf16x4& o) { *(bf16x4*)epi_lds_addr<WN, WM>(smem, j, i, 0, wr, wc, lane) = o; }, m0,
       n0, wr, wc, lane);
   __syncthreads();
-  epi_rows_out<NT, FP8>(d, mx, smem, 0, BM, m0, n0, tid);
+  epi_rows_out<NT, FP8, EPI>(d, mx, smem, 0, BM, m0, n0, tid);
 }
 
-template <int VAR, bool FP8 = false, int GROUP = 4>
+// EPI >= 0: the epilogue kind as a compile-time constant (the default main loop is instantiated per kind: the dead
+// kinds' code and branches leave the epilogue), -1: runtime switch
+template <int VAR, bool FP8 = false, int GROUP = 4, int EPI = -1>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_desc d, const MxExt mx) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -682,7 +712,14 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     }
   }
 
-  gemm_epilogue<NTHREADS, FN, FM, WN, WM, FP8>(d, mx, acc, smem, m0, n0, wr, wc, lane, tid);
+#ifdef VP_GEMM_ABL_NOEPI  // ablation build (tools/gemm_kscan.py): main loop only, accumulators kept live
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(acc[j][i]));
+#else
+  gemm_epilogue<NTHREADS, FN, FM, WN, WM, FP8, EPI>(d, mx, acc, smem, m0, n0, wr, wc, lane, tid);
+#endif
 }
 
 
@@ -710,21 +747,29 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   }
   if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
   const MxExt mx = {};
+  // main loops: 11 = the quadrant-phase pipeline with the two wave groups staggered, instantiated per epilogue kind
+  // (default; +5 % over 5 on every config-2 shape), 5 = the unstaggered pipeline (VP_GEMM_VARIANT=5,
+  // A/B; also K < 512), 1 = the 2-stage ring (K % 64 != 0, e.g. the patch-embed im2col K = 132)
+  static const void* const k11[7] = {
+      (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS>, (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_GELU>,
+      (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_SCALE>, (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_GATED>,
+      (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_ADDROWS>, nullptr,
+      (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_QKNORM_ROPE>};
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<11>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES);
+    for (const void* f : k11)
+      if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr_set = true;
   }
-  // main loops: 11 = the quadrant-phase pipeline with the two wave groups staggered (default: +5 % over 5 on every
-  // config-2 shape), 5 = the unstaggered pipeline (VP_GEMM_VARIANT=5, A/B), 1 = the 2-stage ring
-  // (K % 64 != 0, e.g. the patch-embed im2col K = 132)
-  const char* e = getenv("VP_GEMM_VARIANT");
-  int variant = e != nullptr ? atoi(e) : 11;
+  static const int env_variant = [] {
+    const char* e = getenv("VP_GEMM_VARIANT");
+    return e != nullptr ? atoi(e) : 11;
+  }();
+  int variant = env_variant;
   if (variant != 1 && variant != 5 && variant != 11) variant = 11;
   // the quadrant pipeline adds 32-bit in-tile source offsets to a 64-bit tile base (A) / segment base (W)
   const bool w32 = (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
@@ -732,12 +777,16 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   if (variant != 1 && ((d->K % BK) != 0 || !tile32)) variant = 1;  // needs whole K-tiles
   if (variant == 11 && d->K < 8 * BK) variant = 5;                  // the staggered prologue assumes >= 8 K-tiles
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
-  if (variant == 11)
-    hipLaunchKernelGGL(gemm_bf16_kernel<11>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
-  else if (variant == 5)
+  if (variant == 11) {
+    void* args[] = {(void*)d, (void*)&mx};
+    const hipError_t le = hipLaunchKernel(k11[d->epilogue], dim3(tiles), dim3(NTHREADS), args, LDS_BYTES,
+                                          (hipStream_t)stream);
+    if (le != hipSuccess) return (int)le;
+  } else if (variant == 5) {
     hipLaunchKernelGGL(gemm_bf16_kernel<5>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
-  else
+  } else {
     hipLaunchKernelGGL(gemm_bf16_kernel<1>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
+  }
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
