@@ -816,10 +816,17 @@ extern "C" int vp_gemm_mx_fp8(const vp_gemm_mx_desc* x, void* stream) {
   if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
   // 32-bit DMA source offsets
   if ((int64_t)d->M * d->lda >= ((int64_t)1 << 31) || (int64_t)d->n_seg * d->K >= ((int64_t)1 << 31)) return VP_ERR_ARG;
+  // instantiated per epilogue kind for the block's fp8 GEMMs (QKV: BIAS, FF1: GELU_MXFP8, FF2: GATED); the others
+  // take the runtime switch
+  static const void* const kf[6] = {(const void*)gemm_bf16_kernel<5, true, 4, VP_EPI_BIAS>, nullptr, nullptr,
+                                    (const void*)gemm_bf16_kernel<5, true, 4, VP_EPI_GATED>, nullptr,
+                                    (const void*)gemm_bf16_kernel<5, true, 4, VP_EPI_BIAS_GELU_MXFP8>};
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES_FP8);
+    for (const void* f : kf)
+      if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES_FP8);
     attr_set = true;
   }
   MxExt mx;
@@ -827,8 +834,10 @@ extern "C" int vp_gemm_mx_fp8(const vp_gemm_mx_desc* x, void* stream) {
   for (int s = 0; s < 3; ++s) mx.w_scale[s] = (const uint8_t*)x->w_scale[s];
   mx.c_scale = (uint8_t*)x->c_scale;
   const int tiles = ((d->M + BM - 1) / BM) * (d->N / BN);
-  hipLaunchKernelGGL((gemm_bf16_kernel<5, true>), dim3(tiles), dim3(NTHREADS), LDS_BYTES_FP8, (hipStream_t)stream,
-                     *d, mx);
+  const void* fn = kf[d->epilogue] != nullptr ? kf[d->epilogue] : (const void*)gemm_bf16_kernel<5, true>;
+  void* args[] = {(void*)d, (void*)&mx};
+  const hipError_t le = hipLaunchKernel(fn, dim3(tiles), dim3(NTHREADS), args, LDS_BYTES_FP8, (hipStream_t)stream);
+  if (le != hipSuccess) return (int)le;
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
