@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 8
+#define VP_ABI_VERSION 9
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
@@ -99,6 +99,15 @@ typedef struct vp_gemm_desc {
 } vp_gemm_desc;
 
 int vp_gemm_bf16(const vp_gemm_desc* d, void* stream);
+
+/* Split-K form for GEMMs too small to fill the chip (fewer than 128 output tiles of 256 x 256, e.g. the T5 encoder's
+ * projections at M = 2 x 226 token rows; reference callers: transformers T5EncoderModel, anyl.py:216-256): the K
+ * range is cut into chunks of >= 512, each (tile, chunk) workgroup writes its fp32 partial tile to `workspace`, and a
+ * reduce pass sums the chunks in a fixed order (deterministic) and applies the epilogue (VP_EPI_BIAS, _GELU, _SCALE,
+ * _BIAS_ADDROWS; others never split).  vp_gemm_bf16_workspace_bytes: bytes this descriptor needs (0: no split, and
+ * vp_gemm_bf16_ws then runs vp_gemm_bf16).  vp_gemm_bf16 never splits. */
+int64_t vp_gemm_bf16_workspace_bytes(const vp_gemm_desc* d);
+int vp_gemm_bf16_ws(const vp_gemm_desc* d, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * MX-FP8 (OCP e4m3 elements, one E8M0 power-of-two scale per 32 consecutive K elements) — the fp8 path of

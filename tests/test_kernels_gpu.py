@@ -450,3 +450,45 @@ def test_attention_tail_split_matches_unsplit(Nq, Nk2, monkeypatch):
             kk, vv = torch.cat([kk, hd(kw["k2"])], 2), torch.cat([vv, hd(kw["v2"])], 2)
         ref = _sdpa(hd(q), kk, vv).transpose(1, 2).reshape(B, Nq, D)
         assert rel(out_s, ref) < 1e-2 and rel(out_u, ref) < 1e-2
+
+
+@pytest.mark.parametrize("epi", ["bias", "gelu", "scale", "addrows"])
+@pytest.mark.parametrize("M,Nn,Kk,segs", [(452, 1536, 4096, 3), (200, 2048, 2560, 1), (37, 512, 1024, 1)])
+def test_gemm_splitk_small_m(M, Nn, Kk, segs, epi):
+    """Split-K path (vp_gemm_bf16_ws) for GEMMs with too few output tiles (the T5 encoder's projections): every
+    epilogue it serves against torch fp32, the reduce's fixed chunk order makes it deterministic, and the plan really
+    splits.  Tolerance: bf16 output rounding (the chunked fp32 sum differs from the unsplit one only in fp32 order)."""
+    from videopainter_amd import _native as N
+    from videopainter_amd import kernels as K
+    torch.manual_seed(M + Nn)
+    a = torch.randn(M, Kk, device=dev).bfloat16()
+    ws = [(torch.randn(Nn // segs, Kk, device=dev) * Kk ** -0.5).bfloat16() for _ in range(segs)]
+    bs = [(torch.randn(Nn // segs, device=dev) * 0.1).bfloat16() for _ in range(segs)]
+    w = torch.cat(ws)
+    b = torch.cat(bs)
+    y = (a.float() @ w.float().t() + b.float()).bfloat16().float()
+    kw = {}
+    out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+    if epi == "gelu":
+        kw["epilogue"] = N.EPI_BIAS_GELU
+        ref = F.gelu(y, approximate="tanh")
+    elif epi == "scale":
+        kw.update(epilogue=N.EPI_BIAS_SCALE, alpha=0.7)
+        ref = y * 0.7
+    elif epi == "addrows":
+        out = torch.randn(M, Nn, device=dev).bfloat16()  # in place, like the T5 residual adds
+        kw.update(epilogue=N.EPI_BIAS_ADDROWS, addrows=out)
+        ref = y + out.float()
+    else:
+        ref = y
+    d = N.GemmDesc()
+    d.M, d.N, d.K, d.epilogue, d.n_seg = M, Nn, Kk, kw.get("epilogue", N.EPI_BIAS), Nn // segs
+    assert N.lib().vp_gemm_bf16_workspace_bytes(d) > 0, "expected the split-K plan for this shape"
+    K.gemm(a, ws, bs, out, **kw)
+    got = out.float()
+    err = (got - ref).abs().max().item()
+    assert err <= 0.02 * ref.abs().max().item() + 1e-2, err
+    if epi != "addrows":
+        again = torch.empty_like(out)
+        K.gemm(a, ws, bs, again, **kw)
+        assert torch.equal(again, out)

@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -92,6 +92,8 @@ _SIGS = {
     "vp_build_digest": (C.c_char_p, []),
     "vp_struct_sizes": (None, [C.POINTER(i64)]),
     "vp_gemm_bf16": (i32, [C.POINTER(GemmDesc), vp]),
+    "vp_gemm_bf16_workspace_bytes": (i64, [C.POINTER(GemmDesc)]),
+    "vp_gemm_bf16_ws": (i32, [C.POINTER(GemmDesc), vp, i64, vp]),
     "vp_gemm_mx_fp8": (i32, [C.POINTER(GemmMxDesc), vp]),
     "vp_mx_scale_bytes": (i64, [i64, i64]),
     "vp_mx_quantize_bf16": (i32, [vp, i64, vp, i64, vp, i32, i32, vp]),

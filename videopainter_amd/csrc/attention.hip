@@ -442,9 +442,6 @@ __global__ __launch_bounds__(NW * 64, 4) void attn_fwd(const vp_attn_desc d, con
   // a wave whose 32 queries all lie past Nq (the last query block of a head) only helps with the DMA and the
   // barriers, leaving its SIMD to the co-resident workgroups
   const bool active = qb * QB + wave * 32 < d.Nq;  // wave-uniform
-#ifdef VP_ATTN_AB_PRIO_YOUNG  // A/B build: static priority for the second-dispatched half (MI355X_MICROARCH.md item 4)
-  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-#endif
   issue(tbeg);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();

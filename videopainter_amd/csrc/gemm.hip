@@ -71,6 +71,9 @@ struct MxExt {
   const uint8_t* a_scale;
   const uint8_t* w_scale[3];
   uint8_t* c_scale;
+  // split-K (vp_gemm_bf16_ws): workgroup = (tile, K-chunk); fp32 partial tiles [nsplit][M][N] in ws
+  float* ws;
+  int kchunk, nsplit;
 };
 
 // scale ring of the fp8 path: 4 K-tiles x (A, W) x 1 KiB after the two operand stages (the ring slot of tile t is
@@ -326,7 +329,8 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
 
 // EPI >= 0: the epilogue kind as a compile-time constant (the default main loop is instantiated per kind: the dead
 // kinds' code and branches leave the epilogue), -1: runtime switch
-template <int VAR, bool FP8 = false, int GROUP = 4, int EPI = -1>
+// SPLIT: the split-K instance (fp32 partial tiles to mx.ws, the epilogue runs in gemm_splitk_reduce_kernel)
+template <int VAR, bool FP8 = false, int GROUP = 4, int EPI = -1, bool SPLIT = false>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_desc d, const MxExt mx) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -337,7 +341,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 
   const int tiles_m = (d.M + BM - 1) / BM;
   const int tiles_n = (d.N + BN - 1) / BN;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int t = SPLIT ? lin / mx.nsplit : lin;
+  const int kc = SPLIT ? lin - t * mx.nsplit : 0;  // K-chunk of this workgroup
+  // this workgroup's K range: [kbeg, kbeg + Kloop) (the whole K unless split)
+  const int kbeg = SPLIT ? kc * mx.kchunk : 0;
+  const int Kloop = SPLIT ? min(mx.kchunk, d.K - kbeg) : d.K;
   const int per_group = GROUP * tiles_n;
   const int group_id = t / per_group;
   const int first_m = group_id * GROUP;
@@ -378,7 +387,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     // bf16: a K-tile is 64 elements; fp8: 128 (the same 128 bytes per row, so the LDS images are identical)
     constexpr int EB = FP8 ? 1 : 2;                 // bytes per element
     constexpr int TK = FP8 ? 128 : BK;              // K elements per tile
-    const int nk = (d.K + TK - 1) / TK;
+    const int nk = (Kloop + TK - 1) / TK;
     using Z = std::integral_constant<int, 0>;
     using O = std::integral_constant<int, 1>;
     // Per-lane 32-bit byte offsets of the 4 units' source rows (2 LDS-DMA instructions each) from a wave-uniform
@@ -408,11 +417,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
           const int c = (lane & 7) ^ swz(r);
           if (u < 2) {
             // 64-bit tile base + 32-bit in-tile offset (M * lda can pass 2^31 bytes: FF2 at config 5)
-            ubase[u][i] = (const char*)d.A + (int64_t)m0 * d.lda * EB;
+            ubase[u][i] = (const char*)d.A + ((int64_t)m0 * d.lda + kbeg) * EB;
             uoff[u][i] = (min(m0 + r, d.M - 1) - m0) * (int)d.lda * EB + c * 16;
           } else {
             const int sg = __builtin_amdgcn_readfirstlane(min(n0 + rb, d.N - 1) / d.n_seg);
-            ubase[u][i] = (const char*)d.W[sg];
+            ubase[u][i] = (const char*)d.W[sg] + (int64_t)kbeg * EB;
             uoff[u][i] = ((min(n0 + r, d.N - 1) - sg * d.n_seg) * d.K) * EB + c * 16;
           }
         }
@@ -712,6 +721,19 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     }
   }
 
+  if constexpr (SPLIT) {
+    // fp32 partial tile: lane (j, i) holds 4 consecutive columns of one row (16-byte stores)
+    float* P = mx.ws + (int64_t)kc * d.M * d.N;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wr * WM + i * 16 + (lane & 15);
+        const int n = n0 + wc * WN + j * 16 + (lane >> 4) * 4;
+        if (m < d.M && n < d.N) *(f32x4*)(P + (int64_t)m * d.N + n) = acc[j][i];
+      }
+    return;
+  }
 #ifdef VP_GEMM_ABL_NOEPI  // ablation build (tools/gemm_kscan.py): main loop only, accumulators kept live
 #pragma unroll
   for (int j = 0; j < FN; ++j)
@@ -722,6 +744,73 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 #endif
 }
 
+
+// split-K reduce + epilogue: one thread per 8 consecutive output columns of one row; the chunks are summed in a fixed
+// order, then the same roundings as the fused epilogues (epi_values + epi_rows_out)
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const vp_gemm_desc d, const float* __restrict__ ws,
+                                                                 int nsplit) {
+  const int c8 = d.N >> 3;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)d.M * c8) return;
+  const int m = (int)(idx / c8);
+  const int n = (int)(idx - (int64_t)m * c8) * 8;
+  float a[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = 0.f;
+  const int64_t MN = (int64_t)d.M * d.N;
+  for (int s = 0; s < nsplit; ++s) {
+    const float* p = ws + s * MN + (int64_t)m * d.N + n;
+    const f32x4 lo = *(const f32x4*)p, hi = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] += lo[e];
+      a[4 + e] += hi[e];
+    }
+  }
+  const int sg = (int)(n >= d.n_seg) + (int)(n >= 2 * d.n_seg);
+  const bf16* bp = (const bf16*)d.bias[sg];
+  const int grp = m / d.rows_per_group, gin = m - grp * d.rows_per_group;
+  const int64_t orow = (int64_t)grp * d.group_stride + d.row_offset + gin;
+  bf16x8 o;
+  bf16x8 pv;
+  if (d.epilogue == VP_EPI_BIAS_ADDROWS)
+    pv = *(const bf16x8*)((const bf16*)d.addrows + (int64_t)(gin + d.addrows_offset) * d.addrows_ld + n);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float v = rbf(a[e] + (bp != nullptr ? bf2f(bp[n + e - sg * d.n_seg]) : 0.f));
+    if (d.epilogue == VP_EPI_BIAS_GELU) v = rbf(gelu_tanh(v));
+    else if (d.epilogue == VP_EPI_BIAS_SCALE) v = rbf(v * d.alpha);
+    else if (d.epilogue == VP_EPI_BIAS_ADDROWS) v = bf2f(f2bf(v)) + bf2f(pv[e]);
+    o[e] = f2bf(v);
+  }
+  *(bf16x8*)((bf16*)d.C + orow * d.ldc + n) = o;
+}
+
+// split-K plan: only when fewer than half the CUs would get a tile, whole 512-K chunks (the staggered main loop's
+// minimum), at most one round of workgroups
+struct SplitPlan {
+  int nsplit = 1, kchunk = 0;
+  int64_t ws_bytes = 0;
+};
+SplitPlan split_plan(const vp_gemm_desc* d) {
+  SplitPlan p;
+  const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
+  const bool epi_ok = d->epilogue == VP_EPI_BIAS || d->epilogue == VP_EPI_BIAS_GELU ||
+                      d->epilogue == VP_EPI_BIAS_SCALE || d->epilogue == VP_EPI_BIAS_ADDROWS;
+  if (!epi_ok || tiles >= 128 || (d->K % BK) != 0 || d->K < 1024) return p;
+  const int64_t tile_a = (int64_t)BM * d->lda * 2, wseg = (int64_t)d->n_seg * d->K * 2;
+  if (tile_a >= ((int64_t)1 << 31) || wseg >= ((int64_t)1 << 31)) return p;
+  // the fp32 partials (nsplit x M x N x 4 B, written and read back) should not outweigh the weights (N x K x 2 B)
+  int ns = min(min(256 / tiles, d->K / 512), max(2, d->K / (2 * d->M)));
+  if (ns < 2) return p;
+  const int kt = d->K / BK;
+  const int chunk_t = (kt + ns - 1) / ns;
+  p.kchunk = chunk_t * BK;
+  p.nsplit = (kt + chunk_t - 1) / chunk_t;
+  if (p.nsplit < 2 || d->K - (p.nsplit - 1) * p.kchunk < 8 * BK) return SplitPlan{};  // last chunk >= 8 K-tiles
+  p.ws_bytes = (int64_t)p.nsplit * d->M * d->N * 4;
+  return p;
+}
 
 }  // namespace
 
@@ -765,11 +854,8 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
       if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr_set = true;
   }
-  static const int env_variant = [] {
-    const char* e = getenv("VP_GEMM_VARIANT");
-    return e != nullptr ? atoi(e) : 11;
-  }();
-  int variant = env_variant;
+  const char* e = getenv("VP_GEMM_VARIANT");  // read per call: tests switch it between launches
+  int variant = e != nullptr ? atoi(e) : 11;
   if (variant != 1 && variant != 5 && variant != 11) variant = 11;
   // the quadrant pipeline adds 32-bit in-tile source offsets to a 64-bit tile base (A) / segment base (W)
   const bool w32 = (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
@@ -787,6 +873,44 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   } else {
     hipLaunchKernelGGL(gemm_bf16_kernel<1>, dim3(tiles), dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
   }
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int64_t vp_gemm_bf16_workspace_bytes(const vp_gemm_desc* d) {
+  if (d == nullptr) return -1;
+  return split_plan(d).ws_bytes;
+}
+
+extern "C" int vp_gemm_bf16_ws(const vp_gemm_desc* d, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (d == nullptr) return VP_ERR_ARG;
+  const SplitPlan p = split_plan(d);
+  if (p.nsplit < 2) return vp_gemm_bf16(d, stream);
+  if (workspace == nullptr || workspace_bytes < p.ws_bytes || ((uintptr_t)workspace & 15) != 0) return VP_ERR_ARG;
+  // the same argument checks as the unsplit launch (a zero-tile dry run is not possible: validate by hand)
+  if (d->A == nullptr || d->W[0] == nullptr || d->C == nullptr || d->M <= 0 || d->N <= 0 || (d->N % 8) != 0 ||
+      d->lda < d->K || d->ldc < d->N || (d->lda % 8) != 0 || (d->ldc % 8) != 0 || d->rows_per_group <= 0)
+    return VP_ERR_ARG;
+  const int nsegs = d->W[2] ? 3 : (d->W[1] ? 2 : 1);
+  if (d->n_seg <= 0 || d->n_seg * nsegs != d->N) return VP_ERR_ARG;
+  if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    attr_set = true;
+  }
+  MxExt mx = {};
+  mx.ws = (float*)workspace;
+  mx.kchunk = p.kchunk;
+  mx.nsplit = p.nsplit;
+  const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS, true>), dim3(tiles * p.nsplit), dim3(NTHREADS),
+                     LDS_BYTES, (hipStream_t)stream, *d, mx);
+  VP_CHECK_LAUNCH();
+  const int64_t work = (int64_t)d->M * (d->N / 8);
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, *d, (const float*)workspace, p.nsplit);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }

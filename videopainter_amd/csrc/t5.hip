@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void mul_kernel(const bf16* __restrict__ a, co
 // padded to 66 elements: the score pass reads one key row per lane), 4 waves x QW queries per block.
 // scores = bf16(q.k) (the reference's bf16 matmul output) + bias (bf16 add), softmax in fp32 -> bf16 weights,
 // out = bf16(sum_j w_j v_j) with fp32 accumulation; masked keys (mask[b, j] == 0) get the dtype minimum added.
-constexpr int T5_MAX_L = 512;
+constexpr int T5_MAX_L = 384;  // LDS: K + V + QW weight rows per wave <= 160 KB
 constexpr int QW = 8;  // queries per wave
 constexpr int KROW = 66;
 
@@ -75,7 +75,9 @@ __global__ __launch_bounds__(256) void t5_attention_kernel(const bf16* __restric
   const int Lp = (L + 7) & ~7;                 // 16-byte aligned sub-arrays
   bf16* Ks = (bf16*)smem;                       // [Lp][KROW]
   bf16* Vs = Ks + Lp * KROW;                    // [Lp][64]
-  float* Ps = (float*)(Vs + Lp * 64);           // [4 waves][Lp]
+  float* Bs = (float*)(Vs + Lp * 64);           // [2 Lp]: the head's bias by relative position j - q + L - 1
+  float* Ms = Bs + 2 * Lp;                      // [Lp]: 1 where the key is masked
+  bf16* Ps = (bf16*)(Ms + Lp);                  // [4 waves][QW][Lp]: softmax weights (bf16-rounded values)
   const int nqb = (L + 4 * QW - 1) / (4 * QW);
   const int bh = blockIdx.x / nqb, qb = blockIdx.x - bh * nqb;
   const int b = bh / H, h = bh - b * H;
@@ -89,11 +91,25 @@ __global__ __launch_bounds__(256) void t5_attention_kernel(const bf16* __restric
     for (int e = 0; e < 8; ++e) Ks[j * KROW + c * 8 + e] = kv[e];
     *(bf16x8*)(Vs + j * 64 + c * 8) = vv;
   }
+  // the bucket of (q, j) depends only on j - q (bidirectional T5 buckets): row 0 of the bucket matrix holds
+  // j - q >= 0, column 0 holds j - q <= 0
+  for (int r = tid; r < 2 * L - 1; r += 256) {
+    const int rel = r - (L - 1);
+    const int bk = rel >= 0 ? buckets[rel] : buckets[(int64_t)(-rel) * L];
+    Bs[r] = bf2f(bias_table[bk * H + h]);
+  }
+  for (int j = tid; j < L; j += 256) Ms[j] = (mask != nullptr && mask[(int64_t)b * L + j] == 0) ? 1.f : 0.f;
   __syncthreads();
-  float* P = Ps + wave * Lp;
+  // phase 1, per query of this wave: scores, softmax, the bf16-rounded weights into P[qi][:]; phase 2: one pass over
+  // the keys accumulates all QW queries at once (V row read once per key, QW independent FMA chains; the per-query
+  // serial chain over L keys was latency-bound), in the same key order as before
+  bf16* P = Ps + wave * QW * Lp;
+  int nq = 0;
   for (int qi = 0; qi < QW; ++qi) {
     const int q = (qb * 4 + wave) * QW + qi;
     if (q >= L) break;  // wave-uniform
+    ++nq;
+    bf16* Pq = P + qi * Lp;
     const bf16* qrow = base + (int64_t)q * ld + h * 64;
     float qv[64];
 #pragma unroll
@@ -103,7 +119,13 @@ __global__ __launch_bounds__(256) void t5_attention_kernel(const bf16* __restric
       for (int e = 0; e < 8; ++e) qv[c * 8 + e] = bf2f(v[e]);
     }
     float mx = -INFINITY;
-    for (int j = lane; j < L; j += 64) {
+    float sv[T5_MAX_L / 64];  // this lane's scores (register-resident: fully unrolled indices)
+#pragma unroll
+    for (int i = 0; i < T5_MAX_L / 64; ++i) sv[i] = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < T5_MAX_L / 64; ++i) {
+      const int j = lane + 64 * i;
+      if (j >= L) break;
       float s = 0.f;
       const bf16* kr = Ks + j * KROW;
 #pragma unroll
@@ -112,27 +134,44 @@ __global__ __launch_bounds__(256) void t5_attention_kernel(const bf16* __restric
         s = __builtin_fmaf(qv[e], bf2f(k2[0]), s);
         s = __builtin_fmaf(qv[e + 1], bf2f(k2[1]), s);
       }
-      float sc = rbf(rbf(s) + bf2f(bias_table[buckets[q * L + j] * H + h]));
-      if (mask != nullptr && mask[(int64_t)b * L + j] == 0) sc = rbf(sc + -3.3895313892515355e38f);
-      P[j] = sc;
+      float sc = rbf(rbf(s) + Bs[j - q + L - 1]);
+      if (Ms[j] != 0.f) sc = rbf(sc + -3.3895313892515355e38f);
+      sv[i] = sc;  // this lane's keys j = lane + 64 i
       mx = fmaxf(mx, sc);
     }
     mx = wave_max(mx);
     float sum = 0.f;
-    for (int j = lane; j < L; j += 64) {
-      const float e = __expf(P[j] - mx);
-      P[j] = e;
-      sum += e;
+#pragma unroll
+    for (int i = 0; i < T5_MAX_L / 64; ++i) {
+      const int j = lane + 64 * i;
+      if (j < L) {
+        sv[i] = __expf(sv[i] - mx);
+        sum += sv[i];
+      }
     }
     sum = wave_sum(sum);
     const float inv = 1.f / sum;
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-    // out[d = lane] = sum_j bf16(p_j / sum) v_j[d]
-    float acc = 0.f;
-    for (int j = 0; j < L; ++j) acc = __builtin_fmaf(rbf(P[j] * inv), bf2f(Vs[j * 64 + lane]), acc);
-    out[(int64_t)(b * L + q) * ldo + h * 64 + lane] = f2bf(acc);
-    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < T5_MAX_L / 64; ++i) {
+      const int j = lane + 64 * i;
+      if (j < L) Pq[j] = f2bf(sv[i] * inv);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  // out[q][d = lane] = sum_j w_qj v_j[d]
+  float acc[QW];
+#pragma unroll
+  for (int qi = 0; qi < QW; ++qi) acc[qi] = 0.f;
+  for (int j = 0; j < L; ++j) {
+    const float v = bf2f(Vs[j * 64 + lane]);
+#pragma unroll
+    for (int qi = 0; qi < QW; ++qi) acc[qi] = __builtin_fmaf(bf2f(P[qi * Lp + j]), v, acc[qi]);
+  }
+#pragma unroll
+  for (int qi = 0; qi < QW; ++qi) {
+    const int q = (qb * 4 + wave) * QW + qi;
+    if (qi < nq) out[(int64_t)(b * L + q) * ldo + h * 64 + lane] = f2bf(acc[qi]);
   }
 }
 
@@ -177,10 +216,10 @@ extern "C" int vp_t5_attention_bf16(const void* qkv, int64_t ld, int32_t inner, 
   if (B <= 0 || L <= 0 || H <= 0 || inner != H * 64 || ld < 3 * inner || (ld % 8) || ldo < inner) return VP_ERR_ARG;
   if (L > T5_MAX_L) return VP_ERR_UNSUPPORTED;
   const size_t Lp = (size_t)((L + 7) & ~7);
-  const size_t lds = Lp * KROW * 2 + Lp * 64 * 2 + 4 * Lp * 4;
+  const size_t lds = Lp * KROW * 2 + Lp * 64 * 2 + 3 * Lp * 4 + 4 * QW * Lp * 2;
   static bool attr = false;
   if (!attr) {
-    const size_t mx = (size_t)T5_MAX_L * (KROW * 2 + 64 * 2 + 16);
+    const size_t mx = (size_t)T5_MAX_L * (KROW * 2 + 64 * 2 + 12 + 8 * QW);
     (void)hipFuncSetAttribute((const void*)t5_attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mx);
     attr = true;
   }

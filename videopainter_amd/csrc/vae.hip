@@ -537,11 +537,8 @@ int launch_conv(const vp_conv3d_desc& d, int c8s, int64_t tiles, hipStream_t s) 
     attr = true;
   }
   // VP_CONV_HOIST=0 keeps the per-K-tile tap decode (A/B)
-  static const int hoist_env = [] {
-    const char* e = getenv("VP_CONV_HOIST");
-    return e != nullptr ? atoi(e) : 1;
-  }();
-  if (d.Cin >= 64 && hoist_env != 0)
+  const char* he = getenv("VP_CONV_HOIST");
+  if (d.Cin >= 64 && (he == nullptr || atoi(he) != 0))
     hipLaunchKernelGGL((conv3d_kernel<BN, true>), dim3((unsigned)tiles), dim3(CNT), G::LDS, s, d, c8s);
   else
     hipLaunchKernelGGL((conv3d_kernel<BN, false>), dim3((unsigned)tiles), dim3(CNT), G::LDS, s, d, c8s);

@@ -157,8 +157,16 @@ def gemm(a: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[Opti
     if epilogue == N.EPI_BIAS_ADDROWS:
         _chk(addrows, "addrows")
         d.addrows, d.addrows_ld, d.addrows_offset = _p(addrows), _rowmajor(addrows, "addrows"), addrows_offset
+    L = N.lib()
+    # split-K for GEMMs too small to fill the chip (e.g. T5 at 2 x 226 rows): fp32 partials from the caching
+    # allocator, so they are ordered on the launch stream
+    nb = L.vp_gemm_bf16_workspace_bytes(C.byref(d))
     ev = _t0("gemm")
-    N.check(N.lib().vp_gemm_bf16(C.byref(d), _stream()), "vp_gemm_bf16")
+    if nb > 0:
+        ws = torch.empty(nb, device=out.device, dtype=torch.uint8)
+        N.check(L.vp_gemm_bf16_ws(C.byref(d), _p(ws), nb, _stream()), "vp_gemm_bf16_ws")
+    else:
+        N.check(L.vp_gemm_bf16(C.byref(d), _stream()), "vp_gemm_bf16")
     _t1("gemm", ev)
     return out
 

@@ -86,6 +86,8 @@ class T5EncoderModel(nn.Module):
             mod.register_parameter(parts[-1], self.shared.weight if key == "encoder.embed_tokens.weight"
                                    else _M._empty(*shape))
         self._buckets: Dict[Tuple[int, str], torch.Tensor] = {}
+        self._graphs_on = False
+        self._graph_cache: Dict[tuple, tuple] = {}
         self._qkv: Dict[int, Tuple[torch.Tensor, ...]] = {}
 
     @property
@@ -166,6 +168,73 @@ class T5EncoderModel(nn.Module):
             self._buckets[key] = b
         return b
 
+    def enable_hip_graphs(self, on: bool = True):
+        """Replay the 24-layer stack as one captured HIP graph per (batch, length, masked) shape: the encoder runs
+        once per prompt at M = B x 226 rows, where the ~220 kernel launches of an eager forward (and their host-side
+        descriptor building) take longer than the kernels themselves.  Same kernels, same results."""
+        self._graphs_on = bool(on)
+        if not on:
+            self._graph_cache.clear()
+        return self
+
+    def _layers(self, h, mask, B: int, L: int, output_hidden_states: bool = False):
+        """The encoder stack on the HIP kernels: h [B*L, d_model] bf16 (consumed in place) -> final-norm output."""
+        cfg = self.config
+        dev = h.device
+        buckets = self._bucket_matrix(L, dev)
+        rab = self._layer(0)._modules["0"].SelfAttention.relative_attention_bias.weight
+        H, eps = cfg.num_heads, cfg.layer_norm_epsilon
+        hidden = [h.view(B, L, -1)] if output_hidden_states else None
+        if hidden is not None:
+            hidden[0] = hidden[0].clone()
+        for i in range(cfg.num_layers):
+            ly = self._layer(i)
+            sa, ff = ly._modules["0"], ly._modules["1"]
+            n = K.rms_norm(h, sa.layer_norm.weight, eps)
+            att = sa.SelfAttention
+            qkv = torch.empty(B * L, 3 * H * 64, device=dev, dtype=torch.bfloat16)
+            K.gemm(n, [att.q.weight, att.k.weight, att.v.weight], [None, None, None], qkv)
+            o = K.t5_attention(qkv, B, L, H, rab, buckets, mask)
+            K.gemm(o, [att.o.weight], [None], h, epilogue=N.EPI_BIAS_ADDROWS, addrows=h)
+            n = K.rms_norm(h, ff.layer_norm.weight, eps)
+            dd = ff.DenseReluDense
+            g = torch.empty(B * L, cfg.d_ff, device=dev, dtype=torch.bfloat16)
+            u = torch.empty_like(g)
+            K.gemm(n, [dd.wi_0.weight], [None], g, epilogue=N.EPI_BIAS_GELU)
+            K.gemm(n, [dd.wi_1.weight], [None], u)
+            K.mul(g, u, out=g)
+            K.gemm(g, [dd.wo.weight], [None], h, epilogue=N.EPI_BIAS_ADDROWS, addrows=h)
+            if hidden is not None:
+                hidden.append(h.view(B, L, -1).clone())
+        y = K.rms_norm(h, self.encoder.final_layer_norm.weight, eps).view(B, L, -1)
+        if hidden is not None:
+            hidden[-1] = y
+        return y, hidden
+
+    def _replay(self, h, mask, B: int, L: int):
+        key = (B, L, mask is not None, str(h.device))
+        ent = self._graph_cache.get(key)
+        if ent is None:
+            s_h = h.clone()
+            s_m = None if mask is None else mask.clone()
+            # warm-up on a side stream (allocator, kernel attributes), then capture
+            side = torch.cuda.Stream(device=h.device)
+            side.wait_stream(torch.cuda.current_stream(h.device))
+            with torch.cuda.stream(side):
+                self._layers(s_h.clone(), s_m, B, L)
+            torch.cuda.current_stream(h.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                s_y, _ = self._layers(s_h, s_m, B, L)
+            ent = (graph, s_h, s_m, s_y)
+            self._graph_cache[key] = ent
+        graph, s_h, s_m, s_y = ent
+        s_h.copy_(h)
+        if s_m is not None:
+            s_m.copy_(mask)
+        graph.replay()
+        return s_y.clone()
+
     def forward(self, input_ids: Optional[torch.Tensor] = None, attention_mask: Optional[torch.Tensor] = None,
                 head_mask=None, inputs_embeds: Optional[torch.Tensor] = None, output_attentions: Optional[bool] = None,
                 output_hidden_states: Optional[bool] = None, return_dict: Optional[bool] = None):
@@ -190,32 +259,10 @@ class T5EncoderModel(nn.Module):
                     raise IndexError("input_ids out of the vocabulary range")
                 h = K.embedding_gather(self.shared.weight, ids)
             mask = None if attention_mask is None else attention_mask.to(dev, torch.int64)
-            buckets = self._bucket_matrix(L, dev)
-            rab = self._layer(0)._modules["0"].SelfAttention.relative_attention_bias.weight
-            H, eps = cfg.num_heads, cfg.layer_norm_epsilon
-            hidden = [h.view(B, L, -1)] if output_hidden_states else None
-            for i in range(cfg.num_layers):
-                ly = self._layer(i)
-                sa, ff = ly._modules["0"], ly._modules["1"]
-                n = K.rms_norm(h, sa.layer_norm.weight, eps)
-                att = sa.SelfAttention
-                qkv = torch.empty(B * L, 3 * H * 64, device=dev, dtype=torch.bfloat16)
-                K.gemm(n, [att.q.weight, att.k.weight, att.v.weight], [None, None, None], qkv)
-                o = K.t5_attention(qkv, B, L, H, rab, buckets, mask)
-                K.gemm(o, [att.o.weight], [None], h, epilogue=N.EPI_BIAS_ADDROWS, addrows=h)
-                n = K.rms_norm(h, ff.layer_norm.weight, eps)
-                dd = ff.DenseReluDense
-                g = torch.empty(B * L, cfg.d_ff, device=dev, dtype=torch.bfloat16)
-                u = torch.empty_like(g)
-                K.gemm(n, [dd.wi_0.weight], [None], g, epilogue=N.EPI_BIAS_GELU)
-                K.gemm(n, [dd.wi_1.weight], [None], u)
-                K.mul(g, u, out=g)
-                K.gemm(g, [dd.wo.weight], [None], h, epilogue=N.EPI_BIAS_ADDROWS, addrows=h)
-                if hidden is not None:
-                    hidden.append(h.view(B, L, -1).clone())
-            y = K.rms_norm(h, self.encoder.final_layer_norm.weight, eps).view(B, L, -1)
-            if hidden is not None:
-                hidden[-1] = y
+            if self._graphs_on and not output_hidden_states:
+                y, hidden = self._replay(h, mask, B, L), None
+            else:
+                y, hidden = self._layers(h, mask, B, L, output_hidden_states)
         out = BaseModelOutput(last_hidden_state=y, hidden_states=tuple(hidden) if hidden is not None else None)
         if return_dict is False:
             return out.to_tuple()
