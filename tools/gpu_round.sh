@@ -21,6 +21,7 @@ for step in "$@"; do
     benchq) run bench 900 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     kbench) run kbench 300 python tools/bench_kernels.py --iters 5 ;;
     prof)   export TMPDIR=/tmp; run prof_trace 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    blasprof) export TMPDIR=/tmp; run blasprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/blasprof -o blas --output-format csv -- python tools/blas_calibration.py --rounds 1 --iters 3 ;;
     pmc)    export TMPDIR=/tmp; run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o attn --output-format csv -- python tools/bench_kernels.py --only attention --iters 2 && run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o attn --output-format csv -- python tools/bench_kernels.py --only attention --iters 2 ;;
   esac
 done
