@@ -602,7 +602,9 @@ VP_DEV float f8_exp_pack(const f32x16 (&s)[2], i32x8& pf) {
       const float p1 = __builtin_amdgcn_exp2f(s[hh][4 * w + 1]);
       const float p2 = __builtin_amdgcn_exp2f(s[hh][4 * w + 2]);
       const float p3 = __builtin_amdgcn_exp2f(s[hh][4 * w + 3]);
-      int pk = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, 0, false);
+      // the low-word pack's "old" operand is p0's own bits (dead after this, so its register becomes the result
+      // in place): its high word is overwritten by the second pack, and a literal 0 there costs a v_mov per VGPR
+      int pk = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, __float_as_int(p0), false);
       pk = __builtin_amdgcn_cvt_pk_fp8_f32(p2, p3, pk, true);
       pf[hh * 4 + w] = pk;
       const float a = (p0 + p1) + (p2 + p3);
@@ -781,9 +783,15 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
         i32x8 pf;
         const float ls = f8_exp_pack(s, pf);
         if constexpr (RS) {
-          int w;
-          asm volatile("v_mov_b32 %0, %1" : "=v"(w) : "v"(selw));  // opaque: keeps the tuple inside the loop
-          const i32x8 sel = {w, w, w, w, w, w, w, w};
+          // opaque copy keeps the tuple inside the loop; built as 64-bit halves so the copies are v_mov_b64
+          uint32_t wlo, whi;
+          asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %2" : "=v"(wlo), "=v"(whi) : "v"(selw));
+          const uint64_t w2 = ((uint64_t)whi << 32) | wlo;
+          uint64_t w3, w4, w5;
+          asm volatile("v_mov_b64 %0, %3\n\tv_mov_b64 %1, %3\n\tv_mov_b64 %2, %3" : "=v"(w3), "=v"(w4), "=v"(w5)
+                       : "v"(w2));
+          typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
+          const i32x8 sel = __builtin_bit_cast(i32x8, (u64x4){w2, w3, w4, w5});
           lsum = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(sel, pf, lsum, 0, 0, 0, 127, 0, 127);
         }
         else
