@@ -133,6 +133,11 @@ def main():
     t = timeit(lambda: K.adaln_modulate(xin, lw, lb, mod, T, 1e-5, out=y), args.iters)
     res["adaln"] = dict(ms=t * 1e3, gbps=2 * xin.numel() * 2 / t / 1e9)
     print("adaln", res["adaln"], flush=True)
+    # the read+write ceiling these one-pass kernels are held to: a plain device-to-device copy of the same bytes
+    # (same dtype and layout, so torch hands it to the runtime's copy), the same 1:1 read:write mix as AdaLN / qk-norm
+    t = timeit(lambda: y.copy_(xin), args.iters)
+    res["copy_d2d"] = dict(ms=t * 1e3, gbps=2 * xin.numel() * 2 / t / 1e9)
+    print("copy roofline", res["copy_d2d"], flush=True)
     cos = torch.randn(Nv, 64, device=dev)
     sin = torch.randn(Nv, 64, device=dev)
     lw64 = torch.ones(64, device=dev, dtype=torch.bfloat16)
