@@ -61,7 +61,8 @@ def attn_flops_per_launch() -> float:
 
 
 def profiled_traffic(kind: str):
-    """Latest committed PMC-derived HBM traffic per launch of kernel class `kind` ("attention" | "gemm"):
+    """Latest committed PMC-derived HBM traffic per launch of kernel class `kind` ("attention" | "attention_fp8" |
+    "gemm"):
     profiles/<round>_<kind>_traffic.json, written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE /
     WRITE_SIZE passes (MI355X_MICROARCH.md §HBM correction)."""
     import glob
@@ -421,7 +422,7 @@ def kernel_classes(tl, n_steps: int, fp8: bool, share: float = 1.0):
     out = {}
     peak_a = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
     a_tf = attn_fl_step / (attn_ms * 1e-3) / 1e12
-    traffic, src = profiled_traffic("attention") if not fp8 else (None, None)
+    traffic, src = profiled_traffic("attention_fp8" if fp8 else "attention")
     out["attention"] = {"kernel": "vp_attention_fwd_%s" % ("fp8" if fp8 else "bf16"), "bound": "mfma",
                         "achieved": a_tf, "peak": peak_a, "unit": "TFLOP/s", "frac": a_tf / peak_a,
                         "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": src,

@@ -138,8 +138,15 @@ def _ref_fp64(q8, k8, vt, vs, npad, Nk, H, q_exp, k_exp):
     o = torch.einsum("bhqk,bhkd->bqhd", p / p.sum(dim=-1, keepdim=True), vd)
     return o.reshape(B, Nq, H * 64)
 
+@pytest.fixture(params=["1", "2"], ids=["exp2", "lin"])
+def attn8_variant(request, monkeypatch):
+    """VP_ATTN8_VARIANT: 1 = P by v_exp_f32 + RNE e4m3 pack, 2 = P by linear mantissa interpolation (default)."""
+    monkeypatch.setenv("VP_ATTN8_VARIANT", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("B,H,N,late", [(2, 3, 300, False), (1, 2, 2000, True), (1, 1, 65, False)])
-def test_attention_fp8(B, H, N, late):
+def test_attention_fp8(B, H, N, late, attn8_variant):
     from videopainter_amd import kernels as K
     q, k, v = _attn_case(B, H, N, N, late)
     qd, kd, vd = q.to(dev), k.to(dev), v.to(dev)
@@ -150,8 +157,10 @@ def test_attention_fp8(B, H, N, late):
     out = torch.empty(B, N, H * 64, device=dev, dtype=torch.bfloat16)
     K.attention_fp8(q8, k8, vp, out, H, q_exp, k_exp)
     ref = _ref_fp64(q8, k8, vp.vt, vp.vs, vp.npad, N, H, q_exp, k_exp)
-    # the kernel's own error on top of the operand quantisation: P rounded to e4m3 (2^-4 relative) — on random
-    # data ~2-3 % of the (cancelling) output; a wrong key/slot permutation would give ~100 %
+    # the kernel's own error on top of the operand quantisation: P rounded to e4m3 (2^-4 relative; the linear
+    # codes 3.2 % rms against 2.7 %) — on random data ~2-3 % of the (cancelling) output; a wrong key/slot
+    # permutation would give ~100 %
+    print(f"fp8 attention variant {attn8_variant} B={B} H={H} N={N}: rel vs fp64 {rel(out, ref):.3e}")
     assert rel(out, ref) < 4e-2
     # against the bf16 kernel on the un-quantised operands: the fp8 error band
     o16 = torch.empty_like(out)
@@ -185,7 +194,7 @@ def _sdpa_fp32_chunked(q, k, v, H, scale=0.125, chunk=4096):
     return out
 
 
-def test_attention_fp8_and_bf16_at_config5_length():
+def test_attention_fp8_and_bf16_at_config5_length(attn8_variant):
     """BASELINE config 5's sequence length (N = 226 + 46 800 = 47 026) on two heads, LayerNorm-shaped q / k (what
     the qk-norm feeds the kernel): the fp8 kernel against fp32 attention on the same bf16 operands (re-stated fp8
     band: 6e-2 — P in e4m3 keeps 3 mantissa bits), and both bf16 kernels (running max / bounded scores) within
@@ -214,5 +223,5 @@ def test_attention_fp8_and_bf16_at_config5_length():
     o8 = torch.empty(B, N, H * 64, device=dev, dtype=torch.bfloat16)
     K.attention_fp8(q8, k8, vp, o8, H, q_exp, k_exp)
     r8 = rel(o8, ref)
-    print(f"fp8 attention at N={N}: rel vs fp32 {r8:.3e}")
+    print(f"fp8 attention (variant {attn8_variant}) at N={N}: rel vs fp32 {r8:.3e}")
     assert r8 < 6e-2

@@ -38,15 +38,17 @@ def main():
     ap.add_argument("--variant8", default="", help="fp8 attention kernel variant(s) (VP_ATTN8_VARIANT), e.g. 1,2")
     ap.add_argument("--only", default="", help="attention | attn8 | gemm | mx | norms: run just that kernel (for rocprofv3 "
                     "--pmc passes; attn8 = the fp8 attention only)")
+    ap.add_argument("--video-tokens", type=int, default=17550,
+                    help="video tokens per clip (17550 = config 2's 49f 480x720; 46800 = config 5's 49f 720x1280)")
     args = ap.parse_args()
     dev = "cuda"
-    B, T, Nv, D, H = 2, 226, 17550, 3072, 48
+    B, T, Nv, D, H = 2, 226, args.video_tokens, 3072, 48
     Ntok = T + Nv
     M = B * Ntok
     res = {}
     x = torch.randn(M, 4 * D, device=dev).to(torch.bfloat16)
     shapes = [("qkv", 3 * D, D), ("out", D, D), ("ff1", 4 * D, D), ("ff2", D, 4 * D)]
-    if args.only in ("attention", "norms"):
+    if args.only in ("attention", "attn8", "norms"):
         shapes = []
     if args.only == "mx":
         # MX-FP8 FeedForward GEMMs (BASELINE config 5 path) next to their bf16 versions, interleaved

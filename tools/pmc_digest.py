@@ -2,6 +2,7 @@
 per-dispatch counter means for the GEMM / attention kernels and the derived figures DESIGN.md quotes.
 
     python tools/pmc_digest.py --round r02 --gemm gpurun_out/pmc_gemm_v11 --attn gpurun_out/pmc_attn_vbounded
+    python tools/pmc_digest.py --round r02 --merge --attn8 gpurun_out/pmc_attn8   (tools/pmc_attn8.sh, config-5 shape)
 
 mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): GRBM_GUI_ACTIVE sums the 8 XCDs, so
 GRBM_GUI_ACTIVE / 8 is the kernel's cycle count at the clock the chip held (MI355X_MICROARCH.md, DVFS give-back)."""
@@ -53,10 +54,15 @@ def main():
     ap.add_argument("--round", default="r02")
     ap.add_argument("--gemm", default="")
     ap.add_argument("--attn", default="")
+    ap.add_argument("--attn8", default="", help="fp8 attention passes (tools/pmc_attn8.sh: config-5 shape)")
+    ap.add_argument("--merge", action="store_true", help="add to the round's existing summary instead of replacing it")
     a = ap.parse_args()
-    res = {"source": "rocprofv3 --pmc passes on tools/bench_kernels.py (config-2 shapes, random data), separate "
-                     "runs per counter set; per-dispatch means", "kernels": {}}
-    for d, kind in ((a.gemm, "gemm"), (a.attn, "attention")):
+    path = os.path.join(ROOT, "profiles", f"{a.round}_pmc_summary.json")
+    res = {"source": "rocprofv3 --pmc passes on tools/bench_kernels.py (config-2 shapes, random data; the fp8 "
+                     "attention at config-5 shape), separate runs per counter set; per-dispatch means", "kernels": {}}
+    if a.merge and os.path.exists(path):
+        res["kernels"] = json.load(open(path))["kernels"]
+    for d, kind in ((a.gemm, "gemm"), (a.attn, "attention"), (a.attn8, "attention")):
         if not d:
             continue
         for (name, grid), c in load(d).items():
@@ -66,7 +72,6 @@ def main():
                 continue
             label = f"{name} grid {grid}" + (f" ({GEMM_GRIDS[grid]})" if kind == "gemm" and grid in GEMM_GRIDS else "")
             res["kernels"][label] = {"derived": derived(c), "counters": {k: round(v) for k, v in c.items()}}
-    path = os.path.join(ROOT, "profiles", f"{a.round}_pmc_summary.json")
     with open(path, "w") as f:
         json.dump(res, f, indent=1)
     for k, v in res["kernels"].items():

@@ -613,6 +613,30 @@ VP_DEV float f8_exp_pack(const f32x16 (&s)[2], i32x8& pf) {
   return (ps[0] + ps[1]) + (ps[2] + ps[3]);
 }
 
+// LIN: P in e4m3 by linear mantissa interpolation, one VALU op per score instead of v_exp_f32 (8 issue cycles) plus
+// half a v_cvt_pk_fp8_f32.  The e4m3 code of a positive value 2^x is I = 8 (x + 7) at every power of two (exponent
+// field E = floor(x) + 7, mantissa field M = 8 (2^frac(x) - 1) ~ 8 frac(x)), so with the scores pre-scaled by 8
+// (Q's MFMA scale byte + 3) and C-initialised to LIN_C0 - 8 m, the accumulator holds 8 (s - m + OFF) + 56 - delta
+// and v_cvt_pk_u8_f32 (round to nearest, clamp to [0, 255]) writes the code straight into the packed P^T operand.
+// Interpolating 2^frac linearly instead of rounding 2^frac to 3 bits: relative error of P 3.2 % rms against
+// 2.7 % for exp2 + RNE (delta = 0.45 centres it; 8.3 % vs 5.9 % worst case), and the row sums are taken over the
+// same codes, so O = sum P V / sum P keeps the bias out.  Codes stay <= 8 (OFF + THR) + 56 = 124 < 0x7F (NaN)
+// because the max path still runs every tile; masked (-inf) scores and anything below code 0 clamp to P = 0.
+constexpr float LIN_DELTA = 0.45f;
+
+VP_DEV void f8_lin_pack(const f32x16 (&s)[2], i32x8& pf) {
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      unsigned pk = __builtin_amdgcn_cvt_pk_u8_f32(s[hh][4 * w + 0], 0, 0u);
+      pk = __builtin_amdgcn_cvt_pk_u8_f32(s[hh][4 * w + 1], 1, pk);
+      pk = __builtin_amdgcn_cvt_pk_u8_f32(s[hh][4 * w + 2], 2, pk);
+      pk = __builtin_amdgcn_cvt_pk_u8_f32(s[hh][4 * w + 3], 3, pk);
+      pf[hh * 4 + w] = (int)pk;
+    }
+}
+
 // The kernel.  P is stored as p * 2^7 with the max path every tile and rescale threshold 1.5 (P <= 2^8.5 < 448).
 // RS: the row sums on the matrix pipe instead of 28 VALU adds per lane and tile — the packed P^T operand read as the
 // B operand of ONE v_mfma_scale_f32_16x16x128_f8f6f4 (lane l: column l % 16, K-chunks l / 16 and l / 16 + 4), whose
@@ -621,11 +645,15 @@ VP_DEV float f8_exp_pack(const f32x16 (&s)[2], i32x8& pf) {
 // sum(query n + 16) in row 1, i.e. in lane n's registers 0 and 1.  (The sum is then over the e4m3-ROUNDED P the PV
 // product uses, in fp32.)  At d = 64 the softmax VALU (32 exp2 at 8 cycles + max + pack) outweighs the tile's 4
 // MFMAs (256 cycles), so moving 112 VALU cycles onto a 32-cycle MFMA is the lever.
-template <int NW, int OCC, int SUB, bool RS>
+template <int NW, int OCC, int SUB, bool RS, bool LIN>
 __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_desc dd) {
   static_assert(NW == 8, "the DMA split assumes 8 waves");
+  static_assert(RS || !LIN, "the linear codes are summed on the matrix pipe");
   constexpr int OFF = 7;        // P is stored as p * 2^OFF
   constexpr float THR = 1.5f;   // max path: P <= 2^(OFF + THR) < 448
+  // accumulator units: S = LS (s - m) + C0 (log2 units + OFF for the exp2 form, e4m3 codes for LIN)
+  constexpr float LS = LIN ? 8.f : 1.f;
+  constexpr float C0 = LIN ? 8.f * OFF + 56.f - LIN_DELTA : (float)OFF;
   const vp_attn_desc& d = dd.base;
   constexpr int QB = NW * 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -651,18 +679,20 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
     hq[0] = *(const u32x4*)(qrow + g * 16);
     hq[1] = *(const u32x4*)(qrow + (g + 2) * 16);
   }
-  const int sq = dd.qk_scale & 0xff, sk = (dd.qk_scale >> 8) & 0xff;
+  const int sq = (dd.qk_scale & 0xff) + (LIN ? 3 : 0), sk = (dd.qk_scale >> 8) & 0xff;  // LIN: scores x 8
 
   // DMA: this lane's row of its wave's piece (16 rows x 64 B) and the logical source chunk of its physical chunk,
   // held as ONE byte offset per lane (waves 0-3 stage K, 4-7 stage V^T) from a wave-uniform base that advances by
   // whole tiles; only the last K tile (rows past Nk re-read the last key) recomputes the row from the lane id.  More
   // long-lived address VGPRs get spilled at 128, and the spill reload's vmcnt(0) sits in front of the DMA issue.
   const int ksn = (int)d.k_sn;
-  const int dma = [&] {
-    const int prow = (wave & 3) * 16 + (lane >> 2);
-    const int pch = (lane & 3) ^ swz8(prow);
+  auto dma_off = [&](int ln) {
+    const int prow = (wave & 3) * 16 + (ln >> 2);
+    const int pch = (ln & 3) ^ swz8(prow);
     return wave < 4 ? prow * ksn + pch * 16 : prow * dd.npad + pch * 16;
-  }();
+  };
+  // LIN: recomputed from the lane id at each issue (a few VALU per tile): held across the loop it is spilled
+  const int dma_kept = LIN ? 0 : dma_off(lane);
   const char* kbase = (const char*)d.K + (int64_t)b * d.k_sb + h * 64;
   const char* vtbase = (const char*)d.V + (int64_t)bh * 64 * dd.npad;
   const char* vsbase = (const char*)dd.vs + (int64_t)bh * ntiles * 128;
@@ -676,7 +706,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
       char* slot = smem + ((ti & 1) * SUB + sb) * F8_STAGE;
       if (wave < 4) {
         if (kt * 64 + 64 <= d.Nk) {
-          glds16(kbase + (int64_t)kt * 64 * ksn, dma, slot + wave * 1024);
+          glds16(kbase + (int64_t)kt * 64 * ksn, LIN ? dma_off(lane_id_opaque()) : dma_kept, slot + wave * 1024);
         } else {  // rows past the end re-read the last key (masked later)
           const int ln = lane_id_opaque();
           const int prow = (wave & 3) * 16 + (ln >> 2);
@@ -684,7 +714,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
           glds16(kbase, r * ksn + (((ln & 3) ^ swz8(prow)) << 4), slot + wave * 1024);
         }
       } else {
-        glds16(vtbase + kt * 64, dma, slot + F8_TILE + (wave - 4) * 1024);
+        glds16(vtbase + kt * 64, LIN ? dma_off(lane_id_opaque()) : dma_kept, slot + F8_TILE + (wave - 4) * 1024);
       }
       if (wave == 0 && lane < 8) glds16(vsbase + kt * 128, lane * 16, slot + 2 * F8_TILE);
     }
@@ -700,7 +730,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
   for (int i = 0; i < 16; ++i) {
     o[0][i] = 0.f;
     o[1][i] = 0.f;
-    negm[i] = (float)OFF;
+    negm[i] = C0;
   }
   // RS: this lane's selector word (e4m3 1.0 = 0x38) and the 16x16 accumulator of the row sums.  The 8-VGPR
   // selector tuple is re-materialised from the word next to each row-sum MFMA (after the scores died), not kept
@@ -756,7 +786,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
         for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
         {
           const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-          mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) - (float)OFF;
+          mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) - C0;
+          if constexpr (LIN) mx *= 1.f / LS;
         }
         if (__ballot(mx > thr) != 0ull) {
           const float dm = mx > thr ? mx : 0.f;
@@ -774,14 +805,18 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
           for (int i = 0; i < 16; ++i) {
             o[0][i] *= alpha;
             o[1][i] *= alpha;
-            s[0][i] -= dm;
-            s[1][i] -= dm;
-            negm[i] = (float)OFF - m_run;
+            s[0][i] -= LS * dm;
+            s[1][i] -= LS * dm;
+            negm[i] = C0 - LS * m_run;
           }
           thr = THR;
         }
         i32x8 pf;
-        const float ls = f8_exp_pack(s, pf);
+        float ls = 0.f;
+        if constexpr (LIN) {
+          f8_lin_pack(s, pf);
+        } else
+          ls = f8_exp_pack(s, pf);
         if constexpr (RS) {
           // opaque copy keeps the tuple inside the loop; built as 64-bit halves so the copies are v_mov_b64
           uint32_t wlo, whi;
@@ -985,10 +1020,12 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
     return VP_ERR_ARG;
   if ((int64_t)d.Nk * d.k_sn > 0x7fffffff || (int64_t)64 * dd->npad > 0x7fffffff) return VP_ERR_ARG;
   constexpr int NW = 8;
-  // VP_ATTN8_VARIANT (A/B): 1 = row sums on the VALU, 2 = row sums on the matrix pipe (default); both 128 keys per
-  // barrier at 4 waves/SIMD.  Dropped after round-1 A/B: lazy max (159 VGPRs, spills: 0.21 PF/s), 3 waves/SIMD
-  // (1.01), 64 keys per barrier (1.43 against 1.46).
-  static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, 2, false>, (const void*)attn_fwd_fp8<NW, 4, 2, true>};
+  // VP_ATTN8_VARIANT (A/B): 1 = P by v_exp_f32 + RNE pack, 2 = P by linear mantissa interpolation (LIN, default);
+  // both with the row sums on the matrix pipe, 128 keys per barrier at 4 waves/SIMD.  Dropped after A/B: row sums on
+  // the VALU (1.40 against 1.50 PF/s), lazy max (159 VGPRs, spills: 0.21 PF/s), 3 waves/SIMD (1.01), 64 keys per
+  // barrier (1.43 against 1.46).
+  static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, 2, true, false>,
+                                    (const void*)attn_fwd_fp8<NW, 4, 2, true, true>};
   static bool attr_set = false;
   if (!attr_set) {
     attr_set = true;
