@@ -176,19 +176,33 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
       for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
         for (int r = 0; r < 4; ++r) bv[4 * jj + r] = bp != nullptr ? bf2f(bp[hc + 16 * jj + 4 * g + r]) : 0.f;
+      // the LayerNorm weight / bias quads once per head; per row fragment the RoPE quads are loaded (from row 0 for
+      // text tokens, then not applied) before the reductions, so no load sits on the fragment's critical path
+      bf16x4 lw4[4], lb4[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        lw4[jj] = *(const bf16x4*)((const bf16*)d.qk_ln_w[sgh] + 16 * jj + 4 * g);
+        lb4[jj] = *(const bf16x4*)((const bf16*)d.qk_ln_b[sgh] + 16 * jj + 4 * g);
+      }
+      const bool has_rope = d.rope_cos != nullptr;
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         int tok = tok0 + wr * WM + i * 16 + (lane & 15);
         while (tok >= d.tokens_per_batch) tok -= d.tokens_per_batch;
-        const bool rot = d.rope_cos != nullptr && tok >= d.text_len;
-        const int64_t ro = (int64_t)(tok - d.text_len) * 64;
+        const bool rot = has_rope && tok >= d.text_len;
+        const int64_t ro = rot ? (int64_t)(tok - d.text_len) * 64 : 0;
+        f32x4 cs[4], sn[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          cs[jj] = has_rope ? *(const f32x4*)(d.rope_cos + ro + 16 * jj + 4 * g) : (f32x4){1.f, 1.f, 1.f, 1.f};
+          sn[jj] = has_rope ? *(const f32x4*)(d.rope_sin + ro + 16 * jj + 4 * g) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
         float x[16];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
           for (int r = 0; r < 4; ++r) x[4 * jj + r] = rbf(acc[hh * 4 + jj][i][r] + bv[4 * jj + r]);
-        ln64_rope16<16, 32>(x, g, (const bf16*)d.qk_ln_w[sgh], (const bf16*)d.qk_ln_b[sgh], d.qk_eps[sgh],
-                            rot ? d.rope_cos + ro : nullptr, rot ? d.rope_sin + ro : nullptr);
+        ln64_rope16_regs<16, 32>(x, lw4, lb4, d.qk_eps[sgh], cs, sn, rot);
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           bf16x4 o;

@@ -44,17 +44,32 @@ VP_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
 // / centred variance, rstd = rsqrt(var + eps)), bf16 output (torch LayerNorm on bf16,
 // attention_processor.py:2143-2154), then when cr / sr are given (video tokens) the interleaved-pair rotation in
 // fp32 of the bf16 values, x * cos + rot(x) * sin (embeddings.py:655-701, apply_rotary_emb).
+// s + (s of the lane xor X): 16 / 32 by a permlane swap (VALU: the pair {own, partner} in either order, and the
+// f32 add is commutative, so the sum is the same bits as with the shuffle), other distances by __shfl_xor
+template <int X>
+VP_DEV float add_partner(float v) {
+  if constexpr (X == 16 || X == 32) {
+    const unsigned u = __float_as_uint(v);
+    const auto sw = X == 16 ? __builtin_amdgcn_permlane16_swap(u, u, false, false)
+                            : __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  } else {
+    return v + __shfl_xor(v, X, 64);
+  }
+}
+
+// the arithmetic of ln64_rope16 on operands already in registers (w / bb: the LayerNorm weight / bias quads of
+// columns 16 j + 4 g, cs / sn: the RoPE cos / sin quads; rot: apply the rotation)
 template <int X1, int X2>
-VP_DEV void ln64_rope16(float (&x)[16], int g, const bf16* __restrict__ lw, const bf16* __restrict__ lb, float eps,
-                        const float* __restrict__ cr, const float* __restrict__ sr) {
+VP_DEV void ln64_rope16_regs(float (&x)[16], const bf16x4 (&w)[4], const bf16x4 (&bb)[4], float eps,
+                             const f32x4 (&cs)[4], const f32x4 (&sn)[4], bool rot) {
   // every multiply-add spelled out (fma or not) and no contraction: otherwise hipcc fuses differently in different
   // surroundings (SLP-packed v_pk_mul + v_add in one kernel, v_fmac in another) and the two users drift by an ulp
 #pragma clang fp contract(off)
   float s = 0.f;
 #pragma unroll
   for (int e = 0; e < 16; ++e) s += x[e];
-  s += __shfl_xor(s, X1, 64);
-  s += __shfl_xor(s, X2, 64);
+  s = add_partner<X2>(add_partner<X1>(s));
   const float mean = s * (1.f / 64.f);
   float q = 0.f;
 #pragma unroll
@@ -62,26 +77,48 @@ VP_DEV void ln64_rope16(float (&x)[16], int g, const bf16* __restrict__ lw, cons
     const float t = x[e] - mean;
     q = __builtin_fmaf(t, t, q);
   }
-  q += __shfl_xor(q, X1, 64);
-  q += __shfl_xor(q, X2, 64);
+  q = add_partner<X2>(add_partner<X1>(q));
   const float rstd = rsqrtf(__builtin_fmaf(q, 1.f / 64.f, eps));
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = 16 * j + 4 * g;
-    const bf16x4 w = *(const bf16x4*)(lw + c);
-    const bf16x4 bb = *(const bf16x4*)(lb + c);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      x[4 * j + r] = rbf(__builtin_fmaf((x[4 * j + r] - mean) * rstd, bf2f(w[r]), bf2f(bb[r])));
-    if (cr != nullptr) {
-      const f32x4 cs = *(const f32x4*)(cr + c), sn = *(const f32x4*)(sr + c);
-      const float x0 = x[4 * j], x1 = x[4 * j + 1], x2 = x[4 * j + 2], x3 = x[4 * j + 3];
-      x[4 * j] = __builtin_fmaf(x0, cs[0], -(x1 * sn[0]));
-      x[4 * j + 1] = __builtin_fmaf(x1, cs[1], x0 * sn[1]);
-      x[4 * j + 2] = __builtin_fmaf(x2, cs[2], -(x3 * sn[2]));
-      x[4 * j + 3] = __builtin_fmaf(x3, cs[3], x2 * sn[3]);
-    }
+      x[4 * j + r] = rbf(__builtin_fmaf((x[4 * j + r] - mean) * rstd, bf2f(w[j][r]), bf2f(bb[j][r])));
+    const float x0 = x[4 * j], x1 = x[4 * j + 1], x2 = x[4 * j + 2], x3 = x[4 * j + 3];
+    const float y0 = __builtin_fmaf(x0, cs[j][0], -(x1 * sn[j][0]));
+    const float y1 = __builtin_fmaf(x1, cs[j][1], x0 * sn[j][1]);
+    const float y2 = __builtin_fmaf(x2, cs[j][2], -(x3 * sn[j][2]));
+    const float y3 = __builtin_fmaf(x3, cs[j][3], x2 * sn[j][3]);
+    x[4 * j] = rot ? y0 : x0;
+    x[4 * j + 1] = rot ? y1 : x1;
+    x[4 * j + 2] = rot ? y2 : x2;
+    x[4 * j + 3] = rot ? y3 : x3;
   }
+}
+
+// norm_q / norm_k + apply_rotary_emb on one 64-wide head spread over 4 lanes (g = the lane's quarter, partners at
+// lane xor X1 and xor X2; the 4 lanes are active together), 16 values each: x[4 j + r] is column 16 j + 4 g + r —
+// the layout of a 16x16 MFMA accumulator row (4 consecutive columns per lane, 4 fragments per head), so the QKV
+// GEMM applies it to its accumulators (X1, X2 = 16, 32) and vp_head_norm_rope_* to loaded rows (X1, X2 = 1, 2)
+// with the same arithmetic in the same order (ln64_rope16_regs): bit-equal.  LayerNorm(64) in fp32 from the bf16
+// inputs (two-pass mean / centred variance, rstd = rsqrt(var + eps)), bf16 output (torch LayerNorm on bf16,
+// attention_processor.py:2143-2154), then when cr / sr are given (video tokens) the interleaved-pair rotation in
+// fp32 of the bf16 values, x * cos + rot(x) * sin (embeddings.py:655-701, apply_rotary_emb).  Every operand is
+// loaded before the reductions, so their latency overlaps them.
+template <int X1, int X2>
+VP_DEV void ln64_rope16(float (&x)[16], int g, const bf16* __restrict__ lw, const bf16* __restrict__ lb, float eps,
+                        const float* __restrict__ cr, const float* __restrict__ sr) {
+  bf16x4 w[4], bb[4];
+  f32x4 cs[4], sn[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = 16 * j + 4 * g;
+    w[j] = *(const bf16x4*)(lw + c);
+    bb[j] = *(const bf16x4*)(lb + c);
+    cs[j] = cr != nullptr ? *(const f32x4*)(cr + c) : (f32x4){1.f, 1.f, 1.f, 1.f};
+    sn[j] = cr != nullptr ? *(const f32x4*)(sr + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  ln64_rope16_regs<X1, X2>(x, w, bb, eps, cs, sn, cr != nullptr);
 }
 
 VP_DEV float wave_sum(float v) {
