@@ -148,15 +148,11 @@ class CogvideoXBranchModel(CogVideoXTransformer3DModel):
             x = block.forward_joint(x, T, emb, rope)
             samples.append(x)
         outs = []
-        Nv = Ntok - T
-        epi = NAT.EPI_BIAS if scale == 1.0 else NAT.EPI_BIAS_SCALE
         for s, lin in zip(samples, self.branch_blocks):
-            # the reference slices [:, T:] after the linear (branch_cogvideox.py); only the video rows are computed,
-            # one launch per clip (the text rows sit between the clips' video rows, so A is not one strided matrix)
-            o = torch.empty(B, Nv, D, device=dev, dtype=BF16)
-            for b in range(B):
-                K.gemm(s[b, T:], [lin.weight], [lin.bias], o[b], epilogue=epi, alpha=scale)
-            outs.append(o)
+            o = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
+            epi = NAT.EPI_BIAS if scale == 1.0 else NAT.EPI_BIAS_SCALE
+            K.gemm(s.view(B * Ntok, D), [lin.weight], [lin.bias], o.view(B * Ntok, D), epilogue=epi, alpha=scale)
+            outs.append(o[:, T:])
         outs = None if len(outs) == 0 else outs
         if not return_dict:
             return (outs,)
