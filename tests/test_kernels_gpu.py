@@ -23,11 +23,15 @@ def gemm_variant(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["lazy", "bounded"], ids=lambda v: f"attn_{v}")
+@pytest.fixture(params=["lazy", "bounded", "w32"], ids=lambda v: f"attn_{v}")
 def attn_variant(request, monkeypatch):
-    """lazy: the running-max kernel; bounded: the no-running-max kernel (row sums on the matrix pipe) that the host
-    selects when the qk-norm bounds every score (include/vp_hip.h VP_ATTN_BOUNDED_SCORES)."""
-    monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
+    """lazy: the running-max kernel; bounded: the no-running-max kernel the host selects when the qk-norm bounds
+    every score (include/vp_hip.h VP_ATTN_BOUNDED_SCORES) — two 32-query blocks per wave, row sums on the matrix
+    pipe; w32: the same contract on the 8-wave one-block-per-wave kernel (VP_ATTN_BOUNDED_MODE=w32, A/B)."""
+    if request.param == "w32":
+        monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", "w32")
+    else:
+        monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
     return request.param
 
 

@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--gemm-variants", default="5,11", help="VP_GEMM_VARIANT values, interleaved over 2 rounds")
-    ap.add_argument("--variant", default="", help="attention kernel(s): lazy, bounded (default: both)")
+    ap.add_argument("--variant", default="", help="attention kernel(s): lazy, bounded, w32 (default: lazy, bounded)")
     ap.add_argument("--variant8", default="", help="fp8 attention kernel variant(s) (VP_ATTN8_VARIANT), e.g. 1,2")
     ap.add_argument("--only", default="", help="attention | attn8 | gemm | mx | norms: run just that kernel (for rocprofv3 "
                     "--pmc passes; attn8 = the fp8 attention only)")
@@ -100,8 +100,12 @@ def main():
     variants = tuple(args.variant.split(",")) if args.variant else ("lazy", "bounded")
     if args.only in ("attn8", "norms"):
         variants = ()
-    for rnd in range(1 if args.only else 2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
+    for rnd in range(2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
         for var in variants:
+            if var == "w32":  # the 8-wave one-block-per-wave bounded kernel (A/B)
+                os.environ["VP_ATTN_BOUNDED_MODE"] = var
+            else:
+                os.environ.pop("VP_ATTN_BOUNDED_MODE", None)
             t = timeit(lambda: K.attention(q, k, v, o, H, bounded_scores=var != "lazy"), max(2, args.iters // 2))
             res[f"attention_{var}_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
             print("attention", var, res[f"attention_{var}_r{rnd}"], flush=True)

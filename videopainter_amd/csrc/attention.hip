@@ -29,6 +29,7 @@
 //          needs a second score tile live and spills at 128 VGPRs: 0.97.)
 #include <stdlib.h>
 
+
 #include "vp_common.h"
 
 namespace {
@@ -489,6 +490,175 @@ __global__ __launch_bounds__(NW * 64, 4) void attn_fwd(const vp_attn_desc d, con
 }
 
 
+// ------------------------------------------------------------------------------------------------------------
+// W64 (the BOUNDED-scores default): 4-wave workgroups of the same 256 queries, each wave TWO 32-query blocks.  The K
+// and V^T fragments of a 32-key half are read from LDS once and feed both blocks' MFMAs (half the LDS read bytes per
+// MFMA), and the two blocks' QK^T / exp / PV chains are independent, so a wave overlaps one block's softmax with the
+// other's MFMAs by itself; 2 waves/SIMD (256 VGPRs), two workgroups per CU with independent barriers.
+// ------------------------------------------------------------------------------------------------------------
+constexpr int NW4 = 4;
+constexpr int PPW4 = NP / NW4;
+static_assert(NW4 * 64 == QB, "same query block as the 8-wave kernel");
+
+template <bool TAIL = false>
+__global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_w64(const vp_attn_desc d, const AttnSplit sp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hl = lane >> 5;
+
+  const int nqb = (d.Nq + QB - 1) / QB;
+  const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
+  const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb;
+  const int qb = t - bh * nqb;
+  const int b = bh / d.H;
+  const int h = bh - b * d.H;
+  const int tiles1 = (d.Nk + KB - 1) / KB;
+  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KB - 1) / KB : 0;
+  const int ntiles_all = tiles1 + tiles2;
+  const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
+  const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
+
+  const int qw0 = qb * QB + wave * 64;  // first query of this wave
+  bf16x8 qf[2][4];
+  {
+    const float cq = d.scale * 1.4426950408889634f;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+      const int q = qw0 + qi * 32 + (lane & 31);
+      const int qc = q < d.Nq ? q : d.Nq - 1;
+      const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) {
+        qf[qi][ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[qi][ds][j] = f2bf(bf2f(qf[qi][ds][j]) * cq);
+      }
+    }
+  }
+
+  int prow[PPW4], kch[PPW4], vch[PPW4];
+#pragma unroll
+  for (int i = 0; i < PPW4; ++i) {
+    prow[i] = (wave + i * NW4) * 8 + (lane >> 3);
+    kch[i] = (lane & 7) ^ swz(prow[i]);
+    vch[i] = (lane & 7) ^ vswz(prow[i]);
+  }
+  auto slot_of = [&](int ti) { return smem + (ti & 1) * ST; };
+  auto issue = [&](int ti) {
+    const Seg sg = tile_seg(d, ti, tiles1, b, h);
+    char* slot = slot_of(ti);
+    const int last = sg.n - 1 - sg.key0;
+    const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
+    const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
+    const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
+#pragma unroll
+    for (int i = 0; i < PPW4; ++i) {
+      const int pc = wave + i * NW4;
+      const int r = min(prow[i], last);
+      glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + pc * 1024);
+      glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
+    }
+  };
+
+  const int g = lane >> 4;
+  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
+  const int tcol = 16 * (g & 1) + 4 * (lane & 3);
+  int vo[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh) vo[dh] = trow * 128 + (((dh * 4 + (tcol >> 3)) ^ vswz(trow)) << 4) + (tcol & 7) * 2;
+
+  f32x16 o[2][2];
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o[qi][0][i] = 0.f;
+      o[qi][1][i] = 0.f;
+    }
+  f32x4 lsum[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  bf16x8 sel;
+  {
+    const bf16 one = f2bf((((lane >> 4) & 1) == 0) == ((lane & 15) < 8) ? 1.f : 0.f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sel[e] = one;
+  }
+
+  const bool active = qw0 < d.Nq;  // wave-uniform (the second block may lie partly or wholly past Nq: computed,
+                                   // not stored)
+  issue(tbeg);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int ti = tbeg; ti < tend; ++ti) {
+    if (ti + 1 < tend) issue(ti + 1);
+    const char* Kl = slot_of(ti);
+    const char* Vl = Kl + KT;
+    const Seg sg = tile_seg(d, ti, tiles1, b, h);
+    const int lim = sg.n - sg.key0;
+#pragma unroll
+    for (int kh = 0; kh < HALVES; ++kh) {
+      if (!active) break;
+      // K fragments of this half, shared by the two query blocks
+      bf16x8 kf[4];
+      {
+        const int row = kh * 32 + (lane & 31);
+        const char* kr = Kl + row * 128;
+        const int sw = swz(row);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) kf[c] = *(const bf16x8*)(kr + (((2 * c + hl) ^ sw) << 4));
+      }
+      f32x16 sh[2];
+      const f32x16 z = {};
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi) {
+        sh[qi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[0], qf[qi][0], z, 0, 0, 0);
+#pragma unroll
+        for (int c = 1; c < 4; ++c) sh[qi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[c], qf[qi][c], sh[qi], 0, 0, 0);
+      }
+      if (lim < KB) {
+        mask_half(sh[0], lim, kh, hl);
+        mask_half(sh[1], lim, kh, hl);
+      }
+      bf16x8 pf[2][2];
+      softmax_half_bounded(sh[0], pf[0]);
+      softmax_half_bounded(sh[1], pf[1]);
+      // V^T fragments read once for both blocks
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ks = kh * 2 + j;
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          const char* base = Vl + ks * 16 * 128 + vo[dh];
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * 128));
+          const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[0][dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0][j], o[0][dh], 0, 0, 0);
+          o[1][dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[1][j], o[1][dh], 0, 0, 0);
+        }
+        lsum[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf[0][j], lsum[0], 0, 0, 0);
+        lsum[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf[1][j], lsum[1], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  const int qq = lane & 31;
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi) {
+    const float l_tot = __shfl(lsum[qi][0], qq < 16 ? qq : qq + 16, 64);
+    const int q = qw0 + qi * 32 + qq;
+    if (sp.nsplit > 1) {
+      const int qin = wave * 64 + qi * 32 + qq;
+      store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qin) * 66, o[qi], 0.f, l_tot,
+                    hl);
+    } else {
+      store_out(d, o[qi], l_tot, q, b, h, hl, false, 0.f);
+    }
+  }
+}
+
 // ============================================================================================================
 // fp8 attention (BASELINE config 5: "attn + FFN in fp8").  Both products on the block-scaled e4m3 MFMA
 // v_mfma_scale_f32_32x32x64_f8f6f4 (K = 64 per instruction: QK^T over the whole head in ONE MFMA per 32 keys, PV
@@ -865,10 +1035,12 @@ namespace {
 struct AttnVar {
   const void* fn;
   const void* fn_tail;  // the grid-tail split instance
+  int threads;
 };
 static const AttnVar attn_vars[] = {
-    {(const void*)attn_fwd<MODE_LAZY>, (const void*)attn_fwd<MODE_LAZY, true>},
-    {(const void*)attn_fwd<MODE_BOUNDED>, (const void*)attn_fwd<MODE_BOUNDED, true>},
+    {(const void*)attn_fwd<MODE_LAZY>, (const void*)attn_fwd<MODE_LAZY, true>, NW * 64},
+    {(const void*)attn_fwd<MODE_BOUNDED>, (const void*)attn_fwd<MODE_BOUNDED, true>, NW * 64},
+    {(const void*)attn_fwd_w64<false>, (const void*)attn_fwd_w64<true>, NW4 * 64},
 };
 constexpr int ATTN_NVAR = sizeof(attn_vars) / sizeof(attn_vars[0]);
 
@@ -897,7 +1069,7 @@ int attn_check(const vp_attn_desc* d) {
 
 int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   static bool attr_set = false;
-  static int slots = 0;  // resident workgroups chip-wide (the same for every variant: 128 VGPRs, LDS_BYTES)
+  static int slots_v[ATTN_NVAR] = {};  // resident workgroups chip-wide per variant
   if (!attr_set) {
     attr_set = true;
     int dev = 0, cus = 0;
@@ -906,18 +1078,22 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
     for (int i = 0; i < ATTN_NVAR; ++i) {
       (void)hipFuncSetAttribute(attn_vars[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
       (void)hipFuncSetAttribute(attn_vars[i].fn_tail, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, attn_vars[i].fn, attn_vars[i].threads, LDS_BYTES) !=
+          hipSuccess)
+        per_cu = 0;
+      slots_v[i] = per_cu * cus;
     }
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, attn_vars[0].fn, NW * 64, LDS_BYTES) != hipSuccess)
-      per_cu = 0;
-    slots = per_cu * cus;
   }
+  // BOUNDED scores: the two-blocks-per-wave kernel (default), VP_ATTN_BOUNDED_MODE=lazy the running-max kernel,
+  // =w32 the 8-wave one-block-per-wave kernel (A/B)
   int variant = 0;
   if (d->flags & VP_ATTN_BOUNDED_SCORES) {
     const char* e = getenv("VP_ATTN_BOUNDED_MODE");
-    variant = (e != nullptr && e[0] == 'l') ? 0 : 1;
+    variant = (e != nullptr && e[0] == 'l') ? 0 : (e != nullptr && e[0] == 'w' && e[1] == '3') ? 1 : 2;
   }
   pl.v = &attn_vars[variant];
+  const int slots = slots_v[variant];
   const int nqb = (d->Nq + QB - 1) / QB;
   pl.nblk = (int64_t)d->B * d->H * nqb;
   if (pl.nblk > 0x7fffffff) return VP_ERR_ARG;
@@ -959,13 +1135,13 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   if (main_blocks > 0) {
     const AttnSplit none = {0, 1, nullptr};
     void* args[] = {(void*)d, (void*)&none};
-    le = hipLaunchKernel(v.fn, dim3((unsigned)main_blocks), dim3(NW * 64), args, LDS_BYTES, (hipStream_t)stream);
+    le = hipLaunchKernel(v.fn, dim3((unsigned)main_blocks), dim3(v.threads), args, LDS_BYTES, (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
   }
   if (split) {
     const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace};
     void* args[] = {(void*)d, (void*)&sp};
-    le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(NW * 64), args, LDS_BYTES,
+    le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.threads), args, LDS_BYTES,
                          (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
     const int nthreads = pl.ntail * QB;
