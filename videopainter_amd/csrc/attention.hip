@@ -295,12 +295,15 @@ VP_DEV void store_partial(float* rec, const f32x16 (&o)[2], float m_run, float l
   }
 }
 
-// one thread per (tail block, query): merge the nsplit partials and store like store_out
+// 16 threads per (tail block, query), 4 output dims each: merge the nsplit partials and store like store_out (per
+// element the same operations in the same order as one thread per query: the split count is the only loop)
 __global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d, int t_base, int ntail, int nsplit,
                                                            int qb_size, const float* __restrict__ ws) {
   const int gid = blockIdx.x * 256 + threadIdx.x;
-  if (gid >= ntail * qb_size) return;
-  const int j = gid / qb_size, qi = gid - j * qb_size;
+  const int quad = gid & 15;
+  const int row = gid >> 4;
+  if (row >= ntail * qb_size) return;
+  const int j = row / qb_size, qi = row - j * qb_size;
   const int t = t_base + j;
   const int nqb = (d.Nq + qb_size - 1) / qb_size;
   const int bh = t / nqb, qb = t - bh * nqb;
@@ -310,40 +313,32 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d,
   const float* rec0 = ws + ((int64_t)j * nsplit * qb_size + qi) * 66;
   float mx = -INFINITY;
   for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, rec0[(int64_t)s * qb_size * 66 + 64]);
-  float acc[64];
-#pragma unroll
-  for (int e = 0; e < 64; ++e) acc[e] = 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float l = 0.f;
   for (int s = 0; s < nsplit; ++s) {
     const float* rec = rec0 + (int64_t)s * qb_size * 66;
     const float w = __builtin_amdgcn_exp2f(rec[64] - mx);
     l += rec[65] * w;
-#pragma unroll
-    for (int e = 0; e < 64; e += 4) {
-      const f32x4 v = *(const f32x4*)(rec + e);
-      acc[e] += v[0] * w;
-      acc[e + 1] += v[1] * w;
-      acc[e + 2] += v[2] * w;
-      acc[e + 3] += v[3] * w;
-    }
+    const f32x4 v = *(const f32x4*)(rec + 4 * quad);
+    acc[0] += v[0] * w;
+    acc[1] += v[1] * w;
+    acc[2] += v[2] * w;
+    acc[3] += v[3] * w;
   }
   const float inv = 1.f / l;
-  if (d.lse != nullptr) d.lse[((int64_t)b * d.H + h) * d.Nq + q] = mx + __log2f(l);
-  bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
+  if (d.lse != nullptr && quad == 0) d.lse[((int64_t)b * d.H + h) * d.Nq + q] = mx + __log2f(l);
+  bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64 + 4 * quad;
+  bf16x4 ov;
+  bf16x4 old;
+  if (d.accumulate) old = *(const bf16x4*)orow;
 #pragma unroll
-  for (int e = 0; e < 64; e += 4) {
-    bf16x4 ov;
-    bf16x4 old;
-    if (d.accumulate) old = *(const bf16x4*)(orow + e);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = rbf(acc[e + r] * inv);
-      if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
-      if (d.accumulate) v = bf2f(old[r]) + v;
-      ov[r] = f2bf(v);
-    }
-    *(bf16x4*)(orow + e) = ov;
+  for (int r = 0; r < 4; ++r) {
+    float v = rbf(acc[r] * inv);
+    if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
+    if (d.accumulate) v = bf2f(old[r]) + v;
+    ov[r] = f2bf(v);
   }
+  *(bf16x4*)orow = ov;
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1144,7 +1139,7 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
     le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.threads), args, LDS_BYTES,
                          (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
-    const int nthreads = pl.ntail * QB;
+    const int nthreads = pl.ntail * QB * 16;
     hipLaunchKernelGGL(attn_combine_kernel, dim3((nthreads + 255) / 256), dim3(256), 0, (hipStream_t)stream, *d,
                        (int)main_blocks, pl.ntail, pl.nsplit, QB, (const float*)workspace);
   }
