@@ -299,7 +299,7 @@ def run_config4(args, world: int, rank: int, local: int) -> None:
     if world > 1:
         import torch.distributed as dist
         from videopainter_amd.distributed import WindowStages, init as dist_init
-        dist_init("nccl", device)
+        dist_init(os.environ.get("VP_BENCH_DIST_BACKEND", "nccl"), device)
         stages = WindowStages()
     t_setup = time.time()
     cfg = dict(COGVIDEOX_5B_I2V, sample_height=HL, sample_width=WL)
@@ -475,6 +475,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # VP_BENCH_DIST_BACKEND=gloo: a functional rehearsal of the multi-rank path with several ranks on the GPUs there
+    # are (ranks share a device; the timing then says nothing about scaling); the driver's runs use RCCL, one rank
+    # per GPU
+    backend = os.environ.get("VP_BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if args.config == 4 or args.mode == "stages":
         set_config(2)  # the any-length chain runs 49f 480x720 windows
         run_config4(args, world, rank, local)
@@ -488,7 +494,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
         from videopainter_amd.distributed import init as dist_init
-        dist_init("nccl", device)
+        dist_init(backend, device)
     if args.mode == "cfgpair":
         if world % 2:
             raise SystemExit("--mode cfgpair needs an even number of ranks")
