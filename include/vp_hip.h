@@ -196,7 +196,9 @@ int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, int64_t wor
  * base.Q / base.K: e4m3 [B, N, H*64] written by vp_head_norm_rope_fp8 (strides in bytes, multiples of 16), each
  * carrying one power-of-two factor undone by the E8M0 bytes in qk_scale (bits 0-7: Q, bits 8-15: K; Q's factor
  * also includes scale * log2 e, so base.scale is ignored).  base.V: V^T e4m3 [B, H, 64, npad] and vs: its scales,
- * both from vp_v_pack_fp8.  base.O / out_scale / accumulate as in the bf16 kernel. */
+ * both from vp_v_pack_fp8.  base.O / out_scale / accumulate as in the bf16 kernel.  The probabilities P enter the
+ * PV product (and the row sums) as e4m3 codes of p * 2^7 made by linear mantissa interpolation of exp2 (relative
+ * error 3.2 % rms; env VP_ATTN8_VARIANT=1: exp2 + round-to-nearest e4m3, 2.7 %) — DESIGN.md §3.1. */
 typedef struct vp_attn_fp8_desc {
   vp_attn_desc base;
   const void* vs;
