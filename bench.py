@@ -135,11 +135,14 @@ def cpu_baseline() -> dict:
             out[name] = time.time() - t0
             del sd, h, e
     step_s = {k: v * step_flops() / block_flop() for k, v in out.items()}
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
     return {"value": 1.0 / step_s["bf16"], "unit": "steps/s", "cores": threads, "kind": "port",
+            "affinity_cpus": aff, "host_cpus": os.cpu_count(),
             "value_fp32": 1.0 / step_s["fp32"], "cpu_model": _cpu_model(),
             "sample": f"oracle (plain PyTorch CPU restatement) after a warm-up block: 1 full-size CogVideoXBlock "
                       f"forward at B=2, N={NTOK} took {out['bf16']:.1f} s in bf16 and {out['fp32']:.1f} s in fp32 on "
-                      f"{threads} threads ({_cpu_model()}); step = step FLOP / block FLOP x block time = "
+                      f"{threads} threads (process affinity mask: {aff} of the host's {os.cpu_count()} CPUs; "
+                      f"{_cpu_model()}); step = step FLOP / block FLOP x block time = "
                       f"{step_s['bf16']:.0f} s bf16 / {step_s['fp32']:.0f} s fp32"}
 
 

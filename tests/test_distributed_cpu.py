@@ -40,7 +40,8 @@ def _worker(rank, world, port, q, method="scatter_allgather"):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,method", [(2, "scatter_allgather"), (3, "scatter_allgather"), (2, "broadcast")])
+@pytest.mark.parametrize("world,method", [(2, "scatter_allgather"), (3, "scatter_allgather"), (4, "scatter_allgather"),
+                                          (2, "broadcast")])
 def test_broadcast_and_max_over_ranks_gloo(world, method):
     """Weight replication (both methods; world 3 exercises the padded shards) is an exact copy of rank 0's
     weights on every rank, and the bench's timing rule takes the max over ranks."""

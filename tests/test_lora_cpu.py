@@ -84,3 +84,52 @@ def test_fold_unfold_roundtrip_and_rejects_unknown_modules():
     half = {"transformer.transformer_blocks.0.attn1.to_q.lora_A.weight": torch.zeros(2, 128)}
     with pytest.raises(ValueError):
         fold_lora_(m, half)
+
+
+@pytest.mark.parametrize("fmt", ["peft", "kohya"])
+def test_runtime_scale_refold_is_exact(tmp_path, fmt):
+    """attention_kwargs["scale"] per call (reference cogvideox_transformer_3d.py:490-499): the model keeps the base
+    weights of the adapted layers, so folding at another scale equals folding that scale from scratch, bit for bit,
+    in any order of scales."""
+    from videopainter_amd.lora import fold_lora_
+    sd = _adapter(_model(), 8, 4.0 if fmt == "kohya" else None)
+    save_file(sd, os.path.join(tmp_path, "pytorch_lora_weights.safetensors"))
+
+    def fresh(scale):
+        m = _model()
+        fold_lora_(m, sd, scale)
+        return m.state_dict()
+
+    m = _model()
+    m.load_lora_weights(str(tmp_path), lora_scale=0.5, adapter_name="test_1")
+    assert m.get_list_adapters() == ["test_1"]
+    for scale in (0.5, 1.0, 0.25, 1.0, 0.5):
+        m.set_lora_scale(scale)
+        want = fresh(scale)
+        assert all(torch.equal(v, want[k]) for k, v in m.state_dict().items()), scale
+    with pytest.raises(ValueError, match="already loaded"):
+        m.load_lora_weights(str(tmp_path), adapter_name="test_1")
+
+
+def test_set_adapters_weights_and_fuse(tmp_path):
+    """set_adapters(names, weights) scales each folded adapter (others off); fuse_lora pins the folded scale."""
+    from videopainter_amd.lora import fold_lora_
+    g = torch.Generator().manual_seed(3)
+    sd1, sd2 = _adapter(_model(), 8), _adapter(_model(), 4)
+    for sd in (sd2,):
+        for k in sd:
+            sd[k] = torch.randn(sd[k].shape, generator=g) * 0.05
+    save_file(sd1, os.path.join(tmp_path, "a1.safetensors"))
+    save_file(sd2, os.path.join(tmp_path, "a2.safetensors"))
+    m = _model()
+    m.load_lora_weights(str(tmp_path), weight_name="a1.safetensors", adapter_name="one")
+    m.load_lora_weights(str(tmp_path), weight_name="a2.safetensors", adapter_name="two")
+    m.set_adapters(["two"], [0.5])
+    want = _model()
+    fold_lora_(want, sd2, 0.5)
+    assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), want.state_dict().values()))
+    m.fuse_lora(lora_scale=2.0)   # pinned: 2.0 * 0.5 on adapter two
+    m._call_lora_scale({"scale": 1.0})
+    want = _model()
+    fold_lora_(want, sd2, 1.0)
+    assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), want.state_dict().values()))

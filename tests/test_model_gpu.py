@@ -539,9 +539,21 @@ def test_lora_folded_model_matches_oracle(env, tmp_path):
     assert not torch.equal(folded["transformer_blocks.0.attn1.to_q.weight"],
                            torch.from_numpy(tsd["transformer_blocks.0.attn1.to_q.weight"]).to(torch.bfloat16))
     bs = [g["branch.0"], g["branch.1"]]
+    # the reference's call form for a LoRA scale: attention_kwargs={"scale": s} on every call
     out = m(hidden_states=_d(i["hidden"]), encoder_hidden_states=_d(i["enc"]), timestep=i["timestep"].to(dev),
             image_rotary_emb=i["rope"], branch_block_samples=[_d(b) for b in bs], branch_block_masks=_d(i["mask"]),
-            return_dict=False)[0]
+            attention_kwargs={"scale": 0.5}, return_dict=False)[0]
+    assert all(torch.equal(v.cpu(), folded[k]) for k, v in m.state_dict().items())  # same scale: no re-fold
+    # a call without a scale runs the adapters at 1.0 (the reference's default): re-folded exactly from the base
+    m(hidden_states=_d(i["hidden"]), encoder_hidden_states=_d(i["enc"]), timestep=i["timestep"].to(dev),
+      image_rotary_emb=i["rope"], return_dict=False)
+    with device_scope(dev):
+        m1 = CogVideoXTransformer3DModel(**TINY_CFG)
+    m1.load_diffusers_state_dict({k: torch.from_numpy(v) for k, v in tsd.items()})
+    m1.load_lora_weights(str(tmp_path), lora_scale=1.0)
+    assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), m1.state_dict().values()))
+    m.set_lora_scale(0.5)
+    assert all(torch.equal(v.cpu(), folded[k]) for k, v in m.state_dict().items())
     f32 = {k: v.float() for k, v in folded.items()}
     ref = O.transformer_forward(f32, env["tcfg"], i["hidden"], i["enc"], i["timestep"], i["rope"],
                                 branch_block_samples=bs, branch_block_masks=i["mask"])[0]

@@ -138,3 +138,10 @@ def test_t5_hip_graph_replay_matches_eager():
         for e, r in runs:
             assert torch.equal(e, r)
         assert not torch.equal(runs[0][0], runs[1][0])
+        # a round trip through the host (model CPU offload) moves every parameter: the captured graphs must not be
+        # replayed on the freed storage
+        m.cpu()
+        m.cuda()
+        with torch.no_grad():
+            r2 = m(input_ids=ids, **kw)[0]
+        assert torch.equal(runs[-1][0], r2)

@@ -10,7 +10,7 @@ import torch.multiprocessing as mp
 from videopainter_amd.ulysses import Shard, ThreadComm, DistComm, qkv_to_heads, heads_to_rows
 
 
-@pytest.mark.parametrize("N,T,P", [(17776, 226, 8), (1378, 226, 4), (298, 10, 4), (300, 226, 8), (50, 30, 3)])
+@pytest.mark.parametrize("N,T,P", [(17776, 226, 8), (1378, 226, 4), (298, 10, 4), (600, 226, 2), (80, 30, 2)])
 def test_shard_geometry(N, T, P):
     shards = [Shard(N, T, P, r) for r in range(P)]
     assert sum(s.valid for s in shards) == N and all(s.n * P == s.Npad >= N for s in shards)
@@ -22,6 +22,13 @@ def test_shard_geometry(N, T, P):
         assert s.r0 + s.tl >= T or s.tl == s.n
         vid += list(range(s.v0, s.v0 + s.nv))
     assert vid == list(range(shards[0].Npad - T))
+
+
+@pytest.mark.parametrize("N,T,P", [(300, 226, 8), (50, 30, 3)])
+def test_shard_of_text_rows_only_raises(N, T, P):
+    """T >= ceil(N / P): the first shard would hold no video row (empty proj_out / row-local launches)."""
+    with pytest.raises(ValueError, match="only text rows"):
+        Shard(N, T, P, 0)
 
 
 def _global_qkv(B, Npad, H, P):

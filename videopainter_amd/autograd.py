@@ -187,7 +187,9 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     K.adaln_bwd(x_mid, dxn2, g, T, n2.norm.weight, n2.norm.bias, n2.norm.eps, mod2, n_out=n2o, dn_out=dn2,
                 xhat_out=xh2)
     if need_dmod:
-        h = K.gelu(z)
+        # h exactly as the forward made it: GELU applied in the FF1 GEMM epilogue on the fp32 accumulator (a GELU
+        # of the bf16-rounded z would differ by one rounding, and so would ff2's weight and gate-2 gradients)
+        h = K.linear(xn2.view(M, D), ff0.weight, ff0.bias, gelu=True)
         f = torch.empty(M, D, device=dev, dtype=BF16)
         K.gemm(h, [ff2.weight], [ff2.bias], f)
         dmod2 = _mod_grad(K.colsum(dxn2.view(M, D), tokens_per_batch=Ntok, text_len=T),

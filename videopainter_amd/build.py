@@ -8,8 +8,10 @@ import concurrent.futures as cf
 import glob
 import hashlib
 import os
+import shutil
 import subprocess
 import sys
+import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -67,9 +69,12 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, extra_flags
     if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read().strip() == dg:
         return out
     objs = []
+    # objects in a private directory per build: two builds into one libdir (e.g. an A/B copy with extra flags next
+    # to the default library) must not link each other's objects
+    objdir = tempfile.mkdtemp(dir=libdir, prefix=".obj-" + os.path.basename(out) + "-")
 
     def cc(src):
-        obj = os.path.join(libdir, os.path.basename(src).replace(".hip", ".o"))
+        obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
         extra = PER_FILE_FLAGS.get(os.path.basename(src), []) + (extra_flags or {}).get(os.path.basename(src), [])
         cmd = [HIPCC, *CFLAGS, *extra, f'-DVP_BUILD_DIGEST="{dg}"', "-I", os.path.join(ROOT, "include"), "-c", src,
                "-o", obj]
@@ -79,16 +84,17 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, extra_flags
         return obj
 
     jobs = max(1, min(len(_sources()), int(os.environ.get("MAX_JOBS", "8"))))
-    with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(cc, _sources()))
-    tmp = out + ".tmp"
-    r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], capture_output=True,
-                       text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, out)
-    for o in objs:
-        os.remove(o)
+    try:
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            objs = list(ex.map(cc, _sources()))
+        tmp = os.path.join(objdir, os.path.basename(out))
+        r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, out)
+    finally:
+        shutil.rmtree(objdir, ignore_errors=True)
     with open(stamp, "w") as f:
         f.write(dg)
     if verbose:

@@ -51,6 +51,44 @@ def _buckets(tensors: List[torch.Tensor], limit: int):
         yield cur
 
 
+class _staged:
+    """The tensor a collective should run on: itself on RCCL, a host copy when the backend cannot take device
+    tensors (gloo: the single-GPU rehearsal, VP_BENCH_DIST_BACKEND=gloo).  Copies back on exit, so the caller's
+    code path (and the collective calls) are the same on every backend."""
+
+    def __init__(self, t: torch.Tensor, group=None, writeback: bool = True):
+        self.t = t
+        self.host = t.is_cuda and dist.get_backend(group) != "nccl"
+        self.writeback = writeback
+        self.work = t.detach().cpu() if self.host else t
+
+    def __enter__(self) -> torch.Tensor:
+        return self.work
+
+    def __exit__(self, *exc):
+        if self.host and self.writeback and exc[0] is None:
+            self.t.copy_(self.work)
+        return False
+
+
+def _all_gather_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """all_gather_into_tensor on any backend (gloo takes host tensors only: staged)."""
+    if not out.is_contiguous():
+        raise ValueError("all-gather output must be contiguous")
+    with _staged(out, group) as o, _staged(inp.contiguous(), group, writeback=False) as i:
+        dist.all_gather_into_tensor(o.view(-1), i.view(-1), group=group)  # flat: one layout rule for every backend
+
+
+def _send(t: torch.Tensor, dst: int) -> None:
+    with _staged(t.contiguous(), writeback=False) as w:
+        dist.send(w, dst)
+
+
+def _recv(t: torch.Tensor, src: int) -> None:
+    with _staged(t) as w:
+        dist.recv(w, src)
+
+
 @torch.no_grad()
 def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0, bucket_bytes: int = BUCKET_BYTES,
                       method: str = "scatter_allgather") -> None:
@@ -68,7 +106,8 @@ def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0, bucket_byte
         if world == 1:
             continue
         if method == "broadcast" and len(b) == 1:
-            dist.broadcast(b[0], src=src)
+            with _staged(b[0]) as t:
+                dist.broadcast(t, src=src)
             continue
         n = sum(t.numel() for t in b)
         per = (n + world - 1) // world
@@ -78,28 +117,26 @@ def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0, bucket_byte
             for t in b:
                 flat[off:off + t.numel()].copy_(t.reshape(-1))
                 off += t.numel()
-        if method == "broadcast":
-            dist.broadcast(flat, src=src)
-        elif method == "scatter_allgather":
-            shard = torch.empty(per, dtype=flat.dtype, device=flat.device)
-            if dist.get_backend() == "nccl":
-                # point-to-point scatter (RCCL has no native scatter): batched sends from the source
+        with _staged(flat) as work:
+            if method == "broadcast":
+                dist.broadcast(work, src=src)
+            elif method == "scatter_allgather":
+                # point-to-point scatter (RCCL has no native scatter): batched sends from the source, then one
+                # all-gather of the shards.  The same calls run on every backend (gloo in the CPU tests).
+                shard = torch.empty(per, dtype=work.dtype, device=work.device)
                 ops = []
                 if rank == src:
                     for r in range(world):
                         if r != src:
-                            ops.append(dist.P2POp(dist.isend, flat[r * per:(r + 1) * per], r))
-                    shard.copy_(flat[src * per:(src + 1) * per])
+                            ops.append(dist.P2POp(dist.isend, work[r * per:(r + 1) * per], r))
+                    shard.copy_(work[src * per:(src + 1) * per])
                 else:
                     ops.append(dist.P2POp(dist.irecv, shard, src))
                 for req in dist.batch_isend_irecv(ops):
                     req.wait()
-                dist.all_gather_into_tensor(flat, shard)
+                dist.all_gather_into_tensor(work, shard)
             else:
-                dist.scatter(shard, list(flat.chunk(world)) if rank == src else None, src=src)
-                dist.all_gather(list(flat.chunk(world)), shard)
-        else:
-            raise ValueError(f"unknown replication method {method!r}")
+                raise ValueError(f"unknown replication method {method!r}")
         if rank != src:
             off = 0
             for t in b:
@@ -162,10 +199,7 @@ class CFGPair:
             raise ValueError("each CFG rank holds a batch of 1")
         half = half.contiguous()
         out = torch.empty((2,) + tuple(half.shape[1:]), dtype=half.dtype, device=half.device)
-        if self.backend == "nccl":
-            dist.all_gather_into_tensor(out, half, group=self.group)
-        else:
-            dist.all_gather([out[0:1], out[1:2]], half, group=self.group)
+        _all_gather_rows(out, half, self.group)
         return out
 
 
@@ -200,43 +234,43 @@ class WindowStages:
                      mask: Optional[torch.Tensor], generator: Optional[torch.Generator] = None) -> None:
         dst = self.peer(dst_stage)
         dev = latents.device
-        dist.send(latents.contiguous(), dst)
+        _send(latents.contiguous(), dst)
         gs = generator.get_state() if generator is not None else None
         flags = torch.tensor([0 if states is None else len(states), 0 if mask is None else 1,
                               0 if gs is None else gs.numel()], dtype=torch.int64, device=dev)
-        dist.send(flags, dst)
+        _send(flags, dst)
         if states is not None:
             for k in sorted(states):
-                dist.send(states[k].contiguous(), dst)
+                _send(states[k].contiguous(), dst)
         if mask is not None:
-            dist.send(mask.to(torch.uint8).contiguous(), dst)
+            _send(mask.to(torch.uint8).contiguous(), dst)
         if gs is not None:
-            dist.send(gs.to(dev), dst)
+            _send(gs.to(dev), dst)
 
     def recv_handoff(self, src_stage: int, lat_like: torch.Tensor, state_shape, mask_shape,
                      generator: Optional[torch.Generator] = None):
         src = self.peer(src_stage)
         dev = lat_like.device
         lat = torch.empty_like(lat_like)
-        dist.recv(lat, src)
+        _recv(lat, src)
         flags = torch.empty(3, dtype=torch.int64, device=dev)
-        dist.recv(flags, src)
+        _recv(flags, src)
         n_states, has_mask, gs_n = (int(x) for x in flags.tolist())
         states = None
         if n_states:
             states = {}
             for k in range(n_states):
                 t = torch.empty(state_shape, dtype=lat_like.dtype, device=dev)
-                dist.recv(t, src)
+                _recv(t, src)
                 states[k] = t
         mask = None
         if has_mask:
             m = torch.empty(mask_shape, dtype=torch.uint8, device=dev)
-            dist.recv(m, src)
+            _recv(m, src)
             mask = m.bool()
         if gs_n:
             g = torch.empty(gs_n, dtype=torch.uint8, device=dev)
-            dist.recv(g, src)
+            _recv(g, src)
             if generator is None:
                 raise ValueError("the previous stage handed off a generator state but this rank has no generator")
             generator.set_state(g.cpu())
@@ -251,10 +285,7 @@ class WindowStages:
         for w, t in local.items():
             buf[w // self.stages] = t
         allb = torch.empty((self.world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
-        if dist.get_backend() == "nccl":
-            dist.all_gather_into_tensor(allb, buf)
-        else:
-            dist.all_gather(list(allb.unbind(0)), buf)
+        _all_gather_rows(allb, buf)
         return [allb[self.peer(self.stage_of(w))][w // self.stages] for w in range(n_windows)]
 
 
@@ -317,10 +348,7 @@ def allgather_windows(local: Dict[int, torch.Tensor], n_windows: int, like: torc
             raise ValueError(f"window {w} is not placed on rank {rank}")
         buf[w // world] = t
     allb = torch.empty((world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
-    if dist.get_backend() == "nccl":
-        dist.all_gather_into_tensor(allb, buf)
-    else:
-        dist.all_gather(list(allb.unbind(0)), buf)
+    _all_gather_rows(allb, buf)
     return [allb[w % world][w // world] for w in range(n_windows)]
 
 

@@ -15,6 +15,12 @@ product into W once (`W + s B A`, accumulated in fp32, rounded to the weight dty
 path the adapted weights with no per-step cost.  Kohya-style files (`lora_down` / `lora_up` + `.alpha`) are
 accepted too; their alpha is honoured (alpha / r), as the generic diffusers conversion does.
 
+Runtime scale: the reference scales the adapters per call (`attention_kwargs["scale"]`, default 1.0,
+cogvideox_transformer_3d.py:490-499 -> `scale_lora_layers`).  `attach_lora_` keeps the base weights of the adapted
+layers (a device copy, 4 x 3072^2 bf16 per block) and the adapter factors, so `refold_lora_` can rebuild
+`W0 + s * B A` exactly (the same fp32 expression as the first fold, bit-identical to folding s from scratch)
+whenever a call passes a different scale; the transformer's forward does that before its first launch.
+
 Parity: PEFT is not installed here, so the reference's unfused LoRA forward cannot run; `tests/test_lora_cpu.py`
 checks the fold against the LoRA formula on the module level and the round trip (fold, unfold) — "parity unpinned"
 against PEFT itself.
@@ -101,3 +107,98 @@ def load_lora_into_transformer(transformer: torch.nn.Module, path: str,
 def unfold_lora_(model: torch.nn.Module, sd: Dict[str, torch.Tensor], lora_scale: float = 1.0) -> int:
     """Remove a folded adapter (W -= s B A; exact only up to the weight dtype's rounding)."""
     return fold_lora_(model, sd, -lora_scale)
+
+
+class LoraState:
+    """What the model needs to re-fold at another scale: base weights of the adapted layers, the adapters, the scale
+    currently folded.  Kept in the module's __dict__ (not buffers: the state dict stays the reference's)."""
+
+    def __init__(self):
+        self.base: Dict[str, torch.Tensor] = {}
+        self.adapters: list = []      # [(name, {module: {"A", "B", "alpha"}})]
+        self.scale: Optional[float] = None
+        self.weights: Dict[str, float] = {}   # set_adapters() weights per adapter (1.0 when loaded, 0 = inactive)
+        self.fused = False            # fuse_lora(): the folded scale no longer follows the per-call scale
+
+
+def lora_state(model: torch.nn.Module) -> Optional[LoraState]:
+    return model.__dict__.get("_vp_lora")
+
+
+@torch.no_grad()
+def refold_lora_(model: torch.nn.Module, scale: float) -> int:
+    """W = W0 + scale * sum over adapters of (alpha / r) B A, from the kept base weights (exact: the first fold's
+    expression).  Re-quantises an enabled fp8 QKV projection of the blocks whose weights changed."""
+    st = lora_state(model)
+    if st is None:
+        return 0
+    mods = dict(model.named_modules())
+    for mod, w0 in st.base.items():
+        W = mods[mod].weight
+        acc = w0.to(W.device, torch.float32)
+        for name, pairs in st.adapters:
+            p = pairs.get(mod)
+            if p is None or st.weights.get(name, 1.0) == 0.0:
+                continue
+            r = p["A"].shape[0]
+            s = scale * st.weights.get(name, 1.0) * (p["alpha"] / r if p.get("alpha") is not None else 1.0)
+            acc = acc + s * (p["B"].to(W.device, torch.float32) @ p["A"].to(W.device, torch.float32))
+        W.copy_(acc.to(W.dtype))
+    st.scale = float(scale)
+    for blk in getattr(model, "transformer_blocks", []):
+        if getattr(blk, "qkv_mx", None) is not None:
+            blk.enable_fp8_qkv(True)
+    return len(st.base)
+
+
+@torch.no_grad()
+def attach_lora_(model: torch.nn.Module, sd: Dict[str, torch.Tensor], lora_scale: float = 1.0,
+                 adapter_name: Optional[str] = None, strict: bool = True) -> int:
+    """Register an adapter on `model` and fold it (with every adapter attached before) at `lora_scale`."""
+    mods = dict(model.named_modules())
+    pairs = {}
+    for mod, p in lora_pairs(sd).items():
+        lin = mods.get(mod)
+        if lin is None or not hasattr(lin, "weight"):
+            if strict:
+                raise KeyError(f"LoRA targets {mod}, which the model does not have")
+            continue
+        W = lin.weight
+        if tuple(W.shape) != (p["B"].shape[0], p["A"].shape[1]):
+            raise ValueError(f"LoRA {mod}: B@A is {(p['B'].shape[0], p['A'].shape[1])}, weight is {tuple(W.shape)}")
+        pairs[mod] = {"A": p["A"].to(W.device), "B": p["B"].to(W.device), "alpha": p.get("alpha")}
+    st = lora_state(model)
+    if st is None:
+        st = model.__dict__["_vp_lora"] = LoraState()
+    if st.scale is not None and st.scale != lora_scale:
+        refold_lora_(model, lora_scale)
+    for mod in pairs:
+        if mod not in st.base:
+            st.base[mod] = mods[mod].weight.detach().clone()
+    name = adapter_name or f"default_{len(st.adapters)}"
+    if any(n == name for n, _ in st.adapters):
+        raise ValueError(f"adapter {name!r} is already loaded")
+    st.adapters.append((name, pairs))
+    st.weights[name] = 1.0
+    refold_lora_(model, lora_scale)
+    return len(pairs)
+
+
+@torch.no_grad()
+def set_adapter_weights_(model: torch.nn.Module, names, weights=None) -> None:
+    """PEFT's `set_adapters(names, weights)`: the listed adapters active with their weights, the others off."""
+    st = lora_state(model)
+    if st is None:
+        raise ValueError("no LoRA adapter is loaded")
+    names = [names] if isinstance(names, str) else list(names)
+    known = [n for n, _ in st.adapters]
+    for n in names:
+        if n not in known:
+            raise ValueError(f"adapter {n!r} is not loaded (loaded: {known})")
+    ws = [1.0] * len(names) if weights is None else (
+        [float(weights)] * len(names) if not isinstance(weights, (list, tuple)) else [float(w) for w in weights])
+    if len(ws) != len(names):
+        raise ValueError("one weight per adapter name")
+    st.weights = {n: 0.0 for n in known}
+    st.weights.update(dict(zip(names, ws)))
+    refold_lora_(model, st.scale if st.scale is not None else 1.0)

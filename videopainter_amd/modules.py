@@ -86,6 +86,9 @@ class ModelMixin(nn.Module):
     config_name = W.CONFIG_NAME
     _supports_gradient_checkpointing = True
 
+    def __init__(self):
+        nn.Module.__init__(self)  # never a re-based library base's __init__ (integration.install)
+
     def _init_config(self, kwargs: dict):
         cfg = full_config(kwargs, branch=self._is_branch)
         object.__setattr__(self, "_internal_config", FrozenConfig(cfg))

@@ -66,7 +66,7 @@ class T5EncoderModel(nn.Module):
     _keep_in_fp32_modules = ["wo"]  # reference behaviour recorded for callers; the HIP path computes in bf16
 
     def __init__(self, config=None, **kwargs):
-        super().__init__()
+        nn.Module.__init__(self)  # never a re-based library base's __init__ (integration.install)
         cfg = dict(config.to_dict() if hasattr(config, "to_dict") else (config or {}))
         cfg.update(kwargs)
         cfg = full_t5_config(cfg)
@@ -146,11 +146,15 @@ class T5EncoderModel(nn.Module):
                     raise RuntimeError(f"{k}: shape {tuple(sd[k].shape)} != {tuple(t.shape)}")
                 t.copy_(sd[k].to(device=t.device, dtype=t.dtype))
         self._qkv.clear()
+        self._graph_cache.clear()
         return self
 
     def _apply(self, fn, *args, **kwargs):
+        # .to() / .cpu() / .cuda() may move every parameter: captured graphs hold the old addresses
         self._qkv = {}
         self._buckets = {}
+        if hasattr(self, "_graph_cache"):
+            self._graph_cache.clear()
         return super()._apply(fn, *args, **kwargs)
 
     def get_input_embeddings(self):

@@ -378,10 +378,52 @@ class CogVideoXTransformer3DModel(ModelMixin):
     def load_lora_weights(self, path: str, weight_name: str = "pytorch_lora_weights.safetensors",
                           adapter_name: Optional[str] = None, lora_scale: float = 1.0, **_):
         """The VideoPainterID adapter (PEFT safetensors) folded into to_q/to_k/to_v/to_out.0 at load time
-        (videopainter_amd/lora.py; the reference applies it unfused through PEFT, infer/inpaint.py:310-315)."""
-        from .lora import load_lora_into_transformer
-        load_lora_into_transformer(self, path, weight_name, lora_scale)
+        (videopainter_amd/lora.py; the reference applies it unfused through PEFT, infer/inpaint.py:310-315).
+        `lora_scale` is the scale folded now; every forward re-folds to its own `attention_kwargs["scale"]`
+        (default 1.0, as the reference's per-call scaling) when that differs."""
+        from .lora import attach_lora_, load_lora_state_dict
+        sd = load_lora_state_dict(path, weight_name)
+        if any(k.startswith("transformer.") for k in sd):  # the pipeline-level file (lora_pipeline.py:2653-2656)
+            sd = {k: v for k, v in sd.items() if k.startswith("transformer.")}
+        attach_lora_(self, sd, lora_scale, adapter_name)
         return self
+
+    def get_list_adapters(self):
+        from .lora import lora_state
+        st = lora_state(self)
+        return [n for n, _ in st.adapters] if st is not None else []
+
+    def set_lora_scale(self, scale: float):
+        """Fold the attached adapters at `scale` (what a call with attention_kwargs={"scale": scale} does)."""
+        from .lora import lora_state, refold_lora_
+        st = lora_state(self)
+        if st is not None and st.scale != float(scale):
+            refold_lora_(self, float(scale))
+        return self
+
+    def set_adapters(self, adapter_names, weights=None):
+        """PEFT's set_adapters on the folded adapters: the listed ones active with these weights, the rest off."""
+        from .lora import set_adapter_weights_
+        set_adapter_weights_(self, adapter_names, weights)
+        return self
+
+    def fuse_lora(self, lora_scale: float = 1.0):
+        """The pipeline's `fuse_lora(lora_scale=...)`: fold at `lora_scale` and stop following per-call scales
+        (PEFT's merged layers no longer see `scale_lora_layers`)."""
+        from .lora import lora_state
+        self.set_lora_scale(lora_scale)
+        st = lora_state(self)
+        if st is not None:
+            st.fused = True
+        return self
+
+    def _call_lora_scale(self, attention_kwargs):
+        from .lora import lora_state
+        st = lora_state(self)
+        if st is None or st.fused:
+            return
+        s = attention_kwargs.get("scale", 1.0) if attention_kwargs else 1.0
+        self.set_lora_scale(1.0 if s is None else s)
 
     def enable_fp8_ffn(self, enabled: bool = True):
         """fp8 FeedForward in every block (BASELINE config 5; see CogVideoXBlock.enable_fp8_ffn).  Call after the
@@ -471,8 +513,10 @@ class CogVideoXTransformer3DModel(ModelMixin):
         if self_guidance_hidden_states is not None or self_guidance_masks is not None:
             raise NotImplementedError("self-guidance inputs belong to the self-guidance pipelines (out of scope)")
         attention_kwargs = dict(attention_kwargs) if attention_kwargs is not None else None
+        # LoRA scale per call, default 1.0 (reference :490-499): the folded adapters are re-folded when it changes
+        self._call_lora_scale(attention_kwargs)
         if attention_kwargs is not None:
-            attention_kwargs.pop("scale", None)  # LoRA scale: adapters are folded into the weights at load time
+            attention_kwargs.pop("scale", None)
         dev = self.proj_out.weight.device
         B, F, C, H, W = hidden_states.shape
         cfg = self.config
@@ -565,6 +609,7 @@ class CogVideoXTransformer3DModel(ModelMixin):
             raise NotImplementedError("the previous-clip blend is inference-only (no backward)")
         if return_hidden_states or return_resample_mask or id_pool_resample_learnable:
             raise NotImplementedError("return_hidden_states / resample masks are inference-only (no backward)")
+        self._call_lora_scale(attention_kwargs)
         dev = self.proj_out.weight.device
         B, F, C, H, W = hidden_states.shape
         cfg = self.config

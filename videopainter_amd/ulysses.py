@@ -131,6 +131,11 @@ class Shard:
         self.tl = max(0, min(self.n, self.T - self.r0))       # local text rows (a prefix of the shard)
         self.v0 = max(0, self.r0 - self.T)                    # video index of the first local video row
         self.nv = self.n - self.tl                            # local video rows (padding included)
+        if self.nv == 0:
+            # the whole shard is text (T >= ceil(N / P) with a small clip or a large P): the row-local kernels would
+            # get zero video rows and proj_out an empty launch
+            raise ValueError(f"Ulysses split: shard {self.rank} of {self.P} holds only text rows (N = {self.N}, "
+                             f"T = {self.T}, {self.n} rows per shard); use fewer ranks for this clip size")
 
     def rows(self, x: torch.Tensor) -> torch.Tensor:
         """This shard's rows of a full [B, N, ...] tensor (zero-padded)."""

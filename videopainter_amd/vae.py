@@ -127,7 +127,7 @@ class AutoencoderKLCogVideoX(nn.Module):
                  scaling_factor: float = 1.15258426, shift_factor: Optional[float] = None,
                  latents_mean: Optional[Tuple[float]] = None, latents_std: Optional[Tuple[float]] = None,
                  force_upcast: float = True, use_quant_conv: bool = False, use_post_quant_conv: bool = False):
-        super().__init__()
+        nn.Module.__init__(self)  # never a re-based library base's __init__ (integration.install)
         cfg = full_vae_config(dict(
             in_channels=in_channels, out_channels=out_channels, down_block_types=tuple(down_block_types),
             up_block_types=tuple(up_block_types), block_out_channels=tuple(block_out_channels),
