@@ -87,6 +87,24 @@ def full_block_case(seed: int = 0, dtype=torch.float32, latent=(3, 32, 48), key=
     return dict(weights=w, h=h, e=e, temb=temb, rope=rope)
 
 
+def resample_block_case(dtype=torch.float32):
+    """The ID-resample processor at the headline shape (VERDICT r02 "what's missing" 2): one full-width block with
+    id_pool_resample_learnable=True at config 2's length (latent 13x60x90: N = 226 + 17 550 = 17 776, every attention
+    over 2N = 35 552 keys), B = 1.  resample_mask [1, N] (text rows False, video rows = a jittered centred rectangle
+    per frame, frame 0 clear); window > 0 inputs: the previous window's joint states [1, N, D] and its mask."""
+    c = full_block_case(latent=(13, 60, 90), key="fbr", dtype=dtype)
+    nv = c["h"].shape[1]
+
+    def tok_mask(key):
+        m = make_mask(1, 13, 30, 45, key=key).reshape(1, nv)
+        return torch.cat([torch.zeros(1, 226, dtype=torch.bool), torch.from_numpy(m > 0.5)], dim=1)
+
+    c["resample_mask"] = tok_mask("fbr.mask")
+    c["prev_resample_mask"] = tok_mask("fbr.prevmask")
+    c["prev"] = torch.from_numpy(synth_tensor("fbr.prev", (1, 226 + nv, 3072))).to(dtype)
+    return c
+
+
 PIPE_CASE = dict(num_frames=9, total_frames=18, stride=9, height=128, width=192, steps=2, prev_clip_weight=0.5,
                  id_pool_resample_learnable=True)
 

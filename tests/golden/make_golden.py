@@ -417,6 +417,44 @@ def make_block5():
                                  "ref_bf16_rel": torch.tensor([rel])})
 
 @torch.no_grad()
+def make_block_resample():
+    """The ID-resample processor (attention_processor.py:2223-2304) in one full-width block at config 2's length
+    (N = 17 776, Nk = 2N), B = 1: window 0 (masked self K/V) and a later window (the previous window's states
+    projected to K/V, masked, x prev_clip_weight 0.5), each in fp32 and bf16.  block_resample.safetensors."""
+    import time
+    from diffusers.models.transformers.cogvideox_transformer_3d import CogVideoXBlock
+    from tests.golden.cases import resample_block_case
+    case = resample_block_case()
+    blk = CogVideoXBlock(dim=3072, num_attention_heads=48, attention_head_dim=64, time_embed_dim=512,
+                         attention_bias=True, id_pool_resample_learnable=True).eval()
+    blk.load_state_dict({k: torch.from_numpy(v) for k, v in case["weights"].items()}, strict=True)
+    out = {}
+    for mode in ("r0", "r1"):
+        def run(dt):
+            kw = None
+            if mode == "r1":  # a fresh dict per call: the block rewrites prev_hidden_states in it (:143-147)
+                kw = {"prev_hidden_states": case["prev"].to(dt), "prev_clip_weight": 0.5,
+                      "prev_resample_mask": case["prev_resample_mask"]}
+            h, e = blk.to(dt)(hidden_states=case["h"].to(dt), encoder_hidden_states=case["e"].to(dt),
+                              temb=case["temb"].to(dt), image_rotary_emb=case["rope"],
+                              resample_mask=case["resample_mask"], attention_kwargs=kw)
+            return torch.cat([e, h], dim=1).float()
+
+        t0 = time.time()
+        o32 = run(torch.float32)
+        print(f"block_resample {mode} fp32 {time.time() - t0:.0f}s", flush=True)
+        o16 = run(torch.bfloat16)
+        rel = float((o16.double() - o32.double()).norm() / o32.double().norm())
+        print(f"block_resample {mode} reference bf16 vs fp32 rel-L2 {rel:.3e}", flush=True)
+        flat = o32.reshape(-1)
+        out[f"{mode}.slice"] = flat[::997].clone()
+        out[f"{mode}.bf16.slice"] = o16.reshape(-1)[::997].clone()
+        out[f"{mode}.digest"] = torch.tensor([flat.sum(), flat.abs().sum(), flat.norm()], dtype=torch.float64)
+        out[f"{mode}.ref_bf16_rel"] = torch.tensor([rel])
+    _save("block_resample.safetensors", out)
+
+
+@torch.no_grad()
 def make_vae():
     """The reference AutoencoderKLCogVideoX (tiny and 5b-shaped configs, counter weights): encode -> latent_dist
     mean / logvar and decode of a fixed latent, at 17 frames 64x96 (two encoder frame batches: 9 + 8, so the causal
@@ -528,6 +566,8 @@ if __name__ == "__main__":
         make_config2()
     if "block5" in which:
         make_block5()
+    if "block_resample" in which:
+        make_block_resample()
     if "vae" in which:
         make_vae()
     if "vae_tiled" in which:

@@ -23,13 +23,14 @@ def gemm_variant(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["lazy", "bounded", "w32"], ids=lambda v: f"attn_{v}")
+@pytest.fixture(params=["lazy", "bounded", "w32", "s16", "w64"], ids=lambda v: f"attn_{v}")
 def attn_variant(request, monkeypatch):
     """lazy: the running-max kernel; bounded: the no-running-max kernel the host selects when the qk-norm bounds
-    every score (include/vp_hip.h VP_ATTN_BOUNDED_SCORES) — two 32-query blocks per wave, row sums on the matrix
-    pipe; w32: the same contract on the 8-wave one-block-per-wave kernel (VP_ATTN_BOUNDED_MODE=w32, A/B)."""
-    if request.param == "w32":
-        monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", "w32")
+    every score (include/vp_hip.h VP_ATTN_BOUNDED_SCORES), the library default; w32: the same contract on the 8-wave
+    one-block-per-wave kernel; w64: two 32-query blocks per wave on the 32x32x16 MFMA; s16: 64 queries per wave on
+    the 16x16x32 MFMA (VP_ATTN_BOUNDED_MODE selects the last three)."""
+    if request.param in ("w32", "s16", "w64"):
+        monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", request.param)
     else:
         monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
     return request.param
@@ -446,6 +447,34 @@ def test_attention_tail_split_matches_unsplit(Nq, Nk2, monkeypatch):
     out_u = torch.empty_like(out_s)
     K.attention(q, k, v, out_u, H, **kw)
     # bf16 P is rounded against each range's own running max, so the two differ at bf16 noise level
+    assert rel(out_s, out_u) < 5e-3
+    if Nq < 17776:
+        hd = lambda x: x.float().cpu().reshape(B, -1, H, 64).transpose(1, 2)  # noqa: E731
+        kk, vv = hd(k), hd(v)
+        if Nk2:
+            kk, vv = torch.cat([kk, hd(kw["k2"])], 2), torch.cat([vv, hd(kw["v2"])], 2)
+        ref = _sdpa(hd(q), kk, vv).transpose(1, 2).reshape(B, Nq, D)
+        assert rel(out_s, ref) < 1e-2 and rel(out_u, ref) < 1e-2
+
+
+@pytest.mark.parametrize("mode", ["w64", "s16"])
+@pytest.mark.parametrize("Nq,Nk2", [(1500, 700), (17776, 0)])
+def test_attention_bounded_tail_split_matches_unsplit(Nq, Nk2, mode, monkeypatch):
+    """The bounded-score kernels' grid-tail split instances (partials + merge) against their unsplit launch and, at
+    small size, against fp32 attention."""
+    from videopainter_amd import kernels as K
+    monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", mode)
+    B, H = 2, 2 if Nq < 17776 else 48
+    D = H * 64
+    q, k, v = (bf(rnd(B, Nq, D, seed=s) * 0.5).to(dev) for s in (80, 81, 82))
+    kw = dict(bounded_scores=True)
+    if Nk2:
+        kw.update(k2=bf(rnd(B, Nk2, D, seed=83) * 0.5).to(dev), v2=bf(rnd(B, Nk2, D, seed=84)).to(dev))
+    out_s = torch.empty(B, Nq, D, device=dev, dtype=torch.bfloat16)
+    K.attention(q, k, v, out_s, H, **kw)
+    monkeypatch.setenv("VP_ATTN_NO_SPLIT", "1")
+    out_u = torch.empty_like(out_s)
+    K.attention(q, k, v, out_u, H, **kw)
     assert rel(out_s, out_u) < 5e-3
     if Nq < 17776:
         hd = lambda x: x.float().cpu().reshape(B, -1, H, 64).transpose(1, 2)  # noqa: E731

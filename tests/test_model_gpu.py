@@ -407,8 +407,8 @@ def test_pipelined_window_chain_driver_matches_serial(env):
 @torch.no_grad()
 def test_full_width_block_fp8_ffn_tolerance():
     """BASELINE config 5's fp8 FeedForward (MX-FP8: e4m3 + E8M0 per 32 inputs) on the 5B-width block, against the
-    reference fp32 block.  Re-stated tolerance: the fp8 path may drift from fp32 at most 4x as far as the reference
-    itself does in bf16, plus 1e-2 (e4m3 keeps 3 mantissa bits against bf16's 7)."""
+    reference fp32 block.  Re-stated tolerance: 1.65e-2 from fp32, 1.5x the drift measured in round 2 (1.10e-2;
+    e4m3 keeps 3 mantissa bits against bf16's 7)."""
     from videopainter_amd import device_scope
     from videopainter_amd.transformer import CogVideoXBlock
     from oracle import cogvideox_oracle as O
@@ -432,7 +432,8 @@ def test_full_width_block_fp8_ffn_tolerance():
     oflat = torch.cat([oe, oh], dim=1).reshape(-1).float()
     r8, r16, ro = rel(flat8[::97], g["slice"]), rel(flat16[::97], g["slice"]), rel(oflat[::97], g["slice"])
     print(f"fp8-FFN block vs fp32: {r8:.3e}; bf16 HIP {r16:.3e}; reference bf16 {ro:.3e}")
-    assert r8 <= 4 * ro + 1e-2, (r8, r16, ro)
+    # measured (r02): 1.10e-2; gate 1.5x that (was 4 x ro + 1e-2 = 2.0e-2)
+    assert r8 <= 1.65e-2, (r8, r16, ro)
     # the fp8 delta is confined to the FeedForward branch: compare to the bf16 path's own output
     assert rel(flat8, flat16) < 3e-2
 
@@ -440,7 +441,8 @@ def test_full_width_block_fp8_ffn_tolerance():
 def test_full_width_block_fp8_attention_and_ffn_tolerance():
     """BASELINE config 5 ("attn + FFN in fp8") on the 5B-width block against the reference fp32 block: the fp8
     attention (e4m3 Q/K with static LN-bounded factors, V^T with per-(d, 32 keys) scales, P in e4m3), the MX-FP8
-    FeedForward, then the MX-FP8 QKV projection too.  Re-stated tolerance: at most 6x the reference's own bf16 drift from fp32, plus 2e-2."""
+    FeedForward, then the MX-FP8 QKV projection too.  Re-stated tolerances, 1.5x what round 2 measured: attention
+    alone 4e-3, attention + FFN 1.65e-2, + QKV 1.7e-2 from fp32."""
     from videopainter_amd import device_scope
     from videopainter_amd.transformer import CogVideoXBlock
     from oracle import cogvideox_oracle as O
@@ -473,8 +475,10 @@ def test_full_width_block_fp8_attention_and_ffn_tolerance():
           f"vs bf16 HIP: attn {rel(flata, flat16):.3e}, attn+FFN {rel(flat8, flat16):.3e}")
     rq = rel(flatq[::97], g["slice"])
     print(f"+ fp8 QKV projection: vs fp32 {rq:.3e}, vs bf16 HIP {rel(flatq, flat16):.3e}")
-    assert r8 <= 6 * ro + 2e-2, (r8, ra, ro)
-    assert rq <= 6 * ro + 2e-2, (rq, ro)
+    # measured (r02): attn+FFN 1.10e-2, attention alone 2.64e-3, + QKV 1.13e-2; gates 1.5x those
+    assert r8 <= 1.65e-2, (r8, ra, ro)
+    assert ra <= 4e-3, (ra, ro)
+    assert rq <= 1.7e-2, (rq, ro)
     assert rel(flat8, flat16) < 5e-2 and rel(flatq, flat16) < 5e-2
 
 
@@ -510,7 +514,7 @@ def test_fp8_attention_model_modes(env):
             continue
         r8, r16 = rel(out8, g[gold]), rel(out16, g[gold])
         print(f"fp8 attention {mode}: vs fp32 {r8:.3e} (bf16 HIP {r16:.3e}); vs bf16 {rel(out8, out16):.3e}")
-        assert r8 <= 4 * r16 + 3e-2, (mode, r8, r16)
+        assert r8 <= 1.5 * r16, (mode, r8, r16)  # measured (r02): r8 / r16 = 1.00
 
 
 @torch.no_grad()
@@ -630,7 +634,7 @@ def test_config1_full_model_matches_reference():
     assert r <= gate(float(rb[0]))
     assert r0 <= gate(float(rb[1])) and r1 <= gate(float(rb[2]))
     # config 5's fp8 path (QKV projection, attention, FeedForward in e4m3) at full depth, same reference:
-    # re-stated tolerance 3x the reference's bf16 drift + 2e-2
+    # re-stated tolerance 4e-2 (1.5x the measured fp8 drift)
     tr.enable_fp8()
     br.enable_fp8()
     bs8 = br(hidden_states=_d(inp["video"]), encoder_hidden_states=_d(inp["enc"]),
@@ -642,7 +646,7 @@ def test_config1_full_model_matches_reference():
     r8 = rel(o8.float().reshape(-1)[::37], g["slice"])
     print(f"config 1 full model, fp8 QKV + attention + FFN vs reference fp32: {r8:.3e}; vs HIP bf16 "
           f"{rel(o8, o.float()):.3e}")
-    assert r8 <= 3 * float(rb[0]) + 2e-2
+    assert r8 <= 4e-2  # measured (r02): 2.61-2.66e-2; gate 1.5x (was 3 x reference bf16 drift + 2e-2 = 8.9e-2)
     del tr, br, bs, o, bs8, o8
     torch.cuda.empty_cache()
 
@@ -691,8 +695,8 @@ def test_config2_full_model_matches_reference():
 def test_config5_length_block_matches_reference():
     """BASELINE config 5's sequence length (720x1280: N = 226 + 46 800 = 47 026): one full-width block against the
     reference's fp32 block (tests/golden/block5.safetensors), in bf16 (gate of the reference's own bf16 drift) and
-    with the config-5 fp8 path (QKV, attention, FeedForward in e4m3; re-stated band 6x the reference's bf16 drift
-    + 2e-2, as at N = 1378)."""
+    with the config-5 fp8 path (QKV, attention, FeedForward in e4m3; re-stated band 1.5e-2 = 1.5x
+    the measured fp8 drift)."""
     from videopainter_amd import device_scope
     from videopainter_amd.transformer import CogVideoXBlock
     c = full_block_case(latent=(13, 90, 160), key="fb5")
@@ -717,7 +721,40 @@ def test_config5_length_block_matches_reference():
     print(f"config-5 length block vs reference fp32: bf16 HIP {r16:.3e}, fp8 QKV+attention+FFN {r8:.3e} "
           f"(reference bf16 {rb:.3e}); fp8 vs bf16 HIP {rel(flat8, flat16):.3e}")
     assert r16 <= gate(rb)
-    assert r8 <= 6 * rb + 2e-2
+    assert r8 <= 1.5e-2  # measured (r02): 9.93e-3; gate 1.5x (was 6 x reference bf16 drift + 2e-2 = 3.5e-2)
+
+
+@torch.no_grad()
+def test_resample_block_at_config2_length_matches_reference():
+    """The ID-resample processor (config 4's attention, attention_processor.py:2223-2304) at the headline length:
+    one full-width block at N = 17 776 with every attention over 2N = 35 552 keys, against the reference's fp32 block
+    (tests/golden/block_resample.safetensors): window 0 (masked self K/V as the second segment) and a later window
+    (the previous window's states projected to K/V, masked, x prev_clip_weight 0.5).  Gate: 1.25 x the reference's own
+    bf16 drift + 1e-3."""
+    from videopainter_amd import device_scope
+    from videopainter_amd.transformer import CogVideoXBlock
+    from tests.golden.cases import resample_block_case
+    c = resample_block_case()
+    g = load_file(os.path.join(GOLD, "block_resample.safetensors"))
+    with device_scope(dev):
+        blk = CogVideoXBlock(dim=3072, num_attention_heads=48, attention_head_dim=64, time_embed_dim=512,
+                             attention_bias=True, id_pool_resample_learnable=True)
+    for k, p in blk.state_dict().items():
+        p.copy_(torch.from_numpy(c["weights"][k]))
+    for mode in ("r0", "r1"):
+        kw = None
+        if mode == "r1":
+            kw = {"prev_hidden_states": _d(c["prev"]), "prev_clip_weight": 0.5,
+                  "prev_resample_mask": c["prev_resample_mask"].to(dev)}
+        h, e = blk(hidden_states=_d(c["h"]), encoder_hidden_states=_d(c["e"]), temb=_d(c["temb"]),
+                   image_rotary_emb=c["rope"], resample_mask=c["resample_mask"].to(dev), attention_kwargs=kw)
+        flat = torch.cat([e, h], dim=1).reshape(-1).float().cpu()
+        r = rel(flat[::997], g[f"{mode}.slice"])
+        rb = float(g[f"{mode}.ref_bf16_rel"][0])
+        rbs = rel(g[f"{mode}.bf16.slice"], g[f"{mode}.slice"])
+        print(f"resample block {mode} at N = 17776 (Nk = 35552) vs reference fp32: HIP bf16 {r:.3e} "
+              f"(reference bf16 {rb:.3e}, on the slice {rbs:.3e})")
+        assert r <= gate(rb), (mode, r, rb)
 
 
 @torch.no_grad()

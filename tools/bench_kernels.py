@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--gemm-variants", default="5,11", help="VP_GEMM_VARIANT values, interleaved over 2 rounds")
-    ap.add_argument("--variant", default="", help="attention kernel(s): lazy, bounded, w32 (default: lazy, bounded)")
+    ap.add_argument("--variant", default="", help="attention kernel(s): lazy, bounded, w32, w64, s16 (default: lazy, bounded)")
     ap.add_argument("--variant8", default="", help="fp8 attention kernel variant(s) (VP_ATTN8_VARIANT), e.g. 1,2")
     ap.add_argument("--only", default="", help="attention | attn8 | gemm | mx | norms: run just that kernel (for rocprofv3 "
                     "--pmc passes; attn8 = the fp8 attention only)")
@@ -102,7 +102,7 @@ def main():
         variants = ()
     for rnd in range(2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
         for var in variants:
-            if var == "w32":  # the 8-wave one-block-per-wave bounded kernel (A/B)
+            if var in ("w32", "w64", "s16"):  # bounded-kernel forms (A/B): VP_ATTN_BOUNDED_MODE
                 os.environ["VP_ATTN_BOUNDED_MODE"] = var
             else:
                 os.environ.pop("VP_ATTN_BOUNDED_MODE", None)

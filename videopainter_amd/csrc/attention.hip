@@ -654,6 +654,210 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_w64(const vp_attn_desc d
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// S16: the W64 structure (4-wave workgroups of 256 queries, 64 queries per wave, 128-key tiles through the same
+// 2-slot LDS-DMA ring) on the 16x16x32 bf16 MFMA instead of 32x32x16.  Same FLOPs, same LDS bytes and the same VALU
+// per score; the chip holds a higher clock on the 16x16x32 shape under load (MI355X_MICROARCH.md 'DVFS give-back'
+// item 7: 1.12-1.15x the FLOP/s of the 32x32x16 loop at equal cycles per FLOP).
+// Per 32-key half and wave (4 query tiles qt of 16, 2 key tiles kt of 16, 4 head-dim tiles dt of 16):
+//   S^T[kt][qt] = K[kt] . Q^T[qt]   2 MFMAs each (d = 0..31, 32..63): 16 MFMAs; lane l holds queries l % 16 and keys
+//                                   16 kt + 4 (l / 16) + i (i = 0..3): the query on the lane, as before.
+//   P^T[qt] (B operand, k-slot 8 (l / 16) + j  <->  key 4 (l / 16) + j for j < 4, 16 + 4 (l / 16) + j - 4 after):
+//                                   the lane's own 8 scores, exp2 + pack, no cross-lane move.
+//   O^T[dt][qt] += V^T[dt] . P^T[qt]  16 MFMAs; V^T[dt] (A operand, row d = 16 dt + l % 16, the same k-slots) by two
+//                                   ds_read_b64_tr_b16 (keys 4 (l / 16) + 0..3 and 16 + 4 (l / 16) + 0..3).
+//   l[qt] += ones . P^T[qt]         4 MFMAs: every accumulator row is the query's sum over the half's 32 keys.
+// V image swizzle vswz16 (row r: chunk ^ 2 ((r >> 1) & 3)): the 32 lanes of a transposed read take keys r0 .. r0 + 7
+// of one 16-column block, conflict-free only if rows 4 apart land in different chunk pairs.
+// ------------------------------------------------------------------------------------------------------------
+VP_DEV int vswz16(int row) { return ((row >> 1) & 3) << 1; }
+
+template <bool TAIL = false>
+__global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d, const AttnSplit sp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int c16 = lane & 15;
+
+  const int nqb = (d.Nq + QB - 1) / QB;
+  const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
+  const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb;
+  const int qb = t - bh * nqb;
+  const int b = bh / d.H;
+  const int h = bh - b * d.H;
+  const int tiles1 = (d.Nk + KB - 1) / KB;
+  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KB - 1) / KB : 0;
+  const int ntiles_all = tiles1 + tiles2;
+  const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
+  const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
+
+  const int qw0 = qb * QB + wave * 64;  // first query of this wave
+  bf16x8 qf[4][2];                      // Q^T B operands: query 16 qt + l % 16, dims 32 c + 8 (l / 16) + j
+  {
+    const float cq = d.scale * 1.4426950408889634f;
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      const int q = qw0 + qt * 16 + c16;
+      const int qc = q < d.Nq ? q : d.Nq - 1;
+      const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        qf[qt][c] = *(const bf16x8*)(qrow + c * 32 + g * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[qt][c][j] = f2bf(bf2f(qf[qt][c][j]) * cq);
+      }
+    }
+  }
+
+  int prow[PPW4], kch[PPW4], vch[PPW4];
+#pragma unroll
+  for (int i = 0; i < PPW4; ++i) {
+    prow[i] = (wave + i * NW4) * 8 + (lane >> 3);
+    kch[i] = (lane & 7) ^ swz(prow[i]);
+    vch[i] = (lane & 7) ^ vswz16(prow[i]);
+  }
+  auto slot_of = [&](int ti) { return smem + (ti & 1) * ST; };
+  auto issue = [&](int ti) {
+    const Seg sg = tile_seg(d, ti, tiles1, b, h);
+    char* slot = slot_of(ti);
+    const int last = sg.n - 1 - sg.key0;
+    const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
+    const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
+    const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
+#pragma unroll
+    for (int i = 0; i < PPW4; ++i) {
+      const int pc = wave + i * NW4;
+      const int r = min(prow[i], last);
+      glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + pc * 1024);
+      glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
+    }
+  };
+
+  // transposed V^T reads: lane 4 tq + tp of its 16-lane group addresses key row 4 g + tq (second read: + 16),
+  // columns 16 dt + 4 tp .. + 3; vswz16 depends on row bits 1-2 only, so one offset serves every half and both reads
+  int vo[4];
+  {
+    const int vrow = 4 * g + ((lane & 15) >> 2);
+    const int tp = lane & 3;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) vo[dt] = vrow * 128 + (((2 * dt + (tp >> 1)) ^ vswz16(vrow)) << 4) + (tp & 1) * 8;
+  }
+
+  f32x4 o[4][4];  // O^T[dt][qt]: dims 16 dt + 4 (l / 16) + i of query 16 qt + l % 16
+  f32x4 lsum[4];
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    lsum[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = f2bf(1.f);
+
+  const bool active = qw0 < d.Nq;  // wave-uniform
+  issue(tbeg);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int ti = tbeg; ti < tend; ++ti) {
+    if (ti + 1 < tend) issue(ti + 1);
+    const char* Kl = slot_of(ti);
+    const char* Vl = Kl + KT;
+    const Seg sg = tile_seg(d, ti, tiles1, b, h);
+    const int lim = sg.n - sg.key0;
+#pragma unroll
+    for (int kh = 0; kh < HALVES; ++kh) {
+      if (!active) break;
+      bf16x8 kf[2][2];  // K A operands: key 32 kh + 16 kt + l % 16, dims 32 c + 8 (l / 16) + j
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int row = kh * 32 + kt * 16 + c16;
+        const char* kr = Kl + row * 128;
+        const int sw = swz(row);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) kf[kt][c] = *(const bf16x8*)(kr + (((4 * c + g) ^ sw) << 4));
+      }
+      f32x4 sc[4][2];
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          sc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[qt][0], z, 0, 0, 0);
+          sc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[qt][1], sc[qt][kt], 0, 0, 0);
+        }
+      if (lim < KB) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bool dead = kh * 32 + kt * 16 + 4 * g + i >= lim;
+#pragma unroll
+            for (int qt = 0; qt < 4; ++qt)
+              if (dead) sc[qt][kt][i] = -INFINITY;
+          }
+      }
+      bf16x8 pf[4];
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pf[qt][i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][0][i]));
+          pf[qt][4 + i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][1][i]));
+        }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const char* base = Vl + kh * 32 * 128 + vo[dt];
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 16 * 128));
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt) o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt], o[dt][qt], 0, 0, 0);
+      }
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qt], lsum[qt], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    const float l_tot = lsum[qt][0];
+    const int q = qw0 + qt * 16 + c16;
+    if (sp.nsplit > 1) {
+      float* rec = sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + wave * 64 + qt * 16 + c16) * 66;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) *(f32x4*)(rec + dt * 16 + 4 * g) = o[dt][qt];
+      if (g == 0) {
+        rec[64] = 0.f;
+        rec[65] = l_tot;
+      }
+      continue;
+    }
+    if (q >= d.Nq) continue;
+    const float inv = 1.f / l_tot;
+    if (d.lse != nullptr && g == 0) d.lse[((int64_t)b * d.H + h) * d.Nq + q] = __log2f(l_tot);
+    bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64 + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x4 ov;
+      bf16x4 old;
+      if (d.accumulate) old = *(const bf16x4*)(orow + dt * 16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = rbf(o[dt][qt][r] * inv);
+        if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
+        if (d.accumulate) v = bf2f(old[r]) + v;
+        ov[r] = f2bf(v);
+      }
+      *(bf16x4*)(orow + dt * 16) = ov;
+    }
+  }
+}
+
 // ============================================================================================================
 // fp8 attention (BASELINE config 5: "attn + FFN in fp8").  Both products on the block-scaled e4m3 MFMA
 // v_mfma_scale_f32_32x32x64_f8f6f4 (K = 64 per instruction: QK^T over the whole head in ONE MFMA per 32 keys, PV
@@ -1036,6 +1240,7 @@ static const AttnVar attn_vars[] = {
     {(const void*)attn_fwd<MODE_LAZY>, (const void*)attn_fwd<MODE_LAZY, true>, NW * 64},
     {(const void*)attn_fwd<MODE_BOUNDED>, (const void*)attn_fwd<MODE_BOUNDED, true>, NW * 64},
     {(const void*)attn_fwd_w64<false>, (const void*)attn_fwd_w64<true>, NW4 * 64},
+    {(const void*)attn_fwd_s16<false>, (const void*)attn_fwd_s16<true>, NW4 * 64},
 };
 constexpr int ATTN_NVAR = sizeof(attn_vars) / sizeof(attn_vars[0]);
 
@@ -1085,7 +1290,8 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   int variant = 0;
   if (d->flags & VP_ATTN_BOUNDED_SCORES) {
     const char* e = getenv("VP_ATTN_BOUNDED_MODE");
-    variant = (e != nullptr && e[0] == 'l') ? 0 : (e != nullptr && e[0] == 'w' && e[1] == '3') ? 1 : 2;
+    variant = (e != nullptr && e[0] == 'l') ? 0 : (e != nullptr && e[0] == 'w' && e[1] == '3') ? 1
+            : (e != nullptr && e[0] == 's') ? 3 : 2;
   }
   pl.v = &attn_vars[variant];
   const int slots = slots_v[variant];
