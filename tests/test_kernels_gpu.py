@@ -23,13 +23,18 @@ def gemm_variant(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["lazy", "bounded", "w32", "s16", "w64"], ids=lambda v: f"attn_{v}")
+@pytest.fixture(params=["lazy", "bounded", "w32", "s16", "w64", "a16"], ids=lambda v: f"attn_{v}")
 def attn_variant(request, monkeypatch):
     """lazy: the running-max kernel; bounded: the no-running-max kernel the host selects when the qk-norm bounds
     every score (include/vp_hip.h VP_ATTN_BOUNDED_SCORES), the library default; w32: the same contract on the 8-wave
     one-block-per-wave kernel; w64: two 32-query blocks per wave on the 32x32x16 MFMA; s16: 64 queries per wave on
-    the 16x16x32 MFMA (VP_ATTN_BOUNDED_MODE selects the last three)."""
-    if request.param in ("w32", "s16", "w64"):
+    the 16x16x32 MFMA (VP_ATTN_BOUNDED_MODE selects these three); a16: the anchored-softmax kernel on unbounded
+    scores (VP_ATTN_UNBOUNDED_MODE=a16)."""
+    monkeypatch.delenv("VP_ATTN_UNBOUNDED_MODE", raising=False)
+    if request.param == "a16":
+        monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
+        monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", "a16")
+    elif request.param in ("w32", "s16", "w64"):
         monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", request.param)
     else:
         monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
@@ -39,7 +44,7 @@ def attn_variant(request, monkeypatch):
 def attn_kw(variant, q, k, scale=0.125, k2=None):
     """bounded_scores for the variant, after checking on the host that the inputs satisfy the bound (the contract
     the processors establish from the qk-norm weights)."""
-    if variant == "lazy":
+    if variant in ("lazy", "a16"):
         return {}
     kk = k if k2 is None else torch.cat([k, k2], 1)
     B, Nq, D = q.shape
@@ -219,6 +224,62 @@ def test_attention_forced_rescale(attn_variant):
     K.attention(q.to(dev), k.to(dev), v.to(dev), out, H, **attn_kw(attn_variant, q, k))
     ref = _sdpa(q[:, None], k[:, None], v[:, None])[:, 0]
     assert rel(out, ref) < 1e-2
+
+
+def _ref64(q, k, v, H, scale=0.125):
+    """fp64 attention on the CPU (exact reference for score ranges far beyond fp32 exp)."""
+    B, Nq = q.shape[:2]
+    hd = lambda x: x.double().cpu().reshape(B, -1, H, 64).transpose(1, 2)  # noqa: E731
+    s = hd(q) @ hd(k).transpose(-1, -2) * scale
+    return (torch.softmax(s, -1) @ hd(v)).transpose(1, 2).reshape(B, Nq, H * 64)
+
+
+@pytest.mark.parametrize("mode", ["a16", "lazy"])
+@pytest.mark.parametrize("gamma", [1.0, 6.0])
+def test_attention_large_gamma_scores(gamma, mode, monkeypatch):
+    """qk-LayerNorm outputs with |gamma| up to 6 (scores over hundreds of log2 units, far outside the bounded-score
+    contract): the anchored kernel (no running max) against fp64 attention, at a config-2-like length for 2 heads."""
+    from videopainter_amd import kernels as K
+    monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", mode)
+    B, H, Nn = 1, 2, 4500
+    g = torch.Generator().manual_seed(int(gamma * 10))
+    gam = torch.rand(H * 64, generator=g) * gamma  # per-channel gains in [0, gamma]
+    ln = lambda x: (x - x.mean(-1, keepdim=True)) / x.std(-1, keepdim=True, unbiased=False)  # noqa: E731
+    q = bf(ln(torch.randn(B, Nn, H, 64, generator=g)).reshape(B, Nn, H * 64) * gam)
+    k = bf(ln(torch.randn(B, Nn, H, 64, generator=g)).reshape(B, Nn, H * 64) * gam)
+    v = bf(torch.randn(B, Nn, H * 64, generator=g))
+    out = torch.empty(B, Nn, H * 64, device=dev, dtype=torch.bfloat16)
+    K.attention(q.to(dev), k.to(dev), v.to(dev), out, H)
+    r = rel(out, _ref64(q, k, v, H))
+    hd = lambda x: x.double().reshape(B, -1, H, 64).transpose(1, 2)  # noqa: E731
+    span = float((hd(q) @ hd(k).transpose(-1, -2)).abs().max()) * 0.125 * 1.4426950408889634
+    print(f"gamma {gamma} {mode}: max |score| {span:.0f} log2 units, rel vs fp64 {r:.3e}")
+    assert torch.isfinite(out.float()).all() and r < 1e-2
+
+
+@pytest.mark.parametrize("jump", [40.0, 90.0, 200.0])
+def test_attention_anchored_late_jump(jump, monkeypatch):
+    """The anchored kernel's guarded paths: a late key whose score exceeds every earlier one by `jump` log2 units for
+    half the queries — 40: within the first reference's range; 90: row sums pass 2^64 (the 2^-64 rescale branch);
+    200: exp2 overflows inside a tile (the exact two-pass re-run of the workgroup).  Against fp64 attention."""
+    from videopainter_amd import kernels as K
+    monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", "a16")
+    B, H, Nn = 1, 1, 1500
+    g = torch.Generator().manual_seed(int(jump))
+    q = torch.randn(B, Nn, 64, generator=g) * 0.3
+    k = torch.randn(B, Nn, 64, generator=g) * 0.3
+    v = torch.randn(B, Nn, 64, generator=g)
+    u = torch.randn(64, generator=g)
+    u = u / u.norm()
+    q[:, ::2] += 4.0 * u                       # even queries align with u
+    # key 1300 (tile 10): score vs even queries ~ 4 * a * 0.125 * log2 e  = jump  ->  a = jump / (0.5 * log2 e)
+    k[0, 1300] = u * (jump / (0.5 * 1.4426950408889634))
+    q, k, v = bf(q), bf(k), bf(v)
+    out = torch.empty(B, Nn, 64, device=dev, dtype=torch.bfloat16)
+    K.attention(q.to(dev), k.to(dev), v.to(dev), out, H)
+    r = rel(out, _ref64(q, k, v, H))
+    print(f"late jump {jump}: rel vs fp64 {r:.3e}")
+    assert torch.isfinite(out.float()).all() and r < 1e-2
 
 
 def test_attention_stepwise_max_growth():

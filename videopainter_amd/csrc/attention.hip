@@ -672,7 +672,26 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_w64(const vp_attn_desc d
 // ------------------------------------------------------------------------------------------------------------
 VP_DEV int vswz16(int row) { return ((row >> 1) & 3) << 1; }
 
-template <bool TAIL = false>
+// inf / NaN by the exponent bits (this file builds with -fno-honor-nans: float compares may assume no NaN)
+VP_DEV bool nonfinite(float x) { return (__float_as_uint(x) & 0x7f800000u) == 0x7f800000u; }
+
+VP_DEV float xmax16(float x) {  // max over the 4 lanes c16 + 16 g (one query's lanes)
+  x = fmaxf(x, __shfl_xor(x, 16, 64));
+  return fmaxf(x, __shfl_xor(x, 32, 64));
+}
+
+// ANCH (anchored softmax, no bound on the scores needed): every query's exponent reference m is an actual score of
+// its row — the max over the first 32 keys its workgroup visits — so the row sum is >= 1 (nothing underflows), and
+// p = exp2(s - m) leaves the QK^T MFMA through its C operand (C = -m, free).  m then stays fixed: no running max.
+// After each tile a wave whose row sums passed 2^64 (a rare, wave-uniform branch) rescales those queries' O and l
+// by 2^-64 and raises m by 64.  A row whose scores jump more than ~120 log2 units above m inside one tile would
+// overflow: the kernel checks every output and row sum at the end, and a workgroup that saw a non-finite value re-runs
+// its block exactly (pass 1: the row maxima over all keys; pass 2: p = exp2(s - max) <= 1).  Without ANCH (the host
+// proved |score| <= VP_ATTN_SCORE_BOUND) m = 0 and nothing is checked.
+// ORD 1: the PV phase per query tile (the 4 V^T fragments read first; then per qt: 8 exp2 + 4 packs, its 4 PV
+// MFMAs and its row-sum MFMA), so query tile qt's MFMAs run under qt + 1's transcendental work; ORD 0: all 32 exp2
+// first, then the 16 PV MFMAs, then the 4 row sums.
+template <bool TAIL = false, bool ANCH = false, int ORD = 0>
 __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d, const AttnSplit sp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -748,81 +767,212 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
 
   f32x4 o[4][4];  // O^T[dt][qt]: dims 16 dt + 4 (l / 16) + i of query 16 qt + l % 16
   f32x4 lsum[4];
+  f32x4 negm[4];  // C operand of the QK^T chains: -m of the lane's query (ANCH), else 0
+  float m[4];
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
-    lsum[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    m[qt] = 0.f;
+    negm[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
   bf16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = f2bf(1.f);
 
   const bool active = qw0 < d.Nq;  // wave-uniform
-  issue(tbeg);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int ti = tbeg; ti < tend; ++ti) {
-    if (ti + 1 < tend) issue(ti + 1);
-    const char* Kl = slot_of(ti);
-    const char* Vl = Kl + KT;
-    const Seg sg = tile_seg(d, ti, tiles1, b, h);
-    const int lim = sg.n - sg.key0;
+
+  // one pass over this workgroup's key tiles through the LDS ring; body(Kl, Vl, lim, first_tile) per tile
+  auto tile_loop = [&](auto&& body) {
+    issue(tbeg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int ti = tbeg; ti < tend; ++ti) {
+      if (ti + 1 < tend) issue(ti + 1);
+      const char* Kl = slot_of(ti);
+      const Seg sg = tile_seg(d, ti, tiles1, b, h);
+      if (active) body(Kl, Kl + KT, sg.n - sg.key0, ti == tbeg);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  };
+  // S^T of one 32-key half: key 32 kh + 16 kt + 4 (l / 16) + i, C-initialised with negm (-m, or 0)
+  auto qk_half = [&](const char* Kl, int kh, int lim, f32x4 (&sc)[4][2]) {
+    bf16x8 kf[2][2];  // K A operands: key 32 kh + 16 kt + l % 16, dims 32 c + 8 (l / 16) + j
 #pragma unroll
-    for (int kh = 0; kh < HALVES; ++kh) {
-      if (!active) break;
-      bf16x8 kf[2][2];  // K A operands: key 32 kh + 16 kt + l % 16, dims 32 c + 8 (l / 16) + j
+    for (int kt = 0; kt < 2; ++kt) {
+      const int row = kh * 32 + kt * 16 + c16;
+      const char* kr = Kl + row * 128;
+      const int sw = swz(row);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) kf[kt][c] = *(const bf16x8*)(kr + (((4 * c + g) ^ sw) << 4));
+    }
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        const int row = kh * 32 + kt * 16 + c16;
-        const char* kr = Kl + row * 128;
-        const int sw = swz(row);
-#pragma unroll
-        for (int c = 0; c < 2; ++c) kf[kt][c] = *(const bf16x8*)(kr + (((4 * c + g) ^ sw) << 4));
+        sc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[qt][0], negm[qt], 0, 0, 0);
+        sc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[qt][1], sc[qt][kt], 0, 0, 0);
       }
-      f32x4 sc[4][2];
-      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    if (lim < KB) {
 #pragma unroll
-      for (int qt = 0; qt < 4; ++qt)
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          sc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[qt][0], z, 0, 0, 0);
-          sc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[qt][1], sc[qt][kt], 0, 0, 0);
-        }
-      if (lim < KB) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const bool dead = kh * 32 + kt * 16 + 4 * g + i >= lim;
-#pragma unroll
-            for (int qt = 0; qt < 4; ++qt)
-              if (dead) sc[qt][kt][i] = -INFINITY;
-          }
-      }
-      bf16x8 pf[4];
-#pragma unroll
-      for (int qt = 0; qt < 4; ++qt)
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          pf[qt][i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][0][i]));
-          pf[qt][4 + i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][1][i]));
+          const bool dead = kh * 32 + kt * 16 + 4 * g + i >= lim;
+#pragma unroll
+          for (int qt = 0; qt < 4; ++qt)
+            if (dead) sc[qt][kt][i] = -INFINITY;
         }
+    }
+  };
+  // P = exp2(S) packed as the P^T B operand, then O^T += V^T P^T and the row sums
+  auto pv_half = [&](const char* Vl, int kh, const f32x4 (&sc)[4][2]) {
+    if constexpr (ORD == 1) {
+      bf16x8 vf[4];
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const char* base = Vl + kh * 32 * 128 + vo[dt];
         const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
         const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 16 * 128));
-        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int qt = 0; qt < 4; ++qt) o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt], o[dt][qt], 0, 0, 0);
+        vf[dt] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
-      for (int qt = 0; qt < 4; ++qt) lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qt], lsum[qt], 0, 0, 0);
+      for (int qt = 0; qt < 4; ++qt) {
+        bf16x8 pq;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pq[i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][0][i]));
+          pq[4 + i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][1][i]));
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pq, o[dt][qt], 0, 0, 0);
+        lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pq, lsum[qt], 0, 0, 0);
+      }
+      return;
     }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    bf16x8 pf[4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pf[qt][i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][0][i]));
+        pf[qt][4 + i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][1][i]));
+      }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const char* base = Vl + kh * 32 * 128 + vo[dt];
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 16 * 128));
+      const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt], o[dt][qt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qt], lsum[qt], 0, 0, 0);
+  };
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      lsum[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto set_ref = [&](int qt, float mq) {
+    m[qt] = mq;
+    negm[qt] = (f32x4){-mq, -mq, -mq, -mq};
+  };
+
+  // ---- main pass ----
+  zero_acc();
+  tile_loop([&](const char* Kl, const char* Vl, int lim, bool first_tile) {
+#pragma unroll
+    for (int kh = 0; kh < HALVES; ++kh) {
+      f32x4 sc[4][2];
+      qk_half(Kl, kh, lim, sc);
+      if constexpr (ANCH) {
+        if (first_tile && kh == 0) {  // the anchor: max over the first 32 keys (all valid: key0 < n)
+#pragma unroll
+          for (int qt = 0; qt < 4; ++qt) {
+            float mx = fmaxf(fmaxf(fmaxf(sc[qt][0][0], sc[qt][0][1]), fmaxf(sc[qt][0][2], sc[qt][0][3])),
+                             fmaxf(fmaxf(sc[qt][1][0], sc[qt][1][1]), fmaxf(sc[qt][1][2], sc[qt][1][3])));
+            mx = xmax16(mx);
+            set_ref(qt, mx);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              sc[qt][0][i] -= mx;
+              sc[qt][1][i] -= mx;
+            }
+          }
+        }
+      }
+      pv_half(Vl, kh, sc);
+    }
+    if constexpr (ANCH) {
+      bool big = false;
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) big |= lsum[qt][0] > 0x1p64f;
+      if (__ballot(big) != 0ull) {  // rare: shift the reference of those queries by 64
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt) {
+          const bool bq = lsum[qt][0] > 0x1p64f;
+          const float f = bq ? 0x1p-64f : 1.f;
+          if (bq) set_ref(qt, m[qt] + 64.f);
+          lsum[qt] *= f;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) o[dt][qt] *= f;
+        }
+      }
+    }
+  });
+
+  if constexpr (ANCH) {
+    // any non-finite row sum or output of the block -> the exact two-pass re-run (workgroup-uniform decision)
+    bool bad = false;
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      const float inv = 1.f / lsum[qt][0];
+      bad |= nonfinite(lsum[qt][0]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bad |= nonfinite(o[dt][qt][r] * inv);
+    }
+    int* flag = (int*)smem;  // the ring is idle after the loop's last barrier
+    if (lane == 0) flag[wave] = __ballot(bad && active) != 0ull;
     __builtin_amdgcn_s_barrier();
+    const bool redo = (flag[0] | flag[1] | flag[2] | flag[3]) != 0;
+    __builtin_amdgcn_s_barrier();  // flags read before the ring is refilled
+    if (redo) {
+      // pass 1: exact row maxima
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) set_ref(qt, 0.f);
+      float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      tile_loop([&](const char* Kl, const char*, int lim, bool) {
+#pragma unroll
+        for (int kh = 0; kh < HALVES; ++kh) {
+          f32x4 sc[4][2];
+          qk_half(Kl, kh, lim, sc);
+#pragma unroll
+          for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) mx[qt] = fmaxf(mx[qt], fmaxf(sc[qt][0][i], sc[qt][1][i]));
+        }
+      });
+      // pass 2: p = exp2(s - max) <= 1
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) set_ref(qt, xmax16(mx[qt]));
+      zero_acc();
+      tile_loop([&](const char* Kl, const char* Vl, int lim, bool) {
+#pragma unroll
+        for (int kh = 0; kh < HALVES; ++kh) {
+          f32x4 sc[4][2];
+          qk_half(Kl, kh, lim, sc);
+          pv_half(Vl, kh, sc);
+        }
+      });
+    }
   }
+
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
     const float l_tot = lsum[qt][0];
@@ -832,14 +982,14 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) *(f32x4*)(rec + dt * 16 + 4 * g) = o[dt][qt];
       if (g == 0) {
-        rec[64] = 0.f;
+        rec[64] = m[qt];
         rec[65] = l_tot;
       }
       continue;
     }
     if (q >= d.Nq) continue;
     const float inv = 1.f / l_tot;
-    if (d.lse != nullptr && g == 0) d.lse[((int64_t)b * d.H + h) * d.Nq + q] = __log2f(l_tot);
+    if (d.lse != nullptr && g == 0) d.lse[((int64_t)b * d.H + h) * d.Nq + q] = m[qt] + __log2f(l_tot);
     bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64 + 4 * g;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
@@ -1241,6 +1391,9 @@ static const AttnVar attn_vars[] = {
     {(const void*)attn_fwd<MODE_BOUNDED>, (const void*)attn_fwd<MODE_BOUNDED, true>, NW * 64},
     {(const void*)attn_fwd_w64<false>, (const void*)attn_fwd_w64<true>, NW4 * 64},
     {(const void*)attn_fwd_s16<false>, (const void*)attn_fwd_s16<true>, NW4 * 64},
+    {(const void*)attn_fwd_s16<false, true>, (const void*)attn_fwd_s16<true, true>, NW4 * 64},
+    {(const void*)attn_fwd_s16<false, false, 1>, (const void*)attn_fwd_s16<true, false, 1>, NW4 * 64},
+    {(const void*)attn_fwd_s16<false, true, 1>, (const void*)attn_fwd_s16<true, true, 1>, NW4 * 64},
 };
 constexpr int ATTN_NVAR = sizeof(attn_vars) / sizeof(attn_vars[0]);
 
@@ -1285,14 +1438,21 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
       slots_v[i] = per_cu * cus;
     }
   }
-  // BOUNDED scores: the two-blocks-per-wave kernel (default), VP_ATTN_BOUNDED_MODE=lazy the running-max kernel,
-  // =w32 the 8-wave one-block-per-wave kernel (A/B)
-  int variant = 0;
-  if (d->flags & VP_ATTN_BOUNDED_SCORES) {
-    const char* e = getenv("VP_ATTN_BOUNDED_MODE");
-    variant = (e != nullptr && e[0] == 'l') ? 0 : (e != nullptr && e[0] == 'w' && e[1] == '3') ? 1
-            : (e != nullptr && e[0] == 's') ? 3 : 2;
-  }
+  // BOUNDED scores: the two-blocks-per-wave kernel (default); VP_ATTN_BOUNDED_MODE = lazy (the running-max kernel),
+  // w32 (8 waves, one block per wave), s16 (16x16x32 MFMA), a16 (s16 with the anchored softmax), w64 (default).
+  // Unbounded scores: the running-max kernel; VP_ATTN_UNBOUNDED_MODE=a16 the anchored kernel (A/B).
+  auto pick = [](const char* e, int dflt) {
+    if (e == nullptr || e[0] == 0) return dflt;
+    if (e[0] == 'l') return 0;
+    if (e[0] == 'w' && e[1] == '3') return 1;
+    if (e[0] == 'w' && e[1] == '6') return 2;
+    if (e[0] == 's') return e[3] == 'i' ? 5 : 3;  // s16 / s16i
+    if (e[0] == 'a') return e[3] == 'i' ? 6 : 4;  // a16 / a16i
+    return dflt;
+  };
+  int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 2)
+                                                    : pick(getenv("VP_ATTN_UNBOUNDED_MODE"), 0);
+  if (!(d->flags & VP_ATTN_BOUNDED_SCORES) && variant != 4 && variant != 6) variant = 0;  // unbounded: lazy/anchored
   pl.v = &attn_vars[variant];
   const int slots = slots_v[variant];
   const int nqb = (d->Nq + QB - 1) / QB;
