@@ -467,6 +467,9 @@ def main():
                          "as a window-stage pipeline (point-to-point hand-offs; = --config 4)")
     ap.add_argument("--bcast", default="scatter_allgather", choices=("scatter_allgather", "broadcast"),
                     help="weight replication for N > 1 (distributed.broadcast_module)")
+    ap.add_argument("--qk-gamma", type=float, default=0.0,
+                    help="> 0: every norm_q / norm_k gain drawn U(0.1, G) per channel (trained-like qk-LayerNorm "
+                         "weights; past the static score bound the attention runs the anchored kernel)")
     args = ap.parse_args()
     set_config(args.config)
 
@@ -510,6 +513,18 @@ def main():
 
     t_setup = time.time()
     tr, br, t_bcast = build_models(device, 1234, rank, world, args.bcast)
+    bounded_layers = None
+    if args.qk_gamma > 0:
+        from videopainter_amd.attention_processor import bounded_scores
+        gq = torch.Generator().manual_seed(77)
+        with torch.no_grad():
+            for m in (tr, br):
+                for blk in m.transformer_blocks:
+                    for ln in (blk.attn1.norm_q, blk.attn1.norm_k):
+                        ln.weight.copy_((0.1 + (args.qk_gamma - 0.1) * torch.rand(64, generator=gq)).to(ln.weight))
+        bounded_layers = sum(bounded_scores(blk.attn1) for m in (tr, br) for blk in m.transformer_blocks)
+        log(f"[bench] qk-norm gains U(0.1, {args.qk_gamma}): {bounded_layers} of "
+            f"{len(tr.transformer_blocks) + len(br.transformer_blocks)} layers within the static score bound")
     sch = CogVideoXDPMScheduler(snr_shift_scale=1.0, prediction_type="v_prediction", rescale_betas_zero_snr=True,
                                 clip_sample=False, set_alpha_to_one=True, timestep_spacing="trailing")
     sch.set_timesteps(50)
@@ -609,7 +624,9 @@ def main():
                                     + (", QKV projection + attention + FeedForward in fp8" if args.config == 5
                                        else "")),
                        "clips": clips, "cfg_batch": B, "tokens": NTOK, "layers": L, "branch_layers": LB,
-                       "parallelism": par},
+                       "parallelism": par,
+                       **({"qk_norm_gain_max": args.qk_gamma, "layers_within_static_score_bound": bounded_layers}
+                          if args.qk_gamma > 0 else {})},
             "roofline": rf,
             "roofline_kernels": classes,
             "step_mfma_frac": step_frac,

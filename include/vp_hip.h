@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 9
+#define VP_ABI_VERSION 10
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
@@ -179,6 +179,11 @@ typedef struct vp_attn_desc {
                     from the norm weights: videopainter_amd.kernels.score_bound_log2. */
   float* lse;     /* optional fp32 [B, H, Nq]: per query log2-sum-exp2 of the scaled log2-unit scores (m + log2 l), the
                      softmax statistics vp_attention_bwd_bf16 recomputes P from (bf16 kernel only; NULL: not written) */
+  const int32_t* k2_full; /* optional int32 [B] (device), a hint: segment-2 rows n >= k2_full[b] of V2 are zero
+                             (the caller guarantees it), so those keys enter only the row sums — the resample
+                             processor's null keys, partitioned behind its masked keys by vp_partition_rows_index.
+                             The 16x16x32 kernels skip their V^T DMA, reads and PV products for whole tiles past
+                             k2_full[b]; the other kernels read the zeros.  NULL: no hint. */
 } vp_attn_desc;
 #define VP_ATTN_BOUNDED_SCORES 1
 #define VP_ATTN_SCORE_BOUND 60.0f
@@ -246,7 +251,7 @@ int vp_adaln_modulate_mx_fp8(const void* x, void* q, void* scales, int32_t B, in
 int vp_head_norm_rope_bf16(const void* x_in, int64_t ld_in, int64_t bs_in, void* x_out, int64_t ld_out,
                            int64_t bs_out, int32_t B, int32_t Ntok, int32_t H, int32_t text_len, const void* ln_w,
                            const void* ln_b, float eps, const float* cos, const float* sin, const uint8_t* tok_mask,
-                           int64_t mask_bstride, float pre_scale, void* stream);
+                           int64_t mask_bstride, float pre_scale, const int32_t* dst_rows, void* stream);
 
 /* The same LN(64) + RoPE, output e4m3 (x_bf16 * out_mul, clamped to +-448, RNE) for the fp8 attention; ld_out /
  * bs_out in bytes. */
@@ -256,9 +261,20 @@ int vp_head_norm_rope_fp8(const void* x_in, int64_t ld_in, int64_t bs_in, void* 
                           void* stream);
 
 /* y[b, n, :] = rnd(rnd(x[b, n, :] * tok_mask[b, n]) * scale) — the masked value copy of the resample processor. */
+/* (vp_head_norm_rope_bf16 and vp_mask_scale_rows_bf16 with dst_rows != NULL: output row n of batch b is written to
+ * row dst_rows[b * Ntok + n] — the partition permutation of vp_partition_rows_index; the output must not alias the
+ * input.) */
+
+/* Stable partition of the resample processor's token mask (attention_processor.py:2244-2252): per batch row b,
+ * counts[b] = #{n : mask[b, n] != 0}, dst_rows[b * N + n] = the rank of n among the set rows, or counts[b] + its
+ * rank among the clear rows.  Written once per window (the mask is the same for every layer and step); the masked
+ * keys / values then form the first counts[b] rows of the attention's second segment and the null keys (zero
+ * values) the rest (vp_attn_desc.k2_full). */
+int vp_partition_rows_index(const uint8_t* mask, int64_t mask_bstride, int32_t B, int32_t N, int32_t* dst_rows,
+                            int32_t* counts, void* stream);
 int vp_mask_scale_rows_bf16(const void* x_in, int64_t ld_in, int64_t bs_in, void* y, int64_t ld_out, int64_t bs_out,
                             int32_t B, int32_t Ntok, int32_t D, const uint8_t* tok_mask, int64_t mask_bstride,
-                            float scale, void* stream);
+                            float scale, const int32_t* dst_rows, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * Output head norms — norm_final (cogvideox_transformer_3d.py:617-620) then AdaLayerNorm(chunk_dim=1)

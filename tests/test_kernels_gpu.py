@@ -23,18 +23,18 @@ def gemm_variant(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["lazy", "bounded", "w32", "s16", "w64", "a16"], ids=lambda v: f"attn_{v}")
+@pytest.fixture(params=["lazy", "bounded", "w32", "w64", "a16", "a16i", "s16i"], ids=lambda v: f"attn_{v}")
 def attn_variant(request, monkeypatch):
-    """lazy: the running-max kernel; bounded: the no-running-max kernel the host selects when the qk-norm bounds
-    every score (include/vp_hip.h VP_ATTN_BOUNDED_SCORES), the library default; w32: the same contract on the 8-wave
-    one-block-per-wave kernel; w64: two 32-query blocks per wave on the 32x32x16 MFMA; s16: 64 queries per wave on
-    the 16x16x32 MFMA (VP_ATTN_BOUNDED_MODE selects these three); a16: the anchored-softmax kernel on unbounded
-    scores (VP_ATTN_UNBOUNDED_MODE=a16)."""
+    """Unbounded-score launches: a16 (the anchored-softmax 16x16x32 kernel, the library default), a16i (its
+    per-query-tile PV order), lazy (the running-max kernel; VP_ATTN_UNBOUNDED_MODE).  Bounded-score launches
+    (include/vp_hip.h VP_ATTN_BOUNDED_SCORES, the host proved the bound): bounded = the library default (s16, 64
+    queries per wave on the 16x16x32 MFMA), w32 / w64 / s16i the 8-wave, two-blocks-per-wave 32x32x16 and
+    per-query-tile-PV forms (VP_ATTN_BOUNDED_MODE)."""
     monkeypatch.delenv("VP_ATTN_UNBOUNDED_MODE", raising=False)
-    if request.param == "a16":
-        monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
-        monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", "a16")
-    elif request.param in ("w32", "s16", "w64"):
+    monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
+    if request.param in ("lazy", "a16", "a16i"):
+        monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", request.param)
+    elif request.param in ("w32", "w64", "s16i"):
         monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", request.param)
     else:
         monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
@@ -44,7 +44,7 @@ def attn_variant(request, monkeypatch):
 def attn_kw(variant, q, k, scale=0.125, k2=None):
     """bounded_scores for the variant, after checking on the host that the inputs satisfy the bound (the contract
     the processors establish from the qk-norm weights)."""
-    if variant in ("lazy", "a16"):
+    if variant in ("lazy", "a16", "a16i"):
         return {}
     kk = k if k2 is None else torch.cat([k, k2], 1)
     B, Nq, D = q.shape
@@ -282,11 +282,14 @@ def test_attention_anchored_late_jump(jump, monkeypatch):
     assert torch.isfinite(out.float()).all() and r < 1e-2
 
 
-def test_attention_stepwise_max_growth():
+@pytest.mark.parametrize("mode", ["lazy", "a16"])
+def test_attention_stepwise_max_growth(mode, monkeypatch):
     """Running max grows by 0 / 0.5 / 3 / 8 nats at tile seams, so the deferred-max test (tile sum > 2^8) takes both
-    branches many times within one query block (cdna_hip_programming.md §5.4 rule 26).  (Scores up to ~300 in log2
-    units: outside the bounded-score contract, so only the running-max kernel applies.)"""
+    branches many times within one query block (cdna_hip_programming.md §5.4 rule 26); for the anchored kernel the
+    row sums pass 2^64 repeatedly (its rescale branch).  (Scores up to ~300 in log2 units: outside the bounded-score
+    contract.)"""
     from videopainter_amd import kernels as K
+    monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", mode)
     B, H, Nn = 1, 2, 1100
     g = torch.Generator().manual_seed(80)
     u = torch.randn(64, generator=g)
@@ -586,3 +589,67 @@ def test_gemm_splitk_small_m(M, Nn, Kk, segs, epi):
         again = torch.empty_like(out)
         K.gemm(a, ws, bs, again, **kw)
         assert torch.equal(again, out)
+
+
+@pytest.mark.parametrize("B,N", [(2, 1378), (1, 17776), (3, 65)])
+def test_partition_rows_index_and_permuted_writes(B, N):
+    """vp_partition_rows_index (stable: set rows first, then the clear rows, each in order; device-side counts) and
+    the permuted writes of vp_head_norm_rope_bf16 / vp_mask_scale_rows_bf16 (row n -> dst_rows[b, n]), bit-equal to
+    the unpermuted kernels followed by the permutation."""
+    from videopainter_amd import kernels as K
+    g = torch.Generator().manual_seed(N)
+    m = (torch.rand(B, N, generator=g) < 0.37).to(torch.uint8)
+    m[0, :min(N, 10)] = 0
+    dst, cnt = K.partition_rows_index(m.to(dev))
+    for b in range(B):
+        want = torch.empty(N, dtype=torch.int64)
+        idx1 = torch.nonzero(m[b]).flatten()
+        idx0 = torch.nonzero(m[b] == 0).flatten()
+        want[idx1] = torch.arange(len(idx1))
+        want[idx0] = len(idx1) + torch.arange(len(idx0))
+        assert int(cnt[b]) == len(idx1)
+        assert torch.equal(dst[b].cpu().long(), want)
+    H, T = 2, min(8, N // 2)
+    D = H * 64
+    x = bf(rnd(B, N, D, seed=5)).to(dev)
+    lw, lb = bf(rnd(64, seed=6)).to(dev), bf(rnd(64, seed=7) * 0.1).to(dev)
+    cos, sin = (torch.rand(N - T, 64, generator=g) * 2 - 1).to(dev), (torch.rand(N - T, 64, generator=g) * 2 - 1).to(dev)
+    ref = torch.empty_like(x)
+    K.head_norm_rope(x, ref, H, T, lw, lb, 1e-6, (cos, sin), tok_mask=m.to(dev), pre_scale=0.5)
+    got = torch.empty_like(x)
+    K.head_norm_rope(x, got, H, T, lw, lb, 1e-6, (cos, sin), tok_mask=m.to(dev), pre_scale=0.5, dst_rows=dst)
+    vref = torch.empty_like(x)
+    K.mask_scale_rows(x, vref, m.to(dev), 0.5)
+    vgot = torch.empty_like(x)
+    K.mask_scale_rows(x, vgot, m.to(dev), 0.5, dst_rows=dst)
+    for b in range(B):
+        perm = dst[b].long()
+        assert torch.equal(got[b][perm], ref[b]) and torch.equal(vgot[b][perm], vref[b])
+        assert not vgot[b, int(cnt[b]):].any()  # the null keys' values are zero (the k2_full contract)
+
+
+@pytest.mark.parametrize("mode", ["s16", "a16", "w64"])
+def test_attention_k2_full_hint(mode, monkeypatch):
+    """The k2_full hint (segment-2 keys past k2_full[b] have zero values: row sums only) gives the attention of the
+    same segments without the hint; per-batch split points, one straddling a tile, one past every tile."""
+    from videopainter_amd import kernels as K
+    if mode == "a16":
+        monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", "a16")
+        kw = {}
+    else:
+        monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", mode)
+        kw = dict(bounded_scores=True)
+    B, H, Nn, N2 = 3, 2, 700, 900
+    D = H * 64
+    q, k, v = (bf(rnd(B, Nn, D, seed=s) * 0.5).to(dev) for s in (90, 91, 92))
+    k2, v2 = bf(rnd(B, N2, D, seed=93) * 0.5).to(dev), bf(rnd(B, N2, D, seed=94)).to(dev)
+    full = torch.tensor([300, 0, 900], dtype=torch.int32)
+    for b in range(B):
+        v2[b, int(full[b]):] = 0
+    o_ref = torch.empty(B, Nn, D, device=dev, dtype=torch.bfloat16)
+    K.attention(q, k, v, o_ref, H, k2=k2, v2=v2, **kw)
+    o = torch.empty_like(o_ref)
+    K.attention(q, k, v, o, H, k2=k2, v2=v2, k2_full=full.to(dev), **kw)
+    hd = lambda x: x.float().cpu().reshape(B, -1, H, 64).transpose(1, 2)  # noqa: E731
+    ref = _sdpa(hd(q), torch.cat([hd(k), hd(k2)], 2), torch.cat([hd(v), hd(v2)], 2)).transpose(1, 2).reshape(B, Nn, D)
+    assert rel(o, ref) < 1e-2 and rel(o, o_ref) < 2e-3

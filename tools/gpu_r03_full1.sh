@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 3: full GPU suite on the s16 / anchored defaults, then config-2 (default and gamma-6 qk-norm) and config-4
+# benches, and a kernel-trace profile of the default config-2 bench
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+run() { local name=$1; shift; local to=$1; shift
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"
+  [ $rc -ne 0 ] && exit $rc; return 0; }
+run r03_gtests1 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -rA
+run r03_bench_c2 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline
+run r03_bench_c2_g6 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --qk-gamma 6
+run r03_bench_c4 500 python bench.py --config 4 --steps 2 --warmup 1
+exit 0

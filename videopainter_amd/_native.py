@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -43,7 +43,8 @@ class AttnDesc(C.Structure):
                 ("Nk", i32), ("Nk2", i32),
                 ("K2", vp), ("V2", vp), ("k2_sb", i64), ("k2_sn", i64), ("v2_sb", i64), ("v2_sn", i64),
                 ("O", vp), ("o_sb", i64), ("o_sn", i64),
-                ("scale", f32), ("out_scale", f32), ("accumulate", i32), ("flags", i32), ("lse", vp)]
+                ("scale", f32), ("out_scale", f32), ("accumulate", i32), ("flags", i32), ("lse", vp),
+                ("k2_full", vp)]
 
 
 class GemmMxDesc(C.Structure):
@@ -109,8 +110,9 @@ _SIGS = {
     "vp_head_norm_rope_fp8": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp, vp, f32, vp]),
     "vp_adaln_modulate_bf16": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, f32, vp, i64, vp]),
     "vp_head_norm_rope_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, i64,
-                                     f32, vp]),
-    "vp_mask_scale_rows_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, vp, i64, f32, vp]),
+                                     f32, vp, vp]),
+    "vp_mask_scale_rows_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, vp, i64, f32, vp, vp]),
+    "vp_partition_rows_index": (i32, [vp, i64, i32, i32, vp, vp, vp]),
     "vp_final_norm_bf16": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp, i64, vp]),
     "vp_linear_small_bf16": (i32, [vp, i64, vp, vp, vp, i64, i32, i32, i32, i32, i32, vp]),
     "vp_timestep_embedding_bf16": (i32, [vp, vp, i32, i32, f32, vp]),

@@ -224,22 +224,28 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
         q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
         k2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
         v2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
-        if prev_hidden_states is not None and prev_clip_weight is not None and prev_clip_weight > 0.0:
-            m = _u8(prev_resample_mask)
+        prev = prev_hidden_states is not None and prev_clip_weight is not None and prev_clip_weight > 0.0
+        if not prev and resample_mask is None:
+            raise ValueError("the resample processor needs resample_mask (id_pool_resample needs masks)")
+        m = _u8(prev_resample_mask if prev else resample_mask)
+        # The second segment in partitioned row order: the masked rows' keys / values first, then the null keys (LN
+        # of a zeroed row, rotated) whose values are zero — the attention kernel takes those as row-sum-only keys
+        # (k2_full).  The order of keys does not change attention; env VP_RESAMPLE_PARTITION=0: original order (A/B).
+        dst = cnt = None
+        if os.environ.get("VP_RESAMPLE_PARTITION", "1") != "0":
+            dst, cnt = K.partition_rows_index(m)
+        if prev:
             pkv = _kv(attn, prev_hidden_states.to(BF16).contiguous())
             w = float(prev_clip_weight)
             K.head_norm_rope(pkv[..., :D], k2, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps,
-                             rope, tok_mask=m, pre_scale=w)
-            K.mask_scale_rows(pkv[..., D:], v2, m, w)
+                             rope, tok_mask=m, pre_scale=w, dst_rows=dst)
+            K.mask_scale_rows(pkv[..., D:], v2, m, w, dst_rows=dst)
         else:
-            if resample_mask is None:
-                raise ValueError("the resample processor needs resample_mask (id_pool_resample needs masks)")
-            m = _u8(resample_mask)
             K.head_norm_rope(k, k2, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope,
-                             tok_mask=m, pre_scale=1.0)
-            K.mask_scale_rows(v, v2, m, 1.0)
+                             tok_mask=m, pre_scale=1.0, dst_rows=dst)
+            K.mask_scale_rows(v, v2, m, 1.0, dst_rows=dst)
         K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, attn.norm_q.eps, rope)
         K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope)
         o = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
-        K.attention(q, k, v, o, H, k2=k2, v2=v2, scale=attn.scale, bounded_scores=bounded_scores(attn))
+        K.attention(q, k, v, o, H, k2=k2, v2=v2, scale=attn.scale, bounded_scores=bounded_scores(attn), k2_full=cnt)
         return o

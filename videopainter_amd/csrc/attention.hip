@@ -712,6 +712,9 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
   const int ntiles_all = tiles1 + tiles2;
   const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
   const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
+  // segment-2 keys past k2_full[b] have zero values: their whole tiles skip the V^T DMA, reads and PV MFMAs
+  const int k2f = d.k2_full != nullptr ? __builtin_amdgcn_readfirstlane(d.k2_full[b]) : 0x7fffffff;
+  auto tile_full = [&](int ti) { return ti < tiles1 || (ti - tiles1) * KB < k2f; };
 
   const int qw0 = qb * QB + wave * 64;  // first query of this wave
   bf16x8 qf[4][2];                      // Q^T B operands: query 16 qt + l % 16, dims 32 c + 8 (l / 16) + j
@@ -746,12 +749,21 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
     const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
     const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
     const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
+    if (tile_full(ti)) {
 #pragma unroll
-    for (int i = 0; i < PPW4; ++i) {
-      const int pc = wave + i * NW4;
-      const int r = min(prow[i], last);
-      glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + pc * 1024);
-      glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
+      for (int i = 0; i < PPW4; ++i) {
+        const int pc = wave + i * NW4;
+        const int r = min(prow[i], last);
+        glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + pc * 1024);
+        glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PPW4; ++i) {
+        const int pc = wave + i * NW4;
+        const int r = min(prow[i], last);
+        glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + pc * 1024);
+      }
     }
   };
 
@@ -780,7 +792,7 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
 
   const bool active = qw0 < d.Nq;  // wave-uniform
 
-  // one pass over this workgroup's key tiles through the LDS ring; body(Kl, Vl, lim, first_tile) per tile
+  // one pass over this workgroup's key tiles through the LDS ring; body(Kl, Vl, lim, first_tile, full) per tile
   auto tile_loop = [&](auto&& body) {
     issue(tbeg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -789,13 +801,13 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
       if (ti + 1 < tend) issue(ti + 1);
       const char* Kl = slot_of(ti);
       const Seg sg = tile_seg(d, ti, tiles1, b, h);
-      if (active) body(Kl, Kl + KT, sg.n - sg.key0, ti == tbeg);
+      if (active) body(Kl, Kl + KT, sg.n - sg.key0, ti == tbeg, tile_full(ti));
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
   };
   // S^T of one 32-key half: key 32 kh + 16 kt + 4 (l / 16) + i, C-initialised with negm (-m, or 0)
-  auto qk_half = [&](const char* Kl, int kh, int lim, f32x4 (&sc)[4][2]) {
+  auto qk_half = [&](const char* Kl, int kh, int lim, f32x4 (&sc)[4][2], auto mask_c) {
     bf16x8 kf[2][2];  // K A operands: key 32 kh + 16 kt + l % 16, dims 32 c + 8 (l / 16) + j
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -812,18 +824,22 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
         sc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][0], qf[qt][0], negm[qt], 0, 0, 0);
         sc[qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][1], qf[qt][1], sc[qt][kt], 0, 0, 0);
       }
-    if (lim < KB) {
+    if constexpr (decltype(mask_c)::value) {
+      if (lim < KB) {
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bool dead = kh * 32 + kt * 16 + 4 * g + i >= lim;
+          for (int i = 0; i < 4; ++i) {
+            const bool dead = kh * 32 + kt * 16 + 4 * g + i >= lim;
 #pragma unroll
-          for (int qt = 0; qt < 4; ++qt)
-            if (dead) sc[qt][kt][i] = -INFINITY;
-        }
+            for (int qt = 0; qt < 4; ++qt)
+              if (dead) sc[qt][kt][i] = -INFINITY;
+          }
+      }
     }
   };
+  using MaskT = std::integral_constant<bool, true>;
+  using MaskF = std::integral_constant<bool, false>;
   // P = exp2(S) packed as the P^T B operand, then O^T += V^T P^T and the row sums
   auto pv_half = [&](const char* Vl, int kh, const f32x4 (&sc)[4][2]) {
     if constexpr (ORD == 1) {
@@ -869,6 +885,19 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qt], lsum[qt], 0, 0, 0);
   };
+  // keys with zero values: exp2 + pack and the row sums only
+  auto rs_half = [&](const f32x4 (&sc)[4][2]) {
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      bf16x8 pq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pq[i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][0][i]));
+        pq[4 + i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][1][i]));
+      }
+      lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pq, lsum[qt], 0, 0, 0);
+    }
+  };
   auto zero_acc = [&]() {
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
@@ -884,11 +913,11 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
 
   // ---- main pass ----
   zero_acc();
-  tile_loop([&](const char* Kl, const char* Vl, int lim, bool first_tile) {
+  tile_loop([&](const char* Kl, const char* Vl, int lim, bool first_tile, bool full) {
 #pragma unroll
     for (int kh = 0; kh < HALVES; ++kh) {
       f32x4 sc[4][2];
-      qk_half(Kl, kh, lim, sc);
+      qk_half(Kl, kh, lim, sc, MaskT{});
       if constexpr (ANCH) {
         if (first_tile && kh == 0) {  // the anchor: max over the first 32 keys (all valid: key0 < n)
 #pragma unroll
@@ -905,7 +934,8 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
           }
         }
       }
-      pv_half(Vl, kh, sc);
+      if (full) pv_half(Vl, kh, sc);
+      else rs_half(sc);
     }
     if constexpr (ANCH) {
       bool big = false;
@@ -947,11 +977,11 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
 #pragma unroll
       for (int qt = 0; qt < 4; ++qt) set_ref(qt, 0.f);
       float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-      tile_loop([&](const char* Kl, const char*, int lim, bool) {
+      tile_loop([&](const char* Kl, const char*, int lim, bool, bool) {
 #pragma unroll
         for (int kh = 0; kh < HALVES; ++kh) {
           f32x4 sc[4][2];
-          qk_half(Kl, kh, lim, sc);
+          qk_half(Kl, kh, lim, sc, MaskT{});
 #pragma unroll
           for (int qt = 0; qt < 4; ++qt)
 #pragma unroll
@@ -962,12 +992,13 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
 #pragma unroll
       for (int qt = 0; qt < 4; ++qt) set_ref(qt, xmax16(mx[qt]));
       zero_acc();
-      tile_loop([&](const char* Kl, const char* Vl, int lim, bool) {
+      tile_loop([&](const char* Kl, const char* Vl, int lim, bool, bool full) {
 #pragma unroll
         for (int kh = 0; kh < HALVES; ++kh) {
           f32x4 sc[4][2];
-          qk_half(Kl, kh, lim, sc);
-          pv_half(Vl, kh, sc);
+          qk_half(Kl, kh, lim, sc, MaskT{});
+          if (full) pv_half(Vl, kh, sc);
+          else rs_half(sc);
         }
       });
     }
@@ -1438,9 +1469,11 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
       slots_v[i] = per_cu * cus;
     }
   }
-  // BOUNDED scores: the two-blocks-per-wave kernel (default); VP_ATTN_BOUNDED_MODE = lazy (the running-max kernel),
-  // w32 (8 waves, one block per wave), s16 (16x16x32 MFMA), a16 (s16 with the anchored softmax), w64 (default).
-  // Unbounded scores: the running-max kernel; VP_ATTN_UNBOUNDED_MODE=a16 the anchored kernel (A/B).
+  // BOUNDED scores (the host proved |score| <= VP_ATTN_SCORE_BOUND): the 16x16x32 kernel (s16, default);
+  // VP_ATTN_BOUNDED_MODE = lazy (running max), w32 (8 waves, one 32-query block per wave), w64 (two blocks per wave,
+  // 32x32x16), a16 (s16 with the anchored softmax), s16i / a16i (per-query-tile PV order) for A/B.
+  // Unbounded scores: the anchored s16 kernel (a16, default: no bound needed, no host sync); VP_ATTN_UNBOUNDED_MODE =
+  // lazy (the running-max kernel) or a16i.
   auto pick = [](const char* e, int dflt) {
     if (e == nullptr || e[0] == 0) return dflt;
     if (e[0] == 'l') return 0;
@@ -1450,8 +1483,8 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
     if (e[0] == 'a') return e[3] == 'i' ? 6 : 4;  // a16 / a16i
     return dflt;
   };
-  int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 2)
-                                                    : pick(getenv("VP_ATTN_UNBOUNDED_MODE"), 0);
+  int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 3)
+                                                    : pick(getenv("VP_ATTN_UNBOUNDED_MODE"), 4);
   if (!(d->flags & VP_ATTN_BOUNDED_SCORES) && variant != 4 && variant != 6) variant = 0;  // unbounded: lazy/anchored
   pl.v = &attn_vars[variant];
   const int slots = slots_v[variant];

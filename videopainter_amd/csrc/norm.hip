@@ -224,7 +224,8 @@ __global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restr
                                                             const float* __restrict__ cosp,
                                                             const float* __restrict__ sinp,
                                                             const uint8_t* __restrict__ tok_mask, int64_t mask_bs,
-                                                            float pre_scale, float out_mul) {
+                                                            float pre_scale, float out_mul,
+                                                            const int32_t* __restrict__ dst_rows) {
   const int64_t vec = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
   const int g = threadIdx.x & 3;
   const bool valid = vec < nvec;
@@ -251,7 +252,8 @@ __global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restr
   ln64_rope16<1, 2>(x, g, lw, lb, eps, rot ? cosp + (int64_t)(n - text_len) * 64 : nullptr,
                     rot ? sinp + (int64_t)(n - text_len) * 64 : nullptr);
   if (valid) {
-    const int64_t o = (int64_t)b * bs_out + (int64_t)n * ld_out + h * 64 + g * 4;
+    const int nd = dst_rows != nullptr ? dst_rows[(int64_t)b * Ntok + n] : n;
+    const int64_t o = (int64_t)b * bs_out + (int64_t)nd * ld_out + h * 64 + g * 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if constexpr (FP8) {
@@ -276,7 +278,7 @@ __global__ __launch_bounds__(256) void mask_scale_rows_kernel(const bf16* __rest
                                                              int64_t bs_in, bf16* __restrict__ y, int64_t ld_out,
                                                              int64_t bs_out, int64_t nchunks, int Ntok, int D,
                                                              const uint8_t* __restrict__ tok_mask, int64_t mask_bs,
-                                                             float scale) {
+                                                             float scale, const int32_t* __restrict__ dst_rows) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= nchunks) return;
   const int cpr = D / 8;
@@ -289,7 +291,53 @@ __global__ __launch_bounds__(256) void mask_scale_rows_kernel(const bf16* __rest
   bf16x8 o;
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = f2bf(rbf(rbf(bf2f(x[e]) * m) * scale));
-  *(bf16x8*)(y + (int64_t)b * bs_out + (int64_t)n * ld_out + c * 8) = o;
+  const int nd = dst_rows != nullptr ? dst_rows[(int64_t)b * Ntok + n] : n;
+  *(bf16x8*)(y + (int64_t)b * bs_out + (int64_t)nd * ld_out + c * 8) = o;
+}
+
+// ---- stable partition index of the resample processor's token mask (vp_partition_rows_index): one workgroup per
+// batch row; rows with mask != 0 go first in order, the others after them in order ----
+__global__ __launch_bounds__(1024) void partition_index_kernel(const uint8_t* __restrict__ mask, int64_t mask_bs, int N,
+                                                              int32_t* __restrict__ dst, int32_t* __restrict__ counts) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint8_t* m = mask + (int64_t)b * mask_bs;
+  // pass 1: the number of set rows
+  int cnt = 0;
+  for (int n = tid; n < N; n += 1024) cnt += m[n] != 0;
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  if (lane == 0) wsum[wv] = cnt;
+  __syncthreads();
+  int total = 0;
+  for (int w = 0; w < 16; ++w) total += wsum[w];
+  if (tid == 0) {
+    counts[b] = total;
+    carry = 0;
+  }
+  __syncthreads();
+  // pass 2: 1024-row chunks, exclusive scan of the set flags
+  for (int base = 0; base < N; base += 1024) {
+    const int n = base + tid;
+    const int f = (n < N && m[n] != 0) ? 1 : 0;
+    const unsigned long long bal = __ballot(f);
+    const int below = __popcll(bal & ((1ull << lane) - 1ull));
+    __syncthreads();  // wsum reuse
+    if (lane == 0) wsum[wv] = __popcll(bal);
+    __syncthreads();
+    int pre = carry;
+    for (int w = 0; w < wv; ++w) pre += wsum[w];
+    pre += below;  // set rows before n
+    if (n < N) dst[(int64_t)b * N + n] = f ? pre : total + (n - pre);
+    __syncthreads();
+    if (tid == 0) {
+      int add = 0;
+      for (int w = 0; w < 16; ++w) add += wsum[w];
+      carry += add;
+    }
+    __syncthreads();
+  }
 }
 
 }  // namespace
@@ -338,15 +386,17 @@ extern "C" int vp_head_norm_rope_bf16(const void* x_in, int64_t ld_in, int64_t b
                                       int64_t bs_out, int32_t B, int32_t Ntok, int32_t H, int32_t text_len,
                                       const void* ln_w, const void* ln_b, float eps, const float* cos,
                                       const float* sin, const uint8_t* tok_mask, int64_t mask_bstride,
-                                      float pre_scale, void* stream) {
+                                      float pre_scale, const int32_t* dst_rows, void* stream) {
   if (!x_in || !x_out || !ln_w || !ln_b || B <= 0 || Ntok <= 0 || H <= 0) return VP_ERR_ARG;
+  if (dst_rows != nullptr && x_in == x_out) return VP_ERR_ARG;  // a permuted write must not alias its input
   if ((ld_in % 8) || (ld_out % 8) || (bs_in % 8) || (bs_out % 8)) return VP_ERR_ARG;
   if ((cos == nullptr) != (sin == nullptr)) return VP_ERR_ARG;
   const int64_t nvec = (int64_t)B * Ntok * H;
   const int64_t grid = (nvec + 63) / 64;
   hipLaunchKernelGGL(head_norm_rope_kernel<false>, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
                      (const bf16*)x_in, ld_in, bs_in, x_out, ld_out, bs_out, nvec, Ntok, H, text_len,
-                     (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, tok_mask, mask_bstride, pre_scale, 1.f);
+                     (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, tok_mask, mask_bstride, pre_scale, 1.f,
+                     dst_rows);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
@@ -362,20 +412,30 @@ extern "C" int vp_head_norm_rope_fp8(const void* x_in, int64_t ld_in, int64_t bs
   const int64_t grid = (nvec + 63) / 64;
   hipLaunchKernelGGL(head_norm_rope_kernel<true>, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
                      (const bf16*)x_in, ld_in, bs_in, q_out, ld_out, bs_out, nvec, Ntok, H, text_len,
-                     (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, nullptr, 0, 1.f, out_mul);
+                     (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, nullptr, 0, 1.f, out_mul, nullptr);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
 
 extern "C" int vp_mask_scale_rows_bf16(const void* x_in, int64_t ld_in, int64_t bs_in, void* y, int64_t ld_out,
                                        int64_t bs_out, int32_t B, int32_t Ntok, int32_t D, const uint8_t* tok_mask,
-                                       int64_t mask_bstride, float scale, void* stream) {
+                                       int64_t mask_bstride, float scale, const int32_t* dst_rows, void* stream) {
   if (!x_in || !y || !tok_mask || B <= 0 || Ntok <= 0 || D <= 0 || (D % 8)) return VP_ERR_ARG;
+  if (dst_rows != nullptr && x_in == y) return VP_ERR_ARG;
   if ((ld_in % 8) || (ld_out % 8) || (bs_in % 8) || (bs_out % 8)) return VP_ERR_ARG;
   const int64_t nchunks = (int64_t)B * Ntok * (D / 8);
   hipLaunchKernelGGL(mask_scale_rows_kernel, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, (const bf16*)x_in, ld_in, bs_in, (bf16*)y, ld_out, bs_out, nchunks, Ntok,
-                     D, tok_mask, mask_bstride, scale);
+                     D, tok_mask, mask_bstride, scale, dst_rows);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_partition_rows_index(const uint8_t* mask, int64_t mask_bstride, int32_t B, int32_t N,
+                                       int32_t* dst_rows, int32_t* counts, void* stream) {
+  if (!mask || !dst_rows || !counts || B <= 0 || N <= 0 || mask_bstride < N) return VP_ERR_ARG;
+  hipLaunchKernelGGL(partition_index_kernel, dim3((unsigned)B), dim3(1024), 0, (hipStream_t)stream, mask,
+                     mask_bstride, N, dst_rows, counts);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }

@@ -302,10 +302,12 @@ def mx_mfma_probe(A: torch.Tensor, B: torch.Tensor, sa: torch.Tensor, sb: torch.
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, heads: int, *,
               k2: Optional[torch.Tensor] = None, v2: Optional[torch.Tensor] = None, scale: float = 0.125,
               out_scale: float = 1.0, accumulate: bool = False, bounded_scores: bool = False,
-              lse: Optional[torch.Tensor] = None) -> torch.Tensor:
+              lse: Optional[torch.Tensor] = None, k2_full: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q, k, v, out: [B, N, heads*64] views (last dim contiguous, any row/batch stride); k2 / v2: an optional second
     K/V segment of the same form.  The native side sees only pointers and strides, so every extent is checked here.
-    lse: optional fp32 [B, heads, Nq] receiving the softmax statistics the backward needs."""
+    lse: optional fp32 [B, heads, Nq] receiving the softmax statistics the backward needs.  k2_full: optional int32
+    [B] (device): segment-2 keys at or past k2_full[b] have zero values (v2 rows there must be zero) and enter only the
+    row sums (include/vp_hip.h vp_attn_desc.k2_full)."""
     segs = [(q, "q"), (k, "k"), (v, "v"), (out, "out")]
     if (k2 is None) != (v2 is None):
         raise ValueError("k2 and v2 must be given together")
@@ -333,6 +335,13 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
         d.K2, d.V2 = _p(k2), _p(v2)
         d.k2_sb, d.k2_sn, d.v2_sb, d.v2_sn = k2.stride(0), k2.stride(1), v2.stride(0), v2.stride(1)
         d.Nk2 = k2.shape[1]
+    if k2_full is not None:
+        if k2 is None:
+            raise ValueError("k2_full needs a second segment")
+        _chk(k2_full, "k2_full", torch.int32)
+        if tuple(k2_full.shape) != (q.shape[0],) or not k2_full.is_contiguous():
+            raise ValueError(f"k2_full must be contiguous int32 [{q.shape[0]}]")
+        d.k2_full = _p(k2_full)
     d.O, d.o_sb, d.o_sn = _p(out), out.stride(0), out.stride(1)
     d.scale, d.out_scale, d.accumulate = scale, out_scale, int(accumulate)
     if lse is not None:
@@ -517,8 +526,10 @@ def adaln_modulate(x: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, mod:
 
 
 def head_norm_rope(x_in: torch.Tensor, x_out: torch.Tensor, heads: int, text_len: int, ln_w, ln_b, eps: float,
-                   rope=None, tok_mask: Optional[torch.Tensor] = None, pre_scale: float = 1.0) -> torch.Tensor:
-    """x_in / x_out: [B, N, heads*64] views with contiguous last dim."""
+                   rope=None, tok_mask: Optional[torch.Tensor] = None, pre_scale: float = 1.0,
+                   dst_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x_in / x_out: [B, N, heads*64] views with contiguous last dim.  dst_rows: int32 [B, N] output row of each input
+    row (partition_rows_index), or None."""
     _chk(x_in, "x_in")
     _chk(x_out, "x_out")
     B, Ntok, _ = x_in.shape
@@ -533,21 +544,43 @@ def head_norm_rope(x_in: torch.Tensor, x_out: torch.Tensor, heads: int, text_len
     if tok_mask is not None:
         _chk(tok_mask, "tok_mask", torch.uint8)
         mb = tok_mask.stride(0)
+    _chk_rows(dst_rows, B, Ntok)
     N.check(N.lib().vp_head_norm_rope_bf16(_p(x_in), x_in.stride(1), x_in.stride(0), _p(x_out), x_out.stride(1),
                                            x_out.stride(0), B, Ntok, heads, text_len, _p(ln_w), _p(ln_b), eps,
-                                           _p(cos), _p(sin), _p(tok_mask), mb, pre_scale, _stream()),
+                                           _p(cos), _p(sin), _p(tok_mask), mb, pre_scale, _p(dst_rows), _stream()),
             "vp_head_norm_rope_bf16")
     return x_out
 
 
-def mask_scale_rows(x_in: torch.Tensor, out: torch.Tensor, tok_mask: torch.Tensor, scale: float) -> torch.Tensor:
+def _chk_rows(dst_rows: Optional[torch.Tensor], B: int, Ntok: int) -> None:
+    if dst_rows is not None:
+        _chk(dst_rows, "dst_rows", torch.int32)
+        if tuple(dst_rows.shape) != (B, Ntok) or not dst_rows.is_contiguous():
+            raise ValueError(f"dst_rows must be contiguous int32 [{B}, {Ntok}], got {tuple(dst_rows.shape)}")
+
+
+def partition_rows_index(tok_mask: torch.Tensor):
+    """Stable partition of the token mask [B, N] (uint8): (dst_rows int32 [B, N], counts int32 [B]) — set rows
+    first.  Device-side counts: no host sync."""
+    _chk(tok_mask, "tok_mask", torch.uint8)
+    B, Ntok = tok_mask.shape
+    dst = torch.empty(B, Ntok, device=tok_mask.device, dtype=torch.int32)
+    cnt = torch.empty(B, device=tok_mask.device, dtype=torch.int32)
+    N.check(N.lib().vp_partition_rows_index(_p(tok_mask), tok_mask.stride(0), B, Ntok, _p(dst), _p(cnt), _stream()),
+            "vp_partition_rows_index")
+    return dst, cnt
+
+
+def mask_scale_rows(x_in: torch.Tensor, out: torch.Tensor, tok_mask: torch.Tensor, scale: float,
+                    dst_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
     _chk(x_in, "x_in")
     _chk(out, "out")
     _chk(tok_mask, "tok_mask", torch.uint8)
     B, Ntok, D = x_in.shape
+    _chk_rows(dst_rows, B, Ntok)
     N.check(N.lib().vp_mask_scale_rows_bf16(_p(x_in), x_in.stride(1), x_in.stride(0), _p(out), out.stride(1),
                                             out.stride(0), B, Ntok, D, _p(tok_mask), tok_mask.stride(0), scale,
-                                            _stream()), "vp_mask_scale_rows_bf16")
+                                            _p(dst_rows), _stream()), "vp_mask_scale_rows_bf16")
     return out
 
 
