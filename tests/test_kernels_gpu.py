@@ -17,22 +17,22 @@ def _lib():
     _native.lib()
 
 
-@pytest.fixture(params=["5", "11", "1"], ids=["gemm_v5", "gemm_v11", "gemm_v1"])
+@pytest.fixture(params=["5", "11", "1", "20"], ids=["gemm_v5", "gemm_v11", "gemm_v1", "gemm_v20"])
 def gemm_variant(request, monkeypatch):
     monkeypatch.setenv("VP_GEMM_VARIANT", request.param)
     return request.param
 
 
-@pytest.fixture(params=["lazy", "bounded", "w32", "w64", "a16", "a16i", "s16i"], ids=lambda v: f"attn_{v}")
+@pytest.fixture(params=["lazy", "bounded", "w32", "w64", "a16", "s16i"], ids=lambda v: f"attn_{v}")
 def attn_variant(request, monkeypatch):
-    """Unbounded-score launches: a16 (the anchored-softmax 16x16x32 kernel, the library default), a16i (its
-    per-query-tile PV order), lazy (the running-max kernel; VP_ATTN_UNBOUNDED_MODE).  Bounded-score launches
+    """Unbounded-score launches: a16 (the anchored-softmax 16x16x32 kernel, the library default), lazy (the
+    running-max kernel; VP_ATTN_UNBOUNDED_MODE).  Bounded-score launches
     (include/vp_hip.h VP_ATTN_BOUNDED_SCORES, the host proved the bound): bounded = the library default (s16, 64
     queries per wave on the 16x16x32 MFMA), w32 / w64 / s16i the 8-wave, two-blocks-per-wave 32x32x16 and
     per-query-tile-PV forms (VP_ATTN_BOUNDED_MODE)."""
     monkeypatch.delenv("VP_ATTN_UNBOUNDED_MODE", raising=False)
     monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
-    if request.param in ("lazy", "a16", "a16i"):
+    if request.param in ("lazy", "a16"):
         monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", request.param)
     elif request.param in ("w32", "w64", "s16i"):
         monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", request.param)
@@ -44,7 +44,7 @@ def attn_variant(request, monkeypatch):
 def attn_kw(variant, q, k, scale=0.125, k2=None):
     """bounded_scores for the variant, after checking on the host that the inputs satisfy the bound (the contract
     the processors establish from the qk-norm weights)."""
-    if variant in ("lazy", "a16", "a16i"):
+    if variant in ("lazy", "a16"):
         return {}
     kk = k if k2 is None else torch.cat([k, k2], 1)
     B, Nq, D = q.shape

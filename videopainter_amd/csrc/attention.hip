@@ -968,10 +968,11 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
         for (int r = 0; r < 4; ++r) bad |= nonfinite(o[dt][qt][r] * inv);
     }
     int* flag = (int*)smem;  // the ring is idle after the loop's last barrier
-    if (lane == 0) flag[wave] = __ballot(bad && active) != 0ull;
-    __builtin_amdgcn_s_barrier();
+    const int mine = __ballot(bad && active) != 0ull;
+    if (lane == 0) flag[wave] = mine;
+    __syncthreads();  // (waits for the LDS stores before the barrier)
     const bool redo = (flag[0] | flag[1] | flag[2] | flag[3]) != 0;
-    __builtin_amdgcn_s_barrier();  // flags read before the ring is refilled
+    __syncthreads();  // flags read before the ring is refilled
     if (redo) {
       // pass 1: exact row maxima
 #pragma unroll
@@ -1424,7 +1425,6 @@ static const AttnVar attn_vars[] = {
     {(const void*)attn_fwd_s16<false>, (const void*)attn_fwd_s16<true>, NW4 * 64},
     {(const void*)attn_fwd_s16<false, true>, (const void*)attn_fwd_s16<true, true>, NW4 * 64},
     {(const void*)attn_fwd_s16<false, false, 1>, (const void*)attn_fwd_s16<true, false, 1>, NW4 * 64},
-    {(const void*)attn_fwd_s16<false, true, 1>, (const void*)attn_fwd_s16<true, true, 1>, NW4 * 64},
 };
 constexpr int ATTN_NVAR = sizeof(attn_vars) / sizeof(attn_vars[0]);
 
@@ -1471,21 +1471,21 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   }
   // BOUNDED scores (the host proved |score| <= VP_ATTN_SCORE_BOUND): the 16x16x32 kernel (s16, default);
   // VP_ATTN_BOUNDED_MODE = lazy (running max), w32 (8 waves, one 32-query block per wave), w64 (two blocks per wave,
-  // 32x32x16), a16 (s16 with the anchored softmax), s16i / a16i (per-query-tile PV order) for A/B.
+  // 32x32x16), a16 (s16 with the anchored softmax), s16i (per-query-tile PV order) for A/B.
   // Unbounded scores: the anchored s16 kernel (a16, default: no bound needed, no host sync); VP_ATTN_UNBOUNDED_MODE =
-  // lazy (the running-max kernel) or a16i.
+  // lazy: the running-max kernel.
   auto pick = [](const char* e, int dflt) {
     if (e == nullptr || e[0] == 0) return dflt;
     if (e[0] == 'l') return 0;
     if (e[0] == 'w' && e[1] == '3') return 1;
     if (e[0] == 'w' && e[1] == '6') return 2;
     if (e[0] == 's') return e[3] == 'i' ? 5 : 3;  // s16 / s16i
-    if (e[0] == 'a') return e[3] == 'i' ? 6 : 4;  // a16 / a16i
+    if (e[0] == 'a') return 4;  // a16
     return dflt;
   };
   int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 3)
                                                     : pick(getenv("VP_ATTN_UNBOUNDED_MODE"), 4);
-  if (!(d->flags & VP_ATTN_BOUNDED_SCORES) && variant != 4 && variant != 6) variant = 0;  // unbounded: lazy/anchored
+  if (!(d->flags & VP_ATTN_BOUNDED_SCORES) && variant != 4) variant = 0;  // unbounded: lazy / anchored
   pl.v = &attn_vars[variant];
   const int slots = slots_v[variant];
   const int nqb = (d->Nq + QB - 1) / QB;

@@ -759,6 +759,125 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 }
 
 
+// ------------------------------------------------------------------------------------------------------------
+// VAR 20: 4 waves, one per SIMD, each wave a 128x128 C block (8x8 16x16 fragments = 256 fp32 accumulators held in
+// the AGPR half of the register file by inline-asm MFMAs, so they never move), 256x256x64 tiles through a 2-stage
+// LDS ring filled by LDS-DMA.  Per K-tile and wave: 128 MFMAs (2 k-steps x 64) against 32 ds_read_b128 and 16
+// 1-KiB DMA pieces; ONE barrier per K-tile, placed between the k-steps:
+//   phase A: the 64 MFMAs of k-step 0 (fragments F0, read earlier), with k-step 1's fragments F1 read under them
+//   phase B: wait for tile k+1's DMA (the only one in flight), barrier (every wave's reads of tile k are done),
+//            issue tile k+2's DMA into tile k's stage
+//   phase C: the 64 MFMAs of k-step 1 (F1), with tile k+1's k-step-0 fragments F0 read under them
+// so every fragment read overlaps MFMAs and each DMA has a whole tile time to land.  (The 8-wave quadrant-phase
+// kernel runs 4 barriers per K-tile with 2 waves per SIMD; hipBLASLt's fastest kernels on these shapes use this
+// 4-wave 256x256 shape.)
+// ------------------------------------------------------------------------------------------------------------
+constexpr int NT4 = 256;
+constexpr int WM4 = 128, WN4 = 128, FM4 = WM4 / 16, FN4 = WN4 / 16;
+
+VP_DEV void mfma_acc(f32x4& acc, const bf16x8& w, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(w), "v"(a));
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NT4, 1) void gemm4_kernel(const vp_gemm_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1;  // 0..1 (M)
+  const int wc = wave & 1;   // 0..1 (N)
+
+  const int tiles_m = (d.M + BM - 1) / BM;
+  const int tiles_n = d.N / BN;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GROUP = 4;
+  const int per_group = GROUP * tiles_n;
+  const int group_id = t / per_group;
+  const int first_m = group_id * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + ((t % per_group) % gsz);
+  const int tn = (t % per_group) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = d.K / BK;
+
+  // DMA: piece p (0..31) = tile rows 8p..8p+7 of an operand; wave w issues pieces w + 4i (i = 0..7) of A and of W.
+  // Lane l: row 8p + l/8, physical chunk l%8 <- logical chunk (l%8) ^ swz(row); swz depends on row bits 1-3 and the
+  // piece parity is the wave's, so one per-lane offset + a uniform per-piece step serves all 8 pieces.
+  const int prow0 = 8 * wave + (lane >> 3);  // the lane's row in piece i = 0
+  const int pch = ((lane & 7) ^ swz(prow0)) << 4;
+  const bool full_m = m0 + BM <= d.M;
+  const char* abase = (const char*)d.A + (int64_t)m0 * d.lda * 2;
+  const int sgw = n0 / d.n_seg;  // the tile's weight segment (n_seg % 256 == 0: never straddled)
+  const char* wbase = (const char*)d.W[sgw] + (int64_t)(n0 - sgw * d.n_seg) * d.K * 2;
+  const int aoff = prow0 * (int)d.lda * 2 + pch;
+  const int woff = prow0 * d.K * 2 + pch;
+  auto issue = [&](int kt) {
+    char* st = smem + (kt & 1) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = prow0 + 32 * i;
+      int ao;
+      if (full_m) {
+        ao = aoff + 32 * i * (int)d.lda * 2;
+      } else {
+        ao = (min(m0 + r, d.M - 1) - m0) * (int)d.lda * 2 + pch;
+      }
+      glds16(abase + kt * 128, ao, st + (wave + 4 * i) * 1024);
+      glds16(wbase + kt * 128, woff + 32 * i * d.K * 2, st + TILE_BYTES + (wave + 4 * i) * 1024);
+    }
+  };
+
+  // fragment reads: A rows wr*128 + i*16 + lane%16, W rows wc*128 + j*16 + lane%16, k-step ks: chunk ks*4 + lane/16
+  const int lrow = lane & 15;
+  int lbase[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) lbase[ks] = lrow * 128 + (((ks * 4 + (lane >> 4)) ^ swz(lrow)) << 4);
+  auto read_frags = [&](int kt, int ks, bf16x8 (&a)[FM4], bf16x8 (&w)[FN4]) {
+    const char* st = smem + (kt & 1) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < FM4; ++i) a[i] = *(const bf16x8*)(st + (wr * WM4 + i * 16) * 128 + lbase[ks]);
+#pragma unroll
+    for (int j = 0; j < FN4; ++j) w[j] = *(const bf16x8*)(st + TILE_BYTES + (wc * WN4 + j * 16) * 128 + lbase[ks]);
+  };
+
+  f32x4 acc[FN4][FM4];
+#pragma unroll
+  for (int j = 0; j < FN4; ++j)
+#pragma unroll
+    for (int i = 0; i < FM4; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto mmas = [&](const bf16x8 (&a)[FM4], const bf16x8 (&w)[FN4]) {
+#pragma unroll
+    for (int j = 0; j < FN4; ++j)
+#pragma unroll
+      for (int i = 0; i < FM4; ++i) mfma_acc(acc[j][i], w[j], a[i]);
+  };
+
+  bf16x8 a0[FM4], w0[FN4], a1[FM4], w1[FN4];
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  read_frags(0, 0, a0, w0);
+  for (int kt = 0; kt < nk; ++kt) {
+    // phase A
+    read_frags(kt, 1, a1, w1);
+    mmas(a0, w0);
+    // phase B
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) issue(kt + 2);
+    // phase C
+    if (kt + 1 < nk) read_frags(kt + 1, 0, a0, w0);
+    mmas(a1, w1);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __syncthreads();
+  gemm_epilogue<NT4, FN4, FM4, WN4, WM4, false, EPI>(d, MxExt{}, acc, smem, m0, n0, wr, wc, lane, tid);
+}
+
 // split-K reduce + epilogue: one thread per 8 consecutive output columns of one row; the chunks are summed in a fixed
 // order, then the same roundings as the fused epilogues (epi_values + epi_rows_out)
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const vp_gemm_desc d, const float* __restrict__ ws,
@@ -870,7 +989,33 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   }
   const char* e = getenv("VP_GEMM_VARIANT");  // read per call: tests switch it between launches
   int variant = e != nullptr ? atoi(e) : 11;
-  if (variant != 1 && variant != 5 && variant != 11) variant = 11;
+  if (variant != 1 && variant != 5 && variant != 11 && variant != 20) variant = 11;
+  // 20: the 4-wave AGPR-accumulator kernel (whole 256-column tiles of one weight segment, whole K-tiles, 32-bit
+  // in-tile DMA offsets)
+  if (variant == 20) {
+    const bool ok20 = (d->N % BN) == 0 && (d->n_seg % BN) == 0 && (d->K % BK) == 0 && d->K >= 2 * BK &&
+                      (int64_t)BM * d->lda * 2 < ((int64_t)1 << 31) && (int64_t)BN * d->K * 2 < ((int64_t)1 << 31);
+    if (ok20) {
+      static const void* const k20[7] = {
+          (const void*)gemm4_kernel<VP_EPI_BIAS>, (const void*)gemm4_kernel<VP_EPI_BIAS_GELU>,
+          (const void*)gemm4_kernel<VP_EPI_BIAS_SCALE>, (const void*)gemm4_kernel<VP_EPI_GATED>,
+          (const void*)gemm4_kernel<VP_EPI_BIAS_ADDROWS>, nullptr, (const void*)gemm4_kernel<VP_EPI_BIAS_QKNORM_ROPE>};
+      static bool attr20 = false;
+      if (!attr20) {
+        for (const void* f : k20)
+          if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        attr20 = true;
+      }
+      const int tiles20 = ((d->M + BM - 1) / BM) * (d->N / BN);
+      void* args[] = {(void*)d};
+      const hipError_t le = hipLaunchKernel(k20[d->epilogue], dim3(tiles20), dim3(NT4), args, LDS_BYTES,
+                                            (hipStream_t)stream);
+      if (le != hipSuccess) return (int)le;
+      VP_CHECK_LAUNCH();
+      return VP_OK;
+    }
+    variant = 11;
+  }
   // the quadrant pipeline adds 32-bit in-tile source offsets to a 64-bit tile base (A) / segment base (W)
   const bool w32 = (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
   const bool tile32 = (int64_t)BM * d->lda * 2 < ((int64_t)1 << 31) && w32;
