@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 10
+#define VP_ABI_VERSION 11
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
@@ -184,6 +184,13 @@ typedef struct vp_attn_desc {
                              processor's null keys, partitioned behind its masked keys by vp_partition_rows_index.
                              The 16x16x32 kernels skip their V^T DMA, reads and PV products for whole tiles past
                              k2_full[b]; the other kernels read the zeros.  NULL: no hint. */
+  const int32_t* k2_len;  /* optional int32 [B] (device): segment 2 holds only its first min(k2_len[b], Nk2) keys for
+                             batch row b (the rest are not read) — the resample processor's masked rows when its null
+                             keys are summed in closed form (vp_null_key_mass).  NULL: Nk2 keys for every row. */
+  const float* l_extra;   /* optional fp32 [B, H, Nq] (device): log2 of extra row-sum mass per query, in the kernel's
+                             score units (scale * log2 e * q.k), added to the softmax denominator — the null keys'
+                             total exp2(score) (their values are zero).  -inf: none.  NULL: nothing added.
+                             k2_full / k2_len / l_extra are implemented by the 16x16x32 kernels (launched for them). */
 } vp_attn_desc;
 #define VP_ATTN_BOUNDED_SCORES 1
 #define VP_ATTN_SCORE_BOUND 60.0f
@@ -272,6 +279,27 @@ int vp_head_norm_rope_fp8(const void* x_in, int64_t ld_in, int64_t bs_in, void* 
  * values) the rest (vp_attn_desc.k2_full). */
 int vp_partition_rows_index(const uint8_t* mask, int64_t mask_bstride, int32_t B, int32_t N, int32_t* dst_rows,
                             int32_t* counts, void* stream);
+
+/* The resample processor's null keys in closed form (attention_processor.py:2244-2290 with mask 0: key LN(0) = the
+ * norm_k bias beta, rotated by the position's RoPE on video rows; value 0).  With CogVideoX's separable 3D RoPE
+ * (dims 0-15 by frame, 16-39 by row, 40-63 by column) a null key's score is S_t(t) + S_y(y) + S_x(x), so the
+ * per-query sum of exp2(score) over all null keys factorises over the grid.
+ * vp_mask_null_segments: the null pattern of the token mask [B, T + F*Hh*Ww] (text rows first), once per mask:
+ *   segs (16-byte records, capacity B*F*Hh): per (b, t) the runs of equal consecutive rows that hold null keys —
+ *   byte 0 = first row, 1 = end row, 2 = run count (<= 6, or 255: the row is scanned instead), bytes 4+2k / 5+2k =
+ *   run k's [start, end) columns; meta int32 [B*F + B]: segments per (b, t), then the text rows with mask 0 per b.
+ * vp_null_key_mass: out[b, h, n] = log2 of sum over the null keys of exp2(scale * log2 e * q[b, n, h] . k_null),
+ *   -inf when there is none.  q: the normed + rotated queries [B, N, H*64] bf16 (strides in elements),
+ *   N = T + F*Hh*Ww; beta bf16 [64]; the per-axis RoPE tables fp32: cos_t / sin_t [F][16], cos_y / sin_y [Hh][24],
+ *   cos_x / sin_x [Ww][24].  F <= 16, Hh <= 64, Ww <= 255, vp_null_key_mass_lds_bytes <= 160 KiB. */
+int vp_mask_null_segments(const uint8_t* mask, int64_t mask_bstride, int32_t B, int32_t T, int32_t F, int32_t Hh,
+                          int32_t Ww, void* segs, int32_t* meta, void* stream);
+int64_t vp_null_key_mass_lds_bytes(int32_t F, int32_t Hh, int32_t Ww);
+int vp_null_key_mass(const void* q, int64_t q_sb, int64_t q_sn, int32_t B, int32_t H, int32_t N, int32_t T, int32_t F,
+                     int32_t Hh, int32_t Ww, const void* beta, const float* cos_t, const float* sin_t,
+                     const float* cos_y, const float* sin_y, const float* cos_x, const float* sin_x,
+                     const uint8_t* mask, int64_t mask_bstride, const void* segs, const int32_t* meta, float scale,
+                     float* out, void* stream);
 int vp_mask_scale_rows_bf16(const void* x_in, int64_t ld_in, int64_t bs_in, void* y, int64_t ld_out, int64_t bs_out,
                             int32_t B, int32_t Ntok, int32_t D, const uint8_t* tok_mask, int64_t mask_bstride,
                             float scale, const int32_t* dst_rows, void* stream);

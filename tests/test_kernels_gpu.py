@@ -653,3 +653,128 @@ def test_attention_k2_full_hint(mode, monkeypatch):
     hd = lambda x: x.float().cpu().reshape(B, -1, H, 64).transpose(1, 2)  # noqa: E731
     ref = _sdpa(hd(q), torch.cat([hd(k), hd(k2)], 2), torch.cat([hd(v), hd(v2)], 2)).transpose(1, 2).reshape(B, Nn, D)
     assert rel(o, ref) < 1e-2 and rel(o, o_ref) < 2e-3
+
+
+def _grid_rope(F_, Hh, Ww):
+    from oracle.cogvideox_oracle import prepare_rotary_positional_embeddings
+    cos, sin = prepare_rotary_positional_embeddings(Hh * 16, Ww * 16, F_, 64)
+    return cos.float(), sin.float()
+
+
+def _null_mass_ref(q, H, T, cos, sin, beta, m, scale):
+    """fp64: log2 sum over the mask-0 rows j of 2^(scale log2 e q.k_j), k_j = beta (text) / RoPE(beta) (video)."""
+    B, Ntok, _ = q.shape
+    bt = beta.double().cpu()
+    rot = torch.stack([-bt[1::2], bt[0::2]], -1).reshape(64)  # apply_rotary_emb's interleaved pairs
+    keys = torch.cat([bt[None].expand(T, 64), bt[None] * cos.double() + rot[None] * sin.double()], 0)
+    qh = q.double().cpu().view(B, Ntok, H, 64)
+    s = torch.einsum("bnhd,kd->bhnk", qh, keys) * (scale * 1.4426950408889634)
+    s = s.masked_fill(m.cpu().bool()[:, None, None, :], float("-inf"))
+    return torch.logsumexp(s * 0.6931471805599453, -1) / 0.6931471805599453
+
+
+def test_null_key_mass_matches_explicit_null_keys():
+    """The resample processor's null keys in closed form (resample.hip) against the explicit sum over
+    every mask-0 row in fp64: text rows all / partly null, a video row with 8 runs (the per-column fallback), an
+    all-null and a no-null row, a batch row without any null key (-inf)."""
+    from videopainter_amd import kernels as K
+    B, H, T, F_, Hh, Ww = 3, 3, 7, 3, 5, 16
+    grid = (F_, Hh, Ww)
+    cos, sin = _grid_rope(*grid)
+    Ntok = T + F_ * Hh * Ww
+    g = torch.Generator().manual_seed(5)
+    m = torch.rand(B, Ntok, generator=g) < 0.5
+    m[0, :T] = False
+    vid = m[:, T:].view(B, F_, Hh, Ww)
+    vid[0, 1, 2] = torch.arange(Ww) % 2 == 1
+    vid[1, 0, 0] = False
+    vid[1, 2, 4] = True
+    m[2] = True
+    m8 = m.to(torch.uint8).to(dev)
+    q = bf(rnd(B, Ntok, H * 64, seed=60) * 1.5).to(dev)
+    beta = bf(rnd(64, seed=61) * 0.8).to(dev)
+    axes = K.rope_axis_tables((cos.to(dev), sin.to(dev)), grid)
+    assert axes is not None
+    segs, meta = K.mask_null_segments(m8, T, grid)
+    # the segment records against a host scan: runs of equal consecutive rows with null keys
+    mc = m.cpu()
+    for b in range(B):
+        for t in range(F_):
+            rows = []
+            for y in range(Hh):
+                row = mc[b, T + (t * Hh + y) * Ww:T + (t * Hh + y + 1) * Ww]
+                runs, x = [], 0
+                while x < Ww:
+                    if row[x]:
+                        x += 1
+                        continue
+                    x0 = x
+                    while x < Ww and not row[x]:
+                        x += 1
+                    runs.append((x0, x))
+                rows.append(runs)
+            want = []
+            for y, runs in enumerate(rows):
+                if y > 0 and runs == rows[y - 1] and len(runs) <= 6 and want and want[-1][1] == y:
+                    want[-1][1] = y + 1
+                elif runs:
+                    want.append([y, y + 1, runs])
+            got = segs[(b * F_ + t) * Hh:(b * F_ + t) * Hh + int(meta[b * F_ + t])].cpu()
+            assert len(got) == len(want), (b, t)
+            for r, (y0, y1, runs) in zip(got.tolist(), want):
+                n = len(runs) if len(runs) <= 6 else 255
+                assert (r[0], r[1], r[2]) == (y0, y1, n), (b, t, r, y0, y1, runs)
+                if n != 255:
+                    assert [(r[4 + 2 * k], r[5 + 2 * k]) for k in range(n)] == runs
+        assert int(meta[B * F_ + b]) == int((~mc[b, :T]).sum())
+    assert int(segs[(0 * F_ + 1) * Hh:(0 * F_ + 1) * Hh + int(meta[1]), 2].eq(255).sum()) == 1  # the 8-run row
+    lx = K.null_key_mass(q, H, T, grid, beta, axes, m8, (segs, meta), 0.125).double().cpu()
+    ref = _null_mass_ref(q, H, T, cos, sin, beta, m, 0.125)
+    assert torch.isinf(lx[2]).all() and (lx[2] < 0).all()
+    assert torch.isfinite(lx[:2]).all()
+    err = float((lx[:2] - ref[:2]).abs().max())
+    assert err < 2e-4, err
+
+
+@pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
+@pytest.mark.parametrize("mode", ["s16", "a16"])
+def test_attention_k2_len_and_l_extra(mode, split, monkeypatch):
+    """k2_len (only the first k2_len[b] keys of segment 2) and l_extra (extra row-sum mass per query, log2 score
+    units) against fp64 attention over the truncated segments with 2^l_extra added to each denominator.  At this size
+    every block is in the grid tail: the split launch (with empty key ranges where k2_len = 0 leaves fewer tiles than
+    splits) and the combine kernel carry l_extra; a16 also gets masses far above its anchor (the exact re-run)."""
+    from videopainter_amd import kernels as K
+    if mode == "a16":
+        monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", "a16")
+        kw = {}
+    else:
+        monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", mode)
+        kw = dict(bounded_scores=True)
+    if not split:
+        monkeypatch.setenv("VP_ATTN_NO_SPLIT", "1")
+    B, H, Nn, N2 = 3, 2, 700, 900
+    D = H * 64
+    q, k, v = (bf(rnd(B, Nn, D, seed=s) * 0.5).to(dev) for s in (95, 96, 97))
+    k2, v2 = bf(rnd(B, N2, D, seed=98) * 0.5).to(dev), bf(rnd(B, N2, D, seed=99)).to(dev)
+    klen = torch.tensor([300, 0, 900], dtype=torch.int32)
+    lx = rnd(B, H, Nn, seed=100) * 4.0 + 3.0
+    lx[:, :, ::7] = float("-inf")
+    if mode == "a16":
+        lx[0, 0, 5::50] = 150.0
+        lx[1, 1, 9::60] = 90.0
+    o = torch.empty(B, Nn, D, device=dev, dtype=torch.bfloat16)
+    K.attention(q, k, v, o, H, k2=k2, v2=v2, k2_len=klen.to(dev), l_extra=lx.to(dev), **kw)
+    hd = lambda x: x.double().cpu().reshape(x.shape[0], -1, H, 64).transpose(1, 2)  # noqa: E731
+    ref = torch.empty(B, H, Nn, 64, dtype=torch.float64)
+    for b in range(B):
+        n2 = int(klen[b])
+        kk = torch.cat([hd(k[b:b + 1]), hd(k2[b:b + 1, :n2])], 2)[0]
+        vv = torch.cat([hd(v[b:b + 1]), hd(v2[b:b + 1, :n2])], 2)[0]
+        s = (hd(q[b:b + 1])[0] @ kk.transpose(-1, -2)) * (0.125 * 1.4426950408889634)
+        ex = lx[b].double()
+        mx = torch.maximum(s.amax(-1), ex)
+        p = torch.exp2(s - mx[..., None])
+        ref[b] = (p @ vv) / (p.sum(-1) + torch.exp2(ex - mx))[..., None]
+    ref = ref.transpose(1, 2).reshape(B, Nn, D)
+    assert torch.isfinite(o.float()).all()
+    assert rel(o, ref) < 1e-2, rel(o, ref)

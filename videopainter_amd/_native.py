@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -44,7 +44,7 @@ class AttnDesc(C.Structure):
                 ("K2", vp), ("V2", vp), ("k2_sb", i64), ("k2_sn", i64), ("v2_sb", i64), ("v2_sn", i64),
                 ("O", vp), ("o_sb", i64), ("o_sn", i64),
                 ("scale", f32), ("out_scale", f32), ("accumulate", i32), ("flags", i32), ("lse", vp),
-                ("k2_full", vp)]
+                ("k2_full", vp), ("k2_len", vp), ("l_extra", vp)]
 
 
 class GemmMxDesc(C.Structure):
@@ -113,6 +113,10 @@ _SIGS = {
                                      f32, vp, vp]),
     "vp_mask_scale_rows_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, vp, i64, f32, vp, vp]),
     "vp_partition_rows_index": (i32, [vp, i64, i32, i32, vp, vp, vp]),
+    "vp_mask_null_segments": (i32, [vp, i64, i32, i32, i32, i32, i32, vp, vp, vp]),
+    "vp_null_key_mass_lds_bytes": (i64, [i32, i32, i32]),
+    "vp_null_key_mass": (i32, [vp, i64, i64, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i64,
+                               vp, vp, f32, vp, vp]),
     "vp_final_norm_bf16": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, f32, vp, i64, vp]),
     "vp_linear_small_bf16": (i32, [vp, i64, vp, vp, vp, i64, i32, i32, i32, i32, i32, vp]),
     "vp_timestep_embedding_bf16": (i32, [vp, vp, i32, i32, f32, vp]),

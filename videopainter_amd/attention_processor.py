@@ -26,7 +26,14 @@ from .modules import Dropout, LayerNorm, Linear
 BF16 = torch.bfloat16
 
 
-def _rope_dev(rope, device):
+class RopeTables(tuple):
+    """(cos, sin) fp32 [F*Hh*Ww, 64] on the device, plus the video grid (F, Hh, Ww) they were built for when the
+    transformer's forward knows it (None otherwise): the resample processor needs the grid to sum its null keys in
+    closed form (kernels.null_key_mass)."""
+    grid = None
+
+
+def _rope_dev(rope, device, grid=None):
     if rope is None:
         return None
     cos, sin = rope
@@ -34,7 +41,9 @@ def _rope_dev(rope, device):
         cos = cos.to(device=device, dtype=torch.float32).contiguous()
     if sin.device != device or sin.dtype != torch.float32 or not sin.is_contiguous():
         sin = sin.to(device=device, dtype=torch.float32).contiguous()
-    return cos, sin
+    out = RopeTables((cos, sin))
+    out.grid = tuple(grid) if grid is not None else getattr(rope, "grid", None)
+    return out
 
 
 def _u8(mask: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -207,6 +216,29 @@ class CogVideoXAttnProcessor2_0:
         return out[:, t:], out[:, :t]
 
 
+_MASK_PLANS: dict = {}
+
+
+def _mask_plan(m: torch.Tensor, text_len: int, grid):
+    """(dst_rows, counts, segments) of a resample mask — the stable partition (masked rows first) and, with a grid,
+    the null-key segments (kernels.mask_null_segments) — computed once per mask and reused by every layer of the
+    forward (the transformer hands all blocks the same mask tensor).  Keyed on the mask's storage and version; the
+    entry holds the mask, so its address is not reused while cached; an event orders a reuse on another stream."""
+    key = (m.data_ptr(), m._version, tuple(m.shape), text_len, grid)
+    hit = _MASK_PLANS.get(key)
+    if hit is not None and hit[0] is m:
+        torch.cuda.current_stream(m.device).wait_event(hit[4])
+        return hit[1], hit[2], hit[3]
+    dst, cnt = K.partition_rows_index(m)
+    segments = K.mask_null_segments(m, text_len, grid) if grid is not None else None
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(m.device))
+    if len(_MASK_PLANS) >= 8:
+        _MASK_PLANS.pop(next(iter(_MASK_PLANS)))
+    _MASK_PLANS[key] = (m, dst, cnt, segments, ev)
+    return dst, cnt, segments
+
+
 class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
     """HIP restatement of `CogVideoXAttnProcessor2_0_resample.__call__` (attention_processor.py:2223-2304).
 
@@ -229,11 +261,19 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
             raise ValueError("the resample processor needs resample_mask (id_pool_resample needs masks)")
         m = _u8(prev_resample_mask if prev else resample_mask)
         # The second segment in partitioned row order: the masked rows' keys / values first, then the null keys (LN
-        # of a zeroed row, rotated) whose values are zero — the attention kernel takes those as row-sum-only keys
-        # (k2_full).  The order of keys does not change attention; env VP_RESAMPLE_PARTITION=0: original order (A/B).
-        dst = cnt = None
+        # of a zeroed row = the norm_k bias, rotated) whose values are zero — they only add to the row sums.  The
+        # order of keys does not change attention.  With the video grid known and the RoPE table separable, the
+        # null keys leave the segment (k2_len = the masked-row count) and their row mass is summed in closed form
+        # over the grid (null_key_mass -> l_extra); otherwise they stay as row-sum-only keys
+        # (k2_full).  Env VP_RESAMPLE_NULLMASS=0: keep them as keys; VP_RESAMPLE_PARTITION=0: original order (A/B).
+        dst = cnt = segments = axes = None
+        grid = getattr(rope, "grid", None)
         if os.environ.get("VP_RESAMPLE_PARTITION", "1") != "0":
-            dst, cnt = K.partition_rows_index(m)
+            if (grid is not None and os.environ.get("VP_RESAMPLE_NULLMASS", "1") != "0"
+                    and attn.norm_k.bias is not None and attn.norm_k.bias.dtype == BF16
+                    and K.null_key_mass_supported(grid)):
+                axes = K.rope_axis_tables(rope, grid)
+            dst, cnt, segments = _mask_plan(m, text_len, grid if axes is not None else None)
         if prev:
             pkv = _kv(attn, prev_hidden_states.to(BF16).contiguous())
             w = float(prev_clip_weight)
@@ -247,5 +287,11 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
         K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, attn.norm_q.eps, rope)
         K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope)
         o = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
-        K.attention(q, k, v, o, H, k2=k2, v2=v2, scale=attn.scale, bounded_scores=bounded_scores(attn), k2_full=cnt)
+        if axes is not None:
+            lx = K.null_key_mass(q, H, text_len, grid, attn.norm_k.bias, axes, m, segments, attn.scale)
+            K.attention(q, k, v, o, H, k2=k2, v2=v2, scale=attn.scale, bounded_scores=bounded_scores(attn),
+                        k2_len=cnt, l_extra=lx)
+        else:
+            K.attention(q, k, v, o, H, k2=k2, v2=v2, scale=attn.scale, bounded_scores=bounded_scores(attn),
+                        k2_full=cnt)
         return o

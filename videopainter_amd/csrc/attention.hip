@@ -59,7 +59,8 @@ struct Seg {
   int key0;
 };
 
-VP_DEV Seg tile_seg(const vp_attn_desc& d, int ti, int tiles1, int b, int h) {
+// n2: the keys of segment 2 for this batch row (Nk2, or min(k2_len[b], Nk2) in the 16x16x32 kernels)
+VP_DEV Seg tile_seg(const vp_attn_desc& d, int ti, int tiles1, int b, int h, int n2) {
   Seg s;
   if (ti < tiles1) {
     s.k = (const bf16*)d.K + (int64_t)b * d.k_sb + h * 64;
@@ -73,10 +74,13 @@ VP_DEV Seg tile_seg(const vp_attn_desc& d, int ti, int tiles1, int b, int h) {
     s.v = (const bf16*)d.V2 + (int64_t)b * d.v2_sb + h * 64;
     s.k_sn = d.k2_sn;
     s.v_sn = d.v2_sn;
-    s.n = d.Nk2;
+    s.n = n2;
     s.key0 = (ti - tiles1) * KB;
   }
   return s;
+}
+VP_DEV Seg tile_seg(const vp_attn_desc& d, int ti, int tiles1, int b, int h) {
+  return tile_seg(d, ti, tiles1, b, h, d.Nk2);
 }
 
 // keys past the segment end (the DMA re-read the last key there) get score -inf
@@ -210,7 +214,8 @@ VP_DEV int lane_id_opaque() {
 }
 
 VP_DEV void glds16(const char* sbase, int voff, char* lds) {
-  const unsigned la = (unsigned)(uintptr_t)(lds_void_t*)lds;
+  // (the LDS address is wave-uniform; readfirstlane keeps it an SGPR where the compiler loses track of that)
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)lds);
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(la), "v"(voff), "s"(sbase)
                : "memory", "m0");
 }
@@ -325,6 +330,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d,
     acc[2] += v[2] * w;
     acc[3] += v[3] * w;
   }
+  if (d.l_extra != nullptr) l += __builtin_amdgcn_exp2f(d.l_extra[((int64_t)b * d.H + h) * d.Nq + q] - mx);
   const float inv = 1.f / l;
   if (d.lse != nullptr && quad == 0) d.lse[((int64_t)b * d.H + h) * d.Nq + q] = mx + __log2f(l);
   bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64 + 4 * quad;
@@ -515,7 +521,6 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_w64(const vp_attn_desc d
   const int ntiles_all = tiles1 + tiles2;
   const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
   const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
-
   const int qw0 = qb * QB + wave * 64;  // first query of this wave
   bf16x8 qf[2][4];
   {
@@ -708,8 +713,11 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
   const int b = bh / d.H;
   const int h = bh - b * d.H;
   const int tiles1 = (d.Nk + KB - 1) / KB;
-  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KB - 1) / KB : 0;
+  // segment 2 of this batch row: its first k2_len[b] keys (the resample processor's masked rows), or all Nk2
+  const int n2 = d.k2_len != nullptr ? max(0, min(__builtin_amdgcn_readfirstlane(d.k2_len[b]), d.Nk2)) : d.Nk2;
+  const int tiles2 = n2 > 0 ? (n2 + KB - 1) / KB : 0;
   const int ntiles_all = tiles1 + tiles2;
+  // (a split range may be empty when k2_len shortens this row: its record is O = 0, l = 0, m = 0)
   const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
   const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
   // segment-2 keys past k2_full[b] have zero values: their whole tiles skip the V^T DMA, reads and PV MFMAs
@@ -743,7 +751,7 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
   }
   auto slot_of = [&](int ti) { return smem + (ti & 1) * ST; };
   auto issue = [&](int ti) {
-    const Seg sg = tile_seg(d, ti, tiles1, b, h);
+    const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
     char* slot = slot_of(ti);
     const int last = sg.n - 1 - sg.key0;
     const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
@@ -794,13 +802,14 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
 
   // one pass over this workgroup's key tiles through the LDS ring; body(Kl, Vl, lim, first_tile, full) per tile
   auto tile_loop = [&](auto&& body) {
+    if (tbeg >= tend) return;
     issue(tbeg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     for (int ti = tbeg; ti < tend; ++ti) {
       if (ti + 1 < tend) issue(ti + 1);
       const char* Kl = slot_of(ti);
-      const Seg sg = tile_seg(d, ti, tiles1, b, h);
+      const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
       if (active) body(Kl, Kl + KT, sg.n - sg.key0, ti == tbeg, tile_full(ti));
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -955,6 +964,24 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
     }
   });
 
+  // l_extra: row-sum mass of keys that are not in the segments (log2, score units; the null keys of the resample
+  // processor), added relative to the query's reference m; a tail-split partial leaves it to attn_combine_kernel
+  float lx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  if constexpr (!TAIL) {
+    if (d.l_extra != nullptr) {
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) {
+        const int q = min(qw0 + qt * 16 + c16, d.Nq - 1);
+        lx[qt] = d.l_extra[((int64_t)b * d.H + h) * d.Nq + q];
+      }
+    }
+  }
+  auto add_extra = [&]() {
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) lsum[qt][0] += __builtin_amdgcn_exp2f(lx[qt] - m[qt]);
+  };
+  add_extra();
+
   if constexpr (ANCH) {
     // any non-finite row sum or output of the block -> the exact two-pass re-run (workgroup-uniform decision)
     bool bad = false;
@@ -989,9 +1016,9 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
             for (int i = 0; i < 4; ++i) mx[qt] = fmaxf(mx[qt], fmaxf(sc[qt][0][i], sc[qt][1][i]));
         }
       });
-      // pass 2: p = exp2(s - max) <= 1
+      // pass 2: p = exp2(s - max) <= 1 (the max includes l_extra's log mass)
 #pragma unroll
-      for (int qt = 0; qt < 4; ++qt) set_ref(qt, xmax16(mx[qt]));
+      for (int qt = 0; qt < 4; ++qt) set_ref(qt, fmaxf(xmax16(mx[qt]), lx[qt]));
       zero_acc();
       tile_loop([&](const char* Kl, const char* Vl, int lim, bool, bool full) {
 #pragma unroll
@@ -1002,6 +1029,7 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
           else rs_half(sc);
         }
       });
+      add_extra();
     }
   }
 
@@ -1469,9 +1497,11 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
       slots_v[i] = per_cu * cus;
     }
   }
-  // BOUNDED scores (the host proved |score| <= VP_ATTN_SCORE_BOUND): the 16x16x32 kernel (s16, default);
-  // VP_ATTN_BOUNDED_MODE = lazy (running max), w32 (8 waves, one 32-query block per wave), w64 (two blocks per wave,
-  // 32x32x16), a16 (s16 with the anchored softmax), s16i (per-query-tile PV order) for A/B.
+  // BOUNDED scores (the host proved |score| <= VP_ATTN_SCORE_BOUND): w64 (two 32-query blocks per wave on the
+  // 32x32x16 MFMA, default: 286 vs 300 ms per config-2 step for s16 in alternating bench runs, although s16 wins
+  // standalone at a higher clock); VP_ATTN_BOUNDED_MODE = lazy (running max), w32 (8 waves, one block per wave),
+  // s16 (64 queries per wave on the 16x16x32 MFMA), a16 (s16 with the anchored softmax), s16i (per-query-tile PV
+  // order) for A/B.
   // Unbounded scores: the anchored s16 kernel (a16, default: no bound needed, no host sync); VP_ATTN_UNBOUNDED_MODE =
   // lazy: the running-max kernel.
   auto pick = [](const char* e, int dflt) {
@@ -1483,9 +1513,13 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
     if (e[0] == 'a') return 4;  // a16
     return dflt;
   };
-  int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 3)
+  int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 2)
                                                     : pick(getenv("VP_ATTN_UNBOUNDED_MODE"), 4);
   if (!(d->flags & VP_ATTN_BOUNDED_SCORES) && variant != 4) variant = 0;  // unbounded: lazy / anchored
+  // the resample processor's segment hints (k2_full / k2_len / l_extra) are implemented by the 16x16x32 kernels only:
+  // config 4 runs s16 + k2_full at 11.3 ms per call against 13.8 for a w64 instance with the hint
+  // (profiles/r03_bench_config4_*), so hinted launches take s16 (bounded) / a16 (unbounded)
+  if (d->k2_full != nullptr || d->k2_len != nullptr || d->l_extra != nullptr) variant = (variant == 4) ? 4 : 3;
   pl.v = &attn_vars[variant];
   const int slots = slots_v[variant];
   const int nqb = (d->Nq + QB - 1) / QB;

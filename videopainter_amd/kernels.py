@@ -302,12 +302,16 @@ def mx_mfma_probe(A: torch.Tensor, B: torch.Tensor, sa: torch.Tensor, sb: torch.
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, heads: int, *,
               k2: Optional[torch.Tensor] = None, v2: Optional[torch.Tensor] = None, scale: float = 0.125,
               out_scale: float = 1.0, accumulate: bool = False, bounded_scores: bool = False,
-              lse: Optional[torch.Tensor] = None, k2_full: Optional[torch.Tensor] = None) -> torch.Tensor:
+              lse: Optional[torch.Tensor] = None, k2_full: Optional[torch.Tensor] = None,
+              k2_len: Optional[torch.Tensor] = None, l_extra: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q, k, v, out: [B, N, heads*64] views (last dim contiguous, any row/batch stride); k2 / v2: an optional second
     K/V segment of the same form.  The native side sees only pointers and strides, so every extent is checked here.
     lse: optional fp32 [B, heads, Nq] receiving the softmax statistics the backward needs.  k2_full: optional int32
     [B] (device): segment-2 keys at or past k2_full[b] have zero values (v2 rows there must be zero) and enter only the
-    row sums (include/vp_hip.h vp_attn_desc.k2_full)."""
+    row sums (include/vp_hip.h vp_attn_desc.k2_full).  k2_len: optional int32 [B] (device): only the first
+    min(k2_len[b], Nk2) keys of segment 2 exist for batch row b.  l_extra: optional fp32 [B, heads, Nq]: log2 of
+    extra row-sum mass per query in score units (scale * log2 e * q.k), keys with zero values outside the segments
+    (the resample processor's null keys, null_key_mass)."""
     segs = [(q, "q"), (k, "k"), (v, "v"), (out, "out")]
     if (k2 is None) != (v2 is None):
         raise ValueError("k2 and v2 must be given together")
@@ -342,6 +346,18 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
         if tuple(k2_full.shape) != (q.shape[0],) or not k2_full.is_contiguous():
             raise ValueError(f"k2_full must be contiguous int32 [{q.shape[0]}]")
         d.k2_full = _p(k2_full)
+    if k2_len is not None:
+        if k2 is None:
+            raise ValueError("k2_len needs a second segment")
+        _chk(k2_len, "k2_len", torch.int32)
+        if tuple(k2_len.shape) != (q.shape[0],) or not k2_len.is_contiguous():
+            raise ValueError(f"k2_len must be contiguous int32 [{q.shape[0]}]")
+        d.k2_len = _p(k2_len)
+    if l_extra is not None:
+        _chk(l_extra, "l_extra", torch.float32)
+        if tuple(l_extra.shape) != (q.shape[0], heads, q.shape[1]) or not l_extra.is_contiguous():
+            raise ValueError(f"l_extra must be contiguous fp32 [{q.shape[0]}, {heads}, {q.shape[1]}]")
+        d.l_extra = _p(l_extra)
     d.O, d.o_sb, d.o_sn = _p(out), out.stride(0), out.stride(1)
     d.scale, d.out_scale, d.accumulate = scale, out_scale, int(accumulate)
     if lse is not None:
@@ -569,6 +585,98 @@ def partition_rows_index(tok_mask: torch.Tensor):
     N.check(N.lib().vp_partition_rows_index(_p(tok_mask), tok_mask.stride(0), B, Ntok, _p(dst), _p(cnt), _stream()),
             "vp_partition_rows_index")
     return dst, cnt
+
+
+def rope_axis_tables(rope, grid):
+    """The per-axis factors of CogVideoX's separable 3D RoPE table (embeddings.py:457-530: dims 0-15 rotate by the
+    frame, 16-39 by the row, 40-63 by the column): (cos_t, sin_t [F, 16], cos_y, sin_y [Hh, 24], cos_x, sin_x
+    [Ww, 24]) fp32, or None when the [F*Hh*Ww, 64] table is not exactly that product (checked element-wise on the
+    device; one host sync per new table — the result is cached while the table is alive and unmodified)."""
+    cos, sin = rope[0], rope[1]
+    F_, Hh, Ww = (int(g) for g in grid)
+    key = (cos.data_ptr(), cos._version, sin.data_ptr(), sin._version, F_, Hh, Ww)
+    hit = _AXIS_CACHE.get(key)
+    if hit is not None:
+        return hit[2]
+    res = None
+    if (cos.dim() == 2 and tuple(cos.shape) == (F_ * Hh * Ww, 64) and tuple(sin.shape) == tuple(cos.shape)
+            and cos.dtype == torch.float32 and sin.dtype == torch.float32):
+        parts = []
+        ok = True
+        for tab in (cos, sin):
+            g = tab.view(F_, Hh, Ww, 64)
+            t_, y_, x_ = g[:, 0, 0, 0:16], g[0, :, 0, 16:40], g[0, 0, :, 40:64]
+            ok = ok and torch.equal(g[..., 0:16], t_[:, None, None, :].expand(F_, Hh, Ww, 16))
+            ok = ok and torch.equal(g[..., 16:40], y_[None, :, None, :].expand(F_, Hh, Ww, 24))
+            ok = ok and torch.equal(g[..., 40:64], x_[None, None, :, :].expand(F_, Hh, Ww, 24))
+            parts.append((t_.contiguous(), y_.contiguous(), x_.contiguous()))
+        if ok:
+            (ct, cy, cx), (st, sy, sx) = parts
+            res = (ct, st, cy, sy, cx, sx)
+    if len(_AXIS_CACHE) >= 4:
+        _AXIS_CACHE.pop(next(iter(_AXIS_CACHE)))
+    _AXIS_CACHE[key] = (cos, sin, res)  # (holding the tables keeps their addresses from being reused)
+    return res
+
+
+_AXIS_CACHE: dict = {}
+
+
+def mask_null_segments(tok_mask: torch.Tensor, text_len: int, grid):
+    """The null pattern of tok_mask [B, text_len + F*Hh*Ww] (uint8) for null_key_mass: (segs uint8 [B*F*Hh, 16],
+    meta int32 [B*F + B]) — per (b, frame) the runs of equal consecutive rows holding null keys, and the text rows with
+    mask 0 per b (resample.hip mask_null_segments_kernel).  Computed once per mask (the processor caches it)."""
+    _chk(tok_mask, "tok_mask", torch.uint8)
+    F_, Hh, Ww = (int(g) for g in grid)
+    B, Ntok = tok_mask.shape
+    if Ntok != text_len + F_ * Hh * Ww:
+        raise ValueError(f"tok_mask length {Ntok} != {text_len} + {F_}*{Hh}*{Ww}")
+    if tok_mask.stride(1) != 1:
+        raise ValueError("tok_mask rows must be contiguous")
+    segs = torch.empty(B * F_ * Hh, 16, device=tok_mask.device, dtype=torch.uint8)
+    meta = torch.empty(B * F_ + B, device=tok_mask.device, dtype=torch.int32)
+    N.check(N.lib().vp_mask_null_segments(_p(tok_mask), tok_mask.stride(0), B, text_len, F_, Hh, Ww, _p(segs),
+                                          _p(meta), _stream()), "vp_mask_null_segments")
+    return segs, meta
+
+
+def null_key_mass_supported(grid) -> bool:
+    F_, Hh, Ww = (int(g) for g in grid)
+    return (0 < F_ <= 16 and 0 < Hh <= 64 and 0 < Ww <= 255
+            and N.lib().vp_null_key_mass_lds_bytes(F_, Hh, Ww) <= 160 * 1024)
+
+
+def null_key_mass(q: torch.Tensor, heads: int, text_len: int, grid, beta: torch.Tensor, axis_tables,
+                  tok_mask: torch.Tensor, segments, scale: float) -> torch.Tensor:
+    """log2 of the resample processor's null-key row mass per query, fp32 [B, heads, N] (the attention kernel's
+    l_extra): the keys LN(0) = beta (rotated by the RoPE on video rows) of every mask-0 row, in score units
+    scale * log2 e * q.k (include/vp_hip.h vp_null_key_mass).  q: the normed and rotated queries [B, N, heads*64];
+    segments: mask_null_segments(tok_mask, ...)."""
+    _chk(q, "q")
+    _chk(beta, "beta")
+    _chk(tok_mask, "tok_mask", torch.uint8)
+    segs, meta = segments
+    _chk(segs, "segs", torch.uint8)
+    _chk(meta, "meta", torch.int32)
+    F_, Hh, Ww = (int(g) for g in grid)
+    B, Ntok, D = q.shape
+    if D != heads * 64 or q.stride(-1) != 1 or Ntok != text_len + F_ * Hh * Ww:
+        raise ValueError(f"q must be [B, {text_len} + {F_}*{Hh}*{Ww}, heads*64], got {tuple(q.shape)}")
+    if tuple(beta.shape) != (64,) or not beta.is_contiguous():
+        raise ValueError("beta must be contiguous bf16 [64]")
+    if (tuple(tok_mask.shape) != (B, Ntok) or tok_mask.stride(1) != 1 or tuple(segs.shape) != (B * F_ * Hh, 16)
+            or tuple(meta.shape) != (B * F_ + B,) or not segs.is_contiguous() or not meta.is_contiguous()):
+        raise ValueError("tok_mask / segments do not match q")
+    tabs = list(axis_tables)
+    for t, shp in zip(tabs, ((F_, 16), (F_, 16), (Hh, 24), (Hh, 24), (Ww, 24), (Ww, 24))):
+        _chk(t, "rope axis table", torch.float32)
+        if tuple(t.shape) != shp or not t.is_contiguous():
+            raise ValueError(f"rope axis table must be contiguous fp32 {shp}, got {tuple(t.shape)}")
+    out = torch.empty(B, heads, Ntok, device=q.device, dtype=torch.float32)
+    N.check(N.lib().vp_null_key_mass(_p(q), q.stride(0), q.stride(1), B, heads, Ntok, text_len, F_, Hh, Ww, _p(beta),
+                                     *[_p(t) for t in tabs], _p(tok_mask), tok_mask.stride(0), _p(segs), _p(meta),
+                                     scale, _p(out), _stream()), "vp_null_key_mass")
+    return out
 
 
 def mask_scale_rows(x_in: torch.Tensor, out: torch.Tensor, tok_mask: torch.Tensor, scale: float,

@@ -540,7 +540,7 @@ class CogVideoXTransformer3DModel(ModelMixin):
                 raise ValueError("id_pool_resample needs masks")
             resample_mask = torch.zeros(B, Ntok, device=dev, dtype=torch.bool)
             resample_mask[:, T:] = tok_mask.bool()
-        rope = _rope_dev(image_rotary_emb, dev)
+        rope = _rope_dev(image_rotary_emb, dev, grid=(F, H // p, W // p))
         rm_u8 = _u8(resample_mask)
 
         prev_states = None
