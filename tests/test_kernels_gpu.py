@@ -662,11 +662,13 @@ def _grid_rope(F_, Hh, Ww):
 
 
 def _null_mass_ref(q, H, T, cos, sin, beta, m, scale):
-    """fp64: log2 sum over the mask-0 rows j of 2^(scale log2 e q.k_j), k_j = beta (text) / RoPE(beta) (video)."""
+    """fp64: log2 sum over the mask-0 rows j of 2^(scale log2 e q.k_j), k_j = beta (text) / RoPE(beta) rounded to
+    bf16 (video: the key the reference's bf16 apply_rotary_emb writes)."""
     B, Ntok, _ = q.shape
     bt = beta.double().cpu()
     rot = torch.stack([-bt[1::2], bt[0::2]], -1).reshape(64)  # apply_rotary_emb's interleaved pairs
-    keys = torch.cat([bt[None].expand(T, 64), bt[None] * cos.double() + rot[None] * sin.double()], 0)
+    kv = (bt[None] * cos.double() + rot[None] * sin.double()).to(torch.bfloat16).double()
+    keys = torch.cat([bt[None].expand(T, 64), kv], 0)
     qh = q.double().cpu().view(B, Ntok, H, 64)
     s = torch.einsum("bnhd,kd->bhnk", qh, keys) * (scale * 1.4426950408889634)
     s = s.masked_fill(m.cpu().bool()[:, None, None, :], float("-inf"))
