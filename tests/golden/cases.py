@@ -177,6 +177,34 @@ def config2_inputs(dtype=torch.float32):
                 timestep=torch.tensor([499, 499], dtype=torch.int64), rope=(cos, sin))
 
 
+def config5_cfg():
+    """BASELINE config 5: the 5b-I2V model at 49f 720x1280 (sample 90x160 latent)."""
+    from videopainter_amd.config import COGVIDEOX_5B_I2V
+    cfg = dict(COGVIDEOX_5B_I2V, sample_height=90, sample_width=160)
+    return cfg, dict(cfg, num_layers=2)
+
+
+def config5_inputs(dtype=torch.float32):
+    """Config 5's shape (latent 13x90x160: N = 226 + 46 800 = 47 026) at B = 1 (one CFG half: the model is per
+    sample), deterministic counter inputs like config 2's."""
+    b, f, h, w, t = 1, 13, 90, 160, 226
+    video = synth_tensor("c5.video", (b, f, 16, h, w))
+    image = synth_tensor("c5.image", (b, f, 16, h, w)) * np.float32(0.7)
+    image[:, 1:] = 0.0
+    hidden = np.concatenate([video, image], axis=2)
+    mask = make_mask(b, f, h, w, "c5.mask")
+    masked = synth_tensor("c5.masked", (b, f, 16, h, w)) * (1.0 - mask)
+    branch_cond = np.concatenate([masked, mask], axis=2)
+    enc = synth_tensor("c5.enc", (b, t, 4096))
+    cos, sin = prepare_rotary_positional_embeddings(h * 8, w * 8, f, 64)
+    cv = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dtype)  # noqa: E731
+    return dict(hidden=cv(hidden), video=cv(video), mask=cv(mask), branch_cond=cv(branch_cond), enc=cv(enc),
+                timestep=torch.tensor([499], dtype=torch.int64), rope=(cos, sin))
+
+
+CONFIG5_SEEDS = CONFIG1_SEEDS  # the same counter weights as config 2 (init_synthetic_weights_)
+
+
 # CogVideoX 3D causal VAE (SURVEY.md 8f #1; reference autoencoder_kl_cogvideox.py:922-1376).  Tiny: 32 channels at every
 # level, 1 resnet per block; 5b-shaped: the real CogVideoX-5b VAE config (128/256/256/512, 3 resnets per block, 16
 # latent channels, scaling 0.7).  Weights from the counter generator under the diffusers state-dict names.

@@ -51,7 +51,7 @@ from tests.golden.cases import (TINY_CFG, TINY_BRANCH_CFG, tiny_inputs, tiny_wei
                                 PIPE_CASE, pipe_inputs)
 
 torch.manual_seed(0)
-torch.set_num_threads(8)
+torch.set_num_threads(int(os.environ.get("VP_GOLDEN_THREADS", "8")))
 
 
 def _save(name, tensors, meta=None):
@@ -377,6 +377,14 @@ def _make_full_model(tag, cfg_fn, inputs_fn, seeds, out_stride):
     _save(f"{tag}.safetensors", out, {"cpu_seconds": {"fp32": t32, "bf16": t16}} if tag != "config1" else None)
 
 
+def make_config5():
+    """BASELINE config 5's shape (49f 720x1280, N = 47 026) through the reference, whole model, B = 1 (VERDICT r02
+    "what's missing" 3): noise_pred [1,13,16,90,160] strided slice (every 13th element) in fp32 and the reference's
+    own bf16, + digest."""
+    from tests.golden.cases import config5_cfg, config5_inputs, CONFIG5_SEEDS
+    _make_full_model("config5", config5_cfg, config5_inputs, CONFIG5_SEEDS, 13)
+
+
 def make_config1():
     from tests.golden.cases import config1_cfg, config1_inputs, CONFIG1_SEEDS
     _make_full_model("config1", config1_cfg, config1_inputs, CONFIG1_SEEDS, 37)
@@ -564,6 +572,8 @@ if __name__ == "__main__":
         make_config1()
     if "config2" in which:
         make_config2()
+    if "config5" in which:
+        make_config5()
     if "block5" in which:
         make_block5()
     if "block_resample" in which:

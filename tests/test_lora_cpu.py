@@ -133,3 +133,43 @@ def test_set_adapters_weights_and_fuse(tmp_path):
     want = _model()
     fold_lora_(want, sd2, 1.0)
     assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), want.state_dict().values()))
+
+
+def test_trainable_adapter_fold_sync_and_factor_grads():
+    """add_adapter (PEFT's LoraConfig on to_q/k/v/out.0): factors under PEFT's saved names, base frozen, B = 0 so the
+    folded weights equal the base; an in-place factor update re-folds W0 + (alpha/r) B A before the next forward;
+    the factor gradients from dW match autograd of that expression."""
+    import torch
+    from videopainter_amd import CogVideoXTransformer3DModel
+    from videopainter_amd.lora import lora_factor_grads, sync_trainable_lora_
+    from tests.golden.cases import TINY_CFG
+    tr = CogVideoXTransformer3DModel(**TINY_CFG)
+    tr.init_synthetic_weights_(3)
+    w0 = {n: p.detach().clone() for n, p in tr.named_parameters()}
+    tr.add_adapter({"r": 4, "lora_alpha": 8, "target_modules": ["to_q", "to_k", "to_v", "to_out.0"]})
+    train = {n: p for n, p in tr.named_parameters() if p.requires_grad}
+    L = TINY_CFG["num_layers"]
+    assert len(train) == 8 * L
+    assert set(tr.get_lora_state_dict()) == set(train)
+    assert "transformer_blocks.0.attn1.to_out.0.lora_B.weight" in train
+    lin = tr.transformer_blocks[0].attn1.to_q
+    assert lin.lora_A.weight.shape == (4, lin.weight.shape[1]) and lin.lora_B.weight.shape == (lin.weight.shape[0], 4)
+    assert torch.count_nonzero(lin.lora_B.weight) == 0 and torch.count_nonzero(lin.lora_A.weight) > 0
+    for n, p in tr.named_parameters():
+        if n in w0:
+            assert torch.equal(p, w0[n]), n
+    with torch.no_grad():
+        lin.lora_B.weight.normal_(0, 0.1)
+    assert sync_trainable_lora_(tr) == 1
+    want = (w0["transformer_blocks.0.attn1.to_q.weight"].float()
+            + 2.0 * lin.lora_B.weight.float() @ lin.lora_A.weight.float()).to(lin.weight.dtype)
+    assert torch.equal(lin.weight, want)
+    assert sync_trainable_lora_(tr) == 0
+    # dA = s B^T dW, dB = s dW A^T against autograd
+    A = lin.lora_A.weight.detach().float().requires_grad_()
+    B = lin.lora_B.weight.detach().float().requires_grad_()
+    G = torch.randn(lin.weight.shape)
+    (w0["transformer_blocks.0.attn1.to_q.weight"].float() + 2.0 * B @ A).mul(G).sum().backward()
+    dA, dB = lora_factor_grads(lin, G)
+    assert torch.allclose(dA.float(), A.grad.to(dA.dtype).float(), rtol=2e-2, atol=1e-3)
+    assert torch.allclose(dB.float(), B.grad.to(dB.dtype).float(), rtol=2e-2, atol=1e-3)

@@ -207,3 +207,139 @@ def test_branch_gradients_through_frozen_transformer():
     assert any(n.startswith("time_embedding") for n in used) and any(n.startswith("patch_embed") for n in used)
     for n in used:
         _check(n, ours[n], gp32[n], gp16[n])
+
+
+def _resample_mask(T, tok_mask):
+    m = torch.zeros(tok_mask.shape[0], T + tok_mask.shape[1], dtype=torch.bool)
+    m[:, T:] = tok_mask.bool()
+    return m
+
+
+def test_resample_block_backward_matches_oracle():
+    """One block with the ID-resample processor (window 0: attention over [K; LN(mask . k) + RoPE], [V; mask . v],
+    attention_processor.py:2223-2304), every parameter trainable: d x, d temb and every parameter gradient (the
+    norm_k affine gets the null keys' share) against the oracle's autograd (attn_resample)."""
+    from oracle import cogvideox_oracle as O
+    from videopainter_amd import CogVideoXTransformer3DModel, device_scope
+    from videopainter_amd.autograd import block_apply
+    from videopainter_amd.config import full_config
+    tsd, _ = tiny_weights()
+    with device_scope(dev):
+        tr = CogVideoXTransformer3DModel(**dict(TINY_CFG, id_pool_resample_learnable=True))
+    tr.load_diffusers_state_dict({k: torch.from_numpy(v) for k, v in tsd.items()})
+    cfg = dict(full_config(TINY_CFG), id_pool_resample_learnable=True)
+    i = tiny_inputs()
+    T = i["enc"].shape[1]
+    D = 128
+    Nv = i["rope"][0].shape[0]
+    g = torch.Generator().manual_seed(15)
+    x = torch.randn(2, T + Nv, D, generator=g).bfloat16()
+    temb = torch.randn(2, TINY_CFG["time_embed_dim"], generator=g).bfloat16()
+    dout = torch.randn(2, T + Nv, D, generator=g).bfloat16()
+    tm = (torch.rand(2, Nv, generator=g) < 0.4)
+    rm = _resample_mask(T, tm)
+    blk = tr.transformer_blocks[0]
+    blk.requires_grad_(True)
+    xd = x.to(dev).requires_grad_()
+    td = temb.to(dev).requires_grad_()
+    out = block_apply(blk, xd, T, td, (i["rope"][0].to(dev), i["rope"][1].to(dev)),
+                      resample_mask=rm.to(dev).to(torch.uint8))
+    out.backward(dout.to(dev))
+    names = [n for n, _ in blk.named_parameters()]
+    ours = {n: p.grad for n, p in blk.named_parameters()}
+
+    def oracle(dtype):
+        sd = {k[len("transformer_blocks.0."):]: torch.from_numpy(v).to(dtype).requires_grad_()
+              for k, v in tsd.items() if k.startswith("transformer_blocks.0.")}
+        xo = x.to(dtype).requires_grad_()
+        to = temb.to(dtype).requires_grad_()
+        h, e = O.block_forward({f"b.{k}": v for k, v in sd.items()}, "b", cfg, xo[:, T:], xo[:, :T], to,
+                               i["rope"], resample_mask=rm.to(dtype), resample=True)
+        torch.cat([e, h], 1).backward(dout.to(dtype))
+        return xo.grad, to.grad, {k: sd[k].grad for k in names}
+
+    gx32, gt32, gp32 = oracle(torch.float32)
+    gx16, gt16, gp16 = oracle(torch.bfloat16)
+    _check("dx", xd.grad, gx32, gx16)
+    _check("dtemb", td.grad, gt32, gt16)
+    for n in names:
+        _check(n, ours[n], gp32[n], gp16[n])
+
+
+def test_resample_lora_training_step_matches_oracle():
+    """VideoPainterID's training step (train/train_cogvideox_inpainting_i2v_video_resample.py:1520-1526, 1940-1961):
+    LoRA (r 4, alpha 8) added on to_q / to_k / to_v / to_out.0 of the frozen transformer, resample processor
+    (id_pool_resample_learnable, window 0), frozen branch samples injected under the mask, backward of a random
+    cotangent: the output and every LoRA factor's gradient against the oracle's autograd of
+    W = W0 + (alpha / r) B A.  Then an in-place update of the factors (what the optimizer step does) re-folds the
+    weights before the next forward."""
+    from oracle import cogvideox_oracle as O
+    from videopainter_amd.config import full_config
+    from videopainter_amd import CogVideoXTransformer3DModel, device_scope
+    _, br, tsd, bsd = _models(train_branch=False)
+    with device_scope(dev):
+        tr = CogVideoXTransformer3DModel(**dict(TINY_CFG, id_pool_resample_learnable=True))
+    tr.load_diffusers_state_dict({k: torch.from_numpy(v) for k, v in tsd.items()})
+    tr.add_adapter({"r": 4, "lora_alpha": 8, "init_lora_weights": True,
+                    "target_modules": ["to_q", "to_k", "to_v", "to_out.0"]})
+    trainable = [n for n, p in tr.named_parameters() if p.requires_grad]
+    assert trainable and all(".lora_A.weight" in n or ".lora_B.weight" in n for n in trainable)
+    assert len(trainable) == 2 * 4 * TINY_CFG["num_layers"]
+    g = torch.Generator().manual_seed(7)
+    facs = {}
+    with torch.no_grad():  # PEFT starts B at 0 (dA = 0): a trained-looking pair instead
+        for n, p in tr.named_parameters():
+            if p.requires_grad:
+                p.copy_(torch.randn(p.shape, generator=g) * 0.05)
+                facs[n] = p.detach().float().cpu()
+    i = tiny_inputs()
+    R = torch.randn(i["video"].shape, generator=g).bfloat16()
+    samples = br(hidden_states=i["video"].to(dev).bfloat16(), encoder_hidden_states=i["enc"].to(dev).bfloat16(),
+                 branch_cond=i["branch_cond"].to(dev).bfloat16(), timestep=i["timestep"].to(dev),
+                 image_rotary_emb=i["rope"], return_dict=False)[0]
+    out = tr(hidden_states=i["hidden"].to(dev).bfloat16(), encoder_hidden_states=i["enc"].to(dev).bfloat16(),
+             timestep=i["timestep"].to(dev), image_rotary_emb=i["rope"], branch_block_samples=samples,
+             branch_block_masks=i["mask"].to(dev), id_pool_resample_learnable=True, return_dict=False)[0]
+    assert out.requires_grad
+    out.backward(R.to(dev))
+    ours = {n: p.grad for n, p in tr.named_parameters() if p.requires_grad}
+
+    def oracle(dtype, factors, grad=True):
+        tp = {k: torch.from_numpy(v).to(dtype) for k, v in tsd.items()}
+        leaves = {n: v.detach().clone().to(dtype).requires_grad_(grad) for n, v in factors.items()}
+        for n in leaves:
+            if n.endswith(".lora_A.weight"):
+                mod = n[:-len(".lora_A.weight")]
+                tp[mod + ".weight"] = tp[mod + ".weight"] + 2.0 * (leaves[mod + ".lora_B.weight"] @ leaves[n])
+        bp = {k: torch.from_numpy(v).to(dtype) for k, v in bsd.items()}
+        s = O.branch_forward(bp, full_config(TINY_BRANCH_CFG, True), i["video"].to(dtype), i["enc"].to(dtype),
+                             i["branch_cond"].to(dtype), i["timestep"], i["rope"])
+        o = O.transformer_forward(tp, dict(full_config(TINY_CFG), id_pool_resample_learnable=True),
+                                  i["hidden"].to(dtype), i["enc"].to(dtype), i["timestep"], i["rope"],
+                                  branch_block_samples=s, branch_block_masks=i["mask"].to(dtype),
+                                  id_pool_resample_learnable=True)[0]
+        if grad:
+            o.backward(R.to(dtype))
+        return o.detach(), {n: leaves[n].grad for n in leaves}
+
+    missing = [n for n in trainable if ours[n] is None]
+    assert not missing, (missing, [n for n in trainable if ours[n] is not None][:4])
+    o32, gp32 = oracle(torch.float32, facs)
+    o16, gp16 = oracle(torch.bfloat16, facs)
+    _check("output", out.detach(), o32, o16)
+    for n in trainable:
+        _check(n, ours[n], gp32[n], gp16[n])
+
+    # the optimizer step updates the factors in place: the next forward runs on the re-folded weights
+    with torch.no_grad():
+        for n, p in tr.named_parameters():
+            if p.requires_grad:
+                p.add_(-0.5 * p.grad)
+                facs[n] = p.detach().float().cpu()
+    with torch.no_grad():
+        out2 = tr(hidden_states=i["hidden"].to(dev).bfloat16(), encoder_hidden_states=i["enc"].to(dev).bfloat16(),
+                  timestep=i["timestep"].to(dev), image_rotary_emb=i["rope"], branch_block_samples=samples,
+                  branch_block_masks=i["mask"].to(dev), id_pool_resample_learnable=True, return_dict=False)[0]
+    o2_32 = oracle(torch.float32, facs, grad=False)[0]
+    o2_16 = oracle(torch.bfloat16, facs, grad=False)[0]
+    _check("output after the factor update", out2, o2_32, o2_16)

@@ -20,8 +20,16 @@ path itself (same launches, same rounding points) and whose backward runs only n
     zero-initialised output linears, branch_cogvideox.py:418-426): parameter gradients (inputs are data).
 
 Grad tensors are bf16 like the parameters (fp32 accumulation inside every kernel; the per-column sums are fp32 until
-the final cast).  Out of scope for the backward (NotImplementedError): the fp8 modes, the resample processor, the
-previous-clip blend and `return_hidden_states` — inference-only features of the reference.
+the final cast).
+
+VideoPainterID training (train/train_cogvideox_inpainting_i2v_video_resample.py:1520-1526, 1951-1961): the blocks'
+resample processor (window 0: attention over [K; LN(mask . k) + RoPE] and [V; mask . v],
+attention_processor.py:2223-2304) is differentiable — the backward recomputes both segments explicitly, runs the
+flash backward over all 2N keys and routes the second segment's gradients back through the masked copy (masked rows
+to k / v, the null keys' to the norm_k affine) — and trainable LoRA factors on to_q / to_k / to_v / to_out.0
+(`transformer.add_adapter`, lora.py) get dA = s B^T dW, dB = s dW A^T from each folded weight's gradient.
+Out of scope for the backward (NotImplementedError): the fp8 modes, the previous-clip blend (windows > 0) and
+`return_hidden_states` — inference-only in the reference.
 """
 from __future__ import annotations
 
@@ -32,6 +40,7 @@ import torch
 from . import _native as NAT
 from . import kernels as K
 from .attention_processor import bounded_scores
+from .lora import has_trainable_lora, lora_factor_grads
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -116,19 +125,30 @@ def _small_linear_bwd(G: _Grads, lin, x_in: torch.Tensor, dy: torch.Tensor) -> t
 # the block
 # ------------------------------------------------------------------------------------------------------------------
 
-def _check_block_trainable_path(block) -> None:
+def _check_block_trainable_path(block, resample_mask=None) -> None:
     a = block.attn1
     if block.ff_mx is not None or block.qkv_mx is not None or getattr(a, "fp8_qk_exp", None) is not None:
         raise NotImplementedError("the backward runs the bf16 path: disable the fp8 modes for training")
     from .attention_processor import CogVideoXAttnProcessor2_0_resample
-    if isinstance(a.processor, CogVideoXAttnProcessor2_0_resample):
-        raise NotImplementedError("the resample processor (VideoPainterID inference) has no backward")
+    if isinstance(a.processor, CogVideoXAttnProcessor2_0_resample) and resample_mask is None:
+        raise ValueError("the resample processor needs resample_mask (id_pool_resample needs masks)")
+
+
+def _put_linear_grads(G: _Grads, lin, dw: torch.Tensor) -> None:
+    """The weight gradient of one (possibly LoRA-adapted) projection: to the weight if it trains, to its trainable
+    LoRA factors if it carries them."""
+    G.put(lin.weight, dw)
+    if has_trainable_lora(lin):
+        dA, dB = lora_factor_grads(lin, dw)
+        G.put(lin.lora_A.weight, dA)
+        G.put(lin.lora_B.weight, dB)
 
 
 def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inject_mask: Optional[torch.Tensor],
-                   dout: torch.Tensor, want_dtemb: bool, want_dinject: bool, train: bool):
-    """Gradient-checkpointed backward of `block.forward_joint(x, T, temb, rope, inject=.., inject_mask=..)`.
-    Returns (dx [B, Ntok, D], dtemb or None, dinject [B, Nv, D] or None, _Grads)."""
+                   dout: torch.Tensor, want_dtemb: bool, want_dinject: bool, train: bool,
+                   resample_mask: Optional[torch.Tensor] = None):
+    """Gradient-checkpointed backward of `block.forward_joint(x, T, temb, rope, resample_mask=.., inject=..,
+    inject_mask=..)`.  Returns (dx [B, Ntok, D], dtemb or None, dinject [B, Nv, D] or None, _Grads)."""
     B, Ntok, D = x.shape
     M = B * Ntok
     a = block.attn1
@@ -148,13 +168,29 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     qkv = torch.empty(B, Ntok, 3 * D, device=dev, dtype=BF16)
     K.gemm(xn.view(M, D), [a.to_q.weight, a.to_k.weight, a.to_v.weight], [a.to_q.bias, a.to_k.bias, a.to_v.bias],
            qkv.view(M, 3 * D))
-    qk = torch.empty(B, Ntok, 2 * D, device=dev, dtype=BF16)
-    qn, kn, v = qk[..., :D], qk[..., D:], qkv[..., 2 * D:]
+    resample = resample_mask is not None
+    v = qkv[..., 2 * D:]
+    if resample:
+        # the resample processor's keys / values as one explicit 2N-key sequence: [K; K2], [V; V2] with
+        # K2 = LN(mask . k) + RoPE (masked rows: = K's rows; null rows: the norm_k bias, rotated), V2 = mask . v
+        qn = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
+        kc = torch.empty(B, 2 * Ntok, D, device=dev, dtype=BF16)
+        vc = torch.empty(B, 2 * Ntok, D, device=dev, dtype=BF16)
+        kn = kc[:, :Ntok]
+        K.head_norm_rope(qkv[..., D:2 * D], kc[:, Ntok:], H, T, a.norm_k.weight, a.norm_k.bias, a.norm_k.eps, rope,
+                         tok_mask=resample_mask, pre_scale=1.0)
+        vc[:, :Ntok].copy_(v)
+        K.mask_scale_rows(v, vc[:, Ntok:], resample_mask, 1.0)
+        katt, vatt = kc, vc
+    else:
+        qk = torch.empty(B, Ntok, 2 * D, device=dev, dtype=BF16)
+        qn, kn = qk[..., :D], qk[..., D:]
+        katt, vatt = kn, v
     K.head_norm_rope(qkv[..., :D], qn, H, T, a.norm_q.weight, a.norm_q.bias, a.norm_q.eps, rope)
     K.head_norm_rope(qkv[..., D:2 * D], kn, H, T, a.norm_k.weight, a.norm_k.bias, a.norm_k.eps, rope)
     o = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
     lse = torch.empty(B, H, Ntok, device=dev, dtype=F32)
-    K.attention(qn, kn, v, o, H, scale=a.scale, bounded_scores=bounded_scores(a), lse=lse)
+    K.attention(qn, katt, vatt, o, H, scale=a.scale, bounded_scores=bounded_scores(a), lse=lse)
     x_mid = torch.empty_like(x)
     K.gemm(o.view(M, D), [to_out.weight], [to_out.bias], x_mid.view(M, D), epilogue=NAT.EPI_GATED,
            resid=x.view(M, D), mod=mod1, gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok, text_len=T)
@@ -215,21 +251,45 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
         gate1 = K.colsum(g.view(M, D), ao, tokens_per_batch=Ntok, text_len=T)
         del ao
         if train:
-            G.put(to_out.weight, K.wgrad(dao, o.view(M, D)))
+            _put_linear_grads(G, to_out, K.wgrad(dao, o.view(M, D)))
             G.put(to_out.bias, _total(dao))
     do = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
     _dgrad(dao, to_out.weight, do.view(M, D))
     del dao
     dqkv = torch.empty(B, Ntok, 3 * D, device=dev, dtype=BF16)
-    K.attention_bwd(qn, kn, v, o, do, lse, H, scale=a.scale, dq=dqkv[..., :D], dk=dqkv[..., D:2 * D],
-                    dv=dqkv[..., 2 * D:])
-    del do, o, lse, qk
+    dk2 = None
+    if resample:
+        dkc = torch.empty(B, 2 * Ntok, D, device=dev, dtype=BF16)
+        dvc = torch.empty(B, 2 * Ntok, D, device=dev, dtype=BF16)
+        K.attention_bwd(qn, kc, vc, o, do, lse, H, scale=a.scale, dq=dqkv[..., :D], dk=dkc, dv=dvc)
+        dqkv[..., D:2 * D].copy_(dkc[:, :Ntok])
+        dv2 = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
+        K.mask_scale_rows(dvc[:, Ntok:], dv2, resample_mask, 1.0)  # V2 = mask . v
+        torch.add(dvc[:, :Ntok], dv2, out=dv2)
+        dqkv[..., 2 * D:].copy_(dv2)
+        dk2 = dkc[:, Ntok:]
+        del dvc, dv2, kc, vc
+    else:
+        K.attention_bwd(qn, kn, v, o, do, lse, H, scale=a.scale, dq=dqkv[..., :D], dk=dqkv[..., D:2 * D],
+                        dv=dqkv[..., 2 * D:])
+        del qk
+    del do, o, lse
     dlnq = dlnk = None
     if train and (a.norm_q.weight.requires_grad or a.norm_k.weight.requires_grad):
         dlnq = (torch.zeros(64, device=dev, dtype=F32), torch.zeros(64, device=dev, dtype=F32))
         dlnk = (torch.zeros(64, device=dev, dtype=F32), torch.zeros(64, device=dev, dtype=F32))
     K.head_norm_rope_bwd(qkv[..., :D], dqkv[..., :D], dqkv[..., :D], H, T, a.norm_q, rope, dlnq)
     K.head_norm_rope_bwd(qkv[..., D:2 * D], dqkv[..., D:2 * D], dqkv[..., D:2 * D], H, T, a.norm_k, rope, dlnk)
+    if dk2 is not None:
+        # K2 = LN(mask . k) + RoPE: (LN + RoPE)' at the masked input, then x mask (null rows: LN of a zero row,
+        # whose input gradient the mask cancels; their d beta stays in dlnk)
+        km = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
+        K.mask_scale_rows(qkv[..., D:2 * D], km, resample_mask, 1.0)
+        dkm = K.head_norm_rope_bwd(km, dk2, torch.empty(B, Ntok, D, device=dev, dtype=BF16), H, T, a.norm_k, rope,
+                                   dlnk)
+        K.mask_scale_rows(dkm, km, resample_mask, 1.0)
+        dqkv[..., D:2 * D].add_(km)
+        del km, dkm, dk2, dkc
     del qkv
     if dlnq is not None:
         G.put(a.norm_q.weight, dlnq[0])
@@ -242,7 +302,7 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
         dw = K.wgrad(dqkv.view(M, 3 * D), xn.view(M, D))
         db = _total(dqkv.view(M, 3 * D))
         for s, lin in enumerate((a.to_q, a.to_k, a.to_v)):
-            G.put(lin.weight, dw[s * D:(s + 1) * D])
+            _put_linear_grads(G, lin, dw[s * D:(s + 1) * D])
             G.put(lin.bias, db[s * D:(s + 1) * D])
         del dw
     del dqkv, xn
@@ -267,10 +327,10 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
 
 class _BlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, block, T, rope, inject_mask, x, temb, inject, *params):
-        out = block.forward_joint(x, T, temb, rope, inject=inject,
+    def forward(ctx, block, T, rope, inject_mask, resample_mask, x, temb, inject, *params):
+        out = block.forward_joint(x, T, temb, rope, resample_mask=resample_mask, inject=inject,
                                   inject_mask=inject_mask if inject is not None else None)
-        ctx.block, ctx.T, ctx.rope, ctx.inject_mask = block, T, rope, inject_mask
+        ctx.block, ctx.T, ctx.rope, ctx.inject_mask, ctx.resample_mask = block, T, rope, inject_mask, resample_mask
         ctx.has_inject = inject is not None
         ctx.params = params
         ctx.save_for_backward(x, temb)
@@ -280,19 +340,21 @@ class _BlockFn(torch.autograd.Function):
     def backward(ctx, dout):
         x, temb = ctx.saved_tensors
         need = ctx.needs_input_grad
-        train = any(need[7:])
+        train = any(need[8:])
         dx, dtemb, dinj, G = block_backward(ctx.block, x, ctx.T, temb, ctx.rope,
-                                            ctx.inject_mask if ctx.has_inject else None, dout, need[5],
-                                            need[6] and ctx.has_inject, train)
-        return (None, None, None, None, dx if need[4] else None, dtemb, dinj, *G.out(ctx.params))
+                                            ctx.inject_mask if ctx.has_inject else None, dout, need[6],
+                                            need[7] and ctx.has_inject, train, ctx.resample_mask)
+        return (None, None, None, None, None, dx if need[5] else None, dtemb, dinj, *G.out(ctx.params))
 
 
 def block_apply(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inject: Optional[torch.Tensor] = None,
-                inject_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Differentiable `block.forward_joint` (gradient-checkpointed)."""
-    _check_block_trainable_path(block)
+                inject_mask: Optional[torch.Tensor] = None,
+                resample_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Differentiable `block.forward_joint` (gradient-checkpointed).  resample_mask: the uint8 token mask of the
+    blocks' resample processor (window 0 of VideoPainterID training)."""
+    _check_block_trainable_path(block, resample_mask)
     params = [p for p in block.parameters()]
-    return _BlockFn.apply(block, T, rope, inject_mask, x, temb, inject, *params)
+    return _BlockFn.apply(block, T, rope, inject_mask, resample_mask, x, temb, inject, *params)
 
 
 # ------------------------------------------------------------------------------------------------------------------

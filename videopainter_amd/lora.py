@@ -119,10 +119,38 @@ class LoraState:
         self.scale: Optional[float] = None
         self.weights: Dict[str, float] = {}   # set_adapters() weights per adapter (1.0 when loaded, 0 = inactive)
         self.fused = False            # fuse_lora(): the folded scale no longer follows the per-call scale
+        self.versions: Dict[str, tuple] = {}  # trainable adapters: (A, B) versions folded per module
 
 
 def lora_state(model: torch.nn.Module) -> Optional[LoraState]:
     return model.__dict__.get("_vp_lora")
+
+
+def _fold_module(st: LoraState, mod: str, W: torch.Tensor, scale: float) -> None:
+    acc = st.base[mod].to(W.device, torch.float32)
+    for name, pairs in st.adapters:
+        p = pairs.get(mod)
+        if p is None or st.weights.get(name, 1.0) == 0.0:
+            continue
+        r = p["A"].shape[0]
+        s = scale * st.weights.get(name, 1.0) * (p["alpha"] / r if p.get("alpha") is not None else 1.0)
+        acc = acc + s * (p["B"].detach().to(W.device, torch.float32) @ p["A"].detach().to(W.device, torch.float32))
+    W.copy_(acc.to(W.dtype))
+    ver = _trainable_versions(st, mod)
+    if ver is not None:
+        st.versions[mod] = ver
+
+
+def _trainable_versions(st: LoraState, mod: str):
+    vs = tuple((p["A"]._version, p["B"]._version) for _, pairs in st.adapters for m, p in pairs.items()
+               if m == mod and isinstance(p["A"], torch.nn.Parameter))
+    return vs or None
+
+
+def _requant_fp8(model) -> None:
+    for blk in getattr(model, "transformer_blocks", []):
+        if getattr(blk, "qkv_mx", None) is not None:
+            blk.enable_fp8_qkv(True)
 
 
 @torch.no_grad()
@@ -133,22 +161,115 @@ def refold_lora_(model: torch.nn.Module, scale: float) -> int:
     if st is None:
         return 0
     mods = dict(model.named_modules())
-    for mod, w0 in st.base.items():
-        W = mods[mod].weight
-        acc = w0.to(W.device, torch.float32)
-        for name, pairs in st.adapters:
-            p = pairs.get(mod)
-            if p is None or st.weights.get(name, 1.0) == 0.0:
-                continue
-            r = p["A"].shape[0]
-            s = scale * st.weights.get(name, 1.0) * (p["alpha"] / r if p.get("alpha") is not None else 1.0)
-            acc = acc + s * (p["B"].to(W.device, torch.float32) @ p["A"].to(W.device, torch.float32))
-        W.copy_(acc.to(W.dtype))
+    for mod in st.base:
+        _fold_module(st, mod, mods[mod].weight, scale)
     st.scale = float(scale)
-    for blk in getattr(model, "transformer_blocks", []):
-        if getattr(blk, "qkv_mx", None) is not None:
-            blk.enable_fp8_qkv(True)
+    _requant_fp8(model)
     return len(st.base)
+
+
+@torch.no_grad()
+def sync_trainable_lora_(model: torch.nn.Module) -> int:
+    """Re-fold the modules whose trainable adapter factors changed since their last fold (an optimizer step updates
+    lora_A / lora_B in place, which bumps their version).  Returns the number of modules re-folded."""
+    st = lora_state(model)
+    if st is None or not st.versions:
+        return 0
+    mods = None
+    n = 0
+    for mod, ver in list(st.versions.items()):
+        if _trainable_versions(st, mod) != ver:
+            mods = mods or dict(model.named_modules())
+            _fold_module(st, mod, mods[mod].weight, st.scale if st.scale is not None else 1.0)
+            n += 1
+    if n:
+        _requant_fp8(model)
+    return n
+
+
+class LoraFactor(torch.nn.Module):
+    """One trainable LoRA factor as PEFT names it: `<module>.lora_A.weight` [r, in] / `<module>.lora_B.weight`
+    [out, r] (the keys `get_peft_model_state_dict` saves and `load_lora_weights` reads)."""
+
+    def __init__(self, rows: int, cols: int, device=None, dtype=None):
+        super().__init__()
+        self.weight = torch.nn.Parameter(torch.empty(rows, cols, device=device, dtype=dtype))
+
+
+@torch.no_grad()
+def add_trainable_adapter_(model: torch.nn.Module, r: int, lora_alpha: float, target_modules=TARGETS,
+                           adapter_name: str = "default", init_lora_weights: bool = True,
+                           dtype: Optional[torch.dtype] = None) -> int:
+    """PEFT's `model.add_adapter(LoraConfig(r, lora_alpha, init_lora_weights, target_modules))` (the resample
+    training script, train/train_cogvideox_inpainting_i2v_video_resample.py:1520-1526): a trainable (lora_A, lora_B)
+    pair on every Linear whose name ends in one of `target_modules`, PEFT's default init (A kaiming-uniform
+    a = sqrt(5), B = 0, so the adapted model starts equal to the base), scaling lora_alpha / r.  The factors are
+    registered as `<module>.lora_A.weight` / `.lora_B.weight` parameters; every other parameter of the model is
+    frozen, as PEFT does.  The forward folds W0 + (alpha / r) B A (re-folded whenever an optimizer step changed a
+    factor: `sync_trainable_lora_`); the backward turns the weight gradient into the factors' (autograd.py)."""
+    import math
+    if r <= 0:
+        raise ValueError("LoRA rank must be positive")
+    targets = tuple(target_modules)
+    model.requires_grad_(False)
+    st = lora_state(model)
+    if st is None:
+        st = model.__dict__["_vp_lora"] = LoraState()
+    if any(n == adapter_name for n, _ in st.adapters):
+        raise ValueError(f"adapter {adapter_name!r} is already loaded")
+    pairs = {}
+    for name, lin in list(model.named_modules()):
+        if not any(name == t or name.endswith("." + t) for t in targets) or not hasattr(lin, "weight"):
+            continue
+        if hasattr(lin, "lora_A"):
+            raise ValueError(f"{name} already carries a trainable adapter (one trainable adapter per model)")
+        W = lin.weight
+        out_f, in_f = W.shape
+        dt = dtype or W.dtype
+        lin.lora_A = LoraFactor(r, in_f, W.device, dt)
+        lin.lora_B = LoraFactor(out_f, r, W.device, dt)
+        if init_lora_weights:
+            a = torch.empty(r, in_f, device=W.device, dtype=torch.float32)
+            torch.nn.init.kaiming_uniform_(a, a=math.sqrt(5))
+            lin.lora_A.weight.copy_(a)
+            lin.lora_B.weight.zero_()
+        lin.lora_A.weight.requires_grad_(True)
+        lin.lora_B.weight.requires_grad_(True)
+        pairs[name] = {"A": lin.lora_A.weight, "B": lin.lora_B.weight, "alpha": float(lora_alpha)}
+        lin.__dict__["_vp_lora_train"] = (st, adapter_name, float(lora_alpha))
+        if name not in st.base:
+            st.base[name] = W.detach().clone()
+    if not pairs:
+        raise ValueError(f"no module matches target_modules {targets}")
+    st.adapters.append((adapter_name, pairs))
+    st.weights[adapter_name] = 1.0
+    refold_lora_(model, st.scale if st.scale is not None else 1.0)
+    return len(pairs)
+
+
+def trainable_lora_state_dict(model: torch.nn.Module) -> Dict[str, torch.Tensor]:
+    """`get_peft_model_state_dict(transformer)`: the trainable factors under PEFT's saved names."""
+    return {k: v.detach() for k, v in model.state_dict().items() if ".lora_A.weight" in k or ".lora_B.weight" in k}
+
+
+def has_trainable_lora(lin) -> bool:
+    f = getattr(lin, "lora_A", None)
+    return f is not None and "_vp_lora_train" in lin.__dict__ and (
+        f.weight.requires_grad or lin.lora_B.weight.requires_grad)
+
+
+def lora_factor_grads(lin, dW: torch.Tensor):
+    """(d lora_A, d lora_B) of the trainable adapter on `lin` from the gradient of its folded weight dW [out, in]:
+    W = W0 + s B A with s = call scale x adapter weight x alpha / r gives dA = s B^T dW, dB = s dW A^T (fp32, cast to
+    the factors' dtype)."""
+    st, name, alpha = lin.__dict__["_vp_lora_train"]
+    A, B = lin.lora_A.weight, lin.lora_B.weight
+    r = A.shape[0]
+    s = (st.scale if st.scale is not None else 1.0) * st.weights.get(name, 1.0) * alpha / r
+    g = dW.float()
+    dA = (B.detach().float().t() @ g) * s
+    dB = (g @ A.detach().float().t()) * s
+    return dA.to(A.dtype), dB.to(B.dtype)
 
 
 @torch.no_grad()

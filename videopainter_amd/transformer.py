@@ -417,10 +417,35 @@ class CogVideoXTransformer3DModel(ModelMixin):
             st.fused = True
         return self
 
+    def add_adapter(self, adapter_config, adapter_name: str = "default"):
+        """PEFT's `transformer.add_adapter(LoraConfig(r=..., lora_alpha=..., init_lora_weights=True,
+        target_modules=["to_q", "to_k", "to_v", "to_out.0"]))` (train/train_cogvideox_inpainting_i2v_video_resample.py
+        :1520-1526): trainable lora_A / lora_B factors on the target Linears, everything else frozen
+        (videopainter_amd/lora.py add_trainable_adapter_).  `adapter_config`: any object (or dict) with r,
+        lora_alpha and optionally target_modules / init_lora_weights — peft's LoraConfig itself qualifies."""
+        from .lora import TARGETS, add_trainable_adapter_
+        get = (lambda k, d=None: adapter_config.get(k, d)) if isinstance(adapter_config, dict) else (
+            lambda k, d=None: getattr(adapter_config, k, d))
+        tm = get("target_modules") or TARGETS
+        if isinstance(tm, str):
+            tm = [tm]
+        add_trainable_adapter_(self, int(get("r")), float(get("lora_alpha", get("r"))), tuple(tm), adapter_name,
+                               bool(get("init_lora_weights", True)))
+        return self
+
+    def get_lora_state_dict(self):
+        """The trainable factors under PEFT's saved names (`get_peft_model_state_dict(transformer)`), for
+        `save_lora_weights(transformer_lora_layers=...)`."""
+        from .lora import trainable_lora_state_dict
+        return trainable_lora_state_dict(self)
+
     def _call_lora_scale(self, attention_kwargs):
-        from .lora import lora_state
+        from .lora import lora_state, sync_trainable_lora_
         st = lora_state(self)
-        if st is None or st.fused:
+        if st is None:
+            return
+        sync_trainable_lora_(self)  # trainable factors changed by an optimizer step since the last fold
+        if st.fused:
             return
         s = attention_kwargs.get("scale", 1.0) if attention_kwargs else 1.0
         self.set_lora_scale(1.0 if s is None else s)
@@ -607,8 +632,8 @@ class CogVideoXTransformer3DModel(ModelMixin):
             raise NotImplementedError("timestep_cond / self-guidance are not on the training path")
         if attention_kwargs and attention_kwargs.get("prev_hidden_states") is not None:
             raise NotImplementedError("the previous-clip blend is inference-only (no backward)")
-        if return_hidden_states or return_resample_mask or id_pool_resample_learnable:
-            raise NotImplementedError("return_hidden_states / resample masks are inference-only (no backward)")
+        if return_hidden_states:
+            raise NotImplementedError("return_hidden_states is inference-only (no backward)")
         self._call_lora_scale(attention_kwargs)
         dev = self.proj_out.weight.device
         B, F, C, H, W = hidden_states.shape
@@ -624,6 +649,15 @@ class CogVideoXTransformer3DModel(ModelMixin):
         tok_mask = None
         if branch_block_masks is not None:
             tok_mask = K.patch_mask(branch_block_masks.detach().to(dev), p)
+        resample_mask = rm_u8 = None
+        if id_pool_resample_learnable or return_resample_mask:
+            # the VideoPainterID training step (train_cogvideox_inpainting_i2v_video_resample.py:1951-1961): window
+            # 0's resample processor, differentiable (autograd.block_backward)
+            if tok_mask is None:
+                raise ValueError("id_pool_resample needs masks")
+            resample_mask = torch.zeros(B, T + tok_mask.shape[1], device=dev, dtype=torch.bool)
+            resample_mask[:, T:] = tok_mask.bool()
+            rm_u8 = _u8(resample_mask)
         rope = _rope_dev(image_rotary_emb, dev)
         bs = None
         if branch_block_samples is not None:
@@ -637,10 +671,10 @@ class CogVideoXTransformer3DModel(ModelMixin):
                     inj = bs[i // interval]
                 elif i < len(bs):
                     inj = bs[i]
-            x = AG.block_apply(block, x, T, emb, rope, inj, tok_mask if inj is not None else None)
+            x = AG.block_apply(block, x, T, emb, rope, inj, tok_mask if inj is not None else None, rm_u8)
         output = AG.head_apply(self, x, emb, (B, F, H, W, T))
         if not return_dict:
-            return (output,)
+            return (output,)  # (the reference returns the mask only together with the hidden states)
         return Transformer2DModelOutput(sample=output)
 
 
