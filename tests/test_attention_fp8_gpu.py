@@ -138,9 +138,10 @@ def _ref_fp64(q8, k8, vt, vs, npad, Nk, H, q_exp, k_exp):
     o = torch.einsum("bhqk,bhkd->bqhd", p / p.sum(dim=-1, keepdim=True), vd)
     return o.reshape(B, Nq, H * 64)
 
-@pytest.fixture(params=["1", "2"], ids=["exp2", "lin"])
+@pytest.fixture(params=["1", "2", "3"], ids=["exp2", "lin", "lin2"])
 def attn8_variant(request, monkeypatch):
-    """VP_ATTN8_VARIANT: 1 = P by v_exp_f32 + RNE e4m3 pack, 2 = P by linear mantissa interpolation (default)."""
+    """VP_ATTN8_VARIANT: 1 = P by v_exp_f32 + RNE e4m3 pack, 2 = P by linear mantissa interpolation, 3 = the same
+    codes packed by v_cvt_pknorm_u16_f32 + a byte gather (default)."""
     monkeypatch.setenv("VP_ATTN8_VARIANT", request.param)
     return request.param
 

@@ -1203,6 +1203,24 @@ VP_DEV float f8_exp_pack(const f32x16 (&s)[2], i32x8& pf) {
 // because the max path still runs every tile; masked (-inf) scores and anything below code 0 clamp to P = 0.
 constexpr float LIN_DELTA = 0.45f;
 
+// LIN 2: the same linear codes, two per v_cvt_pknorm_u16_f32 (the accumulator holds code / 2^16: the Q scale byte
+// takes 2^-13 instead of 2^3 and C0 / LS are scaled alike; round(code (1 - 2^-16)) equals round(code) up to a 2e-3
+// shift of the rounding boundary for codes <= 124) and a v_perm_b32 that gathers the 4 low bytes of two packed
+// u16 pairs: 3 VALU per 4 scores instead of 4.  The u16 codes must stay below 256 for the byte gather, which the
+// max path (every tile) guarantees: codes <= 8 (OFF + THR) + 56; masked (-inf) and negative values clamp to 0.
+VP_DEV void f8_lin2_pack(const f32x16 (&s)[2], i32x8& pf) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const u16x2 lo = __builtin_amdgcn_cvt_pknorm_u16(s[hh][4 * w + 0], s[hh][4 * w + 1]);
+      const u16x2 hi = __builtin_amdgcn_cvt_pknorm_u16(s[hh][4 * w + 2], s[hh][4 * w + 3]);
+      pf[hh * 4 + w] = (int)__builtin_amdgcn_perm(__builtin_bit_cast(unsigned, hi), __builtin_bit_cast(unsigned, lo),
+                                                  0x06040200u);
+    }
+}
+
 VP_DEV void f8_lin_pack(const f32x16 (&s)[2], i32x8& pf) {
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh)
@@ -1224,15 +1242,17 @@ VP_DEV void f8_lin_pack(const f32x16 (&s)[2], i32x8& pf) {
 // sum(query n + 16) in row 1, i.e. in lane n's registers 0 and 1.  (The sum is then over the e4m3-ROUNDED P the PV
 // product uses, in fp32.)  At d = 64 the softmax VALU (32 exp2 at 8 cycles + max + pack) outweighs the tile's 4
 // MFMAs (256 cycles), so moving 112 VALU cycles onto a 32-cycle MFMA is the lever.
-template <int NW, int OCC, int SUB, bool RS, bool LIN>
+template <int NW, int OCC, int SUB, bool RS, int LIN>
 __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_desc dd) {
   static_assert(NW == 8, "the DMA split assumes 8 waves");
   static_assert(RS || !LIN, "the linear codes are summed on the matrix pipe");
   constexpr int OFF = 7;        // P is stored as p * 2^OFF
   constexpr float THR = 1.5f;   // max path: P <= 2^(OFF + THR) < 448
-  // accumulator units: S = LS (s - m) + C0 (log2 units + OFF for the exp2 form, e4m3 codes for LIN)
-  constexpr float LS = LIN ? 8.f : 1.f;
-  constexpr float C0 = LIN ? 8.f * OFF + 56.f - LIN_DELTA : (float)OFF;
+  // accumulator units: S = LS (s - m) + C0 (log2 units + OFF for the exp2 form, e4m3 codes for LIN, codes / 2^16
+  // for LIN 2)
+  constexpr float USC = LIN == 2 ? 0x1p-16f : 1.f;
+  constexpr float LS = LIN ? 8.f * USC : 1.f;
+  constexpr float C0 = LIN ? (8.f * OFF + 56.f - LIN_DELTA) * USC : (float)OFF;
   const vp_attn_desc& d = dd.base;
   constexpr int QB = NW * 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1258,7 +1278,8 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
     hq[0] = *(const u32x4*)(qrow + g * 16);
     hq[1] = *(const u32x4*)(qrow + (g + 2) * 16);
   }
-  const int sq = (dd.qk_scale & 0xff) + (LIN ? 3 : 0), sk = (dd.qk_scale >> 8) & 0xff;  // LIN: scores x 8
+  // LIN: scores x 8 (LIN 2: x 8 / 2^16)
+  const int sq = (dd.qk_scale & 0xff) + (LIN == 2 ? 3 - 16 : LIN ? 3 : 0), sk = (dd.qk_scale >> 8) & 0xff;
 
   // DMA: this lane's row of its wave's piece (16 rows x 64 B) and the logical source chunk of its physical chunk,
   // held as ONE byte offset per lane (waves 0-3 stage K, 4-7 stage V^T) from a wave-uniform base that advances by
@@ -1392,7 +1413,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
         }
         i32x8 pf;
         float ls = 0.f;
-        if constexpr (LIN) {
+        if constexpr (LIN == 2) {
+          f8_lin2_pack(s, pf);
+        } else if constexpr (LIN) {
           f8_lin_pack(s, pf);
         } else
           ls = f8_exp_pack(s, pf);
@@ -1624,21 +1647,24 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
     return VP_ERR_ARG;
   if ((int64_t)d.Nk * d.k_sn > 0x7fffffff || (int64_t)64 * dd->npad > 0x7fffffff) return VP_ERR_ARG;
   constexpr int NW = 8;
-  // VP_ATTN8_VARIANT (A/B): 1 = P by v_exp_f32 + RNE pack, 2 = P by linear mantissa interpolation (LIN, default);
+  // VP_ATTN8_VARIANT (A/B): 1 = P by v_exp_f32 + RNE pack, 2 = P by linear mantissa interpolation (LIN),
+  // 3 = the same codes packed two per v_cvt_pknorm_u16_f32 + a byte gather (LIN 2, default: 2.11-2.15 against
+  // 2.04-2.11 PF/s for 2, interleaved at config 5's length, profiles/r03_fp8_lin2_ab.log);
   // both with the row sums on the matrix pipe, 128 keys per barrier at 4 waves/SIMD.  Dropped after A/B: row sums on
   // the VALU (1.40 against 1.50 PF/s), lazy max (159 VGPRs, spills: 0.21 PF/s), 3 waves/SIMD (1.01), 64 keys per
   // barrier (1.43 against 1.46).
-  static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, 2, true, false>,
-                                    (const void*)attn_fwd_fp8<NW, 4, 2, true, true>};
+  static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, 2, true, 0>,
+                                    (const void*)attn_fwd_fp8<NW, 4, 2, true, 1>,
+                                    (const void*)attn_fwd_fp8<NW, 4, 2, true, 2>};
   static bool attr_set = false;
   if (!attr_set) {
     attr_set = true;
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 3; ++i)
       (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * F8_STAGE);
   }
   const char* e = getenv("VP_ATTN8_VARIANT");
   int variant = e != nullptr ? atoi(e) : 0;
-  if (variant < 1 || variant > 2) variant = 2;
+  if (variant < 1 || variant > 3) variant = 3;
   const int nqb = (d.Nq + NW * 32 - 1) / (NW * 32);
   const int64_t grid = (int64_t)d.B * d.H * nqb;
   if (grid > 0x7fffffff) return VP_ERR_ARG;
