@@ -269,7 +269,8 @@ int vp_head_norm_rope_fp8(const void* x_in, int64_t ld_in, int64_t bs_in, void* 
 
 /* y[b, n, :] = rnd(rnd(x[b, n, :] * tok_mask[b, n]) * scale) — the masked value copy of the resample processor. */
 /* (vp_head_norm_rope_bf16 and vp_mask_scale_rows_bf16 with dst_rows != NULL: output row n of batch b is written to
- * row dst_rows[b * Ntok + n] — the partition permutation of vp_partition_rows_index; the output must not alias the
+ * row dst_rows[b * Ntok + n] — the partition permutation of vp_partition_rows_index; a negative entry skips the row
+ * (neither read nor written: the null rows when their keys are summed in closed form); the output must not alias the
  * input.) */
 
 /* Stable partition of the resample processor's token mask (attention_processor.py:2244-2252): per batch row b,

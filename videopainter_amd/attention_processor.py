@@ -230,7 +230,11 @@ def _mask_plan(m: torch.Tensor, text_len: int, grid):
         torch.cuda.current_stream(m.device).wait_event(hit[4])
         return hit[1], hit[2], hit[3]
     dst, cnt = K.partition_rows_index(m)
-    segments = K.mask_null_segments(m, text_len, grid) if grid is not None else None
+    segments = None
+    if grid is not None:
+        segments = K.mask_null_segments(m, text_len, grid)
+        # only the masked rows are segment 2 now: the null rows' copies are skipped (dst -1)
+        dst = torch.where(m.bool(), dst, torch.full_like(dst, -1))
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(m.device))
     if len(_MASK_PLANS) >= 8:
@@ -252,10 +256,6 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
         B, Ntok, D = x.shape
         H = attn.heads
         rope = _rope_dev(image_rotary_emb, x.device)
-        qkv = _qkv(attn, x) if qkv is None else qkv  # (the block may hand over an fp8 projection)
-        q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
-        k2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
-        v2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
         prev = prev_hidden_states is not None and prev_clip_weight is not None and prev_clip_weight > 0.0
         if not prev and resample_mask is None:
             raise ValueError("the resample processor needs resample_mask (id_pool_resample needs masks)")
@@ -274,18 +274,30 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
                     and K.null_key_mass_supported(grid)):
                 axes = K.rope_axis_tables(rope, grid)
             dst, cnt, segments = _mask_plan(m, text_len, grid if axes is not None else None)
+        # with the null keys in closed form segment 2 holds masked rows only, and those of window 0 are rows of the
+        # normed + rotated K itself: q / k then leave the QKV GEMM through the fused norm + RoPE epilogue
+        fused = axes is not None and qkv is None and _fusable_norms(attn)
+        if qkv is None:  # (the block may hand over an fp8 projection)
+            qkv = _qkv(attn, x, (text_len, rope) if fused else None)
+        q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
+        k2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
+        v2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
         if prev:
             pkv = _kv(attn, prev_hidden_states.to(BF16).contiguous())
             w = float(prev_clip_weight)
             K.head_norm_rope(pkv[..., :D], k2, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps,
                              rope, tok_mask=m, pre_scale=w, dst_rows=dst)
             K.mask_scale_rows(pkv[..., D:], v2, m, w, dst_rows=dst)
+        elif fused:  # LN(1 . k) + RoPE of a masked row is K's row (bit-equal: the epilogue's arithmetic)
+            K.mask_scale_rows(k, k2, m, 1.0, dst_rows=dst)
+            K.mask_scale_rows(v, v2, m, 1.0, dst_rows=dst)
         else:
             K.head_norm_rope(k, k2, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope,
                              tok_mask=m, pre_scale=1.0, dst_rows=dst)
             K.mask_scale_rows(v, v2, m, 1.0, dst_rows=dst)
-        K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, attn.norm_q.eps, rope)
-        K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope)
+        if not fused:
+            K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, attn.norm_q.eps, rope)
+            K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope)
         o = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
         if axes is not None:
             lx = K.null_key_mass(q, H, text_len, grid, attn.norm_k.bias, axes, m, segments, attn.scale)

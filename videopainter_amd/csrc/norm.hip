@@ -234,6 +234,8 @@ __global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restr
   const int64_t bn = vv / H;
   const int n = (int)(bn % Ntok);
   const int b = (int)(bn / Ntok);
+  const int nd = dst_rows != nullptr ? dst_rows[(int64_t)b * Ntok + n] : n;
+  if (nd < 0) return;  // a row the caller does not need (uniform over the vector's 4 lanes; no block barrier here)
   const bf16* src = xin + (int64_t)b * bs_in + (int64_t)n * ld_in + h * 64 + g * 4;
   float m = 1.f;
   if (tok_mask != nullptr) m = tok_mask[(int64_t)b * mask_bs + n] ? 1.f : 0.f;
@@ -252,7 +254,6 @@ __global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restr
   ln64_rope16<1, 2>(x, g, lw, lb, eps, rot ? cosp + (int64_t)(n - text_len) * 64 : nullptr,
                     rot ? sinp + (int64_t)(n - text_len) * 64 : nullptr);
   if (valid) {
-    const int nd = dst_rows != nullptr ? dst_rows[(int64_t)b * Ntok + n] : n;
     const int64_t o = (int64_t)b * bs_out + (int64_t)nd * ld_out + h * 64 + g * 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -286,12 +287,13 @@ __global__ __launch_bounds__(256) void mask_scale_rows_kernel(const bf16* __rest
   const int64_t bn = i / cpr;
   const int n = (int)(bn % Ntok);
   const int b = (int)(bn / Ntok);
+  const int nd = dst_rows != nullptr ? dst_rows[(int64_t)b * Ntok + n] : n;
+  if (nd < 0) return;  // a row the caller does not need
   const float m = tok_mask[(int64_t)b * mask_bs + n] ? 1.f : 0.f;
   const bf16x8 x = *(const bf16x8*)(xin + (int64_t)b * bs_in + (int64_t)n * ld_in + c * 8);
   bf16x8 o;
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = f2bf(rbf(rbf(bf2f(x[e]) * m) * scale));
-  const int nd = dst_rows != nullptr ? dst_rows[(int64_t)b * Ntok + n] : n;
   *(bf16x8*)(y + (int64_t)b * bs_out + (int64_t)nd * ld_out + c * 8) = o;
 }
 
