@@ -692,6 +692,65 @@ def test_config2_full_model_matches_reference():
 
 
 @torch.no_grad()
+def test_config5_full_model_matches_reference():
+    """BASELINE config 5's shape through the whole model (VERDICT r02 "what's missing" 3): the 5b-I2V config at
+    sample 90x160 (49f 720x1280 -> N = 226 + 46 800), 42 layers + 2-layer branch, B = 1, against the REFERENCE's fp32
+    forward of the same counter weights and inputs (tests/golden/config5.safetensors, make_golden.py config5): the
+    bf16 path within the reference's own bf16 drift gate, and the config-5 fp8 path (MX-FP8 QKV / FeedForward + fp8
+    attention, `enable_fp8`) against the same fp32 reference."""
+    path = os.path.join(GOLD, "config5.safetensors")
+    if not os.path.exists(path):
+        pytest.skip("config5 golden not generated")
+    from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, device_scope
+    from tests.golden.cases import config5_cfg, config5_inputs, CONFIG5_SEEDS
+    g = load_file(path)
+    tcfg, bcfg = config5_cfg()
+    with device_scope(dev):
+        tr = CogVideoXTransformer3DModel(**tcfg)
+        br = CogvideoXBranchModel(**bcfg)
+    tr.init_synthetic_weights_(CONFIG5_SEEDS[0])
+    br.init_synthetic_weights_(CONFIG5_SEEDS[1])
+    inp = config5_inputs()
+    rb = g["ref_bf16_rel"].double()
+    d = g["digest"].double()
+
+    def run():
+        bs = br(hidden_states=_d(inp["video"]), encoder_hidden_states=_d(inp["enc"]),
+                branch_cond=_d(inp["branch_cond"]), timestep=inp["timestep"].to(dev), image_rotary_emb=inp["rope"],
+                return_dict=False)[0]
+        o = tr(hidden_states=_d(inp["hidden"]), encoder_hidden_states=_d(inp["enc"]),
+               timestep=inp["timestep"].to(dev), image_rotary_emb=inp["rope"], branch_block_samples=bs,
+               branch_block_masks=_d(inp["mask"]), return_dict=False)[0]
+        assert o.shape == (1, 13, 16, 90, 160)
+        return o.float().reshape(-1), [b.float().reshape(-1)[::997].cpu() for b in bs]
+
+    of, bsl = run()
+    assert torch.isfinite(of).all()
+    r = rel(of[::13], g["slice"])
+    r_vs16 = rel(of[::13], g["bf16.slice"])
+    r0, r1 = rel(bsl[0], g["branch.0.slice"]), rel(bsl[1], g["branch.1.slice"])
+    print(f"config 5 full model (bf16) vs reference fp32: noise_pred {r:.3e} (reference bf16 {float(rb[0]):.3e}; HIP "
+          f"vs reference bf16 {r_vs16:.3e}), branch {r0:.3e} / {r1:.3e} (reference bf16 {float(rb[1]):.3e} / "
+          f"{float(rb[2]):.3e})")
+    assert r <= gate(float(rb[0]))
+    assert r0 <= gate(float(rb[1])) and r1 <= gate(float(rb[2]))
+    assert abs(float(of.double().abs().sum()) / float(d[1]) - 1.0) < 2 * float(rb[0])
+    tr.enable_fp8()
+    br.enable_fp8()
+    of8, _ = run()
+    assert torch.isfinite(of8).all()
+    r8 = rel(of8[::13], g["slice"])
+    print(f"config 5 full model (fp8: MX-FP8 QKV / FeedForward + fp8 attention) vs reference fp32: {r8:.3e}; "
+          f"vs this model in bf16 {rel(of8, of):.3e}")
+    assert r8 <= FP8_CONFIG5_MODEL_GATE
+    del tr, br
+    torch.cuda.empty_cache()
+
+
+FP8_CONFIG5_MODEL_GATE = 6e-2  # set from the first measurement (see DESIGN.md §4)
+
+
+@torch.no_grad()
 def test_config5_length_block_matches_reference():
     """BASELINE config 5's sequence length (720x1280: N = 226 + 46 800 = 47 026): one full-width block against the
     reference's fp32 block (tests/golden/block5.safetensors), in bf16 (gate of the reference's own bf16 drift) and
