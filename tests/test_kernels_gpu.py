@@ -23,18 +23,18 @@ def gemm_variant(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["lazy", "bounded", "w32", "w64", "a16", "s16i"], ids=lambda v: f"attn_{v}")
+@pytest.fixture(params=["lazy", "bounded", "w32", "w64", "a16", "s16i", "p1"], ids=lambda v: f"attn_{v}")
 def attn_variant(request, monkeypatch):
     """Unbounded-score launches: a16 (the anchored-softmax 16x16x32 kernel, the library default), lazy (the
     running-max kernel; VP_ATTN_UNBOUNDED_MODE).  Bounded-score launches
     (include/vp_hip.h VP_ATTN_BOUNDED_SCORES, the host proved the bound): bounded = the library default (s16, 64
-    queries per wave on the 16x16x32 MFMA), w32 / w64 / s16i the 8-wave, two-blocks-per-wave 32x32x16 and
-    per-query-tile-PV forms (VP_ATTN_BOUNDED_MODE)."""
+    queries per wave on the 16x16x32 MFMA), w32 / w64 / s16i / p1 the 8-wave, two-blocks-per-wave 32x32x16,
+    per-query-tile-PV and one-wave-per-SIMD software-pipelined forms (VP_ATTN_BOUNDED_MODE)."""
     monkeypatch.delenv("VP_ATTN_UNBOUNDED_MODE", raising=False)
     monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
     if request.param in ("lazy", "a16"):
         monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", request.param)
-    elif request.param in ("w32", "w64", "s16i"):
+    elif request.param in ("w32", "w64", "s16i", "p1"):
         monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", request.param)
     else:
         monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
@@ -521,7 +521,7 @@ def test_attention_tail_split_matches_unsplit(Nq, Nk2, monkeypatch):
         assert rel(out_s, ref) < 1e-2 and rel(out_u, ref) < 1e-2
 
 
-@pytest.mark.parametrize("mode", ["w64", "s16"])
+@pytest.mark.parametrize("mode", ["w64", "s16", "p1"])
 @pytest.mark.parametrize("Nq,Nk2", [(1500, 700), (17776, 0)])
 def test_attention_bounded_tail_split_matches_unsplit(Nq, Nk2, mode, monkeypatch):
     """The bounded-score kernels' grid-tail split instances (partials + merge) against their unsplit launch and, at

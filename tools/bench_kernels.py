@@ -102,7 +102,7 @@ def main():
         variants = ()
     for rnd in range(2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
         for var in variants:
-            if var in ("w32", "w64", "s16", "a16", "s16i"):  # bounded-kernel forms (A/B)
+            if var in ("w32", "w64", "s16", "a16", "s16i", "p1"):  # bounded-kernel forms (A/B)
                 os.environ["VP_ATTN_BOUNDED_MODE"] = var
             else:
                 os.environ.pop("VP_ATTN_BOUNDED_MODE", None)

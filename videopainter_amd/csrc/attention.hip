@@ -660,6 +660,331 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_w64(const vp_attn_desc d
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// P1 (BOUNDED scores): one wave per SIMD (cdna_hip_programming.md "4-wave, one-wave-per-SIMD" attention form).  The
+// W64 math (4 waves x 64 queries = two 32-query blocks per wave, 32x32x16 MFMA, row sums on the matrix pipe), but one
+// workgroup per CU with the whole register file per wave, a 4-slot LDS ring (tiles DMA'd two ahead) and the work of
+// a wave software-pipelined over "jobs" j = (32-key half, query block): step j runs the QK^T of job j + 1 and the PV
+// (+ row sum) of job j - 1 on the matrix pipe while the VALU does job j's exp2 + bf16 packs, so every MFMA gap holds
+// two v_exp_f32 and one pack (8 + 16 + 4.5 issue cycles of the 32) instead of relying on a second wave to fill it.
+// The K / V^T fragments of a half are read one step ahead (double-buffered by half parity); the pipeline runs across
+// tile boundaries: the last step of a tile waits for the next tile, passes the tile barrier, reads its first K
+// fragments, runs its PV first and the next tile's first QK^T last (the LDS latency under the 4 PV MFMAs).
+// ------------------------------------------------------------------------------------------------------------
+constexpr int P1_SLOTS = 4;
+constexpr int P1_LDS = P1_SLOTS * ST;  // 128 KB: one workgroup per CU
+
+struct P1Regs {
+  bf16x8 qf[2][4];  // Q^T of the two query blocks (pre-scaled)
+  f32x16 o[2][2];   // O^T[block][dim half]
+  f32x16 s[2];      // S^T of the job in flight per block
+  u32x4 pf[2][2];   // packed bf16 P^T per block, 16-key slabs
+  bf16x8 kf[2][4];  // K fragments by half parity
+  bf16x8 vf[2][4];  // V^T fragments by half parity: [slab j * 2 + dim half]
+  f32x4 lsum[2];
+};
+
+VP_DEV void p1_read_k(const char* Kl, int kh, int lane, bf16x8 (&kf)[4]) {
+  const int hl = lane >> 5;
+  const int row = kh * 32 + (lane & 31);
+  const char* kr = Kl + row * 128;
+  const int sw = swz(row);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) kf[c] = *(const bf16x8*)(kr + (((2 * c + hl) ^ sw) << 4));
+}
+
+VP_DEV void p1_read_v(const char* Vl, int kh, const int (&vo)[2], bf16x8 (&vf)[4]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const char* base = Vl + (kh * 2 + j) * 16 * 128 + vo[dh];
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * 128));
+      vf[j * 2 + dh] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+}
+
+// The schedule is pinned by hand: every MFMA (a builtin, so the compiler still sees its hazards, e.g. when it copies
+// an accumulator) sits alone between two sched_barrier(0), and the gap's fillers (2 v_exp_f32 + 1 pack, volatile asm:
+// kept in program order) follow it.  The compiler allocates registers and places the lgkmcnt waits of the LDS reads,
+// which stay where the step puts them.  Filler hazards it cannot see inside asm, and why none needs a wait state: the
+// exps read S at least a whole 4-MFMA group after the MFMA chain that wrote it; each pack reads exps issued one gap
+// earlier (the transcendental -> VALU distance).
+VP_DEV void p1_fence() { __builtin_amdgcn_sched_barrier(0); }
+VP_DEV void p1_exp(float& p0, float& p1, float s0, float s1) {
+  asm volatile("v_exp_f32 %0, %2\n\tv_exp_f32 %1, %3" : "=&v"(p0), "=&v"(p1) : "v"(s0), "v"(s1));
+}
+VP_DEV uint32_t p1_pack(float a, float b) {
+  uint32_t w;
+  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(a), "v"(b));
+  return w;
+}
+VP_DEV bf16x8 as_bf16x8(const u32x4& w) { return __builtin_bit_cast(bf16x8, w); }
+
+// one pipeline step: the QK^T chain of block QB_ (K buffer KB_; skipped when !QK) interleaved with the PV MFMAs of
+// block PB (V buffer VB_) so that no MFMA waits on the one before it, then the two row-sum MFMAs; every gap holds the
+// next exp pair of block EB's 16 scores and the pack of the pair before:
+//   g0 QK c0 | g1 PV (slab 0, d 0-31) | g2 QK c1 | g3 PV (0, 32-63) | g4 QK c2 | g5 PV (1, 0-31) | g6 QK c3 |
+//   g7 PV (1, 32-63) | row sum slab 0 | row sum slab 1
+template <int EB, int QB_, int PB, int KB_, int VB_, bool QK>
+VP_DEV void p1_step(P1Regs& r, const bf16x8& sel) {
+  float p[16];
+  const f32x16 z = {};
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const int c = g >> 1;
+    if ((g & 1) == 0) {
+      if constexpr (QK) {
+        p1_fence();
+        r.s[QB_] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.kf[KB_][c], r.qf[QB_][c], c == 0 ? z : r.s[QB_], 0, 0, 0);
+        p1_fence();
+      }
+    } else {
+      p1_fence();
+      r.o[PB][c & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.vf[VB_][c], as_bf16x8(r.pf[PB][c >> 1]),
+                                                                r.o[PB][c & 1], 0, 0, 0);
+      p1_fence();
+    }
+    p1_exp(p[2 * g], p[2 * g + 1], r.s[EB][2 * g], r.s[EB][2 * g + 1]);
+    if (g > 0) r.pf[EB][(g - 1) >> 2][(g - 1) & 3] = p1_pack(p[2 * g - 2], p[2 * g - 1]);
+  }
+  p1_fence();
+  r.lsum[PB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[PB][0]), r.lsum[PB], 0, 0, 0);
+  p1_fence();
+  r.pf[EB][1][3] = p1_pack(p[14], p[15]);
+  p1_fence();
+  r.lsum[PB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[PB][1]), r.lsum[PB], 0, 0, 0);
+  p1_fence();
+}
+
+// keys past the segment end (lane key (i & 3) + 8 (i >> 2) + 4 hl of the half >= rem = lim - 32 h): score -inf.  In
+// asm so that the compiler cannot hoist the compares out of the (rare, uniform) masked branch into every step.
+VP_DEV void p1_mask(f32x16& s, int rem, int hl4) {
+  const float ninf = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float x = s[i];
+    int t;
+    asm volatile(
+        "v_add_u32 %1, %3, %4\n\t"
+        "v_cmp_le_i32 vcc, %2, %1\n\t"
+        "v_cndmask_b32 %0, %0, %5, vcc"
+        : "+v"(x), "=&v"(t)
+        : "s"(rem), "v"(hl4), "i"((i & 3) + 8 * (i >> 2)), "v"(ninf)
+        : "vcc");
+    s[i] = x;
+  }
+}
+
+// one 128-key tile = 8 steps (halves h = 0..3 x blocks 0, 1).  Step (h, b) exps job (h, b)'s scores while the
+// matrix pipe runs the QK^T of the next job and the PV of the previous one:
+//   even step (h, 0): read K(h+1), V(h) | QK (h, 1) [K(h)] + PV (h-1, 1) [V(h-1)]
+//   odd  step (h, 1):                     QK (h+1, 0) [K(h+1)] + PV (h, 0) [V(h)]
+// K and V^T fragments double-buffered by half parity, each read a whole step ahead of its first use.  On entry s[0]
+// holds job (0, 0)'s scores, kf[0] K(0) of this tile, vf[1] / pf[1] the previous tile's V(3) / last P (zeros before
+// the first tile).  The tile seam is at the start of step (3, 0): wait for the next tile (vmcnt: one tile per wave
+// left in flight unless wait_all), pass the barrier, read its K(0); last: no next tile (that QK^T is skipped).
+// masked: keys >= lim get score -inf (a segment's partial last tile; a uniform branch before the step).
+VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn, int lim, bool masked, bool last,
+                    bool wait_all, int lane, const int (&vo)[2]) {
+  const int hl = lane >> 5;
+  const char* Vl = Kl + KT;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    // even step (h, 0)
+    if (h < 3) {
+      p1_read_k(Kl, h + 1, lane, r.kf[(h + 1) & 1]);
+    } else if (!last) {
+      if (wait_all)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      p1_read_k(Kn, 0, lane, r.kf[0]);
+    }
+    p1_read_v(Vl, h, vo, r.vf[h & 1]);
+    if (masked) p1_mask(r.s[0], lim - 32 * h, 4 * hl);
+    if (h & 1)
+      p1_step<0, 1, 1, 1, 0, true>(r, sel);
+    else
+      p1_step<0, 1, 1, 0, 1, true>(r, sel);
+    // odd step (h, 1)
+    if (masked) p1_mask(r.s[1], lim - 32 * h, 4 * hl);
+    if (h < 3 || !last) {
+      if (h & 1)
+        p1_step<1, 0, 0, 0, 1, true>(r, sel);
+      else
+        p1_step<1, 0, 0, 1, 0, true>(r, sel);
+    } else {
+      p1_step<1, 0, 0, 0, 1, false>(r, sel);
+    }
+  }
+}
+
+template <bool TAIL = false>
+__global__ __launch_bounds__(NW4 * 64, 1) void attn_fwd_p1(const vp_attn_desc d, const AttnSplit sp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hl = lane >> 5;
+
+  const int nqb = (d.Nq + QB - 1) / QB;
+  const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
+  const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb;
+  const int qb = t - bh * nqb;
+  const int b = bh / d.H;
+  const int h = bh - b * d.H;
+  const int tiles1 = (d.Nk + KB - 1) / KB;
+  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KB - 1) / KB : 0;
+  const int ntiles_all = tiles1 + tiles2;
+  const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
+  const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
+  const int qw0 = qb * QB + wave * 64;
+
+  P1Regs r;
+  {
+    const float cq = d.scale * 1.4426950408889634f;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+      const int q = qw0 + qi * 32 + (lane & 31);
+      const int qc = q < d.Nq ? q : d.Nq - 1;
+      const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+#pragma unroll
+      for (int ds = 0; ds < 4; ++ds) {
+        r.qf[qi][ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r.qf[qi][ds][j] = f2bf(bf2f(r.qf[qi][ds][j]) * cq);
+      }
+    }
+  }
+  int prow[PPW4], kch[PPW4], vch[PPW4];
+#pragma unroll
+  for (int i = 0; i < PPW4; ++i) {
+    prow[i] = (wave + i * NW4) * 8 + (lane >> 3);
+    kch[i] = (lane & 7) ^ swz(prow[i]);
+    vch[i] = (lane & 7) ^ vswz(prow[i]);
+  }
+  auto slot_of = [&](int ti) { return smem + (ti & (P1_SLOTS - 1)) * ST; };
+  // full tiles of segment 1 (all but possibly its last): one scalar base per operand and tile, the lane offsets fixed
+  // (voff_*); segment 2 and partial tiles take the general path (rows past the end re-read the last key)
+  int voff_k[PPW4], voff_v[PPW4];
+#pragma unroll
+  for (int i = 0; i < PPW4; ++i) {
+    voff_k[i] = (prow[i] * (int)d.k_sn + kch[i] * 8) * 2;
+    voff_v[i] = (prow[i] * (int)d.v_sn + vch[i] * 8) * 2;
+  }
+  const char* kseg1 = (const char*)((const bf16*)d.K + (int64_t)b * d.k_sb + h * 64);
+  const char* vseg1 = (const char*)((const bf16*)d.V + (int64_t)b * d.v_sb + h * 64);
+  const int64_t ktile_bytes = (int64_t)KB * d.k_sn * 2, vtile_bytes = (int64_t)KB * d.v_sn * 2;
+  const int full1 = d.Nk / KB;  // full tiles of segment 1
+  auto issue = [&](int ti) {
+    char* slot = slot_of(ti);
+    if (ti < full1) {
+      const char* kb = kseg1 + ti * ktile_bytes;
+      const char* vb = vseg1 + ti * vtile_bytes;
+#pragma unroll
+      for (int i = 0; i < PPW4; ++i) {
+        const int pc = wave + i * NW4;
+        glds16(kb, voff_k[i], slot + pc * 1024);
+        glds16(vb, voff_v[i], slot + KT + pc * 1024);
+      }
+      return;
+    }
+    const Seg sg = tile_seg(d, ti, tiles1, b, h);
+    const int last = sg.n - 1 - sg.key0;
+    const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
+    const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
+    const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
+#pragma unroll
+    for (int i = 0; i < PPW4; ++i) {
+      const int pc = wave + i * NW4;
+      const int rr = min(prow[i], last);
+      glds16(kb, (rr * ksn + kch[i] * 8) * 2, slot + pc * 1024);
+      glds16(vb, (rr * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
+    }
+  };
+  static_assert(2 * PPW4 == 8, "vmcnt(8) in p1_tile = one tile of DMA per wave");
+
+  const int g = lane >> 4;
+  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
+  const int tcol = 16 * (g & 1) + 4 * (lane & 3);
+  int vo[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh) vo[dh] = trow * 128 + (((dh * 4 + (tcol >> 3)) ^ vswz(trow)) << 4) + (tcol & 7) * 2;
+
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      r.o[qi][0][i] = 0.f;
+      r.o[qi][1][i] = 0.f;
+    }
+    r.lsum[qi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) r.pf[qi][j] = (u32x4){0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) r.vf[1][c] = (bf16x8){};  // job -1: 0 x 0
+  bf16x8 sel;
+  {
+    const bf16 one = f2bf((((lane >> 4) & 1) == 0) == ((lane & 15) < 8) ? 1.f : 0.f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sel[e] = one;
+  }
+
+  issue(tbeg);
+  if (tbeg + 1 < tend) {
+    issue(tbeg + 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  p1_read_k(slot_of(tbeg), 0, lane, r.kf[0]);
+  {
+    const f32x16 z = {};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      r.s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.kf[0][c], r.qf[0][c], c == 0 ? z : r.s[0], 0, 0, 0);
+  }
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // S -> the first (asm) exp
+  for (int ti = tbeg; ti < tend; ++ti) {
+    if (ti + 2 < tend) issue(ti + 2);
+    int lim = KB;
+    if (ti >= full1) {
+      const Seg sg = tile_seg(d, ti, tiles1, b, h);
+      lim = sg.n - sg.key0;
+    }
+    p1_tile(r, sel, slot_of(ti), slot_of(ti + 1), __builtin_amdgcn_readfirstlane(lim), lim < KB, ti + 1 >= tend,
+            ti + 2 >= tend, lane, vo);
+  }
+  // drain: PV + row sums of the last job (3, 1)
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    r.o[1][c & 1] =
+        __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.vf[1][c], as_bf16x8(r.pf[1][c >> 1]), r.o[1][c & 1], 0, 0, 0);
+  r.lsum[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[1][0]), r.lsum[1], 0, 0, 0);
+  r.lsum[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[1][1]), r.lsum[1], 0, 0, 0);
+
+  const int qq = lane & 31;
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi) {
+    const float l_tot = __shfl(r.lsum[qi][0], qq < 16 ? qq : qq + 16, 64);
+    const int q = qw0 + qi * 32 + qq;
+    if (sp.nsplit > 1) {
+      const int qin = wave * 64 + qi * 32 + qq;
+      store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qin) * 66, r.o[qi], 0.f, l_tot,
+                    hl);
+    } else {
+      store_out(d, r.o[qi], l_tot, q, b, h, hl, false, 0.f);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // S16: the W64 structure (4-wave workgroups of 256 queries, 64 queries per wave, 128-key tiles through the same
 // 2-slot LDS-DMA ring) on the 16x16x32 bf16 MFMA instead of 32x32x16.  Same FLOPs, same LDS bytes and the same VALU
 // per score; the chip holds a higher clock on the 16x16x32 shape under load (MI355X_MICROARCH.md 'DVFS give-back'
@@ -1468,14 +1793,16 @@ struct AttnVar {
   const void* fn;
   const void* fn_tail;  // the grid-tail split instance
   int threads;
+  int lds;  // dynamic LDS bytes
 };
 static const AttnVar attn_vars[] = {
-    {(const void*)attn_fwd<MODE_LAZY>, (const void*)attn_fwd<MODE_LAZY, true>, NW * 64},
-    {(const void*)attn_fwd<MODE_BOUNDED>, (const void*)attn_fwd<MODE_BOUNDED, true>, NW * 64},
-    {(const void*)attn_fwd_w64<false>, (const void*)attn_fwd_w64<true>, NW4 * 64},
-    {(const void*)attn_fwd_s16<false>, (const void*)attn_fwd_s16<true>, NW4 * 64},
-    {(const void*)attn_fwd_s16<false, true>, (const void*)attn_fwd_s16<true, true>, NW4 * 64},
-    {(const void*)attn_fwd_s16<false, false, 1>, (const void*)attn_fwd_s16<true, false, 1>, NW4 * 64},
+    {(const void*)attn_fwd<MODE_LAZY>, (const void*)attn_fwd<MODE_LAZY, true>, NW * 64, LDS_BYTES},
+    {(const void*)attn_fwd<MODE_BOUNDED>, (const void*)attn_fwd<MODE_BOUNDED, true>, NW * 64, LDS_BYTES},
+    {(const void*)attn_fwd_w64<false>, (const void*)attn_fwd_w64<true>, NW4 * 64, LDS_BYTES},
+    {(const void*)attn_fwd_s16<false>, (const void*)attn_fwd_s16<true>, NW4 * 64, LDS_BYTES},
+    {(const void*)attn_fwd_s16<false, true>, (const void*)attn_fwd_s16<true, true>, NW4 * 64, LDS_BYTES},
+    {(const void*)attn_fwd_s16<false, false, 1>, (const void*)attn_fwd_s16<true, false, 1>, NW4 * 64, LDS_BYTES},
+    {(const void*)attn_fwd_p1<false>, (const void*)attn_fwd_p1<true>, NW4 * 64, P1_LDS},
 };
 constexpr int ATTN_NVAR = sizeof(attn_vars) / sizeof(attn_vars[0]);
 
@@ -1511,10 +1838,10 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     for (int i = 0; i < ATTN_NVAR; ++i) {
-      (void)hipFuncSetAttribute(attn_vars[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-      (void)hipFuncSetAttribute(attn_vars[i].fn_tail, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      (void)hipFuncSetAttribute(attn_vars[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize, attn_vars[i].lds);
+      (void)hipFuncSetAttribute(attn_vars[i].fn_tail, hipFuncAttributeMaxDynamicSharedMemorySize, attn_vars[i].lds);
       int per_cu = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, attn_vars[i].fn, attn_vars[i].threads, LDS_BYTES) !=
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, attn_vars[i].fn, attn_vars[i].threads, attn_vars[i].lds) !=
           hipSuccess)
         per_cu = 0;
       slots_v[i] = per_cu * cus;
@@ -1534,6 +1861,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
     if (e[0] == 'w' && e[1] == '6') return 2;
     if (e[0] == 's') return e[3] == 'i' ? 5 : 3;  // s16 / s16i
     if (e[0] == 'a') return 4;  // a16
+    if (e[0] == 'p') return 6;  // p1
     return dflt;
   };
   int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 2)
@@ -1586,13 +1914,13 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   if (main_blocks > 0) {
     const AttnSplit none = {0, 1, nullptr};
     void* args[] = {(void*)d, (void*)&none};
-    le = hipLaunchKernel(v.fn, dim3((unsigned)main_blocks), dim3(v.threads), args, LDS_BYTES, (hipStream_t)stream);
+    le = hipLaunchKernel(v.fn, dim3((unsigned)main_blocks), dim3(v.threads), args, v.lds, (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
   }
   if (split) {
     const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace};
     void* args[] = {(void*)d, (void*)&sp};
-    le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.threads), args, LDS_BYTES,
+    le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.threads), args, v.lds,
                          (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
     const int nthreads = pl.ntail * QB * 16;

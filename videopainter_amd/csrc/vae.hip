@@ -245,6 +245,186 @@ __global__ __launch_bounds__(CNT, 2) void conv3d_kernel(const vp_conv3d_desc d, 
   }
 }
 
+// ---- PIPE: the counted-vmcnt pipeline for the wide convolutions (Cin >= 64, Cout > 64) ----
+// 8 waves, 256 pixels x 128 channels per workgroup (4 x 2 waves of 64 x 64, the same per-wave fragment code as above),
+// 64-K tiles through a 3-slot LDS ring (48 KB per slot, one workgroup per CU, 2 waves per SIMD).  The DMA of tile
+// kt + 2 is issued right after the barrier that opens tile kt, so two tiles' loads stay in flight across every
+// barrier and the wait before it is counted (vmcnt(6): the next tile's 6 loads per thread may still be pending),
+// never a drain — the GEMM's pipelining rule (cdna_hip_programming.md §5 "Pipelining across barriers").  The DMA is
+// inline asm: with the builtin the compiler would wait for every LDS-DMA write before each LDS read.
+constexpr int PBM = 256, PBN = 128, PNT = 512, PSLOTS = 3;
+constexpr int P_A = PBM * CBK * 2;                           // 32 KB
+constexpr int P_B = PBN * CBK * 2;                           // 16 KB
+constexpr int P_STAGE = P_A + P_B;                           // 48 KB
+constexpr int P_LDS = PSLOTS * P_STAGE + VP_CONV_MAX_T * 4;  // 144.5 KB
+constexpr int P_AI = PBM * 8 / PNT;                          // A chunks (DMA instructions) per thread and K-tile
+constexpr int P_BI = PBN * 8 / PNT;                          // B chunks
+static_assert(P_AI == 4 && P_BI == 2, "vmcnt(6) below = one K-tile of DMA per thread");
+
+VP_DEV void glds16_asm(const void* src, char* lds) {
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(la), "v"(src) : "memory", "m0");
+}
+
+__global__ __launch_bounds__(PNT, 1) void conv3d_pipe_kernel(const vp_conv3d_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* tmapl = (int*)(smem + PSLOTS * P_STAGE);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  constexpr int FM = 4, FN = 4, WM = 64, WN = 64;
+
+  const int HWo = d.Hout * d.Wout;
+  const int64_t THWo = (int64_t)d.Tout * HWo;
+  const int64_t M = (int64_t)d.B * THWo;
+  const int tiles_n = (d.Cout + PBN - 1) / PBN;
+  const int tl = xcd_remap(blockIdx.x, gridDim.x);
+  const int n0 = (tl % tiles_n) * PBN;
+  const int64_t m0 = (int64_t)(tl / tiles_n) * PBM;
+
+  const int nv = d.Tout + d.kt - 1;
+  for (int v = tid; v < nv; v += PNT) tmapl[v] = d.tmap[v];
+
+  const int C8 = d.Cin >> 3;
+  const int khw = d.kh * d.kw;
+  const int kc_total = d.kt * khw * C8;
+  const int64_t Ktot = (int64_t)kc_total * 8;
+  const int Hu = d.Hin * d.uh, Wu = d.Win * d.uw;
+  const int ush = d.uh >> 1, usw = d.uw >> 1;
+  const int64_t HWi = (int64_t)d.Hin * d.Win;
+  int rb[P_AI], rt[P_AI], ry[P_AI], rx[P_AI];
+  bool rv[P_AI];
+#pragma unroll
+  for (int i = 0; i < P_AI; ++i) {
+    const int r = (i * 8 + wave) * 8 + (lane >> 3);
+    const int64_t m = m0 + r;
+    rv[i] = m < M;
+    const int64_t mm = rv[i] ? m : 0;
+    const int b = (int)(mm / THWo);
+    const int rem = (int)(mm - (int64_t)b * THWo);
+    const int t = rem / HWo;
+    const int rem2 = rem - t * HWo;
+    const int yo = rem2 / d.Wout;
+    const int xo = rem2 - yo * d.Wout;
+    rb[i] = b;
+    rt[i] = t;
+    ry[i] = yo * d.sh - d.ph;
+    rx[i] = xo * d.sw - d.pw;
+  }
+  const bf16* X = (const bf16*)d.x;
+  const bf16* Hs = (const bf16*)d.hist;
+  const bf16* Wt = (const bf16*)d.w;
+  const char* abase[P_AI];
+  int amask[P_AI];
+  const char* wbase[P_BI];
+#pragma unroll
+  for (int j = 0; j < P_BI; ++j) {
+    const int r = (j * 8 + wave) * 8 + (lane >> 3);
+    const int n = min(n0 + r, d.Cout - 1);
+    wbase[j] = (const char*)(Wt + (int64_t)n * Ktot + (((lane & 7) ^ cswz(r)) << 3));
+  }
+  const int tpt = C8 >> 3;  // K-tiles per tap
+  auto set_tap = [&](int tap) {
+    const int dt = khw == 1 ? tap : tap / khw;
+    const int rem = tap - dt * khw;
+    const int dy = d.kw == 1 ? rem : rem / 3;
+    const int dx = rem - dy * d.kw;
+#pragma unroll
+    for (int i = 0; i < P_AI; ++i) {
+      const int r = (i * 8 + wave) * 8 + (lane >> 3);
+      const int yu = ry[i] + dy, xu = rx[i] + dx;
+      const bf16* p = nullptr;
+      if (rv[i] && yu >= 0 && yu < Hu && xu >= 0 && xu < Wu) {
+        const int f = tmapl[rt[i] + dt];
+        const int64_t pix = (f >= 0 ? (int64_t)rb[i] * d.x_frames + f : (int64_t)rb[i] * d.hist_frames + (-1 - f)) *
+                                HWi + (int64_t)(yu >> ush) * d.Win + (xu >> usw);
+        p = (f >= 0 ? X : Hs) + pix * d.Cin;
+      }
+      amask[i] = p != nullptr ? -1 : 0;
+      abase[i] = p != nullptr ? (const char*)(p + (((lane & 7) ^ cswz(r)) << 3)) : (const char*)g_zero16;
+    }
+  };
+  auto stage = [&](int kt, char* buf) {
+    if ((kt & (tpt - 1)) == 0) set_tap(kt / tpt);
+    const int cb = (kt & (tpt - 1)) * 128;
+#pragma unroll
+    for (int i = 0; i < P_AI; ++i) glds16_asm(abase[i] + (cb & amask[i]), buf + (i * 8 + wave) * 1024);
+#pragma unroll
+    for (int j = 0; j < P_BI; ++j) glds16_asm(wbase[j] + (int64_t)kt * 128, buf + P_A + (j * 8 + wave) * 1024);
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int i = 0; i < FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  __syncthreads();  // tmap in LDS
+  const int nk = kc_total / 8;  // Cin >= 64: whole 64-channel K-tiles
+  stage(0, smem);
+  if (nk > 1) stage(1, smem + P_STAGE);
+  const int lrow = lane & 15;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nk) stage(kt + 2, smem + ((kt + 2) % PSLOTS) * P_STAGE);
+    const char* cur = smem + (kt % PSLOTS) * P_STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 4 + (lane >> 4);
+      bf16x8 af[FM], wf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wr * WM + i * 16 + lrow;
+        af[i] = *(const bf16x8*)(cur + row * 128 + ((ch ^ cswz(row)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wc * WN + j * 16 + lrow;
+        wf[j] = *(const bf16x8*)(cur + P_A + row * 128 + ((ch ^ cswz(row)) << 4));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  const bf16* bias = (const bf16*)d.bias;
+  const bf16* R = (const bf16*)d.resid;
+  bf16* Y = (bf16*)d.y;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wc * WN + j * 16 + (lane >> 4) * 4;
+    if (n >= d.ldy) continue;
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = (bias != nullptr && n + r < d.Cout) ? bf2f(bias[n + r]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int64_t m = m0 + wr * WM + i * 16 + lrow;
+      if (m >= M) continue;
+      bf16x4 rv4;
+      if (R != nullptr && n < d.Cout) rv4 = *(const bf16x4*)(R + m * d.ldr + n);
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = rbf(acc[j][i][r] + bv[r]);
+        if (R != nullptr && n < d.Cout) v += bf2f(rv4[r]);
+        o[r] = f2bf(n + r < d.Cout ? v : 0.f);
+      }
+      *(bf16x4*)(Y + m * d.ldy + n) = o;
+    }
+  }
+}
+
 // ---- GroupNorm ----
 constexpr int GN_MAX_BLOCKS = 1024;
 
@@ -583,6 +763,20 @@ extern "C" int vp_conv3d_bf16(const vp_conv3d_desc* d, void* stream) {
     const int64_t t = tiles_m * ((d->Cout + 63) / 64);
     if (t >= (1ll << 31)) return VP_ERR_UNSUPPORTED;
     return launch_conv<64>(*d, c8s, t, s);
+  }
+  // wide convolutions (Cin >= 64): the counted-vmcnt pipeline; VP_CONV_PIPE=0 keeps the 2-stage ring (A/B)
+  const char* pe = getenv("VP_CONV_PIPE");
+  if (d->Cin >= 64 && (pe == nullptr || atoi(pe) != 0)) {
+    const int64_t t = ((M + PBM - 1) / PBM) * ((d->Cout + PBN - 1) / PBN);
+    if (t >= (1ll << 31)) return VP_ERR_UNSUPPORTED;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)conv3d_pipe_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, P_LDS);
+      attr = true;
+    }
+    hipLaunchKernelGGL(conv3d_pipe_kernel, dim3((unsigned)t), dim3(PNT), P_LDS, s, *d);
+    VP_CHECK_LAUNCH();
+    return VP_OK;
   }
   const int64_t t = tiles_m * ((d->Cout + 127) / 128);
   if (t >= (1ll << 31)) return VP_ERR_UNSUPPORTED;
