@@ -213,6 +213,13 @@ VP_DEV int lane_id_opaque() {
   return l;
 }
 
+// the same with the LDS destination given as a 32-bit LDS byte address (wave-uniform, e.g. a precomputed base of
+// the dynamic LDS plus a constant): no generic -> LDS pointer conversion (and its null check) per instruction
+VP_DEV void glds16_lds(const char* sbase, int voff, unsigned la) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(la), "v"(voff), "s"(sbase)
+               : "memory", "m0");
+}
+
 VP_DEV void glds16(const char* sbase, int voff, char* lds) {
   // (the LDS address is wave-uniform; readfirstlane keeps it an SGPR where the compiler loses track of that)
   const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)lds);
@@ -501,7 +508,10 @@ constexpr int NW4 = 4;
 constexpr int PPW4 = NP / NW4;
 static_assert(NW4 * 64 == QB, "same query block as the 8-wave kernel");
 
-template <bool TAIL = false>
+// FAST: the full tiles of segment 1 are DMA'd from one scalar base per operand and tile with per-lane offsets fixed
+// for the whole loop (no per-tile segment lookup, row clamp or 64-bit offset multiply); segment 2 and partial tiles
+// take the general path with the lane's rows recomputed from the lane id.
+template <bool TAIL = false, bool FAST = false>
 __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_w64(const vp_attn_desc d, const AttnSplit sp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -539,15 +549,8 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_w64(const vp_attn_desc d
     }
   }
 
-  int prow[PPW4], kch[PPW4], vch[PPW4];
-#pragma unroll
-  for (int i = 0; i < PPW4; ++i) {
-    prow[i] = (wave + i * NW4) * 8 + (lane >> 3);
-    kch[i] = (lane & 7) ^ swz(prow[i]);
-    vch[i] = (lane & 7) ^ vswz(prow[i]);
-  }
   auto slot_of = [&](int ti) { return smem + (ti & 1) * ST; };
-  auto issue = [&](int ti) {
+  auto issue_general = [&](int ti, int ln) {
     const Seg sg = tile_seg(d, ti, tiles1, b, h);
     char* slot = slot_of(ti);
     const int last = sg.n - 1 - sg.key0;
@@ -557,9 +560,62 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_w64(const vp_attn_desc d
 #pragma unroll
     for (int i = 0; i < PPW4; ++i) {
       const int pc = wave + i * NW4;
-      const int r = min(prow[i], last);
-      glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + pc * 1024);
-      glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
+      const int prow = pc * 8 + (ln >> 3);
+      const int r = min(prow, last);
+      glds16(kb, (r * ksn + (((ln & 7) ^ swz(prow)) * 8)) * 2, slot + pc * 1024);
+      glds16(vb, (r * vsn + (((ln & 7) ^ vswz(prow)) * 8)) * 2, slot + KT + pc * 1024);
+    }
+  };
+  int prow[PPW4], kch[PPW4], vch[PPW4];
+  if constexpr (!FAST) {
+#pragma unroll
+    for (int i = 0; i < PPW4; ++i) {
+      prow[i] = (wave + i * NW4) * 8 + (lane >> 3);
+      kch[i] = (lane & 7) ^ swz(prow[i]);
+      vch[i] = (lane & 7) ^ vswz(prow[i]);
+    }
+  }
+  int voff_k[PPW4], voff_v[PPW4];
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < PPW4; ++i) {
+      const int prow = (wave + i * NW4) * 8 + (lane >> 3);
+      voff_k[i] = (prow * (int)d.k_sn + (((lane & 7) ^ swz(prow)) * 8)) * 2;
+      voff_v[i] = (prow * (int)d.v_sn + (((lane & 7) ^ vswz(prow)) * 8)) * 2;
+    }
+  }
+  const char* kseg1 = (const char*)((const bf16*)d.K + (int64_t)b * d.k_sb + h * 64);
+  const char* vseg1 = (const char*)((const bf16*)d.V + (int64_t)b * d.v_sb + h * 64);
+  const int full1 = d.Nk / KB;
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem) + wave * 1024;
+  auto issue = [&](int ti) {
+    if constexpr (FAST) {
+      if (ti < full1) {
+        const unsigned la = lds0 + (ti & 1) * ST;
+        const char* kb = kseg1 + (int64_t)ti * KB * d.k_sn * 2;
+        const char* vb = vseg1 + (int64_t)ti * KB * d.v_sn * 2;
+#pragma unroll
+        for (int i = 0; i < PPW4; ++i) {
+          glds16_lds(kb, voff_k[i], la + i * NW4 * 1024);
+          glds16_lds(vb, voff_v[i], la + KT + i * NW4 * 1024);
+        }
+        return;
+      }
+      issue_general(ti, lane_id_opaque());
+    } else {
+      const Seg sg = tile_seg(d, ti, tiles1, b, h);
+      char* slot = slot_of(ti);
+      const int last = sg.n - 1 - sg.key0;
+      const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
+      const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
+      const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
+#pragma unroll
+      for (int i = 0; i < PPW4; ++i) {
+        const int pc = wave + i * NW4;
+        const int r = min(prow[i], last);
+        glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + pc * 1024);
+        glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
+      }
     }
   };
 
@@ -1803,6 +1859,7 @@ static const AttnVar attn_vars[] = {
     {(const void*)attn_fwd_s16<false, true>, (const void*)attn_fwd_s16<true, true>, NW4 * 64, LDS_BYTES},
     {(const void*)attn_fwd_s16<false, false, 1>, (const void*)attn_fwd_s16<true, false, 1>, NW4 * 64, LDS_BYTES},
     {(const void*)attn_fwd_p1<false>, (const void*)attn_fwd_p1<true>, NW4 * 64, P1_LDS},
+    {(const void*)attn_fwd_w64<false, true>, (const void*)attn_fwd_w64<true, true>, NW4 * 64, LDS_BYTES},
 };
 constexpr int ATTN_NVAR = sizeof(attn_vars) / sizeof(attn_vars[0]);
 
@@ -1858,13 +1915,13 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
     if (e == nullptr || e[0] == 0) return dflt;
     if (e[0] == 'l') return 0;
     if (e[0] == 'w' && e[1] == '3') return 1;
-    if (e[0] == 'w' && e[1] == '6') return 2;
+    if (e[0] == 'w' && e[1] == '6') return e[3] == 'f' ? 7 : 2;  // w64 / w64f
     if (e[0] == 's') return e[3] == 'i' ? 5 : 3;  // s16 / s16i
     if (e[0] == 'a') return 4;  // a16
     if (e[0] == 'p') return 6;  // p1
     return dflt;
   };
-  int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 2)
+  int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 7)
                                                     : pick(getenv("VP_ATTN_UNBOUNDED_MODE"), 4);
   if (!(d->flags & VP_ATTN_BOUNDED_SCORES) && variant != 4) variant = 0;  // unbounded: lazy / anchored
   // the resample processor's segment hints (k2_full / k2_len / l_extra) are implemented by the 16x16x32 kernels only:
