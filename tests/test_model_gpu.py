@@ -747,7 +747,7 @@ def test_config5_full_model_matches_reference():
     torch.cuda.empty_cache()
 
 
-FP8_CONFIG5_MODEL_GATE = 6e-2  # set from the first measurement
+FP8_CONFIG5_MODEL_GATE = 4.1e-2  # 1.5x the measured 2.690e-2 (profiles/r03_config5_full_model_test.log)
 
 
 @torch.no_grad()
