@@ -23,18 +23,19 @@ def gemm_variant(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["lazy", "bounded", "w32", "w64", "a16", "s16i", "p1"], ids=lambda v: f"attn_{v}")
+@pytest.fixture(params=["lazy", "bounded", "w32", "w64", "w64f", "a16", "s16i", "p1", "p2"], ids=lambda v: f"attn_{v}")
 def attn_variant(request, monkeypatch):
     """Unbounded-score launches: a16 (the anchored-softmax 16x16x32 kernel, the library default), lazy (the
     running-max kernel; VP_ATTN_UNBOUNDED_MODE).  Bounded-score launches
     (include/vp_hip.h VP_ATTN_BOUNDED_SCORES, the host proved the bound): bounded = the library default (s16, 64
-    queries per wave on the 16x16x32 MFMA), w32 / w64 / s16i / p1 the 8-wave, two-blocks-per-wave 32x32x16,
-    per-query-tile-PV and one-wave-per-SIMD software-pipelined forms (VP_ATTN_BOUNDED_MODE)."""
+    queries per wave on the 16x16x32 MFMA), w32 / w64 / w64f / s16i / p1 / p2 the 8-wave, two-blocks-per-wave
+    32x32x16 (w64f: scalar-base DMA), per-query-tile-PV and software-pipelined (one / two workgroups per CU) forms
+    (VP_ATTN_BOUNDED_MODE)."""
     monkeypatch.delenv("VP_ATTN_UNBOUNDED_MODE", raising=False)
     monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
     if request.param in ("lazy", "a16"):
         monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", request.param)
-    elif request.param in ("w32", "w64", "s16i", "p1"):
+    elif request.param in ("w32", "w64", "w64f", "s16i", "p1", "p2"):
         monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", request.param)
     else:
         monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
@@ -521,7 +522,7 @@ def test_attention_tail_split_matches_unsplit(Nq, Nk2, monkeypatch):
         assert rel(out_s, ref) < 1e-2 and rel(out_u, ref) < 1e-2
 
 
-@pytest.mark.parametrize("mode", ["w64", "s16", "p1"])
+@pytest.mark.parametrize("mode", ["w64", "w64f", "s16", "p1", "p2"])
 @pytest.mark.parametrize("Nq,Nk2", [(1500, 700), (17776, 0)])
 def test_attention_bounded_tail_split_matches_unsplit(Nq, Nk2, mode, monkeypatch):
     """The bounded-score kernels' grid-tail split instances (partials + merge) against their unsplit launch and, at
@@ -628,7 +629,7 @@ def test_partition_rows_index_and_permuted_writes(B, N):
         assert not vgot[b, int(cnt[b]):].any()  # the null keys' values are zero (the k2_full contract)
 
 
-@pytest.mark.parametrize("mode", ["s16", "a16", "w64"])
+@pytest.mark.parametrize("mode", ["s16", "a16", "w64", "p2"])
 def test_attention_k2_full_hint(mode, monkeypatch):
     """The k2_full hint (segment-2 keys past k2_full[b] have zero values: row sums only) gives the attention of the
     same segments without the hint; per-batch split points, one straddling a tile, one past every tile."""
@@ -739,7 +740,7 @@ def test_null_key_mass_matches_explicit_null_keys():
 
 
 @pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
-@pytest.mark.parametrize("mode", ["s16", "a16"])
+@pytest.mark.parametrize("mode", ["s16", "a16", "p2", "p1"])
 def test_attention_k2_len_and_l_extra(mode, split, monkeypatch):
     """k2_len (only the first k2_len[b] keys of segment 2) and l_extra (extra row-sum mass per query, log2 score
     units) against fp64 attention over the truncated segments with 2^l_extra added to each denominator.  At this size

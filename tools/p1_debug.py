@@ -36,7 +36,7 @@ def run(Nq, Nk, mode, split):
         print("   ratio o/ref row", q0, [round(x, 3) for x in (o.float().cpu()[0, q0, :8] / ref[0, q0, :8]).tolist()])
 
 
-for mode in ("w64", "p1", "w64f"):
+for mode in ("p1", "p2"):
     for Nq, Nk, split in ((256, 128, False), (256, 256, False), (256, 640, False), (256, 300, False),
                           (300, 300, True), (512, 1024, False)):
         run(Nq, Nk, mode, split)

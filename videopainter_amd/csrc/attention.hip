@@ -841,6 +841,11 @@ VP_DEV void p1_mask(f32x16& s, int rem, int hl4) {
 // the first tile).  The tile seam is at the start of step (3, 0): wait for the next tile (vmcnt: one tile per wave
 // left in flight unless wait_all), pass the barrier, read its K(0); last: no next tile (that QK^T is skipped).
 // masked: keys >= lim get score -inf (a segment's partial last tile; a uniform branch before the step).
+// SL = 2 (two workgroups per CU, a 2-slot ring, 256 registers per wave): the next tile's DMA is issued at the top of
+// the tile into the slot this tile's predecessor used, so every read of a slot comes before the seam barrier; V^T is
+// single-buffered (read after the even step's PV, a 4-MFMA group before the odd step's), and the seam moves to the
+// end of step (3, 0), after V(3) is read
+template <int SL>
 VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn, int lim, bool masked, bool last,
                     bool wait_all, int lane, const int (&vo)[2]) {
   const int hl = lane >> 5;
@@ -850,7 +855,7 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
     // even step (h, 0)
     if (h < 3) {
       p1_read_k(Kl, h + 1, lane, r.kf[(h + 1) & 1]);
-    } else if (!last) {
+    } else if (SL == 4 && !last) {
       if (wait_all)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else
@@ -859,27 +864,39 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
       asm volatile("" ::: "memory");
       p1_read_k(Kn, 0, lane, r.kf[0]);
     }
-    p1_read_v(Vl, h, vo, r.vf[h & 1]);
+    if constexpr (SL == 4) p1_read_v(Vl, h, vo, r.vf[h & 1]);
     if (masked) p1_mask(r.s[0], lim - 32 * h, 4 * hl);
-    if (h & 1)
+    if constexpr (SL == 2) {
+      if (h & 1)
+        p1_step<0, 1, 1, 1, 0, true>(r, sel);
+      else
+        p1_step<0, 1, 1, 0, 0, true>(r, sel);
+      p1_read_v(Vl, h, vo, r.vf[0]);
+      if (h == 3 && !last) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        p1_read_k(Kn, 0, lane, r.kf[0]);
+      }
+    } else if (h & 1) {
       p1_step<0, 1, 1, 1, 0, true>(r, sel);
-    else
+    } else {
       p1_step<0, 1, 1, 0, 1, true>(r, sel);
+    }
     // odd step (h, 1)
     if (masked) p1_mask(r.s[1], lim - 32 * h, 4 * hl);
-    if (h < 3 || !last) {
-      if (h & 1)
-        p1_step<1, 0, 0, 0, 1, true>(r, sel);
-      else
-        p1_step<1, 0, 0, 1, 0, true>(r, sel);
-    } else {
-      p1_step<1, 0, 0, 0, 1, false>(r, sel);
-    }
+    // (the last tile's step (3, 1) runs its QK^T too, on stale K fragments, result unused: one code path, so the
+    // accumulators keep their registers through the tile)
+    constexpr int VO = SL == 2 ? 0 : -1;
+    if (h & 1)
+      p1_step<1, 0, 0, 0, VO < 0 ? 1 : 0, true>(r, sel);
+    else
+      p1_step<1, 0, 0, 1, 0, true>(r, sel);
   }
 }
 
-template <bool TAIL = false>
-__global__ __launch_bounds__(NW4 * 64, 1) void attn_fwd_p1(const vp_attn_desc d, const AttnSplit sp) {
+template <bool TAIL = false, int SL = 4>
+__global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const vp_attn_desc d, const AttnSplit sp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -894,7 +911,9 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_fwd_p1(const vp_attn_desc d,
   const int b = bh / d.H;
   const int h = bh - b * d.H;
   const int tiles1 = (d.Nk + KB - 1) / KB;
-  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KB - 1) / KB : 0;
+  // segment 2 of this batch row: its first k2_len[b] keys (the resample processor's masked rows), or all Nk2
+  const int n2 = d.k2_len != nullptr ? max(0, min(__builtin_amdgcn_readfirstlane(d.k2_len[b]), d.Nk2)) : d.Nk2;
+  const int tiles2 = n2 > 0 ? (n2 + KB - 1) / KB : 0;
   const int ntiles_all = tiles1 + tiles2;
   const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
   const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
@@ -916,40 +935,36 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_fwd_p1(const vp_attn_desc d,
       }
     }
   }
-  int prow[PPW4], kch[PPW4], vch[PPW4];
-#pragma unroll
-  for (int i = 0; i < PPW4; ++i) {
-    prow[i] = (wave + i * NW4) * 8 + (lane >> 3);
-    kch[i] = (lane & 7) ^ swz(prow[i]);
-    vch[i] = (lane & 7) ^ vswz(prow[i]);
-  }
-  auto slot_of = [&](int ti) { return smem + (ti & (P1_SLOTS - 1)) * ST; };
+  auto slot_of = [&](int ti) { return smem + (ti & (SL - 1)) * ST; };
   // full tiles of segment 1 (all but possibly its last): one scalar base per operand and tile, the lane offsets fixed
-  // (voff_*); segment 2 and partial tiles take the general path (rows past the end re-read the last key)
+  // (voff_*), the LDS destination from a precomputed base; segment 2 and partial tiles take the general path with the
+  // lane's rows recomputed from the lane id (rows past the end re-read the last key)
   int voff_k[PPW4], voff_v[PPW4];
 #pragma unroll
   for (int i = 0; i < PPW4; ++i) {
-    voff_k[i] = (prow[i] * (int)d.k_sn + kch[i] * 8) * 2;
-    voff_v[i] = (prow[i] * (int)d.v_sn + vch[i] * 8) * 2;
+    const int prow = (wave + i * NW4) * 8 + (lane >> 3);
+    voff_k[i] = (prow * (int)d.k_sn + (((lane & 7) ^ swz(prow)) * 8)) * 2;
+    voff_v[i] = (prow * (int)d.v_sn + (((lane & 7) ^ vswz(prow)) * 8)) * 2;
   }
   const char* kseg1 = (const char*)((const bf16*)d.K + (int64_t)b * d.k_sb + h * 64);
   const char* vseg1 = (const char*)((const bf16*)d.V + (int64_t)b * d.v_sb + h * 64);
-  const int64_t ktile_bytes = (int64_t)KB * d.k_sn * 2, vtile_bytes = (int64_t)KB * d.v_sn * 2;
-  const int full1 = d.Nk / KB;  // full tiles of segment 1
+  const int full1 = d.Nk / KB;
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem) + wave * 1024;
   auto issue = [&](int ti) {
-    char* slot = slot_of(ti);
     if (ti < full1) {
-      const char* kb = kseg1 + ti * ktile_bytes;
-      const char* vb = vseg1 + ti * vtile_bytes;
+      const unsigned la = lds0 + (ti & (SL - 1)) * ST;
+      const char* kb = kseg1 + (int64_t)ti * KB * d.k_sn * 2;
+      const char* vb = vseg1 + (int64_t)ti * KB * d.v_sn * 2;
 #pragma unroll
       for (int i = 0; i < PPW4; ++i) {
-        const int pc = wave + i * NW4;
-        glds16(kb, voff_k[i], slot + pc * 1024);
-        glds16(vb, voff_v[i], slot + KT + pc * 1024);
+        glds16_lds(kb, voff_k[i], la + i * NW4 * 1024);
+        glds16_lds(vb, voff_v[i], la + KT + i * NW4 * 1024);
       }
       return;
     }
-    const Seg sg = tile_seg(d, ti, tiles1, b, h);
+    const int ln = lane_id_opaque();
+    const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
+    char* slot = slot_of(ti);
     const int last = sg.n - 1 - sg.key0;
     const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
     const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
@@ -957,9 +972,10 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_fwd_p1(const vp_attn_desc d,
 #pragma unroll
     for (int i = 0; i < PPW4; ++i) {
       const int pc = wave + i * NW4;
-      const int rr = min(prow[i], last);
-      glds16(kb, (rr * ksn + kch[i] * 8) * 2, slot + pc * 1024);
-      glds16(vb, (rr * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
+      const int prow = pc * 8 + (ln >> 3);
+      const int rr = min(prow, last);
+      glds16(kb, (rr * ksn + (((ln & 7) ^ swz(prow)) * 8)) * 2, slot + pc * 1024);
+      glds16(vb, (rr * vsn + (((ln & 7) ^ vswz(prow)) * 8)) * 2, slot + KT + pc * 1024);
     }
   };
   static_assert(2 * PPW4 == 8, "vmcnt(8) in p1_tile = one tile of DMA per wave");
@@ -983,7 +999,7 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_fwd_p1(const vp_attn_desc d,
     for (int j = 0; j < 2; ++j) r.pf[qi][j] = (u32x4){0u, 0u, 0u, 0u};
   }
 #pragma unroll
-  for (int c = 0; c < 4; ++c) r.vf[1][c] = (bf16x8){};  // job -1: 0 x 0
+  for (int c = 0; c < 4; ++c) r.vf[SL == 2 ? 0 : 1][c] = (bf16x8){};  // job -1: 0 x 0
   bf16x8 sel;
   {
     const bf16 one = f2bf((((lane >> 4) & 1) == 0) == ((lane & 15) < 8) ? 1.f : 0.f);
@@ -991,15 +1007,17 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_fwd_p1(const vp_attn_desc d,
     for (int e = 0; e < 8; ++e) sel[e] = one;
   }
 
-  issue(tbeg);
-  if (tbeg + 1 < tend) {
+  // (a tail-split range is empty when k2_len leaves this row fewer tiles than splits: its record is O = 0, l = 0)
+  const bool any = tbeg < tend;  // workgroup-uniform
+  if (any) issue(tbeg);
+  if (SL == 4 && tbeg + 1 < tend) {
     issue(tbeg + 1);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
-  p1_read_k(slot_of(tbeg), 0, lane, r.kf[0]);
+  if (any) p1_read_k(slot_of(tbeg), 0, lane, r.kf[0]);
   {
     const f32x16 z = {};
 #pragma unroll
@@ -1008,28 +1026,31 @@ __global__ __launch_bounds__(NW4 * 64, 1) void attn_fwd_p1(const vp_attn_desc d,
   }
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // S -> the first (asm) exp
   for (int ti = tbeg; ti < tend; ++ti) {
-    if (ti + 2 < tend) issue(ti + 2);
+    if (ti + SL / 2 < tend) issue(ti + SL / 2);
     int lim = KB;
     if (ti >= full1) {
-      const Seg sg = tile_seg(d, ti, tiles1, b, h);
+      const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
       lim = sg.n - sg.key0;
     }
-    p1_tile(r, sel, slot_of(ti), slot_of(ti + 1), __builtin_amdgcn_readfirstlane(lim), lim < KB, ti + 1 >= tend,
+    p1_tile<SL>(r, sel, slot_of(ti), slot_of(ti + 1), __builtin_amdgcn_readfirstlane(lim), lim < KB, ti + 1 >= tend,
             ti + 2 >= tend, lane, vo);
   }
   // drain: PV + row sums of the last job (3, 1)
 #pragma unroll
   for (int c = 0; c < 4; ++c)
-    r.o[1][c & 1] =
-        __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.vf[1][c], as_bf16x8(r.pf[1][c >> 1]), r.o[1][c & 1], 0, 0, 0);
+    r.o[1][c & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.vf[SL == 2 ? 0 : 1][c], as_bf16x8(r.pf[1][c >> 1]),
+                                                            r.o[1][c & 1], 0, 0, 0);
   r.lsum[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[1][0]), r.lsum[1], 0, 0, 0);
   r.lsum[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[1][1]), r.lsum[1], 0, 0, 0);
 
   const int qq = lane & 31;
 #pragma unroll
   for (int qi = 0; qi < 2; ++qi) {
-    const float l_tot = __shfl(r.lsum[qi][0], qq < 16 ? qq : qq + 16, 64);
+    float l_tot = __shfl(r.lsum[qi][0], qq < 16 ? qq : qq + 16, 64);
     const int q = qw0 + qi * 32 + qq;
+    // l_extra: row-sum mass of keys outside the segments (the resample processor's null keys, log2 score units;
+    // bounded mode: reference point 0); a tail-split partial leaves it to attn_combine_kernel
+    if (!TAIL && d.l_extra != nullptr) l_tot += __builtin_amdgcn_exp2f(d.l_extra[((int64_t)b * d.H + h) * d.Nq + min(q, d.Nq - 1)]);
     if (sp.nsplit > 1) {
       const int qin = wave * 64 + qi * 32 + qq;
       store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qin) * 66, r.o[qi], 0.f, l_tot,
@@ -1860,6 +1881,7 @@ static const AttnVar attn_vars[] = {
     {(const void*)attn_fwd_s16<false, false, 1>, (const void*)attn_fwd_s16<true, false, 1>, NW4 * 64, LDS_BYTES},
     {(const void*)attn_fwd_p1<false>, (const void*)attn_fwd_p1<true>, NW4 * 64, P1_LDS},
     {(const void*)attn_fwd_w64<false, true>, (const void*)attn_fwd_w64<true, true>, NW4 * 64, LDS_BYTES},
+    {(const void*)attn_fwd_p1<false, 2>, (const void*)attn_fwd_p1<true, 2>, NW4 * 64, 2 * ST},
 };
 constexpr int ATTN_NVAR = sizeof(attn_vars) / sizeof(attn_vars[0]);
 
@@ -1904,11 +1926,11 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
       slots_v[i] = per_cu * cus;
     }
   }
-  // BOUNDED scores (the host proved |score| <= VP_ATTN_SCORE_BOUND): w64 (two 32-query blocks per wave on the
-  // 32x32x16 MFMA, default: 286 vs 300 ms per config-2 step for s16 in alternating bench runs, although s16 wins
-  // standalone at a higher clock); VP_ATTN_BOUNDED_MODE = lazy (running max), w32 (8 waves, one block per wave),
-  // s16 (64 queries per wave on the 16x16x32 MFMA), a16 (s16 with the anchored softmax), s16i (per-query-tile PV
-  // order) for A/B.
+  // BOUNDED scores (the host proved |score| <= VP_ATTN_SCORE_BOUND): p2 (default since round 3: the software-pipelined
+  // p1 steps at two workgroups per CU, 6.04 vs 6.49 ms per config-2 call for w64f, profiles/r03_attn_p2_ab.log);
+  // VP_ATTN_BOUNDED_MODE = w64f (two 32-query blocks per wave, scalar-base DMA), w64 (the same with the general DMA),
+  // lazy (running max), w32 (8 waves, one block per wave), s16 (64 queries per wave on the 16x16x32 MFMA), a16 (s16
+  // with the anchored softmax), s16i (per-query-tile PV order), p1 (one workgroup per CU) for A/B.
   // Unbounded scores: the anchored s16 kernel (a16, default: no bound needed, no host sync); VP_ATTN_UNBOUNDED_MODE =
   // lazy: the running-max kernel.
   auto pick = [](const char* e, int dflt) {
@@ -1918,16 +1940,22 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
     if (e[0] == 'w' && e[1] == '6') return e[3] == 'f' ? 7 : 2;  // w64 / w64f
     if (e[0] == 's') return e[3] == 'i' ? 5 : 3;  // s16 / s16i
     if (e[0] == 'a') return 4;  // a16
-    if (e[0] == 'p') return 6;  // p1
+    if (e[0] == 'p') return e[1] == '2' ? 8 : 6;  // p1 / p2 (the p1 pipeline at two workgroups per CU)
     return dflt;
   };
-  int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 7)
+  int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 8)
                                                     : pick(getenv("VP_ATTN_UNBOUNDED_MODE"), 4);
   if (!(d->flags & VP_ATTN_BOUNDED_SCORES) && variant != 4) variant = 0;  // unbounded: lazy / anchored
-  // the resample processor's segment hints (k2_full / k2_len / l_extra) are implemented by the 16x16x32 kernels only:
-  // config 4 runs s16 + k2_full at 11.3 ms per call against 13.8 for a w64 instance with the hint
-  // (profiles/r03_bench_config4_*), so hinted launches take s16 (bounded) / a16 (unbounded)
-  if (d->k2_full != nullptr || d->k2_len != nullptr || d->l_extra != nullptr) variant = (variant == 4) ? 4 : 3;
+  // the resample processor's segment hints: k2_len / l_extra (the closed-form null keys, the default) are taken by
+  // s16 / a16 and p1 / p2; k2_full (null keys as zero-value keys) by the 16x16x32 kernels only (config 4 ran s16 +
+  // k2_full at 11.3 ms per call against 13.8 for a w64 instance with the hint, profiles/r03_bench_config4_*), so a
+  // k2_full launch, and any hinted launch of another kernel, takes s16 (bounded) / a16 (unbounded)
+  if (d->k2_full != nullptr || d->k2_len != nullptr || d->l_extra != nullptr) {
+    if (variant == 4 || ((variant == 6 || variant == 8) && d->k2_full == nullptr)) {
+    } else {
+      variant = 3;
+    }
+  }
   pl.v = &attn_vars[variant];
   const int slots = slots_v[variant];
   const int nqb = (d->Nq + QB - 1) / QB;
