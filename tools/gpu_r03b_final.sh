@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 3 (second session) final tree: full GPU suite, smoke, config-2 bench, rocprof trace, config-5 bench
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+run() { local name=$1; shift; local to=$1; shift
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"
+  [ $rc -ne 0 ] && exit $rc; return 0; }
+run r03c_gtests 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -rA
+run r03c_smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+run r03c_bench 600 python bench.py
+rm -rf gpurun_out/r03c_prof
+run r03c_prof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r03c_prof -o bench --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+run r03c_bench_c5 500 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline
+exit 0

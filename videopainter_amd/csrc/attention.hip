@@ -777,6 +777,9 @@ VP_DEV uint32_t p1_pack(float a, float b) {
 }
 VP_DEV bf16x8 as_bf16x8(const u32x4& w) { return __builtin_bit_cast(bf16x8, w); }
 
+#ifndef VP_P1_RS_SPREAD
+#define VP_P1_RS_SPREAD 0
+#endif
 // one pipeline step: the QK^T chain of block QB_ (K buffer KB_; skipped when !QK) interleaved with the PV MFMAs of
 // block PB (V buffer VB_) so that no MFMA waits on the one before it, then the two row-sum MFMAs; every gap holds the
 // next exp pair of block EB's 16 scores and the pack of the pair before:
@@ -803,9 +806,18 @@ VP_DEV void p1_step(P1Regs& r, const bf16x8& sel) {
     }
     p1_exp(p[2 * g], p[2 * g + 1], r.s[EB][2 * g], r.s[EB][2 * g + 1]);
     if (g > 0) r.pf[EB][(g - 1) >> 2][(g - 1) & 3] = p1_pack(p[2 * g - 2], p[2 * g - 1]);
+#if VP_P1_RS_SPREAD
+    if (g == 3) {  // slab 0's row sum as soon as slab 0's PV MFMAs are issued (the two sums are not back to back)
+      p1_fence();
+      r.lsum[PB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[PB][0]), r.lsum[PB], 0, 0, 0);
+      p1_fence();
+    }
+#endif
   }
+#if !VP_P1_RS_SPREAD
   p1_fence();
   r.lsum[PB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[PB][0]), r.lsum[PB], 0, 0, 0);
+#endif
   p1_fence();
   r.pf[EB][1][3] = p1_pack(p[14], p[15]);
   p1_fence();
@@ -918,6 +930,9 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
   const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
   const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
   const int qw0 = qb * QB + wave * 64;
+#ifdef VP_P1_PRIO
+  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);  // A/B: static priority for every other workgroup
+#endif
 
   P1Regs r;
   {
