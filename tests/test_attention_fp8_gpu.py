@@ -138,15 +138,19 @@ def _ref_fp64(q8, k8, vt, vs, npad, Nk, H, q_exp, k_exp):
     o = torch.einsum("bhqk,bhkd->bqhd", p / p.sum(dim=-1, keepdim=True), vd)
     return o.reshape(B, Nq, H * 64)
 
-@pytest.fixture(params=["1", "2", "3"], ids=["exp2", "lin", "lin2"])
+@pytest.fixture(params=["1", "2", "3", "4"], ids=["exp2", "lin", "lin2", "lin2p"])
 def attn8_variant(request, monkeypatch):
     """VP_ATTN8_VARIANT: 1 = P by v_exp_f32 + RNE e4m3 pack, 2 = P by linear mantissa interpolation, 3 = the same
-    codes packed by v_cvt_pknorm_u16_f32 + a byte gather (default)."""
+    codes packed by v_cvt_pknorm_u16_f32 + a byte gather (default), 4 = the lin2 codes in the software-pipelined
+    kernel (f8p)."""
     monkeypatch.setenv("VP_ATTN8_VARIANT", request.param)
     return request.param
 
 
-@pytest.mark.parametrize("B,H,N,late", [(2, 3, 300, False), (1, 2, 2000, True), (1, 1, 65, False)])
+# tile counts 5 / 32 / 2 / 1 / 3: both tail paths of the pipelined kernel (an odd and an even number of tiles after
+# the first), a single partial tile, a one-key last tile
+@pytest.mark.parametrize("B,H,N,late", [(2, 3, 300, False), (1, 2, 2000, True), (1, 1, 65, False), (1, 2, 40, False),
+                                        (2, 1, 130, False)])
 def test_attention_fp8(B, H, N, late, attn8_variant):
     from videopainter_amd import kernels as K
     q, k, v = _attn_case(B, H, N, N, late)

@@ -780,19 +780,27 @@ VP_DEV bf16x8 as_bf16x8(const u32x4& w) { return __builtin_bit_cast(bf16x8, w); 
 #ifndef VP_P1_RS_SPREAD
 #define VP_P1_RS_SPREAD 0
 #endif
+#ifndef VP_P1_SEAM
+#define VP_P1_SEAM 0
+#endif
 // one pipeline step: the QK^T chain of block QB_ (K buffer KB_; skipped when !QK) interleaved with the PV MFMAs of
 // block PB (V buffer VB_) so that no MFMA waits on the one before it, then the two row-sum MFMAs; every gap holds the
 // next exp pair of block EB's 16 scores and the pack of the pair before:
 //   g0 QK c0 | g1 PV (slab 0, d 0-31) | g2 QK c1 | g3 PV (0, 32-63) | g4 QK c2 | g5 PV (1, 0-31) | g6 QK c3 |
 //   g7 PV (1, 32-63) | row sum slab 0 | row sum slab 1
-template <int EB, int QB_, int PB, int KB_, int VB_, bool QK>
+// SEAM (the tile-seam step, VP_P1_SEAM A/B): MFMA order PV0 PV1 QK0 PV2 QK1 PV3 QK2 QK3, so the K fragments read
+// right after the seam barrier get two MFMAs of cover; the QK^T chain then ends one gap later, and an s_nop pads the
+// distance to the next step's first (asm) exp of its result
+template <int EB, int QB_, int PB, int KB_, int VB_, bool QK, bool SEAM = false>
 VP_DEV void p1_step(P1Regs& r, const bf16x8& sel) {
   float p[16];
   const f32x16 z = {};
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
-    const int c = g >> 1;
-    if ((g & 1) == 0) {
+    constexpr int seam_kind[8] = {1, 1, 0, 1, 0, 1, 0, 0};  // 0 = QK, 1 = PV
+    constexpr int seam_idx[8] = {0, 1, 0, 2, 1, 3, 2, 3};
+    const int c = SEAM ? seam_idx[g] : g >> 1;
+    if ((SEAM ? seam_kind[g] : (g & 1)) == 0) {
       if constexpr (QK) {
         p1_fence();
         r.s[QB_] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.kf[KB_][c], r.qf[QB_][c], c == 0 ? z : r.s[QB_], 0, 0, 0);
@@ -823,6 +831,7 @@ VP_DEV void p1_step(P1Regs& r, const bf16x8& sel) {
   p1_fence();
   r.lsum[PB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[PB][1]), r.lsum[PB], 0, 0, 0);
   p1_fence();
+  if constexpr (SEAM) asm volatile("s_nop 7" ::: "memory");
 }
 
 // keys past the segment end (lane key (i & 3) + 8 (i >> 2) + 4 hl of the half >= rem = lim - 32 h): score -inf.  In
@@ -900,7 +909,9 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
     // (the last tile's step (3, 1) runs its QK^T too, on stale K fragments, result unused: one code path, so the
     // accumulators keep their registers through the tile)
     constexpr int VO = SL == 2 ? 0 : -1;
-    if (h & 1)
+    if (SL == 2 && VP_P1_SEAM && h == 3)
+      p1_step<1, 0, 0, 0, VO < 0 ? 1 : 0, true, true>(r, sel);
+    else if (h & 1)
       p1_step<1, 0, 0, 0, VO < 0 ? 1 : 0, true>(r, sel);
     else
       p1_step<1, 0, 0, 1, 0, true>(r, sel);
@@ -1876,6 +1887,292 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
     store_out(d, o, l_run, q, b, h, g);
   }
 }
+
+// ---- f8p (VP_ATTN8_VARIANT=4): the fp8 kernel as a software pipeline, the p1 schedule carried over to e4m3.  4 waves
+// x 32 queries per workgroup at two workgroups per CU (256 VGPRs: two score buffers live), an 8-tile LDS ring filled
+// up to five tiles ahead with one barrier per two 64-key tiles.  Step j issues PV of tile j-1 (while tile j's max runs
+// beside it), then QK^T of tile j+1 while tile j's rescale decision and linear codes (LIN 2) are computed beside it;
+// tile j's row-sum MFMA closes the step.  A
+// rescale scales O after PV(j-1) and lsum after RS(j-1): the compiler's wait on those results is the only exposed
+// MFMA latency, on the (rare after the first tiles) rescale path.
+constexpr int F8P_SLOTS = 8;
+constexpr int F8P_STAGE = 2 * F8_TILE + 1024;  // K, V^T, the scales (128 B used)
+constexpr int F8P_LDS = F8P_SLOTS * F8P_STAGE;
+constexpr int F8P_OFF = 7;
+constexpr float F8P_THR = 1.5f;
+constexpr float F8P_LS = 8.f * 0x1p-16f;
+constexpr float F8P_C0 = (8.f * F8P_OFF + 56.f - LIN_DELTA) * 0x1p-16f;
+
+struct F8PRegs {
+  i32x8 qf;
+  f32x16 negm;
+  f32x16 o[2];
+  f32x16 s[2][2];  // [job parity][key half]
+  i32x8 pf[2];     // [job parity]
+  i32x8 kf[2];
+  i32x8 vf[2];
+  i32x8 sel;
+  f32x4 lsum;
+  float m_run, thr;
+  int vsw;
+};
+
+// P codes of one 32-key half (LIN 2, see f8_lin2_pack) into pf VGPRs 4 hh .. 4 hh + 3
+VP_DEV void f8p_pack_half(const f32x16& s, i32x8& pf, int hh) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const u16x2 lo = __builtin_amdgcn_cvt_pknorm_u16(s[4 * w + 0], s[4 * w + 1]);
+    const u16x2 hi = __builtin_amdgcn_cvt_pknorm_u16(s[4 * w + 2], s[4 * w + 3]);
+    pf[hh * 4 + w] = (int)__builtin_amdgcn_perm(__builtin_bit_cast(unsigned, hi), __builtin_bit_cast(unsigned, lo),
+                                                0x06040200u);
+  }
+}
+
+VP_DEV float f8p_max16(const f32x16& s) {
+  float a = fmaxf(fmaxf(s[0], s[1]), s[2]), c = fmaxf(fmaxf(s[3], s[4]), s[5]);
+  a = fmaxf(fmaxf(a, s[6]), s[7]);
+  c = fmaxf(fmaxf(c, s[8]), s[9]);
+  a = fmaxf(fmaxf(a, s[10]), s[11]);
+  c = fmaxf(fmaxf(c, s[12]), s[13]);
+  a = fmaxf(fmaxf(a, s[14]), s[15]);
+  return fmaxf(a, c);
+}
+
+// S^T = K Q^T + (-m) by asm: a fresh (early-clobber) destination with -m kept in its own registers; the builtin form
+// makes the compiler copy -m into the MFMA's C registers with 8 v_mov_b64 per step.  The hazard recognizer cannot
+// see into asm: the first VALU read of the result comes a full step later (after the row-sum MFMA, the seam and a PV
+// MFMA), far past the 19 wait states a 16-pass XDL result needs; the prologue pads explicitly.
+VP_DEV void f8p_qk(f32x16& s, const i32x8& kf, const i32x8& qf, const f32x16& negm, int sk, int sq) {
+  asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %3, %4, %5 op_sel_hi:[0,0,0]"
+               : "=&v"(s)
+               : "v"(kf), "v"(qf), "v"(negm), "v"(sk), "v"(sq));
+}
+
+// one pipeline step for job j (parity CUR): PV(j-1) if PV, QK(j+1) if QK, MASK: job j is the last (partial) tile
+template <int CUR, bool PV, bool QK, bool MASK, class RV>
+VP_DEV void f8p_step(F8PRegs& r, int lim, int sk, int sq, int g, RV&& read_v_own) {
+  constexpr int NXT = CUR ^ 1;  // = the parity of job j - 1 and of job j + 1
+  f32x16(&s)[2] = r.s[CUR];
+  if constexpr (MASK) {
+    if (lim < 64) {
+      mask_half(s[0], lim, 0, g);
+      mask_half(s[1], lim, 1, g);
+    }
+  }
+  p1_fence();
+  if constexpr (PV) r.o[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(r.vf[0], r.pf[NXT], r.o[0], 0, 0, 0, r.vsw, 0, 127);
+  float mx = f8p_max16(s[0]);
+  p1_fence();
+  if constexpr (PV) r.o[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(r.vf[1], r.pf[NXT], r.o[1], 0, 0, 1, r.vsw, 0, 127);
+  mx = fmaxf(mx, f8p_max16(s[1]));
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    mx = (fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) - F8P_C0) * (1.f / F8P_LS);
+  }
+  p1_fence();
+  // job j's V^T fragments for PV(j) in the next step (the PV MFMAs above were their last readers): a full step
+  // of cover for the LDS latency
+  read_v_own();
+  p1_fence();
+  // QK^T of job j + 1 with the current -m, issued before job j's rescale decision so the decision is off the matrix
+  // pipe's path; a rescale corrects that half afterwards (the second half is issued with the updated -m)
+  if constexpr (QK) f8p_qk(r.s[NXT][0], r.kf[0], r.qf, r.negm, sk, sq);
+  if (__ballot(mx > r.thr) != 0ull) {
+    // the asm QK^T above still reads -m and writes S: the wait states a VALU write / read of them needs
+    if constexpr (QK) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+    const float dm = mx > r.thr ? mx : 0.f;
+    const float alpha = __builtin_amdgcn_exp2f(-dm);
+    // lane n < 16 holds the sums of queries n and n + 16: alpha of lane n + 16 by a row swap (VALU; a ds_bpermute
+    // here would make the compiler drain the LDS queue, the V^T reads in flight, before the next MFMA)
+    const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(alpha), __float_as_uint(alpha), false, false);
+    r.lsum[0] *= alpha;
+    r.lsum[1] *= __uint_as_float(a16[1]);
+    r.m_run += dm;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      r.o[0][i] *= alpha;
+      r.o[1][i] *= alpha;
+      s[0][i] -= F8P_LS * dm;
+      s[1][i] -= F8P_LS * dm;
+      r.negm[i] -= F8P_LS * dm;
+      if constexpr (QK) r.s[NXT][0][i] -= F8P_LS * dm;
+    }
+    // opaque: known as a splat, -m is otherwise kept once and copied into the MFMA's C registers every step
+    asm volatile("" : "+v"(r.negm));
+    r.thr = F8P_THR;
+  }
+  f8p_pack_half(s[0], r.pf[CUR], 0);
+  p1_fence();
+  if constexpr (QK) f8p_qk(r.s[NXT][1], r.kf[1], r.qf, r.negm, sk, sq);
+  f8p_pack_half(s[1], r.pf[CUR], 1);
+  p1_fence();
+  r.lsum = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(r.sel, r.pf[CUR], r.lsum, 0, 0, 0, 127, 0, 127);
+  p1_fence();
+}
+
+template <int P>
+VP_DEV void f8p_drain(F8PRegs& r) {
+  r.o[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(r.vf[0], r.pf[P], r.o[0], 0, 0, 0, r.vsw, 0, 127);
+  r.o[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(r.vf[1], r.pf[P], r.o[1], 0, 0, 1, r.vsw, 0, 127);
+}
+
+__global__ __launch_bounds__(256, 2) void attn_fwd_fp8p(const vp_attn_fp8_desc dd) {
+  const vp_attn_desc& d = dd.base;
+  constexpr int QB = 4 * 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 5;
+
+  const int nqb = (d.Nq + QB - 1) / QB;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb;
+  const int qb = t - bh * nqb;
+  const int b = bh / d.H;
+  const int h = bh - b * d.H;
+  const int ntiles = dd.npad >> 6;
+
+  F8PRegs r;
+  const int q = qb * QB + wave * 32 + (lane & 31);
+  {
+    const int qc = q < d.Nq ? q : d.Nq - 1;  // rows past Nq compute on the last query; store_out skips them
+    const uint8_t* qrow = (const uint8_t*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+    u32x4* hq = (u32x4*)&r.qf;
+    hq[0] = *(const u32x4*)(qrow + g * 16);
+    hq[1] = *(const u32x4*)(qrow + (g + 2) * 16);
+  }
+  const int sq = (dd.qk_scale & 0xff) + 3 - 16, sk = (dd.qk_scale >> 8) & 0xff;
+
+  // DMA: wave w stages K rows 16w .. 16w + 15 and V^T rows 16w .. (one 16-byte chunk per lane each), wave 0 lanes
+  // 0-7 also the V^T scales: 2 (waves 1-3) / 3 (wave 0) vmcnt entries per tile
+  const int ksn = (int)d.k_sn;
+  const int prow = wave * 16 + (lane >> 2);
+  const int pch = ((lane & 3) ^ swz8(prow)) << 4;
+  const int offk = prow * ksn + pch, offv = prow * dd.npad + pch;
+  const char* kbase = (const char*)d.K + (int64_t)b * d.k_sb + h * 64;
+  const char* vtbase = (const char*)d.V + (int64_t)bh * 64 * dd.npad;
+  const char* vsbase = (const char*)dd.vs + (int64_t)bh * ntiles * 128;
+  auto slot = [&](int kt) { return smem + (kt & (F8P_SLOTS - 1)) * F8P_STAGE; };
+  // LDS-DMA destinations as 32-bit LDS addresses from one wave-uniform base (no generic-pointer conversion and
+  // null check per instruction); the scales by all of wave 0's lanes (lane l re-reads chunk l % 8 into byte 16 l
+  // of the slot's 1 KB scale area, of which the first 128 bytes are the layout) so no lane mask is needed
+  const unsigned lds_base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem);
+  const int full_k = d.Nk >> 6;
+  const int offs = (lane & 7) * 16;
+  auto issue = [&](int kt) {
+    const unsigned st = lds_base + (unsigned)((kt & (F8P_SLOTS - 1)) * F8P_STAGE);
+    if (kt < full_k) {
+      glds16_lds(kbase + (int64_t)kt * 64 * ksn, offk, st + wave * 1024);
+    } else {  // rows past the end re-read the last key (masked later)
+      const int ln = lane_id_opaque();
+      const int pr = wave * 16 + (ln >> 2);
+      const int rr = min(kt * 64 + pr, d.Nk - 1);
+      glds16_lds(kbase, rr * ksn + (((ln & 3) ^ swz8(pr)) << 4), st + wave * 1024);
+    }
+    glds16_lds(vtbase + kt * 64, offv, st + F8_TILE + wave * 1024);
+    if (wave == 0) glds16_lds(vsbase + kt * 128, offs, st + 2 * F8_TILE);
+  };
+  const int r0 = lane & 31;
+  const int ca = (g ^ swz8(r0)) << 4, cb = ((g + 2) ^ swz8(r0)) << 4;
+  auto read_k = [&](int kt) {
+    const char* st = slot(kt);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const char* kr = st + (hh * 32 + r0) * 64;
+      u32x4* hk = (u32x4*)&r.kf[hh];
+      hk[0] = *(const u32x4*)(kr + ca);
+      hk[1] = *(const u32x4*)(kr + cb);
+    }
+  };
+  // the scale word first: the compiler zero-extends it at the next join, and LDS reads complete in order, so its
+  // wait there leaves the four V^T reads behind it in flight
+  auto read_v = [&](int kt) {
+    const char* st = slot(kt);
+    r.vsw = *(const unsigned short*)(st + 2 * F8_TILE + lane * 2);
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const char* vr = st + F8_TILE + (dh * 32 + r0) * 64;
+      u32x4* hv = (u32x4*)&r.vf[dh];
+      hv[0] = *(const u32x4*)(vr + ca);
+      hv[1] = *(const u32x4*)(vr + cb);
+    }
+  };
+  // one barrier per two tiles: before steps j, j + 1 (j odd) tiles j + 1 and j + 2 have landed (issued at least two
+  // steps earlier; tiles j + 3, j + 4 may still be in flight), all waves are past steps j - 2, j - 1, so the slots of
+  // tiles j - 3, j - 2 are free for tiles j + 5, j + 6
+  auto seam2 = [&](int j) {
+    if (j + 4 < ntiles) {
+      if (wave == 0)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (j + 5 < ntiles) issue(j + 5);
+    if (j + 6 < ntiles) issue(j + 6);
+  };
+
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    r.o[0][i] = 0.f;
+    r.o[1][i] = 0.f;
+    r.negm[i] = F8P_C0;
+  }
+  asm volatile("" : "+v"(r.negm));
+  r.lsum = (f32x4){0.f, 0.f, 0.f, 0.f};
+  r.m_run = 0.f;
+  r.thr = -INFINITY;
+  {
+    const int col = lane & 15, c = lane >> 4;
+    const int w = ((col == 0 && (c & 1) == 0) || (col == 1 && (c & 1) == 1)) ? 0x38383838 : 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.sel[i] = w;
+  }
+
+  for (int kt = 0; kt < 6; ++kt)
+    if (kt < ntiles) issue(kt);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  read_k(0);
+  f8p_qk(r.s[0][0], r.kf[0], r.qf, r.negm, sk, sq);
+  f8p_qk(r.s[0][1], r.kf[1], r.qf, r.negm, sk, sq);
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  const int last = ntiles - 1;
+  const int lim_last = d.Nk - last * 64;
+  auto rv = [&](int kt) { return [&read_v, kt]() { read_v(kt); }; };
+  if (ntiles == 1) {
+    f8p_step<0, false, false, true>(r, lim_last, sk, sq, g, rv(0));
+    f8p_drain<0>(r);
+  } else {
+    read_k(1);  // tiles 0 .. 5 landed in the prologue
+    f8p_step<0, false, true, false>(r, 64, sk, sq, g, rv(0));
+    int j = 1;
+    for (; j + 2 < ntiles; j += 2) {
+      seam2(j);
+      read_k(j + 1);
+      f8p_step<1, true, true, false>(r, 64, sk, sq, g, rv(j));
+      read_k(j + 2);
+      f8p_step<0, true, true, false>(r, 64, sk, sq, g, rv(j + 1));
+    }
+    if (j == ntiles - 2) {
+      seam2(j);
+      read_k(j + 1);
+      f8p_step<1, true, true, false>(r, 64, sk, sq, g, rv(j));
+      f8p_step<0, true, false, true>(r, lim_last, sk, sq, g, rv(j + 1));
+      f8p_drain<0>(r);
+    } else {
+      f8p_step<1, true, false, true>(r, lim_last, sk, sq, g, rv(j));
+      f8p_drain<1>(r);
+    }
+  }
+  const int qq = lane & 31;
+  const float v0 = __shfl(r.lsum[0], qq & 15, 64), v1 = __shfl(r.lsum[1], qq & 15, 64);
+  store_out(d, r.o, qq < 16 ? v0 : v1, q, b, h, g, false);
+}
 }  // namespace
 
 namespace {
@@ -2080,7 +2377,9 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
   // 2.04-2.11 PF/s for 2, interleaved at config 5's length, profiles/r03_fp8_lin2_ab.log);
   // both with the row sums on the matrix pipe, 128 keys per barrier at 4 waves/SIMD.  Dropped after A/B: row sums on
   // the VALU (1.40 against 1.50 PF/s), lazy max (159 VGPRs, spills: 0.21 PF/s), 3 waves/SIMD (1.01), 64 keys per
-  // barrier (1.43 against 1.46).
+  // barrier (1.43 against 1.46); 4 = f8p, the lin2 codes in a p1-style software pipeline at 2 waves/SIMD: parity
+  // identical to 3, but 0.93-0.94x its speed (profiles/r03_f8p_ab_rejected.log: at two waves per SIMD the wave's own
+  // instruction issue, ~13 VALU + ~6 SALU per MFMA, not the matrix pipe, sets the step), kept for A/B.
   static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, 2, true, 0>,
                                     (const void*)attn_fwd_fp8<NW, 4, 2, true, 1>,
                                     (const void*)attn_fwd_fp8<NW, 4, 2, true, 2>};
@@ -2089,10 +2388,22 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
     attr_set = true;
     for (int i = 0; i < 3; ++i)
       (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * F8_STAGE);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_fp8p, hipFuncAttributeMaxDynamicSharedMemorySize, F8P_LDS);
   }
   const char* e = getenv("VP_ATTN8_VARIANT");
   int variant = e != nullptr ? atoi(e) : 0;
-  if (variant < 1 || variant > 3) variant = 3;
+  if (variant < 1 || variant > 4) variant = 3;
+  if (variant == 4) {
+    const int nqb4 = (d.Nq + 127) / 128;
+    const int64_t grid4 = (int64_t)d.B * d.H * nqb4;
+    if (grid4 > 0x7fffffff) return VP_ERR_ARG;
+    void* args4[] = {(void*)dd};
+    const hipError_t le4 = hipLaunchKernel((const void*)attn_fwd_fp8p, dim3((unsigned)grid4), dim3(256), args4,
+                                           F8P_LDS, (hipStream_t)stream);
+    if (le4 != hipSuccess) return (int)le4;
+    VP_CHECK_LAUNCH();
+    return VP_OK;
+  }
   const int nqb = (d.Nq + NW * 32 - 1) / (NW * 32);
   const int64_t grid = (int64_t)d.B * d.H * nqb;
   if (grid > 0x7fffffff) return VP_ERR_ARG;
