@@ -783,6 +783,9 @@ VP_DEV bf16x8 as_bf16x8(const u32x4& w) { return __builtin_bit_cast(bf16x8, w); 
 #ifndef VP_P1_SEAM
 #define VP_P1_SEAM 0
 #endif
+#ifndef VP_F8_GENERIC_DMA
+#define VP_F8_GENERIC_DMA 0
+#endif
 // one pipeline step: the QK^T chain of block QB_ (K buffer KB_; skipped when !QK) interleaved with the PV MFMAs of
 // block PB (V buffer VB_) so that no MFMA waits on the one before it, then the two row-sum MFMAs; every gap holds the
 // next exp pair of block EB's 16 scores and the pack of the pair before:
@@ -1726,25 +1729,32 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
   const char* vsbase = (const char*)dd.vs + (int64_t)bh * ntiles * 128;
   // ring slot ti holds SUB consecutive 64-key tiles (one barrier per SUB tiles)
   const int nsup = (ntiles + SUB - 1) / SUB;
+  // LDS destinations as 32-bit LDS addresses from one wave-uniform base (no generic-pointer conversion and null
+  // check per DMA instruction)
+  const unsigned lds_smem = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem);
+  const unsigned lds_base = lds_smem + (wave < 4 ? wave * 1024 : F8_TILE + (wave - 4) * 1024);
+#if VP_F8_GENERIC_DMA  // A/B: the generic-pointer destination (conversion + null check per instruction)
+  auto glds16_lds = [&](const char* sbase, int voff, unsigned la) { glds16(sbase, voff, smem + (la - lds_smem)); };
+#endif
   auto issue = [&](int ti) {
 #pragma unroll
     for (int sb = 0; sb < SUB; ++sb) {
       const int kt = ti * SUB + sb;
       if (SUB > 1 && kt >= ntiles) break;  // wave-uniform
-      char* slot = smem + ((ti & 1) * SUB + sb) * F8_STAGE;
+      const unsigned st = lds_base + ((ti & 1) * SUB + sb) * F8_STAGE;
       if (wave < 4) {
         if (kt * 64 + 64 <= d.Nk) {
-          glds16(kbase + (int64_t)kt * 64 * ksn, LIN ? dma_off(lane_id_opaque()) : dma_kept, slot + wave * 1024);
+          glds16_lds(kbase + (int64_t)kt * 64 * ksn, LIN ? dma_off(lane_id_opaque()) : dma_kept, st);
         } else {  // rows past the end re-read the last key (masked later)
           const int ln = lane_id_opaque();
           const int prow = (wave & 3) * 16 + (ln >> 2);
           const int r = min(kt * 64 + prow, d.Nk - 1);
-          glds16(kbase, r * ksn + (((ln & 3) ^ swz8(prow)) << 4), slot + wave * 1024);
+          glds16_lds(kbase, r * ksn + (((ln & 3) ^ swz8(prow)) << 4), st);
         }
       } else {
-        glds16(vtbase + kt * 64, LIN ? dma_off(lane_id_opaque()) : dma_kept, slot + F8_TILE + (wave - 4) * 1024);
+        glds16_lds(vtbase + kt * 64, LIN ? dma_off(lane_id_opaque()) : dma_kept, st);
       }
-      if (wave == 0 && lane < 8) glds16(vsbase + kt * 128, lane * 16, slot + 2 * F8_TILE);
+      if (wave == 0 && lane < 8) glds16_lds(vsbase + kt * 128, lane * 16, st + 2 * F8_TILE);  // wave 0: st = slot + 0
     }
   };
 
