@@ -89,6 +89,27 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def physical_cores() -> int:
+    """Physical cores in this process's affinity mask (SMT siblings counted once): the thread count the CPU
+    baseline runs at (the reference CPU path on the node's own host cores).  VP_CPU_BASELINE_THREADS
+    overrides."""
+    env = int(os.environ.get("VP_CPU_BASELINE_THREADS", "0") or 0)
+    if env > 0:
+        return env
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    seen = set()
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id") as f:
+                pkg = f.read().strip()
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id") as f:
+                core = f.read().strip()
+            seen.add((pkg, core))
+        except OSError:
+            seen.add(("cpu", c))
+    return max(1, len(seen))
+
+
 def _oracle_block_weights(g, dtype):
     from videopainter_amd.config import block_shapes
     sd = {}
@@ -115,7 +136,8 @@ def cpu_baseline() -> dict:
     step is the 44 blocks).  `--cpu-baseline-only --cpu-full-step` times a whole step instead
     (profiles/r02_cpu_full_step.json)."""
     from oracle import cogvideox_oracle as O
-    threads = torch.get_num_threads()
+    threads = physical_cores()
+    torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     rope = O.prepare_rotary_positional_embeddings(480, 720, F, 64)
     out = {}
@@ -137,11 +159,13 @@ def cpu_baseline() -> dict:
     step_s = {k: v * step_flops() / block_flop() for k, v in out.items()}
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
     return {"value": 1.0 / step_s["bf16"], "unit": "steps/s", "cores": threads, "kind": "port",
+            "threads": torch.get_num_threads(), "physical_cores_in_affinity": physical_cores(),
             "affinity_cpus": aff, "host_cpus": os.cpu_count(),
             "value_fp32": 1.0 / step_s["fp32"], "cpu_model": _cpu_model(),
             "sample": f"oracle (plain PyTorch CPU restatement) after a warm-up block: 1 full-size CogVideoXBlock "
                       f"forward at B=2, N={NTOK} took {out['bf16']:.1f} s in bf16 and {out['fp32']:.1f} s in fp32 on "
-                      f"{threads} threads (process affinity mask: {aff} of the host's {os.cpu_count()} CPUs; "
+                      f"{threads} threads = the physical cores of the process affinity mask ({aff} of the host's "
+                      f"{os.cpu_count()} logical CPUs; "
                       f"{_cpu_model()}); step = step FLOP / block FLOP x block time = "
                       f"{step_s['bf16']:.0f} s bf16 / {step_s['fp32']:.0f} s fp32"}
 
@@ -149,9 +173,10 @@ def cpu_baseline() -> dict:
 def cpu_full_step(dtype=torch.bfloat16) -> dict:
     """One complete config-2 denoising step on the CPU through the oracle: branch (2 blocks) + transformer (42
     blocks) forward at B=2 with the full 5b-I2V weights (random, std 1/sqrt(fan_in)), CFG + DPM step + replace-gt;
-    timed after a warm-up block.  ~7 min in bf16 on 16 threads."""
+    timed after a warm-up block, on the physical cores of the affinity mask (~7 min in bf16 on 16 threads)."""
     from oracle import cogvideox_oracle as O
     from videopainter_amd.config import COGVIDEOX_5B_I2V, full_config, state_dict_shapes
+    torch.set_num_threads(physical_cores())
     g = torch.Generator().manual_seed(0)
     tcfg = full_config(dict(COGVIDEOX_5B_I2V))
     bcfg = full_config(dict(COGVIDEOX_5B_I2V, num_layers=LB), True)
@@ -226,15 +251,23 @@ def build_models(device, seed: int, rank: int, world: int, bcast: str = "scatter
         br.init_synthetic_weights_(seed + 1)
     t_b = None
     if world > 1:
-        from videopainter_amd.distributed import barrier, broadcast_module
-        torch.cuda.synchronize()
-        barrier(device)
-        t0 = time.perf_counter()
-        for m in (tr, br):
-            broadcast_module(m, src=0, method=bcast)
-        torch.cuda.synchronize()
-        barrier(device)
-        t_b = time.perf_counter() - t0
+        # replicate with the chosen method (timed), check every rank's bytes against rank 0's (per-bucket digests:
+        # the first hardware run of the RCCL-only code paths validates itself), then time the other method too
+        from videopainter_amd.distributed import barrier, broadcast_module, verify_replicas
+        t_b = {}
+        for method in (bcast, "broadcast" if bcast == "scatter_allgather" else "scatter_allgather"):
+            torch.cuda.synchronize()
+            barrier(device)
+            t0 = time.perf_counter()
+            for m in (tr, br):
+                broadcast_module(m, src=0, method=method)
+            torch.cuda.synchronize()
+            barrier(device)
+            t_b[method] = time.perf_counter() - t0
+            checks = [verify_replicas(m) for m in (tr, br)]
+            if not all(ok for ok, _ in checks):
+                raise RuntimeError(f"weight replication ({method}) left ranks with different weights")
+            t_b[method + "_verified_buckets"] = sum(n for _, n in checks)
     torch.cuda.synchronize()
     return tr, br, t_b
 
@@ -560,7 +593,7 @@ def main():
             del ref16, out8, lmi
         log(f"[bench] config 5: fp8 QKV+attention+FFN noise_pred vs bf16 rel-L2 {fp8_drift:.3e}")
     log(f"[bench] setup {time.time() - t_setup:.1f}s; rank {rank}/{world}"
-        + (f"; weight broadcast ({args.bcast}) {t_bcast:.2f}s" if t_bcast is not None else ""))
+        + (f"; weight replication {t_bcast}" if t_bcast is not None else ""))
 
     def one(i):
         k = i % len(timesteps)

@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 11
+#define VP_ABI_VERSION 12
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
@@ -174,9 +174,12 @@ typedef struct vp_attn_desc {
   float scale, out_scale;
   int32_t accumulate;
   int32_t flags; /* VP_ATTN_BOUNDED_SCORES: the caller guarantees |scale * q.k| * log2(e) <= VP_ATTN_SCORE_BOUND for
-                    every (query, key) pair, so the kernel runs without a running max (exact: bf16/fp32 hold
+                    every (query, key) pair, so the kernel runs without a reference point (p2: exact, bf16/fp32 hold
                     2^+-60 and O / l is invariant to the reference point).  CogVideoX's qk-LayerNorm gives the bound
-                    from the norm weights: videopainter_amd.kernels.score_bound_log2. */
+                    from the norm weights: videopainter_amd.kernels.score_bound_log2.  Without the flag (any
+                    scores): p2a, the same pipeline with an anchored reference point, plus a re-run of the blocks it
+                    flags by the exact anchored 16x16x32 kernel — which needs the workspace of
+                    vp_attention_fwd_bf16_ws (without one the 16x16x32 kernel runs alone). */
   float* lse;     /* optional fp32 [B, H, Nq]: per query log2-sum-exp2 of the scaled log2-unit scores (m + log2 l), the
                      softmax statistics vp_attention_bwd_bf16 recomputes P from (bf16 kernel only; NULL: not written) */
   const int32_t* k2_full; /* optional int32 [B] (device), a hint: segment-2 rows n >= k2_full[b] of V2 are zero
@@ -190,7 +193,8 @@ typedef struct vp_attn_desc {
   const float* l_extra;   /* optional fp32 [B, H, Nq] (device): log2 of extra row-sum mass per query, in the kernel's
                              score units (scale * log2 e * q.k), added to the softmax denominator — the null keys'
                              total exp2(score) (their values are zero).  -inf: none.  NULL: nothing added.
-                             k2_full / k2_len / l_extra are implemented by the 16x16x32 kernels (launched for them). */
+                             k2_len / l_extra are taken by the s16 / a16 and the p2 / p2a kernels, k2_full by the
+                             16x16x32 kernels only (a k2_full launch runs s16 / a16). */
 } vp_attn_desc;
 #define VP_ATTN_BOUNDED_SCORES 1
 #define VP_ATTN_SCORE_BOUND 60.0f
@@ -203,6 +207,12 @@ int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream);
  * -1: invalid descriptor).  A null or too small workspace runs the unsplit grid. */
 int64_t vp_attention_workspace_bytes(const vp_attn_desc* d);
 int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* 1 when the attention kernel variant `name` (the values of the A/B environment switches VP_ATTN_BOUNDED_MODE /
+ * VP_ATTN_UNBOUNDED_MODE: "p2", "p2a", "s16", "a16", and with a VP_ATTN_EXTRA_VARIANTS build "lazy", "w32", "w64",
+ * "w64f", "s16i", "p1"; "fp8:N" for the fp8 kernel's VP_ATTN8_VARIANT = N: 2 and 3, and 1 and 4 with that build) is
+ * in this library, else 0.  Host-only.  A launch that names a variant outside the build returns VP_ERR_UNSUPPORTED. */
+int vp_attention_variant_built(const char* name);
 
 /* fp8 attention (BASELINE config 5 "attn + FFN in fp8"; same math as vp_attention_fwd_bf16, single K/V segment).
  * base.Q / base.K: e4m3 [B, N, H*64] written by vp_head_norm_rope_fp8 (strides in bytes, multiples of 16), each

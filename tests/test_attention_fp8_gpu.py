@@ -142,7 +142,10 @@ def _ref_fp64(q8, k8, vt, vs, npad, Nk, H, q_exp, k_exp):
 def attn8_variant(request, monkeypatch):
     """VP_ATTN8_VARIANT: 1 = P by v_exp_f32 + RNE e4m3 pack, 2 = P by linear mantissa interpolation, 3 = the same
     codes packed by v_cvt_pknorm_u16_f32 + a byte gather (default), 4 = the lin2 codes in the software-pipelined
-    kernel (f8p)."""
+    kernel (f8p).  1 and 4 are rejected A/B forms, built only with VP_ATTN_EXTRA_VARIANTS=1."""
+    from videopainter_amd import kernels as K
+    if not K.attention_variant_built("fp8:" + request.param):
+        pytest.skip(f"fp8 attention variant {request.param} is not in this build (VP_ATTN_EXTRA_VARIANTS)")
     monkeypatch.setenv("VP_ATTN8_VARIANT", request.param)
     return request.param
 

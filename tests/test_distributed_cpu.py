@@ -59,6 +59,48 @@ def test_broadcast_and_max_over_ranks_gloo(world, method):
     assert all(r[2] == float(world) for r in res)
 
 
+def _digest_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from videopainter_amd.distributed import init, broadcast_module, verify_replicas
+    from videopainter_amd import CogVideoXTransformer3DModel
+    from tests.golden.cases import TINY_CFG
+    init("gloo")
+    torch.manual_seed(200 + rank)
+    m = CogVideoXTransformer3DModel(**TINY_CFG)
+    with torch.no_grad():
+        for p in m.state_dict().values():
+            p.copy_(torch.randn(p.shape))
+    before = verify_replicas(m, bucket_bytes=1 << 16)
+    broadcast_module(m, src=0, bucket_bytes=1 << 16)
+    after = verify_replicas(m, bucket_bytes=1 << 16)
+    with torch.no_grad():  # one flipped bit of one weight on the last rank
+        if rank == world - 1:
+            w = m.transformer_blocks[1].attn1.to_k.weight
+            w.view(torch.int16)[3, 5] ^= 1
+    corrupted = verify_replicas(m, bucket_bytes=1 << 16)
+    q.put((rank, before, after, corrupted))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_replica_digests_detect_divergence_gloo():
+    """bench.py's self-check of the weight replication (distributed.verify_replicas, per-bucket digests compared by
+    a MIN and a MAX all-reduce): different weights before the broadcast are caught, identical weights after it
+    pass, and a single flipped bit on one rank afterwards is caught on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_digest_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for _, before, after, corrupted in res:
+        assert before[0] is False and after[0] is True and corrupted[0] is False
+        assert after[1] > 1  # several buckets (the multi-bucket path)
+
+
 def _bench_worker(rank, world, port, mode, q):
     """bench.py's rank logic (clip assignment, warm-up + barrier-bracketed timed steps, max over ranks, whole-job
     value) with the toy window step instead of the HIP model (GPU-free)."""

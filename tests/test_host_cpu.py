@@ -103,3 +103,22 @@ def test_scheduler_host_scalars_match_oracle():
 def test_dynamic_cfg_matches_reference_formula():
     g = O.dynamic_cfg_scale(6.0, 50, 999)
     assert math.isclose(g, 1 + 6.0 * ((1 - math.cos(math.pi * ((50 - 999) / 50) ** 5.0)) / 2))
+
+
+def test_fuse_qkv_projections_is_a_documented_no_op():
+    """cogvideox_transformer_3d.py:432-470: the drop-in's Q, K, V always run as one GEMM, so fuse / unfuse keep the
+    weights and state-dict keys and restore the processors like the reference."""
+    import torch
+    from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel
+    from tests.golden.cases import TINY_CFG, TINY_BRANCH_CFG
+    for cls, cfg in ((CogVideoXTransformer3DModel, TINY_CFG), (CogvideoXBranchModel, TINY_BRANCH_CFG)):
+        m = cls(**cfg)
+        m.init_synthetic_weights_(3, host_exact=True)
+        before = {k: v.clone() for k, v in m.state_dict().items()}
+        procs = m.attn_processors
+        m.fuse_qkv_projections()
+        assert m.original_attn_processors == procs
+        after = m.state_dict()
+        assert list(after) == list(before) and all(torch.equal(after[k], before[k]) for k in before)
+        m.unfuse_qkv_projections()
+        assert m.attn_processors == procs

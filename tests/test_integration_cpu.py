@@ -55,3 +55,20 @@ def test_install_is_reversible_without_the_reference():
     finally:
         integration.uninstall()
     assert modules.ModelMixin.__bases__ == (nn.Module,) and t5.T5EncoderModel.__bases__ == (nn.Module,)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="the reference is not present on this machine")
+def test_reference_pipeline_call_runs_on_the_drop_ins():
+    """The reference CogVideoXI2VDualInpaintAnyLPipeline.__call__ (the infer/inpaint.py call: 2 windows, ID-resample +
+    prev-clip, CFG, mask_add, replace_gt) on the drop-ins (tests/pipeline_call_check.py): the recorded contract is
+    current, every attribute the pipeline reads resolves on the drop-ins with the reference's value, every call it
+    makes binds to the drop-in signatures, and the loop run on the drop-in transformer / branch objects (oracle
+    compute behind their signatures) gives the reference pipeline's frames."""
+    r = subprocess.run([sys.executable, os.path.join(HERE, "pipeline_call_check.py"), "check"], capture_output=True,
+                       text=True, timeout=840, cwd=os.path.dirname(HERE))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["recorded_calls"] == res["calls_bound"] >= 14
+    assert res["attrs_resolved"] == res["recorded_attrs"] > 0
+    assert res["frames_max_abs_diff"] < 1e-3

@@ -23,29 +23,37 @@ def gemm_variant(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["lazy", "bounded", "w32", "w64", "w64f", "a16", "s16i", "p1", "p2"], ids=lambda v: f"attn_{v}")
-def attn_variant(request, monkeypatch):
-    """Unbounded-score launches: a16 (the anchored-softmax 16x16x32 kernel, the library default), lazy (the
-    running-max kernel; VP_ATTN_UNBOUNDED_MODE).  Bounded-score launches
-    (include/vp_hip.h VP_ATTN_BOUNDED_SCORES, the host proved the bound): bounded = the library default (s16, 64
-    queries per wave on the 16x16x32 MFMA), w32 / w64 / w64f / s16i / p1 / p2 the 8-wave, two-blocks-per-wave
-    32x32x16 (w64f: scalar-base DMA), per-query-tile-PV and software-pipelined (one / two workgroups per CU) forms
-    (VP_ATTN_BOUNDED_MODE)."""
-    monkeypatch.delenv("VP_ATTN_UNBOUNDED_MODE", raising=False)
-    monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
-    if request.param in ("lazy", "a16"):
-        monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", request.param)
-    elif request.param in ("w32", "w64", "w64f", "s16i", "p1", "p2"):
-        monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", request.param)
-    else:
+UNBOUNDED_VARIANTS = ("p2a", "a16", "lazy")
+
+
+def need_variant(name, monkeypatch=None):
+    """Skip unless the attention variant is in this library build (the rejected A/B variants need
+    VP_ATTN_EXTRA_VARIANTS=1); with monkeypatch, select it through its environment switch."""
+    from videopainter_amd import kernels as K
+    if not K.attention_variant_built(name):
+        pytest.skip(f"attention variant {name} is not in this build (VP_ATTN_EXTRA_VARIANTS)")
+    if monkeypatch is not None:
+        monkeypatch.delenv("VP_ATTN_UNBOUNDED_MODE", raising=False)
         monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
+        monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE" if name in UNBOUNDED_VARIANTS else "VP_ATTN_BOUNDED_MODE", name)
+
+
+@pytest.fixture(params=["p2a", "a16", "p2", "s16", "lazy", "w32", "w64", "w64f", "s16i", "p1"],
+                ids=lambda v: f"attn_{v}")
+def attn_variant(request, monkeypatch):
+    """Unbounded-score launches (no VP_ATTN_BOUNDED_SCORES): p2a (the library default: the p2 pipeline with an
+    anchored reference point and the a16 re-run of flagged blocks), a16 (the anchored-softmax 16x16x32 kernel), lazy
+    (the running-max kernel).  Bounded-score launches (include/vp_hip.h VP_ATTN_BOUNDED_SCORES, the host proved the
+    bound): p2 (the library default), s16, and the A/B variants of a VP_ATTN_EXTRA_VARIANTS build (w32 / w64 / w64f /
+    s16i / p1)."""
+    need_variant(request.param, monkeypatch)
     return request.param
 
 
 def attn_kw(variant, q, k, scale=0.125, k2=None):
     """bounded_scores for the variant, after checking on the host that the inputs satisfy the bound (the contract
     the processors establish from the qk-norm weights)."""
-    if variant in ("lazy", "a16"):
+    if variant in UNBOUNDED_VARIANTS:
         return {}
     kk = k if k2 is None else torch.cat([k, k2], 1)
     B, Nq, D = q.shape
@@ -235,13 +243,13 @@ def _ref64(q, k, v, H, scale=0.125):
     return (torch.softmax(s, -1) @ hd(v)).transpose(1, 2).reshape(B, Nq, H * 64)
 
 
-@pytest.mark.parametrize("mode", ["a16", "lazy"])
+@pytest.mark.parametrize("mode", ["p2a", "a16", "lazy"])
 @pytest.mark.parametrize("gamma", [1.0, 6.0])
 def test_attention_large_gamma_scores(gamma, mode, monkeypatch):
     """qk-LayerNorm outputs with |gamma| up to 6 (scores over hundreds of log2 units, far outside the bounded-score
     contract): the anchored kernel (no running max) against fp64 attention, at a config-2-like length for 2 heads."""
     from videopainter_amd import kernels as K
-    monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", mode)
+    need_variant(mode, monkeypatch)
     B, H, Nn = 1, 2, 4500
     g = torch.Generator().manual_seed(int(gamma * 10))
     gam = torch.rand(H * 64, generator=g) * gamma  # per-channel gains in [0, gamma]
@@ -258,13 +266,15 @@ def test_attention_large_gamma_scores(gamma, mode, monkeypatch):
     assert torch.isfinite(out.float()).all() and r < 1e-2
 
 
+@pytest.mark.parametrize("mode", ["p2a", "a16"])
 @pytest.mark.parametrize("jump", [40.0, 90.0, 200.0])
-def test_attention_anchored_late_jump(jump, monkeypatch):
-    """The anchored kernel's guarded paths: a late key whose score exceeds every earlier one by `jump` log2 units for
-    half the queries — 40: within the first reference's range; 90: row sums pass 2^64 (the 2^-64 rescale branch);
-    200: exp2 overflows inside a tile (the exact two-pass re-run of the workgroup).  Against fp64 attention."""
+def test_attention_anchored_late_jump(jump, mode, monkeypatch):
+    """The anchored kernels' guarded paths: a late key whose score exceeds every earlier one by `jump` log2 units for
+    half the queries — 40: within the first reference's range; 90: row sums pass 2^64 (a16) / 2^62 (p2a): the
+    rescale branch; 200: exp2 overflows inside a tile (a16: the exact two-pass re-run of the workgroup; p2a: the block
+    is flagged and re-run by a16).  Against fp64 attention."""
     from videopainter_amd import kernels as K
-    monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", "a16")
+    need_variant(mode, monkeypatch)
     B, H, Nn = 1, 1, 1500
     g = torch.Generator().manual_seed(int(jump))
     q = torch.randn(B, Nn, 64, generator=g) * 0.3
@@ -283,14 +293,14 @@ def test_attention_anchored_late_jump(jump, monkeypatch):
     assert torch.isfinite(out.float()).all() and r < 1e-2
 
 
-@pytest.mark.parametrize("mode", ["lazy", "a16"])
+@pytest.mark.parametrize("mode", ["p2a", "lazy", "a16"])
 def test_attention_stepwise_max_growth(mode, monkeypatch):
     """Running max grows by 0 / 0.5 / 3 / 8 nats at tile seams, so the deferred-max test (tile sum > 2^8) takes both
     branches many times within one query block (cdna_hip_programming.md §5.4 rule 26); for the anchored kernel the
     row sums pass 2^64 repeatedly (its rescale branch).  (Scores up to ~300 in log2 units: outside the bounded-score
     contract.)"""
     from videopainter_amd import kernels as K
-    monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", mode)
+    need_variant(mode, monkeypatch)
     B, H, Nn = 1, 2, 1100
     g = torch.Generator().manual_seed(80)
     u = torch.randn(64, generator=g)
@@ -522,13 +532,13 @@ def test_attention_tail_split_matches_unsplit(Nq, Nk2, monkeypatch):
         assert rel(out_s, ref) < 1e-2 and rel(out_u, ref) < 1e-2
 
 
-@pytest.mark.parametrize("mode", ["w64", "w64f", "s16", "p1", "p2"])
+@pytest.mark.parametrize("mode", ["p2", "s16", "w64", "w64f", "p1"])
 @pytest.mark.parametrize("Nq,Nk2", [(1500, 700), (17776, 0)])
 def test_attention_bounded_tail_split_matches_unsplit(Nq, Nk2, mode, monkeypatch):
     """The bounded-score kernels' grid-tail split instances (partials + merge) against their unsplit launch and, at
     small size, against fp32 attention."""
     from videopainter_amd import kernels as K
-    monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", mode)
+    need_variant(mode, monkeypatch)
     B, H = 2, 2 if Nq < 17776 else 48
     D = H * 64
     q, k, v = (bf(rnd(B, Nq, D, seed=s) * 0.5).to(dev) for s in (80, 81, 82))
@@ -629,17 +639,13 @@ def test_partition_rows_index_and_permuted_writes(B, N):
         assert not vgot[b, int(cnt[b]):].any()  # the null keys' values are zero (the k2_full contract)
 
 
-@pytest.mark.parametrize("mode", ["s16", "a16", "w64", "p2"])
+@pytest.mark.parametrize("mode", ["s16", "a16", "p2a", "p2", "w64"])
 def test_attention_k2_full_hint(mode, monkeypatch):
     """The k2_full hint (segment-2 keys past k2_full[b] have zero values: row sums only) gives the attention of the
     same segments without the hint; per-batch split points, one straddling a tile, one past every tile."""
     from videopainter_amd import kernels as K
-    if mode == "a16":
-        monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", "a16")
-        kw = {}
-    else:
-        monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", mode)
-        kw = dict(bounded_scores=True)
+    need_variant(mode, monkeypatch)
+    kw = {} if mode in UNBOUNDED_VARIANTS else dict(bounded_scores=True)
     B, H, Nn, N2 = 3, 2, 700, 900
     D = H * 64
     q, k, v = (bf(rnd(B, Nn, D, seed=s) * 0.5).to(dev) for s in (90, 91, 92))
@@ -740,19 +746,16 @@ def test_null_key_mass_matches_explicit_null_keys():
 
 
 @pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
-@pytest.mark.parametrize("mode", ["s16", "a16", "p2", "p1"])
+@pytest.mark.parametrize("mode", ["s16", "a16", "p2a", "p2", "p1"])
 def test_attention_k2_len_and_l_extra(mode, split, monkeypatch):
     """k2_len (only the first k2_len[b] keys of segment 2) and l_extra (extra row-sum mass per query, log2 score
     units) against fp64 attention over the truncated segments with 2^l_extra added to each denominator.  At this size
     every block is in the grid tail: the split launch (with empty key ranges where k2_len = 0 leaves fewer tiles than
-    splits) and the combine kernel carry l_extra; a16 also gets masses far above its anchor (the exact re-run)."""
+    splits) and the combine kernel carry l_extra; a16 / p2a also get masses far above their anchors (a16: the exact
+    re-run; p2a: a non-finite row sum, so the block is flagged and re-run by a16)."""
     from videopainter_amd import kernels as K
-    if mode == "a16":
-        monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE", "a16")
-        kw = {}
-    else:
-        monkeypatch.setenv("VP_ATTN_BOUNDED_MODE", mode)
-        kw = dict(bounded_scores=True)
+    need_variant(mode, monkeypatch)
+    kw = {} if mode in UNBOUNDED_VARIANTS else dict(bounded_scores=True)
     if not split:
         monkeypatch.setenv("VP_ATTN_NO_SPLIT", "1")
     B, H, Nn, N2 = 3, 2, 700, 900
@@ -762,7 +765,7 @@ def test_attention_k2_len_and_l_extra(mode, split, monkeypatch):
     klen = torch.tensor([300, 0, 900], dtype=torch.int32)
     lx = rnd(B, H, Nn, seed=100) * 4.0 + 3.0
     lx[:, :, ::7] = float("-inf")
-    if mode == "a16":
+    if mode in UNBOUNDED_VARIANTS:
         lx[0, 0, 5::50] = 150.0
         lx[1, 1, 9::60] = 90.0
     o = torch.empty(B, Nn, D, device=dev, dtype=torch.bfloat16)

@@ -102,11 +102,13 @@ def main():
         variants = ()
     for rnd in range(2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
         for var in variants:
-            if var in ("w32", "w64", "s16", "a16", "s16i", "p1"):  # bounded-kernel forms (A/B)
-                os.environ["VP_ATTN_BOUNDED_MODE"] = var
-            else:
-                os.environ.pop("VP_ATTN_BOUNDED_MODE", None)
-            t = timeit(lambda: K.attention(q, k, v, o, H, bounded_scores=var != "lazy"), max(2, args.iters // 2))
+            # unbounded-score kernels (p2a = the default without a proven bound, a16, lazy) vs bounded ones
+            unb = var in ("lazy", "a16", "p2a")
+            os.environ.pop("VP_ATTN_BOUNDED_MODE", None)
+            os.environ.pop("VP_ATTN_UNBOUNDED_MODE", None)
+            if var != "bounded":
+                os.environ["VP_ATTN_UNBOUNDED_MODE" if unb else "VP_ATTN_BOUNDED_MODE"] = var
+            t = timeit(lambda: K.attention(q, k, v, o, H, bounded_scores=not unb), max(2, args.iters // 2))
             res[f"attention_{var}_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
             print("attention", var, res[f"attention_{var}_r{rnd}"], flush=True)
     if args.only == "attention":  # bf16 attention only (rocprofv3 --pmc passes filter on the kernel name)

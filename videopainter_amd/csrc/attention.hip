@@ -28,9 +28,14 @@
 //          (Measured at config 2: 1.15 PF/s against 1.13 for LAZY; the same no-max kernel with the sums on the VALU
 //          needs a second score tile live and spills at 128 VGPRs: 0.97.)
 #include <stdlib.h>
+#include <string.h>
 
 
 #include "vp_common.h"
+
+#ifndef VP_ATTN_EXTRA_VARIANTS
+#define VP_ATTN_EXTRA_VARIANTS 0
+#endif
 
 namespace {
 
@@ -50,6 +55,9 @@ enum { MODE_LAZY = 0, MODE_BOUNDED = 1 };
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 VP_DEV int swz(int row) { return (row >> 1) & 7; }
+
+// inf / NaN by the exponent bits (this file builds with -fno-honor-nans: float compares may assume no NaN)
+VP_DEV bool nonfinite(float x) { return (__float_as_uint(x) & 0x7f800000u) == 0x7f800000u; }
 
 struct Seg {
   const bf16* k;
@@ -290,7 +298,23 @@ struct AttnSplit {
   int t_base;   // first block index of this launch
   int nsplit;   // 1: normal launch; > 1: key-range split of blocks t_base + blockIdx.x / nsplit
   float* ws;    // partials: [block - t_base][split][query in block (QB)][66] = O[64], m, l
+  // anchored p2 (p2a) redo flags, one int per main-grid block then one per (tail block, split): written 0 / 1 by every
+  // p2a workgroup (1 = a non-finite or underflowing row: nothing stored), read by the combine pass (skips a flagged
+  // tail block) and by the redo launch of the anchored 16x16x32 kernel (runs only the flagged blocks); NULL: none
+  int* flags;
+  int flag_main;     // main-grid blocks (the tail's flags follow them)
+  int flag_nsplit;   // splits per tail block
+  int redo;          // a16 redo launch: a workgroup whose block is not flagged returns at once
 };
+
+// is block t flagged by its p2a workgroup(s)?
+VP_DEV bool block_flagged(const AttnSplit& sp, int t) {
+  if (t < sp.flag_main) return sp.flags[t] != 0;
+  const int* f = sp.flags + sp.flag_main + (int64_t)(t - sp.flag_main) * sp.flag_nsplit;
+  int any = 0;
+  for (int s = 0; s < sp.flag_nsplit; ++s) any |= f[s];
+  return any != 0;
+}
 
 // O^T accumulator layout of one lane (store_out): dim d = dh*32 + 8*gq + 4*hl + r  <->  o[dh][4*gq + r]
 VP_DEV void store_partial(float* rec, const f32x16 (&o)[2], float m_run, float l_tot, int hl) {
@@ -310,12 +334,18 @@ VP_DEV void store_partial(float* rec, const f32x16 (&o)[2], float m_run, float l
 // 16 threads per (tail block, query), 4 output dims each: merge the nsplit partials and store like store_out (per
 // element the same operations in the same order as one thread per query: the split count is the only loop)
 __global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d, int t_base, int ntail, int nsplit,
-                                                           int qb_size, const float* __restrict__ ws) {
+                                                           int qb_size, const float* __restrict__ ws,
+                                                           const int* __restrict__ flags) {
   const int gid = blockIdx.x * 256 + threadIdx.x;
   const int quad = gid & 15;
   const int row = gid >> 4;
   if (row >= ntail * qb_size) return;
   const int j = row / qb_size, qi = row - j * qb_size;
+  if (flags != nullptr) {  // p2a: a flagged tail block is left to the redo launch (nothing stored here)
+    int any = 0;
+    for (int s = 0; s < nsplit; ++s) any |= flags[t_base + j * nsplit + s];
+    if (any) return;
+  }
   const int t = t_base + j;
   const int nqb = (d.Nq + qb_size - 1) / qb_size;
   const int bh = t / nqb, qb = t - bh * nqb;
@@ -325,6 +355,10 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d,
   const float* rec0 = ws + ((int64_t)j * nsplit * qb_size + qi) * 66;
   float mx = -INFINITY;
   for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, rec0[(int64_t)s * qb_size * 66 + 64]);
+  // the extra mass enters the reference point too, so no weight below exceeds 1 (a mass far above every partial's
+  // reference would otherwise overflow the denominator)
+  const float lx = d.l_extra != nullptr ? d.l_extra[((int64_t)b * d.H + h) * d.Nq + q] : -INFINITY;
+  mx = fmaxf(mx, lx);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float l = 0.f;
   for (int s = 0; s < nsplit; ++s) {
@@ -337,7 +371,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d,
     acc[2] += v[2] * w;
     acc[3] += v[3] * w;
   }
-  if (d.l_extra != nullptr) l += __builtin_amdgcn_exp2f(d.l_extra[((int64_t)b * d.H + h) * d.Nq + q] - mx);
+  if (d.l_extra != nullptr) l += __builtin_amdgcn_exp2f(lx - mx);
   const float inv = 1.f / l;
   if (d.lse != nullptr && quad == 0) d.lse[((int64_t)b * d.H + h) * d.Nq + q] = mx + __log2f(l);
   bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64 + 4 * quad;
@@ -737,6 +771,8 @@ struct P1Regs {
   bf16x8 kf[2][4];  // K fragments by half parity
   bf16x8 vf[2][4];  // V^T fragments by half parity: [slab j * 2 + dim half]
   f32x4 lsum[2];
+  f32x16 negm;      // anchored (p2a): C operand of every QK^T chain = -anchor (wave-uniform), unused otherwise
+  float anc;        // the wave's anchor (log2 score units)
 };
 
 VP_DEV void p1_read_k(const char* Kl, int kh, int lane, bf16x8 (&kf)[4]) {
@@ -794,7 +830,7 @@ VP_DEV bf16x8 as_bf16x8(const u32x4& w) { return __builtin_bit_cast(bf16x8, w); 
 // SEAM (the tile-seam step, VP_P1_SEAM A/B): MFMA order PV0 PV1 QK0 PV2 QK1 PV3 QK2 QK3, so the K fragments read
 // right after the seam barrier get two MFMAs of cover; the QK^T chain then ends one gap later, and an s_nop pads the
 // distance to the next step's first (asm) exp of its result
-template <int EB, int QB_, int PB, int KB_, int VB_, bool QK, bool SEAM = false>
+template <int EB, int QB_, int PB, int KB_, int VB_, bool QK, bool SEAM = false, bool ANCH = false>
 VP_DEV void p1_step(P1Regs& r, const bf16x8& sel) {
   float p[16];
   const f32x16 z = {};
@@ -806,7 +842,15 @@ VP_DEV void p1_step(P1Regs& r, const bf16x8& sel) {
     if ((SEAM ? seam_kind[g] : (g & 1)) == 0) {
       if constexpr (QK) {
         p1_fence();
-        r.s[QB_] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.kf[KB_][c], r.qf[QB_][c], c == 0 ? z : r.s[QB_], 0, 0, 0);
+        // anchored: the chain starts from C = -anchor, so S - anchor leaves the matrix pipe (no VALU).  Its first MFMA
+        // is inline asm with an early-clobber destination (as qk_half_ci): with the builtin the compiler coalesces the
+        // rescale branch's update of s[0] with -anchor and copies the tuple (8 v_mov_b64) before the chain
+        if (ANCH && c == 0)
+          asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3"
+                       : "=&v"(r.s[QB_]) : "v"(r.kf[KB_][0]), "v"(r.qf[QB_][0]), "v"(r.negm));
+        else
+          r.s[QB_] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.kf[KB_][c], r.qf[QB_][c], c == 0 ? z : r.s[QB_], 0,
+                                                             0, 0);
         p1_fence();
       }
     } else {
@@ -869,7 +913,7 @@ VP_DEV void p1_mask(f32x16& s, int rem, int hl4) {
 // the tile into the slot this tile's predecessor used, so every read of a slot comes before the seam barrier; V^T is
 // single-buffered (read after the even step's PV, a 4-MFMA group before the odd step's), and the seam moves to the
 // end of step (3, 0), after V(3) is read
-template <int SL>
+template <int SL, bool ANCH = false>
 VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn, int lim, bool masked, bool last,
                     bool wait_all, int lane, const int (&vo)[2]) {
   const int hl = lane >> 5;
@@ -892,9 +936,9 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
     if (masked) p1_mask(r.s[0], lim - 32 * h, 4 * hl);
     if constexpr (SL == 2) {
       if (h & 1)
-        p1_step<0, 1, 1, 1, 0, true>(r, sel);
+        p1_step<0, 1, 1, 1, 0, true, false, ANCH>(r, sel);
       else
-        p1_step<0, 1, 1, 0, 0, true>(r, sel);
+        p1_step<0, 1, 1, 0, 0, true, false, ANCH>(r, sel);
       p1_read_v(Vl, h, vo, r.vf[0]);
       if (h == 3 && !last) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -913,16 +957,58 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
     // accumulators keep their registers through the tile)
     constexpr int VO = SL == 2 ? 0 : -1;
     if (SL == 2 && VP_P1_SEAM && h == 3)
-      p1_step<1, 0, 0, 0, VO < 0 ? 1 : 0, true, true>(r, sel);
+      p1_step<1, 0, 0, 0, VO < 0 ? 1 : 0, true, true, ANCH>(r, sel);
     else if (h & 1)
-      p1_step<1, 0, 0, 0, VO < 0 ? 1 : 0, true>(r, sel);
+      p1_step<1, 0, 0, 0, VO < 0 ? 1 : 0, true, false, ANCH>(r, sel);
     else
-      p1_step<1, 0, 0, 1, 0, true>(r, sel);
+      p1_step<1, 0, 0, 1, 0, true, false, ANCH>(r, sel);
+  }
+  if constexpr (ANCH) {
+    // Anchored: a wave whose partial row sums passed 2^62 (a rare, wave-uniform branch) moves its anchor up by 64.
+    // State after step (3, 1): o / lsum of block 0 through job (3, 0) and of block 1 through job (2, 1); pf[1] = the
+    // packed P of job (3, 1) (its PV and row sum run in the next step); s[0] = the next tile's job (0, 0) scores —
+    // all relative to the old anchor, so all of them are scaled by 2^-64 (P, O, l) or moved by -64 (S).
+    float big = 0.f;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) big = fmaxf(big, r.lsum[qi][j]);
+    if (__ballot(!(big <= 0x1p62f)) != 0ull) {
+      const float f = 0x1p-64f;
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi) {
+        r.lsum[qi] *= f;
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) r.o[qi][dh] *= f;
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t w = r.pf[1][j][e];
+          const float lo = __uint_as_float(w << 16) * f, hi = __uint_as_float(w & 0xffff0000u) * f;
+          r.pf[1][j][e] = (uint32_t)__builtin_bit_cast(uint16_t, f2bf(lo)) |
+                          ((uint32_t)__builtin_bit_cast(uint16_t, f2bf(hi)) << 16);
+        }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) r.s[0][i] -= 64.f;
+      r.anc += 64.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) r.negm[i] = -r.anc;
+    }
   }
 }
 
-template <bool TAIL = false, int SL = 4>
+// ANCH (p2a, SL = 2 only): the anchored softmax on the p2 pipeline, for scores with no proven bound.  The wave's
+// reference point (anchor) is an actual score: the max over its 64 queries and the first 32 keys it visits; it enters
+// every QK^T chain as the C operand (C = -anchor: no VALU), and moves up by 64 when a partial row sum passes 2^62
+// (p1_tile).  At the end a workgroup with a non-finite output or row sum (a score more than ~127 log2 units above
+// the anchor inside one tile), or a row sum under 2^-96 (a query whose scores sit far below the wave's anchor, where
+// small terms would underflow) stores nothing and raises its flag in sp.flags; the launcher then re-runs exactly
+// those blocks with the anchored 16x16x32 kernel (per-query anchors and its exact two-pass re-run).
+template <bool TAIL = false, int SL = 4, bool ANCH = false>
 __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const vp_attn_desc d, const AttnSplit sp) {
+  static_assert(!ANCH || SL == 2, "the anchored form is the two-workgroups-per-CU pipeline");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1052,6 +1138,26 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
 #pragma unroll
     for (int c = 0; c < 4; ++c)
       r.s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.kf[0][c], r.qf[0][c], c == 0 ? z : r.s[0], 0, 0, 0);
+    r.anc = 0.f;
+    if constexpr (ANCH) {
+      // the anchor: max over both blocks' scores of the first 32 keys (rows past a segment end re-read its last key,
+      // queries past Nq re-read the last query: every value is a real score).  Block 1's job (0, 1) is recomputed by
+      // the first step with C = -anchor.
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        r.s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.kf[0][c], r.qf[1][c], c == 0 ? z : r.s[1], 0, 0, 0);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fmaxf(r.s[0][i], r.s[1][i]));
+#pragma unroll
+      for (int sh = 1; sh < 64; sh <<= 1) mx = fmaxf(mx, __shfl_xor(mx, sh, 64));
+      r.anc = any ? __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(mx))) : -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        r.s[0][i] -= r.anc;
+        r.negm[i] = -r.anc;
+      }
+    }
   }
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // S -> the first (asm) exp
   for (int ti = tbeg; ti < tend; ++ti) {
@@ -1061,8 +1167,8 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
       const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
       lim = sg.n - sg.key0;
     }
-    p1_tile<SL>(r, sel, slot_of(ti), slot_of(ti + 1), __builtin_amdgcn_readfirstlane(lim), lim < KB, ti + 1 >= tend,
-            ti + 2 >= tend, lane, vo);
+    p1_tile<SL, ANCH>(r, sel, slot_of(ti), slot_of(ti + 1), __builtin_amdgcn_readfirstlane(lim), lim < KB,
+                      ti + 1 >= tend, ti + 2 >= tend, lane, vo);
   }
   // drain: PV + row sums of the last job (3, 1)
 #pragma unroll
@@ -1073,19 +1179,52 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
   r.lsum[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[1][1]), r.lsum[1], 0, 0, 0);
 
   const int qq = lane & 31;
+  float l_tot[2];
 #pragma unroll
   for (int qi = 0; qi < 2; ++qi) {
-    float l_tot = __shfl(r.lsum[qi][0], qq < 16 ? qq : qq + 16, 64);
+    l_tot[qi] = __shfl(r.lsum[qi][0], qq < 16 ? qq : qq + 16, 64);
     const int q = qw0 + qi * 32 + qq;
-    // l_extra: row-sum mass of keys outside the segments (the resample processor's null keys, log2 score units;
-    // bounded mode: reference point 0); a tail-split partial leaves it to attn_combine_kernel
-    if (!TAIL && d.l_extra != nullptr) l_tot += __builtin_amdgcn_exp2f(d.l_extra[((int64_t)b * d.H + h) * d.Nq + min(q, d.Nq - 1)]);
+    // l_extra: row-sum mass of keys outside the segments (the resample processor's null keys, log2 score units,
+    // relative to the reference point: 0 when bounded, the anchor when anchored); a tail-split partial leaves it to
+    // attn_combine_kernel
+    if (!TAIL && d.l_extra != nullptr)
+      l_tot[qi] += __builtin_amdgcn_exp2f(d.l_extra[((int64_t)b * d.H + h) * d.Nq + min(q, d.Nq - 1)] - r.anc);
+  }
+  if constexpr (ANCH) {
+    // any non-finite row sum or output, or a row sum under 2^-96 (its terms would underflow), in the workgroup ->
+    // store nothing, flag the block for the exact re-run (workgroup-uniform decision through 16 bytes of LDS past
+    // the ring; the barrier also retires every wave's last reads of the ring)
+    bool bad = false;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi) {
+      // (a tail-split partial of an empty key range holds no mass: only its non-finite values count.  A non-empty
+      // partial whose row sum underflowed is flagged too — its anchor, shared by the wave, sits far above that
+      // query's scores, and the combine's weights relative to it would underflow as well.)
+      bad |= nonfinite(l_tot[qi]) || (any && !(l_tot[qi] >= 0x1p-96f));
+      const float inv = 1.f / l_tot[qi];
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) bad |= nonfinite(sp.nsplit == 1 ? r.o[qi][dh][i] * inv : r.o[qi][dh][i]);
+    }
+    int* wflag = (int*)(smem + 2 * ST);
+    const int mine = __ballot(bad) != 0ull;
+    if (lane == 0) wflag[wave] = mine;
+    __syncthreads();
+    const int redo = wflag[0] | wflag[1] | wflag[2] | wflag[3];
+    if (tid == 0 && sp.flags != nullptr)
+      sp.flags[sp.nsplit > 1 ? sp.flag_main + (t - sp.t_base) * sp.nsplit + split : t] = redo;
+    if (redo) return;
+  }
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi) {
+    const int q = qw0 + qi * 32 + qq;
     if (sp.nsplit > 1) {
       const int qin = wave * 64 + qi * 32 + qq;
-      store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qin) * 66, r.o[qi], 0.f, l_tot,
-                    hl);
+      store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qin) * 66, r.o[qi], r.anc,
+                    l_tot[qi], hl);
     } else {
-      store_out(d, r.o[qi], l_tot, q, b, h, hl, false, 0.f);
+      store_out(d, r.o[qi], l_tot[qi], q, b, h, hl, false, r.anc);
     }
   }
 }
@@ -1108,8 +1247,6 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
 // ------------------------------------------------------------------------------------------------------------
 VP_DEV int vswz16(int row) { return ((row >> 1) & 3) << 1; }
 
-// inf / NaN by the exponent bits (this file builds with -fno-honor-nans: float compares may assume no NaN)
-VP_DEV bool nonfinite(float x) { return (__float_as_uint(x) & 0x7f800000u) == 0x7f800000u; }
 
 VP_DEV float xmax16(float x) {  // max over the 4 lanes c16 + 16 g (one query's lanes)
   x = fmaxf(x, __shfl_xor(x, 16, 64));
@@ -1139,6 +1276,8 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
   const int nqb = (d.Nq + QB - 1) / QB;
   const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
   const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
+  // redo launch after the anchored p2: only the blocks p2a flagged (workgroup-uniform: one block per workgroup)
+  if (sp.redo && !block_flagged(sp, t)) return;
   const int bh = t / nqb;
   const int qb = t - bh * nqb;
   const int b = bh / d.H;
@@ -1898,6 +2037,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
   }
 }
 
+#if VP_ATTN_EXTRA_VARIANTS  // rejected A/B variant: outside the default library
 // ---- f8p (VP_ATTN8_VARIANT=4): the fp8 kernel as a software pipeline, the p1 schedule carried over to e4m3.  4 waves
 // x 32 queries per workgroup at two workgroups per CU (256 VGPRs: two score buffers live), an 8-tile LDS ring filled
 // up to five tiles ahead with one barrier per two 64-key tiles.  Step j issues PV of tile j-1 (while tile j's max runs
@@ -2183,35 +2323,48 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_fp8p(const vp_attn_fp8_desc d
   const float v0 = __shfl(r.lsum[0], qq & 15, 64), v1 = __shfl(r.lsum[1], qq & 15, 64);
   store_out(d, r.o, qq < 16 ? v0 : v1, q, b, h, g, false);
 }
+#endif  // VP_ATTN_EXTRA_VARIANTS
 }  // namespace
 
 namespace {
-// kernels: LAZY for unbounded scores, BOUNDED for VP_ATTN_BOUNDED_SCORES (env VP_ATTN_BOUNDED_MODE=lazy runs the
-// LAZY kernel there too: A/B)
+// The attention kernels of the default library (VP_ATTN_EXTRA_VARIANTS=1 adds the rejected A/B variants: lazy / w32 =
+// the 8-wave kernels, w64 = the two-blocks-per-wave kernel with the general DMA, s16i, p1 = the one-workgroup-per-CU
+// pipeline; the fp8 exp2 + RNE form and f8p: DESIGN.md §3, §7).
 struct AttnVar {
+  const char* name;
   const void* fn;
   const void* fn_tail;  // the grid-tail split instance
   int threads;
   int lds;  // dynamic LDS bytes
 };
+#if VP_ATTN_EXTRA_VARIANTS
+#define VP_EXTRA(a, b) (const void*)a, (const void*)b
+#else
+#define VP_EXTRA(a, b) nullptr, nullptr
+#endif
+enum { V_LAZY, V_W32, V_W64, V_S16, V_A16, V_S16I, V_P1, V_W64F, V_P2, V_P2A, V_NVAR };
 static const AttnVar attn_vars[] = {
-    {(const void*)attn_fwd<MODE_LAZY>, (const void*)attn_fwd<MODE_LAZY, true>, NW * 64, LDS_BYTES},
-    {(const void*)attn_fwd<MODE_BOUNDED>, (const void*)attn_fwd<MODE_BOUNDED, true>, NW * 64, LDS_BYTES},
-    {(const void*)attn_fwd_w64<false>, (const void*)attn_fwd_w64<true>, NW4 * 64, LDS_BYTES},
-    {(const void*)attn_fwd_s16<false>, (const void*)attn_fwd_s16<true>, NW4 * 64, LDS_BYTES},
-    {(const void*)attn_fwd_s16<false, true>, (const void*)attn_fwd_s16<true, true>, NW4 * 64, LDS_BYTES},
-    {(const void*)attn_fwd_s16<false, false, 1>, (const void*)attn_fwd_s16<true, false, 1>, NW4 * 64, LDS_BYTES},
-    {(const void*)attn_fwd_p1<false>, (const void*)attn_fwd_p1<true>, NW4 * 64, P1_LDS},
-    {(const void*)attn_fwd_w64<false, true>, (const void*)attn_fwd_w64<true, true>, NW4 * 64, LDS_BYTES},
-    {(const void*)attn_fwd_p1<false, 2>, (const void*)attn_fwd_p1<true, 2>, NW4 * 64, 2 * ST},
+    {"lazy", VP_EXTRA(attn_fwd<MODE_LAZY>, (attn_fwd<MODE_LAZY, true>)), NW * 64, LDS_BYTES},
+    {"w32", VP_EXTRA(attn_fwd<MODE_BOUNDED>, (attn_fwd<MODE_BOUNDED, true>)), NW * 64, LDS_BYTES},
+    {"w64", VP_EXTRA(attn_fwd_w64<false>, attn_fwd_w64<true>), NW4 * 64, LDS_BYTES},
+    {"s16", (const void*)attn_fwd_s16<false>, (const void*)attn_fwd_s16<true>, NW4 * 64, LDS_BYTES},
+    {"a16", (const void*)attn_fwd_s16<false, true>, (const void*)attn_fwd_s16<true, true>, NW4 * 64, LDS_BYTES},
+    {"s16i", VP_EXTRA((attn_fwd_s16<false, false, 1>), (attn_fwd_s16<true, false, 1>)), NW4 * 64, LDS_BYTES},
+    {"p1", VP_EXTRA(attn_fwd_p1<false>, attn_fwd_p1<true>), NW4 * 64, P1_LDS},
+    {"w64f", VP_EXTRA((attn_fwd_w64<false, true>), (attn_fwd_w64<true, true>)), NW4 * 64, LDS_BYTES},
+    {"p2", (const void*)attn_fwd_p1<false, 2>, (const void*)attn_fwd_p1<true, 2>, NW4 * 64, 2 * ST},
+    {"p2a", (const void*)attn_fwd_p1<false, 2, true>, (const void*)attn_fwd_p1<true, 2, true>, NW4 * 64, 2 * ST + 16},
 };
-constexpr int ATTN_NVAR = sizeof(attn_vars) / sizeof(attn_vars[0]);
+#undef VP_EXTRA
+static_assert(sizeof(attn_vars) / sizeof(attn_vars[0]) == V_NVAR, "variant table");
 
 struct AttnPlan {
   const AttnVar* v;
+  int var;
   int64_t nblk;
   int ntail = 0, nsplit = 1;  // tail split: the last ntail blocks as ntail * nsplit key-range workgroups
-  int64_t ws_bytes = 0;
+  int64_t ws_bytes = 0;       // tail partials, then (p2a) the redo flags
+  int64_t part_bytes = 0;     // the tail partials' part of it
 };
 
 int attn_check(const vp_attn_desc* d) {
@@ -2230,15 +2383,23 @@ int attn_check(const vp_attn_desc* d) {
   return VP_OK;
 }
 
+int variant_by_name(const char* e) {
+  if (e == nullptr || e[0] == 0) return -1;
+  for (int i = 0; i < V_NVAR; ++i)
+    if (strcmp(e, attn_vars[i].name) == 0) return i;
+  return -2;
+}
+
 int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   static bool attr_set = false;
-  static int slots_v[ATTN_NVAR] = {};  // resident workgroups chip-wide per variant
+  static int slots_v[V_NVAR] = {};  // resident workgroups chip-wide per variant
   if (!attr_set) {
     attr_set = true;
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    for (int i = 0; i < ATTN_NVAR; ++i) {
+    for (int i = 0; i < V_NVAR; ++i) {
+      if (attn_vars[i].fn == nullptr) continue;
       (void)hipFuncSetAttribute(attn_vars[i].fn, hipFuncAttributeMaxDynamicSharedMemorySize, attn_vars[i].lds);
       (void)hipFuncSetAttribute(attn_vars[i].fn_tail, hipFuncAttributeMaxDynamicSharedMemorySize, attn_vars[i].lds);
       int per_cu = 0;
@@ -2248,36 +2409,28 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
       slots_v[i] = per_cu * cus;
     }
   }
-  // BOUNDED scores (the host proved |score| <= VP_ATTN_SCORE_BOUND): p2 (default since round 3: the software-pipelined
-  // p1 steps at two workgroups per CU, 6.04 vs 6.49 ms per config-2 call for w64f, profiles/r03_attn_p2_ab.log);
-  // VP_ATTN_BOUNDED_MODE = w64f (two 32-query blocks per wave, scalar-base DMA), w64 (the same with the general DMA),
-  // lazy (running max), w32 (8 waves, one block per wave), s16 (64 queries per wave on the 16x16x32 MFMA), a16 (s16
-  // with the anchored softmax), s16i (per-query-tile PV order), p1 (one workgroup per CU) for A/B.
-  // Unbounded scores: the anchored s16 kernel (a16, default: no bound needed, no host sync); VP_ATTN_UNBOUNDED_MODE =
-  // lazy: the running-max kernel.
-  auto pick = [](const char* e, int dflt) {
-    if (e == nullptr || e[0] == 0) return dflt;
-    if (e[0] == 'l') return 0;
-    if (e[0] == 'w' && e[1] == '3') return 1;
-    if (e[0] == 'w' && e[1] == '6') return e[3] == 'f' ? 7 : 2;  // w64 / w64f
-    if (e[0] == 's') return e[3] == 'i' ? 5 : 3;  // s16 / s16i
-    if (e[0] == 'a') return 4;  // a16
-    if (e[0] == 'p') return e[1] == '2' ? 8 : 6;  // p1 / p2 (the p1 pipeline at two workgroups per CU)
-    return dflt;
-  };
-  int variant = (d->flags & VP_ATTN_BOUNDED_SCORES) ? pick(getenv("VP_ATTN_BOUNDED_MODE"), 8)
-                                                    : pick(getenv("VP_ATTN_UNBOUNDED_MODE"), 4);
-  if (!(d->flags & VP_ATTN_BOUNDED_SCORES) && variant != 4) variant = 0;  // unbounded: lazy / anchored
+  // BOUNDED scores (the host proved |score| <= VP_ATTN_SCORE_BOUND): p2, the software-pipelined p1 steps at two
+  // workgroups per CU (6.04 vs 6.49 ms per config-2 call for w64f, profiles/r03_attn_p2_ab.log).
+  // Unbounded scores: p2a, the same pipeline with the anchored softmax and a redo launch of a16 for the blocks it
+  // flags (needs the workspace for its flags; without one: a16).  VP_ATTN_BOUNDED_MODE / VP_ATTN_UNBOUNDED_MODE name
+  // another variant of the table (A/B; a variant outside this build is VP_ERR_UNSUPPORTED).
+  const bool bounded = (d->flags & VP_ATTN_BOUNDED_SCORES) != 0;
+  int variant = variant_by_name(getenv(bounded ? "VP_ATTN_BOUNDED_MODE" : "VP_ATTN_UNBOUNDED_MODE"));
+  if (variant == -2) return VP_ERR_UNSUPPORTED;
+  if (variant < 0) variant = bounded ? V_P2 : V_P2A;
+  // an unbounded launch needs a kernel that does not assume the bound: lazy, a16 or p2a
+  if (!bounded && variant != V_LAZY && variant != V_A16 && variant != V_P2A) return VP_ERR_UNSUPPORTED;
+  if (attn_vars[variant].fn == nullptr) return VP_ERR_UNSUPPORTED;
   // the resample processor's segment hints: k2_len / l_extra (the closed-form null keys, the default) are taken by
-  // s16 / a16 and p1 / p2; k2_full (null keys as zero-value keys) by the 16x16x32 kernels only (config 4 ran s16 +
-  // k2_full at 11.3 ms per call against 13.8 for a w64 instance with the hint, profiles/r03_bench_config4_*), so a
-  // k2_full launch, and any hinted launch of another kernel, takes s16 (bounded) / a16 (unbounded)
+  // s16 / a16 and p1 / p2 / p2a; k2_full (null keys as zero-value keys) by the 16x16x32 kernels only (config 4 ran
+  // s16 + k2_full at 11.3 ms per call against 13.8 for a w64 instance with the hint, profiles/r03_bench_config4_*),
+  // so a k2_full launch, and any hinted launch of another kernel, takes s16 (bounded) / a16 (unbounded)
   if (d->k2_full != nullptr || d->k2_len != nullptr || d->l_extra != nullptr) {
-    if (variant == 4 || ((variant == 6 || variant == 8) && d->k2_full == nullptr)) {
-    } else {
-      variant = 3;
-    }
+    const bool takes = variant == V_S16 || variant == V_A16 ||
+                       ((variant == V_P1 || variant == V_P2 || variant == V_P2A) && d->k2_full == nullptr);
+    if (!takes) variant = bounded ? V_S16 : V_A16;
   }
+  pl.var = variant;
   pl.v = &attn_vars[variant];
   const int slots = slots_v[variant];
   const int nqb = (d->Nq + QB - 1) / QB;
@@ -2292,13 +2445,24 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
       if (S >= 2) {
         pl.ntail = tail;
         pl.nsplit = S;
-        pl.ws_bytes = (int64_t)tail * S * QB * 66 * 4;
+        pl.part_bytes = (int64_t)tail * S * QB * 66 * 4;
       }
     }
   }
+  pl.ws_bytes = pl.part_bytes;
+  if (variant == V_P2A) pl.ws_bytes += ((pl.nblk - pl.ntail) + (int64_t)pl.ntail * pl.nsplit) * 4;
   return VP_OK;
 }
 }  // namespace
+
+extern "C" int vp_attention_variant_built(const char* name) {
+  if (name != nullptr && strncmp(name, "fp8:", 4) == 0) {  // the fp8 kernel's VP_ATTN8_VARIANT values
+    const int f = atoi(name + 4);
+    return f == 2 || f == 3 || ((f == 1 || f == 4) && VP_ATTN_EXTRA_VARIANTS) ? 1 : 0;
+  }
+  const int v = variant_by_name(name);
+  return v >= 0 && attn_vars[v].fn != nullptr ? 1 : 0;
+}
 
 extern "C" int64_t vp_attention_workspace_bytes(const vp_attn_desc* d) {
   if (attn_check(d) != VP_OK) return -1;
@@ -2314,25 +2478,42 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   AttnPlan pl;
   rc = attn_plan(d, pl);
   if (rc != VP_OK) return rc;
+  const bool have_ws = workspace != nullptr && workspace_bytes >= pl.ws_bytes && ((uintptr_t)workspace & 15) == 0;
+  if (pl.var == V_P2A && !have_ws) {
+    // p2a needs its redo flags: without the workspace, the anchored 16x16x32 kernel alone (unsplit)
+    pl.var = V_A16;
+    pl.v = &attn_vars[V_A16];
+    pl.ntail = 0;
+    pl.nsplit = 1;
+  }
   const AttnVar& v = *pl.v;
-  const bool split = pl.ntail > 0 && workspace != nullptr && workspace_bytes >= pl.ws_bytes;
+  const bool split = pl.ntail > 0 && have_ws;
   const int64_t main_blocks = split ? pl.nblk - pl.ntail : pl.nblk;
+  int* flags = pl.var == V_P2A ? (int*)((char*)workspace + pl.part_bytes) : nullptr;
   hipError_t le = hipSuccess;
   if (main_blocks > 0) {
-    const AttnSplit none = {0, 1, nullptr};
+    const AttnSplit none = {0, 1, nullptr, flags, (int)main_blocks, pl.nsplit, 0};
     void* args[] = {(void*)d, (void*)&none};
     le = hipLaunchKernel(v.fn, dim3((unsigned)main_blocks), dim3(v.threads), args, v.lds, (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
   }
   if (split) {
-    const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace};
+    const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace, flags, (int)main_blocks, pl.nsplit, 0};
     void* args[] = {(void*)d, (void*)&sp};
     le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.threads), args, v.lds,
                          (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
     const int nthreads = pl.ntail * QB * 16;
     hipLaunchKernelGGL(attn_combine_kernel, dim3((nthreads + 255) / 256), dim3(256), 0, (hipStream_t)stream, *d,
-                       (int)main_blocks, pl.ntail, pl.nsplit, QB, (const float*)workspace);
+                       (int)main_blocks, pl.ntail, pl.nsplit, QB, (const float*)workspace, (const int*)flags);
+  }
+  if (flags != nullptr) {
+    // the blocks p2a flagged, exactly, with the anchored 16x16x32 kernel (every other workgroup returns at once)
+    const AttnVar& r = attn_vars[V_A16];
+    const AttnSplit rs = {0, 1, nullptr, flags, (int)main_blocks, split ? pl.nsplit : 1, 1};
+    void* args[] = {(void*)d, (void*)&rs};
+    le = hipLaunchKernel(r.fn, dim3((unsigned)pl.nblk), dim3(r.threads), args, r.lds, (hipStream_t)stream);
+    if (le != hipSuccess) return (int)le;
   }
   VP_CHECK_LAUNCH();
   return VP_OK;
@@ -2390,19 +2571,31 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
   // barrier (1.43 against 1.46); 4 = f8p, the lin2 codes in a p1-style software pipeline at 2 waves/SIMD: parity
   // identical to 3, but 0.93-0.94x its speed (profiles/r03_f8p_ab_rejected.log: at two waves per SIMD the wave's own
   // instruction issue, ~13 VALU + ~6 SALU per MFMA, not the matrix pipe, sets the step), kept for A/B.
+  // variants 1 (exp2 + RNE) and 4 (f8p) are rejected A/B forms: built only with VP_ATTN_EXTRA_VARIANTS
+#if VP_ATTN_EXTRA_VARIANTS
   static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, 2, true, 0>,
                                     (const void*)attn_fwd_fp8<NW, 4, 2, true, 1>,
                                     (const void*)attn_fwd_fp8<NW, 4, 2, true, 2>};
+#else
+  static const void* const fns[] = {nullptr, (const void*)attn_fwd_fp8<NW, 4, 2, true, 1>,
+                                    (const void*)attn_fwd_fp8<NW, 4, 2, true, 2>};
+#endif
   static bool attr_set = false;
   if (!attr_set) {
     attr_set = true;
     for (int i = 0; i < 3; ++i)
-      (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * F8_STAGE);
+      if (fns[i] != nullptr)
+        (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * F8_STAGE);
+#if VP_ATTN_EXTRA_VARIANTS
     (void)hipFuncSetAttribute((const void*)attn_fwd_fp8p, hipFuncAttributeMaxDynamicSharedMemorySize, F8P_LDS);
+#endif
   }
   const char* e = getenv("VP_ATTN8_VARIANT");
   int variant = e != nullptr ? atoi(e) : 0;
   if (variant < 1 || variant > 4) variant = 3;
+#if !VP_ATTN_EXTRA_VARIANTS
+  if (variant == 1 || variant == 4) return VP_ERR_UNSUPPORTED;
+#else
   if (variant == 4) {
     const int nqb4 = (d.Nq + 127) / 128;
     const int64_t grid4 = (int64_t)d.B * d.H * nqb4;
@@ -2414,6 +2607,7 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
     VP_CHECK_LAUNCH();
     return VP_OK;
   }
+#endif
   const int nqb = (d.Nq + NW * 32 - 1) / (NW * 32);
   const int64_t grid = (int64_t)d.B * d.H * nqb;
   if (grid > 0x7fffffff) return VP_ERR_ARG;

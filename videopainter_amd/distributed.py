@@ -150,6 +150,48 @@ def broadcast_module(module: torch.nn.Module, src: int = 0, bucket_bytes: int = 
     broadcast_tensors(list(module.state_dict().values()), src=src, bucket_bytes=bucket_bytes, method=method)
 
 
+@torch.no_grad()
+def bucket_digests(tensors: Iterable[torch.Tensor], bucket_bytes: int = BUCKET_BYTES) -> torch.Tensor:
+    """Per replication bucket (the buckets broadcast_tensors sends): the sum of the raw bit patterns and their sum
+    weighted by (position mod 997) + 1, in int64 on the tensors' device — one row [sum, weighted] per bucket.  Two
+    ranks agree on a row only if the bucket's bytes agree (up to a collision of both sums)."""
+    rows = []
+    for b in _buckets([t for t in tensors if t.numel() > 0], bucket_bytes):
+        s0 = torch.zeros((), dtype=torch.int64, device=b[0].device)
+        s1 = torch.zeros((), dtype=torch.int64, device=b[0].device)
+        off = 0
+        for t in b:
+            flat = t.detach().reshape(-1)
+            isz = flat.element_size()
+            bits = flat.view({1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[isz]).to(torch.int64)
+            if isz == 2:
+                bits = bits & 0xFFFF
+            elif isz == 4:
+                bits = bits & 0xFFFFFFFF
+            w = (torch.arange(off, off + flat.numel(), device=flat.device, dtype=torch.int64) % 997) + 1
+            s0 += bits.sum()
+            s1 += (bits * w).sum()
+            off += flat.numel()
+        rows.append(torch.stack([s0, s1]))
+    return torch.stack(rows) if rows else torch.zeros(0, 2, dtype=torch.int64)
+
+
+@torch.no_grad()
+def verify_replicas(module: torch.nn.Module, bucket_bytes: int = BUCKET_BYTES, group=None):
+    """After broadcast_module: does every rank hold rank 0's bytes?  Each rank digests its buckets
+    (bucket_digests, on the device), one all-reduce of MIN and one of MAX compare them across ranks (the same calls
+    on RCCL and gloo).  Returns (identical on every rank, number of buckets); collective: every rank must call it."""
+    d = bucket_digests(list(module.state_dict().values()), bucket_bytes)
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return True, int(d.shape[0])
+    lo, hi = d.clone(), d.clone()
+    with _staged(lo, group) as a:
+        dist.all_reduce(a, op=dist.ReduceOp.MIN, group=group)
+    with _staged(hi, group) as a:
+        dist.all_reduce(a, op=dist.ReduceOp.MAX, group=group)
+    return bool(torch.equal(lo, hi)), int(d.shape[0])
+
+
 def max_over_ranks(value: float, device=None) -> float:
     """The bench's timing rule: the slowest rank's elapsed time."""
     if not dist.is_initialized() or dist.get_world_size() == 1:

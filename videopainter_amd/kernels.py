@@ -380,6 +380,12 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
     return out
 
 
+def attention_variant_built(name: str) -> bool:
+    """Is the attention kernel variant `name` (a value of VP_ATTN_BOUNDED_MODE / VP_ATTN_UNBOUNDED_MODE) in the
+    library?  The rejected A/B variants are built only with VP_ATTN_EXTRA_VARIANTS=1 (host-only query)."""
+    return bool(N.lib().vp_attention_variant_built(name.encode()))
+
+
 def attention_bwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor, do: torch.Tensor,
                   lse: torch.Tensor, heads: int, scale: float = 0.125, dq: Optional[torch.Tensor] = None,
                   dk: Optional[torch.Tensor] = None, dv: Optional[torch.Tensor] = None):

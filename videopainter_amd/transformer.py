@@ -505,6 +505,25 @@ class CogVideoXTransformer3DModel(ModelMixin):
             if hasattr(m, "set_processor"):
                 m.set_processor(processor.pop(f"{name}.processor") if isinstance(processor, dict) else processor)
 
+    # -- QKV fusion switches (reference :431-470) --
+    def fuse_qkv_projections(self):
+        """Reference :432-456 fuses to_q / to_k / to_v of every Attention into one projection and installs
+        FusedCogVideoXAttnProcessor2_0.  Here Q, K and V always run as ONE GEMM over the three weight segments with
+        the qk-norm + RoPE epilogue (CogVideoXBlock.forward_joint), so there is nothing to fuse: the call records
+        the processors like the reference (for unfuse) and leaves weights, state-dict keys and outputs unchanged."""
+        for _, proc in self.attn_processors.items():
+            if "Added" in type(proc).__name__:
+                raise ValueError("`fuse_qkv_projections()` is not supported for models having added KV projections.")
+        self.original_attn_processors = self.attn_processors
+        self._qkv_fused = True
+
+    def unfuse_qkv_projections(self):
+        """Reference :459-470: restores the processors recorded by fuse_qkv_projections (a no-op for the math, as
+        fusing is)."""
+        if getattr(self, "original_attn_processors", None) is not None:
+            self.set_attn_processor(self.original_attn_processors)
+        self._qkv_fused = False
+
     # -- shared pieces --
     def _time_embed(self, timestep, batch: int, device) -> torch.Tensor:
         if not torch.is_tensor(timestep):
