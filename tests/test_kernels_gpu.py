@@ -17,7 +17,8 @@ def _lib():
     _native.lib()
 
 
-@pytest.fixture(params=["5", "11", "1", "20"], ids=["gemm_v5", "gemm_v11", "gemm_v1", "gemm_v20"])
+@pytest.fixture(params=["5", "11", "12", "13", "30", "1", "20"],
+                ids=["gemm_v5", "gemm_v11", "gemm_v12", "gemm_v13", "gemm_v30", "gemm_v1", "gemm_v20"])
 def gemm_variant(request, monkeypatch):
     monkeypatch.setenv("VP_GEMM_VARIANT", request.param)
     return request.param
@@ -44,7 +45,7 @@ def attn_variant(request, monkeypatch):
     """Unbounded-score launches (no VP_ATTN_BOUNDED_SCORES): p2a (the library default: the p2 pipeline with an
     anchored reference point and the a16 re-run of flagged blocks), a16 (the anchored-softmax 16x16x32 kernel), lazy
     (the running-max kernel).  Bounded-score launches (include/vp_hip.h VP_ATTN_BOUNDED_SCORES, the host proved the
-    bound): p2 (the library default), s16, and the A/B variants of a VP_ATTN_EXTRA_VARIANTS build (w32 / w64 / w64f /
+    bound; the library default is p2a there too): p2, s16, and the A/B variants of a VP_ATTN_EXTRA_VARIANTS build (w32 / w64 / w64f /
     s16i / p1)."""
     need_variant(request.param, monkeypatch)
     return request.param
@@ -413,8 +414,9 @@ def test_gemm_qknorm_rope_epilogue_matches_separate_kernels(H, T, rope, gemm_var
 
 @pytest.mark.parametrize("Kk", [512, 640, 3072])
 def test_gemm_staggered_matches_quadrant_pipeline(Kk, monkeypatch):
-    """Variant 11 (the quadrant pipeline with the two wave groups staggered by one barrier) gives variant 5's result
-    bit for bit for every epilogue kind — same MFMA order per accumulator — with ragged M, nk = 8 / 10 / 48 K-tiles
+    """Variant 11 (the quadrant pipeline with the two wave groups staggered by one barrier) and variant 12 (two
+    32-MFMA phases and one barrier per K-tile) and variant 30 (two workgroups per CU, 256 x 128 tiles, 32-K steps)
+    give variant 5's result bit for bit for every epilogue kind — same MFMA order per accumulator — with ragged M, nk = 8 / 10 / 48 K-tiles
     (the steady loop, the 4-tile tail and the shortest staggered prologue), the row remap and the injection."""
     from types import SimpleNamespace
 
@@ -449,14 +451,14 @@ def test_gemm_staggered_matches_quadrant_pipeline(Kk, monkeypatch):
     for name, fn in cases.items():
         width = 3 * D if name in ("bias3", "qknorm") else D
         outs = []
-        for v in ("5", "11"):
+        for v in ("5", "11", "12", "13", "30"):
             monkeypatch.setenv("VP_GEMM_VARIANT", v)
             o = torch.full((B, Ntok, width), float("nan"), device=dev, dtype=torch.bfloat16)
             if name == "addrows":
                 o.zero_()
             fn(o)
             outs.append(o)
-        assert torch.equal(outs[0], outs[1]), name
+        assert all(torch.equal(outs[0], o) for o in outs[1:]), name
         assert not torch.isnan(outs[1].float()).any(), name
 
 
@@ -659,7 +661,8 @@ def test_attention_k2_full_hint(mode, monkeypatch):
     K.attention(q, k, v, o, H, k2=k2, v2=v2, k2_full=full.to(dev), **kw)
     hd = lambda x: x.float().cpu().reshape(B, -1, H, 64).transpose(1, 2)  # noqa: E731
     ref = _sdpa(hd(q), torch.cat([hd(k), hd(k2)], 2), torch.cat([hd(v), hd(v2)], 2)).transpose(1, 2).reshape(B, Nn, D)
-    assert rel(o, ref) < 1e-2 and rel(o, o_ref) < 2e-3
+    # (p2a does not take the hint: the hinted launch runs a16, whose bf16 P is rounded against other anchors)
+    assert rel(o, ref) < 1e-2 and rel(o, o_ref) < (5e-3 if mode == "p2a" else 2e-3)
 
 
 def _grid_rope(F_, Hh, Ww):

@@ -136,6 +136,25 @@ def test_fused_qkv_norm_rope_bit_exact_vs_separate_launches(env, monkeypatch):
 
 
 @torch.no_grad()
+def test_resample_mask_plan_built_once_per_forward(env, monkeypatch):
+    """The resample processor's mask plan (row partition + null-key segments) is built once per transformer forward
+    and found by every later layer (the uint8 mask reaches the processors as the same tensor): one
+    vp_partition_rows_index launch per forward, not one per layer."""
+    from videopainter_amd import attention_processor as AP
+    from videopainter_amd import kernels as K
+    i, g = env["inp"], env["g"]
+    calls = []
+    orig = K.partition_rows_index
+    monkeypatch.setattr(K, "partition_rows_index", lambda m: calls.append(1) or orig(m))
+    AP._MASK_PLANS.clear()
+    env["trr"](hidden_states=_d(i["hidden"]), encoder_hidden_states=_d(i["enc"]), timestep=i["timestep"].to(dev),
+               image_rotary_emb=i["rope"], branch_block_samples=[_d(g["branch.0"]), _d(g["branch.1"])],
+               branch_block_masks=_d(i["mask"]), id_pool_resample_learnable=True, return_dict=False)
+    torch.cuda.synchronize()
+    assert len(calls) == 1, len(calls)
+
+
+@torch.no_grad()
 def test_resample_processor_matches_reference(env):
     from oracle import cogvideox_oracle as O
     i, g = env["inp"], env["g"]

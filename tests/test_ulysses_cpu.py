@@ -98,3 +98,19 @@ def test_dist_comm_matches_thread_comm_gloo():
         assert torch.equal(full, want[rank])
         assert torch.equal(back, g[:, rank * n:(rank + 1) * n, :H * 64])
         assert torch.equal(gat, torch.stack([torch.full((2, 3), 0.0), torch.full((2, 3), 1.0)]))
+
+
+def test_transformer_view_applies_the_per_call_lora_scale(monkeypatch):
+    """The head-parallel view re-folds attached LoRA adapters to the call's attention_kwargs["scale"] (default 1.0)
+    before its forward, as the single-GPU forward does."""
+    import types
+    import torch
+    from videopainter_amd import ulysses as U
+    seen = []
+    model = types.SimpleNamespace(config=types.SimpleNamespace(patch_size=2), proj_out=None,
+                                  _call_lora_scale=lambda kw: seen.append(dict(kw) if kw else kw))
+    monkeypatch.setattr(U, "transformer_forward", lambda *a, **k: (torch.zeros(1), []))
+    view = U._TransformerView(model, types.SimpleNamespace(comm=None, rank=0))
+    view(torch.zeros(1), torch.zeros(1, 3, 4), 0, attention_kwargs={"scale": 0.5}, return_dict=False)
+    view(torch.zeros(1), torch.zeros(1, 3, 4), 0, return_dict=False)
+    assert seen == [{"scale": 0.5}, None]

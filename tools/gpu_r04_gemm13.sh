@@ -1,0 +1,13 @@
+#!/bin/bash
+# GEMM variant 30 (two workgroups per CU): GEMM tests, interleaved kernel A/B 11 / 30, config-2 bench with 30
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+run() { local name=$1; shift; local to=$1; shift
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; tail -3 "gpurun_out/$name.log"
+  [ $rc -ne 0 ] && { tail -40 "gpurun_out/$name.log"; exit $rc; }; return 0; }
+run r04_gemm13_tests 600 python -u -m pytest tests/test_kernels_gpu.py -k "gemm" -x -q --timeout 120 --timeout-method thread
+run r04_gemm13_ab 300 python tools/bench_kernels.py --only gemm --gemm-variants 11,13 --iters 10
+VP_GEMM_VARIANT=13 run r04_bench_g13 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline
+run r04_bench_def2 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline
+exit 0

@@ -47,8 +47,13 @@ def _rope_dev(rope, device, grid=None):
 
 
 def _u8(mask: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """A token mask as contiguous uint8 (the kernels test a byte for non-zero).  An already contiguous uint8 mask is
+    returned as is — the same tensor — so the per-forward mask plan (_mask_plan, keyed on the tensor) is built once
+    and found by every layer."""
     if mask is None:
         return None
+    if mask.dtype == torch.uint8 and mask.is_contiguous():
+        return mask
     if mask.dtype == torch.bool:
         return mask.contiguous().view(torch.uint8)
     return (mask != 0).to(torch.uint8).contiguous()

@@ -2409,15 +2409,17 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
       slots_v[i] = per_cu * cus;
     }
   }
-  // BOUNDED scores (the host proved |score| <= VP_ATTN_SCORE_BOUND): p2, the software-pipelined p1 steps at two
-  // workgroups per CU (6.04 vs 6.49 ms per config-2 call for w64f, profiles/r03_attn_p2_ab.log).
-  // Unbounded scores: p2a, the same pipeline with the anchored softmax and a redo launch of a16 for the blocks it
-  // flags (needs the workspace for its flags; without one: a16).  VP_ATTN_BOUNDED_MODE / VP_ATTN_UNBOUNDED_MODE name
-  // another variant of the table (A/B; a variant outside this build is VP_ERR_UNSUPPORTED).
+  // p2a for every launch: the p2 pipeline (the software-pipelined p1 steps at two workgroups per CU, 6.04 vs 6.49 ms
+  // per config-2 call for w64f, profiles/r03_attn_p2_ab.log) with the anchored softmax and a redo launch of a16 for
+  // the blocks it flags (needs the workspace for its flags; without one: a16).  With VP_ATTN_BOUNDED_SCORES (the host
+  // proved |score| <= VP_ATTN_SCORE_BOUND) VP_ATTN_BOUNDED_MODE may name p2 (no anchor) or s16; without it
+  // VP_ATTN_UNBOUNDED_MODE may name a16 (A/B; a variant outside this build is VP_ERR_UNSUPPORTED).
   const bool bounded = (d->flags & VP_ATTN_BOUNDED_SCORES) != 0;
   int variant = variant_by_name(getenv(bounded ? "VP_ATTN_BOUNDED_MODE" : "VP_ATTN_UNBOUNDED_MODE"));
   if (variant == -2) return VP_ERR_UNSUPPORTED;
-  if (variant < 0) variant = bounded ? V_P2 : V_P2A;
+  // default: p2a for every launch (6.13 ms per config-2 call against 6.15-6.30 for p2 interleaved,
+  // profiles/r04_attn_p2a_ab.log: the anchor costs nothing and no bound has to hold); p2 stays the bounded challenger
+  if (variant < 0) variant = V_P2A;
   // an unbounded launch needs a kernel that does not assume the bound: lazy, a16 or p2a
   if (!bounded && variant != V_LAZY && variant != V_A16 && variant != V_P2A) return VP_ERR_UNSUPPORTED;
   if (attn_vars[variant].fn == nullptr) return VP_ERR_UNSUPPORTED;

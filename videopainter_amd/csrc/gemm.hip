@@ -246,19 +246,23 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
   }
 }
 
-// the LDS C image address of fragment (j, i)'s 4 values for this lane (image row = tile row - row0)
-template <int WN, int WM>
+// the LDS C image address of fragment (j, i)'s 4 values for this lane (image row = tile row - row0); CTS: bytes per
+// image row (tile columns x 2 + a bank-conflict pad)
+template <int WN, int WM, int CTS = CT_STRIDE>
 VP_DEV char* epi_lds_addr(char* img, int j, int i, int row0, int wr, int wc, int lane) {
-  return img + (wr * WM + i * 16 + (lane & 15) - row0) * CT_STRIDE + (wc * WN + j * 16 + (lane >> 4) * 4) * 2;
+  return img + (wr * WM + i * 16 + (lane & 15) - row0) * CTS + (wc * WN + j * 16 + (lane >> 4) * 4) * 2;
 }
 
-// image rows [0, nrows) = tile rows row0.. out to C (coalesced 16-byte row stores + the row-wise epilogues)
-template <int NT, bool FP8, int EPI = -1>
+// image rows [0, nrows) = tile rows row0.. out to C (coalesced 16-byte row stores + the row-wise epilogues); BNC:
+// the tile's columns (256, or 128 for the two-workgroups-per-CU kernel)
+template <int NT, bool FP8, int EPI = -1, int BNC = BN>
 VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* smem, int row0, int nrows, int m0,
                          int n0, int tid) {
+  constexpr int CPR = BNC / 8;        // 16-byte chunks per tile row
+  constexpr int CTS = BNC * 2 + 8;
   const int epi = EPI >= 0 ? EPI : d.epilogue;
   bf16* C = (bf16*)d.C;
-  const int chunk = tid & 31;         // 16-byte chunk within the 512-byte tile row
+  const int chunk = tid & (CPR - 1);  // 16-byte chunk within the tile row
   const int ncol = n0 + chunk * 8;
   // row bookkeeping without an integer division per row: the image rows are consecutive matrix rows, so the output
   // group (rows_per_group) and the batch (tokens_per_batch) of the image's first row are computed once and the
@@ -270,11 +274,11 @@ VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* sme
   const bool need_b = epi == VP_EPI_GATED;
   const int b0 = need_b ? mbase / tpb : 0, tk0 = need_b ? mbase - b0 * tpb : 0;
 #pragma unroll 1
-  for (int it = 0; it < nrows / (NT / 32); ++it) {
-    const int mloc = it * (NT / 32) + (tid >> 5);
+  for (int it = 0; it < nrows / (NT / CPR); ++it) {
+    const int mloc = it * (NT / CPR) + tid / CPR;
     const int m = mbase + mloc;
     if (m >= d.M || ncol >= d.N) continue;
-    bf16x8 v = *(const bf16x8*)(smem + mloc * CT_STRIDE + chunk * 16);
+    bf16x8 v = *(const bf16x8*)(smem + mloc * CTS + chunk * 16);
     int grp = grp0, gin = gin0 + mloc;
     while (gin >= rpg) {
       gin -= rpg;
@@ -388,7 +392,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (VAR == 5 || VAR == 11) {
+  if constexpr (VAR == 5 || VAR == 11 || VAR == 12 || VAR == 13) {
     // Quadrant-phase pipeline.  Each wave's 128x64 C block is split into 4 quadrants (64 rows x 32 cols); a K-tile
     // (BK = 64) runs as 4 phases of 16 MFMAs, in the quadrant order (A0,B0) (A0,B1) (A1,B1) (A1,B0) so each phase
     // needs ONE new operand subtile, which is read from LDS into registers during the previous phase.  The LDS
@@ -594,6 +598,99 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     };
+    if constexpr (VAR == 12) {
+      // VAR 12: two phases of 32 MFMAs per K-tile and ONE barrier per K-tile.  Phase 0 of tile k runs quadrant-row 0
+      // against both quadrant-columns (A0 x B0, then A0 x B1), phase 1 quadrant-row 1 (A1 x B0, then A1 x B1).
+      // Register fragments: a0 / a1 (A quadrant-rows), b0 / b1 (B quadrant-cols).  Reads, each into registers
+      // nothing is still reading:
+      //   phase 0 (k): B1(k) first (needed by its second half), then A1(k);
+      //   phase 1 (k): after its first half (the last use of b0): A0(k + 1) and B0(k + 1).
+      // LDS-DMA: the whole of tile k + 2 (4 units, 8 instructions per wave) at the top of phase 1 (k), spread over
+      // that phase's first 16 MFMAs, into the stage tile k used.  The one barrier, at the top of phase 1 (k), follows
+      // every wave's vmcnt(0) (tile k + 1, issued one K-tile earlier, has landed: A0 / B0 (k + 1) are read in this
+      // phase, B1 / A1 (k + 1) in the next) and lgkmcnt(0) (every read of tile k has returned: its stage may be
+      // refilled).  So a wave runs 64 MFMAs per barrier, and its partner wave on the SIMD (the other half of the
+      // workgroup) hides the reads and the barrier wait.
+      FragA a0, a1;
+      FragB b0, b1;
+      auto dma_tile = [&](int tile, int part) {  // part p of 4: unit p of the tile (2 instructions)
+        if (tile < nk) issue_unit(part, tile);
+      };
+      // prologue: tiles 0 and 1 in flight, tile 0 landed and published, A0 / B0 (0) read
+      for (int u = 0; u < 4; ++u) dma_tile(0, u);
+      for (int u = 0; u < 4; ++u) dma_tile(1, u);
+      if (nk > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      readA(a0, Z{}, Z{});
+      readB(b0, Z{}, Z{});
+      const int sz = 0, so = 0;
+      auto mma4 = [&](const FragA& a, const FragB& bb, auto qm_c, auto qn_c, int grp) {  // 4 MFMAs: one A fragment row
+        constexpr int qm = decltype(qm_c)::value, qn = decltype(qn_c)::value;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qn * 2 + j][qm * 4 + grp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                bb[ks * 2 + j], a[ks * 4 + grp], acc[qn * 2 + j][qm * 4 + grp], 0, 0, 0);
+      };
+      // STEADY: tile k + 2 exists (k + 2 < nk), so the DMA and the next reads are unconditional (no branch in the
+      // loop body)
+      auto tile12 = [&](int k, auto par_c, auto steady_c) {
+        using P = decltype(par_c);
+        using NP = std::integral_constant<int, 1 - P::value>;
+        constexpr bool STEADY = decltype(steady_c)::value;
+        const bool more = STEADY || k + 1 < nk;
+        // ---- phase 0 ----
+        // the previous phase's reads of a0 / b0 (issued a 16-MFMA group ago) retire here, before this phase's
+        // reads: the builtin wait tells the compiler's wait pass so (it otherwise waits lgkmcnt(0) for the new reads
+        // too at the loop head, before the first MFMA)
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_sched_barrier(0);
+        readB(b1, P{}, O{});
+        readA(a1, P{}, O{});
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        mma(a0, b0, Z{}, Z{}, sz, so);
+        mma(a0, b1, Z{}, O{}, sz, so);
+        __builtin_amdgcn_s_setprio(0);
+        // ---- phase 1 ----
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if constexpr (STEADY) issue_unit(g, k + 2);
+          else dma_tile(k + 2, g);
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_setprio(1);
+          mma4(a1, b0, O{}, Z{}, g);
+          __builtin_amdgcn_s_setprio(0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (more) {
+          readA(a0, NP{}, Z{});
+          readB(b0, NP{}, Z{});
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        mma(a1, b1, O{}, O{}, sz, so);
+        __builtin_amdgcn_s_setprio(0);
+      };
+      using T_ = std::integral_constant<bool, true>;
+      using F_ = std::integral_constant<bool, false>;
+      int k = 0;
+      for (; k + 3 < nk; k += 2) {
+        tile12(k, Z{}, T_{});
+        tile12(k + 1, O{}, T_{});
+      }
+      // tail (at most 3 tiles; k is even here, so the parities are static)
+      if (k < nk) tile12(k, Z{}, F_{});
+      if (k + 1 < nk) tile12(k + 1, O{}, F_{});
+      if (k + 2 < nk) tile12(k + 2, Z{}, F_{});
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+    } else {
     // VAR 11 = VAR 5 with the two wave groups STAGGERED (cdna_hip_programming.md §5 "256² 8-phase template",
     // MI355X_MICROARCH.md "Two waves per SIMD" item 9): every slot is [memory part] barrier [16 MFMAs] barrier and
     // waves 4-7 (quadrant-row 1, one wave on each SIMD) run one barrier behind waves 0-3, so on every SIMD one
@@ -602,7 +699,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     // BEFORE the slot that reads it (the reader group may be a barrier ahead of the issuer group), so a slot waits
     // for the unit issued 6 slots earlier (vmcnt(10)) and reads the one issued 7 earlier; a slot's own reads retire
     // (lgkmcnt(0)) before its first barrier, so the v5 refill distance (one slot after the last read) still holds.
-    constexpr bool STAGGER = VAR == 11;
+    // VAR 13 = VAR 11 with each slot's fragment reads issued BEFORE its vmcnt wait and LDS-DMA issue, so the read
+    // latency runs under the DMA issue instead of after it (the reads of slot s are of units published at slot s - 1)
+    constexpr bool STAGGER = VAR == 11 || VAR == 13;
+    constexpr bool RFIRST = VAR == 13;
     FragA a0, a1;
     FragB bx, by;
     // prologue: slots -9..-2 (tiles 0 and 1, and nothing that overwrites tile 0's quadrant-row-0 A before it is
@@ -658,26 +758,30 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
       auto cluster_end = [&]() {
         if constexpr (STAGGER) __builtin_amdgcn_s_barrier();
       };
-      slot(s0);
+      if constexpr (!RFIRST) slot(s0);
       readB(b1, P{}, O{});
+      if constexpr (RFIRST) slot(s0);
       cluster();
       mma(a0, b0, Z{}, Z{}, sc.a0, sc.w);
       cluster_end();
-      slot(s0 + 1);
+      if constexpr (!RFIRST) slot(s0 + 1);
       readA(a1, P{}, O{});
+      if constexpr (RFIRST) slot(s0 + 1);
       cluster();
       mma(a0, b1, Z{}, O{}, sc.a0, sc.w);
       cluster_end();
-      slot(s0 + 2);
+      if constexpr (!RFIRST) slot(s0 + 2);
       if (more) {
         readA(a0, NP{}, Z{});
         readS(scn, k + 1);
       }
+      if constexpr (RFIRST) slot(s0 + 2);
       cluster();
       mma(a1, b1, O{}, O{}, sc.a1, sc.w);
       cluster_end();
-      slot(s0 + 3);
+      if constexpr (!RFIRST) slot(s0 + 3);
       if (more) readB(b1, NP{}, Z{});  // b1's registers carry the next tile's quadrant-col 0
+      if constexpr (RFIRST) slot(s0 + 3);
       cluster();
       mma(a1, b0, O{}, Z{}, sc.a1, sc.w);
       cluster_end();
@@ -700,6 +804,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if constexpr (FP8) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");  // asm MFMA results
     __syncthreads();
+    }  // VAR 5 / 11
   } else if constexpr (VAR == 1) {
     const int nk = (d.K + BK - 1) / BK;
     stage_tile(arow, d.K, 0, smem, wave, lane);
@@ -878,6 +983,119 @@ __global__ __launch_bounds__(NT4, 1) void gemm4_kernel(const vp_gemm_desc d) {
   gemm_epilogue<NT4, FN4, FM4, WN4, WM4, false, EPI>(d, MxExt{}, acc, smem, m0, n0, wr, wc, lane, tid);
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// VAR 30: TWO workgroups per CU.  A 256 x 128 tile per workgroup of 4 waves (2 (M) x 2 (N), 128 x 64 per wave: the
+// same 8 x 4 fragments, registers and epilogue as the 8-wave kernel), K-steps of 32 through a 3-stage LDS ring
+// (24 KiB per stage: 72 KiB per workgroup, two workgroups per CU), one barrier per K-step.  The two waves on a SIMD
+// belong to different workgroups, so one's barrier wait, fragment-read latency, DMA issue or epilogue runs beside the
+// other's MFMAs (the structure that made the p2 attention faster) instead of the whole CU reaching its barriers and
+// its epilogue burst together.
+// LDS image of a stage: A [256][32] then B [128][32] bf16, 64-byte rows, 16-byte chunk p = c ^ h((row >> 2) & 3),
+// h = {0, 2, 3, 1}: the four lane groups of a ds_read_b128 fragment read (16 rows x 4 chunks) hit 16 distinct slots
+// of the 256-byte bank row.  Filled by LDS-DMA (1 KiB = 16 rows per instruction, swizzle on the source address).
+// ------------------------------------------------------------------------------------------------------------
+constexpr int BM2 = 256, BN2 = 128, BK2 = 32, NT2 = 256;
+constexpr int A2_BYTES = BM2 * BK2 * 2;             // 16 KiB
+constexpr int STAGE2 = A2_BYTES + BN2 * BK2 * 2;    // 24 KiB
+constexpr int CTS2 = BN2 * 2 + 8;
+constexpr int LDS2 = (3 * STAGE2 > BM2 * CTS2) ? 3 * STAGE2 : BM2 * CTS2;
+static_assert(BM2 * CTS2 <= 3 * STAGE2, "the epilogue image fits in the ring");
+
+VP_DEV int h2(int row) { return (0x1E >> (((row >> 2) & 3) * 2)) & 3; }  // {0, 2, 3, 1}[(row >> 2) & 3]
+
+template <int EPI>
+__global__ __launch_bounds__(NT2, 2) void gemm2_kernel(const vp_gemm_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1;  // 0..1 (M)
+  const int wc = wave & 1;   // 0..1 (N)
+
+  const int tiles_m = (d.M + BM2 - 1) / BM2;
+  const int tiles_n = d.N / BN2;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GROUP = 4;
+  const int per_group = GROUP * tiles_n;
+  const int group_id = t / per_group;
+  const int first_m = group_id * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + ((t % per_group) % gsz);
+  const int tn = (t % per_group) / gsz;
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int nk = d.K / BK2;
+
+  // DMA: instruction p of a stage covers image rows 16p .. 16p + 15 (A: p = 0..15, B: p = 16..23); wave w issues
+  // p = w + 4i (i = 0..5).  Lane l: row 16p + l / 4, physical chunk l % 4 <- logical chunk (l % 4) ^ h(row); h
+  // depends on row bits 2-3 only, so one per-lane offset per operand serves every piece (+ a scalar row step).
+  const int prow = lane >> 2;  // row within the piece
+  const int pch = ((lane & 3) ^ h2(prow)) * 16;
+  const char* abase = (const char*)d.A + (int64_t)m0 * d.lda * 2;
+  const int sgw = n0 / d.n_seg;  // the tile's weight segment (n_seg % 128 == 0: never straddled)
+  const char* wbase = (const char*)d.W[sgw] + (int64_t)(n0 - sgw * d.n_seg) * d.K * 2;
+  // A offsets of the wave's 4 pieces, rows clamped to the last row (the ragged last row tile re-reads it)
+  int aoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) aoff[i] = (min(m0 + 16 * (wave + 4 * i) + prow, d.M - 1) - m0) * (int)d.lda * 2 + pch;
+  const int woff = prow * d.K * 2 + pch;
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)smem);
+  auto glds = [&](const char* sb, int voff, unsigned la) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(la), "v"(voff), "s"(sb)
+                 : "memory", "m0");
+  };
+  auto issue = [&](int kt) {
+    const unsigned st = lds0 + (kt % 3) * STAGE2;
+    const int kb = kt * BK2 * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds(abase + kb, aoff[i], st + (wave + 4 * i) * 1024);  // A pieces 0..15
+#pragma unroll
+    for (int i = 0; i < 2; ++i)  // B pieces 16..23
+      glds(wbase + kb, woff + 16 * (wave + 4 * i) * d.K * 2, st + (16 + wave + 4 * i) * 1024);
+  };
+
+  // fragment reads: A rows wr * 128 + 16 i + lane % 16, B rows wc * 64 + 16 j + lane % 16; chunk lane / 16
+  const int lrow = lane & 15;
+  const int lbase = lrow * 64 + (((lane >> 4) ^ h2(lrow)) << 4);
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  if (nk > 1) issue(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // step kt's DMA (issued two steps ago) landed for this wave; the barrier publishes it for all waves and tells
+    // that every wave's reads of step kt - 1 returned (lgkmcnt(0)), so its stage takes step kt + 2
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 2 < nk) issue(kt + 2);
+    const char* st = smem + (kt % 3) * STAGE2;
+    bf16x8 bf[4], af[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = *(const bf16x8*)(st + A2_BYTES + (wc * 64 + j * 16) * 64 + lbase);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = *(const bf16x8*)(st + (wr * 128 + i * 16) * 64 + lbase);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[j][i], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  epi_values<4, 8, 64, 128, EPI>(
+      d, acc,
+      [&](int j, int i, const bf16x4& o) { *(bf16x4*)epi_lds_addr<64, 128, CTS2>(smem, j, i, 0, wr, wc, lane) = o; },
+      m0, n0, wr, wc, lane);
+  __syncthreads();
+  epi_rows_out<NT2, false, EPI, BN2>(d, MxExt{}, smem, 0, BM2, m0, n0, tid);
+}
+
 // split-K reduce + epilogue: one thread per 8 consecutive output columns of one row; the chunks are summed in a fixed
 // order, then the same roundings as the fused epilogues (epi_values + epi_rows_out)
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const vp_gemm_desc d, const float* __restrict__ ws,
@@ -977,8 +1195,22 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
       (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_SCALE>, (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_GATED>,
       (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_ADDROWS>, nullptr,
       (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_QKNORM_ROPE>};
+  static const void* const k13[7] = {
+      (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS>, (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_GELU>,
+      (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_SCALE>, (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_GATED>,
+      (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_ADDROWS>, nullptr,
+      (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_QKNORM_ROPE>};
+  static const void* const k12[7] = {
+      (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS>, (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_GELU>,
+      (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_SCALE>, (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_GATED>,
+      (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_ADDROWS>, nullptr,
+      (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_QKNORM_ROPE>};
   static bool attr_set = false;
   if (!attr_set) {
+    for (const void* f : k12)
+      if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    for (const void* f : k13)
+      if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -989,7 +1221,34 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   }
   const char* e = getenv("VP_GEMM_VARIANT");  // read per call: tests switch it between launches
   int variant = e != nullptr ? atoi(e) : 11;
-  if (variant != 1 && variant != 5 && variant != 11 && variant != 20) variant = 11;
+  if (variant != 1 && variant != 5 && variant != 11 && variant != 12 && variant != 13 && variant != 20 && variant != 30)
+    variant = 11;
+  // 30: two workgroups per CU, 256 x 128 tiles (whole 128-column tiles of one weight segment, whole 32-K steps,
+  // 32-bit in-tile DMA offsets)
+  if (variant == 30) {
+    const bool ok30 = (d->N % BN2) == 0 && (d->n_seg % BN2) == 0 && (d->K % BK2) == 0 &&
+                      (int64_t)BM2 * d->lda * 2 < ((int64_t)1 << 31) && (int64_t)BN2 * d->K * 2 < ((int64_t)1 << 31);
+    if (ok30) {
+      static const void* const k30[7] = {
+          (const void*)gemm2_kernel<VP_EPI_BIAS>, (const void*)gemm2_kernel<VP_EPI_BIAS_GELU>,
+          (const void*)gemm2_kernel<VP_EPI_BIAS_SCALE>, (const void*)gemm2_kernel<VP_EPI_GATED>,
+          (const void*)gemm2_kernel<VP_EPI_BIAS_ADDROWS>, nullptr, (const void*)gemm2_kernel<VP_EPI_BIAS_QKNORM_ROPE>};
+      static bool attr30 = false;
+      if (!attr30) {
+        for (const void* f : k30)
+          if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        attr30 = true;
+      }
+      const int tiles30 = ((d->M + BM2 - 1) / BM2) * (d->N / BN2);
+      void* args[] = {(void*)d};
+      const hipError_t le = hipLaunchKernel(k30[d->epilogue], dim3(tiles30), dim3(NT2), args, LDS2,
+                                            (hipStream_t)stream);
+      if (le != hipSuccess) return (int)le;
+      VP_CHECK_LAUNCH();
+      return VP_OK;
+    }
+    variant = 11;
+  }
   // 20: the 4-wave AGPR-accumulator kernel (whole 256-column tiles of one weight segment, whole K-tiles, 32-bit
   // in-tile DMA offsets)
   if (variant == 20) {
@@ -1020,9 +1279,15 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   const bool w32 = (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
   const bool tile32 = (int64_t)BM * d->lda * 2 < ((int64_t)1 << 31) && w32;
   if (variant != 1 && ((d->K % BK) != 0 || !tile32)) variant = 1;  // needs whole K-tiles
-  if (variant == 11 && d->K < 8 * BK) variant = 5;                  // the staggered prologue assumes >= 8 K-tiles
+  if ((variant == 11 || variant == 13) && d->K < 8 * BK) variant = 5;  // the staggered prologue assumes >= 8 K-tiles
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
-  if (variant == 11) {
+  if (variant == 12 || variant == 13) {
+    void* args[] = {(void*)d, (void*)&mx};
+    const void* const* kt = variant == 12 ? k12 : k13;
+    const hipError_t le = hipLaunchKernel(kt[d->epilogue], dim3(tiles), dim3(NTHREADS), args, LDS_BYTES,
+                                          (hipStream_t)stream);
+    if (le != hipSuccess) return (int)le;
+  } else if (variant == 11) {
     void* args[] = {(void*)d, (void*)&mx};
     const hipError_t le = hipLaunchKernel(k11[d->epilogue], dim3(tiles), dim3(NTHREADS), args, LDS_BYTES,
                                           (hipStream_t)stream);
