@@ -135,13 +135,14 @@ def test_set_adapters_weights_and_fuse(tmp_path):
     assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), want.state_dict().values()))
 
 
-def test_trainable_adapter_fold_sync_and_factor_grads():
-    """add_adapter (PEFT's LoraConfig on to_q/k/v/out.0): factors under PEFT's saved names, base frozen, B = 0 so the
-    folded weights equal the base; an in-place factor update re-folds W0 + (alpha/r) B A before the next forward;
-    the factor gradients from dW match autograd of that expression."""
+def test_trainable_adapter_runs_unfused_on_augmented_operands():
+    """add_adapter (PEFT's LoraConfig on to_q/k/v/out.0): factors under PEFT's saved names, base frozen, B = 0; the
+    adapter is never folded (W stays W0 after a factor update: the delta is added in output space, as PEFT's
+    unfused forward does); the projection's K-augmented operands [x | x A^T] x [W0 | s B]^T equal
+    x W0^T + s (x A^T) B^T, with the factors of q / k / v in their own rank blocks."""
     import torch
     from videopainter_amd import CogVideoXTransformer3DModel
-    from videopainter_amd.lora import lora_factor_grads, sync_trainable_lora_
+    from videopainter_amd.lora import AUG_ALIGN, AugmentedProjection, trainable_pair
     from tests.golden.cases import TINY_CFG
     tr = CogVideoXTransformer3DModel(**TINY_CFG)
     tr.init_synthetic_weights_(3)
@@ -152,24 +153,35 @@ def test_trainable_adapter_fold_sync_and_factor_grads():
     assert len(train) == 8 * L
     assert set(tr.get_lora_state_dict()) == set(train)
     assert "transformer_blocks.0.attn1.to_out.0.lora_B.weight" in train
-    lin = tr.transformer_blocks[0].attn1.to_q
+    a = tr.transformer_blocks[0].attn1
+    lin = a.to_q
     assert lin.lora_A.weight.shape == (4, lin.weight.shape[1]) and lin.lora_B.weight.shape == (lin.weight.shape[0], 4)
     assert torch.count_nonzero(lin.lora_B.weight) == 0 and torch.count_nonzero(lin.lora_A.weight) > 0
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for l in (a.to_q, a.to_k, a.to_v):
+            l.lora_B.weight.copy_(torch.randn(l.lora_B.weight.shape, generator=g) * 0.1)
     for n, p in tr.named_parameters():
         if n in w0:
-            assert torch.equal(p, w0[n]), n
+            assert torch.equal(p, w0[n]), n   # never folded
+    A, B, s = trainable_pair(lin)
+    assert A is lin.lora_A.weight and B is lin.lora_B.weight and s == 2.0
+    tr._call_lora_scale({"scale": 0.5})
+    assert trainable_pair(lin)[2] == 1.0
+    tr._call_lora_scale({"scale": 1.0})
+    aug = AugmentedProjection.of((a.to_q, a.to_k, a.to_v))
+    assert aug.R == 12 and aug.Rp == AUG_ALIGN and aug.offs == [0, 4, 8]
+    x = torch.randn(16, aug.K, generator=g)
+    xa = torch.cat([x, x @ aug.a_cat().float().t()], 1)
+    for l, w in zip((a.to_q, a.to_k, a.to_v), aug.weights()):
+        assert w.shape == (l.weight.shape[0], aug.K + aug.Rp)
+        want = x @ l.weight.float().t() + 2.0 * (x @ l.lora_A.weight.float().t()) @ l.lora_B.weight.float().t()
+        got = xa @ w.float().t()
+        assert torch.allclose(got, want, rtol=2e-2, atol=2e-2), (got - want).abs().max()
+    # an in-place factor update (the optimizer step) rebuilds the cached operands
+    w_before = aug.weights()[0]
     with torch.no_grad():
-        lin.lora_B.weight.normal_(0, 0.1)
-    assert sync_trainable_lora_(tr) == 1
-    want = (w0["transformer_blocks.0.attn1.to_q.weight"].float()
-            + 2.0 * lin.lora_B.weight.float() @ lin.lora_A.weight.float()).to(lin.weight.dtype)
-    assert torch.equal(lin.weight, want)
-    assert sync_trainable_lora_(tr) == 0
-    # dA = s B^T dW, dB = s dW A^T against autograd
-    A = lin.lora_A.weight.detach().float().requires_grad_()
-    B = lin.lora_B.weight.detach().float().requires_grad_()
-    G = torch.randn(lin.weight.shape)
-    (w0["transformer_blocks.0.attn1.to_q.weight"].float() + 2.0 * B @ A).mul(G).sum().backward()
-    dA, dB = lora_factor_grads(lin, G)
-    assert torch.allclose(dA.float(), A.grad.to(dA.dtype).float(), rtol=2e-2, atol=1e-3)
-    assert torch.allclose(dB.float(), B.grad.to(dB.dtype).float(), rtol=2e-2, atol=1e-3)
+        lin.lora_B.weight.add_(1.0)
+    w_after = AugmentedProjection.of((a.to_q, a.to_k, a.to_v)).weights()[0]
+    assert w_after is not w_before and not torch.equal(w_after, w_before)
+    assert AugmentedProjection.of((tr.transformer_blocks[0].ff.net[0].proj,)) is None

@@ -271,8 +271,8 @@ def test_resample_lora_training_step_matches_oracle():
     LoRA (r 4, alpha 8) added on to_q / to_k / to_v / to_out.0 of the frozen transformer, resample processor
     (id_pool_resample_learnable, window 0), frozen branch samples injected under the mask, backward of a random
     cotangent: the output and every LoRA factor's gradient against the oracle's autograd of
-    W = W0 + (alpha / r) B A.  Then an in-place update of the factors (what the optimizer step does) re-folds the
-    weights before the next forward."""
+    W = W0 + (alpha / r) B A (our adapters run unfused: the projections on K-augmented operands).  Then an in-place
+    update of the factors (what the optimizer step does) reaches the next forward through the rebuilt operands."""
     from oracle import cogvideox_oracle as O
     from videopainter_amd.config import full_config
     from videopainter_amd import CogVideoXTransformer3DModel, device_scope
@@ -343,3 +343,50 @@ def test_resample_lora_training_step_matches_oracle():
     o2_32 = oracle(torch.float32, facs, grad=False)[0]
     o2_16 = oracle(torch.bfloat16, facs, grad=False)[0]
     _check("output after the factor update", out2, o2_32, o2_16)
+
+
+def test_unfused_lora_keeps_a_sub_ulp_factor_update():
+    """PEFT applies a trainable adapter unfused (y = x W0^T + s (x A^T) B^T), so a factor update far below a bf16
+    ulp of W0 still moves the projection.  Weights of magnitude 1 (ulp 2^-7) with s B A = 2e-3 per element: folding
+    would leave W0 bit-identical (the update is < half an ulp), while the augmented GEMM adds the delta
+    s (x A^T) B^T (~0.25, several output ulps) in fp32.  q / k / v of the fused QKV and to_out.0 against fp32."""
+    from videopainter_amd import CogVideoXTransformer3DModel, device_scope
+    from videopainter_amd.attention_processor import _qkv, project_out
+    with device_scope(dev):
+        tr = CogVideoXTransformer3DModel(**TINY_CFG)
+    tr.init_synthetic_weights_(5)
+    tr.add_adapter({"r": 4, "lora_alpha": 8, "target_modules": ["to_q", "to_k", "to_v", "to_out.0"]})
+    a = tr.transformer_blocks[0].attn1
+    g = torch.Generator().manual_seed(11)
+    lins = (a.to_q, a.to_k, a.to_v, a.to_out[0])
+    D = a.to_q.weight.shape[1]
+    sgn = torch.where(torch.rand(D, generator=g) < 0.5, -1.0, 1.0)
+    with torch.no_grad():
+        for l in lins:
+            l.weight.copy_(torch.where(torch.rand(l.weight.shape, generator=g) < 0.5, -1.0, 1.0))
+            l.bias.zero_()
+            A = torch.zeros_like(l.lora_A.weight, device="cpu")
+            A[0] = sgn
+            l.lora_A.weight.copy_(A)
+            l.lora_B.weight.fill_(1e-3)   # s B A = 2 * 1e-3 * (+-1): a quarter of W0's ulp
+    x = (sgn[None, :] * (0.5 + torch.rand(64, D, generator=g))).to(torch.bfloat16)
+
+    def want(l):
+        xf = x.float()
+        return xf @ l.weight.float().cpu().t() + 2.0 * (xf @ l.lora_A.weight.float().cpu().t()) @ \
+            l.lora_B.weight.float().cpu().t()
+
+    q = _qkv(a, x.view(1, 64, D).to(dev)).view(64, 3, -1)
+    o = torch.empty(64, a.to_out[0].weight.shape[0], device=dev, dtype=torch.bfloat16)
+    project_out(a.to_out[0], x.to(dev), o)
+    torch.cuda.synchronize()
+    for got, l in ((q[:, 0], a.to_q), (q[:, 1], a.to_k), (q[:, 2], a.to_v), (o, a.to_out[0])):
+        w = want(l)
+        base = x.float() @ l.weight.float().cpu().t()
+        delta = (w - base).abs().mean().item()
+        assert delta > 0.2, delta
+        err = (got.float().cpu() - w).abs()
+        # bf16 output rounding (relative 2^-9) plus the bf16 T = x A^T and s B: far below the delta a fold loses
+        assert bool((err <= w.abs() * 2.0 ** -8 + 0.01).all()), err.max().item()
+        assert err.mean().item() < 0.25 * delta, (err.mean().item(), delta)
+        assert ((got.float().cpu() - base).abs().mean().item()) > 0.5 * delta

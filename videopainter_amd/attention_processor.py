@@ -21,6 +21,7 @@ import torch.nn as nn
 
 from . import _native as NAT
 from . import kernels as K
+from .lora import AugmentedProjection
 from .modules import Dropout, LayerNorm, Linear
 
 BF16 = torch.bfloat16
@@ -101,11 +102,15 @@ def _qkv(attn, x: torch.Tensor, norm_rope=None) -> torch.Tensor:
                       dtype=BF16)
     ws = [attn.to_q.weight, attn.to_k.weight, attn.to_v.weight]
     bs = [attn.to_q.bias, attn.to_k.bias, attn.to_v.bias]
+    a = x.reshape(-1, D)
+    aug = AugmentedProjection.of((attn.to_q, attn.to_k, attn.to_v))
+    if aug is not None:  # trainable LoRA factors, unfused (lora.AugmentedProjection)
+        a, ws = aug.input(a), aug.weights()
     if norm_rope is None:
-        K.gemm(x.reshape(-1, D), ws, bs, out.view(B * Ntok, -1))
+        K.gemm(a, ws, bs, out.view(B * Ntok, -1))
     else:
         text_len, rope = norm_rope
-        K.gemm(x.reshape(-1, D), ws, bs, out.view(B * Ntok, -1), epilogue=NAT.EPI_BIAS_QKNORM_ROPE,
+        K.gemm(a, ws, bs, out.view(B * Ntok, -1), epilogue=NAT.EPI_BIAS_QKNORM_ROPE,
                qk_norm=(attn.norm_q, attn.norm_k), rope=rope, tokens_per_batch=Ntok, text_len=text_len)
     return out
 
@@ -113,9 +118,22 @@ def _qkv(attn, x: torch.Tensor, norm_rope=None) -> torch.Tensor:
 def _kv(attn, x: torch.Tensor) -> torch.Tensor:
     B, Ntok, D = x.shape
     out = torch.empty(B, Ntok, 2 * D, device=x.device, dtype=BF16)
-    K.gemm(x.reshape(-1, D), [attn.to_k.weight, attn.to_v.weight], [attn.to_k.bias, attn.to_v.bias],
-           out.view(B * Ntok, -1))
+    a, ws = x.reshape(-1, D), [attn.to_k.weight, attn.to_v.weight]
+    aug = AugmentedProjection.of((attn.to_k, attn.to_v))
+    if aug is not None:
+        a, ws = aug.input(a), aug.weights()
+    K.gemm(a, ws, [attn.to_k.bias, attn.to_v.bias], out.view(B * Ntok, -1))
     return out
+
+
+def project_out(lin, o2d: torch.Tensor, out2d: torch.Tensor, **gemm_kw) -> torch.Tensor:
+    """to_out.0 on [M, D] rows with any GEMM epilogue (the block's gated residual), its trainable LoRA factor pair
+    applied unfused (lora.AugmentedProjection) when it carries one."""
+    a, ws = o2d, [lin.weight]
+    aug = AugmentedProjection.of((lin,))
+    if aug is not None:
+        a, ws = aug.input(o2d), aug.weights()
+    return K.gemm(a, ws, [lin.bias], out2d, **gemm_kw)
 
 
 def _fusable_norms(attn) -> bool:
@@ -217,7 +235,8 @@ class CogVideoXAttnProcessor2_0:
         x = torch.cat([encoder_hidden_states, hidden_states], dim=1).to(BF16).contiguous()
         o = self.attend(attn, x, t, image_rotary_emb, prev_hidden_states, prev_clip_weight, resample_mask,
                         prev_resample_mask)
-        out = K.linear(o, attn.to_out[0].weight, attn.to_out[0].bias)
+        out = torch.empty_like(o)
+        project_out(attn.to_out[0], o.view(-1, o.shape[-1]), out.view(-1, o.shape[-1]))
         return out[:, t:], out[:, :t]
 
 

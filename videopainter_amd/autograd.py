@@ -27,7 +27,8 @@ resample processor (window 0: attention over [K; LN(mask . k) + RoPE] and [V; ma
 attention_processor.py:2223-2304) is differentiable — the backward recomputes both segments explicitly, runs the
 flash backward over all 2N keys and routes the second segment's gradients back through the masked copy (masked rows
 to k / v, the null keys' to the norm_k affine) — and trainable LoRA factors on to_q / to_k / to_v / to_out.0
-(`transformer.add_adapter`, lora.py) get dA = s B^T dW, dB = s dW A^T from each folded weight's gradient.
+(`transformer.add_adapter`, lora.py) run unfused like PEFT's, on K-augmented operands (lora.AugmentedProjection):
+dA = dT^T x and dB = s dy^T T from the augmented projection's gradients (dT = s dy B, T = x A^T).
 Out of scope for the backward (NotImplementedError): the fp8 modes, the previous-clip blend (windows > 0) and
 `return_hidden_states` — inference-only in the reference.
 """
@@ -40,7 +41,8 @@ import torch
 from . import _native as NAT
 from . import kernels as K
 from .attention_processor import bounded_scores
-from .lora import has_trainable_lora, lora_factor_grads
+from .attention_processor import project_out
+from .lora import AugmentedProjection
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -73,6 +75,54 @@ def _qkv_t(attn) -> torch.Tensor:
         c = (key, wt)
         attn._vp_qkv_t = c
     return c[1]
+
+
+def _aug_tail_t(aug: AugmentedProjection) -> torch.Tensor:
+    """[Rp, sum out_i] = cat(W_aug_i[:, K:])^T = cat(s B_i, zero-padded)^T (cached on the first Linear, keyed like the
+    augmented weights)."""
+    ws = aug.weights()
+    key = tuple(id(l) for l in aug.lins) + aug._key()
+    owner = aug.lins[0]
+    c = owner.__dict__.get("_vp_aug_tail_t")
+    if c is None or c[0] != key:
+        n = sum(w.shape[0] for w in ws)
+        wt = torch.empty(aug.Rp, n, device=ws[0].device, dtype=BF16)
+        off = 0
+        for w in ws:
+            K.transpose(w[:, aug.K:], out=wt[:, off:off + w.shape[0]])
+            off += w.shape[0]
+        c = (key, wt)
+        owner.__dict__["_vp_aug_tail_t"] = c
+    return c[1]
+
+
+def _aug_dgrad(aug: AugmentedProjection, dy2: torch.Tensor, x2: torch.Tensor, out2: torch.Tensor, train: bool,
+               G: "_Grads", dw_aug: Optional[torch.Tensor] = None) -> None:
+    """Backward of the unfused-LoRA projection y = x_aug W_aug^T (lora.AugmentedProjection), given out2 = dy W
+    (the base dgrad): out2 += dT A_cat with dT = dy W_aug[:, K:] (= s dy B per adapter); with train, the factor
+    gradients dB = s (dy^T T) [the tail of dW_aug = dy^T x_aug, passed in as dw_aug, whose head is dW] and
+    dA = dT^T x."""
+    Kd = aug.K
+    M = dy2.shape[0]
+    dT = torch.empty(M, aug.Rp, device=dy2.device, dtype=BF16)
+    K.gemm(dy2, [_aug_tail_t(aug)], [None], dT)
+    dxl = torch.empty(M, Kd, device=dy2.device, dtype=BF16)
+    K.gemm(dT, [aug.a_cat_t()], [None], dxl)  # dT A_cat
+    K.axpy(out2, dxl, out=out2)
+    if train:
+        dA = K.wgrad(dT, x2)  # [Rp, K]
+        row = 0
+        for lin, pr, off in zip(aug.lins, aug.pairs, aug.offs):
+            n = lin.weight.shape[0]
+            if dw_aug is not None:
+                G.put(lin.weight, dw_aug[row:row + n, :Kd])
+            if pr is not None:
+                A, B, sc = pr
+                r = A.shape[0]
+                if dw_aug is not None:
+                    G.put(lin.lora_B.weight, dw_aug[row:row + n, Kd + off:Kd + off + r].float() * sc)
+                G.put(lin.lora_A.weight, dA[off:off + r])
+            row += n
 
 
 def _dgrad(dy2: torch.Tensor, w: torch.Tensor, out2: torch.Tensor) -> torch.Tensor:
@@ -135,13 +185,8 @@ def _check_block_trainable_path(block, resample_mask=None) -> None:
 
 
 def _put_linear_grads(G: _Grads, lin, dw: torch.Tensor) -> None:
-    """The weight gradient of one (possibly LoRA-adapted) projection: to the weight if it trains, to its trainable
-    LoRA factors if it carries them."""
+    """The weight gradient of one projection without a trainable adapter (those go through _aug_dgrad)."""
     G.put(lin.weight, dw)
-    if has_trainable_lora(lin):
-        dA, dB = lora_factor_grads(lin, dw)
-        G.put(lin.lora_A.weight, dA)
-        G.put(lin.lora_B.weight, dB)
 
 
 def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inject_mask: Optional[torch.Tensor],
@@ -166,8 +211,12 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     mod2 = n2.modulation(temb)
     xn = K.adaln_modulate(x, n1.norm.weight, n1.norm.bias, mod1, T, n1.norm.eps)
     qkv = torch.empty(B, Ntok, 3 * D, device=dev, dtype=BF16)
-    K.gemm(xn.view(M, D), [a.to_q.weight, a.to_k.weight, a.to_v.weight], [a.to_q.bias, a.to_k.bias, a.to_v.bias],
-           qkv.view(M, 3 * D))
+    # trainable LoRA factors run unfused: the projections on K-augmented operands (lora.AugmentedProjection)
+    qaug = AugmentedProjection.of((a.to_q, a.to_k, a.to_v))
+    oaug = AugmentedProjection.of((to_out,))
+    xq = xn.view(M, D) if qaug is None else qaug.input(xn.view(M, D))
+    K.gemm(xq, [a.to_q.weight, a.to_k.weight, a.to_v.weight] if qaug is None else qaug.weights(),
+           [a.to_q.bias, a.to_k.bias, a.to_v.bias], qkv.view(M, 3 * D))
     resample = resample_mask is not None
     v = qkv[..., 2 * D:]
     if resample:
@@ -192,8 +241,8 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     lse = torch.empty(B, H, Ntok, device=dev, dtype=F32)
     K.attention(qn, katt, vatt, o, H, scale=a.scale, bounded_scores=bounded_scores(a), lse=lse)
     x_mid = torch.empty_like(x)
-    K.gemm(o.view(M, D), [to_out.weight], [to_out.bias], x_mid.view(M, D), epilogue=NAT.EPI_GATED,
-           resid=x.view(M, D), mod=mod1, gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok, text_len=T)
+    project_out(to_out, o.view(M, D), x_mid.view(M, D), epilogue=NAT.EPI_GATED, resid=x.view(M, D), mod=mod1,
+                gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok, text_len=T)
     xn2 = K.adaln_modulate(x_mid, n2.norm.weight, n2.norm.bias, mod2, T, n2.norm.eps)
     z = torch.empty(M, F4, device=dev, dtype=BF16)
     K.gemm(xn2.view(M, D), [ff0.weight], [ff0.bias], z)
@@ -245,17 +294,23 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     # ---- attention + gated residual 1 ----
     dao = torch.empty(M, D, device=dev, dtype=BF16)
     K.rowscale(g.view(M, D), dao, Ntok, T, mod1, 2, 5)
+    dw_out = None
     if need_dmod:
         ao = torch.empty(M, D, device=dev, dtype=BF16)
-        K.gemm(o.view(M, D), [to_out.weight], [to_out.bias], ao)
+        project_out(to_out, o.view(M, D), ao)
         gate1 = K.colsum(g.view(M, D), ao, tokens_per_batch=Ntok, text_len=T)
         del ao
         if train:
-            _put_linear_grads(G, to_out, K.wgrad(dao, o.view(M, D)))
+            if oaug is None:
+                _put_linear_grads(G, to_out, K.wgrad(dao, o.view(M, D)))
+            else:
+                dw_out = K.wgrad(dao, oaug.input(o.view(M, D)))
             G.put(to_out.bias, _total(dao))
     do = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
     _dgrad(dao, to_out.weight, do.view(M, D))
-    del dao
+    if oaug is not None:
+        _aug_dgrad(oaug, dao, o.view(M, D), do.view(M, D), train and need_dmod, G, dw_out)
+    del dao, dw_out
     dqkv = torch.empty(B, Ntok, 3 * D, device=dev, dtype=BF16)
     dk2 = None
     if resample:
@@ -299,13 +354,18 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     dxn = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
     K.gemm(dqkv.view(M, 3 * D), [_qkv_t(a)], [None], dxn.view(M, D))
     if train:
-        dw = K.wgrad(dqkv.view(M, 3 * D), xn.view(M, D))
+        dw = K.wgrad(dqkv.view(M, 3 * D), xq)
         db = _total(dqkv.view(M, 3 * D))
         for s, lin in enumerate((a.to_q, a.to_k, a.to_v)):
-            _put_linear_grads(G, lin, dw[s * D:(s + 1) * D])
+            if qaug is None:
+                _put_linear_grads(G, lin, dw[s * D:(s + 1) * D])
             G.put(lin.bias, db[s * D:(s + 1) * D])
+        if qaug is not None:
+            _aug_dgrad(qaug, dqkv.view(M, 3 * D), xn.view(M, D), dxn.view(M, D), True, G, dw)
         del dw
-    del dqkv, xn
+    elif qaug is not None:
+        _aug_dgrad(qaug, dqkv.view(M, 3 * D), xn.view(M, D), dxn.view(M, D), False, G)
+    del dqkv, xn, xq
     n1o = dn1 = xh1 = None
     if need_dmod:
         n1o, dn1, xh1 = (torch.empty_like(x) for _ in range(3))

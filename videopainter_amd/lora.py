@@ -119,7 +119,7 @@ class LoraState:
         self.scale: Optional[float] = None
         self.weights: Dict[str, float] = {}   # set_adapters() weights per adapter (1.0 when loaded, 0 = inactive)
         self.fused = False            # fuse_lora(): the folded scale no longer follows the per-call scale
-        self.versions: Dict[str, tuple] = {}  # trainable adapters: (A, B) versions folded per module
+        self.trainable: set = set()   # adapters added by add_trainable_adapter_: applied unfused, never folded
 
 
 def lora_state(model: torch.nn.Module) -> Optional[LoraState]:
@@ -130,21 +130,12 @@ def _fold_module(st: LoraState, mod: str, W: torch.Tensor, scale: float) -> None
     acc = st.base[mod].to(W.device, torch.float32)
     for name, pairs in st.adapters:
         p = pairs.get(mod)
-        if p is None or st.weights.get(name, 1.0) == 0.0:
+        if p is None or st.weights.get(name, 1.0) == 0.0 or name in st.trainable:
             continue
         r = p["A"].shape[0]
         s = scale * st.weights.get(name, 1.0) * (p["alpha"] / r if p.get("alpha") is not None else 1.0)
         acc = acc + s * (p["B"].detach().to(W.device, torch.float32) @ p["A"].detach().to(W.device, torch.float32))
     W.copy_(acc.to(W.dtype))
-    ver = _trainable_versions(st, mod)
-    if ver is not None:
-        st.versions[mod] = ver
-
-
-def _trainable_versions(st: LoraState, mod: str):
-    vs = tuple((p["A"]._version, p["B"]._version) for _, pairs in st.adapters for m, p in pairs.items()
-               if m == mod and isinstance(p["A"], torch.nn.Parameter))
-    return vs or None
 
 
 def _requant_fp8(model) -> None:
@@ -168,25 +159,6 @@ def refold_lora_(model: torch.nn.Module, scale: float) -> int:
     return len(st.base)
 
 
-@torch.no_grad()
-def sync_trainable_lora_(model: torch.nn.Module) -> int:
-    """Re-fold the modules whose trainable adapter factors changed since their last fold (an optimizer step updates
-    lora_A / lora_B in place, which bumps their version).  Returns the number of modules re-folded."""
-    st = lora_state(model)
-    if st is None or not st.versions:
-        return 0
-    mods = None
-    n = 0
-    for mod, ver in list(st.versions.items()):
-        if _trainable_versions(st, mod) != ver:
-            mods = mods or dict(model.named_modules())
-            _fold_module(st, mod, mods[mod].weight, st.scale if st.scale is not None else 1.0)
-            n += 1
-    if n:
-        _requant_fp8(model)
-    return n
-
-
 class LoraFactor(torch.nn.Module):
     """One trainable LoRA factor as PEFT names it: `<module>.lora_A.weight` [r, in] / `<module>.lora_B.weight`
     [out, r] (the keys `get_peft_model_state_dict` saves and `load_lora_weights` reads)."""
@@ -205,8 +177,10 @@ def add_trainable_adapter_(model: torch.nn.Module, r: int, lora_alpha: float, ta
     pair on every Linear whose name ends in one of `target_modules`, PEFT's default init (A kaiming-uniform
     a = sqrt(5), B = 0, so the adapted model starts equal to the base), scaling lora_alpha / r.  The factors are
     registered as `<module>.lora_A.weight` / `.lora_B.weight` parameters; every other parameter of the model is
-    frozen, as PEFT does.  The forward folds W0 + (alpha / r) B A (re-folded whenever an optimizer step changed a
-    factor: `sync_trainable_lora_`); the backward turns the weight gradient into the factors' (autograd.py)."""
+    frozen, as PEFT does.  The adapter runs UNFUSED like PEFT's (y = x W0^T + s (x A^T) B^T, the delta added in
+    output space, so updates far below a bf16 ulp of W0 still reach the forward): the projection GEMM runs on the
+    K-augmented operands [x | x A^T] and [W0 | s B] (`AugmentedProjection`) with its fused epilogue unchanged; the
+    backward splits the augmented gradients into the factors' (autograd.py)."""
     import math
     if r <= 0:
         raise ValueError("LoRA rank must be positive")
@@ -243,6 +217,7 @@ def add_trainable_adapter_(model: torch.nn.Module, r: int, lora_alpha: float, ta
         raise ValueError(f"no module matches target_modules {targets}")
     st.adapters.append((adapter_name, pairs))
     st.weights[adapter_name] = 1.0
+    st.trainable.add(adapter_name)
     refold_lora_(model, st.scale if st.scale is not None else 1.0)
     return len(pairs)
 
@@ -250,26 +225,6 @@ def add_trainable_adapter_(model: torch.nn.Module, r: int, lora_alpha: float, ta
 def trainable_lora_state_dict(model: torch.nn.Module) -> Dict[str, torch.Tensor]:
     """`get_peft_model_state_dict(transformer)`: the trainable factors under PEFT's saved names."""
     return {k: v.detach() for k, v in model.state_dict().items() if ".lora_A.weight" in k or ".lora_B.weight" in k}
-
-
-def has_trainable_lora(lin) -> bool:
-    f = getattr(lin, "lora_A", None)
-    return f is not None and "_vp_lora_train" in lin.__dict__ and (
-        f.weight.requires_grad or lin.lora_B.weight.requires_grad)
-
-
-def lora_factor_grads(lin, dW: torch.Tensor):
-    """(d lora_A, d lora_B) of the trainable adapter on `lin` from the gradient of its folded weight dW [out, in]:
-    W = W0 + s B A with s = call scale x adapter weight x alpha / r gives dA = s B^T dW, dB = s dW A^T (fp32, cast to
-    the factors' dtype)."""
-    st, name, alpha = lin.__dict__["_vp_lora_train"]
-    A, B = lin.lora_A.weight, lin.lora_B.weight
-    r = A.shape[0]
-    s = (st.scale if st.scale is not None else 1.0) * st.weights.get(name, 1.0) * alpha / r
-    g = dW.float()
-    dA = (B.detach().float().t() @ g) * s
-    dB = (g @ A.detach().float().t()) * s
-    return dA.to(A.dtype), dB.to(B.dtype)
 
 
 @torch.no_grad()
@@ -323,3 +278,114 @@ def set_adapter_weights_(model: torch.nn.Module, names, weights=None) -> None:
     st.weights = {n: 0.0 for n in known}
     st.weights.update(dict(zip(names, ws)))
     refold_lora_(model, st.scale if st.scale is not None else 1.0)
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# Trainable adapters, unfused: K-augmented projection operands
+# ------------------------------------------------------------------------------------------------------------------
+
+def trainable_pair(lin):
+    """(A, B, s) of the trainable (unfused) adapter on the Linear `lin`, or None: A [r, in], B [out, r] (the
+    parameters themselves), s = call scale x adapter weight x alpha / r (PEFT's scaling)."""
+    t = lin.__dict__.get("_vp_lora_train")
+    if t is None or getattr(lin, "lora_A", None) is None:
+        return None
+    st, name, alpha = t
+    w = st.weights.get(name, 1.0)
+    if w == 0.0:
+        return None
+    A, B = lin.lora_A.weight, lin.lora_B.weight
+    s = (st.scale if st.scale is not None else 1.0) * w * alpha / A.shape[0]
+    return A, B, s
+
+
+AUG_ALIGN = 64  # the augmented K is padded to whole 64-wide K-tiles of the GEMM (zero columns / rows)
+
+
+class AugmentedProjection:
+    """One GEMM over several projections (the fused QKV, the prev-clip K/V, to_out) whose Linears carry trainable
+    adapters, as PEFT computes them unfused: y_i = x W_i^T + b_i + s_i (x A_i^T) B_i^T, as ONE GEMM on
+    K-augmented operands
+        x_aug = [x | T],  T = x [A_1; A_2; ...]^T  (bf16, zero-padded to a multiple of 64 columns),
+        W_aug_i = [W_i | 0 .. s_i B_i .. 0]        (bf16, s_i B_i in projection i's rank block),
+    so the fused epilogues (qk-norm + RoPE, gated residual) see the adapted projection, and the delta enters in the
+    fp32 accumulator (a factor update far below a bf16 ulp of W still changes the output, which folding it into a
+    bf16 weight loses).  Built per forward from the live factors (cached on their versions and the scale)."""
+
+    def __init__(self, lins):
+        self.lins = list(lins)
+        self.pairs = [trainable_pair(l) for l in self.lins]
+        self.offs = []
+        off = 0
+        for p in self.pairs:
+            self.offs.append(off)
+            off += p[0].shape[0] if p is not None else 0
+        self.R = off
+        self.Rp = (off + AUG_ALIGN - 1) // AUG_ALIGN * AUG_ALIGN
+        self.K = self.lins[0].weight.shape[1]
+
+    @staticmethod
+    def of(lins):
+        """The augmentation of these projections, or None when none carries a trainable adapter."""
+        if not any(trainable_pair(l) is not None for l in lins):
+            return None
+        return AugmentedProjection(lins)
+
+    def _key(self):
+        return tuple((p[0]._version, p[1]._version, p[0].data_ptr(), p[1].data_ptr(), p[2]) if p is not None
+                     else None for p in self.pairs) + tuple((l.weight._version, l.weight.data_ptr())
+                                                            for l in self.lins)
+
+    def a_cat(self) -> torch.Tensor:
+        """[Rp, K] bf16: the A factors stacked (zero rows for the padding)."""
+        owner = self.lins[0]
+        key = ("A", tuple(id(l) for l in self.lins)) + self._key()
+        c = owner.__dict__.get("_vp_aug_A")
+        if c is None or c[0] != key:
+            W = self.lins[0].weight
+            a = torch.zeros(self.Rp, self.K, device=W.device, dtype=torch.bfloat16)
+            for p, o in zip(self.pairs, self.offs):
+                if p is not None:
+                    a[o:o + p[0].shape[0]].copy_(p[0].detach())
+            c = (key, a)
+            owner.__dict__["_vp_aug_A"] = c
+        return c[1]
+
+    def a_cat_t(self) -> torch.Tensor:
+        """[K, Rp] bf16 = a_cat()^T (the dgrad operand of T = x A_cat^T)."""
+        from . import kernels as K
+        owner = self.lins[0]
+        key = ("At", tuple(id(l) for l in self.lins)) + self._key()
+        c = owner.__dict__.get("_vp_aug_At")
+        if c is None or c[0] != key:
+            c = (key, K.transpose(self.a_cat()))
+            owner.__dict__["_vp_aug_At"] = c
+        return c[1]
+
+    def weights(self):
+        """[W_aug_i] bf16 [out_i, K + Rp] (one per Linear)."""
+        out = []
+        key = self._key()
+        for i, (l, p) in enumerate(zip(self.lins, self.pairs)):
+            k = ("W", tuple(id(x) for x in self.lins), i) + key
+            c = l.__dict__.get("_vp_aug_W")
+            if c is None or c[0] != k:
+                W = l.weight.detach()
+                w = torch.zeros(W.shape[0], self.K + self.Rp, device=W.device, dtype=torch.bfloat16)
+                w[:, :self.K].copy_(W)
+                if p is not None:
+                    o = self.offs[i]
+                    w[:, self.K + o:self.K + o + p[0].shape[0]].copy_((p[1].detach().float() * p[2]))
+                c = (k, w)
+                l.__dict__["_vp_aug_W"] = c
+            out.append(c[1])
+        return out
+
+    def input(self, x2d: torch.Tensor) -> torch.Tensor:
+        """x_aug [M, K + Rp] = [x | x A_cat^T] (one GEMM for T)."""
+        from . import kernels as K
+        M = x2d.shape[0]
+        xa = torch.empty(M, self.K + self.Rp, device=x2d.device, dtype=torch.bfloat16)
+        xa[:, :self.K].copy_(x2d)
+        K.gemm(x2d, [self.a_cat()], [None], xa[:, self.K:])
+        return xa

@@ -26,7 +26,7 @@ import torch.nn as nn
 from . import kernels as K
 from . import _native as NAT
 from .attention_processor import (Attention, CogVideoXAttnProcessor2_0, CogVideoXAttnProcessor2_0_resample,
-                                  _rope_dev, _u8)
+                                  _rope_dev, _u8, project_out)
 from .embeddings import joint_sincos_pos_embedding
 from .modules import Conv2dPatch, Dropout, LayerNorm, Linear, ModelMixin, _empty
 
@@ -227,6 +227,9 @@ class CogVideoXBlock(nn.Module):
             self.qkv_mx = None
             return
         a = self.attn1
+        from .lora import trainable_pair
+        if any(trainable_pair(l) is not None for l in (a.to_q, a.to_k, a.to_v)):
+            raise NotImplementedError("fp8 QKV with trainable (unfused) LoRA factors: merge or drop the adapter first")
         ws = (a.to_q.weight, a.to_k.weight, a.to_v.weight)
         if any(w.shape[0] % 256 or w.shape[1] % 128 for w in ws):
             raise ValueError("fp8 QKV needs widths that are multiples of 256")
@@ -285,9 +288,8 @@ class CogVideoXBlock(nn.Module):
         del qkv
         del xn, pn
         x_mid = torch.empty_like(x)
-        to_out = self.attn1.to_out[0]
-        K.gemm(o.view(B * Ntok, D), [to_out.weight], [to_out.bias], x_mid.view(B * Ntok, D), epilogue=NAT.EPI_GATED,
-               resid=xf, mod=mod1, gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok, text_len=text_len)
+        project_out(self.attn1.to_out[0], o.view(B * Ntok, D), x_mid.view(B * Ntok, D), epilogue=NAT.EPI_GATED,
+                    resid=xf, mod=mod1, gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok, text_len=text_len)
         del o
         mod2 = self.norm2.modulation(temb)
         ff0 = self.ff.net[0].proj
@@ -440,11 +442,10 @@ class CogVideoXTransformer3DModel(ModelMixin):
         return trainable_lora_state_dict(self)
 
     def _call_lora_scale(self, attention_kwargs):
-        from .lora import lora_state, sync_trainable_lora_
+        from .lora import lora_state
         st = lora_state(self)
         if st is None:
             return
-        sync_trainable_lora_(self)  # trainable factors changed by an optimizer step since the last fold
         if st.fused:
             return
         s = attention_kwargs.get("scale", 1.0) if attention_kwargs else 1.0
