@@ -383,9 +383,46 @@ def transformer_forward(sd: SD, cfg: dict, hidden_states, encoder_hidden_states,
     return (out,)
 
 
+def layer_norm_zero_wo_text(sd: SD, p: str, h, temb, eps):
+    """`CogVideoXLayerNormZero.forward_wo_text` DF/models/normalization.py:381-386 (the video chunks only)."""
+    shift, scale, gate, _, _, _ = linear(F.silu(temb), sd, p + ".linear").chunk(6, dim=1)
+    h = layer_norm(h, sd, p + ".norm", eps) * (1 + scale)[:, None, :] + shift[:, None, :]
+    return h, gate[:, None, :]
+
+
+def attn_wo_text(sd: SD, p: str, heads: int, h, rope):
+    """`CogVideoXAttnProcessor2_0_wo_text.__call__` DF/models/attention_processor.py:2306-2366: self-attention over
+    the video tokens alone, RoPE on every token."""
+    b = h.shape[0]
+    q = _heads(linear(h, sd, p + ".to_q"), b, heads)
+    k = _heads(linear(h, sd, p + ".to_k"), b, heads)
+    v = _heads(linear(h, sd, p + ".to_v"), b, heads)
+    q = layer_norm(q, sd, p + ".norm_q", 1e-6)
+    k = layer_norm(k, sd, p + ".norm_k", 1e-6)
+    if rope is None:
+        # the reference computes the attention inside its `if image_rotary_emb is not None:` (:2349-2356): without
+        # RoPE its input goes on to the head merge (:2358, transpose(1, 2) of a [B, N, D] tensor) and to_out
+        return linear(h.transpose(1, 2).reshape(b, -1, h.shape[-1]), sd, p + ".to_out.0")
+    q = apply_rotary_emb(q, *rope)
+    k = apply_rotary_emb(k, *rope)
+    o = F.scaled_dot_product_attention(q, k, v)
+    o = o.transpose(1, 2).reshape(b, -1, q.shape[1] * q.shape[3])
+    return linear(o, sd, p + ".to_out.0")
+
+
+def block_forward_wo_text(sd: SD, p: str, cfg: dict, h, temb, rope):
+    """`CogVideoXBlock.forward_wo_text` DF/models/transformers/cogvideox_transformer_3d.py:186-216."""
+    eps = cfg.get("norm_eps", 1e-5)
+    nh, gate = layer_norm_zero_wo_text(sd, p + ".norm1", h, temb, eps)
+    h = h + gate * attn_wo_text(sd, p + ".attn1", cfg["num_attention_heads"], nh, rope)
+    nh, gate_ff = layer_norm_zero_wo_text(sd, p + ".norm2", h, temb, eps)
+    return h + gate_ff * feed_forward(sd, p + ".ff", nh)
+
+
 def branch_forward(sd: SD, cfg: dict, hidden_states, encoder_hidden_states, branch_cond, timestep,
-                   image_rotary_emb=None, conditioning_scale=1.0):
-    """`CogvideoXBranchModel.forward` DF/models/branch_cogvideox.py:295-434 (wo_text=False).  Returns the list."""
+                   image_rotary_emb=None, conditioning_scale=1.0, wo_text=False):
+    """`CogvideoXBranchModel.forward` DF/models/branch_cogvideox.py:295-434 (wo_text: the blocks' forward_wo_text on
+    the video tokens, :400-412; the text embedding is computed and left unused, :362-366).  Returns the list."""
     dtype = hidden_states.dtype
     inner = cfg["num_attention_heads"] * cfg["attention_head_dim"]
     emb = time_embed(sd, timestep, inner, dtype)
@@ -395,7 +432,10 @@ def branch_forward(sd: SD, cfg: dict, hidden_states, encoder_hidden_states, bran
     nl = len([k for k in sd if k.endswith(".norm1.linear.weight") and k.startswith("transformer_blocks.")])
     samples = []
     for i in range(nl):
-        h, e = block_forward(sd, f"transformer_blocks.{i}", cfg, h, e, emb, image_rotary_emb)
+        if wo_text:
+            h = block_forward_wo_text(sd, f"transformer_blocks.{i}", cfg, h, emb, image_rotary_emb)
+        else:
+            h, e = block_forward(sd, f"transformer_blocks.{i}", cfg, h, e, emb, image_rotary_emb)
         samples.append(h)
     outs = [linear(s, sd, f"branch_blocks.{j}") for j, s in enumerate(samples)]
     return [(o * conditioning_scale).to(dtype) for o in outs]

@@ -11,6 +11,7 @@ Fixtures (all fp32):
   tiny_*.safetensors    — tiny config (2 heads x 64, 4 layers, 2-layer branch, latent 3x16x24, T=8), the branch,
                           the transformer in std / mask-less / add_first / ID-resample (window 0 and prev-window) /
                           prev-clip modes.
+  wo_text.safetensors   — the tiny branch with wo_text=True (blocks on the video tokens alone), fp32 and bf16.
   sched.safetensors     — CogVideoXDPMScheduler: trailing timesteps, 3 steps incl. the 2nd-order branch, add_noise.
   pipe_tiny.safetensors — CogVideoXI2VDualInpaintAnyLPipeline, tiny model + tiny VAE, 2 windows x 2 steps, ID-resample
                           with prev_clip_weight 0.5: the VAE-side latents it produced (captured), every scheduler noise
@@ -122,6 +123,27 @@ def make_tiny():
             return_dict=False)[0]
     out["resample1.out"] = o
     _save("tiny.safetensors", out)
+
+
+@torch.no_grad()
+def make_wo_text():
+    """The tiny branch built and run with wo_text=True (branch_cogvideox.py:74,123,400-412: the blocks' forward_wo_text
+    and CogVideoXAttnProcessor2_0_wo_text), fp32 and the reference's own bf16 run."""
+    from diffusers.models.branch_cogvideox import CogvideoXBranchModel
+    inp = tiny_inputs()
+    _, bsd = tiny_weights()
+    out = {}
+    for dt, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+        br = CogvideoXBranchModel(**dict(TINY_BRANCH_CFG, wo_text=True)).eval()
+        br.load_state_dict({k: torch.from_numpy(v) for k, v in bsd.items()}, strict=True)
+        br = br.to(dt)
+        rope = tuple(r.to(dt) for r in inp["rope"])
+        bs = br(hidden_states=inp["video"].to(dt), encoder_hidden_states=inp["enc"].to(dt),
+                branch_cond=inp["branch_cond"].to(dt), timestep=inp["timestep"], image_rotary_emb=rope,
+                wo_text=True, return_dict=False)[0]
+        for j, s in enumerate(bs):
+            out[f"wo_text.{tag}.{j}"] = s
+    _save("wo_text.safetensors", out)
 
 
 @torch.no_grad()
@@ -568,6 +590,8 @@ def make_t5():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["tiny", "sched", "pipe", "block"]
+    if "wo_text" in which:
+        make_wo_text()
     if "config1" in which:
         make_config1()
     if "config2" in which:

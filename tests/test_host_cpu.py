@@ -122,3 +122,27 @@ def test_fuse_qkv_projections_is_a_documented_no_op():
         assert list(after) == list(before) and all(torch.equal(after[k], before[k]) for k in before)
         m.unfuse_qkv_projections()
         assert m.attn_processors == procs
+
+
+def test_branch_wo_text_construction():
+    """wo_text (branch_cogvideox.py:74,123,263-269): the flag reaches the config and every block's processor, and
+    from_transformer carries it; the forward's mode check runs before any device work."""
+    import pytest
+    import torch
+    from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel
+    from videopainter_amd.attention_processor import CogVideoXAttnProcessor2_0_wo_text
+    from tests.golden.cases import TINY_CFG, TINY_BRANCH_CFG
+    br = CogvideoXBranchModel(**dict(TINY_BRANCH_CFG, wo_text=True))
+    assert br.config.wo_text is True and br.wo_text
+    assert all(isinstance(b.attn1.processor, CogVideoXAttnProcessor2_0_wo_text) and b.wo_text
+               for b in br.transformer_blocks)
+    tr = CogVideoXTransformer3DModel(**TINY_CFG)
+    tr.init_synthetic_weights_(2)
+    b2 = CogvideoXBranchModel.from_transformer(tr, num_layers=2, attention_head_dim=64, num_attention_heads=2,
+                                               wo_text=True)
+    assert b2.config.wo_text is True and all(b.wo_text for b in b2.transformer_blocks)
+    assert not any(b.wo_text for b in CogvideoXBranchModel(**TINY_BRANCH_CFG).transformer_blocks)
+    x = torch.zeros(1, 3, 16, 16, 24)
+    with pytest.raises(ValueError):
+        b2(hidden_states=x, encoder_hidden_states=torch.zeros(1, 8, 32), branch_cond=torch.zeros(1, 3, 17, 16, 24),
+           timestep=torch.tensor([10]), image_rotary_emb=None, wo_text=True)

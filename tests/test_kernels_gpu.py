@@ -1,5 +1,7 @@
 """Numerics of each HIP kernel against a plain-PyTorch fp32 reference of the same op (GPU only)."""
 
+import math
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -414,7 +416,8 @@ def test_gemm_qknorm_rope_epilogue_matches_separate_kernels(H, T, rope, gemm_var
 
 @pytest.mark.parametrize("Kk", [512, 640, 3072])
 def test_gemm_staggered_matches_quadrant_pipeline(Kk, monkeypatch):
-    """Variant 11 (the quadrant pipeline with the two wave groups staggered by one barrier) and variant 12 (two
+    """Variant 11 (the quadrant pipeline with the two wave groups staggered by one barrier), variant 13 (the default:
+    11 with each slot's fragment reads before its DMA), variant 12 (two
     32-MFMA phases and one barrier per K-tile) and variant 30 (two workgroups per CU, 256 x 128 tiles, 32-K steps)
     give variant 5's result bit for bit for every epilogue kind — same MFMA order per accumulator — with ragged M, nk = 8 / 10 / 48 K-tiles
     (the steady loop, the 4-tile tail and the shortest staggered prologue), the row remap and the injection."""
@@ -786,4 +789,36 @@ def test_attention_k2_len_and_l_extra(mode, split, monkeypatch):
         ref[b] = (p @ vv) / (p.sum(-1) + torch.exp2(ex - mx))[..., None]
     ref = ref.transpose(1, 2).reshape(B, Nn, D)
     assert torch.isfinite(o.float()).all()
+    assert rel(o, ref) < 1e-2, rel(o, ref)
+
+
+@pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
+@pytest.mark.parametrize("spread", [False, True], ids=["even", "spread"])
+@pytest.mark.parametrize("mode", ["p2a", "a16", "p2", "s16", "lazy"])
+def test_attention_lse_matches_reference(mode, spread, split, monkeypatch):
+    """The softmax statistics the backward reads (lse = log2 sum_k 2^(scale log2e q.k), fp32 [B, H, Nq]) and the
+    output against fp64, per variant.  spread: queries of very different norms in one wave (x0.02 .. x2.5), so an
+    anchored kernel's shared reference point sits far above some queries' scores."""
+    from videopainter_amd import kernels as K
+    need_variant(mode, monkeypatch)
+    if not split:
+        monkeypatch.setenv("VP_ATTN_NO_SPLIT", "1")
+    B, H, Nn = 2, 2, 700
+    D = H * 64
+    q, k, v = (rnd(B, Nn, D, seed=s) * 0.5 for s in (195, 196, 197))
+    if spread:
+        q = q * torch.where(torch.arange(Nn) % 3 == 0, 0.02, 2.5)[None, :, None]
+    q, k, v = (bf(x).to(dev) for x in (q, k, v))
+    kw = attn_kw(mode, q, k)
+    o = torch.empty(B, Nn, D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, Nn, device=dev, dtype=torch.float32)
+    K.attention(q, k, v, o, H, lse=lse, **kw)
+    hd = lambda x: x.double().cpu().reshape(B, -1, H, 64).transpose(1, 2)  # noqa: E731
+    s = (hd(q) @ hd(k).transpose(-1, -2)) * (0.125 * 1.4426950408889634)
+    ref_lse = torch.logsumexp(s * math.log(2.0), -1) / math.log(2.0)
+    ref = (torch.softmax(s * math.log(2.0), -1) @ hd(v)).transpose(1, 2).reshape(B, Nn, D)
+    err = float((lse.double().cpu() - ref_lse).abs().max())
+    bias = float((lse.double().cpu() - ref_lse).mean())
+    print(f"lse {mode} spread={spread} split={split}: max err {err:.2e} mean {bias:.2e} out rel {rel(o, ref):.2e}")
+    assert err < 4e-3, err
     assert rel(o, ref) < 1e-2, rel(o, ref)

@@ -82,6 +82,32 @@ def test_branch_matches_reference(env):
 
 
 @torch.no_grad()
+def test_branch_wo_text_matches_reference(env):
+    """The branch built and run with wo_text=True (branch_cogvideox.py:74,123,400-412; the training scripts'
+    --wo_text) against the reference's fp32 run, gated on the reference's own bf16 run (tests/golden/wo_text)."""
+    from videopainter_amd import CogvideoXBranchModel, device_scope
+    i = env["inp"]
+    g = load_file(os.path.join(GOLD, "wo_text.safetensors"))
+    _, bsd = tiny_weights()
+    with device_scope(dev):
+        br = CogvideoXBranchModel(**dict(TINY_BRANCH_CFG, wo_text=True))
+    br.load_diffusers_state_dict({k: torch.from_numpy(v) for k, v in bsd.items()})
+    kw = dict(hidden_states=_d(i["video"]), encoder_hidden_states=_d(i["enc"]), branch_cond=_d(i["branch_cond"]),
+              timestep=i["timestep"].to(dev), image_rotary_emb=i["rope"], return_dict=False)
+    bs = br(wo_text=True, **kw)[0]
+    for j in range(2):
+        want, ref16 = g[f"wo_text.f32.{j}"], g[f"wo_text.bf16.{j}"]
+        assert bs[j].shape == want.shape
+        r, r16 = rel(bs[j], want), rel(ref16, want)
+        print(f"wo_text branch.{j}: HIP {r:.3e} reference bf16 {r16:.3e}")
+        assert r <= gate(r16), (j, r, r16)
+    with pytest.raises(ValueError):
+        br(wo_text=False, **kw)
+    with pytest.raises(ValueError):
+        env["br"](wo_text=True, **kw)
+
+
+@torch.no_grad()
 @pytest.mark.parametrize("mode", ["std", "nomask", "addfirst", "prevclip"])
 def test_transformer_matches_reference(env, mode):
     from oracle import cogvideox_oracle as O

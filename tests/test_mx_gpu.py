@@ -70,8 +70,15 @@ def test_mx_quantize_bit_exact():
     assert float(err.max()) <= float(x.float().abs().max()) * 2 ** -4
 
 
+@pytest.fixture(params=["5", "13"], ids=["gemm8_v5", "gemm8_v13"])
+def gemm8_variant(request, monkeypatch):
+    """fp8 GEMM main loop: 13 (default: the bf16 default's staggered read-first pipeline) or 5 (VP_GEMM8_VARIANT)."""
+    monkeypatch.setenv("VP_GEMM8_VARIANT", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("M,Nn,Kk", [(300, 512, 256), (700, 768, 384), (513, 256, 3072), (256, 512, 1536)])
-def test_gemm_mx_bias(M, Nn, Kk):
+def test_gemm_mx_bias(M, Nn, Kk, gemm8_variant):
     """fp8 GEMM against the fp64 product of the dequantised operands (the only error left is fp32 accumulation and
     the bf16 output rounding); short K runs the pipeline's tail only, K >= 640 its steady state."""
     from videopainter_amd import kernels as K
@@ -88,7 +95,24 @@ def test_gemm_mx_bias(M, Nn, Kk):
     assert rel(out, a.double() @ w.double().T + b.double()) < 6e-2
 
 
-def test_gemm_mx_gelu_to_mx_and_gated():
+def test_gemm_mx_main_loops_bit_identical(monkeypatch):
+    """The two fp8 main loops run the same MFMAs in the same order per accumulator: bit-identical outputs."""
+    from videopainter_amd import kernels as K
+    g = torch.Generator().manual_seed(5)
+    M, Nn, Kk = 1000, 768, 2048
+    a = torch.randn(M, Kk, generator=g).to(torch.bfloat16)
+    w = (torch.randn(Nn, Kk, generator=g) * Kk ** -0.5).to(torch.bfloat16)
+    A, W = K.mx_quantize(a.to(dev)), K.mx_quantize(w.to(dev))
+    outs = []
+    for v in ("5", "13"):
+        monkeypatch.setenv("VP_GEMM8_VARIANT", v)
+        out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
+        K.gemm_mx(A, [W], [None], out)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_gemm_mx_gelu_to_mx_and_gated(gemm8_variant):
     """FF1 (bias + GELU-tanh, output re-quantised to MX in the epilogue) feeding FF2 (gated residual + masked branch
     injection), the fp8 FeedForward of the block."""
     from videopainter_amd import kernels as K

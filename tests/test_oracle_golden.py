@@ -43,6 +43,19 @@ def test_branch(tiny):
         assert rel(s, tiny["gold"][f"branch.{j}"]) < 1e-5
 
 
+def test_branch_wo_text(tiny):
+    """wo_text (branch_cogvideox.py:400-412): the blocks' forward_wo_text on the video tokens alone."""
+    i = tiny["inp"]
+    gold = load_file(os.path.join(GOLD, "wo_text.safetensors"))
+    outs = O.branch_forward(tiny["bsd"], tiny["bcfg"], i["video"], i["enc"], i["branch_cond"], i["timestep"],
+                            i["rope"], wo_text=True)
+    assert len(outs) == TINY_BRANCH_CFG["num_layers"]
+    for j, o in enumerate(outs):
+        assert rel(o, gold[f"wo_text.f32.{j}"]) <= 1e-5, j
+        # a different function of the inputs than the text-conditioned branch
+        assert rel(o, tiny["gold"][f"branch.{j}"]) > 1e-4
+
+
 def test_transformer_std_with_hidden_states(tiny):
     i = tiny["inp"]
     bs = [tiny["gold"]["branch.0"], tiny["gold"]["branch.1"]]

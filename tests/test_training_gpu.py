@@ -106,12 +106,12 @@ def test_head_norm_rope_backward_matches_autograd(K):
 # block and model against the oracle's autograd
 # ------------------------------------------------------------------------------------------------------------------
 
-def _models(train_branch=True):
+def _models(train_branch=True, wo_text=False):
     from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, device_scope
     tsd, bsd = tiny_weights()
     with device_scope(dev):
         tr = CogVideoXTransformer3DModel(**TINY_CFG)
-        br = CogvideoXBranchModel(**TINY_BRANCH_CFG)
+        br = CogvideoXBranchModel(**dict(TINY_BRANCH_CFG, wo_text=wo_text))
     tr.load_diffusers_state_dict({k: torch.from_numpy(v) for k, v in tsd.items()})
     br.load_diffusers_state_dict({k: torch.from_numpy(v) for k, v in bsd.items()})
     br.requires_grad_(train_branch)
@@ -166,18 +166,20 @@ def test_block_backward_matches_oracle():
         _check(n, ours[n], gp32[n], gp16[n])
 
 
-def test_branch_gradients_through_frozen_transformer():
+@pytest.mark.parametrize("wo_text", [False, True], ids=["text", "wo_text"])
+def test_branch_gradients_through_frozen_transformer(wo_text):
     """The training step (train_cogvideox_inpainting_i2v_video.py:1856-1892): branch (trainable) -> samples injected
-    into the frozen transformer under the mask -> output -> backward.  Every branch parameter gradient."""
+    into the frozen transformer under the mask -> output -> backward.  Every branch parameter gradient.  wo_text:
+    the script's --wo_text (:556-558, passed at :1403 and :1864), the branch's blocks on the video tokens alone."""
     from oracle import cogvideox_oracle as O
     from videopainter_amd.config import full_config
-    tr, br, tsd, bsd = _models()
+    tr, br, tsd, bsd = _models(wo_text=wo_text)
     i = tiny_inputs()
     g = torch.Generator().manual_seed(6)
     R = torch.randn(i["video"].shape, generator=g).bfloat16()
     samples = br(hidden_states=i["video"].to(dev).bfloat16(), encoder_hidden_states=i["enc"].to(dev).bfloat16(),
                  branch_cond=i["branch_cond"].to(dev).bfloat16(), timestep=i["timestep"].to(dev),
-                 image_rotary_emb=i["rope"], return_dict=False)[0]
+                 image_rotary_emb=i["rope"], wo_text=wo_text, return_dict=False)[0]
     out = tr(hidden_states=i["hidden"].to(dev).bfloat16(), encoder_hidden_states=i["enc"].to(dev).bfloat16(),
              timestep=i["timestep"].to(dev), image_rotary_emb=i["rope"], branch_block_samples=samples,
              branch_block_masks=i["mask"].to(dev), return_dict=False)[0]
@@ -191,7 +193,7 @@ def test_branch_gradients_through_frozen_transformer():
         tp = {k: torch.from_numpy(v).to(dtype) for k, v in tsd.items()}
         bp = {k: torch.from_numpy(v).to(dtype).requires_grad_(k in trainable) for k, v in bsd.items()}
         s = O.branch_forward(bp, full_config(TINY_BRANCH_CFG, True), i["video"].to(dtype), i["enc"].to(dtype),
-                             i["branch_cond"].to(dtype), i["timestep"], i["rope"])
+                             i["branch_cond"].to(dtype), i["timestep"], i["rope"], wo_text=wo_text)
         o = O.transformer_forward(tp, full_config(TINY_CFG), i["hidden"].to(dtype), i["enc"].to(dtype),
                                   i["timestep"], i["rope"], branch_block_samples=s,
                                   branch_block_masks=i["mask"].to(dtype))[0]

@@ -15,7 +15,8 @@ def __getattr__(name):
     if name in ("CogvideoXBranchModel", "CogvideoxBranchOutput"):
         from . import branch
         return getattr(branch, name)
-    if name in ("CogVideoXAttnProcessor2_0", "CogVideoXAttnProcessor2_0_resample", "Attention"):
+    if name in ("CogVideoXAttnProcessor2_0", "CogVideoXAttnProcessor2_0_resample", "CogVideoXAttnProcessor2_0_wo_text",
+                "Attention"):
         from . import attention_processor
         return getattr(attention_processor, name)
     if name in ("CogVideoXDPMScheduler",):

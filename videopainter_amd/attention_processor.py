@@ -240,6 +240,26 @@ class CogVideoXAttnProcessor2_0:
         return out[:, t:], out[:, :t]
 
 
+class CogVideoXAttnProcessor2_0_wo_text(CogVideoXAttnProcessor2_0):
+    """HIP restatement of `CogVideoXAttnProcessor2_0_wo_text.__call__` (attention_processor.py:2306-2366): the
+    branch's text-free mode, self-attention over the video tokens alone with RoPE on every token — `attend` with
+    text_len = 0.  Without RoPE the reference never runs its attention (the call sits inside its
+    `if image_rotary_emb is not None:`, :2349-2356) and projects its scrambled input instead; that form is not
+    restated: no RoPE raises."""
+
+    def __call__(self, attn, hidden_states: torch.Tensor, encoder_hidden_states: Optional[torch.Tensor] = None,
+                 attention_mask: Optional[torch.Tensor] = None, image_rotary_emb=None) -> torch.Tensor:
+        if attention_mask is not None:
+            raise NotImplementedError("attention_mask is never set on the CogVideoX path (SURVEY.md §3.2)")
+        if image_rotary_emb is None:
+            raise ValueError("the wo_text processor attends only with image_rotary_emb (attention_processor.py:2349)")
+        x = hidden_states.to(BF16).contiguous()
+        o = self.attend(attn, x, 0, image_rotary_emb)
+        out = torch.empty_like(o)
+        project_out(attn.to_out[0], o.view(-1, o.shape[-1]), out.view(-1, o.shape[-1]))
+        return out
+
+
 _MASK_PLANS: dict = {}
 
 

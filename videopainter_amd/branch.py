@@ -17,7 +17,7 @@ import torch.nn as nn
 
 from . import kernels as K
 from . import _native as NAT
-from .attention_processor import _rope_dev
+from .attention_processor import CogVideoXAttnProcessor2_0_wo_text, _rope_dev
 from .config import patch_in_channels
 from .modules import Linear
 from .transformer import BF16, CogVideoXTransformer3DModel, _bf
@@ -44,8 +44,12 @@ class CogvideoXBranchModel(CogVideoXTransformer3DModel):
         kw = {k: v for k, v in locals().items() if k not in ("self", "__class__")}
         self._pending_cfg = kw
         super().__init__(**{k: v for k, v in kw.items() if k != "wo_text"})
-        if wo_text:
-            raise NotImplementedError("wo_text branches are not used by the VideoPainter inference scripts")
+        self.wo_text = bool(wo_text)
+        if wo_text:  # the blocks' text-free processor (branch_cogvideox.py:123, cogvideox_transformer_3d.py:96-97)
+            for blk in self.transformer_blocks:
+                blk.wo_text = True
+                blk.processor = CogVideoXAttnProcessor2_0_wo_text()
+                blk.attn1.set_processor(blk.processor)
         inner = num_attention_heads * attention_head_dim
         self.branch_blocks = nn.ModuleList([Linear(inner, inner) for _ in range(num_layers)])
         self.branch_x_embedder = Linear(in_channels, inner)
@@ -114,11 +118,19 @@ class CogvideoXBranchModel(CogVideoXTransformer3DModel):
                 attention_kwargs: Optional[Dict[str, Any]] = None, mask_add: Optional[bool] = False,
                 wo_text: Optional[bool] = False, return_dict: bool = True):
         """branch_cogvideox.py:295-434.  Returns a list of [B, Nv, D] bf16 injection tensors (views of one
-        [B, T + Nv, D] buffer per block; the text rows of that buffer are scratch)."""
+        [B, T + Nv, D] buffer per block; the text rows of that buffer are scratch).  wo_text (:382-412, the training
+        scripts' --wo_text): the blocks run on the video tokens alone (`forward_joint` with no text rows = the
+        reference's `forward_wo_text`: the video AdaLN chunks, attention over the video tokens with RoPE on all of
+        them, the video gates); the text embedding is computed and left unused, as the reference does.  The mode
+        needs a branch built with wo_text=True and the reverse (the reference's blocks fail on either mismatch)."""
         from . import autograd as AG
         train = AG.needs_grad(self, hidden_states, encoder_hidden_states, branch_cond)
-        if wo_text:
-            raise NotImplementedError("wo_text branches are not used by the VideoPainter inference scripts")
+        if bool(wo_text) != self.wo_text:
+            raise ValueError(f"forward(wo_text={bool(wo_text)}) on a branch built with wo_text={self.wo_text} (the "
+                             "reference's blocks take the matching processor at construction, "
+                             "cogvideox_transformer_3d.py:96-97)")
+        if wo_text and image_rotary_emb is None:
+            raise ValueError("wo_text attends only with image_rotary_emb (attention_processor.py:2349)")
         if timestep_cond is not None:
             raise ValueError("timestep_cond requires a cond_proj, which CogVideoX's TimestepEmbedding does not have")
         dev = self.proj_out.weight.device
@@ -135,6 +147,8 @@ class CogvideoXBranchModel(CogVideoXTransformer3DModel):
         if train:
             # the training step's branch call (train_cogvideox_inpainting_i2v_video.py:1856-1865): differentiable
             x = AG.patch_embed_apply(self.patch_embed, enc, hs, bc)
+            if wo_text:
+                x, T = x[:, T:].contiguous(), 0
             outs = []
             for block, lin in zip(self.transformer_blocks, self.branch_blocks):
                 x = AG.block_apply(block, x, T, emb, rope)
@@ -142,6 +156,8 @@ class CogvideoXBranchModel(CogVideoXTransformer3DModel):
             outs = None if len(outs) == 0 else outs
             return (outs,) if not return_dict else CogvideoxBranchOutput(branch_block_samples=outs)
         x = self.patch_embed.embed(enc, hs, bc)
+        if wo_text:  # the video rows alone (one copy per forward); the blocks see no text
+            x, T = x[:, T:].contiguous(), 0
         Ntok = x.shape[1]
         samples = []
         for i, block in enumerate(self.transformer_blocks):

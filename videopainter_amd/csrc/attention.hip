@@ -1151,6 +1151,10 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
       for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fmaxf(r.s[0][i], r.s[1][i]));
 #pragma unroll
       for (int sh = 1; sh < 64; sh <<= 1) mx = fmaxf(mx, __shfl_xor(mx, sh, 64));
+      // rounded up to an integer: P = 2^(S - anchor) is then 2^S with an exact exponent shift (its bf16 rounding and
+      // so every output are those of the unanchored p2 up to the fp32 rounding of S - anchor), independent of which
+      // queries share the wave
+      mx = __builtin_ceilf(mx);
       r.anc = any ? __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(mx))) : -INFINITY;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -1503,7 +1507,7 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
           for (int qt = 0; qt < 4; ++qt) {
             float mx = fmaxf(fmaxf(fmaxf(sc[qt][0][0], sc[qt][0][1]), fmaxf(sc[qt][0][2], sc[qt][0][3])),
                              fmaxf(fmaxf(sc[qt][1][0], sc[qt][1][1]), fmaxf(sc[qt][1][2], sc[qt][1][3])));
-            mx = xmax16(mx);
+            mx = __builtin_ceilf(xmax16(mx));  // an integer reference: exact exponent shifts of 2^S (as p2a's)
             set_ref(qt, mx);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -1588,7 +1592,7 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
       });
       // pass 2: p = exp2(s - max) <= 1 (the max includes l_extra's log mass)
 #pragma unroll
-      for (int qt = 0; qt < 4; ++qt) set_ref(qt, fmaxf(xmax16(mx[qt]), lx[qt]));
+      for (int qt = 0; qt < 4; ++qt) set_ref(qt, __builtin_ceilf(fmaxf(xmax16(mx[qt]), lx[qt])));
       zero_acc();
       tile_loop([&](const char* Kl, const char* Vl, int lim, bool, bool full) {
 #pragma unroll

@@ -1187,9 +1187,11 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   }
   if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
   const MxExt mx = {};
-  // main loops: 11 = the quadrant-phase pipeline with the two wave groups staggered, instantiated per epilogue kind
-  // (default; +5 % over 5 on every config-2 shape), 5 = the unstaggered pipeline (VP_GEMM_VARIANT=5,
-  // A/B; also K < 512), 1 = the 2-stage ring (K % 64 != 0, e.g. the patch-embed im2col K = 132)
+  // main loops: 13 = the quadrant-phase pipeline with the two wave groups staggered and each slot's fragment reads
+  // issued before its DMA, instantiated per epilogue kind (default: +3.6-5.2 % over 11 on every config-2 shape and
+  // 283.7 against 295.4 ms of GEMM per step, profiles/r04_gemm13_ab.log), 11 = the same with the reads after the DMA
+  // (VP_GEMM_VARIANT=11, A/B), 5 = the unstaggered pipeline (A/B; also K < 512), 1 = the 2-stage ring (K % 64 != 0,
+  // e.g. the patch-embed im2col K = 132)
   static const void* const k11[7] = {
       (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS>, (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_GELU>,
       (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_SCALE>, (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_GATED>,
@@ -1220,9 +1222,9 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
     attr_set = true;
   }
   const char* e = getenv("VP_GEMM_VARIANT");  // read per call: tests switch it between launches
-  int variant = e != nullptr ? atoi(e) : 11;
+  int variant = e != nullptr ? atoi(e) : 13;
   if (variant != 1 && variant != 5 && variant != 11 && variant != 12 && variant != 13 && variant != 20 && variant != 30)
-    variant = 11;
+    variant = 13;
   // 30: two workgroups per CU, 256 x 128 tiles (whole 128-column tiles of one weight segment, whole 32-K steps,
   // 32-bit in-tile DMA offsets)
   if (variant == 30) {
@@ -1247,7 +1249,7 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
       VP_CHECK_LAUNCH();
       return VP_OK;
     }
-    variant = 11;
+    variant = 13;
   }
   // 20: the 4-wave AGPR-accumulator kernel (whole 256-column tiles of one weight segment, whole K-tiles, 32-bit
   // in-tile DMA offsets)
@@ -1273,7 +1275,7 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
       VP_CHECK_LAUNCH();
       return VP_OK;
     }
-    variant = 11;
+    variant = 13;
   }
   // the quadrant pipeline adds 32-bit in-tile source offsets to a 64-bit tile base (A) / segment base (W)
   const bool w32 = (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
@@ -1329,7 +1331,7 @@ extern "C" int vp_gemm_bf16_ws(const vp_gemm_desc* d, void* workspace, int64_t w
   mx.kchunk = p.kchunk;
   mx.nsplit = p.nsplit;
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS, true>), dim3(tiles * p.nsplit), dim3(NTHREADS),
+  hipLaunchKernelGGL((gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS, true>), dim3(tiles * p.nsplit), dim3(NTHREADS),
                      LDS_BYTES, (hipStream_t)stream, *d, mx);
   VP_CHECK_LAUNCH();
   const int64_t work = (int64_t)d->M * (d->N / 8);
@@ -1365,24 +1367,35 @@ extern "C" int vp_gemm_mx_fp8(const vp_gemm_mx_desc* x, void* stream) {
   // 32-bit DMA source offsets
   if ((int64_t)d->M * d->lda >= ((int64_t)1 << 31) || (int64_t)d->n_seg * d->K >= ((int64_t)1 << 31)) return VP_ERR_ARG;
   // instantiated per epilogue kind for the block's fp8 GEMMs (QKV: BIAS, FF1: GELU_MXFP8, FF2: GATED); the others
-  // take the runtime switch
+  // take the runtime switch of variant 5
   static const void* const kf[6] = {(const void*)gemm_bf16_kernel<5, true, 4, VP_EPI_BIAS>, nullptr, nullptr,
                                     (const void*)gemm_bf16_kernel<5, true, 4, VP_EPI_GATED>, nullptr,
                                     (const void*)gemm_bf16_kernel<5, true, 4, VP_EPI_BIAS_GELU_MXFP8>};
+  // 13 (default, nk >= 8): the staggered read-first pipeline of the bf16 default on the e4m3 operands — config 5's
+  // fp8 GEMMs 446.7 against 466.3 ms per step with 5 (profiles/r04_c5_gemm8_ab.log); VP_GEMM8_VARIANT=5: the
+  // unstaggered loop (A/B; also nk < 8)
+  static const void* const kf13[6] = {(const void*)gemm_bf16_kernel<13, true, 4, VP_EPI_BIAS>, nullptr, nullptr,
+                                      (const void*)gemm_bf16_kernel<13, true, 4, VP_EPI_GATED>, nullptr,
+                                      (const void*)gemm_bf16_kernel<13, true, 4, VP_EPI_BIAS_GELU_MXFP8>};
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<5, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES_FP8);
     for (const void* f : kf)
       if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES_FP8);
+    for (const void* f : kf13)
+      if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES_FP8);
     attr_set = true;
   }
+  const char* e8 = getenv("VP_GEMM8_VARIANT");  // read per call (A/B)
+  const bool use13 = (e8 == nullptr || atoi(e8) != 5) && d->K / 128 >= 8 && kf13[d->epilogue] != nullptr;
   MxExt mx;
   mx.a_scale = (const uint8_t*)x->a_scale;
   for (int s = 0; s < 3; ++s) mx.w_scale[s] = (const uint8_t*)x->w_scale[s];
   mx.c_scale = (uint8_t*)x->c_scale;
   const int tiles = ((d->M + BM - 1) / BM) * (d->N / BN);
-  const void* fn = kf[d->epilogue] != nullptr ? kf[d->epilogue] : (const void*)gemm_bf16_kernel<5, true>;
+  const void* fn = use13 ? kf13[d->epilogue]
+                   : kf[d->epilogue] != nullptr ? kf[d->epilogue] : (const void*)gemm_bf16_kernel<5, true>;
   void* args[] = {(void*)d, (void*)&mx};
   const hipError_t le = hipLaunchKernel(fn, dim3(tiles), dim3(NTHREADS), args, LDS_BYTES_FP8, (hipStream_t)stream);
   if (le != hipSuccess) return (int)le;

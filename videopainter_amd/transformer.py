@@ -26,6 +26,7 @@ import torch.nn as nn
 from . import kernels as K
 from . import _native as NAT
 from .attention_processor import (Attention, CogVideoXAttnProcessor2_0, CogVideoXAttnProcessor2_0_resample,
+                                  CogVideoXAttnProcessor2_0_wo_text,
                                   _rope_dev, _u8, project_out)
 from .embeddings import joint_sincos_pos_embedding
 from .modules import Conv2dPatch, Dropout, LayerNorm, Linear, ModelMixin, _empty
@@ -193,13 +194,13 @@ class CogVideoXBlock(nn.Module):
         super().__init__()
         if activation_fn != "gelu-approximate":
             raise NotImplementedError(f"activation_fn={activation_fn!r}: CogVideoX uses gelu-approximate")
-        if wo_text:
-            raise NotImplementedError("wo_text branch blocks are not on the VideoPainter inference path")
         if not qk_norm:
             raise NotImplementedError("CogVideoX uses qk_norm=True")
         self.norm1 = CogVideoXLayerNormZero(time_embed_dim, dim, norm_elementwise_affine, norm_eps, bias=True)
-        self.processor = CogVideoXAttnProcessor2_0_resample() if id_pool_resample_learnable else \
-            CogVideoXAttnProcessor2_0()
+        # wo_text (the branch's text-free mode, :96-97): the blocks run `forward_joint` with no text rows
+        self.wo_text = bool(wo_text)
+        self.processor = CogVideoXAttnProcessor2_0_wo_text() if wo_text else \
+            CogVideoXAttnProcessor2_0_resample() if id_pool_resample_learnable else CogVideoXAttnProcessor2_0()
         self.attn1 = Attention(query_dim=dim, dim_head=attention_head_dim, heads=num_attention_heads, eps=1e-6,
                                bias=attention_bias, out_bias=attention_out_bias, processor=self.processor)
         self.norm2 = CogVideoXLayerNormZero(time_embed_dim, dim, norm_elementwise_affine, norm_eps, bias=True)
