@@ -143,6 +143,12 @@ VP_DEV void mfma_mx(f32x4& acc, const i32x8& w, const i32x8& a, int sw, int sa) 
                  : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
 }
 
+#ifndef VP_GEMM_EPI_OLD
+#define VP_GEMM_EPI_OLD 0
+#endif
+#ifndef VP_GEMM_EPI_RPRE
+#define VP_GEMM_EPI_RPRE 0
+#endif
 // ---- fused epilogue shared by the GEMM kernels: acc[j][i] = the 16x16 fragment (W rows j, A rows i) of a wave
 // whose C block is rows wr*WM.., cols wc*WN.. of the BM x BN tile.  Three pieces: epi_values (per-fragment bias /
 // activation / qk-norm in registers -> bf16), epi_to_lds (a wave's values into the LDS C image), epi_rows_out (NT
@@ -171,11 +177,24 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
     if (epi == VP_EPI_BIAS_QKNORM_ROPE && nh < d.N && sgh < 2) {
       const bf16* bp = (const bf16*)d.bias[sgh];
       const int hc = nh - sgh * d.n_seg;  // column within the segment
+      // one 8-byte load per 4 columns, all issued before any use (16 scalar bf16 loads came out of the compiler as
+      // 16 serialised round trips, each behind its own vmcnt(0))
       float bv[16];
+#if VP_GEMM_EPI_OLD  // (A/B build: the round-3 form)
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
         for (int r = 0; r < 4; ++r) bv[4 * jj + r] = bp != nullptr ? bf2f(bp[hc + 16 * jj + 4 * g + r]) : 0.f;
+#else
+      bf16x4 b4[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        b4[jj] = bp != nullptr ? *(const bf16x4*)(bp + hc + 16 * jj + 4 * g) : bf16x4{};
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[4 * jj + r] = bp != nullptr ? bf2f(b4[jj][r]) : 0.f;
+#endif
       // the LayerNorm weight / bias quads once per head; per row fragment the RoPE quads are loaded (from row 0 for
       // text tokens, then not applied) before the reductions, so no load sits on the fragment's critical path
       bf16x4 lw4[4], lb4[4];
@@ -185,18 +204,32 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
         lb4[jj] = *(const bf16x4*)((const bf16*)d.qk_ln_b[sgh] + 16 * jj + 4 * g);
       }
       const bool has_rope = d.rope_cos != nullptr;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
+      // the RoPE quads of row fragment i + 1 are loaded before fragment i's reductions (double-buffered), so their
+      // latency runs under the previous fragment's work instead of in front of each fragment
+      f32x4 csb[2][4], snb[2][4];
+      bool rotb[2];
+      auto load_rope = [&](int i, f32x4 (&cs)[4], f32x4 (&sn)[4], bool& rot) {
         int tok = tok0 + wr * WM + i * 16 + (lane & 15);
         while (tok >= d.tokens_per_batch) tok -= d.tokens_per_batch;
-        const bool rot = has_rope && tok >= d.text_len;
+        rot = has_rope && tok >= d.text_len;
         const int64_t ro = rot ? (int64_t)(tok - d.text_len) * 64 : 0;
-        f32x4 cs[4], sn[4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           cs[jj] = has_rope ? *(const f32x4*)(d.rope_cos + ro + 16 * jj + 4 * g) : (f32x4){1.f, 1.f, 1.f, 1.f};
           sn[jj] = has_rope ? *(const f32x4*)(d.rope_sin + ro + 16 * jj + 4 * g) : (f32x4){0.f, 0.f, 0.f, 0.f};
         }
+      };
+      load_rope(0, csb[0], snb[0], rotb[0]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#if VP_GEMM_EPI_OLD
+        if (i > 0) load_rope(i, csb[i & 1], snb[i & 1], rotb[i & 1]);
+#else
+        if (i + 1 < FM) load_rope(i + 1, csb[(i + 1) & 1], snb[(i + 1) & 1], rotb[(i + 1) & 1]);
+#endif
+        const f32x4(&cs)[4] = csb[i & 1];
+        const f32x4(&sn)[4] = snb[i & 1];
+        const bool rot = rotb[i & 1];
         float x[16];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
@@ -219,16 +252,24 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
       const int nloc = wc * WN + j * 16 + g * 4;  // 4 consecutive columns
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
       {
-        // the 4 columns share a segment (n_seg % 8 == 0)
+        // the 4 columns share a segment (n_seg % 8 == 0) and are all in range or all out (N % 8 == 0, the first
+        // column a multiple of 4): one 8-byte load
         const int sg = seg_of(n0 + nloc);
         const bf16* bp = (const bf16*)d.bias[sg];
+        const int n = n0 + nloc;
+#if VP_GEMM_EPI_OLD
         if (bp != nullptr) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int n = n0 + nloc + r;
-            if (FULL_N || n < d.N) bv[r] = bf2f(bp[n - sg * d.n_seg]);
-          }
+          for (int r = 0; r < 4; ++r)
+            if (FULL_N || n + r < d.N) bv[r] = bf2f(bp[n + r - sg * d.n_seg]);
         }
+#else
+        if (bp != nullptr && (FULL_N || n < d.N)) {
+          const bf16x4 b4 = *(const bf16x4*)(bp + n - sg * d.n_seg);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bv[r] = bf2f(b4[r]);
+        }
+#endif
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
@@ -255,9 +296,9 @@ VP_DEV char* epi_lds_addr(char* img, int j, int i, int row0, int wr, int wc, int
 
 // image rows [0, nrows) = tile rows row0.. out to C (coalesced 16-byte row stores + the row-wise epilogues); BNC:
 // the tile's columns (256, or 128 for the two-workgroups-per-CU kernel)
-template <int NT, bool FP8, int EPI = -1, int BNC = BN>
+template <int NT, bool FP8, int EPI = -1, int BNC = BN, int NPRE = 0>
 VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* smem, int row0, int nrows, int m0,
-                         int n0, int tid) {
+                         int n0, int tid, const bf16x8* rpre = nullptr) {
   constexpr int CPR = BNC / 8;        // 16-byte chunks per tile row
   constexpr int CTS = BNC * 2 + 8;
   const int epi = EPI >= 0 ? EPI : d.epilogue;
@@ -273,7 +314,9 @@ VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* sme
   const int tpb = d.tokens_per_batch;
   const bool need_b = epi == VP_EPI_GATED;
   const int b0 = need_b ? mbase / tpb : 0, tk0 = need_b ? mbase - b0 * tpb : 0;
-#pragma unroll 1
+  // NPRE > 0: the gated epilogue's residual rows were loaded before the LDS image (rpre[it]); the loop is unrolled
+  // so they stay in registers
+#pragma unroll(NPRE > 0 ? NPRE : 1)
   for (int it = 0; it < nrows / (NT / CPR); ++it) {
     const int mloc = it * (NT / CPR) + tid / CPR;
     const int m = mbase + mloc;
@@ -305,7 +348,7 @@ VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* sme
       }
       const bf16* g = (const bf16*)(tok < d.text_len ? d.gate_text : d.gate) + (int64_t)b * d.gate_bstride + ncol;
       const bf16x8 gv = *(const bf16x8*)g;
-      const bf16x8 rv = *(const bf16x8*)((const bf16*)d.R + orow * d.ldr + ncol);
+      const bf16x8 rv = NPRE > 0 ? rpre[it] : *(const bf16x8*)((const bf16*)d.R + orow * d.ldr + ncol);
       bool inj = false;
       bf16x8 iv;
       if (d.inject != nullptr && tok >= d.text_len) {
@@ -337,6 +380,37 @@ VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* sme
 template <int NT, int FN, int FM, int WN, int WM, bool FP8, int EPI = -1>
 VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&acc)[FN][FM], char* smem, int m0,
                           int n0, int wr, int wc, int lane, int tid) {
+#if VP_GEMM_EPI_RPRE
+  if constexpr (EPI == VP_EPI_GATED && !FP8 && NT == NTHREADS) {
+    // the residual rows of this thread's row pass, loaded before the LDS image is written (their latency and the
+    // round's residual burst run under epi_values and the barrier instead of inside the row loop)
+    constexpr int CPR = BN / 8, NPRE = BM / (NT / CPR);
+    bf16x8 rpre[NPRE];
+    const int chunk = tid & (CPR - 1);
+    const int ncol = n0 + chunk * 8;
+    const int rpg = d.rows_per_group;
+    const int grp0 = m0 / rpg, gin0 = m0 - grp0 * rpg;
+#pragma unroll
+    for (int it = 0; it < NPRE; ++it) {
+      const int mloc = it * (NT / CPR) + tid / CPR;
+      int grp = grp0, gin = gin0 + mloc;
+      while (gin >= rpg) {
+        gin -= rpg;
+        ++grp;
+      }
+      const int64_t orow = (int64_t)grp * d.group_stride + d.row_offset + gin;
+      rpre[it] = (m0 + mloc < d.M && ncol < d.N) ? *(const bf16x8*)((const bf16*)d.R + orow * d.ldr + ncol)
+                                                  : bf16x8{};
+    }
+    epi_values<FN, FM, WN, WM, EPI>(
+        d, acc,
+        [&](int j, int i, const bf16x4& o) { *(bf16x4*)epi_lds_addr<WN, WM>(smem, j, i, 0, wr, wc, lane) = o; },
+        m0, n0, wr, wc, lane);
+    __syncthreads();
+    epi_rows_out<NT, FP8, EPI, BN, NPRE>(d, mx, smem, 0, BM, m0, n0, tid, rpre);
+    return;
+  }
+#endif
   epi_values<FN, FM, WN, WM, EPI>(
       d, acc,
       [&](int j, int i, const bf16x4& o) { *(bf16x4*)epi_lds_addr<WN, WM>(smem, j, i, 0, wr, wc, lane) = o; }, m0,

@@ -16,16 +16,73 @@ __global__ __launch_bounds__(LS_THREADS) void linear_small_kernel(const bf16* __
                                                                  int act_out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* xs = (bf16*)smem;  // [M][K] act_in(x), bf16
-  for (int i = threadIdx.x; i < M * K; i += LS_THREADS) {
-    const int m = i / K, k = i - m * K;
-    float v = bf2f(x[(int64_t)m * ldx + k]);
-    if (act_in == 1) v = rbf(silu(v));
-    xs[i] = f2bf(v);
+  if ((K % 8) == 0 && (ldx % 8) == 0 && ((uintptr_t)x & 15) == 0) {  // 16-byte chunks (one load per thread)
+    const int kc = K / 8;
+    for (int i = threadIdx.x; i < M * kc; i += LS_THREADS) {
+      const int m = i / kc, c = i - m * kc;
+      bf16x8 v8 = *(const bf16x8*)(x + (int64_t)m * ldx + c * 8);
+      if (act_in == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v8[e] = f2bf(rbf(silu(bf2f(v8[e]))));
+      }
+      *(bf16x8*)(xs + m * K + c * 8) = v8;
+    }
+  } else {
+    for (int i = threadIdx.x; i < M * K; i += LS_THREADS) {
+      const int m = i / K, k = i - m * K;
+      float v = bf2f(x[(int64_t)m * ldx + k]);
+      if (act_in == 1) v = rbf(silu(v));
+      xs[i] = f2bf(v);
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int nch = K / 8;
+  const int nbase = (blockIdx.x * (LS_THREADS / 64) + wave) * LS_COLS_PER_WAVE;
+  if (nch <= 64 && nbase + LS_COLS_PER_WAVE <= N) {
+    // K <= 512 (the AdaLN / time-embedding linears): one 16-byte chunk per lane and column; the wave's 4 weight
+    // loads are issued together, then the products and the reductions (the loop below takes one load round trip
+    // per column)
+    bf16x8 w[LS_COLS_PER_WAVE];
+    const bool on = lane < nch;
+#pragma unroll
+    for (int cc = 0; cc < LS_COLS_PER_WAVE; ++cc)
+      w[cc] = on ? *(const bf16x8*)(W + (int64_t)(nbase + cc) * K + lane * 8) : bf16x8{};
+    float acc[LS_COLS_PER_WAVE][16];
+#pragma unroll
+    for (int cc = 0; cc < LS_COLS_PER_WAVE; ++cc)
+#pragma unroll
+      for (int m = 0; m < 16; ++m) acc[cc][m] = 0.f;
+    if (on) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        if (m < M) {
+          const bf16x8 xv = *(const bf16x8*)(xs + m * K + lane * 8);
+#pragma unroll
+          for (int cc = 0; cc < LS_COLS_PER_WAVE; ++cc)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[cc][m] = fmaf(bf2f(w[cc][e]), bf2f(xv[e]), acc[cc][m]);
+        }
+      }
+    }
+#pragma unroll
+    for (int cc = 0; cc < LS_COLS_PER_WAVE; ++cc) {
+      const int n = nbase + cc;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        if (m < M) {
+          float s = wave_sum(acc[cc][m]);
+          if (lane == 0) {
+            float v = rbf(s + (bias ? bf2f(bias[n]) : 0.f));
+            if (act_out == 1) v = rbf(silu(v));
+            y[(int64_t)m * ldy + n] = f2bf(v);
+          }
+        }
+      }
+    }
+    return;
+  }
   for (int cc = 0; cc < LS_COLS_PER_WAVE; ++cc) {
     const int n = (blockIdx.x * (LS_THREADS / 64) + wave) * LS_COLS_PER_WAVE + cc;
     if (n >= N) break;
