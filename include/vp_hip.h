@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 12
+#define VP_ABI_VERSION 13
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
@@ -99,6 +99,11 @@ typedef struct vp_gemm_desc {
 } vp_gemm_desc;
 
 int vp_gemm_bf16(const vp_gemm_desc* d, void* stream);
+
+/* 1 when the GEMM main loop VP_GEMM_VARIANT = variant (1, 5, 11, 13 = the default; 12, 20, 30 only in a
+ * VP_GEMM_EXTRA_VARIANTS build: the rejected A/B loops) is in this library, else 0.  Host-only.  vp_gemm_bf16 returns
+ * VP_ERR_UNSUPPORTED for a variant outside the build.  (ABI 13.) */
+int vp_gemm_variant_built(int variant);
 
 /* Split-K form for GEMMs too small to fill the chip (fewer than 128 output tiles of 256 x 256, e.g. the T5 encoder's
  * projections at M = 2 x 226 token rows; reference callers: transformers T5EncoderModel, anyl.py:216-256): the K

@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -105,6 +105,7 @@ _SIGS = {
     "vp_attention_workspace_bytes": (i64, [C.POINTER(AttnDesc)]),
     "vp_attention_fwd_bf16_ws": (i32, [C.POINTER(AttnDesc), vp, i64, vp]),
     "vp_attention_variant_built": (i32, [C.c_char_p]),
+    "vp_gemm_variant_built": (i32, [i32]),
     "vp_v_pack_fp8_bytes": (i64, [i32, i32, i32, C.POINTER(i64), C.POINTER(i64)]),
     "vp_v_pack_fp8": (i32, [vp, i64, i64, i32, i32, i32, vp, vp, vp]),
     "vp_mx_mfma_probe32": (i32, [vp, vp, vp, vp, vp, vp]),

@@ -143,11 +143,13 @@ VP_DEV void mfma_mx(f32x4& acc, const i32x8& w, const i32x8& a, int sw, int sa) 
                  : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
 }
 
-#ifndef VP_GEMM_EPI_OLD
-#define VP_GEMM_EPI_OLD 0
+#ifndef VP_GEMM_EXTRA_VARIANTS
+#define VP_GEMM_EXTRA_VARIANTS 0
 #endif
+// the gated epilogue loads its residual rows before the LDS image (default; 0 = inside the row loop, A/B:
+// profiles/r04_gemm_epi_ab.log, out-projection 0.574-0.582 vs 0.630 ms)
 #ifndef VP_GEMM_EPI_RPRE
-#define VP_GEMM_EPI_RPRE 0
+#define VP_GEMM_EPI_RPRE 1
 #endif
 // ---- fused epilogue shared by the GEMM kernels: acc[j][i] = the 16x16 fragment (W rows j, A rows i) of a wave
 // whose C block is rows wr*WM.., cols wc*WN.. of the BM x BN tile.  Three pieces: epi_values (per-fragment bias /
@@ -180,12 +182,6 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
       // one 8-byte load per 4 columns, all issued before any use (16 scalar bf16 loads came out of the compiler as
       // 16 serialised round trips, each behind its own vmcnt(0))
       float bv[16];
-#if VP_GEMM_EPI_OLD  // (A/B build: the round-3 form)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bv[4 * jj + r] = bp != nullptr ? bf2f(bp[hc + 16 * jj + 4 * g + r]) : 0.f;
-#else
       bf16x4 b4[4];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
@@ -194,7 +190,6 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
       for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
         for (int r = 0; r < 4; ++r) bv[4 * jj + r] = bp != nullptr ? bf2f(b4[jj][r]) : 0.f;
-#endif
       // the LayerNorm weight / bias quads once per head; per row fragment the RoPE quads are loaded (from row 0 for
       // text tokens, then not applied) before the reductions, so no load sits on the fragment's critical path
       bf16x4 lw4[4], lb4[4];
@@ -222,11 +217,7 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
       load_rope(0, csb[0], snb[0], rotb[0]);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-#if VP_GEMM_EPI_OLD
-        if (i > 0) load_rope(i, csb[i & 1], snb[i & 1], rotb[i & 1]);
-#else
         if (i + 1 < FM) load_rope(i + 1, csb[(i + 1) & 1], snb[(i + 1) & 1], rotb[(i + 1) & 1]);
-#endif
         const f32x4(&cs)[4] = csb[i & 1];
         const f32x4(&sn)[4] = snb[i & 1];
         const bool rot = rotb[i & 1];
@@ -257,19 +248,11 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
         const int sg = seg_of(n0 + nloc);
         const bf16* bp = (const bf16*)d.bias[sg];
         const int n = n0 + nloc;
-#if VP_GEMM_EPI_OLD
-        if (bp != nullptr) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (FULL_N || n + r < d.N) bv[r] = bf2f(bp[n + r - sg * d.n_seg]);
-        }
-#else
         if (bp != nullptr && (FULL_N || n < d.N)) {
           const bf16x4 b4 = *(const bf16x4*)(bp + n - sg * d.n_seg);
 #pragma unroll
           for (int r = 0; r < 4; ++r) bv[r] = bf2f(b4[r]);
         }
-#endif
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
@@ -1239,6 +1222,11 @@ SplitPlan split_plan(const vp_gemm_desc* d) {
 
 }  // namespace
 
+extern "C" int vp_gemm_variant_built(int variant) {
+  if (variant == 1 || variant == 5 || variant == 11 || variant == 13) return 1;
+  return (variant == 12 || variant == 20 || variant == 30) && VP_GEMM_EXTRA_VARIANTS ? 1 : 0;
+}
+
 extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   if (d == nullptr || d->A == nullptr || d->W[0] == nullptr || d->C == nullptr) return VP_ERR_ARG;
   if (d->M <= 0 || d->N <= 0 || d->K <= 0 || (d->K % 8) != 0 || (d->N % 8) != 0) return VP_ERR_ARG;
@@ -1276,11 +1264,15 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
       (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_SCALE>, (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_GATED>,
       (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_ADDROWS>, nullptr,
       (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_QKNORM_ROPE>};
+#if VP_GEMM_EXTRA_VARIANTS
   static const void* const k12[7] = {
       (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS>, (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_GELU>,
       (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_SCALE>, (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_GATED>,
       (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_ADDROWS>, nullptr,
       (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_QKNORM_ROPE>};
+#else
+  static const void* const k12[7] = {};
+#endif
   static bool attr_set = false;
   if (!attr_set) {
     for (const void* f : k12)
@@ -1299,6 +1291,10 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   int variant = e != nullptr ? atoi(e) : 13;
   if (variant != 1 && variant != 5 && variant != 11 && variant != 12 && variant != 13 && variant != 20 && variant != 30)
     variant = 13;
+  // the rejected A/B loops (12, 20, 30: profiles/r04_gemm_v12_ab_rejected.log, r04_gemm_v30_ab_rejected.log,
+  // DESIGN.md §3) are built only with -DVP_GEMM_EXTRA_VARIANTS=1 (vp_gemm_variant_built)
+  if (!vp_gemm_variant_built(variant)) return VP_ERR_UNSUPPORTED;
+#if VP_GEMM_EXTRA_VARIANTS
   // 30: two workgroups per CU, 256 x 128 tiles (whole 128-column tiles of one weight segment, whole 32-K steps,
   // 32-bit in-tile DMA offsets)
   if (variant == 30) {
@@ -1351,6 +1347,7 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
     }
     variant = 13;
   }
+#endif
   // the quadrant pipeline adds 32-bit in-tile source offsets to a 64-bit tile base (A) / segment base (W)
   const bool w32 = (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
   const bool tile32 = (int64_t)BM * d->lda * 2 < ((int64_t)1 << 31) && w32;

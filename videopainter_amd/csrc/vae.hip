@@ -225,8 +225,14 @@ __global__ __launch_bounds__(CNT, 2) void conv3d_kernel(const vp_conv3d_desc d, 
     const int n = n0 + wc * G::WN + j * 16 + (lane >> 4) * 4;
     if (n >= d.ldy) continue;
     float bv[4];
+    if (bias != nullptr && n + 3 < d.Cout) {  // one 8-byte load (per-element loads came out as serial round trips)
+      const bf16x4 b4 = *(const bf16x4*)(bias + n);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bv[r] = (bias != nullptr && n + r < d.Cout) ? bf2f(bias[n + r]) : 0.f;
+      for (int r = 0; r < 4; ++r) bv[r] = bf2f(b4[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = (bias != nullptr && n + r < d.Cout) ? bf2f(bias[n + r]) : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < G::FM; ++i) {
       const int64_t m = m0 + wr * G::WM + i * 16 + lrow;
@@ -405,8 +411,14 @@ __global__ __launch_bounds__(PNT, 1) void conv3d_pipe_kernel(const vp_conv3d_des
     const int n = n0 + wc * WN + j * 16 + (lane >> 4) * 4;
     if (n >= d.ldy) continue;
     float bv[4];
+    if (bias != nullptr && n + 3 < d.Cout) {  // one 8-byte load (per-element loads came out as serial round trips)
+      const bf16x4 b4 = *(const bf16x4*)(bias + n);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bv[r] = (bias != nullptr && n + r < d.Cout) ? bf2f(bias[n + r]) : 0.f;
+      for (int r = 0; r < 4; ++r) bv[r] = bf2f(b4[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = (bias != nullptr && n + r < d.Cout) ? bf2f(bias[n + r]) : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int64_t m = m0 + wr * WM + i * 16 + lrow;

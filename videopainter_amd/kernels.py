@@ -386,6 +386,12 @@ def attention_variant_built(name: str) -> bool:
     return bool(N.lib().vp_attention_variant_built(name.encode()))
 
 
+def gemm_variant_built(variant) -> bool:
+    """Is the GEMM main loop VP_GEMM_VARIANT = variant in this library build (the rejected 12 / 20 / 30 need
+    VP_GEMM_EXTRA_VARIANTS=1)?"""
+    return bool(N.lib().vp_gemm_variant_built(int(variant)))
+
+
 def attention_bwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Tensor, do: torch.Tensor,
                   lse: torch.Tensor, heads: int, scale: float = 0.125, dq: Optional[torch.Tensor] = None,
                   dk: Optional[torch.Tensor] = None, dv: Optional[torch.Tensor] = None):
