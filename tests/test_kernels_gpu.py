@@ -825,3 +825,24 @@ def test_attention_lse_matches_reference(mode, spread, split, monkeypatch):
     print(f"lse {mode} spread={spread} split={split}: max err {err:.2e} mean {bias:.2e} out rel {rel(o, ref):.2e}")
     assert err < 4e-3, err
     assert rel(o, ref) < 1e-2, rel(o, ref)
+
+
+@pytest.mark.parametrize("M,K_,act_in,act_out", [(2, 512, 1, 0), (1, 512, 0, 1), (2, 256, 0, 0), (2, 3072, 1, 0)])
+def test_linear_small_fast_path_bit_identical(M, K_, act_in, act_out):
+    """vp_linear_small_bf16's weight-streaming kernel (M <= 2, K <= 512, 16-byte aligned rows) against its general
+    kernel (taken here through an x row stride that is not a multiple of 8): the same per-lane products and wave sums,
+    so bit-identical; both against torch fp32."""
+    from videopainter_amd import kernels as K
+    x = bf(rnd(M, K_, seed=300))
+    w, b = bf(rnd(4100, K_, std=K_ ** -0.5, seed=301)), bf(rnd(4100, std=0.1, seed=302))
+    xd = x.to(dev)
+    xs = torch.zeros(M, K_ + 4, device=dev, dtype=torch.bfloat16)
+    xs[:, :K_] = xd
+    y_fast = K.linear_small(xd, w.to(dev), b.to(dev), act_in=act_in, act_out=act_out)
+    y_gen = K.linear_small(xs[:, :K_], w.to(dev), b.to(dev), act_in=act_in, act_out=act_out)
+    assert torch.equal(y_fast, y_gen)
+    xin = bf(F.silu(x.float())).float() if act_in else x.float()
+    ref = F.linear(xin, w.float(), b.float())
+    if act_out:
+        ref = F.silu(ref)
+    assert rel(y_fast, ref) < 6e-3

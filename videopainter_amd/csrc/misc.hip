@@ -39,50 +39,6 @@ __global__ __launch_bounds__(LS_THREADS) void linear_small_kernel(const bf16* __
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int nch = K / 8;
-  const int nbase = (blockIdx.x * (LS_THREADS / 64) + wave) * LS_COLS_PER_WAVE;
-  if (nch <= 64 && nbase + LS_COLS_PER_WAVE <= N) {
-    // K <= 512 (the AdaLN / time-embedding linears): one 16-byte chunk per lane and column; the wave's 4 weight
-    // loads are issued together, then the products and the reductions (the loop below takes one load round trip
-    // per column)
-    bf16x8 w[LS_COLS_PER_WAVE];
-    const bool on = lane < nch;
-#pragma unroll
-    for (int cc = 0; cc < LS_COLS_PER_WAVE; ++cc)
-      w[cc] = on ? *(const bf16x8*)(W + (int64_t)(nbase + cc) * K + lane * 8) : bf16x8{};
-    float acc[LS_COLS_PER_WAVE][16];
-#pragma unroll
-    for (int cc = 0; cc < LS_COLS_PER_WAVE; ++cc)
-#pragma unroll
-      for (int m = 0; m < 16; ++m) acc[cc][m] = 0.f;
-    if (on) {
-#pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        if (m < M) {
-          const bf16x8 xv = *(const bf16x8*)(xs + m * K + lane * 8);
-#pragma unroll
-          for (int cc = 0; cc < LS_COLS_PER_WAVE; ++cc)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc[cc][m] = fmaf(bf2f(w[cc][e]), bf2f(xv[e]), acc[cc][m]);
-        }
-      }
-    }
-#pragma unroll
-    for (int cc = 0; cc < LS_COLS_PER_WAVE; ++cc) {
-      const int n = nbase + cc;
-#pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        if (m < M) {
-          float s = wave_sum(acc[cc][m]);
-          if (lane == 0) {
-            float v = rbf(s + (bias ? bf2f(bias[n]) : 0.f));
-            if (act_out == 1) v = rbf(silu(v));
-            y[(int64_t)m * ldy + n] = f2bf(v);
-          }
-        }
-      }
-    }
-    return;
-  }
   for (int cc = 0; cc < LS_COLS_PER_WAVE; ++cc) {
     const int n = (blockIdx.x * (LS_THREADS / 64) + wave) * LS_COLS_PER_WAVE + cc;
     if (n >= N) break;
@@ -268,10 +224,65 @@ extern "C" void vp_struct_sizes(int64_t* out) {
   out[6] = (int64_t)sizeof(vp_attn_bwd_desc);
 }
 
+// M <= 2 rows (the CFG pair's AdaLN / time-embedding vectors), K <= 512: a weight-streaming kernel.  Each wave owns
+// LSF_COLS columns and each lane one 16-byte K-chunk of every column, so a wave has LSF_COLS x 1 KiB of weights in
+// flight at once (the general kernel above has one column's 1 KiB per round trip); x comes straight from global
+// memory (2 x 16 bytes per lane), no LDS and no barrier.  Same per-lane products and wave sums as the general
+// kernel: bit-identical results.
+constexpr int LSF_COLS = 8;
+__global__ __launch_bounds__(LS_THREADS) void linear_small_fast_kernel(const bf16* __restrict__ x, int64_t ldx,
+                                                                      const bf16* __restrict__ W,
+                                                                      const bf16* __restrict__ bias,
+                                                                      bf16* __restrict__ y, int64_t ldy, int M, int N,
+                                                                      int K, int act_in, int act_out) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nbase = (blockIdx.x * (LS_THREADS / 64) + wave) * LSF_COLS;
+  const bool on = lane < K / 8;
+  bf16x8 w[LSF_COLS];
+#pragma unroll
+  for (int cc = 0; cc < LSF_COLS; ++cc)
+    w[cc] = (on && nbase + cc < N) ? *(const bf16x8*)(W + (int64_t)(nbase + cc) * K + lane * 8) : bf16x8{};
+  bf16x8 xv[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    xv[m] = (on && m < M) ? *(const bf16x8*)(x + (int64_t)m * ldx + lane * 8) : bf16x8{};
+    if (act_in == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[m][e] = f2bf(rbf(silu(bf2f(xv[m][e]))));
+    }
+  }
+#pragma unroll
+  for (int cc = 0; cc < LSF_COLS; ++cc) {
+    const int n = nbase + cc;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      if (m >= M) continue;
+      float acc = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc = fmaf(bf2f(w[cc][e]), bf2f(xv[m][e]), acc);
+      const float sum = wave_sum(acc);
+      if (lane == 0 && n < N) {
+        float v = rbf(sum + (bias ? bf2f(bias[n]) : 0.f));
+        if (act_out == 1) v = rbf(silu(v));
+        y[(int64_t)m * ldy + n] = f2bf(v);
+      }
+    }
+  }
+}
+
 extern "C" int vp_linear_small_bf16(const void* x, int64_t ldx, const void* W, const void* bias, void* y,
                                     int64_t ldy, int32_t M, int32_t N, int32_t K, int32_t act_in, int32_t act_out,
                                     void* stream) {
   if (!x || !W || !y || M <= 0 || M > 16 || N <= 0 || K <= 0 || (K % 8) || ldx < K || ldy < N) return VP_ERR_ARG;
+  if (M <= 2 && K <= 512 && (ldx % 8) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)W & 15) == 0) {
+    const int cpb = (LS_THREADS / 64) * LSF_COLS;
+    hipLaunchKernelGGL(linear_small_fast_kernel, dim3((N + cpb - 1) / cpb), dim3(LS_THREADS), 0, (hipStream_t)stream,
+                       (const bf16*)x, ldx, (const bf16*)W, (const bf16*)bias, (bf16*)y, ldy, M, N, K, act_in,
+                       act_out);
+    VP_CHECK_LAUNCH();
+    return VP_OK;
+  }
   const size_t lds = (size_t)M * K * 2;
   if (lds > 160 * 1024) return VP_ERR_ARG;
   const int cols_per_block = (LS_THREADS / 64) * LS_COLS_PER_WAVE;
