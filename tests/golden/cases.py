@@ -177,6 +177,18 @@ def config2_inputs(dtype=torch.float32):
                 timestep=torch.tensor([499, 499], dtype=torch.int64), rope=(cos, sin))
 
 
+def config4_inputs(dtype=torch.float32):
+    """Config 4's processor at config 2's shape, B = 1: batch row 0 of config 2's inputs, plus a second latent for
+    the later window (another counter stream)."""
+    i = config2_inputs(dtype)
+    out = {k: (v[:1].contiguous() if isinstance(v, torch.Tensor) and k != "timestep" else v) for k, v in i.items()}
+    out["timestep"] = i["timestep"][:1]
+    b, f, h, w = 1, 13, 60, 90
+    video2 = synth_tensor("c4.video2", (b, f, 16, h, w))
+    out["hidden2"] = torch.cat([torch.from_numpy(video2).to(dtype), out["hidden"][:, :, 16:]], dim=2).contiguous()
+    return out
+
+
 def config5_cfg():
     """BASELINE config 5: the 5b-I2V model at 49f 720x1280 (sample 90x160 latent)."""
     from videopainter_amd.config import COGVIDEOX_5B_I2V

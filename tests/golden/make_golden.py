@@ -11,6 +11,8 @@ Fixtures (all fp32):
   tiny_*.safetensors    — tiny config (2 heads x 64, 4 layers, 2-layer branch, latent 3x16x24, T=8), the branch,
                           the transformer in std / mask-less / add_first / ID-resample (window 0 and prev-window) /
                           prev-clip modes.
+  config4.safetensors   — the 42-layer ID-resample transformer + branch at N = 17 776, B = 1: window 0 and a later
+                          window with prev_hidden_states / prev_clip_weight 0.5 (fp32 + bf16 slices).
   wo_text.safetensors   — the tiny branch with wo_text=True (blocks on the video tokens alone), fp32 and bf16.
   sched.safetensors     — CogVideoXDPMScheduler: trailing timesteps, 3 steps incl. the 2nd-order branch, add_noise.
   pipe_tiny.safetensors — CogVideoXI2VDualInpaintAnyLPipeline, tiny model + tiny VAE, 2 windows x 2 steps, ID-resample
@@ -399,6 +401,64 @@ def _make_full_model(tag, cfg_fn, inputs_fn, seeds, out_stride):
     _save(f"{tag}.safetensors", out, {"cpu_seconds": {"fp32": t32, "bf16": t16}} if tag != "config1" else None)
 
 
+@torch.no_grad()
+def make_config4():
+    """BASELINE config 4's processor at full depth and length: the reference's 42-layer
+    transformer built with id_pool_resample_learnable=True + the 2-layer branch at config 2's shape (N = 17 776), B = 1,
+    two windows: window 0 (the resample processor's masked self K/V over 2N keys) returning its 42 hidden states and
+    resample mask, then a later window on another latent with those states as prev_hidden_states, prev_clip_weight 0.5
+    and prev_resample_mask (attention over [K; masked previous-window K]).  fp32 and the reference's own bf16 run:
+    strided slices of both windows' noise_pred + digests."""
+    import time
+    from diffusers.models.transformers.cogvideox_transformer_3d import CogVideoXTransformer3DModel
+    from diffusers.models.branch_cogvideox import CogvideoXBranchModel
+    from tests.golden.cases import config2_cfg, config4_inputs, CONFIG2_SEEDS
+    tcfg, bcfg = config2_cfg()
+    tcfg = dict(tcfg, id_pool_resample_learnable=True)
+    with torch.device("meta"):
+        tr = CogVideoXTransformer3DModel(**tcfg).eval()
+        br = CogvideoXBranchModel(**bcfg).eval()
+    tr = _fill_synthetic(tr, CONFIG2_SEEDS[0])
+    br = _fill_synthetic(br, CONFIG2_SEEDS[1])
+    inp = config4_inputs()
+
+    def fwd(dt):
+        c = lambda x: x.to(dt)  # noqa: E731
+        bs = br(hidden_states=c(inp["video"]), encoder_hidden_states=c(inp["enc"]), branch_cond=c(inp["branch_cond"]),
+                timestep=inp["timestep"], image_rotary_emb=inp["rope"], return_dict=False)[0]
+        o0, hs, rm = tr(hidden_states=c(inp["hidden"]), encoder_hidden_states=c(inp["enc"]),
+                        timestep=inp["timestep"], image_rotary_emb=inp["rope"], branch_block_samples=bs,
+                        branch_block_masks=c(inp["mask"]), id_pool_resample_learnable=True,
+                        return_hidden_states=True, return_resample_mask=True, return_dict=False)
+        prev = {i: h for i, h in enumerate(hs)}
+        o1 = tr(hidden_states=c(inp["hidden2"]), encoder_hidden_states=c(inp["enc"]), timestep=inp["timestep"],
+                image_rotary_emb=inp["rope"], branch_block_samples=bs, branch_block_masks=c(inp["mask"]),
+                attention_kwargs={"prev_hidden_states": prev, "prev_clip_weight": 0.5, "prev_resample_mask": rm},
+                id_pool_resample_learnable=True, return_dict=False)[0]
+        return o0.float(), o1.float()
+
+    t0 = time.time()
+    a32, b32 = fwd(torch.float32)
+    t32 = time.time() - t0
+    print(f"config4: fp32 {t32:.0f}s", flush=True)
+    tr.to(torch.bfloat16)
+    br.to(torch.bfloat16)
+    t0 = time.time()
+    a16, b16 = fwd(torch.bfloat16)
+    t16 = time.time() - t0
+    print(f"config4: bf16 {t16:.0f}s", flush=True)
+    rel = lambda a, b: float((a.double() - b.double()).norm() / b.double().norm())  # noqa: E731
+    out = {}
+    for tag, o32, o16 in (("w0", a32, a16), ("w1", b32, b16)):
+        flat = o32.reshape(-1)
+        out[f"{tag}.slice"] = flat[::7].clone()
+        out[f"{tag}.bf16.slice"] = o16.reshape(-1)[::7].clone()
+        out[f"{tag}.digest"] = torch.tensor([flat.sum(), flat.abs().sum(), flat.norm()], dtype=torch.float64)
+        out[f"{tag}.ref_bf16_rel"] = torch.tensor([rel(o16, o32)])
+        print(f"config4 {tag}: reference bf16 vs fp32 rel-L2 {rel(o16, o32):.3e}", flush=True)
+    _save("config4.safetensors", out, {"cpu_seconds": {"fp32": t32, "bf16": t16}})
+
+
 def make_config5():
     """BASELINE config 5's shape (49f 720x1280, N = 47 026) through the reference, whole model, B = 1 (VERDICT r02
     "what's missing" 3): noise_pred [1,13,16,90,160] strided slice (every 13th element) in fp32 and the reference's
@@ -598,6 +658,8 @@ if __name__ == "__main__":
         make_config2()
     if "config5" in which:
         make_config5()
+    if "config4" in which:
+        make_config4()
     if "block5" in which:
         make_block5()
     if "block_resample" in which:

@@ -185,6 +185,36 @@ def test_gemm_gated_inject_and_remap(gemm_variant):
     assert float(out2[:, :T].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("inject", [True, False], ids=["inject", "noinject"])
+def test_gemm_gated_row_pass_forms_bit_identical(inject):
+    """The gated epilogue's branch-free row pass (tokens_per_batch, rows_per_group >= 256: preloaded residual rows,
+    the tile's gate vectors, injection flags staged in LDS) against its per-row form (taken here by cutting the output
+    into groups of 128 rows at the same places: rows_per_group = group_stride = 128), bit for bit: same arithmetic per
+    element.  Rows of both batches and the text / video split land in one tile (Ntok = 320)."""
+    from videopainter_amd import kernels as K
+    from videopainter_amd import _native as N
+    B, T, Nv, D, Kk = 2, 64, 256, 512, 512
+    Ntok = T + Nv
+    M = B * Ntok
+    a = bf(rnd(M, Kk, seed=40)).to(dev)
+    w = bf(rnd(D, Kk, std=Kk ** -0.5, seed=41)).to(dev)
+    b = bf(rnd(D, std=0.1, seed=42)).to(dev)
+    resid = bf(rnd(B, Ntok, D, seed=43)).to(dev)
+    mod = bf(rnd(B, 6 * D, seed=44)).to(dev)
+    kw = dict(epilogue=N.EPI_GATED, resid=resid, mod=mod, tokens_per_batch=Ntok, text_len=T)
+    if inject:
+        inj = bf(rnd(B, Nv, D, seed=45)).to(dev)
+        tm = (torch.rand(B, Nv, generator=torch.Generator().manual_seed(4)) > 0.5).to(torch.uint8).to(dev)
+        kw.update(inject=inj, inject_ld=D, inject_bstride=Nv * D, inject_mask=tm)
+    assert M % 128 == 0
+    outs = []
+    for rpg in (M, 128):
+        out = torch.empty(B, Ntok, D, device=dev, dtype=torch.bfloat16)
+        K.gemm(a, [w], [b], out.view(-1, D), rows_per_group=rpg, group_stride=rpg, **kw)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+
+
 def _sdpa(q, k, v):
     return F.scaled_dot_product_attention(q.float(), k.float(), v.float())
 

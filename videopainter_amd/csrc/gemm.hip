@@ -26,7 +26,9 @@ constexpr int FM = WM / 16, FN = WN / 16;
 constexpr int TILE_BYTES = BM * BK * 2;       // 32 KB per operand tile
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;   // A + B
 constexpr int CT_STRIDE = BN * 2 + 8;         // bytes per C row in the epilogue LDS image (bank-conflict pad)
-constexpr int LDS_BYTES = (2 * STAGE_BYTES > BM * CT_STRIDE) ? 2 * STAGE_BYTES : BM * CT_STRIDE;
+// the gated epilogue's per-row injection flags (one byte per tile row) sit past the C image
+constexpr int EPI_FLAG_OFF = BM * CT_STRIDE;
+constexpr int LDS_BYTES = (2 * STAGE_BYTES > EPI_FLAG_OFF + BM) ? 2 * STAGE_BYTES : EPI_FLAG_OFF + BM;
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void g_void;
@@ -150,6 +152,10 @@ VP_DEV void mfma_mx(f32x4& acc, const i32x8& w, const i32x8& a, int sw, int sa) 
 // profiles/r04_gemm_epi_ab.log, out-projection 0.574-0.582 vs 0.630 ms)
 #ifndef VP_GEMM_EPI_RPRE
 #define VP_GEMM_EPI_RPRE 1
+#endif
+// the gated row pass's branch-free form (epi_rows_gated; 0 = the per-row form for every tile, A/B)
+#ifndef VP_GEMM_GATED_FAST
+#define VP_GEMM_GATED_FAST 1
 #endif
 // ---- fused epilogue shared by the GEMM kernels: acc[j][i] = the 16x16 fragment (W rows j, A rows i) of a wave
 // whose C block is rows wr*WM.., cols wc*WN.. of the BM x BN tile.  Three pieces: epi_values (per-fragment bias /
@@ -360,6 +366,82 @@ VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* sme
 }
 
 
+// The gated row pass with the residual rows preloaded (rpre), for tiles whose rows cross at most one batch and one
+// output-group boundary (tokens_per_batch, rows_per_group >= BM): every load of the pass is issued up front and
+// branch-free — the <= 4 gate vectors the tile's rows use (text / video x 2 batches), the 16 rows' injection-mask bytes,
+// then their injection rows — so the pass waits for memory twice instead of three times per row (the per-row form
+// with its data-dependent branches came out of the compiler fully serialised).  Same arithmetic per element as
+// epi_rows_out: bit-identical.
+template <int NT, int NPRE>
+VP_DEV void epi_rows_gated(const vp_gemm_desc& d, const char* smem, int m0, int n0, int tid,
+                           const bf16x8 (&rpre)[NPRE]) {
+  constexpr int CPR = BN / 8, CTS = BN * 2 + 8, RS = NT / CPR;
+  const int chunk = tid & (CPR - 1);
+  const int ncol = n0 + chunk * 8;
+  const bool col_ok = ncol < d.N;
+  const int r0 = tid / CPR;
+  const int rpg = d.rows_per_group, tpb = d.tokens_per_batch, T = d.text_len;
+  const int grp0 = m0 / rpg, gin0 = m0 - grp0 * rpg;
+  const int b0 = m0 / tpb, tk0 = m0 - b0 * tpb;
+  // the tile's gate vectors: batch b0, and b0 + 1 when the tile reaches it (uniform)
+  const bool two_b = tk0 + BM > tpb && (int64_t)(b0 + 1) * tpb < d.M;
+  const bf16* gvid = (const bf16*)d.gate + ncol;
+  const bf16* gtxt = (const bf16*)d.gate_text + ncol;
+  const bf16x8 gv0 = col_ok ? *(const bf16x8*)(gvid + (int64_t)b0 * d.gate_bstride) : bf16x8{};
+  const bf16x8 gt0 = col_ok ? *(const bf16x8*)(gtxt + (int64_t)b0 * d.gate_bstride) : bf16x8{};
+  const bf16x8 gv1 = (col_ok && two_b) ? *(const bf16x8*)(gvid + (int64_t)(b0 + 1) * d.gate_bstride) : bf16x8{};
+  const bf16x8 gt1 = (col_ok && two_b) ? *(const bf16x8*)(gtxt + (int64_t)(b0 + 1) * d.gate_bstride) : bf16x8{};
+  const bool has_inj = d.inject != nullptr;
+  uint32_t injbits = 0;  // bit it: row it takes the injection (flags staged in LDS by gemm_epilogue, one per row)
+  if (has_inj) {
+    // the flags of rows r0 + 16 it are bytes it of one 16-byte LDS word (stored transposed by gemm_epilogue)
+    static_assert(NPRE == 16 && RS == 16, "the flag layout assumes 16 rows per step and 16 steps");
+    const u32x4 fw = *(const u32x4*)(smem + EPI_FLAG_OFF + r0 * 16);
+#pragma unroll
+    for (int it = 0; it < NPRE; ++it)
+      injbits |= (col_ok && ((fw[it >> 2] >> (8 * (it & 3))) & 0xffu) != 0 ? 1u : 0u) << it;
+  }
+  bf16x8 iv[NPRE];
+#pragma unroll
+  for (int it = 0; it < NPRE; ++it) {
+    const int mloc = it * RS + r0;
+    int tok = tk0 + mloc, b = b0;
+    if (tok >= tpb) {
+      tok -= tpb;
+      ++b;
+    }
+    iv[it] = ((injbits >> it) & 1u) ? *(const bf16x8*)((const bf16*)d.inject + (int64_t)b * d.inject_bstride +
+                                                       (int64_t)(tok - T) * d.inject_ld + ncol)
+                                    : bf16x8{};
+  }
+  bf16* C = (bf16*)d.C;
+#pragma unroll
+  for (int it = 0; it < NPRE; ++it) {
+    const int mloc = it * RS + r0;
+    if (m0 + mloc >= d.M || !col_ok) continue;
+    bf16x8 v = *(const bf16x8*)(smem + mloc * CTS + chunk * 16);
+    int gin = gin0 + mloc, grp = grp0;
+    if (gin >= rpg) {
+      gin -= rpg;
+      ++grp;
+    }
+    int tok = tk0 + mloc;
+    const bool hi = tok >= tpb;
+    if (hi) tok -= tpb;
+    const bf16x8 gv = tok < T ? (hi ? gt1 : gt0) : (hi ? gv1 : gv0);
+    const bf16x8 rv = rpre[it];
+    const bool inj = (injbits >> it) & 1u;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float o = rbf(bf2f(rv[e]) + rbf(bf2f(gv[e]) * bf2f(v[e])));
+      if (inj) o = rbf(o + bf2f(iv[it][e]));
+      v[e] = f2bf(o);
+    }
+    const int64_t orow = (int64_t)grp * d.group_stride + d.row_offset + gin;
+    *(bf16x8*)(C + orow * d.ldc + ncol) = v;
+  }
+}
+
 template <int NT, int FN, int FM, int WN, int WM, bool FP8, int EPI = -1>
 VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&acc)[FN][FM], char* smem, int m0,
                           int n0, int wr, int wc, int lane, int tid) {
@@ -373,6 +455,18 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
     const int ncol = n0 + chunk * 8;
     const int rpg = d.rows_per_group;
     const int grp0 = m0 / rpg, gin0 = m0 - grp0 * rpg;
+    if (d.inject != nullptr && tid < BM) {
+      // the injection flag of tile row tid: a video row whose mask byte is 0 (or no mask); one byte load per row
+      // for the whole tile, read back from LDS by the row pass (flags area past the C image: no overlap with the
+      // ring or the image)
+      const int m = m0 + tid;
+      const int tpb = d.tokens_per_batch;
+      const int b = m / tpb, tok = m - b * tpb;
+      const bool vid = m < d.M && tok >= d.text_len;
+      const bool f = vid && (d.inject_mask == nullptr ||
+                             d.inject_mask[(int64_t)b * d.inject_mask_bstride + (tok - d.text_len)] == 0);
+      smem[EPI_FLAG_OFF + (tid & 15) * 16 + (tid >> 4)] = f ? 1 : 0;  // row tid -> word tid % 16, byte tid / 16
+    }
 #pragma unroll
     for (int it = 0; it < NPRE; ++it) {
       const int mloc = it * (NT / CPR) + tid / CPR;
@@ -390,7 +484,10 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
         [&](int j, int i, const bf16x4& o) { *(bf16x4*)epi_lds_addr<WN, WM>(smem, j, i, 0, wr, wc, lane) = o; },
         m0, n0, wr, wc, lane);
     __syncthreads();
-    epi_rows_out<NT, FP8, EPI, BN, NPRE>(d, mx, smem, 0, BM, m0, n0, tid, rpre);
+    if (VP_GEMM_GATED_FAST && d.tokens_per_batch >= BM && d.rows_per_group >= BM)
+      epi_rows_gated<NT, NPRE>(d, smem, m0, n0, tid, rpre);
+    else
+      epi_rows_out<NT, FP8, EPI, BN, NPRE>(d, mx, smem, 0, BM, m0, n0, tid, rpre);
     return;
   }
 #endif
