@@ -215,6 +215,25 @@ def test_gemm_gated_row_pass_forms_bit_identical(inject):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("epi", ["bias", "gelu"])
+def test_gemm_plain_row_pass_forms_bit_identical(epi):
+    """Output row placement of the epilogues without row-wise inputs: one row group (rows_per_group = M) and groups of
+    128 rows at group_stride 128 (the same output rows) give the same bits."""
+    from videopainter_amd import kernels as K
+    from videopainter_amd import _native as N
+    M, D, Kk = 640, 768, 512
+    a = bf(rnd(M, Kk, seed=50)).to(dev)
+    w = bf(rnd(D, Kk, std=Kk ** -0.5, seed=51)).to(dev)
+    b = bf(rnd(D, std=0.1, seed=52)).to(dev)
+    e = N.EPI_BIAS if epi == "bias" else N.EPI_BIAS_GELU
+    outs = []
+    for rpg in (M, 128):
+        out = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+        K.gemm(a, [w], [b], out, epilogue=e, rows_per_group=rpg, group_stride=rpg)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+
+
 def _sdpa(q, k, v):
     return F.scaled_dot_product_attention(q.float(), k.float(), v.float())
 

@@ -496,6 +496,9 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
       [&](int j, int i, const bf16x4& o) { *(bf16x4*)epi_lds_addr<WN, WM>(smem, j, i, 0, wr, wc, lane) = o; }, m0,
       n0, wr, wc, lane);
   __syncthreads();
+  // (the row loop stays rolled for the epilogues without row-wise inputs: an unrolled, branch-free form issued the
+  // 16 image reads together but was 1-1.5 % slower on QKV / FF1, profiles/r04_gemm_plain_rowpass_ab_rejected.log —
+  // the pass is store-issue bound, as round 2's unroll A/B found)
   epi_rows_out<NT, FP8, EPI>(d, mx, smem, 0, BM, m0, n0, tid);
 }
 
