@@ -234,6 +234,33 @@ def test_gemm_plain_row_pass_forms_bit_identical(epi):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("epi", ["bias", "gelu"])
+def test_gemm_tail_split_round(epi, monkeypatch):
+    """Tail mode (gemm.hip tail_plan): 17 x 16 = 272 tiles on the 256-CU chip leave a last round of 16 tiles, which
+    runs as split-K workgroups (2 x 512-K chunks, compact fp32 partials) + a reduce that applies the epilogue; the
+    ragged last M-tile is among them.  Against torch fp32 and against the same GEMM without the tail split
+    (VP_GEMM_NO_TAIL): the two differ only by the fp32 summation order of two K halves."""
+    from videopainter_amd import kernels as K
+    from videopainter_amd import _native as N
+    M, D, Kk = 17 * 256 - 100, 4096, 1024
+    a = bf(rnd(M, Kk, seed=60)).to(dev)
+    w = bf(rnd(D, Kk, std=Kk ** -0.5, seed=61)).to(dev)
+    b = bf(rnd(D, std=0.1, seed=62)).to(dev)
+    e = N.EPI_BIAS if epi == "bias" else N.EPI_BIAS_GELU
+    out = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    K.gemm(a, [w], [b], out, epilogue=e)
+    monkeypatch.setenv("VP_GEMM_NO_TAIL", "1")
+    ref_k = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    K.gemm(a, [w], [b], ref_k, epilogue=e)
+    y = a.float() @ w.float().T + b.float()
+    if epi == "gelu":
+        y = F.gelu(y, approximate="tanh")
+    assert rel(out, y) < 4e-3
+    diff = (out.float() - ref_k.float()).abs()
+    assert float(diff.max()) <= float(ref_k.float().abs().max()) * 2 ** -7
+    assert rel(out, ref_k) < 1e-3
+
+
 def _sdpa(q, k, v):
     return F.scaled_dot_product_attention(q.float(), k.float(), v.float())
 

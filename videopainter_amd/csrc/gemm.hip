@@ -73,9 +73,11 @@ struct MxExt {
   const uint8_t* a_scale;
   const uint8_t* w_scale[3];
   uint8_t* c_scale;
-  // split-K (vp_gemm_bf16_ws): workgroup = (tile, K-chunk); fp32 partial tiles [nsplit][M][N] in ws
+  // split-K (vp_gemm_bf16_ws): workgroup = (tile, K-chunk); fp32 partial tiles [nsplit][M][N] in ws, or (tail mode:
+  // the last partial round of a large GEMM) tiles t_base.. with compact partials [tile - t_base][nsplit][BM][BN]
   float* ws;
   int kchunk, nsplit;
+  int t_base, tail;
 };
 
 // scale ring of the fp8 path: 4 K-tiles x (A, W) x 1 KiB after the two operand stages (the ring slot of tile t is
@@ -517,8 +519,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
   const int tiles_m = (d.M + BM - 1) / BM;
   const int tiles_n = (d.N + BN - 1) / BN;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int t = SPLIT ? lin / mx.nsplit : lin;
-  const int kc = SPLIT ? lin - t * mx.nsplit : 0;  // K-chunk of this workgroup
+  const int t = SPLIT ? mx.t_base + lin / mx.nsplit : lin;
+  const int kc = SPLIT ? lin % mx.nsplit : 0;  // K-chunk of this workgroup
   // this workgroup's K range: [kbeg, kbeg + Kloop) (the whole K unless split)
   const int kbeg = SPLIT ? kc * mx.kchunk : 0;
   const int Kloop = SPLIT ? min(mx.kchunk, d.K - kbeg) : d.K;
@@ -999,6 +1001,18 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 
   if constexpr (SPLIT) {
     // fp32 partial tile: lane (j, i) holds 4 consecutive columns of one row (16-byte stores)
+    if (mx.tail) {  // compact: this workgroup's BM x BN slab
+      float* P = mx.ws + ((int64_t)(t - mx.t_base) * mx.nsplit + kc) * (BM * BN);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int ml = wr * WM + i * 16 + (lane & 15);
+          const int nl = wc * WN + j * 16 + (lane >> 4) * 4;
+          *(f32x4*)(P + ml * BN + nl) = acc[j][i];
+        }
+      return;
+    }
     float* P = mx.ws + (int64_t)kc * d.M * d.N;
 #pragma unroll
     for (int j = 0; j < FN; ++j)
@@ -1255,6 +1269,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm2_kernel(const vp_gemm_desc d) {
 
 // split-K reduce + epilogue: one thread per 8 consecutive output columns of one row; the chunks are summed in a fixed
 // order, then the same roundings as the fused epilogues (epi_values + epi_rows_out)
+VP_DEV void splitk_epilogue(const vp_gemm_desc& d, int m, int n, const float (&a)[8]);
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const vp_gemm_desc d, const float* __restrict__ ws,
                                                                  int nsplit) {
   const int c8 = d.N >> 3;
@@ -1275,6 +1290,41 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const vp_gemm_d
       a[4 + e] += hi[e];
     }
   }
+  splitk_epilogue(d, m, n, a);
+}
+
+// tail mode: the last partial round's tiles (t_base..) from their compact partial slabs; 32 blocks of 256 threads
+// per tile (8 rows x 32 eight-column chunks each); the tile coordinates as the GEMM kernel's grouped order (GROUP 4)
+__global__ __launch_bounds__(256) void gemm_tail_reduce_kernel(const vp_gemm_desc d, const float* __restrict__ ws,
+                                                               int t_base, int nsplit) {
+  const int j = blockIdx.x >> 5;
+  const int r = (blockIdx.x & 31) * 8 + (threadIdx.x >> 5);
+  const int c = threadIdx.x & 31;
+  const int t = t_base + j;
+  const int tiles_m = (d.M + BM - 1) / BM, tiles_n = (d.N + BN - 1) / BN;
+  constexpr int GROUP = 4;
+  const int per_group = GROUP * tiles_n;
+  const int first_m = (t / per_group) * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + ((t % per_group) % gsz), tn = (t % per_group) / gsz;
+  const int m = tm * BM + r, n = tn * BN + c * 8;
+  if (m >= d.M || n >= d.N) return;
+  float a[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float* p = ws + ((int64_t)j * nsplit + s) * (BM * BN) + r * BN + c * 8;
+    const f32x4 lo = *(const f32x4*)p, hi = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] += lo[e];
+      a[4 + e] += hi[e];
+    }
+  }
+  splitk_epilogue(d, m, n, a);
+}
+
+VP_DEV void splitk_epilogue(const vp_gemm_desc& d, int m, int n, const float (&a)[8]) {
   const int sg = (int)(n >= d.n_seg) + (int)(n >= 2 * d.n_seg);
   const bf16* bp = (const bf16*)d.bias[sg];
   const int grp = m / d.rows_per_group, gin = m - grp * d.rows_per_group;
@@ -1283,9 +1333,10 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const vp_gemm_d
   bf16x8 pv;
   if (d.epilogue == VP_EPI_BIAS_ADDROWS)
     pv = *(const bf16x8*)((const bf16*)d.addrows + (int64_t)(gin + d.addrows_offset) * d.addrows_ld + n);
+  const bf16x8 b8 = bp != nullptr ? *(const bf16x8*)(bp + n - sg * d.n_seg) : bf16x8{};
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    float v = rbf(a[e] + (bp != nullptr ? bf2f(bp[n + e - sg * d.n_seg]) : 0.f));
+    float v = rbf(a[e] + (bp != nullptr ? bf2f(b8[e]) : 0.f));
     if (d.epilogue == VP_EPI_BIAS_GELU) v = rbf(gelu_tanh(v));
     else if (d.epilogue == VP_EPI_BIAS_SCALE) v = rbf(v * d.alpha);
     else if (d.epilogue == VP_EPI_BIAS_ADDROWS) v = bf2f(f2bf(v)) + bf2f(pv[e]);
@@ -1299,13 +1350,51 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const vp_gemm_d
 struct SplitPlan {
   int nsplit = 1, kchunk = 0;
   int64_t ws_bytes = 0;
+  int tail = 0;  // > 0: tail mode (the last `tail` tiles split, the others one main launch)
 };
+int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+    cus = n;
+  }
+  return cus;
+}
+// Tail mode: a large GEMM whose last round of tiles (one 8-wave workgroup per CU) is at most a quarter full runs that
+// round as split-K workgroups over whole 512-K chunks (one round, compact fp32 partials) plus a reduce that applies
+// the epilogue, instead of a round of whole tiles on a mostly idle chip (config 2's FF1: 6 672 tiles = 26 rounds +
+// 16).  The default main loop only (VP_GEMM_VARIANT unset or 13), and the epilogues the reduce implements.
+SplitPlan tail_plan(const vp_gemm_desc* d, int tiles) {
+  SplitPlan p;
+  const char* e = getenv("VP_GEMM_VARIANT");
+  if ((e != nullptr && atoi(e) != 13) || getenv("VP_GEMM_NO_TAIL") != nullptr) return p;
+  const int cus = device_cus();
+  const int tail = tiles % cus;
+  if (tiles <= cus || tail == 0 || 4 * tail > cus) return p;
+  if ((d->N % BN) != 0 || (d->K % BK) != 0) return p;
+  const int nk = d->K / BK;
+  const int ns = min(cus / tail, nk / 8);
+  if (ns < 2) return p;
+  const int chunk_t = (nk + ns - 1) / ns;
+  p.kchunk = chunk_t * BK;
+  p.nsplit = (nk + chunk_t - 1) / chunk_t;
+  if (p.nsplit < 2 || d->K - (p.nsplit - 1) * p.kchunk < 8 * BK) return SplitPlan{};
+  p.tail = tail;
+  p.ws_bytes = (int64_t)tail * p.nsplit * BM * BN * 4;
+  return p;
+}
 SplitPlan split_plan(const vp_gemm_desc* d) {
   SplitPlan p;
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
   const bool epi_ok = d->epilogue == VP_EPI_BIAS || d->epilogue == VP_EPI_BIAS_GELU ||
                       d->epilogue == VP_EPI_BIAS_SCALE || d->epilogue == VP_EPI_BIAS_ADDROWS;
-  if (!epi_ok || tiles >= 128 || (d->K % BK) != 0 || d->K < 1024) return p;
+  if (!epi_ok || (d->K % BK) != 0) return p;
+  const int64_t tile_a0 = (int64_t)BM * d->lda * 2, wseg0 = (int64_t)d->n_seg * d->K * 2;
+  if (tiles >= 128) return (tile_a0 < ((int64_t)1 << 31) && wseg0 < ((int64_t)1 << 31)) ? tail_plan(d, tiles) : p;
+  if (d->K < 1024) return p;
   const int64_t tile_a = (int64_t)BM * d->lda * 2, wseg = (int64_t)d->n_seg * d->K * 2;
   if (tile_a >= ((int64_t)1 << 31) || wseg >= ((int64_t)1 << 31)) return p;
   // the fp32 partials (nsplit x M x N x 4 B, written and read back) should not outweigh the weights (N x K x 2 B)
@@ -1327,7 +1416,8 @@ extern "C" int vp_gemm_variant_built(int variant) {
   return (variant == 12 || variant == 20 || variant == 30) && VP_GEMM_EXTRA_VARIANTS ? 1 : 0;
 }
 
-extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
+// main_tiles > 0: launch only the first main_tiles tiles of the grouped order (tail mode's main launch)
+static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles) {
   if (d == nullptr || d->A == nullptr || d->W[0] == nullptr || d->C == nullptr) return VP_ERR_ARG;
   if (d->M <= 0 || d->N <= 0 || d->K <= 0 || (d->K % 8) != 0 || (d->N % 8) != 0) return VP_ERR_ARG;
   if (d->lda < d->K || d->ldc < d->N || (d->lda % 8) != 0 || (d->ldc % 8) != 0) return VP_ERR_ARG;
@@ -1453,7 +1543,8 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   const bool tile32 = (int64_t)BM * d->lda * 2 < ((int64_t)1 << 31) && w32;
   if (variant != 1 && ((d->K % BK) != 0 || !tile32)) variant = 1;  // needs whole K-tiles
   if ((variant == 11 || variant == 13) && d->K < 8 * BK) variant = 5;  // the staggered prologue assumes >= 8 K-tiles
-  const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
+  const int all_tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
+  const int tiles = main_tiles > 0 ? min(main_tiles, all_tiles) : all_tiles;
   if (variant == 12 || variant == 13) {
     void* args[] = {(void*)d, (void*)&mx};
     const void* const* kt = variant == 12 ? k12 : k13;
@@ -1474,6 +1565,8 @@ extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) {
   return VP_OK;
 }
 
+extern "C" int vp_gemm_bf16(const vp_gemm_desc* d, void* stream) { return gemm_bf16_launch(d, stream, 0); }
+
 extern "C" int64_t vp_gemm_bf16_workspace_bytes(const vp_gemm_desc* d) {
   if (d == nullptr) return -1;
   return split_plan(d).ws_bytes;
@@ -1493,7 +1586,7 @@ extern "C" int vp_gemm_bf16_ws(const vp_gemm_desc* d, void* workspace, int64_t w
   if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS, true>,
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr_set = true;
   }
@@ -1502,6 +1595,21 @@ extern "C" int vp_gemm_bf16_ws(const vp_gemm_desc* d, void* workspace, int64_t w
   mx.kchunk = p.kchunk;
   mx.nsplit = p.nsplit;
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
+  if (p.tail > 0) {
+    // tail mode: every tile but the last p.tail as one main launch (the validation and main loop of vp_gemm_bf16),
+    // the tail tiles as split-K workgroups into compact partials, then their reduce + epilogue
+    const int rc = gemm_bf16_launch(d, stream, tiles - p.tail);
+    if (rc != VP_OK) return rc;
+    mx.t_base = tiles - p.tail;
+    mx.tail = 1;
+    hipLaunchKernelGGL((gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS, true>), dim3(p.tail * p.nsplit),
+                       dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
+    VP_CHECK_LAUNCH();
+    hipLaunchKernelGGL(gemm_tail_reduce_kernel, dim3(p.tail * 32), dim3(256), 0, (hipStream_t)stream, *d,
+                       (const float*)workspace, tiles - p.tail, p.nsplit);
+    VP_CHECK_LAUNCH();
+    return VP_OK;
+  }
   hipLaunchKernelGGL((gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS, true>), dim3(tiles * p.nsplit), dim3(NTHREADS),
                      LDS_BYTES, (hipStream_t)stream, *d, mx);
   VP_CHECK_LAUNCH();
