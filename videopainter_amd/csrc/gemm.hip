@@ -78,6 +78,7 @@ struct MxExt {
   float* ws;
   int kchunk, nsplit;
   int t_base, tail;
+  int group;  // M-tiles per tile group of the grouped order (0: the kernel's GROUP)
 };
 
 // scale ring of the fp8 path: 4 K-tiles x (A, W) x 1 KiB after the two operand stages (the ring slot of tile t is
@@ -524,10 +525,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
   // this workgroup's K range: [kbeg, kbeg + Kloop) (the whole K unless split)
   const int kbeg = SPLIT ? kc * mx.kchunk : 0;
   const int Kloop = SPLIT ? min(mx.kchunk, d.K - kbeg) : d.K;
-  const int per_group = GROUP * tiles_n;
+  const int G = mx.group > 0 ? mx.group : GROUP;
+  const int per_group = G * tiles_n;
   const int group_id = t / per_group;
-  const int first_m = group_id * GROUP;
-  const int gsz = min(tiles_m - first_m, GROUP);
+  const int first_m = group_id * G;
+  const int gsz = min(tiles_m - first_m, G);
   const int tm = first_m + ((t % per_group) % gsz);
   const int tn = (t % per_group) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -1296,13 +1298,12 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const vp_gemm_d
 // tail mode: the last partial round's tiles (t_base..) from their compact partial slabs; 32 blocks of 256 threads
 // per tile (8 rows x 32 eight-column chunks each); the tile coordinates as the GEMM kernel's grouped order (GROUP 4)
 __global__ __launch_bounds__(256) void gemm_tail_reduce_kernel(const vp_gemm_desc d, const float* __restrict__ ws,
-                                                               int t_base, int nsplit) {
+                                                               int t_base, int nsplit, int GROUP) {
   const int j = blockIdx.x >> 5;
   const int r = (blockIdx.x & 31) * 8 + (threadIdx.x >> 5);
   const int c = threadIdx.x & 31;
   const int t = t_base + j;
   const int tiles_m = (d.M + BM - 1) / BM, tiles_n = (d.N + BN - 1) / BN;
-  constexpr int GROUP = 4;
   const int per_group = GROUP * tiles_n;
   const int first_m = (t / per_group) * GROUP;
   const int gsz = min(tiles_m - first_m, GROUP);
@@ -1416,6 +1417,14 @@ extern "C" int vp_gemm_variant_built(int variant) {
   return (variant == 12 || variant == 20 || variant == 30) && VP_GEMM_EXTRA_VARIANTS ? 1 : 0;
 }
 
+// M-tiles per group of the grouped tile order (VP_GEMM_GROUP overrides, A/B; read per call)
+static int gemm_group(const vp_gemm_desc* d) {
+  (void)d;
+  const char* g = getenv("VP_GEMM_GROUP");
+  const int v = g != nullptr ? atoi(g) : 0;
+  return v > 0 && v <= 64 ? v : 4;
+}
+
 // main_tiles > 0: launch only the first main_tiles tiles of the grouped order (tail mode's main launch)
 static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles) {
   if (d == nullptr || d->A == nullptr || d->W[0] == nullptr || d->C == nullptr) return VP_ERR_ARG;
@@ -1438,7 +1447,8 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
     if (d->inject != nullptr && ((d->inject_ld % 8) != 0 || (d->inject_bstride % 8) != 0)) return VP_ERR_ARG;
   }
   if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
-  const MxExt mx = {};
+  MxExt mx = {};
+  mx.group = gemm_group(d);
   // main loops: 13 = the quadrant-phase pipeline with the two wave groups staggered and each slot's fragment reads
   // issued before its DMA, instantiated per epilogue kind (default: +3.6-5.2 % over 11 on every config-2 shape and
   // 283.7 against 295.4 ms of GEMM per step, profiles/r04_gemm13_ab.log), 11 = the same with the reads after the DMA
@@ -1602,11 +1612,12 @@ extern "C" int vp_gemm_bf16_ws(const vp_gemm_desc* d, void* workspace, int64_t w
     if (rc != VP_OK) return rc;
     mx.t_base = tiles - p.tail;
     mx.tail = 1;
+    mx.group = gemm_group(d);
     hipLaunchKernelGGL((gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS, true>), dim3(p.tail * p.nsplit),
                        dim3(NTHREADS), LDS_BYTES, (hipStream_t)stream, *d, mx);
     VP_CHECK_LAUNCH();
     hipLaunchKernelGGL(gemm_tail_reduce_kernel, dim3(p.tail * 32), dim3(256), 0, (hipStream_t)stream, *d,
-                       (const float*)workspace, tiles - p.tail, p.nsplit);
+                       (const float*)workspace, tiles - p.tail, p.nsplit, mx.group);
     VP_CHECK_LAUNCH();
     return VP_OK;
   }
@@ -1668,7 +1679,7 @@ extern "C" int vp_gemm_mx_fp8(const vp_gemm_mx_desc* x, void* stream) {
   }
   const char* e8 = getenv("VP_GEMM8_VARIANT");  // read per call (A/B)
   const bool use13 = (e8 == nullptr || atoi(e8) != 5) && d->K / 128 >= 8 && kf13[d->epilogue] != nullptr;
-  MxExt mx;
+  MxExt mx = {};  // (zero: no split, the kernel's GROUP)
   mx.a_scale = (const uint8_t*)x->a_scale;
   for (int s = 0; s < 3; ++s) mx.w_scale[s] = (const uint8_t*)x->w_scale[s];
   mx.c_scale = (uint8_t*)x->c_scale;
