@@ -138,11 +138,12 @@ def _ref_fp64(q8, k8, vt, vs, npad, Nk, H, q_exp, k_exp):
     o = torch.einsum("bhqk,bhkd->bqhd", p / p.sum(dim=-1, keepdim=True), vd)
     return o.reshape(B, Nq, H * 64)
 
-@pytest.fixture(params=["1", "2", "3", "4"], ids=["exp2", "lin", "lin2", "lin2p"])
+@pytest.fixture(params=["1", "2", "3", "4", "5"], ids=["exp2", "lin", "lin2", "lin2p", "skew"])
 def attn8_variant(request, monkeypatch):
     """VP_ATTN8_VARIANT: 1 = P by v_exp_f32 + RNE e4m3 pack, 2 = P by linear mantissa interpolation, 3 = the same
-    codes packed by v_cvt_pknorm_u16_f32 + a byte gather (default), 4 = the lin2 codes in the software-pipelined
-    kernel (f8p).  1 and 4 are rejected A/B forms, built only with VP_ATTN_EXTRA_VARIANTS=1."""
+    codes packed by v_cvt_pknorm_u16_f32 + a byte gather, 4 = the lin2 codes in the software-pipelined
+    kernel (f8p), 5 = the lin2 kernel with its tile loop skewed by one tile (default).  1 and 4 are rejected A/B
+    forms, built only with VP_ATTN_EXTRA_VARIANTS=1."""
     from videopainter_amd import kernels as K
     if not K.attention_variant_built("fp8:" + request.param):
         pytest.skip(f"fp8 attention variant {request.param} is not in this build (VP_ATTN_EXTRA_VARIANTS)")
@@ -179,6 +180,32 @@ def test_attention_fp8(B, H, N, late, attn8_variant):
     K.attention_fp8(q8, k8, vp, o2, H, q_exp, k_exp, out_scale=0.7)
     K.attention_fp8(q8, k8, vp, o2, H, q_exp, k_exp, out_scale=0.3, accumulate=True)
     assert rel(o2, out) < 1e-2
+
+
+# partial last tiles of every size class (1, 3, 4, 5, 33, 63 keys) and one- to three-tile sequences
+@pytest.mark.parametrize("N", [65, 67, 68, 69, 97, 127, 128, 129, 1000])
+@pytest.mark.parametrize("var", ["5"])
+def test_attention_fp8_skewed_bit_identical(N, var, monkeypatch):
+    """The skewed loop (variant 5, the default) computes the same P codes, rescale decisions and accumulation order as
+    variant 3; its last-tile mask zeroes the P codes of the keys past Nk (duplicates of key Nk - 1) where variant 3
+    sets their scores to -inf: the outputs are equal bit for bit, also through the blend epilogue."""
+    from videopainter_amd import kernels as K
+    B, H = 2, 3
+    q, k, v = _attn_case(B, H, N, 1000 + N, late_spike=N >= 1000)
+    q_exp, k_exp = 5, 4
+    q8 = e4m3(q.float() * 0.125 * K.LOG2E * 2.0 ** q_exp).to(dev)
+    k8 = e4m3(k.float() * 2.0 ** k_exp).to(dev)
+    vp = K.v_pack_fp8(v.to(dev), H)
+    outs = {}
+    for vv in ("3", var):
+        monkeypatch.setenv("VP_ATTN8_VARIANT", vv)
+        o = torch.empty(B, N, H * 64, device=dev, dtype=torch.bfloat16)
+        K.attention_fp8(q8, k8, vp, o, H, q_exp, k_exp, out_scale=0.7)
+        K.attention_fp8(q8, k8, vp, o, H, q_exp, k_exp, out_scale=0.3, accumulate=True)
+        outs[vv] = o
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[var].float()).all()
+    assert torch.equal(outs["3"].view(torch.int16), outs[var].view(torch.int16))
 
 
 def _ln_rows(x, H):

@@ -30,6 +30,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 
 #include "vp_common.h"
 
@@ -2041,6 +2043,236 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
   }
 }
 
+// Skewed fp8 attention (variants 5 / 6): the lin-2 kernel above with the wave's tile loop turned by one tile —
+// QK^T of tile t is issued first, then PV and the row sums of tile t - 1, then the softmax of tile t — so the three
+// MFMAs of t - 1 (160 matrix cycles) cover the QK^T result latency that the unskewed loop waits out in s_nops (two
+// 17-state pads per tile).  The PV of t - 1 reads its V^T after the ring moved on by one tile, so the ring has 3
+// slots (SUB tiles each): the DMA into slot (i + 1) % 3 at superstep i cannot race a skewed read of slot (i - 1) % 3.
+// Each wave has ONE DMA source (waves 0-3: 16 K rows, 4-7: 16 V^T rows) as a wave-uniform base + tile stride and
+// one kept per-lane offset, so a tile's issue is an address add and the LDS-DMA (the last K tile, whose rows past
+// Nk re-read the last key, takes the clamped form).  Same arithmetic, same order of accumulation as variant 3
+// (bit-identical results, tests/test_attention_fp8_gpu.py).  The first skewed PV is a zero P against tile 0.
+constexpr int F8S_SLOTS = 3;
+typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+typedef __attribute__((address_space(3))) const unsigned short lds_u16;
+template <int SUB>
+__global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc dd) {
+  constexpr int NW = 8;
+  constexpr int OFF = 7;
+  constexpr float THR = 1.5f;
+  constexpr float USC = 0x1p-16f;
+  constexpr float LS = 8.f * USC;
+  constexpr float C0 = (8.f * OFF + 56.f - LIN_DELTA) * USC;
+  const vp_attn_desc& d = dd.base;
+  constexpr int QB = NW * 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 5;
+
+  const int nqb = (d.Nq + QB - 1) / QB;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb;
+  const int qb = t - bh * nqb;
+  const int b = bh / d.H;
+  const int h = bh - b * d.H;
+  const int ntiles = dd.npad >> 6;
+
+  const int q = qb * QB + wave * 32 + (lane & 31);
+  const int qc = q < d.Nq ? q : d.Nq - 1;
+  i32x8 qf;
+  {
+    const uint8_t* qrow = (const uint8_t*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+    u32x4* hq = (u32x4*)&qf;
+    hq[0] = *(const u32x4*)(qrow + g * 16);
+    hq[1] = *(const u32x4*)(qrow + (g + 2) * 16);
+  }
+  const int sq = (dd.qk_scale & 0xff) + 3 - 16, sk = (dd.qk_scale >> 8) & 0xff;
+
+  // DMA source of this wave: rows (wave & 3) * 16 + lane / 4 of each 64-row tile, physical chunk lane % 4 holding
+  // logical chunk (lane % 4) ^ swz8(row) (swz8(row) = (lane / 16) % 4 here)
+  const bool kw = wave < 4;
+  const int ksn = (int)d.k_sn;
+  const int pch = (lane & 3) ^ ((lane >> 4) & 3);
+  const int rstride = kw ? ksn : (int)dd.npad;
+  const int voff = (lane >> 2) * rstride + pch * 16;
+  const char* kbase = (const char*)d.K + (int64_t)b * d.k_sb + h * 64;
+  const char* src0 = kw ? kbase + (int64_t)(wave & 3) * 16 * ksn
+                        : (const char*)d.V + ((int64_t)bh * 64 + (wave & 3) * 16) * dd.npad;
+  const int64_t tstride = kw ? (int64_t)64 * ksn : 64;
+  const int nfull = kw ? d.Nk >> 6 : ntiles;  // tiles whose rows all lie below Nk
+  const char* vsbase = (const char*)dd.vs + (int64_t)bh * ntiles * 128;
+  const unsigned lds_smem = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem);
+  const unsigned lds_w = lds_smem + (kw ? wave * 1024 : F8_TILE + (wave - 4) * 1024);
+  const int nsup = (ntiles + SUB - 1) / SUB;
+  auto issue = [&](int ti, int slot) {
+#pragma unroll
+    for (int sb = 0; sb < SUB; ++sb) {
+      const int kt = ti * SUB + sb;
+      if (SUB > 1 && kt >= ntiles) break;  // wave-uniform
+      const unsigned st = lds_w + (slot * SUB + sb) * F8_STAGE;
+      if (kt < nfull) {
+        glds16_lds(src0 + kt * tstride, voff, st);
+      } else {  // the last K tile: rows past Nk re-read the last key (masked later)
+        const int ln = lane_id_opaque();
+        const int r = min(kt * 64 + (wave & 3) * 16 + (ln >> 2), d.Nk - 1);
+        glds16_lds(kbase, r * ksn + pch * 16, st);
+      }
+      if (wave == 0 && lane < 8) glds16_lds(vsbase + kt * 128, lane * 16, st + 2 * F8_TILE);
+    }
+  };
+
+  const int r0 = lane & 31;
+  // per-lane LDS addresses of the two 16-byte chunks of row r0 (K at +0, V^T at +F8_TILE, row + 32 at +2048) and
+  // of this lane's V^T scale pair, LDS base included: opaque, so each stays one VGPR and every tile's read is that
+  // VGPR + an immediate (the compiler re-derives base + lane offset per tile otherwise)
+  unsigned la = lds_smem + r0 * 64 + ((g ^ swz8(r0)) << 4), lb = lds_smem + r0 * 64 + (((g + 2) ^ swz8(r0)) << 4);
+  unsigned lsv = lds_smem + 2 * F8_TILE + lane * 2;
+  asm volatile("" : "+v"(la), "+v"(lb), "+v"(lsv));
+  // the QK^T scale operands held in VGPRs (2 registers; re-materialised from SGPRs they cost 2 v_mov per tile)
+  int skv = sk, sqv = sq;
+  asm volatile("" : "+v"(skv), "+v"(sqv));
+  float m_run = 0.f, thr = -INFINITY;
+  f32x16 o[2], negm;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    o[0][i] = 0.f;
+    o[1][i] = 0.f;
+    negm[i] = C0;
+  }
+  const int col = lane & 15, cq = lane >> 4;
+  const int selw = ((col == 0 && (cq & 1) == 0) || (col == 1 && (cq & 1) == 1)) ? 0x38383838 : 0;
+  f32x4 lsum = {0.f, 0.f, 0.f, 0.f};
+  // (no inactive waves: the last query block's waves past Nq run on clamped duplicate queries, store_out drops them)
+  i32x8 pf = {0, 0, 0, 0, 0, 0, 0, 0};
+  // the skewed PV + row sums of the previous tile (P in pf, its stage at byte offset pst: a constant at every call
+  // site inside the unrolled ring, so all LDS addresses are a kept lane base + an immediate offset)
+  auto load_v = [&](i32x8& vf, int pst, int dh) {
+    u32x4* hv = (u32x4*)&vf;
+    hv[0] = *(const lds_u32x4*)(uintptr_t)(la + pst + F8_TILE + dh * 2048);
+    hv[1] = *(const lds_u32x4*)(uintptr_t)(lb + pst + F8_TILE + dh * 2048);
+  };
+  auto pv_prev = [&](int pst) {
+    const int vsw = *(const lds_u16*)(uintptr_t)(lsv + pst);
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      i32x8 vf;
+      load_v(vf, pst, dh);
+      if (dh == 0)
+        o[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[0], 0, 0, 0, vsw, 0, 127);
+      else
+        o[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[1], 0, 0, 1, vsw, 0, 127);
+      // one V^T half live at a time (the scores of the next tile are live through this phase)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t wlo, whi;
+    asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %2" : "=v"(wlo), "=v"(whi) : "v"(selw));
+    const uint64_t w2 = ((uint64_t)whi << 32) | wlo;
+    uint64_t w3, w4, w5;
+    asm volatile("v_mov_b64 %0, %3\n\tv_mov_b64 %1, %3\n\tv_mov_b64 %2, %3" : "=v"(w3), "=v"(w4), "=v"(w5) : "v"(w2));
+    typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
+    const i32x8 sel = __builtin_bit_cast(i32x8, (u64x4){w2, w3, w4, w5});
+    lsum = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(sel, pf, lsum, 0, 0, 0, 127, 0, 127);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // one tile: QK^T of tile kt, the skewed PV + row sums of the previous tile, then the softmax of kt into pf.
+  // Keys past Nk (last tile) duplicate key Nk - 1 (the DMA clamp), so they leave the tile max as it is and only
+  // their P codes are zeroed, after the pack: the result equals variant 3's -inf scores bit for bit.
+  i32x8 kq[2];  // the K^T fragments of the tile
+  auto load_k = [&](int stoff) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      u32x4* hk = (u32x4*)&kq[hh];
+      hk[0] = *(const lds_u32x4*)(uintptr_t)(la + stoff + hh * 2048);
+      hk[1] = *(const lds_u32x4*)(uintptr_t)(lb + stoff + hh * 2048);
+    }
+  };
+  auto step = [&](int kt, int stoff, int pst) {
+    f32x16 s[2];
+    load_k(stoff);
+
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+      s[hh] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kq[hh], qf, negm, 0, 0, 0, skv, 0, sqv);
+    // phases pinned in program order: the K fragments die at the QK^T issue, before the V^T reads of pv_prev
+    __builtin_amdgcn_sched_barrier(0);
+    pv_prev(pst);
+    float mx = s[0][0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[0][i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = (fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) - C0) * (1.f / LS);
+    }
+    if (__ballot(mx > thr) != 0ull) {
+      const float dm = mx > thr ? mx : 0.f;
+      const float alpha = __builtin_amdgcn_exp2f(-dm);
+      const float a16 = __shfl(alpha, (lane_id_opaque() + 16) & 63, 64);
+      lsum[0] *= alpha;
+      lsum[1] *= a16;
+      m_run += dm;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        o[0][i] *= alpha;
+        o[1][i] *= alpha;
+        s[0][i] -= LS * dm;
+        s[1][i] -= LS * dm;
+        negm[i] = C0 - LS * m_run;
+      }
+      thr = THR;
+    }
+    f8_lin2_pack(s, pf);
+    const int lim = d.Nk - kt * 64;
+    if (lim < 64) {  // byte j of pf[4 hh + w] is key 32 hh + 8 w + 4 g + j (lane id opaque: nothing hoisted)
+      const int kb = 4 * (lane_id_opaque() >> 5);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int n = lim - (32 * (i >> 2) + 8 * (i & 3) + kb);
+        const unsigned mk = n >= 4 ? ~0u : n <= 0 ? 0u : (1u << (8 * n)) - 1u;
+        pf[i] &= (int)mk;
+      }
+    }
+  };
+  // the first skewed PV (superstep 0, sub-tile 0) reads the stage ring slot 2's last sub-tile would hold: zeroed
+  // V^T and scales there, against P = 0, add exactly 0
+  constexpr int ZST = ((F8S_SLOTS - 1) * SUB + SUB - 1) * F8_STAGE + F8_TILE;
+  if (tid < (F8_TILE + 128) / 16) *(u32x4*)(smem + ZST + tid * 16) = (u32x4){0u, 0u, 0u, 0u};
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // one superstep on ring slot SL (a constant): DMA of the next superstep into slot SL + 1, SUB tiles, barrier
+  auto superstep = [&](int ti, auto SLC) {
+    constexpr int SL = decltype(SLC)::value;
+    constexpr int NSL = SL == F8S_SLOTS - 1 ? 0 : SL + 1;
+    constexpr int PSL = SL == 0 ? F8S_SLOTS - 1 : SL - 1;
+    if (ti + 1 < nsup) issue(ti + 1, NSL);
+#pragma unroll
+    for (int sb = 0; sb < SUB; ++sb) {
+      const int kt = ti * SUB + sb;
+      if (SUB > 1 && kt >= ntiles) break;
+      step(kt, (SL * SUB + sb) * F8_STAGE, sb == 0 ? (PSL * SUB + SUB - 1) * F8_STAGE : (SL * SUB + sb - 1) * F8_STAGE);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int ti = 0; ti < nsup; ti += F8S_SLOTS) {
+    superstep(ti, std::integral_constant<int, 0>{});
+    if (ti + 1 < nsup) superstep(ti + 1, std::integral_constant<int, 1>{});
+    if (ti + 2 < nsup) superstep(ti + 2, std::integral_constant<int, 2>{});
+  }
+  {  // the last tile's PV
+    const int lt = ntiles - 1, lti = lt / SUB;
+    pv_prev(((lti % F8S_SLOTS) * SUB + lt - lti * SUB) * F8_STAGE);
+  }
+  const int qq = lane & 31;
+  const float v0 = __shfl(lsum[0], qq & 15, 64), v1 = __shfl(lsum[1], qq & 15, 64);
+  store_out(d, o, qq < 16 ? v0 : v1, q, b, h, g, false);
+}
+
 #if VP_ATTN_EXTRA_VARIANTS  // rejected A/B variant: outside the default library
 // ---- f8p (VP_ATTN8_VARIANT=4): the fp8 kernel as a software pipeline, the p1 schedule carried over to e4m3.  4 waves
 // x 32 queries per workgroup at two workgroups per CU (256 VGPRs: two score buffers live), an 8-tile LDS ring filled
@@ -2464,7 +2696,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
 extern "C" int vp_attention_variant_built(const char* name) {
   if (name != nullptr && strncmp(name, "fp8:", 4) == 0) {  // the fp8 kernel's VP_ATTN8_VARIANT values
     const int f = atoi(name + 4);
-    return f == 2 || f == 3 || ((f == 1 || f == 4) && VP_ATTN_EXTRA_VARIANTS) ? 1 : 0;
+    return f == 2 || f == 3 || f == 5 || ((f == 1 || f == 4) && VP_ATTN_EXTRA_VARIANTS) ? 1 : 0;
   }
   const int v = variant_by_name(name);
   return v >= 0 && attn_vars[v].fn != nullptr ? 1 : 0;
@@ -2577,6 +2809,10 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
   // barrier (1.43 against 1.46); 4 = f8p, the lin2 codes in a p1-style software pipeline at 2 waves/SIMD: parity
   // identical to 3, but 0.93-0.94x its speed (profiles/r03_f8p_ab_rejected.log: at two waves per SIMD the wave's own
   // instruction issue, ~13 VALU + ~6 SALU per MFMA, not the matrix pipe, sets the step), kept for A/B.
+  // 5 = the lin-2 kernel with its tile loop skewed by one tile (attn_fwd_fp8s; default since round 4: bit-identical
+  // to 3, 2.28-2.30 against 2.22-2.24 PF/s interleaved at config 5's length, profiles/r04_fp8_skew_ab.log; a 3-tile
+  // ring slot (1.26-1.71), K^T read one tile ahead (spills) and the first V^T half read beside K^T (-1.2 %) were
+  // measured and dropped).
   // variants 1 (exp2 + RNE) and 4 (f8p) are rejected A/B forms: built only with VP_ATTN_EXTRA_VARIANTS
 #if VP_ATTN_EXTRA_VARIANTS
   static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, 2, true, 0>,
@@ -2592,13 +2828,28 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
     for (int i = 0; i < 3; ++i)
       if (fns[i] != nullptr)
         (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * F8_STAGE);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_fp8s<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              F8S_SLOTS * 2 * F8_STAGE);
 #if VP_ATTN_EXTRA_VARIANTS
     (void)hipFuncSetAttribute((const void*)attn_fwd_fp8p, hipFuncAttributeMaxDynamicSharedMemorySize, F8P_LDS);
 #endif
   }
   const char* e = getenv("VP_ATTN8_VARIANT");
   int variant = e != nullptr ? atoi(e) : 0;
-  if (variant < 1 || variant > 4) variant = 3;
+  if (variant < 1 || variant > 5) variant = 5;
+  if (variant == 5) {  // the skewed loop (default)
+    constexpr int sub = 2;
+    const int nqb5 = (d.Nq + NW * 32 - 1) / (NW * 32);
+    const int64_t grid5 = (int64_t)d.B * d.H * nqb5;
+    if (grid5 > 0x7fffffff) return VP_ERR_ARG;
+    void* args5[] = {(void*)dd};
+    const hipError_t le5 =
+        hipLaunchKernel((const void*)attn_fwd_fp8s<sub>, dim3((unsigned)grid5),
+                        dim3(NW * 64), args5, F8S_SLOTS * sub * F8_STAGE, (hipStream_t)stream);
+    if (le5 != hipSuccess) return (int)le5;
+    VP_CHECK_LAUNCH();
+    return VP_OK;
+  }
 #if !VP_ATTN_EXTRA_VARIANTS
   if (variant == 1 || variant == 4) return VP_ERR_UNSUPPORTED;
 #else
