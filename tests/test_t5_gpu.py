@@ -71,6 +71,33 @@ def test_t5_attention_matches_torch(K, L, H, masked):
     assert r < 1e-2
 
 
+@pytest.mark.parametrize("L,H,masked", [(226, 64, False), (226, 2, True), (77, 4, False), (33, 3, True),
+                                         (384, 2, False)])
+def test_t5_attention_mfma_matches_scalar_kernel(K, L, H, masked, monkeypatch):
+    """The MFMA T5 attention (default) against the scalar-FMA kernel (VP_T5_ATTN=scalar) on the same operands: the
+    same roundings (bf16 scores + bias, fp32 softmax, bf16 weights), only the fp32 summation orders differ, so the
+    outputs agree to a few bf16 ulps; key padding (L not a multiple of 32) and masked keys included."""
+    from videopainter_amd.t5 import relative_position_buckets
+    torch.manual_seed(7 * L + H)
+    B = 2
+    qkv = (0.25 * torch.randn(B * L, 3 * H * 64, device="cuda")).bfloat16()
+    table = (0.5 * torch.randn(32, H, device="cuda")).bfloat16()
+    buckets = relative_position_buckets(L, 32, 128).cuda()
+    mask = None
+    if masked:
+        mask = torch.ones(B, L, dtype=torch.int64, device="cuda")
+        mask[0, L // 3:] = 0
+        mask[1, L - 5:] = 0
+    out = K.t5_attention(qkv, B, L, H, table, buckets, mask)
+    monkeypatch.setenv("VP_T5_ATTN", "scalar")
+    ref = K.t5_attention(qkv, B, L, H, table, buckets, mask)
+    r = rel(out.float(), ref.float())
+    print(f"t5 attention mfma vs scalar L={L} H={H} masked={masked}: rel {r:.2e}, "
+          f"max |d| {(out.float() - ref.float()).abs().max().item():.2e}")
+    assert torch.isfinite(out.float()).all()
+    assert r < 3e-3
+
+
 def _model(cfg, seed):
     from videopainter_amd.t5 import T5EncoderModel
     from tests.golden.cases import t5_weights

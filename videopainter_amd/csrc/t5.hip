@@ -5,6 +5,9 @@
 // Reference algorithm: transformers `modeling_t5.py` (pinned transformers==4.42.2 in the reference's
 // requirements.txt): T5LayerNorm, T5DenseGatedActDense, T5Attention (compute_bias / _relative_position_bucket),
 // called by the pipeline's `_get_t5_prompt_embeds` (…_anyl.py:216-256).
+#include <stdlib.h>
+#include <string.h>
+
 #include "vp_common.h"
 
 namespace {
@@ -175,6 +178,141 @@ __global__ __launch_bounds__(256) void t5_attention_kernel(const bf16* __restric
   }
 }
 
+// MFMA form (default; the scalar kernel above stays as the A/B, VP_T5_ATTN=scalar).  One workgroup per (batch, head,
+// 64 queries), 4 waves x 16 queries.  K [Lp][64] (16-byte chunk c of row r at c ^ (r & 7)) and V^T [64][Lp + 4] of
+// the head in LDS, keys padded to whole 32-key chunks (zero rows).  S^T = K Q^T on v_mfma_f32_16x16x32_bf16 (A = 16
+// key rows from LDS, B = this wave's 16 queries from global, two MFMAs per 16 keys over d = 64): lane (ql, g) holds
+// the scores of query ql for keys 16 kb + 4 g + r.  The same roundings as the scalar kernel: bf16(q.k) + bias (bf16
+// add), the dtype minimum on masked keys, fp32 softmax (max / sum across the 4 lane groups), bf16 weights; then
+// O^T = V^T P^T on the same MFMA, 32 keys per step: the B operand's K-slots 8 g .. 8 g + 7 hold this lane's keys
+// {4 g .. 4 g + 3} and {16 + 4 g .. 16 + 4 g + 3} of the chunk straight from the score layout, and the A operand
+// reads V^T at the same keys (two 8-byte reads per row).  fp32 accumulation, one bf16 rounding at the store.
+constexpr int T5M_MAXKB = T5_MAX_L / 16;
+
+__global__ __launch_bounds__(256, 2) void t5_attention_mfma_kernel(const bf16* __restrict__ qkv, int64_t ld, int inner,
+                                                                int L, int H, const bf16* __restrict__ bias_table,
+                                                                const int32_t* __restrict__ buckets,
+                                                                const int64_t* __restrict__ mask, bf16* __restrict__ out,
+                                                                int64_t ldo) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int Lp = (L + 31) & ~31;
+  const int VS = Lp + 4;
+  bf16* Ks = (bf16*)smem;              // [Lp][64]
+  bf16* Vt = Ks + Lp * 64;             // [64][VS]
+  float* Bs = (float*)(Vt + 64 * VS);  // [2 Lp]: bias by relative position j - q + L - 1
+  float* Ms = Bs + 2 * Lp;             // [Lp]: 1 where the key is masked
+  const int nqb = (L + 63) / 64;
+  const int bh = blockIdx.x / nqb, qb = blockIdx.x - bh * nqb;
+  const int b = bh / H, h = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16* base = qkv + (int64_t)b * L * ld;
+  for (int i = tid; i < Lp * 8; i += 256) {
+    const int j = i >> 3, c = i & 7;
+    bf16x8 kv, vv;
+    if (j < L) {
+      kv = *(const bf16x8*)(base + (int64_t)j * ld + inner + h * 64 + c * 8);
+      vv = *(const bf16x8*)(base + (int64_t)j * ld + 2 * inner + h * 64 + c * 8);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) kv[e] = vv[e] = (bf16)0.f;
+    }
+    *(bf16x8*)(Ks + j * 64 + ((c ^ (j & 7)) << 3)) = kv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) Vt[(c * 8 + e) * VS + j] = vv[e];
+  }
+  for (int r = tid; r < 2 * L - 1; r += 256) {
+    const int rel = r - (L - 1);
+    const int bk = rel >= 0 ? buckets[rel] : buckets[(int64_t)(-rel) * L];
+    Bs[r] = bf2f(bias_table[bk * H + h]);
+  }
+  for (int j = tid; j < L; j += 256) Ms[j] = (mask != nullptr && mask[(int64_t)b * L + j] == 0) ? 1.f : 0.f;
+  __syncthreads();
+
+  const int ql = lane & 15, g = lane >> 4;
+  const int q = qb * 64 + wave * 16 + ql;
+  const int qc = q < L ? q : L - 1;  // rows past L compute on the last query and are not stored
+  const bf16* qrow = base + (int64_t)qc * ld + h * 64;
+  const bf16x8 qf0 = *(const bf16x8*)(qrow + 8 * g), qf1 = *(const bf16x8*)(qrow + 32 + 8 * g);
+  const int nkb = Lp >> 4;
+  f32x4 s[T5M_MAXKB];
+#pragma unroll
+  for (int kb = 0; kb < T5M_MAXKB; ++kb) {
+    if (kb < nkb) {  // wave-uniform (no break: the loop must unroll for s[] to stay in registers)
+      const int r = kb * 16 + ql;
+      const bf16x8 a0 = *(const bf16x8*)(Ks + r * 64 + ((g ^ (r & 7)) << 3));
+      const bf16x8 a1 = *(const bf16x8*)(Ks + r * 64 + (((4 + g) ^ (r & 7)) << 3));
+      f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, qf0, z, 0, 0, 0);
+      s[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, qf1, z, 0, 0, 0);
+    }
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < T5M_MAXKB; ++kb) {
+    if (kb < nkb) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = kb * 16 + 4 * g + r;
+        float t = -INFINITY;
+        if (k < L) {
+          t = rbf(rbf(s[kb][r]) + Bs[k - qc + L - 1]);
+          if (Ms[k] != 0.f) t = rbf(t + -3.3895313892515355e38f);
+        }
+        s[kb][r] = t;
+        mx = fmaxf(mx, t);
+      }
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < T5M_MAXKB; ++kb) {
+    if (kb < nkb) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = kb * 16 + 4 * g + r < L ? __expf(s[kb][r] - mx) : 0.f;
+        s[kb][r] = p;
+        sum += p;
+      }
+    }
+  }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+  f32x4 o[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) o[db] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < T5M_MAXKB / 2; ++c) {
+    if (2 * c < nkb) {
+      bf16x8 pb;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pb[r] = f2bf(s[2 * c][r] * inv);
+        pb[4 + r] = f2bf(s[2 * c + 1][r] * inv);
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const bf16* vr = Vt + (db * 16 + ql) * VS + 32 * c + 4 * g;
+        const bf16x4 lo = *(const bf16x4*)vr, hi = *(const bf16x4*)(vr + 16);
+        const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, o[db], 0, 0, 0);
+      }
+    }
+  }
+  if (q < L) {
+    bf16* orow = out + (int64_t)(b * L + q) * ldo + h * 64;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      bf16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[db][r]);
+      *(bf16x4*)(orow + db * 16 + 4 * g) = v;
+    }
+  }
+}
+
 int grid_for(int64_t work) {
   const int64_t g = (work + 255) / 256;
   return (int)(g < 1 ? 1 : (g > (1 << 20) ? (1 << 20) : g));
@@ -215,6 +353,24 @@ extern "C" int vp_t5_attention_bf16(const void* qkv, int64_t ld, int32_t inner, 
   if (qkv == nullptr || bias_table == nullptr || buckets == nullptr || out == nullptr) return VP_ERR_ARG;
   if (B <= 0 || L <= 0 || H <= 0 || inner != H * 64 || ld < 3 * inner || (ld % 8) || ldo < inner) return VP_ERR_ARG;
   if (L > T5_MAX_L) return VP_ERR_UNSUPPORTED;
+  const char* ev = getenv("VP_T5_ATTN");
+  if (ev == nullptr || strcmp(ev, "scalar") != 0) {  // the MFMA kernel (default)
+    if ((ldo % 4) != 0) return VP_ERR_ARG;
+    const size_t Lp32 = (size_t)((L + 31) & ~31);
+    const size_t lds_m = Lp32 * 64 * 2 + 64 * (Lp32 + 4) * 2 + 3 * Lp32 * 4;
+    static bool attr_m = false;
+    if (!attr_m) {
+      const size_t mx = (size_t)T5_MAX_L * 64 * 2 + 64 * (T5_MAX_L + 4) * 2 + 3 * T5_MAX_L * 4;
+      (void)hipFuncSetAttribute((const void*)t5_attention_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)mx);
+      attr_m = true;
+    }
+    const int nqb_m = (L + 63) / 64;
+    hipLaunchKernelGGL(t5_attention_mfma_kernel, dim3(B * H * nqb_m), dim3(256), lds_m, (hipStream_t)stream,
+                       (const bf16*)qkv, ld, inner, L, H, (const bf16*)bias_table, buckets, mask, (bf16*)out, ldo);
+    VP_CHECK_LAUNCH();
+    return 0;
+  }
   const size_t Lp = (size_t)((L + 7) & ~7);
   const size_t lds = Lp * KROW * 2 + Lp * 64 * 2 + 3 * Lp * 4 + 4 * QW * Lp * 2;
   static bool attr = false;
