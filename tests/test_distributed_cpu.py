@@ -4,10 +4,29 @@ import os
 import socket
 
 import pytest
+import numpy as np
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+
+
+def _portable(x):
+    """Tensors crossing the result queue as numpy copies: a queued torch tensor is shared by file descriptor through
+    the sending process, which may already have exited when the parent reads it (FileNotFoundError under load)."""
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy().copy()
+    if isinstance(x, (list, tuple)):
+        return type(x)(_portable(v) for v in x)
+    return x
+
+
+def _restore(x):
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(x)
+    if isinstance(x, (list, tuple)):
+        return type(x)(_restore(v) for v in x)
+    return x
 
 def _free_port():
     s = socket.socket()
@@ -35,7 +54,7 @@ def _worker(rank, world, port, q, method="scatter_allgather"):
     if rank == 0:
         assert all(torch.equal(a, b) for a, b in zip(want, m.state_dict().values()))
     t = max_over_ranks(1.0 + rank)
-    q.put((rank, digest, t))
+    q.put(_portable((rank, digest, t)))
     dist.destroy_process_group()
 
 
@@ -51,7 +70,7 @@ def test_broadcast_and_max_over_ranks_gloo(world, method):
     ps = [ctx.Process(target=_worker, args=(r, world, port, q, method)) for r in range(world)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=240) for _ in ps]
+    res = [_restore(q.get(timeout=240)) for _ in ps]
     for p in ps:
         p.join(60)
     res.sort()
@@ -78,7 +97,7 @@ def _digest_worker(rank, world, port, q):
             w = m.transformer_blocks[1].attn1.to_k.weight
             w.view(torch.int16)[3, 5] ^= 1
     corrupted = verify_replicas(m, bucket_bytes=1 << 16)
-    q.put((rank, before, after, corrupted))
+    q.put(_portable((rank, before, after, corrupted)))
     dist.destroy_process_group()
 
 
@@ -93,7 +112,7 @@ def test_replica_digests_detect_divergence_gloo():
     ps = [ctx.Process(target=_digest_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = sorted(q.get(timeout=240) for _ in ps)
+    res = sorted(_restore(q.get(timeout=240)) for _ in ps)
     for p in ps:
         p.join(60)
     for _, before, after, corrupted in res:
@@ -126,7 +145,7 @@ def _bench_worker(rank, world, port, mode, q):
     elapsed = bench.timed_steps(one, lambda: barrier(), warmup=2, steps=3)
     emax = max_over_ranks(elapsed)
     n_clips, value = bench.job_value(emax, 3, world, mode)
-    q.put((rank, clip, state["x"].clone(), elapsed, emax, n_clips, value))
+    q.put(_portable((rank, clip, state["x"].clone(), elapsed, emax, n_clips, value)))
     dist.destroy_process_group()
 
 
@@ -142,7 +161,7 @@ def test_bench_rank_logic_gloo(mode):
     ps = [ctx.Process(target=_bench_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = sorted([q.get(timeout=240) for _ in ps], key=lambda r: r[0])
+    res = sorted([_restore(q.get(timeout=240)) for _ in ps], key=lambda r: r[0])
     for p in ps:
         p.join(60)
     emax = max(r[3] for r in res)
@@ -247,7 +266,7 @@ def _chain_worker(rank, world, port, cfg_split, n_clips, n_windows, q):
     rows = 1 if cfg_split else 2
     vids = run_window_chain(stages, clips, _toy_window(stages.pair, clips), _image_for, _assemble,
                             torch.empty(SHAPE), (rows, NTOK, DD), (rows, NTOK))
-    q.put((rank, [v.clone() for v in vids]))
+    q.put(_portable((rank, [v.clone() for v in vids])))
     dist.destroy_process_group()
 
 
@@ -259,7 +278,7 @@ def _run(world, cfg_split, n_clips, n_windows):
           for r in range(world)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=240) for _ in ps]
+    res = [_restore(q.get(timeout=240)) for _ in ps]
     for p in ps:
         p.join(60)
     return res
@@ -288,7 +307,7 @@ def _concurrent_worker(rank, world, port, n_windows, q):
         return win["x"] * 2 + w
 
     out = run_windows_concurrent(wins, rw, _assemble, torch.empty(SHAPE))
-    q.put((rank, out.clone(), ran))
+    q.put(_portable((rank, out.clone(), ran)))
     dist.destroy_process_group()
 
 
@@ -304,7 +323,7 @@ def test_concurrent_windows_allgather_gloo():
     ps = [ctx.Process(target=_concurrent_worker, args=(r, world, port, n_windows, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=100) for _ in ps]
+    res = [_restore(q.get(timeout=100)) for _ in ps]
     for p in ps:
         p.join(60)
     for rank, out, ran in res:

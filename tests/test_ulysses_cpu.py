@@ -3,11 +3,30 @@ communicator's semantics against the thread-emulated one — on the CPU (gloo, w
 import socket
 
 import pytest
+import numpy as np
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from videopainter_amd.ulysses import Shard, ThreadComm, DistComm, qkv_to_heads, heads_to_rows
+
+
+def _portable(x):
+    """Tensors crossing the result queue as numpy copies: a queued torch tensor is shared by file descriptor through
+    the sending process, which may already have exited when the parent reads it (FileNotFoundError under load)."""
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy().copy()
+    if isinstance(x, (list, tuple)):
+        return type(x)(_portable(v) for v in x)
+    return x
+
+
+def _restore(x):
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(x)
+    if isinstance(x, (list, tuple)):
+        return type(x)(_restore(v) for v in x)
+    return x
 
 
 @pytest.mark.parametrize("N,T,P", [(17776, 226, 8), (1378, 226, 4), (298, 10, 4), (600, 226, 2), (80, 30, 2)])
@@ -74,7 +93,7 @@ def _worker(rank, world, port, q):
     full = qkv_to_heads(comm, rank, g[:, rank * n:(rank + 1) * n].contiguous())
     back = heads_to_rows(comm, rank, full[..., :H * 64 // world].contiguous())
     gat = comm.all_gather(rank, torch.full((2, 3), float(rank)))
-    q.put((rank, full, back, gat))
+    q.put(_portable((rank, full, back, gat)))
     dist.destroy_process_group()
 
 
@@ -87,7 +106,7 @@ def test_dist_comm_matches_thread_comm_gloo():
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = sorted([q.get(timeout=240) for _ in ps], key=lambda t: t[0])
+    res = sorted([_restore(q.get(timeout=240)) for _ in ps], key=lambda t: t[0])
     for p in ps:
         p.join(60)
     B, n, H = 2, 3, 4
