@@ -1969,11 +1969,14 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
         for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
         {
           const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-          mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) - C0;
-          if constexpr (LIN) mx *= 1.f / LS;
+          mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
         }
+        // the threshold in accumulator units (thr = -inf, then C0 + LS THR): the log2-unit max is formed only on
+        // the (rare) rescale path
         if (__ballot(mx > thr) != 0ull) {
-          const float dm = mx > thr ? mx : 0.f;
+          float ml = mx - C0;
+          if constexpr (LIN) ml *= 1.f / LS;
+          const float dm = mx > thr ? ml : 0.f;
           const float alpha = __builtin_amdgcn_exp2f(-dm);
           if constexpr (RS) {
             // lane n < 16 holds the sums of queries n (this lane's) and n + 16 (lane n + 16's)
@@ -1992,7 +1995,7 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
             s[1][i] -= LS * dm;
             negm[i] = C0 - LS * m_run;
           }
-          thr = THR;
+          thr = C0 + LS * THR;
         }
         i32x8 pf;
         float ls = 0.f;
@@ -2206,10 +2209,10 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc d
     for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
     {
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = (fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) - C0) * (1.f / LS);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
     }
-    if (__ballot(mx > thr) != 0ull) {
-      const float dm = mx > thr ? mx : 0.f;
+    if (__ballot(mx > thr) != 0ull) {  // thr in accumulator units, as in attn_fwd_fp8
+      const float dm = mx > thr ? (mx - C0) * (1.f / LS) : 0.f;
       const float alpha = __builtin_amdgcn_exp2f(-dm);
       const float a16 = __shfl(alpha, (lane_id_opaque() + 16) & 63, 64);
       lsum[0] *= alpha;
@@ -2223,7 +2226,7 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc d
         s[1][i] -= LS * dm;
         negm[i] = C0 - LS * m_run;
       }
-      thr = THR;
+      thr = C0 + LS * THR;
     }
     f8_lin2_pack(s, pf);
     const int lim = d.Nk - kt * 64;
@@ -2812,7 +2815,7 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
   // 5 = the lin-2 kernel with its tile loop skewed by one tile (attn_fwd_fp8s; default since round 4: bit-identical
   // to 3, 2.28-2.30 against 2.22-2.24 PF/s interleaved at config 5's length, profiles/r04_fp8_skew_ab.log; a 3-tile
   // ring slot (1.26-1.71), K^T read one tile ahead (spills) and the first V^T half read beside K^T (-1.2 %) were
-  // measured and dropped).
+  // measured and dropped; so was its MFMA issue at raised wave priority, within noise, profiles/r04_skew3_ab.log).
   // variants 1 (exp2 + RNE) and 4 (f8p) are rejected A/B forms: built only with VP_ATTN_EXTRA_VARIANTS
 #if VP_ATTN_EXTRA_VARIANTS
   static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, 2, true, 0>,
