@@ -2815,7 +2815,7 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
   // 5 = the lin-2 kernel with its tile loop skewed by one tile (attn_fwd_fp8s; default since round 4: bit-identical
   // to 3, 2.28-2.30 against 2.22-2.24 PF/s interleaved at config 5's length, profiles/r04_fp8_skew_ab.log; a 3-tile
   // ring slot (1.26-1.71), K^T read one tile ahead (spills) and the first V^T half read beside K^T (-1.2 %) were
-  // measured and dropped; so was its MFMA issue at raised wave priority, within noise, profiles/r04_skew3_ab.log).
+  // measured and dropped; so was its MFMA issue at raised wave priority, within noise, profiles/r04_fp8_prio_ab_rejected.log).
   // variants 1 (exp2 + RNE) and 4 (f8p) are rejected A/B forms: built only with VP_ATTN_EXTRA_VARIANTS
 #if VP_ATTN_EXTRA_VARIANTS
   static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, 2, true, 0>,
