@@ -272,6 +272,11 @@ VP_DEV void glds16_asm(const void* src, char* lds) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(la), "v"(src) : "memory", "m0");
 }
 
+// V2 (default, VP_CONV_PIPE=2; 1 = the round-3 form): the tap's 4 frame-map reads issued together (each was a
+// branch with its own lgkmcnt(0) wait, run by all 8 waves at once right after the barrier with the matrix pipe idle),
+// both half-steps' fragments read before the first MFMA, and the next DMA + tap math issued between the two groups of
+// 16 MFMAs, so that address work runs beside the matrix pipe.
+template <bool V2>
 __global__ __launch_bounds__(PNT, 1) void conv3d_pipe_kernel(const vp_conv3d_desc d) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* tmapl = (int*)(smem + PSLOTS * P_STAGE);
@@ -335,13 +340,18 @@ __global__ __launch_bounds__(PNT, 1) void conv3d_pipe_kernel(const vp_conv3d_des
     const int rem = tap - dt * khw;
     const int dy = d.kw == 1 ? rem : rem / 3;
     const int dx = rem - dy * d.kw;
+    int fm[P_AI];  // V2: the frame maps of the 4 rows read together (rt + dt <= Tout + kt - 2 for every row)
+    if constexpr (V2) {
+#pragma unroll
+      for (int i = 0; i < P_AI; ++i) fm[i] = tmapl[rt[i] + dt];
+    }
 #pragma unroll
     for (int i = 0; i < P_AI; ++i) {
       const int r = (i * 8 + wave) * 8 + (lane >> 3);
       const int yu = ry[i] + dy, xu = rx[i] + dx;
       const bf16* p = nullptr;
       if (rv[i] && yu >= 0 && yu < Hu && xu >= 0 && xu < Wu) {
-        const int f = tmapl[rt[i] + dt];
+        const int f = V2 ? fm[i] : tmapl[rt[i] + dt];
         const int64_t pix = (f >= 0 ? (int64_t)rb[i] * d.x_frames + f : (int64_t)rb[i] * d.hist_frames + (-1 - f)) *
                                 HWi + (int64_t)(yu >> ush) * d.Win + (xu >> usw);
         p = (f >= 0 ? X : Hs) + pix * d.Cin;
@@ -377,8 +387,41 @@ __global__ __launch_bounds__(PNT, 1) void conv3d_pipe_kernel(const vp_conv3d_des
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 2 < nk) stage(kt + 2, smem + ((kt + 2) % PSLOTS) * P_STAGE);
     const char* cur = smem + (kt % PSLOTS) * P_STAGE;
+    if constexpr (V2) {
+      bf16x8 af[2][FM], wf[2][FN];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = wr * WM + i * 16 + lrow;
+          af[ks][i] = *(const bf16x8*)(cur + row * 128 + ((ch ^ cswz(row)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = wc * WN + j * 16 + lrow;
+          wf[ks][j] = *(const bf16x8*)(cur + P_A + row * 128 + ((ch ^ cswz(row)) << 4));
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][j], af[ks][i], acc[j][i], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        if (ks == 0) {  // the next DMA (and, on a tap change, its gather addresses) beside the first 16 MFMAs
+          __builtin_amdgcn_sched_barrier(0);
+          if (kt + 2 < nk) stage(kt + 2, smem + ((kt + 2) % PSLOTS) * P_STAGE);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      continue;
+    }
+    if (kt + 2 < nk) stage(kt + 2, smem + ((kt + 2) % PSLOTS) * P_STAGE);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + (lane >> 4);
@@ -776,17 +819,25 @@ extern "C" int vp_conv3d_bf16(const vp_conv3d_desc* d, void* stream) {
     if (t >= (1ll << 31)) return VP_ERR_UNSUPPORTED;
     return launch_conv<64>(*d, c8s, t, s);
   }
-  // wide convolutions (Cin >= 64): the counted-vmcnt pipeline; VP_CONV_PIPE=0 keeps the 2-stage ring (A/B)
+  // wide convolutions (Cin >= 64): the counted-vmcnt pipeline (VP_CONV_PIPE: 2 = V2, default; 1 = its round-3 form;
+  // 0 = the 2-stage ring; A/B)
   const char* pe = getenv("VP_CONV_PIPE");
-  if (d->Cin >= 64 && (pe == nullptr || atoi(pe) != 0)) {
+  const int pipe = pe != nullptr ? atoi(pe) : 2;
+  if (d->Cin >= 64 && pipe != 0) {
     const int64_t t = ((M + PBM - 1) / PBM) * ((d->Cout + PBN - 1) / PBN);
     if (t >= (1ll << 31)) return VP_ERR_UNSUPPORTED;
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)conv3d_pipe_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, P_LDS);
+      (void)hipFuncSetAttribute((const void*)conv3d_pipe_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                P_LDS);
+      (void)hipFuncSetAttribute((const void*)conv3d_pipe_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                P_LDS);
       attr = true;
     }
-    hipLaunchKernelGGL(conv3d_pipe_kernel, dim3((unsigned)t), dim3(PNT), P_LDS, s, *d);
+    if (pipe == 1)
+      hipLaunchKernelGGL(conv3d_pipe_kernel<false>, dim3((unsigned)t), dim3(PNT), P_LDS, s, *d);
+    else
+      hipLaunchKernelGGL(conv3d_pipe_kernel<true>, dim3((unsigned)t), dim3(PNT), P_LDS, s, *d);
     VP_CHECK_LAUNCH();
     return VP_OK;
   }
