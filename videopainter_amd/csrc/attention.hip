@@ -2091,6 +2091,9 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc d
     hq[0] = *(const u32x4*)(qrow + g * 16);
     hq[1] = *(const u32x4*)(qrow + (g + 2) * 16);
   }
+  // Q's loads complete here, before the first LDS-DMA: the compiler cannot see the asm DMAs, so a vmcnt wait for Q
+  // left to the first MFMA inside the loop would also wait for the DMA that superstep has just issued
+  asm volatile("" ::"v"(qf));
   const int sq = (dd.qk_scale & 0xff) + 3 - 16, sk = (dd.qk_scale >> 8) & 0xff;
 
   // DMA source of this wave: rows (wave & 3) * 16 + lane / 4 of each 64-row tile, physical chunk lane % 4 holding
@@ -2138,11 +2141,15 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc d
   asm volatile("" : "+v"(skv), "+v"(sqv));
   float m_run = 0.f, thr = -INFINITY;
   f32x16 o[2], negm;
+  // the initial C operand from an opaque copy of C0: otherwise the compiler ties the rescale path's C0 to the initial
+  // splat and keeps a 16-register tuple of it in scratch (68 B per lane, stored by every wave: +0.5 GB of writes)
+  float c0v = C0;
+  asm volatile("" : "+v"(c0v));
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     o[0][i] = 0.f;
     o[1][i] = 0.f;
-    negm[i] = C0;
+    negm[i] = c0v;
   }
   const int col = lane & 15, cq = lane >> 4;
   const int selw = ((col == 0 && (cq & 1) == 0) || (col == 1 && (cq & 1) == 1)) ? 0x38383838 : 0;
