@@ -1967,13 +1967,14 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
         for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[0][i]);
 #pragma unroll
         for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
-        {
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-          mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-        }
-        // the threshold in accumulator units (thr = -inf, then C0 + LS THR): the log2-unit max is formed only on
-        // the (rare) rescale path
+        // the threshold in accumulator units (thr = -inf, then C0 + LS THR), tested on each lane's half-row max: a
+        // query's max (its two lanes, l and l ^ 32) passes iff one of them does, so the ballot decides the same and
+        // the pair max and its log2-unit form are computed only on the (rare) rescale path
         if (__ballot(mx > thr) != 0ull) {
+          {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+            mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+          }
           float ml = mx - C0;
           if constexpr (LIN) ml *= 1.f / LS;
           const float dm = mx > thr ? ml : 0.f;
@@ -2214,11 +2215,11 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc d
     for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[0][i]);
 #pragma unroll
     for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
-    {
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-    }
-    if (__ballot(mx > thr) != 0ull) {  // thr in accumulator units, as in attn_fwd_fp8
+    if (__ballot(mx > thr) != 0ull) {  // per-lane half-row max against thr in accumulator units, as in attn_fwd_fp8
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      }
       const float dm = mx > thr ? (mx - C0) * (1.f / LS) : 0.f;
       const float alpha = __builtin_amdgcn_exp2f(-dm);
       const float a16 = __shfl(alpha, (lane_id_opaque() + 16) & 63, 64);
