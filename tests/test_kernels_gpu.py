@@ -872,6 +872,37 @@ def test_attention_k2_len_and_l_extra(mode, split, monkeypatch):
 
 
 @pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
+@pytest.mark.parametrize("mode", ["p2a", "p2"])
+def test_attention_segment2_fast_path_bit_identical(mode, split, monkeypatch):
+    """Segment 2 with segment 1's row strides (the resample processor's layout: K2 / V2 as slices of a [B, N, 3D]
+    buffer) streams its full 128-key tiles on segment 1's precomputed lane offsets; the same keys as contiguous
+    tensors take the general DMA path.  Only the addressing differs, so the outputs are equal bit for bit — with
+    k2_len leaving partial and whole-tile segment ends (0, 128, 300, 1024 keys) and l_extra."""
+    from videopainter_amd import kernels as K
+    need_variant(mode, monkeypatch)
+    kw = {} if mode in UNBOUNDED_VARIANTS else dict(bounded_scores=True)
+    if not split:
+        monkeypatch.setenv("VP_ATTN_NO_SPLIT", "1")
+    B, H, Nn = 4, 2, 700
+    D = H * 64
+    qkv = bf(rnd(B, Nn, 3 * D, seed=61) * 0.5).to(dev)
+    q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
+    kv2 = bf(rnd(B, 1024, 3 * D, seed=62) * 0.5).to(dev)
+    k2s, v2s = kv2[..., :D], kv2[..., D:2 * D]
+    assert k2s.stride(1) == k.stride(1) and v2s.stride(1) == v.stride(1)
+    klen = torch.tensor([300, 0, 1024, 128], dtype=torch.int32, device=dev)
+    lx = (rnd(B, H, Nn, seed=63) * 4.0 + 3.0).to(dev)
+    outs = []
+    for k2, v2 in ((k2s, v2s), (k2s.contiguous(), v2s.contiguous())):
+        o = torch.empty(B, Nn, D, device=dev, dtype=torch.bfloat16)
+        K.attention(q, k, v, o, H, k2=k2, v2=v2, k2_len=klen, l_extra=lx, **kw)
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+
+
+@pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
 @pytest.mark.parametrize("spread", [False, True], ids=["even", "spread"])
 @pytest.mark.parametrize("mode", ["p2a", "a16", "p2", "s16", "lazy"])
 def test_attention_lse_matches_reference(mode, spread, split, monkeypatch):

@@ -324,8 +324,15 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
         if qkv is None:  # (the block may hand over an fp8 projection)
             qkv = _qkv(attn, x, (text_len, rope) if fused else None)
         q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
-        k2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
-        v2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
+        # segment 2 with the row stride of the fused QKV output (3 D): the attention kernel then streams its full tiles
+        # on the same precomputed lane offsets as segment 1
+        # (VP_RESAMPLE_K2_STRIDED=0: contiguous k2 / v2, the general per-lane DMA path; A/B)
+        if os.environ.get("VP_RESAMPLE_K2_STRIDED", "1") != "0":
+            kv2 = torch.empty(B, Ntok, 3 * D, device=x.device, dtype=BF16)
+            k2, v2 = kv2[..., :D], kv2[..., D:2 * D]
+        else:
+            k2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
+            v2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
         if prev:
             pkv = _kv(attn, prev_hidden_states.to(BF16).contiguous())
             w = float(prev_clip_weight)

@@ -1066,12 +1066,20 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
   const char* kseg1 = (const char*)((const bf16*)d.K + (int64_t)b * d.k_sb + h * 64);
   const char* vseg1 = (const char*)((const bf16*)d.V + (int64_t)b * d.v_sb + h * 64);
   const int full1 = d.Nk / KB;
+  // segment 2 (the resample processor's masked keys) takes the same fast path for its full tiles when its rows have
+  // segment 1's strides (the processor allocates them so): the same lane offsets, its own base
+  const bool seg2fast = d.K2 != nullptr && d.k2_sn == d.k_sn && d.v2_sn == d.v_sn;
+  const int full2 = seg2fast ? n2 / KB : 0;
+  const char* kseg2 = seg2fast ? (const char*)((const bf16*)d.K2 + (int64_t)b * d.k2_sb + h * 64) : nullptr;
+  const char* vseg2 = seg2fast ? (const char*)((const bf16*)d.V2 + (int64_t)b * d.v2_sb + h * 64) : nullptr;
   const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem) + wave * 1024;
   auto issue = [&](int ti) {
-    if (ti < full1) {
+    const bool s1 = ti < full1;
+    if (s1 || (ti >= tiles1 && ti - tiles1 < full2)) {
       const unsigned la = lds0 + (ti & (SL - 1)) * ST;
-      const char* kb = kseg1 + (int64_t)ti * KB * d.k_sn * 2;
-      const char* vb = vseg1 + (int64_t)ti * KB * d.v_sn * 2;
+      const int tt = s1 ? ti : ti - tiles1;
+      const char* kb = (s1 ? kseg1 : kseg2) + (int64_t)tt * KB * d.k_sn * 2;
+      const char* vb = (s1 ? vseg1 : vseg2) + (int64_t)tt * KB * d.v_sn * 2;
 #pragma unroll
       for (int i = 0; i < PPW4; ++i) {
         glds16_lds(kb, voff_k[i], la + i * NW4 * 1024);
