@@ -411,6 +411,9 @@ def run_config4(args, world: int, rank: int, local: int) -> None:
                                       f"{world}-stage window pipeline (P2P hand-off), {n_clips} clips"},
             "step_flop_mean": fl / n_steps,
             "step_mfma_frac": fl / elapsed / world / (PEAK_BF16_TFLOPS * 1e12),
+            "flop_basis": "the reference's work: attention over all 2N keys (K and its masked copy); the HIP path sums "
+                          "the masked copy's null keys in closed form and streams only the masked rows, so it executes "
+                          "fewer MFMA FLOPs than counted here",
             "attention_ms_per_launch": attn_ms, "output_latents": list(out[0].shape),
         }
         print(json.dumps(line), flush=True)
