@@ -2162,6 +2162,7 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc d
   }
   const int col = lane & 15, cq = lane >> 4;
   const int selw = ((col == 0 && (cq & 1) == 0) || (col == 1 && (cq & 1) == 1)) ? 0x38383838 : 0;
+  const uint64_t selp = ((uint64_t)(uint32_t)selw << 32) | (uint32_t)selw;
   f32x4 lsum = {0.f, 0.f, 0.f, 0.f};
   // (no inactive waves: the last query block's waves past Nq run on clamped duplicate queries, store_out drops them)
   i32x8 pf = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -2185,11 +2186,11 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc d
       // one V^T half live at a time (the scores of the next tile are live through this phase)
       __builtin_amdgcn_sched_barrier(0);
     }
-    uint32_t wlo, whi;
-    asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %2" : "=v"(wlo), "=v"(whi) : "v"(selw));
-    const uint64_t w2 = ((uint64_t)whi << 32) | wlo;
-    uint64_t w3, w4, w5;
-    asm volatile("v_mov_b64 %0, %3\n\tv_mov_b64 %1, %3\n\tv_mov_b64 %2, %3" : "=v"(w3), "=v"(w4), "=v"(w5) : "v"(w2));
+    // the 8-VGPR selector tuple from the resident (selw, selw) pair: 4 v_mov_b64 (opaque, so the tuple is rebuilt
+    // here rather than kept live through the softmax)
+    uint64_t w2, w3, w4, w5;
+    asm volatile("v_mov_b64 %0, %4\n\tv_mov_b64 %1, %4\n\tv_mov_b64 %2, %4\n\tv_mov_b64 %3, %4"
+                 : "=v"(w2), "=v"(w3), "=v"(w4), "=v"(w5) : "v"(selp));
     typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
     const i32x8 sel = __builtin_bit_cast(i32x8, (u64x4){w2, w3, w4, w5});
     lsum = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(sel, pf, lsum, 0, 0, 0, 127, 0, 127);
