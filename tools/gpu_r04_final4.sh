@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-4 HEAD check after the fp8 selector change: full GPU suite, smoke, default bench line
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -rA > gpurun_out/r04f4_gtests.log 2>&1; rc=$?; echo "gtests rc=$rc"; tail -1 gpurun_out/r04f4_gtests.log; [ $rc -ne 0 ] && { grep -E "FAILED|Error" gpurun_out/r04f4_gtests.log | head; exit $rc; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04f4_smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/r04f4_smoke.log
+
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python -u bench.py > gpurun_out/r04f4_bench.log 2>&1; rc=$?; echo "bench rc=$rc"; grep "^{" gpurun_out/r04f4_bench.log | cut -c1-400
+exit $rc
