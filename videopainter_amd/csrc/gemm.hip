@@ -1679,7 +1679,8 @@ extern "C" int vp_gemm_mx_fp8(const vp_gemm_mx_desc* x, void* stream) {
   }
   const char* e8 = getenv("VP_GEMM8_VARIANT");  // read per call (A/B)
   const bool use13 = (e8 == nullptr || atoi(e8) != 5) && d->K / 128 >= 8 && kf13[d->epilogue] != nullptr;
-  MxExt mx = {};  // (zero: no split, the kernel's GROUP)
+  MxExt mx = {};  // no split; the grouped tile order of the bf16 path (VP_GEMM_GROUP, default 4)
+  mx.group = gemm_group(d);
   mx.a_scale = (const uint8_t*)x->a_scale;
   for (int s = 0; s < 3; ++s) mx.w_scale[s] = (const uint8_t*)x->w_scale[s];
   mx.c_scale = (uint8_t*)x->c_scale;
