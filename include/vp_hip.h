@@ -26,10 +26,17 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 13
+#define VP_ABI_VERSION 14
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
+/* A/B switches of the library (kernel-variant selection only, never numerics of the default path):
+ * VP_GEMM_VARIANT, VP_GEMM_NO_TAIL, VP_GEMM_GROUP, VP_GEMM8_VARIANT, VP_ATTN_BOUNDED_MODE, VP_ATTN_UNBOUNDED_MODE,
+ * VP_ATTN_NO_SPLIT, VP_ATTN8_VARIANT, VP_T5_ATTN, VP_CONV_HOIST, VP_CONV_PIPE.  Each is read from the environment
+ * once, when the library is loaded; afterwards only vp_set_knob changes it (value NULL = unset), e.g. a test that
+ * runs two variants on the same operands.  Returns VP_ERR_ARG for an unknown name or a value over 31 bytes.  Host
+ * only; not thread-safe against launches in flight on other host threads.  (ABI 14.) */
+int vp_set_knob(const char* name, const char* value);
 /* sizeof of the descriptor structs as compiled into the library: out[0..6] = gemm, attn, dpm, gemm_mx, attn_fp8,
  * conv3d, attn_bwd (ABI check) */
 void vp_struct_sizes(int64_t* out);

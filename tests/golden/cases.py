@@ -189,6 +189,48 @@ def config4_inputs(dtype=torch.float32):
     return out
 
 
+# BASELINE config 4's chained any-length loop at full size (VERDICT r04 "next" 7): the reference pipeline
+# (CogVideoXI2VDualInpaintAnyLPipeline.__call__, anyl.py:759-1069) on the 42-layer ID-resample transformer + branch
+# (config-2 weights), 98 frames 480x720 = 2 windows of 49 at stride 49, 1 DPM step per window, prev_clip_weight 0.5.
+# The VAE is replaced by a counter-generated latent source (its encode returns `chain4_vae_latent(k)` for the k-th
+# encode call; the VAE has its own goldens), so every window input is regenerable here and on the GPU box.
+CHAIN4_CASE = dict(num_frames=49, total_frames=98, stride=49, height=480, width=720, steps=1, prev_clip_weight=0.5,
+                   id_pool_resample_learnable=True, seed=42)
+# the k-th vae.encode call of the reference run: window 0 encodes the first frame, the video, the masked video;
+# window 1 (conditioned on window 0's last latent, no first-frame encode) the video and the masked video
+CHAIN4_VAE_CALLS = (("w0.image", 1), ("w0.video", 13), ("w0.masked", 13), ("w1.video", 13), ("w1.masked", 13))
+
+
+def chain4_vae_latent(k: int):
+    """The stub VAE's k-th posterior sample [1, 16, lf, 60, 90] (bf16-valued; scaling_factor 1.0)."""
+    name, lf = CHAIN4_VAE_CALLS[k]
+    return torch.from_numpy(synth_tensor(f"c4chain.vae.{name}", (1, 16, lf, 60, 90)))
+
+
+def chain4_pixel_masks():
+    """[98, 480, 720] binary pixel masks (frame 0 clear: first_frame_gt)."""
+    c = CHAIN4_CASE
+    return make_mask(1, c["total_frames"], c["height"], c["width"], "c4chain.mask", first_frame_gt=True)[0, :, 0]
+
+
+def chain4_prompts():
+    return (torch.from_numpy(synth_tensor("c4chain.prompt", (1, 226, 4096))),
+            torch.from_numpy(synth_tensor("c4chain.neg", (1, 226, 4096))))
+
+
+def chain4_draws():
+    """The reference run's generator draws in its order (pinned by the digests in config4_chain.safetensors): per
+    window the initial noise (prepare_latents), then one scheduler noise per DPM step; all fp32 [1, 13, 16, 60, 90]
+    from torch.Generator().manual_seed(42) (the stub VAE draws nothing)."""
+    c = CHAIN4_CASE
+    g = torch.Generator().manual_seed(c["seed"])
+    out = []
+    for _ in range(c["total_frames"] // c["stride"]):
+        for _ in range(1 + c["steps"]):
+            out.append(torch.randn((1, 13, 16, 60, 90), generator=g, dtype=torch.float32))
+    return out
+
+
 def config5_cfg():
     """BASELINE config 5: the 5b-I2V model at 49f 720x1280 (sample 90x160 latent)."""
     from videopainter_amd.config import COGVIDEOX_5B_I2V

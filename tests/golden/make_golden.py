@@ -459,6 +459,152 @@ def make_config4():
     _save("config4.safetensors", out, {"cpu_seconds": {"fp32": t32, "bf16": t16}})
 
 
+@torch.no_grad()
+def make_config4_chain(mini=False):
+    """BASELINE config 4's CHAINED any-length loop at full size (VERDICT r04 "next" 7): the reference pipeline's own
+    __call__ (anyl.py:759-1069: window slicing, the previous window's last latent as the next window's image
+    latent, the last-step 42-layer hidden states + resample mask handed to the next window, dynamic CFG, replace-gt,
+    overlap averaging) on the 42-layer ID-resample transformer + 2-layer branch (config-2 counter weights), 2 windows
+    x 49 frames at stride 49, 480x720, 1 DPM step per window, prev_clip_weight 0.5 — fp32, then the reference's own
+    bf16 run on the same generator draws.
+
+    Harness-side substitutions (none touches the step loop's arithmetic):
+      * the VAE: a real tiny AutoencoderKLCogVideoX sets the pipeline's scale factors, but its `encode` returns the
+        counter latents `cases.chain4_vae_latent(k)` (scaling_factor 1.0) — the VAE is pinned by its own goldens;
+      * the last window's transformer calls run with return_hidden_states=False (nothing reads that window's states:
+        anyl.py:981 keeps them only for window_idx < n_windows - 1), which keeps the fp32 run inside 64 GB;
+      * the bf16 run replays the fp32 run's generator draws cast to bf16, so its drift is arithmetic only.
+    Stored: strided slices + digest of the final latents, the bf16 drift, the draws' digests (the GPU test
+    regenerates them, cases.chain4_draws) and the latent mask the pipeline built (uint8).
+    `mini=True`: a 2-layer 2-head model at the same shapes, written to /tmp (checks the machinery in minutes)."""
+    import time
+    import types
+    import diffusers.schedulers.scheduling_dpm_cogvideox as dpm_mod
+    import diffusers.pipelines.cogvideo.pipeline_cogvideox_inpainting_i2v_branch_anyl as anyl_mod
+    from diffusers import AutoencoderKLCogVideoX, CogVideoXDPMScheduler
+    from diffusers.models.transformers.cogvideox_transformer_3d import CogVideoXTransformer3DModel
+    from diffusers.models.branch_cogvideox import CogvideoXBranchModel
+    from PIL import Image
+    from safetensors.torch import save_file as _sf
+    from tests.golden.cases import (config2_cfg, CONFIG2_SEEDS, CHAIN4_CASE, CHAIN4_VAE_CALLS, chain4_vae_latent,
+                                    chain4_pixel_masks, chain4_prompts)
+    c = CHAIN4_CASE
+    tcfg, bcfg = config2_cfg()
+    tcfg = dict(tcfg, id_pool_resample_learnable=True)
+    if mini:
+        tcfg = dict(tcfg, num_layers=2, num_attention_heads=2)
+        bcfg = dict(bcfg, num_layers=1, num_attention_heads=2)
+    t0 = time.time()
+    with torch.device("meta"):
+        tr = CogVideoXTransformer3DModel(**tcfg).eval()
+        br = CogvideoXBranchModel(**bcfg).eval()
+    tr = _fill_synthetic(tr, CONFIG2_SEEDS[0])
+    br = _fill_synthetic(br, CONFIG2_SEEDS[1])
+    print(f"chain4: weights {time.time() - t0:.0f}s", flush=True)
+    torch.manual_seed(1234)
+    vae = AutoencoderKLCogVideoX(block_out_channels=(32, 32, 32, 32), layers_per_block=1, latent_channels=16,
+                                 norm_num_groups=32, temporal_compression_ratio=4, scaling_factor=1.0).eval()
+    calls = []
+
+    def stub_encode(x, *a, **k):
+        kk = len(calls)
+        name, lf = CHAIN4_VAE_CALLS[kk]
+        if x.shape[2] != (1 if name.endswith("image") else c["num_frames"]):
+            raise RuntimeError(f"unexpected encode #{kk} ({name}) of {tuple(x.shape)}")
+        calls.append(name)
+        z = chain4_vae_latent(kk).to(x.dtype)
+        return types.SimpleNamespace(latent_dist=types.SimpleNamespace(sample=lambda generator=None: z))
+    vae.encode = stub_encode
+
+    pm = chain4_pixel_masks()
+    n = c["total_frames"]
+    black = Image.fromarray(np.zeros((c["height"], c["width"], 3), dtype=np.uint8))
+    frames = [black] * n
+    masks = [Image.fromarray(np.repeat((pm[i] * 255).astype(np.uint8)[..., None], 3, axis=-1)) for i in range(n)]
+    pe, ne = chain4_prompts()
+
+    def run(dt, replay=None):
+        calls.clear()
+        draws, rec_mask = [], []
+
+        def rn(*a, **k):
+            if replay is not None:
+                x = replay[len(draws)].to(k.get("dtype") or torch.float32)
+            else:
+                x = orig_rn(*a, **k)
+            draws.append(x.clone())
+            return x
+        orig_rn = anyl_mod.randn_tensor
+        anyl_mod.randn_tensor = rn
+        dpm_mod.randn_tensor = rn
+        orig_fwd = tr.forward
+
+        def fwd(*a, **k):
+            akw = k.get("attention_kwargs") or {}
+            if "prev_hidden_states" in akw:  # the last window: its states are never read
+                assert c["steps"] == 1
+                k = dict(k, return_hidden_states=False)
+                return (orig_fwd(*a, **k)[0], [], None)
+            return orig_fwd(*a, **k)
+        tr.forward = fwd
+        orig_mask = pipe.prepare_mask_latents
+
+        def prepm(*a, **k):
+            o = orig_mask(*a, **k)
+            rec_mask.append(o[0].clone())
+            return o
+        pipe.prepare_mask_latents = prepm
+        try:
+            res = pipe(prompt_embeds=pe.to(dt), negative_prompt_embeds=ne.to(dt), image=frames[0], video=frames,
+                       masks=masks, num_frames=c["num_frames"], height=c["height"], width=c["width"],
+                       num_inference_steps=c["steps"], use_dynamic_cfg=True, guidance_scale=6.0,
+                       generator=torch.Generator().manual_seed(c["seed"]), strength=1.0, replace_gt=True,
+                       mask_add=True, stride=c["stride"], prev_clip_weight=c["prev_clip_weight"],
+                       id_pool_resample_learnable=True, output_type="latent", return_dict=False)[0]
+        finally:
+            anyl_mod.randn_tensor = orig_rn
+            dpm_mod.randn_tensor = orig_rn
+            tr.forward = orig_fwd
+            pipe.prepare_mask_latents = orig_mask
+        assert calls == [nm for nm, _ in CHAIN4_VAE_CALLS], calls
+        return res.float(), draws, rec_mask
+
+    sch = CogVideoXDPMScheduler(snr_shift_scale=1.0, prediction_type="v_prediction", rescale_betas_zero_snr=True,
+                                clip_sample=False, set_alpha_to_one=True, timestep_spacing="trailing",
+                                beta_start=0.00085, beta_end=0.012)
+    from diffusers.pipelines.cogvideo.pipeline_cogvideox_inpainting_i2v_branch_anyl import (
+        CogVideoXI2VDualInpaintAnyLPipeline)
+    pipe = CogVideoXI2VDualInpaintAnyLPipeline(tokenizer=None, text_encoder=None, vae=vae, transformer=tr,
+                                               scheduler=sch, branch=br)
+    t0 = time.time()
+    o32, draws, masks32 = run(torch.float32)
+    t32 = time.time() - t0
+    print(f"chain4: fp32 {t32:.0f}s, final {tuple(o32.shape)}, {len(draws)} draws", flush=True)
+    tr.to(torch.bfloat16)
+    br.to(torch.bfloat16)
+    t0 = time.time()
+    o16, _, masks16 = run(torch.bfloat16, replay=draws)
+    t16 = time.time() - t0
+    rel = lambda a, b: float((a.double() - b.double()).norm() / b.double().norm())  # noqa: E731
+    d16 = rel(o16, o32)
+    print(f"chain4: bf16 {t16:.0f}s, reference bf16 vs fp32 rel-L2 {d16:.3e}", flush=True)
+    dig = lambda t: torch.tensor([t.double().sum(), t.double().abs().sum(), t.double().norm()],  # noqa: E731
+                                 dtype=torch.float64)
+    flat = o32.reshape(-1)
+    out = {"slice": flat[::7].clone(), "bf16.slice": o16.reshape(-1)[::7].clone(), "digest": dig(o32),
+           "final_shape": torch.tensor(o32.shape, dtype=torch.float32), "ref_bf16_rel": torch.tensor([d16])}
+    for i, d in enumerate(draws):
+        out[f"draw.{i}.digest"] = dig(d)
+    for w, m in enumerate(masks32):  # [2, 1, 13, 60, 90] (CFG-doubled, before the pipeline's permute)
+        out[f"w{w}.mask"] = m[:1].to(torch.uint8)
+    out = {k: (v.contiguous() if v.dtype in (torch.float64, torch.uint8) else v.detach().float().contiguous())
+           for k, v in out.items()}
+    path = "/tmp/config4_chain_mini.safetensors" if mini else os.path.join(HERE, "config4_chain.safetensors")
+    _sf(out, path, metadata={"case": json.dumps(c), "cpu_seconds": json.dumps({"fp32": t32, "bf16": t16}),
+                             "mini": json.dumps(mini)})
+    print("wrote", path, flush=True)
+
+
 def make_config5():
     """BASELINE config 5's shape (49f 720x1280, N = 47 026) through the reference, whole model, B = 1 (VERDICT r02
     "what's missing" 3): noise_pred [1,13,16,90,160] strided slice (every 13th element) in fp32 and the reference's
@@ -660,6 +806,10 @@ if __name__ == "__main__":
         make_config5()
     if "config4" in which:
         make_config4()
+    if "config4_chain" in which:
+        make_config4_chain()
+    if "config4_chain_mini" in which:
+        make_config4_chain(mini=True)
     if "block5" in which:
         make_block5()
     if "block_resample" in which:

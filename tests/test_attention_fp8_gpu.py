@@ -139,7 +139,7 @@ def _ref_fp64(q8, k8, vt, vs, npad, Nk, H, q_exp, k_exp):
     return o.reshape(B, Nq, H * 64)
 
 @pytest.fixture(params=["1", "2", "3", "4", "5"], ids=["exp2", "lin", "lin2", "lin2p", "skew"])
-def attn8_variant(request, monkeypatch):
+def attn8_variant(request, knobs):
     """VP_ATTN8_VARIANT: 1 = P by v_exp_f32 + RNE e4m3 pack, 2 = P by linear mantissa interpolation, 3 = the same
     codes packed by v_cvt_pknorm_u16_f32 + a byte gather, 4 = the lin2 codes in the software-pipelined
     kernel (f8p), 5 = the lin2 kernel with its tile loop skewed by one tile (default).  1 and 4 are rejected A/B
@@ -147,7 +147,7 @@ def attn8_variant(request, monkeypatch):
     from videopainter_amd import kernels as K
     if not K.attention_variant_built("fp8:" + request.param):
         pytest.skip(f"fp8 attention variant {request.param} is not in this build (VP_ATTN_EXTRA_VARIANTS)")
-    monkeypatch.setenv("VP_ATTN8_VARIANT", request.param)
+    knobs.setenv("VP_ATTN8_VARIANT", request.param)
     return request.param
 
 
@@ -185,7 +185,7 @@ def test_attention_fp8(B, H, N, late, attn8_variant):
 # partial last tiles of every size class (1, 3, 4, 5, 33, 63 keys) and one- to three-tile sequences
 @pytest.mark.parametrize("N", [65, 67, 68, 69, 97, 127, 128, 129, 1000])
 @pytest.mark.parametrize("var", ["5"])
-def test_attention_fp8_skewed_bit_identical(N, var, monkeypatch):
+def test_attention_fp8_skewed_bit_identical(N, var, knobs):
     """The skewed loop (variant 5, the default) computes the same P codes, rescale decisions and accumulation order as
     variant 3; its last-tile mask zeroes the P codes of the keys past Nk (duplicates of key Nk - 1) where variant 3
     sets their scores to -inf: the outputs are equal bit for bit, also through the blend epilogue."""
@@ -198,7 +198,7 @@ def test_attention_fp8_skewed_bit_identical(N, var, monkeypatch):
     vp = K.v_pack_fp8(v.to(dev), H)
     outs = {}
     for vv in ("3", var):
-        monkeypatch.setenv("VP_ATTN8_VARIANT", vv)
+        knobs.setenv("VP_ATTN8_VARIANT", vv)
         o = torch.empty(B, N, H * 64, device=dev, dtype=torch.bfloat16)
         K.attention_fp8(q8, k8, vp, o, H, q_exp, k_exp, out_scale=0.7)
         K.attention_fp8(q8, k8, vp, o, H, q_exp, k_exp, out_scale=0.3, accumulate=True)

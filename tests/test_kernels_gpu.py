@@ -21,38 +21,38 @@ def _lib():
 
 @pytest.fixture(params=["5", "11", "12", "13", "30", "1", "20"],
                 ids=["gemm_v5", "gemm_v11", "gemm_v12", "gemm_v13", "gemm_v30", "gemm_v1", "gemm_v20"])
-def gemm_variant(request, monkeypatch):
+def gemm_variant(request, knobs):
     from videopainter_amd import kernels as K
     if not K.gemm_variant_built(request.param):
         pytest.skip(f"GEMM variant {request.param} is not in this build (VP_GEMM_EXTRA_VARIANTS)")
-    monkeypatch.setenv("VP_GEMM_VARIANT", request.param)
+    knobs.setenv("VP_GEMM_VARIANT", request.param)
     return request.param
 
 
 UNBOUNDED_VARIANTS = ("p2a", "a16", "lazy")
 
 
-def need_variant(name, monkeypatch=None):
+def need_variant(name, knobs=None):
     """Skip unless the attention variant is in this library build (the rejected A/B variants need
-    VP_ATTN_EXTRA_VARIANTS=1); with monkeypatch, select it through its environment switch."""
+    VP_ATTN_EXTRA_VARIANTS=1); with knobs, select it through its environment switch."""
     from videopainter_amd import kernels as K
     if not K.attention_variant_built(name):
         pytest.skip(f"attention variant {name} is not in this build (VP_ATTN_EXTRA_VARIANTS)")
-    if monkeypatch is not None:
-        monkeypatch.delenv("VP_ATTN_UNBOUNDED_MODE", raising=False)
-        monkeypatch.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
-        monkeypatch.setenv("VP_ATTN_UNBOUNDED_MODE" if name in UNBOUNDED_VARIANTS else "VP_ATTN_BOUNDED_MODE", name)
+    if knobs is not None:
+        knobs.delenv("VP_ATTN_UNBOUNDED_MODE", raising=False)
+        knobs.delenv("VP_ATTN_BOUNDED_MODE", raising=False)
+        knobs.setenv("VP_ATTN_UNBOUNDED_MODE" if name in UNBOUNDED_VARIANTS else "VP_ATTN_BOUNDED_MODE", name)
 
 
 @pytest.fixture(params=["p2a", "a16", "p2", "s16", "lazy", "w32", "w64", "w64f", "s16i", "p1"],
                 ids=lambda v: f"attn_{v}")
-def attn_variant(request, monkeypatch):
+def attn_variant(request, knobs):
     """Unbounded-score launches (no VP_ATTN_BOUNDED_SCORES): p2a (the library default: the p2 pipeline with an
     anchored reference point and the a16 re-run of flagged blocks), a16 (the anchored-softmax 16x16x32 kernel), lazy
     (the running-max kernel).  Bounded-score launches (include/vp_hip.h VP_ATTN_BOUNDED_SCORES, the host proved the
     bound; the library default is p2a there too): p2, s16, and the A/B variants of a VP_ATTN_EXTRA_VARIANTS build (w32 / w64 / w64f /
     s16i / p1)."""
-    need_variant(request.param, monkeypatch)
+    need_variant(request.param, knobs)
     return request.param
 
 
@@ -235,7 +235,7 @@ def test_gemm_plain_row_pass_forms_bit_identical(epi):
 
 
 @pytest.mark.parametrize("epi", ["bias", "gelu"])
-def test_gemm_tail_split_round(epi, monkeypatch):
+def test_gemm_tail_split_round(epi, knobs):
     """Tail mode (gemm.hip tail_plan): 17 x 16 = 272 tiles on the 256-CU chip leave a last round of 16 tiles, which
     runs as split-K workgroups (2 x 512-K chunks, compact fp32 partials) + a reduce that applies the epilogue; the
     ragged last M-tile is among them.  Against torch fp32 and against the same GEMM without the tail split
@@ -249,7 +249,7 @@ def test_gemm_tail_split_round(epi, monkeypatch):
     e = N.EPI_BIAS if epi == "bias" else N.EPI_BIAS_GELU
     out = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
     K.gemm(a, [w], [b], out, epilogue=e)
-    monkeypatch.setenv("VP_GEMM_NO_TAIL", "1")
+    knobs.setenv("VP_GEMM_NO_TAIL", "1")
     ref_k = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
     K.gemm(a, [w], [b], ref_k, epilogue=e)
     y = a.float() @ w.float().T + b.float()
@@ -327,11 +327,11 @@ def _ref64(q, k, v, H, scale=0.125):
 
 @pytest.mark.parametrize("mode", ["p2a", "a16", "lazy"])
 @pytest.mark.parametrize("gamma", [1.0, 6.0])
-def test_attention_large_gamma_scores(gamma, mode, monkeypatch):
+def test_attention_large_gamma_scores(gamma, mode, knobs):
     """qk-LayerNorm outputs with |gamma| up to 6 (scores over hundreds of log2 units, far outside the bounded-score
     contract): the anchored kernel (no running max) against fp64 attention, at a config-2-like length for 2 heads."""
     from videopainter_amd import kernels as K
-    need_variant(mode, monkeypatch)
+    need_variant(mode, knobs)
     B, H, Nn = 1, 2, 4500
     g = torch.Generator().manual_seed(int(gamma * 10))
     gam = torch.rand(H * 64, generator=g) * gamma  # per-channel gains in [0, gamma]
@@ -350,13 +350,13 @@ def test_attention_large_gamma_scores(gamma, mode, monkeypatch):
 
 @pytest.mark.parametrize("mode", ["p2a", "a16"])
 @pytest.mark.parametrize("jump", [40.0, 90.0, 200.0])
-def test_attention_anchored_late_jump(jump, mode, monkeypatch):
+def test_attention_anchored_late_jump(jump, mode, knobs):
     """The anchored kernels' guarded paths: a late key whose score exceeds every earlier one by `jump` log2 units for
     half the queries — 40: within the first reference's range; 90: row sums pass 2^64 (a16) / 2^62 (p2a): the
     rescale branch; 200: exp2 overflows inside a tile (a16: the exact two-pass re-run of the workgroup; p2a: the block
     is flagged and re-run by a16).  Against fp64 attention."""
     from videopainter_amd import kernels as K
-    need_variant(mode, monkeypatch)
+    need_variant(mode, knobs)
     B, H, Nn = 1, 1, 1500
     g = torch.Generator().manual_seed(int(jump))
     q = torch.randn(B, Nn, 64, generator=g) * 0.3
@@ -376,13 +376,13 @@ def test_attention_anchored_late_jump(jump, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["p2a", "lazy", "a16"])
-def test_attention_stepwise_max_growth(mode, monkeypatch):
+def test_attention_stepwise_max_growth(mode, knobs):
     """Running max grows by 0 / 0.5 / 3 / 8 nats at tile seams, so the deferred-max test (tile sum > 2^8) takes both
     branches many times within one query block (cdna_hip_programming.md §5.4 rule 26); for the anchored kernel the
     row sums pass 2^64 repeatedly (its rescale branch).  (Scores up to ~300 in log2 units: outside the bounded-score
     contract.)"""
     from videopainter_amd import kernels as K
-    need_variant(mode, monkeypatch)
+    need_variant(mode, knobs)
     B, H, Nn = 1, 2, 1100
     g = torch.Generator().manual_seed(80)
     u = torch.randn(64, generator=g)
@@ -494,7 +494,7 @@ def test_gemm_qknorm_rope_epilogue_matches_separate_kernels(H, T, rope, gemm_var
 
 
 @pytest.mark.parametrize("Kk", [512, 640, 3072])
-def test_gemm_staggered_matches_quadrant_pipeline(Kk, monkeypatch):
+def test_gemm_staggered_matches_quadrant_pipeline(Kk, knobs):
     """Variant 11 (the quadrant pipeline with the two wave groups staggered by one barrier), variant 13 (the default:
     11 with each slot's fragment reads before its DMA), variant 12 (two
     32-MFMA phases and one barrier per K-tile) and variant 30 (two workgroups per CU, 256 x 128 tiles, 32-K steps)
@@ -534,7 +534,7 @@ def test_gemm_staggered_matches_quadrant_pipeline(Kk, monkeypatch):
         width = 3 * D if name in ("bias3", "qknorm") else D
         outs = []
         for v in [x for x in ("5", "11", "12", "13", "30") if K.gemm_variant_built(x)]:
-            monkeypatch.setenv("VP_GEMM_VARIANT", v)
+            knobs.setenv("VP_GEMM_VARIANT", v)
             o = torch.full((B, Ntok, width), float("nan"), device=dev, dtype=torch.bfloat16)
             if name == "addrows":
                 o.zero_()
@@ -577,7 +577,7 @@ def test_linear_small_timestep_patchify_unpatchify_mask():
 
 
 @pytest.mark.parametrize("Nq,Nk2", [(333, 0), (1500, 700), (17776, 0)])
-def test_attention_tail_split_matches_unsplit(Nq, Nk2, monkeypatch):
+def test_attention_tail_split_matches_unsplit(Nq, Nk2, knobs):
     """The grid-tail split (last partial round of workgroups run as key-range workgroups + a merge pass) against the
     unsplit launch of the default kernel: the same attention up to the merge's rounding; at config-2 length the
     split is exactly what the step runs (6720 blocks on 512 slots)."""
@@ -602,7 +602,7 @@ def test_attention_tail_split_matches_unsplit(Nq, Nk2, monkeypatch):
     assert N.lib().vp_attention_workspace_bytes(C.byref(d)) > 0  # the split is active for this shape
     out_s = torch.empty(B, Nq, D, device=dev, dtype=torch.bfloat16)
     K.attention(q, k, v, out_s, H, **kw)
-    monkeypatch.setenv("VP_ATTN_NO_SPLIT", "1")
+    knobs.setenv("VP_ATTN_NO_SPLIT", "1")
     out_u = torch.empty_like(out_s)
     K.attention(q, k, v, out_u, H, **kw)
     # bf16 P is rounded against each range's own running max, so the two differ at bf16 noise level
@@ -618,11 +618,11 @@ def test_attention_tail_split_matches_unsplit(Nq, Nk2, monkeypatch):
 
 @pytest.mark.parametrize("mode", ["p2", "s16", "w64", "w64f", "p1"])
 @pytest.mark.parametrize("Nq,Nk2", [(1500, 700), (17776, 0)])
-def test_attention_bounded_tail_split_matches_unsplit(Nq, Nk2, mode, monkeypatch):
+def test_attention_bounded_tail_split_matches_unsplit(Nq, Nk2, mode, knobs):
     """The bounded-score kernels' grid-tail split instances (partials + merge) against their unsplit launch and, at
     small size, against fp32 attention."""
     from videopainter_amd import kernels as K
-    need_variant(mode, monkeypatch)
+    need_variant(mode, knobs)
     B, H = 2, 2 if Nq < 17776 else 48
     D = H * 64
     q, k, v = (bf(rnd(B, Nq, D, seed=s) * 0.5).to(dev) for s in (80, 81, 82))
@@ -631,7 +631,7 @@ def test_attention_bounded_tail_split_matches_unsplit(Nq, Nk2, mode, monkeypatch
         kw.update(k2=bf(rnd(B, Nk2, D, seed=83) * 0.5).to(dev), v2=bf(rnd(B, Nk2, D, seed=84)).to(dev))
     out_s = torch.empty(B, Nq, D, device=dev, dtype=torch.bfloat16)
     K.attention(q, k, v, out_s, H, **kw)
-    monkeypatch.setenv("VP_ATTN_NO_SPLIT", "1")
+    knobs.setenv("VP_ATTN_NO_SPLIT", "1")
     out_u = torch.empty_like(out_s)
     K.attention(q, k, v, out_u, H, **kw)
     assert rel(out_s, out_u) < 5e-3
@@ -724,11 +724,11 @@ def test_partition_rows_index_and_permuted_writes(B, N):
 
 
 @pytest.mark.parametrize("mode", ["s16", "a16", "p2a", "p2", "w64"])
-def test_attention_k2_full_hint(mode, monkeypatch):
+def test_attention_k2_full_hint(mode, knobs):
     """The k2_full hint (segment-2 keys past k2_full[b] have zero values: row sums only) gives the attention of the
     same segments without the hint; per-batch split points, one straddling a tile, one past every tile."""
     from videopainter_amd import kernels as K
-    need_variant(mode, monkeypatch)
+    need_variant(mode, knobs)
     kw = {} if mode in UNBOUNDED_VARIANTS else dict(bounded_scores=True)
     B, H, Nn, N2 = 3, 2, 700, 900
     D = H * 64
@@ -832,17 +832,17 @@ def test_null_key_mass_matches_explicit_null_keys():
 
 @pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
 @pytest.mark.parametrize("mode", ["s16", "a16", "p2a", "p2", "p1"])
-def test_attention_k2_len_and_l_extra(mode, split, monkeypatch):
+def test_attention_k2_len_and_l_extra(mode, split, knobs):
     """k2_len (only the first k2_len[b] keys of segment 2) and l_extra (extra row-sum mass per query, log2 score
     units) against fp64 attention over the truncated segments with 2^l_extra added to each denominator.  At this size
     every block is in the grid tail: the split launch (with empty key ranges where k2_len = 0 leaves fewer tiles than
     splits) and the combine kernel carry l_extra; a16 / p2a also get masses far above their anchors (a16: the exact
     re-run; p2a: a non-finite row sum, so the block is flagged and re-run by a16)."""
     from videopainter_amd import kernels as K
-    need_variant(mode, monkeypatch)
+    need_variant(mode, knobs)
     kw = {} if mode in UNBOUNDED_VARIANTS else dict(bounded_scores=True)
     if not split:
-        monkeypatch.setenv("VP_ATTN_NO_SPLIT", "1")
+        knobs.setenv("VP_ATTN_NO_SPLIT", "1")
     B, H, Nn, N2 = 3, 2, 700, 900
     D = H * 64
     q, k, v = (bf(rnd(B, Nn, D, seed=s) * 0.5).to(dev) for s in (95, 96, 97))
@@ -873,16 +873,16 @@ def test_attention_k2_len_and_l_extra(mode, split, monkeypatch):
 
 @pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
 @pytest.mark.parametrize("mode", ["p2a", "p2"])
-def test_attention_segment2_fast_path_bit_identical(mode, split, monkeypatch):
+def test_attention_segment2_fast_path_bit_identical(mode, split, knobs):
     """Segment 2 with segment 1's row strides (the resample processor's layout: K2 / V2 as slices of a [B, N, 3D]
     buffer) streams its full 128-key tiles on segment 1's precomputed lane offsets; the same keys as contiguous
     tensors take the general DMA path.  Only the addressing differs, so the outputs are equal bit for bit — with
     k2_len leaving partial and whole-tile segment ends (0, 128, 300, 1024 keys) and l_extra."""
     from videopainter_amd import kernels as K
-    need_variant(mode, monkeypatch)
+    need_variant(mode, knobs)
     kw = {} if mode in UNBOUNDED_VARIANTS else dict(bounded_scores=True)
     if not split:
-        monkeypatch.setenv("VP_ATTN_NO_SPLIT", "1")
+        knobs.setenv("VP_ATTN_NO_SPLIT", "1")
     B, H, Nn = 4, 2, 700
     D = H * 64
     qkv = bf(rnd(B, Nn, 3 * D, seed=61) * 0.5).to(dev)
@@ -905,14 +905,14 @@ def test_attention_segment2_fast_path_bit_identical(mode, split, monkeypatch):
 @pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
 @pytest.mark.parametrize("spread", [False, True], ids=["even", "spread"])
 @pytest.mark.parametrize("mode", ["p2a", "a16", "p2", "s16", "lazy"])
-def test_attention_lse_matches_reference(mode, spread, split, monkeypatch):
+def test_attention_lse_matches_reference(mode, spread, split, knobs):
     """The softmax statistics the backward reads (lse = log2 sum_k 2^(scale log2e q.k), fp32 [B, H, Nq]) and the
     output against fp64, per variant.  spread: queries of very different norms in one wave (x0.02 .. x2.5), so an
     anchored kernel's shared reference point sits far above some queries' scores."""
     from videopainter_amd import kernels as K
-    need_variant(mode, monkeypatch)
+    need_variant(mode, knobs)
     if not split:
-        monkeypatch.setenv("VP_ATTN_NO_SPLIT", "1")
+        knobs.setenv("VP_ATTN_NO_SPLIT", "1")
     B, H, Nn = 2, 2, 700
     D = H * 64
     q, k, v = (rnd(B, Nn, D, seed=s) * 0.5 for s in (195, 196, 197))

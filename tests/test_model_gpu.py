@@ -143,7 +143,7 @@ def test_transformer_matches_reference(env, mode):
 
 
 @torch.no_grad()
-def test_fused_qkv_norm_rope_bit_exact_vs_separate_launches(env, monkeypatch):
+def test_fused_qkv_norm_rope_bit_exact_vs_separate_launches(env, knobs):
     """The QKV GEMM with the qk-norm + RoPE epilogue (default) gives the model output of the separate
     vp_head_norm_rope_bf16 launches (VP_NO_QKV_FUSION=1) bit for bit, incl. the returned hidden states."""
     i, g = env["inp"], env["g"]
@@ -154,7 +154,7 @@ def test_fused_qkv_norm_rope_bit_exact_vs_separate_launches(env, monkeypatch):
                          timestep=i["timestep"].to(dev), image_rotary_emb=i["rope"], branch_block_samples=bs,
                          branch_block_masks=i["mask"], return_hidden_states=True, return_dict=False)
     fused = run()
-    monkeypatch.setenv("VP_NO_QKV_FUSION", "1")
+    knobs.setenv("VP_NO_QKV_FUSION", "1")
     sep = run()
     assert torch.equal(fused[0], sep[0])
     for k in range(4):
@@ -162,7 +162,7 @@ def test_fused_qkv_norm_rope_bit_exact_vs_separate_launches(env, monkeypatch):
 
 
 @torch.no_grad()
-def test_resample_mask_plan_built_once_per_forward(env, monkeypatch):
+def test_resample_mask_plan_built_once_per_forward(env, knobs):
     """The resample processor's mask plan (row partition + null-key segments) is built once per transformer forward
     and found by every later layer (the uint8 mask reaches the processors as the same tensor): one
     vp_partition_rows_index launch per forward, not one per layer."""
@@ -171,7 +171,7 @@ def test_resample_mask_plan_built_once_per_forward(env, monkeypatch):
     i, g = env["inp"], env["g"]
     calls = []
     orig = K.partition_rows_index
-    monkeypatch.setattr(K, "partition_rows_index", lambda m: calls.append(1) or orig(m))
+    knobs.setattr(K, "partition_rows_index", lambda m: calls.append(1) or orig(m))
     AP._MASK_PLANS.clear()
     env["trr"](hidden_states=_d(i["hidden"]), encoder_hidden_states=_d(i["enc"]), timestep=i["timestep"].to(dev),
                image_rotary_emb=i["rope"], branch_block_samples=[_d(g["branch.0"]), _d(g["branch.1"])],

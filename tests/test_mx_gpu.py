@@ -71,9 +71,9 @@ def test_mx_quantize_bit_exact():
 
 
 @pytest.fixture(params=["5", "13"], ids=["gemm8_v5", "gemm8_v13"])
-def gemm8_variant(request, monkeypatch):
+def gemm8_variant(request, knobs):
     """fp8 GEMM main loop: 13 (default: the bf16 default's staggered read-first pipeline) or 5 (VP_GEMM8_VARIANT)."""
-    monkeypatch.setenv("VP_GEMM8_VARIANT", request.param)
+    knobs.setenv("VP_GEMM8_VARIANT", request.param)
     return request.param
 
 
@@ -95,7 +95,7 @@ def test_gemm_mx_bias(M, Nn, Kk, gemm8_variant):
     assert rel(out, a.double() @ w.double().T + b.double()) < 6e-2
 
 
-def test_gemm_mx_main_loops_bit_identical(monkeypatch):
+def test_gemm_mx_main_loops_bit_identical(knobs):
     """The two fp8 main loops run the same MFMAs in the same order per accumulator: bit-identical outputs."""
     from videopainter_amd import kernels as K
     g = torch.Generator().manual_seed(5)
@@ -105,7 +105,7 @@ def test_gemm_mx_main_loops_bit_identical(monkeypatch):
     A, W = K.mx_quantize(a.to(dev)), K.mx_quantize(w.to(dev))
     outs = []
     for v in ("5", "13"):
-        monkeypatch.setenv("VP_GEMM8_VARIANT", v)
+        knobs.setenv("VP_GEMM8_VARIANT", v)
         out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
         K.gemm_mx(A, [W], [None], out)
         outs.append(out)

@@ -73,7 +73,7 @@ def test_t5_attention_matches_torch(K, L, H, masked):
 
 @pytest.mark.parametrize("L,H,masked", [(226, 64, False), (226, 2, True), (77, 4, False), (33, 3, True),
                                          (384, 2, False)])
-def test_t5_attention_mfma_matches_scalar_kernel(K, L, H, masked, monkeypatch):
+def test_t5_attention_mfma_matches_scalar_kernel(K, L, H, masked, knobs):
     """The MFMA T5 attention (default) against the scalar-FMA kernel (VP_T5_ATTN=scalar) on the same operands: the
     same roundings (bf16 scores + bias, fp32 softmax, bf16 weights), only the fp32 summation orders differ, so the
     outputs agree to a few bf16 ulps; key padding (L not a multiple of 32) and masked keys included."""
@@ -89,7 +89,7 @@ def test_t5_attention_mfma_matches_scalar_kernel(K, L, H, masked, monkeypatch):
         mask[0, L // 3:] = 0
         mask[1, L - 5:] = 0
     out = K.t5_attention(qkv, B, L, H, table, buckets, mask)
-    monkeypatch.setenv("VP_T5_ATTN", "scalar")
+    knobs.setenv("VP_T5_ATTN", "scalar")
     ref = K.t5_attention(qkv, B, L, H, table, buckets, mask)
     r = rel(out.float(), ref.float())
     print(f"t5 attention mfma vs scalar L={L} H={H} masked={masked}: rel {r:.2e}, "

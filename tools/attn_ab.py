@@ -37,11 +37,11 @@ def main():
     for r in range(a.rounds):
         for kind, m in arms:
             if kind == "b":
-                os.environ["VP_ATTN_BOUNDED_MODE"] = m
-                os.environ.pop("VP_ATTN_UNBOUNDED_MODE", None)
+                K.set_knob("VP_ATTN_BOUNDED_MODE", m)
+                K.set_knob("VP_ATTN_UNBOUNDED_MODE", None)
             else:
-                os.environ["VP_ATTN_UNBOUNDED_MODE"] = m
-                os.environ.pop("VP_ATTN_BOUNDED_MODE", None)
+                K.set_knob("VP_ATTN_UNBOUNDED_MODE", m)
+                K.set_knob("VP_ATTN_BOUNDED_MODE", None)
             t = timeit(lambda: K.attention(q, k, v, o, H, bounded_scores=kind == "b"), a.iters)
             res[f"{kind}:{m}"].append(t * 1e3)
             print(f"round {r} {kind}:{m}: {t * 1e3:.3f} ms {fl / t / 1e12:.0f} TF/s", flush=True)

@@ -26,7 +26,7 @@ def main():
     fl = 4 * B * H * N * N * 64
     for r in range(a.rounds):
         for m in a.modes.split(","):
-            os.environ["VP_ATTN_BOUNDED_MODE"] = m
+            K.set_knob("VP_ATTN_BOUNDED_MODE", m)
             t = timeit(lambda: K.attention(q, k, v, o, H, bounded_scores=True), a.iters)
             print(f"round {r} {m}: {t * 1e3:.3f} ms {fl / t / 1e12:.0f} TF/s", flush=True)
 

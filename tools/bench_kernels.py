@@ -81,12 +81,12 @@ def main():
             out = torch.empty(M, Nn, device=dev, dtype=torch.bfloat16)
             a = x[:, :Kk]
             for gv in args.gemm_variants.split(","):
-                os.environ["VP_GEMM_VARIANT"] = gv
+                K.set_knob("VP_GEMM_VARIANT", gv)
                 t = timeit(lambda: K.gemm(a, [w], [b], out, lda=x.stride(0)), args.iters)
                 res[f"gemm{gv}_{name}_r{rnd}"] = dict(ms=t * 1e3, tflops=2 * M * Nn * Kk / t / 1e12)
                 print(f"gemm v{gv}", name, res[f"gemm{gv}_{name}_r{rnd}"], flush=True)
             del w, b, out
-        os.environ.pop("VP_GEMM_VARIANT", None)
+        K.set_knob("VP_GEMM_VARIANT", None)
     del x
     qkv = torch.randn(B, Ntok, 3 * D, device=dev).to(torch.bfloat16)
     o = torch.empty(B, Ntok, D, device=dev, dtype=torch.bfloat16)
@@ -104,10 +104,10 @@ def main():
         for var in variants:
             # unbounded-score kernels (p2a = the default without a proven bound, a16, lazy) vs bounded ones
             unb = var in ("lazy", "a16", "p2a")
-            os.environ.pop("VP_ATTN_BOUNDED_MODE", None)
-            os.environ.pop("VP_ATTN_UNBOUNDED_MODE", None)
+            K.set_knob("VP_ATTN_BOUNDED_MODE", None)
+            K.set_knob("VP_ATTN_UNBOUNDED_MODE", None)
             if var != "bounded":
-                os.environ["VP_ATTN_UNBOUNDED_MODE" if unb else "VP_ATTN_BOUNDED_MODE"] = var
+                K.set_knob("VP_ATTN_UNBOUNDED_MODE" if unb else "VP_ATTN_BOUNDED_MODE", var)
             t = timeit(lambda: K.attention(q, k, v, o, H, bounded_scores=not unb), max(2, args.iters // 2))
             res[f"attention_{var}_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
             print("attention", var, res[f"attention_{var}_r{rnd}"], flush=True)
@@ -126,11 +126,11 @@ def main():
         for rnd in range(2):
             for var in (args.variant8.split(",") if args.variant8 else [""]):
                 if var:
-                    os.environ["VP_ATTN8_VARIANT"] = var
+                    K.set_knob("VP_ATTN8_VARIANT", var)
                 t = timeit(lambda: K.attention_fp8(q8, k8, vp, o, H, q_exp, k_exp), max(2, args.iters // 2))
                 res[f"attention_fp8_v{var}_r{rnd}"] = dict(ms=t * 1e3, tflops=fl / t / 1e12)
                 print("attention fp8", var, res[f"attention_fp8_v{var}_r{rnd}"], flush=True)
-        os.environ.pop("VP_ATTN8_VARIANT", None)
+        K.set_knob("VP_ATTN8_VARIANT", None)
         print(json.dumps(res))
         return
     xin = torch.randn(B, Ntok, D, device=dev).to(torch.bfloat16)

@@ -28,8 +28,8 @@ def run(q, k, v, H, mode, bounded, nosplit):
     for kk in ("VP_ATTN_UNBOUNDED_MODE", "VP_ATTN_BOUNDED_MODE", "VP_ATTN_NO_SPLIT"):
         os.environ.pop(kk, None)
     if nosplit:
-        os.environ["VP_ATTN_NO_SPLIT"] = "1"
-    os.environ["VP_ATTN_BOUNDED_MODE" if bounded else "VP_ATTN_UNBOUNDED_MODE"] = mode
+        K.set_knob("VP_ATTN_NO_SPLIT", "1")
+    K.set_knob("VP_ATTN_BOUNDED_MODE" if bounded else "VP_ATTN_UNBOUNDED_MODE", mode)
     o = torch.empty_like(q)
     K.attention(q, k, v, o, H, bounded_scores=bounded)
     torch.cuda.synchronize()

@@ -10,11 +10,11 @@ from videopainter_amd import kernels as K  # noqa: E402
 
 
 def run(Nq, Nk, mode, split):
-    os.environ["VP_ATTN_BOUNDED_MODE"] = mode
+    K.set_knob("VP_ATTN_BOUNDED_MODE", mode)
     if split:
-        os.environ.pop("VP_ATTN_NO_SPLIT", None)
+        K.set_knob("VP_ATTN_NO_SPLIT", None)
     else:
-        os.environ["VP_ATTN_NO_SPLIT"] = "1"
+        K.set_knob("VP_ATTN_NO_SPLIT", "1")
     g = torch.Generator().manual_seed(0)
     B, H = 1, 1
     q = (torch.randn(B, Nq, 64, generator=g) * 0.5).bfloat16()

@@ -22,11 +22,11 @@ def main():
         for kept in ("1", "0"):
             os.environ["VP_P2_KEPT"] = kept
             if bounded:
-                os.environ["VP_ATTN_BOUNDED_MODE"] = "p2"
+                K.set_knob("VP_ATTN_BOUNDED_MODE", "p2")
             K.attention(q, k, v, o, H, bounded_scores=bounded)
             torch.cuda.synchronize()
             outs[kept] = o.clone()
-            os.environ.pop("VP_ATTN_BOUNDED_MODE", None)
+            K.set_knob("VP_ATTN_BOUNDED_MODE", None)
         same = torch.equal(outs["1"].view(torch.int16), outs["0"].view(torch.int16))
         print(f"{'p2 (bounded)' if bounded else 'p2a'}: kept vs slot-base outputs bit-identical: {same}", flush=True)
         if not same:

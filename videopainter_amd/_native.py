@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -91,6 +91,7 @@ EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS, EPI_BIAS_G
 _SIGS = {
     "vp_abi_version": (i32, []),
     "vp_build_digest": (C.c_char_p, []),
+    "vp_set_knob": (i32, [C.c_char_p, C.c_char_p]),
     "vp_struct_sizes": (None, [C.POINTER(i64)]),
     "vp_gemm_bf16": (i32, [C.POINTER(GemmDesc), vp]),
     "vp_gemm_bf16_workspace_bytes": (i64, [C.POINTER(GemmDesc)]),
@@ -162,6 +163,11 @@ _SIGS = {
 
 EXPORTS = tuple(_SIGS)
 
+# the library's A/B knobs (vp_set_knob): read from the environment once at load; knob_values mirrors them
+KNOBS = ("VP_GEMM_VARIANT", "VP_GEMM_NO_TAIL", "VP_GEMM_GROUP", "VP_GEMM8_VARIANT", "VP_ATTN_BOUNDED_MODE",
+         "VP_ATTN_UNBOUNDED_MODE", "VP_ATTN_NO_SPLIT", "VP_ATTN8_VARIANT", "VP_T5_ATTN", "VP_CONV_HOIST", "VP_CONV_PIPE")
+knob_values: dict = {}
+
 _lib = None
 _lock = threading.Lock()
 
@@ -199,6 +205,7 @@ def lib():
                 C.sizeof(AttnFp8Desc), C.sizeof(Conv3dDesc), C.sizeof(AttnBwdDesc))
         if tuple(sizes) != want:
             raise HipLibraryError(f"descriptor size mismatch lib={tuple(sizes)} python={want}; rebuild")
+        knob_values.update({k: os.environ.get(k) for k in KNOBS})  # what the library read at load
         _lib = L
         return L
 

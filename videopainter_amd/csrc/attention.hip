@@ -54,6 +54,45 @@ static_assert(NP % NW == 0, "pieces per wave");
 
 enum { MODE_LAZY = 0, MODE_BOUNDED = 1 };
 
+// ---- diagnostic builds only (tools/attn_clock.py builds them into their own library; the default library has
+// none of this).  VP_CLOCK_STAMPS: every workgroup of p2 / p2a / s16 / a16 stamps s_memtime and s_memrealtime before
+// and after its key loop into vp_clock_buf (MI355X_MICROARCH.md 'DVFS give-back' item 6: in-kernel clock =
+// delta memtime / delta realtime x 100 MHz); the stamps go to that buffer only, never into an output.
+// VP_P1_ABL (p2 / p2a only, outputs invalid): bit 0 = no K / V DMA after the prologue (the loop re-reads stale
+// tiles), bit 1 = the softmax's v_exp_f32 replaced by v_mov_b32 — which part of the loop's power holds the clock.
+#ifndef VP_CLOCK_STAMPS
+#define VP_CLOCK_STAMPS 0
+#endif
+#ifndef VP_P1_ABL
+#define VP_P1_ABL 0
+#endif
+#if VP_CLOCK_STAMPS
+constexpr int CLOCK_SLOTS = 1 << 15;
+__device__ unsigned long long vp_clock_buf[CLOCK_SLOTS * 4];
+struct ClockStamp {
+  unsigned long long t0, r0;
+  __device__ __forceinline__ void start() {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  __device__ __forceinline__ void stop(int tid) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && blockIdx.x < CLOCK_SLOTS) {  // one lane, plain vector stores
+      unsigned long long* p = vp_clock_buf + (size_t)blockIdx.x * 4;
+      p[0] = t0;
+      p[1] = r0;
+      p[2] = t1;
+      p[3] = r1;
+    }
+  }
+};
+#else
+struct ClockStamp {
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void stop(int) {}
+};
+#endif
+
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 VP_DEV int swz(int row) { return (row >> 1) & 7; }
@@ -806,7 +845,11 @@ VP_DEV void p1_read_v(const char* Vl, int kh, const int (&vo)[2], bf16x8 (&vf)[4
 // earlier (the transcendental -> VALU distance).
 VP_DEV void p1_fence() { __builtin_amdgcn_sched_barrier(0); }
 VP_DEV void p1_exp(float& p0, float& p1, float s0, float s1) {
+#if VP_P1_ABL & 2
+  asm volatile("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=&v"(p0), "=&v"(p1) : "v"(s0), "v"(s1));
+#else
   asm volatile("v_exp_f32 %0, %2\n\tv_exp_f32 %1, %3" : "=&v"(p0), "=&v"(p1) : "v"(s0), "v"(s1));
+#endif
 }
 VP_DEV uint32_t p1_pack(float a, float b) {
   uint32_t w;
@@ -1174,8 +1217,10 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
     }
   }
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // S -> the first (asm) exp
+  ClockStamp ck;
+  ck.start();
   for (int ti = tbeg; ti < tend; ++ti) {
-    if (ti + SL / 2 < tend) issue(ti + SL / 2);
+    if (ti + SL / 2 < tend && (!(VP_P1_ABL & 1) || ti == tbeg)) issue(ti + SL / 2);
     int lim = KB;
     if (ti >= full1) {
       const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
@@ -1191,6 +1236,7 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
                                                             r.o[1][c & 1], 0, 0, 0);
   r.lsum[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[1][0]), r.lsum[1], 0, 0, 0);
   r.lsum[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[1][1]), r.lsum[1], 0, 0, 0);
+  ck.stop(tid);
 
   const int qq = lane & 31;
   float l_tot[2];
@@ -1506,6 +1552,8 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
 
   // ---- main pass ----
   zero_acc();
+  ClockStamp ck;
+  ck.start();
   tile_loop([&](const char* Kl, const char* Vl, int lim, bool first_tile, bool full) {
 #pragma unroll
     for (int kh = 0; kh < HALVES; ++kh) {
@@ -1547,6 +1595,7 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
       }
     }
   });
+  ck.stop(tid);
 
   // l_extra: row-sum mass of keys that are not in the segments (log2, score units; the null keys of the resample
   // processor), added relative to the query's reference m; a tail-split partial leaves it to attn_combine_kernel
@@ -2671,7 +2720,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   // proved |score| <= VP_ATTN_SCORE_BOUND) VP_ATTN_BOUNDED_MODE may name p2 (no anchor) or s16; without it
   // VP_ATTN_UNBOUNDED_MODE may name a16 (A/B; a variant outside this build is VP_ERR_UNSUPPORTED).
   const bool bounded = (d->flags & VP_ATTN_BOUNDED_SCORES) != 0;
-  int variant = variant_by_name(getenv(bounded ? "VP_ATTN_BOUNDED_MODE" : "VP_ATTN_UNBOUNDED_MODE"));
+  int variant = variant_by_name(vp_knob(bounded ? VPK_ATTN_BOUNDED_MODE : VPK_ATTN_UNBOUNDED_MODE));
   if (variant == -2) return VP_ERR_UNSUPPORTED;
   // default: p2a for every launch (6.13 ms per config-2 call against 6.15-6.30 for p2 interleaved,
   // profiles/r04_attn_p2a_ab.log: the anchor costs nothing and no bound has to hold); p2 stays the bounded challenger
@@ -2694,7 +2743,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   const int nqb = (d->Nq + QB - 1) / QB;
   pl.nblk = (int64_t)d->B * d->H * nqb;
   if (pl.nblk > 0x7fffffff) return VP_ERR_ARG;
-  const char* ns = getenv("VP_ATTN_NO_SPLIT");
+  const char* ns = vp_knob(VPK_ATTN_NO_SPLIT);
   if (slots > 0 && (ns == nullptr || ns[0] == '0')) {
     const int tail = (int)(pl.nblk % slots);
     const int ntile = (d->Nk + KB - 1) / KB + (d->Nk2 > 0 ? (d->Nk2 + KB - 1) / KB : 0);
@@ -2781,6 +2830,14 @@ extern "C" int vp_attention_fwd_bf16(const vp_attn_desc* d, void* stream) {
   return vp_attention_fwd_bf16_ws(d, nullptr, 0, stream);
 }
 
+#if VP_CLOCK_STAMPS
+// diagnostic builds only (not in include/vp_hip.h): the stamps of the last launches, 4 x u64 per workgroup slot
+extern "C" int vp_diag_clock_read(void* host, int64_t slots) {
+  if (host == nullptr || slots <= 0 || slots > CLOCK_SLOTS) return VP_ERR_ARG;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vp_clock_buf), (size_t)slots * 32, 0, hipMemcpyDeviceToHost);
+}
+#endif
+
 extern "C" int vp_mx_mfma_probe32(const void* A, const void* B, const void* sa, const void* sb, float* C,
                                   void* stream) {
   if (!A || !B || !sa || !sb || !C) return VP_ERR_ARG;
@@ -2854,7 +2911,7 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
     (void)hipFuncSetAttribute((const void*)attn_fwd_fp8p, hipFuncAttributeMaxDynamicSharedMemorySize, F8P_LDS);
 #endif
   }
-  const char* e = getenv("VP_ATTN8_VARIANT");
+  const char* e = vp_knob(VPK_ATTN8_VARIANT);
   int variant = e != nullptr ? atoi(e) : 0;
   if (variant < 1 || variant > 5) variant = 5;
   if (variant == 5) {  // the skewed loop (default)

@@ -1370,8 +1370,8 @@ int device_cus() {
 // 16).  The default main loop only (VP_GEMM_VARIANT unset or 13), and the epilogues the reduce implements.
 SplitPlan tail_plan(const vp_gemm_desc* d, int tiles) {
   SplitPlan p;
-  const char* e = getenv("VP_GEMM_VARIANT");
-  if ((e != nullptr && atoi(e) != 13) || getenv("VP_GEMM_NO_TAIL") != nullptr) return p;
+  const char* e = vp_knob(VPK_GEMM_VARIANT);
+  if ((e != nullptr && atoi(e) != 13) || vp_knob(VPK_GEMM_NO_TAIL) != nullptr) return p;
   const int cus = device_cus();
   const int tail = tiles % cus;
   if (tiles <= cus || tail == 0 || 4 * tail > cus) return p;
@@ -1417,10 +1417,10 @@ extern "C" int vp_gemm_variant_built(int variant) {
   return (variant == 12 || variant == 20 || variant == 30) && VP_GEMM_EXTRA_VARIANTS ? 1 : 0;
 }
 
-// M-tiles per group of the grouped tile order (VP_GEMM_GROUP overrides, A/B; read per call)
+// M-tiles per group of the grouped tile order (the VP_GEMM_GROUP knob overrides, A/B)
 static int gemm_group(const vp_gemm_desc* d) {
   (void)d;
-  const char* g = getenv("VP_GEMM_GROUP");
+  const char* g = vp_knob(VPK_GEMM_GROUP);
   const int v = g != nullptr ? atoi(g) : 0;
   return v > 0 && v <= 64 ? v : 4;
 }
@@ -1487,7 +1487,7 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
       if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr_set = true;
   }
-  const char* e = getenv("VP_GEMM_VARIANT");  // read per call: tests switch it between launches
+  const char* e = vp_knob(VPK_GEMM_VARIANT);  // the knob table (vp_set_knob): tests switch it between launches
   int variant = e != nullptr ? atoi(e) : 13;
   if (variant != 1 && variant != 5 && variant != 11 && variant != 12 && variant != 13 && variant != 20 && variant != 30)
     variant = 13;
@@ -1677,7 +1677,7 @@ extern "C" int vp_gemm_mx_fp8(const vp_gemm_mx_desc* x, void* stream) {
       if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES_FP8);
     attr_set = true;
   }
-  const char* e8 = getenv("VP_GEMM8_VARIANT");  // read per call (A/B)
+  const char* e8 = vp_knob(VPK_GEMM8_VARIANT);  // (A/B knob)
   const bool use13 = (e8 == nullptr || atoi(e8) != 5) && d->K / 128 >= 8 && kf13[d->epilogue] != nullptr;
   MxExt mx = {};  // no split; the grouped tile order of the bf16 path (VP_GEMM_GROUP, default 4)
   mx.group = gemm_group(d);

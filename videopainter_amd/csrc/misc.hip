@@ -1,6 +1,9 @@
 // Conditioning-path and data-movement kernels of the denoising step (gfx950): small-M linears (time embedding,
 // AdaLN modulation vectors), sinusoidal timestep embedding, patchify / token mask / unpatchify, the fused
 // CFG + DPM-Solver + replace-gt step glue, and a device-side synthetic-weight generator.
+#include <stdlib.h>
+#include <string.h>
+
 #include "vp_common.h"
 
 namespace {
@@ -213,6 +216,50 @@ extern "C" int vp_abi_version(void) { return VP_ABI_VERSION; }
 #define VP_BUILD_DIGEST "unknown"
 #endif
 extern "C" const char* vp_build_digest(void) { return VP_BUILD_DIGEST; }
+
+// ---- A/B knobs: the environment read ONCE (the first vp_knob / vp_set_knob call, from the load-time constructor
+// below), kept in a table; launches read the table, never the environment ----
+namespace {
+const char* const knob_names[VPK_COUNT] = {"VP_GEMM_VARIANT",        "VP_GEMM_NO_TAIL",   "VP_GEMM_GROUP",
+                                           "VP_GEMM8_VARIANT",       "VP_ATTN_BOUNDED_MODE",
+                                           "VP_ATTN_UNBOUNDED_MODE", "VP_ATTN_NO_SPLIT",  "VP_ATTN8_VARIANT",
+                                           "VP_T5_ATTN",             "VP_CONV_HOIST",     "VP_CONV_PIPE"};
+struct KnobTable {
+  char val[VPK_COUNT][32];
+  bool set[VPK_COUNT];
+  KnobTable() {
+    for (int k = 0; k < VPK_COUNT; ++k) {
+      const char* e = getenv(knob_names[k]);
+      set[k] = e != nullptr && strlen(e) < sizeof(val[k]);
+      val[k][0] = 0;
+      if (set[k]) strcpy(val[k], e);
+    }
+  }
+};
+KnobTable& knobs() {
+  static KnobTable t;  // initialised once (thread-safe static), at library load by the constructor below
+  return t;
+}
+__attribute__((constructor)) void knobs_at_load() { (void)knobs(); }
+}  // namespace
+
+const char* vp_knob(int k) {
+  KnobTable& t = knobs();
+  return k >= 0 && k < VPK_COUNT && t.set[k] ? t.val[k] : nullptr;
+}
+
+extern "C" int vp_set_knob(const char* name, const char* value) {
+  if (name == nullptr || (value != nullptr && strlen(value) >= 32)) return VP_ERR_ARG;
+  KnobTable& t = knobs();
+  for (int k = 0; k < VPK_COUNT; ++k) {
+    if (strcmp(name, knob_names[k]) != 0) continue;
+    t.set[k] = value != nullptr;
+    t.val[k][0] = 0;
+    if (value != nullptr) strcpy(t.val[k], value);
+    return VP_OK;
+  }
+  return VP_ERR_ARG;
+}
 
 extern "C" void vp_struct_sizes(int64_t* out) {
   out[0] = (int64_t)sizeof(vp_gemm_desc);

@@ -353,7 +353,7 @@ extern "C" int vp_t5_attention_bf16(const void* qkv, int64_t ld, int32_t inner, 
   if (qkv == nullptr || bias_table == nullptr || buckets == nullptr || out == nullptr) return VP_ERR_ARG;
   if (B <= 0 || L <= 0 || H <= 0 || inner != H * 64 || ld < 3 * inner || (ld % 8) || ldo < inner) return VP_ERR_ARG;
   if (L > T5_MAX_L) return VP_ERR_UNSUPPORTED;
-  const char* ev = getenv("VP_T5_ATTN");
+  const char* ev = vp_knob(VPK_T5_ATTN);
   if (ev == nullptr || strcmp(ev, "scalar") != 0) {  // the MFMA kernel (default)
     if ((ldo % 4) != 0) return VP_ERR_ARG;
     const size_t Lp32 = (size_t)((L + 31) & ~31);

@@ -772,7 +772,7 @@ int launch_conv(const vp_conv3d_desc& d, int c8s, int64_t tiles, hipStream_t s) 
     attr = true;
   }
   // VP_CONV_HOIST=0 keeps the per-K-tile tap decode (A/B)
-  const char* he = getenv("VP_CONV_HOIST");
+  const char* he = vp_knob(VPK_CONV_HOIST);
   if (d.Cin >= 64 && (he == nullptr || atoi(he) != 0))
     hipLaunchKernelGGL((conv3d_kernel<BN, true>), dim3((unsigned)tiles), dim3(CNT), G::LDS, s, d, c8s);
   else
@@ -821,7 +821,7 @@ extern "C" int vp_conv3d_bf16(const vp_conv3d_desc* d, void* stream) {
   }
   // wide convolutions (Cin >= 64): the counted-vmcnt pipeline (VP_CONV_PIPE: 2 = V2, default; 1 = its round-3 form;
   // 0 = the 2-stage ring; A/B)
-  const char* pe = getenv("VP_CONV_PIPE");
+  const char* pe = vp_knob(VPK_CONV_PIPE);
   const int pipe = pe != nullptr ? atoi(pe) : 2;
   if (d->Cin >= 64 && pipe != 0) {
     const int64_t t = ((M + PBM - 1) / PBM) * ((d->Cout + PBN - 1) / PBN);

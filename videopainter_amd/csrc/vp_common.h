@@ -200,7 +200,25 @@ VP_DEV u32x2 mx_quantize_quarter(const float (&v)[8], uint8_t& scale_byte) {
   return mx_pack8(v, mx_inv_scale(s));
 }
 
-#define VP_CHECK_LAUNCH()                                 \
+// A/B knobs (include/vp_hip.h vp_set_knob): the environment read once at library load (misc.hip), then only
+// vp_set_knob.  vp_knob(k) = the value, or nullptr when unset — what getenv of the same name returned.
+enum VpKnob {
+  VPK_GEMM_VARIANT,
+  VPK_GEMM_NO_TAIL,
+  VPK_GEMM_GROUP,
+  VPK_GEMM8_VARIANT,
+  VPK_ATTN_BOUNDED_MODE,
+  VPK_ATTN_UNBOUNDED_MODE,
+  VPK_ATTN_NO_SPLIT,
+  VPK_ATTN8_VARIANT,
+  VPK_T5_ATTN,
+  VPK_CONV_HOIST,
+  VPK_CONV_PIPE,
+  VPK_COUNT
+};
+const char* vp_knob(int k);
+
+#define VP_CHECK_LAUNCH()                               \
   do {                                                      \
     hipError_t _e = hipGetLastError();                      \
     if (_e != hipSuccess) return (int)_e;                   \

@@ -386,6 +386,33 @@ def attention_variant_built(name: str) -> bool:
     return bool(N.lib().vp_attention_variant_built(name.encode()))
 
 
+def set_knob(name: str, value: Optional[str]) -> Optional[str]:
+    """Switch one of the library's A/B knobs (include/vp_hip.h vp_set_knob: kernel-variant selection, read from the
+    environment once when the library loads) for the launches that follow; value None = unset.  Returns the previous
+    value, so a caller can restore it."""
+    if name not in N.KNOBS:
+        raise ValueError(f"unknown knob {name!r} (one of {N.KNOBS})")
+    L = N.lib()
+    prev = N.knob_values.get(name)
+    N.check(L.vp_set_knob(name.encode(), None if value is None else str(value).encode()), f"vp_set_knob({name})")
+    N.knob_values[name] = None if value is None else str(value)
+    return prev
+
+
+class knob:
+    """Context manager form of `set_knob`: `with kernels.knob("VP_GEMM_VARIANT", 11): ...`."""
+
+    def __init__(self, name: str, value: Optional[str]):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        self.prev = set_knob(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_knob(self.name, self.prev)
+
+
 def gemm_variant_built(variant) -> bool:
     """Is the GEMM main loop VP_GEMM_VARIANT = variant in this library build (the rejected 12 / 20 / 30 need
     VP_GEMM_EXTRA_VARIANTS=1)?"""

@@ -106,18 +106,13 @@ class ModelMixin(nn.Module):
     def device(self):
         return next(self.parameters()).device
 
-    # -- training-compat toggles (backward kernels are out of scope for this round: SURVEY.md §8f #3) --
+    # -- training toggles (modeling_utils.py:160).  The block backward always recomputes from the block input
+    # (autograd._BlockFn), i.e. it is checkpointed whether or not the flag is set --
     def enable_gradient_checkpointing(self):
         self.gradient_checkpointing = True
 
     def disable_gradient_checkpointing(self):
         self.gradient_checkpointing = False
-
-    def _check_inference(self, *tensors):
-        if torch.is_grad_enabled() and (any(p.requires_grad for p in self.parameters()) or
-                                        any(isinstance(t, torch.Tensor) and t.requires_grad for t in tensors)):
-            raise NotImplementedError("videopainter_amd implements the denoising forward only (no backward kernels "
-                                      "yet); call under torch.no_grad() with requires_grad_(False) parameters")
 
     # -- construction / weights --
     @classmethod
