@@ -52,10 +52,10 @@ def main():
     o = torch.empty(B, Ntok, D, device="cuda", dtype=torch.bfloat16)
     q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
     fl = 4 * B * H * Ntok * Ntok * 64
-    nblk = B * H * ((Ntok + 255) // 256)
     res = {}
     for var in args.variants.split(","):
-        unb = var in ("a16", "p2a")
+        nblk = B * H * ((Ntok + 511) // 512 if var == "p2w" else (Ntok + 255) // 256)
+        unb = var in ("a16", "p2a", "p2w")
         K.set_knob("VP_ATTN_BOUNDED_MODE", None)
         K.set_knob("VP_ATTN_UNBOUNDED_MODE", None)
         K.set_knob("VP_ATTN_UNBOUNDED_MODE" if unb else "VP_ATTN_BOUNDED_MODE", var)

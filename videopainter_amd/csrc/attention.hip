@@ -346,10 +346,16 @@ struct AttnSplit {
   int flag_main;     // main-grid blocks (the tail's flags follow them)
   int flag_nsplit;   // splits per tail block
   int redo;          // a16 redo launch: a workgroup whose block is not flagged returns at once
+  int flag_shift;    // redo of p2w: flags are per 512-query block (two of a16's 256-query blocks): shift 1
 };
 
 // is block t flagged by its p2a workgroup(s)?
-VP_DEV bool block_flagged(const AttnSplit& sp, int t) {
+VP_DEV bool block_flagged(const AttnSplit& sp, int t, int Nq) {
+  if (sp.flag_shift) {  // t: a 256-query block; the flags are per (256 << flag_shift)-query block of the same head
+    const int nqb = (Nq + 255) / 256, nqbw = (Nq + (256 << sp.flag_shift) - 1) / (256 << sp.flag_shift);
+    const int bh = t / nqb;
+    t = bh * nqbw + ((t - bh * nqb) >> sp.flag_shift);
+  }
   if (t < sp.flag_main) return sp.flags[t] != 0;
   const int* f = sp.flags + sp.flag_main + (int64_t)(t - sp.flag_main) * sp.flag_nsplit;
   int any = 0;
@@ -958,7 +964,9 @@ VP_DEV void p1_mask(f32x16& s, int rem, int hl4) {
 // the tile into the slot this tile's predecessor used, so every read of a slot comes before the seam barrier; V^T is
 // single-buffered (read after the even step's PV, a 4-MFMA group before the odd step's), and the seam moves to the
 // end of step (3, 0), after V(3) is read
-template <int SL, bool ANCH = false>
+// VMC (SL = 2): the seam's vmcnt when the tile after next is already in flight (p2w: a 4-slot ring, tile t + 2
+// issued at the top of tile t, VMC = this tile's DMA instructions per wave; 0 for the 2-slot ring)
+template <int SL, bool ANCH = false, int VMC = 0>
 VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn, int lim, bool masked, bool last,
                     bool wait_all, int lane, const int (&vo)[2]) {
   const int hl = lane >> 5;
@@ -986,7 +994,10 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
         p1_step<0, 1, 1, 0, 0, true, false, ANCH>(r, sel);
       p1_read_v(Vl, h, vo, r.vf[0]);
       if (h == 3 && !last) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (VMC == 0 || wait_all)
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VMC) : "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         p1_read_k(Kn, 0, lane, r.kf[0]);
@@ -1051,16 +1062,26 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
 // the anchor inside one tile), or a row sum under 2^-96 (a query whose scores sit far below the wave's anchor, where
 // small terms would underflow) stores nothing and raises its flag in sp.flags; the launcher then re-runs exactly
 // those blocks with the anchored 16x16x32 kernel (per-query anchors and its exact two-pass re-run).
-template <bool TAIL = false, int SL = 4, bool ANCH = false>
-__global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const vp_attn_desc d, const AttnSplit sp) {
+// NWV = 8 (p2w, SL = 2 only): the same per-wave pipeline in 8-wave workgroups of 512 queries, one per CU, on a 4-slot
+// ring (tile t + 2 issued at the top of tile t): a K / V tile loaded once serves twice the queries, so each wave
+// issues half the LDS-DMA instructions per tile (4 instead of 8) — the DMA issue is ~7 % of p2a's time
+// (tools/attn_clock.py ablation) — and the L2 -> LDS bytes per FLOP halve.
+template <bool TAIL = false, int SL = 4, bool ANCH = false, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_fwd_p1(const vp_attn_desc d,
+                                                                                        const AttnSplit sp) {
   static_assert(!ANCH || SL == 2, "the anchored form is the two-workgroups-per-CU pipeline");
+  static_assert(NWV == 4 || (NWV == 8 && SL == 2), "8-wave workgroups run the p2 schedule");
+  constexpr int QBV = NWV * 64;               // queries per workgroup
+  constexpr int PPWV = NP / NWV;              // DMA pieces per operand, wave and tile
+  constexpr int RING = NWV == 8 ? 4 : SL;     // LDS ring slots
+  constexpr int AHEAD = RING / 2;             // tiles issued ahead
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hl = lane >> 5;
 
-  const int nqb = (d.Nq + QB - 1) / QB;
+  const int nqb = (d.Nq + QBV - 1) / QBV;
   const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
   const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
   const int bh = t / nqb;
@@ -1074,7 +1095,7 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
   const int ntiles_all = tiles1 + tiles2;
   const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
   const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
-  const int qw0 = qb * QB + wave * 64;
+  const int qw0 = qb * QBV + wave * 64;
 #ifdef VP_P1_PRIO
   if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);  // A/B: static priority for every other workgroup
 #endif
@@ -1095,14 +1116,14 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
       }
     }
   }
-  auto slot_of = [&](int ti) { return smem + (ti & (SL - 1)) * ST; };
+  auto slot_of = [&](int ti) { return smem + (ti & (RING - 1)) * ST; };
   // full tiles of segment 1 (all but possibly its last): one scalar base per operand and tile, the lane offsets fixed
   // (voff_*), the LDS destination from a precomputed base; segment 2 and partial tiles take the general path with the
   // lane's rows recomputed from the lane id (rows past the end re-read the last key)
-  int voff_k[PPW4], voff_v[PPW4];
+  int voff_k[PPWV], voff_v[PPWV];
 #pragma unroll
-  for (int i = 0; i < PPW4; ++i) {
-    const int prow = (wave + i * NW4) * 8 + (lane >> 3);
+  for (int i = 0; i < PPWV; ++i) {
+    const int prow = (wave + i * NWV) * 8 + (lane >> 3);
     voff_k[i] = (prow * (int)d.k_sn + (((lane & 7) ^ swz(prow)) * 8)) * 2;
     voff_v[i] = (prow * (int)d.v_sn + (((lane & 7) ^ vswz(prow)) * 8)) * 2;
   }
@@ -1119,14 +1140,14 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
   auto issue = [&](int ti) {
     const bool s1 = ti < full1;
     if (s1 || (ti >= tiles1 && ti - tiles1 < full2)) {
-      const unsigned la = lds0 + (ti & (SL - 1)) * ST;
+      const unsigned la = lds0 + (ti & (RING - 1)) * ST;
       const int tt = s1 ? ti : ti - tiles1;
       const char* kb = (s1 ? kseg1 : kseg2) + (int64_t)tt * KB * d.k_sn * 2;
       const char* vb = (s1 ? vseg1 : vseg2) + (int64_t)tt * KB * d.v_sn * 2;
 #pragma unroll
-      for (int i = 0; i < PPW4; ++i) {
-        glds16_lds(kb, voff_k[i], la + i * NW4 * 1024);
-        glds16_lds(vb, voff_v[i], la + KT + i * NW4 * 1024);
+      for (int i = 0; i < PPWV; ++i) {
+        glds16_lds(kb, voff_k[i], la + i * NWV * 1024);
+        glds16_lds(vb, voff_v[i], la + KT + i * NWV * 1024);
       }
       return;
     }
@@ -1138,8 +1159,8 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
     const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
     const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
 #pragma unroll
-    for (int i = 0; i < PPW4; ++i) {
-      const int pc = wave + i * NW4;
+    for (int i = 0; i < PPWV; ++i) {
+      const int pc = wave + i * NWV;
       const int prow = pc * 8 + (ln >> 3);
       const int rr = min(prow, last);
       glds16(kb, (rr * ksn + (((ln & 7) ^ swz(prow)) * 8)) * 2, slot + pc * 1024);
@@ -1178,9 +1199,9 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
   // (a tail-split range is empty when k2_len leaves this row fewer tiles than splits: its record is O = 0, l = 0)
   const bool any = tbeg < tend;  // workgroup-uniform
   if (any) issue(tbeg);
-  if (SL == 4 && tbeg + 1 < tend) {
+  if (AHEAD == 2 && tbeg + 1 < tend) {
     issue(tbeg + 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPWV) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -1220,14 +1241,15 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
   ClockStamp ck;
   ck.start();
   for (int ti = tbeg; ti < tend; ++ti) {
-    if (ti + SL / 2 < tend && (!(VP_P1_ABL & 1) || ti == tbeg)) issue(ti + SL / 2);
+    if (ti + AHEAD < tend && (!(VP_P1_ABL & 1) || ti == tbeg)) issue(ti + AHEAD);
     int lim = KB;
     if (ti >= full1) {
       const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
       lim = sg.n - sg.key0;
     }
-    p1_tile<SL, ANCH>(r, sel, slot_of(ti), slot_of(ti + 1), __builtin_amdgcn_readfirstlane(lim), lim < KB,
-                      ti + 1 >= tend, ti + 2 >= tend, lane, vo);
+    p1_tile<SL, ANCH, RING == 4 && SL == 2 ? 2 * PPWV : 0>(r, sel, slot_of(ti), slot_of(ti + 1),
+                                                            __builtin_amdgcn_readfirstlane(lim), lim < KB,
+                                                            ti + 1 >= tend, ti + 2 >= tend, lane, vo);
   }
   // drain: PV + row sums of the last job (3, 1)
 #pragma unroll
@@ -1267,11 +1289,13 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
 #pragma unroll
         for (int i = 0; i < 16; ++i) bad |= nonfinite(sp.nsplit == 1 ? r.o[qi][dh][i] * inv : r.o[qi][dh][i]);
     }
-    int* wflag = (int*)(smem + 2 * ST);
+    int* wflag = (int*)(smem + RING * ST);
     const int mine = __ballot(bad) != 0ull;
     if (lane == 0) wflag[wave] = mine;
     __syncthreads();
-    const int redo = wflag[0] | wflag[1] | wflag[2] | wflag[3];
+    int redo = 0;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) redo |= wflag[w];
     if (tid == 0 && sp.flags != nullptr)
       sp.flags[sp.nsplit > 1 ? sp.flag_main + (t - sp.t_base) * sp.nsplit + split : t] = redo;
     if (redo) return;
@@ -1281,7 +1305,7 @@ __global__ __launch_bounds__(NW4 * 64, SL == 4 ? 1 : 2) void attn_fwd_p1(const v
     const int q = qw0 + qi * 32 + qq;
     if (sp.nsplit > 1) {
       const int qin = wave * 64 + qi * 32 + qq;
-      store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qin) * 66, r.o[qi], r.anc,
+      store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QBV + qin) * 66, r.o[qi], r.anc,
                     l_tot[qi], hl);
     } else {
       store_out(d, r.o[qi], l_tot[qi], q, b, h, hl, false, r.anc);
@@ -1337,7 +1361,7 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
   const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
   const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
   // redo launch after the anchored p2: only the blocks p2a flagged (workgroup-uniform: one block per workgroup)
-  if (sp.redo && !block_flagged(sp, t)) return;
+  if (sp.redo && !block_flagged(sp, t, d.Nq)) return;
   const int bh = t / nqb;
   const int qb = t - bh * nqb;
   const int b = bh / d.H;
@@ -2641,13 +2665,14 @@ struct AttnVar {
   const void* fn_tail;  // the grid-tail split instance
   int threads;
   int lds;  // dynamic LDS bytes
+  int qb = QB;  // queries per workgroup
 };
 #if VP_ATTN_EXTRA_VARIANTS
 #define VP_EXTRA(a, b) (const void*)a, (const void*)b
 #else
 #define VP_EXTRA(a, b) nullptr, nullptr
 #endif
-enum { V_LAZY, V_W32, V_W64, V_S16, V_A16, V_S16I, V_P1, V_W64F, V_P2, V_P2A, V_NVAR };
+enum { V_LAZY, V_W32, V_W64, V_S16, V_A16, V_S16I, V_P1, V_W64F, V_P2, V_P2A, V_P2W, V_NVAR };
 static const AttnVar attn_vars[] = {
     {"lazy", VP_EXTRA(attn_fwd<MODE_LAZY>, (attn_fwd<MODE_LAZY, true>)), NW * 64, LDS_BYTES},
     {"w32", VP_EXTRA(attn_fwd<MODE_BOUNDED>, (attn_fwd<MODE_BOUNDED, true>)), NW * 64, LDS_BYTES},
@@ -2659,6 +2684,9 @@ static const AttnVar attn_vars[] = {
     {"w64f", VP_EXTRA((attn_fwd_w64<false, true>), (attn_fwd_w64<true, true>)), NW4 * 64, LDS_BYTES},
     {"p2", (const void*)attn_fwd_p1<false, 2>, (const void*)attn_fwd_p1<true, 2>, NW4 * 64, 2 * ST},
     {"p2a", (const void*)attn_fwd_p1<false, 2, true>, (const void*)attn_fwd_p1<true, 2, true>, NW4 * 64, 2 * ST + 16},
+    // p2a in 8-wave workgroups of 512 queries on a 4-slot ring (attn_fwd_p1 NWV = 8)
+    {"p2w", (const void*)attn_fwd_p1<false, 2, true, 8>, (const void*)attn_fwd_p1<true, 2, true, 8>, 8 * 64,
+     4 * ST + 32, 512},
 };
 #undef VP_EXTRA
 static_assert(sizeof(attn_vars) / sizeof(attn_vars[0]) == V_NVAR, "variant table");
@@ -2725,8 +2753,9 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   // default: p2a for every launch (6.13 ms per config-2 call against 6.15-6.30 for p2 interleaved,
   // profiles/r04_attn_p2a_ab.log: the anchor costs nothing and no bound has to hold); p2 stays the bounded challenger
   if (variant < 0) variant = V_P2A;
-  // an unbounded launch needs a kernel that does not assume the bound: lazy, a16 or p2a
-  if (!bounded && variant != V_LAZY && variant != V_A16 && variant != V_P2A) return VP_ERR_UNSUPPORTED;
+  // an unbounded launch needs a kernel that does not assume the bound: lazy, a16, p2a or p2w
+  const bool anchored = variant == V_P2A || variant == V_P2W;
+  if (!bounded && variant != V_LAZY && variant != V_A16 && !anchored) return VP_ERR_UNSUPPORTED;
   if (attn_vars[variant].fn == nullptr) return VP_ERR_UNSUPPORTED;
   // the resample processor's segment hints: k2_len / l_extra (the closed-form null keys, the default) are taken by
   // s16 / a16 and p1 / p2 / p2a; k2_full (null keys as zero-value keys) by the 16x16x32 kernels only (config 4 ran
@@ -2734,13 +2763,13 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   // so a k2_full launch, and any hinted launch of another kernel, takes s16 (bounded) / a16 (unbounded)
   if (d->k2_full != nullptr || d->k2_len != nullptr || d->l_extra != nullptr) {
     const bool takes = variant == V_S16 || variant == V_A16 ||
-                       ((variant == V_P1 || variant == V_P2 || variant == V_P2A) && d->k2_full == nullptr);
+                       ((variant == V_P1 || variant == V_P2 || anchored) && d->k2_full == nullptr);
     if (!takes) variant = bounded ? V_S16 : V_A16;
   }
   pl.var = variant;
   pl.v = &attn_vars[variant];
   const int slots = slots_v[variant];
-  const int nqb = (d->Nq + QB - 1) / QB;
+  const int nqb = (d->Nq + pl.v->qb - 1) / pl.v->qb;
   pl.nblk = (int64_t)d->B * d->H * nqb;
   if (pl.nblk > 0x7fffffff) return VP_ERR_ARG;
   const char* ns = vp_knob(VPK_ATTN_NO_SPLIT);
@@ -2752,12 +2781,12 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
       if (S >= 2) {
         pl.ntail = tail;
         pl.nsplit = S;
-        pl.part_bytes = (int64_t)tail * S * QB * 66 * 4;
+        pl.part_bytes = (int64_t)tail * S * pl.v->qb * 66 * 4;
       }
     }
   }
   pl.ws_bytes = pl.part_bytes;
-  if (variant == V_P2A) pl.ws_bytes += ((pl.nblk - pl.ntail) + (int64_t)pl.ntail * pl.nsplit) * 4;
+  if (pl.var == V_P2A || pl.var == V_P2W) pl.ws_bytes += ((pl.nblk - pl.ntail) + (int64_t)pl.ntail * pl.nsplit) * 4;
   return VP_OK;
 }
 }  // namespace
@@ -2786,8 +2815,9 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   rc = attn_plan(d, pl);
   if (rc != VP_OK) return rc;
   const bool have_ws = workspace != nullptr && workspace_bytes >= pl.ws_bytes && ((uintptr_t)workspace & 15) == 0;
-  if (pl.var == V_P2A && !have_ws) {
-    // p2a needs its redo flags: without the workspace, the anchored 16x16x32 kernel alone (unsplit)
+  if ((pl.var == V_P2A || pl.var == V_P2W) && !have_ws) {
+    // p2a / p2w need their redo flags: without the workspace, the anchored 16x16x32 kernel alone (unsplit)
+    pl.nblk = (int64_t)d->B * d->H * ((d->Nq + QB - 1) / QB);  // a16's 256-query blocks
     pl.var = V_A16;
     pl.v = &attn_vars[V_A16];
     pl.ntail = 0;
@@ -2796,7 +2826,7 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   const AttnVar& v = *pl.v;
   const bool split = pl.ntail > 0 && have_ws;
   const int64_t main_blocks = split ? pl.nblk - pl.ntail : pl.nblk;
-  int* flags = pl.var == V_P2A ? (int*)((char*)workspace + pl.part_bytes) : nullptr;
+  int* flags = pl.var == V_P2A || pl.var == V_P2W ? (int*)((char*)workspace + pl.part_bytes) : nullptr;
   hipError_t le = hipSuccess;
   if (main_blocks > 0) {
     const AttnSplit none = {0, 1, nullptr, flags, (int)main_blocks, pl.nsplit, 0};
@@ -2810,16 +2840,19 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
     le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.threads), args, v.lds,
                          (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
-    const int nthreads = pl.ntail * QB * 16;
+    const int nthreads = pl.ntail * v.qb * 16;
     hipLaunchKernelGGL(attn_combine_kernel, dim3((nthreads + 255) / 256), dim3(256), 0, (hipStream_t)stream, *d,
-                       (int)main_blocks, pl.ntail, pl.nsplit, QB, (const float*)workspace, (const int*)flags);
+                       (int)main_blocks, pl.ntail, pl.nsplit, v.qb, (const float*)workspace, (const int*)flags);
   }
   if (flags != nullptr) {
-    // the blocks p2a flagged, exactly, with the anchored 16x16x32 kernel (every other workgroup returns at once)
+    // the blocks p2a / p2w flagged, exactly, with the anchored 16x16x32 kernel (every other workgroup returns at
+    // once); its blocks are 256 queries, p2w's flags per 512 (flag_shift)
     const AttnVar& r = attn_vars[V_A16];
-    const AttnSplit rs = {0, 1, nullptr, flags, (int)main_blocks, split ? pl.nsplit : 1, 1};
+    const int shift = v.qb == 512 ? 1 : 0;
+    const AttnSplit rs = {0, 1, nullptr, flags, (int)main_blocks, split ? pl.nsplit : 1, 1, shift};
+    const int64_t rblk = (int64_t)d->B * d->H * ((d->Nq + QB - 1) / QB);
     void* args[] = {(void*)d, (void*)&rs};
-    le = hipLaunchKernel(r.fn, dim3((unsigned)pl.nblk), dim3(r.threads), args, r.lds, (hipStream_t)stream);
+    le = hipLaunchKernel(r.fn, dim3((unsigned)rblk), dim3(r.threads), args, r.lds, (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
   }
   VP_CHECK_LAUNCH();
