@@ -966,9 +966,11 @@ VP_DEV void p1_mask(f32x16& s, int rem, int hl4) {
 // end of step (3, 0), after V(3) is read
 // VMC (SL = 2): the seam's vmcnt when the tile after next is already in flight (p2w: a 4-slot ring, tile t + 2
 // issued at the top of tile t, VMC = this tile's DMA instructions per wave; 0 for the 2-slot ring)
+// sync (SL = 2): the seam waits for the DMA and passes the barrier (false: the next tile was published by an earlier
+// barrier — p2w's one barrier per two tiles)
 template <int SL, bool ANCH = false, int VMC = 0>
 VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn, int lim, bool masked, bool last,
-                    bool wait_all, int lane, const int (&vo)[2]) {
+                    bool wait_all, int lane, const int (&vo)[2], bool sync = true) {
   const int hl = lane >> 5;
   const char* Vl = Kl + KT;
 #pragma unroll
@@ -994,11 +996,13 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
         p1_step<0, 1, 1, 0, 0, true, false, ANCH>(r, sel);
       p1_read_v(Vl, h, vo, r.vf[0]);
       if (h == 3 && !last) {
-        if (VMC == 0 || wait_all)
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VMC) : "memory");
-        __builtin_amdgcn_s_barrier();
+        if (sync) {
+          if (VMC == 0 || wait_all)
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VMC) : "memory");
+          __builtin_amdgcn_s_barrier();
+        }
         asm volatile("" ::: "memory");
         p1_read_k(Kn, 0, lane, r.kf[0]);
       }
@@ -1066,11 +1070,14 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
 // ring (tile t + 2 issued at the top of tile t): a K / V tile loaded once serves twice the queries, so each wave
 // issues half the LDS-DMA instructions per tile (4 instead of 8) — the DMA issue is ~7 % of p2a's time
 // (tools/attn_clock.py ablation) — and the L2 -> LDS bytes per FLOP halve.
-template <bool TAIL = false, int SL = 4, bool ANCH = false, int NWV = 4>
+// TPB = 2 (p2w only): one barrier per two tiles — tiles t + 2 and t + 3 issued together at the top of every even tile
+// of the range, both waited for and published by the barrier at the seam of the odd tile before them.
+template <bool TAIL = false, int SL = 4, bool ANCH = false, int NWV = 4, int TPB = 1>
 __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_fwd_p1(const vp_attn_desc d,
                                                                                         const AttnSplit sp) {
   static_assert(!ANCH || SL == 2, "the anchored form is the two-workgroups-per-CU pipeline");
   static_assert(NWV == 4 || (NWV == 8 && SL == 2), "8-wave workgroups run the p2 schedule");
+  static_assert(TPB == 1 || NWV == 8, "one barrier per two tiles needs the 4-slot ring");
   constexpr int QBV = NWV * 64;               // queries per workgroup
   constexpr int PPWV = NP / NWV;              // DMA pieces per operand, wave and tile
   constexpr int RING = NWV == 8 ? 4 : SL;     // LDS ring slots
@@ -1199,7 +1206,10 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
   // (a tail-split range is empty when k2_len leaves this row fewer tiles than splits: its record is O = 0, l = 0)
   const bool any = tbeg < tend;  // workgroup-uniform
   if (any) issue(tbeg);
-  if (AHEAD == 2 && tbeg + 1 < tend) {
+  if (TPB == 2 && tbeg + 1 < tend) {  // both tiles of the first pair, published by the prologue barrier
+    issue(tbeg + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (AHEAD == 2 && tbeg + 1 < tend) {
     issue(tbeg + 1);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPWV) : "memory");
   } else {
@@ -1241,15 +1251,25 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
   ClockStamp ck;
   ck.start();
   for (int ti = tbeg; ti < tend; ++ti) {
-    if (ti + AHEAD < tend && (!(VP_P1_ABL & 1) || ti == tbeg)) issue(ti + AHEAD);
+    bool sync = true;
+    if constexpr (TPB == 2) {
+      const bool even = ((ti - tbeg) & 1) == 0;
+      if (even) {
+        if (ti + 2 < tend) issue(ti + 2);
+        if (ti + 3 < tend) issue(ti + 3);
+      }
+      sync = !even;
+    } else if (ti + AHEAD < tend && (!(VP_P1_ABL & 1) || ti == tbeg)) {
+      issue(ti + AHEAD);
+    }
     int lim = KB;
     if (ti >= full1) {
       const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
       lim = sg.n - sg.key0;
     }
-    p1_tile<SL, ANCH, RING == 4 && SL == 2 ? 2 * PPWV : 0>(r, sel, slot_of(ti), slot_of(ti + 1),
-                                                            __builtin_amdgcn_readfirstlane(lim), lim < KB,
-                                                            ti + 1 >= tend, ti + 2 >= tend, lane, vo);
+    p1_tile<SL, ANCH, RING == 4 && SL == 2 && TPB == 1 ? 2 * PPWV : 0>(
+        r, sel, slot_of(ti), slot_of(ti + 1), __builtin_amdgcn_readfirstlane(lim), lim < KB, ti + 1 >= tend,
+        TPB == 2 || ti + 2 >= tend, lane, vo, sync);
   }
   // drain: PV + row sums of the last job (3, 1)
 #pragma unroll
@@ -2672,7 +2692,7 @@ struct AttnVar {
 #else
 #define VP_EXTRA(a, b) nullptr, nullptr
 #endif
-enum { V_LAZY, V_W32, V_W64, V_S16, V_A16, V_S16I, V_P1, V_W64F, V_P2, V_P2A, V_P2W, V_NVAR };
+enum { V_LAZY, V_W32, V_W64, V_S16, V_A16, V_S16I, V_P1, V_W64F, V_P2, V_P2A, V_P2W, V_P2W2, V_NVAR };
 static const AttnVar attn_vars[] = {
     {"lazy", VP_EXTRA(attn_fwd<MODE_LAZY>, (attn_fwd<MODE_LAZY, true>)), NW * 64, LDS_BYTES},
     {"w32", VP_EXTRA(attn_fwd<MODE_BOUNDED>, (attn_fwd<MODE_BOUNDED, true>)), NW * 64, LDS_BYTES},
@@ -2686,6 +2706,9 @@ static const AttnVar attn_vars[] = {
     {"p2a", (const void*)attn_fwd_p1<false, 2, true>, (const void*)attn_fwd_p1<true, 2, true>, NW4 * 64, 2 * ST + 16},
     // p2a in 8-wave workgroups of 512 queries on a 4-slot ring (attn_fwd_p1 NWV = 8)
     {"p2w", (const void*)attn_fwd_p1<false, 2, true, 8>, (const void*)attn_fwd_p1<true, 2, true, 8>, 8 * 64,
+     4 * ST + 32, 512},
+    // p2w with one barrier per two tiles
+    {"p2w2", (const void*)attn_fwd_p1<false, 2, true, 8, 2>, (const void*)attn_fwd_p1<true, 2, true, 8, 2>, 8 * 64,
      4 * ST + 32, 512},
 };
 #undef VP_EXTRA
@@ -2754,7 +2777,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   // profiles/r04_attn_p2a_ab.log: the anchor costs nothing and no bound has to hold); p2 stays the bounded challenger
   if (variant < 0) variant = V_P2A;
   // an unbounded launch needs a kernel that does not assume the bound: lazy, a16, p2a or p2w
-  const bool anchored = variant == V_P2A || variant == V_P2W;
+  const bool anchored = variant == V_P2A || variant == V_P2W || variant == V_P2W2;
   if (!bounded && variant != V_LAZY && variant != V_A16 && !anchored) return VP_ERR_UNSUPPORTED;
   if (attn_vars[variant].fn == nullptr) return VP_ERR_UNSUPPORTED;
   // the resample processor's segment hints: k2_len / l_extra (the closed-form null keys, the default) are taken by
@@ -2786,7 +2809,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
     }
   }
   pl.ws_bytes = pl.part_bytes;
-  if (pl.var == V_P2A || pl.var == V_P2W) pl.ws_bytes += ((pl.nblk - pl.ntail) + (int64_t)pl.ntail * pl.nsplit) * 4;
+  if (pl.var == V_P2A || pl.var == V_P2W || pl.var == V_P2W2) pl.ws_bytes += ((pl.nblk - pl.ntail) + (int64_t)pl.ntail * pl.nsplit) * 4;
   return VP_OK;
 }
 }  // namespace
@@ -2815,7 +2838,7 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   rc = attn_plan(d, pl);
   if (rc != VP_OK) return rc;
   const bool have_ws = workspace != nullptr && workspace_bytes >= pl.ws_bytes && ((uintptr_t)workspace & 15) == 0;
-  if ((pl.var == V_P2A || pl.var == V_P2W) && !have_ws) {
+  if ((pl.var == V_P2A || pl.var == V_P2W || pl.var == V_P2W2) && !have_ws) {
     // p2a / p2w need their redo flags: without the workspace, the anchored 16x16x32 kernel alone (unsplit)
     pl.nblk = (int64_t)d->B * d->H * ((d->Nq + QB - 1) / QB);  // a16's 256-query blocks
     pl.var = V_A16;
@@ -2826,7 +2849,7 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   const AttnVar& v = *pl.v;
   const bool split = pl.ntail > 0 && have_ws;
   const int64_t main_blocks = split ? pl.nblk - pl.ntail : pl.nblk;
-  int* flags = pl.var == V_P2A || pl.var == V_P2W ? (int*)((char*)workspace + pl.part_bytes) : nullptr;
+  int* flags = pl.var == V_P2A || pl.var == V_P2W || pl.var == V_P2W2 ? (int*)((char*)workspace + pl.part_bytes) : nullptr;
   hipError_t le = hipSuccess;
   if (main_blocks > 0) {
     const AttnSplit none = {0, 1, nullptr, flags, (int)main_blocks, pl.nsplit, 0};
