@@ -240,7 +240,8 @@ def cpu_full_step(dtype=torch.bfloat16) -> dict:
 
 def build_models(device, seed: int, rank: int, world: int, bcast: str = "scatter_allgather"):
     """Random-init 5b-I2V transformer + 2-layer branch; for N>1 initialised on rank 0 and broadcast over RCCL.
-    Returns (transformer, branch, broadcast seconds or None)."""
+    Returns (transformer, branch, replication record or None): {"seconds": the chosen method's time (float),
+    "method", "per_method": {method: seconds}, "verified_buckets": {method: count}}."""
     from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, device_scope
     from videopainter_amd.config import COGVIDEOX_5B_I2V
     # config 5 (720x1280): random-init 5b-shaped model whose learned positional embedding is sized for the latent
@@ -257,7 +258,7 @@ def build_models(device, seed: int, rank: int, world: int, bcast: str = "scatter
         # replicate with the chosen method (timed), check every rank's bytes against rank 0's (per-bucket digests:
         # the first hardware run of the RCCL-only code paths validates itself), then time the other method too
         from videopainter_amd.distributed import barrier, broadcast_module, verify_replicas
-        t_b = {}
+        t_b = {"method": bcast, "per_method": {}, "verified_buckets": {}}
         for method in (bcast, "broadcast" if bcast == "scatter_allgather" else "scatter_allgather"):
             torch.cuda.synchronize()
             barrier(device)
@@ -266,11 +267,12 @@ def build_models(device, seed: int, rank: int, world: int, bcast: str = "scatter
                 broadcast_module(m, src=0, method=method)
             torch.cuda.synchronize()
             barrier(device)
-            t_b[method] = time.perf_counter() - t0
+            t_b["per_method"][method] = time.perf_counter() - t0
             checks = [verify_replicas(m) for m in (tr, br)]
             if not all(ok for ok, _ in checks):
                 raise RuntimeError(f"weight replication ({method}) left ranks with different weights")
-            t_b[method + "_verified_buckets"] = sum(n for _, n in checks)
+            t_b["verified_buckets"][method] = sum(n for _, n in checks)
+        t_b["seconds"] = t_b["per_method"][bcast]
     torch.cuda.synchronize()
     return tr, br, t_b
 
@@ -506,6 +508,9 @@ def main():
                          "as a window-stage pipeline (point-to-point hand-offs; = --config 4)")
     ap.add_argument("--bcast", default="scatter_allgather", choices=("scatter_allgather", "broadcast"),
                     help="weight replication for N > 1 (distributed.broadcast_module)")
+    ap.add_argument("--lora-rank", type=int, default=0,
+                    help="> 0: a synthetic VideoPainterID-style adapter of this rank on every transformer block's "
+                         "to_q / to_k / to_v / to_out.0, loaded as the reference loads it (unfused, PEFT's forward)")
     ap.add_argument("--qk-gamma", type=float, default=0.0,
                     help="> 0: every norm_q / norm_k gain drawn U(0.1, G) per channel (trained-like qk-LayerNorm "
                          "weights; past the static score bound the attention runs the anchored kernel)")
@@ -552,6 +557,21 @@ def main():
 
     t_setup = time.time()
     tr, br, t_bcast = build_models(device, 1234, rank, world, args.bcast)
+    if args.lora_rank > 0:
+        from videopainter_amd.lora import attach_lora_
+        gl = torch.Generator(device=device).manual_seed(91)
+        lsd = {}
+        for i, blk in enumerate(tr.transformer_blocks):
+            for t, lin in (("to_q", blk.attn1.to_q), ("to_k", blk.attn1.to_k), ("to_v", blk.attn1.to_v),
+                           ("to_out.0", blk.attn1.to_out[0])):
+                o_f, i_f = lin.weight.shape
+                lsd[f"transformer_blocks.{i}.attn1.{t}.lora_A.weight"] = (
+                    torch.randn(args.lora_rank, i_f, device=device, generator=gl) * i_f ** -0.5).to(torch.bfloat16)
+                lsd[f"transformer_blocks.{i}.attn1.{t}.lora_B.weight"] = (
+                    torch.randn(o_f, args.lora_rank, device=device, generator=gl) * 0.01).to(torch.bfloat16)
+        attach_lora_(tr, lsd, 1.0, "vpid")
+        del lsd
+        log(f"[bench] rank-{args.lora_rank} LoRA on {4 * len(tr.transformer_blocks)} projections, unfused")
     bounded_layers = None
     if args.qk_gamma > 0:
         from videopainter_amd.attention_processor import bounded_scores
@@ -665,7 +685,9 @@ def main():
                        "clips": clips, "cfg_batch": B, "tokens": NTOK, "layers": L, "branch_layers": LB,
                        "parallelism": par,
                        **({"qk_norm_gain_max": args.qk_gamma, "layers_within_static_score_bound": bounded_layers}
-                          if args.qk_gamma > 0 else {})},
+                          if args.qk_gamma > 0 else {}),
+                       **({"lora_rank": args.lora_rank, "lora": "unfused (PEFT's forward), not in step_flop"}
+                          if args.lora_rank > 0 else {})},
             "roofline": rf,
             "roofline_kernels": classes,
             "step_mfma_frac": step_frac,
@@ -673,7 +695,8 @@ def main():
             "step_flop": step_flops(),
             "gemm_ms_per_step": classes["gemm"]["ms_per_step"],
             "attention_ms_per_step": classes["attention"]["ms_per_step"],
-            "weight_broadcast_s": t_bcast,
+            "weight_broadcast_s": t_bcast["seconds"] if t_bcast else None,
+            "weight_replication": t_bcast,
             "timing": "timed steps uninstrumented; per-kernel numbers from a separate instrumented pass of "
                       f"{n_prof} steps (HIP events on the launch stream)",
             "cpu_baseline": cpu,

@@ -103,6 +103,15 @@ typedef struct vp_gemm_desc {
   float qk_eps[2];
   const float* rope_cos; /* NULL: no RoPE (image_rotary_emb None) */
   const float* rope_sin;
+  /* Per-segment A tail (unfused LoRA, PEFT's y = x W^T + s (x A^T) B^T as ONE GEMM on K-augmented operands;
+   * DF/loaders/lora_pipeline.py:2632-2705 load_lora_into_transformer, infer/inpaint.py:310-316): a_tail_k > 0 splits
+   * K at a_tail_k; for k >= a_tail_k, segment s reads A column k + a_tail_off[s] (its own rank block of
+   * T = x [A_0; A_1; ...]^T stored after x in the same rows), so every weight segment carries only its own rank
+   * (W_s = [W0_s | s B_s], K = a_tail_k + r).  Needs K % 64 == a_tail_k % 64 == 0, n_seg % 256 == 0 with more than one
+   * segment, the default
+   * main loop (VP_ERR_UNSUPPORTED otherwise) and epilogue BIAS, GATED or BIAS_QKNORM_ROPE.  0: no tail.  (ABI 14.) */
+  int32_t a_tail_k, pad3;
+  int64_t a_tail_off[3];
 } vp_gemm_desc;
 
 int vp_gemm_bf16(const vp_gemm_desc* d, void* stream);

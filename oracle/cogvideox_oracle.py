@@ -122,7 +122,16 @@ def apply_rotary_emb(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> t
 # ------------------------------------------------------------------------------------------------------------------
 
 def linear(x, sd: SD, p: str):
-    return F.linear(x, sd[p + ".weight"], sd.get(p + ".bias"))
+    """nn.Linear; with LoRA factors in the state dict (`<p>.lora_A.weight` [r, in], `<p>.lora_B.weight` [out, r] and
+    the scaling `<p>.lora_scaling`), PEFT's UNMERGED LoRA Linear forward, which the reference runs for the
+    VideoPainterID adapter (infer/inpaint.py:310-316: load_lora_weights, fuse_lora commented out; peft is an unpinned
+    requirement, requirements.txt:21, not installed here — its published `lora.Linear.forward`:
+    result = base_layer(x); result = result + lora_B(lora_A(dropout(x))) * scaling, dropout 0 at inference)."""
+    y = F.linear(x, sd[p + ".weight"], sd.get(p + ".bias"))
+    A = sd.get(p + ".lora_A.weight")
+    if A is not None:
+        y = y + F.linear(F.linear(x, A), sd[p + ".lora_B.weight"]) * float(sd[p + ".lora_scaling"])
+    return y
 
 
 def layer_norm(x, sd: SD, p: str, eps: float):

@@ -13,7 +13,8 @@ Steps, each an assertion:
   4. after install(), both reference pipelines the scripts build (infer/inpaint.py:286-316 and
      train/train_cogvideox_inpainting_i2v_video.py:1949-1958) construct with every drop-in passed, and hold them;
   5. `pipe.load_lora_weights(dir, weight_name=..., adapter_name="test_1", target_modules=["transformer"])`
-     (infer/inpaint.py:310-315) folds the adapter into the drop-in, `get_list_adapters()` reports it.
+     (infer/inpaint.py:310-315) attaches the adapter to the drop-in unfused, `get_list_adapters()` reports it,
+     `fuse_lora` folds it.
 Prints one JSON line with what it checked.
 """
 import json
@@ -124,7 +125,15 @@ def main(tmp: str) -> None:
     assert adapters == {"transformer": ["test_1"]}, adapters
     A = sd["transformer.transformer_blocks.0.attn1.to_q.lora_A.weight"]
     B = sd["transformer.transformer_blocks.0.attn1.to_q.lora_B.weight"]
-    assert torch.equal(tr.transformer_blocks[0].attn1.to_q.weight, (w0 + B @ A).to(dt))
+    # applied unfused, as the reference's PEFT does: W0 untouched, the augmented weight tail = s B (s = 1)
+    from videopainter_amd.lora import AugmentedProjection
+    q = tr.transformer_blocks[0].attn1.to_q
+    assert torch.equal(q.weight.float(), w0)
+    wa = AugmentedProjection.of((q,)).weights()[0]
+    assert torch.equal(wa[:, :w0.shape[1]].float(), w0) and torch.equal(wa[:, w0.shape[1]:w0.shape[1] + 4],
+                                                                       B.to(dt).float().to(dt))
+    pipe.fuse_lora(lora_scale=1.0)  # the explicit fold (infer/inpaint.py:316, commented out there)
+    assert torch.equal(q.weight, (w0 + B.to(dt).float() @ A.to(dt).float()).to(dt))
     print(json.dumps({"rejected_before_install": rejected, "rebased": rebased,
                       "pipelines": ["CogVideoXI2VDualInpaintAnyLPipeline", "CogVideoXI2VDualInpaintPipeline"],
                       "lora_adapters": adapters}))

@@ -493,6 +493,60 @@ def test_gemm_qknorm_rope_epilogue_matches_separate_kernels(H, T, rope, gemm_var
         assert rel(got.view(B, Ntok, 3 * D)[..., s * D:(s + 1) * D], n.transpose(1, 2).reshape(B, Ntok, D)) < 8e-3
 
 
+@pytest.mark.parametrize("r", [64, 256])
+def test_gemm_a_tail_matches_materialized_operands(r):
+    """The per-segment A tail (vp_gemm_desc.a_tail_k / a_tail_off; unfused LoRA, lora.AugmentedProjection): segment s
+    of one launch reading x_aug = [x | T_0 | T_1 | T_2] with its K-tiles past K0 shifted to T_s gives, bit for bit,
+    the GEMM of that segment alone on the materialised operand [x | T_s] — for the fused QKV with its qk-norm + RoPE
+    epilogue, the plain bias epilogue and the gated residual of to_out (one segment) — and ragged M."""
+    from types import SimpleNamespace
+
+    from videopainter_amd import _native as N
+    from videopainter_amd import kernels as K
+    B, T, Nv, H = 2, 37, 1263, 4
+    Ntok, D = T + Nv, H * 64
+    K0 = 512
+    xa = bf(rnd(B * Ntok, K0 + 3 * r, seed=140)).to(dev)
+    ws = [bf(rnd(D, K0 + r, std=(K0 + r) ** -0.5, seed=141 + i)).to(dev) for i in range(3)]
+    bs = [bf(rnd(D, std=0.1, seed=144 + i)).to(dev) for i in range(3)]
+    lns = tuple(SimpleNamespace(weight=bf(1 + 0.1 * rnd(64, seed=147 + i)).to(dev),
+                                bias=bf(0.1 * rnd(64, seed=149 + i)).to(dev), eps=1e-6) for i in range(2))
+    cos, sin = rnd(Nv, 64, seed=151).to(dev), rnd(Nv, 64, seed=152).to(dev)
+    resid = bf(rnd(B, Ntok, D, seed=153)).to(dev)
+    mod = bf(rnd(B, 6 * D, seed=154)).to(dev)
+    tail = (K0, [0, r, 2 * r])
+    mat = [torch.cat([xa[:, :K0], xa[:, K0 + s * r:K0 + (s + 1) * r]], 1).contiguous() for s in range(3)]
+    # bias, 3 segments
+    o = torch.empty(B * Ntok, 3 * D, device=dev, dtype=torch.bfloat16)
+    K.gemm(xa, ws, bs, o, a_tail=tail)
+    for s in range(3):
+        ref = torch.empty(B * Ntok, D, device=dev, dtype=torch.bfloat16)
+        K.gemm(mat[s], [ws[s]], [bs[s]], ref)
+        assert torch.equal(o[:, s * D:(s + 1) * D], ref), ("bias", s)
+    # the fused QKV epilogue: q / k through LayerNorm(64) + RoPE, v plain (materialised: one 3-segment launch on a
+    # stacked operand is impossible, so compare each segment's pre-norm GEMM through the unfused epilogue kernels)
+    o = torch.empty(B, Ntok, 3 * D, device=dev, dtype=torch.bfloat16)
+    K.gemm(xa, ws, bs, o.view(-1, 3 * D), epilogue=N.EPI_BIAS_QKNORM_ROPE, qk_norm=lns, rope=(cos, sin),
+           tokens_per_batch=Ntok, text_len=T, a_tail=tail)
+    for s in range(3):
+        pre = torch.empty(B, Ntok, D, device=dev, dtype=torch.bfloat16)
+        K.gemm(mat[s], [ws[s]], [bs[s]], pre.view(-1, D))
+        if s < 2:
+            ref = torch.empty_like(pre)
+            K.head_norm_rope(pre, ref, H, T, lns[s].weight, lns[s].bias, lns[s].eps, (cos, sin))
+        else:
+            ref = pre
+        assert torch.equal(o[..., s * D:(s + 1) * D], ref), ("qknorm", s)
+    # the gated residual (to_out: one segment reading T_0)
+    o = torch.empty(B * Ntok, D, device=dev, dtype=torch.bfloat16)
+    K.gemm(xa, ws[:1], bs[:1], o, epilogue=N.EPI_GATED, resid=resid, mod=mod, tokens_per_batch=Ntok, text_len=T,
+           a_tail=(K0, [0]))
+    ref = torch.empty_like(o)
+    K.gemm(mat[0], ws[:1], bs[:1], ref, epilogue=N.EPI_GATED, resid=resid, mod=mod, tokens_per_batch=Ntok,
+           text_len=T)
+    assert torch.equal(o, ref)
+
+
 @pytest.mark.parametrize("Kk", [512, 640, 3072])
 def test_gemm_staggered_matches_quadrant_pipeline(Kk, knobs):
     """Variant 11 (the quadrant pipeline with the two wave groups staggered by one barrier), variant 13 (the default:

@@ -33,7 +33,8 @@ class GemmDesc(C.Structure):
                 ("inject", vp), ("inject_ld", i64), ("inject_bstride", i64), ("inject_mask", vp),
                 ("inject_mask_bstride", i64),
                 ("addrows", vp), ("addrows_ld", i64), ("addrows_offset", i64),
-                ("qk_ln_w", vp * 2), ("qk_ln_b", vp * 2), ("qk_eps", f32 * 2), ("rope_cos", vp), ("rope_sin", vp)]
+                ("qk_ln_w", vp * 2), ("qk_ln_b", vp * 2), ("qk_eps", f32 * 2), ("rope_cos", vp), ("rope_sin", vp),
+                ("a_tail_k", i32), ("pad3", i32), ("a_tail_off", i64 * 3)]
 
 
 class AttnDesc(C.Structure):

@@ -104,14 +104,15 @@ def _qkv(attn, x: torch.Tensor, norm_rope=None) -> torch.Tensor:
     bs = [attn.to_q.bias, attn.to_k.bias, attn.to_v.bias]
     a = x.reshape(-1, D)
     aug = AugmentedProjection.of((attn.to_q, attn.to_k, attn.to_v))
-    if aug is not None:  # trainable LoRA factors, unfused (lora.AugmentedProjection)
-        a, ws = aug.input(a), aug.weights()
-    if norm_rope is None:
-        K.gemm(a, ws, bs, out.view(B * Ntok, -1))
-    else:
+    kw = {}
+    if norm_rope is not None:
         text_len, rope = norm_rope
-        K.gemm(a, ws, bs, out.view(B * Ntok, -1), epilogue=NAT.EPI_BIAS_QKNORM_ROPE,
-               qk_norm=(attn.norm_q, attn.norm_k), rope=rope, tokens_per_batch=Ntok, text_len=text_len)
+        kw = dict(epilogue=NAT.EPI_BIAS_QKNORM_ROPE, qk_norm=(attn.norm_q, attn.norm_k), rope=rope,
+                  tokens_per_batch=Ntok, text_len=text_len)
+    if aug is not None:  # LoRA adapters, unfused (lora.AugmentedProjection)
+        aug.gemm(aug.input(a), bs, out.view(B * Ntok, -1), **kw)
+    else:
+        K.gemm(a, ws, bs, out.view(B * Ntok, -1), **kw)
     return out
 
 
@@ -121,19 +122,19 @@ def _kv(attn, x: torch.Tensor) -> torch.Tensor:
     a, ws = x.reshape(-1, D), [attn.to_k.weight, attn.to_v.weight]
     aug = AugmentedProjection.of((attn.to_k, attn.to_v))
     if aug is not None:
-        a, ws = aug.input(a), aug.weights()
-    K.gemm(a, ws, [attn.to_k.bias, attn.to_v.bias], out.view(B * Ntok, -1))
+        aug.gemm(aug.input(a), [attn.to_k.bias, attn.to_v.bias], out.view(B * Ntok, -1))
+    else:
+        K.gemm(a, ws, [attn.to_k.bias, attn.to_v.bias], out.view(B * Ntok, -1))
     return out
 
 
 def project_out(lin, o2d: torch.Tensor, out2d: torch.Tensor, **gemm_kw) -> torch.Tensor:
-    """to_out.0 on [M, D] rows with any GEMM epilogue (the block's gated residual), its trainable LoRA factor pair
-    applied unfused (lora.AugmentedProjection) when it carries one."""
-    a, ws = o2d, [lin.weight]
+    """to_out.0 on [M, D] rows with any GEMM epilogue (the block's gated residual), its LoRA adapters applied
+    unfused (lora.AugmentedProjection) when it carries any."""
     aug = AugmentedProjection.of((lin,))
     if aug is not None:
-        a, ws = aug.input(o2d), aug.weights()
-    return K.gemm(a, ws, [lin.bias], out2d, **gemm_kw)
+        return aug.gemm(aug.input(o2d), [lin.bias], out2d, **gemm_kw)
+    return K.gemm(o2d, [lin.weight], [lin.bias], out2d, **gemm_kw)
 
 
 def _fusable_norms(attn) -> bool:

@@ -78,18 +78,19 @@ def _qkv_t(attn) -> torch.Tensor:
 
 
 def _aug_tail_t(aug: AugmentedProjection) -> torch.Tensor:
-    """[Rp, sum out_i] = cat(W_aug_i[:, K:])^T = cat(s B_i, zero-padded)^T (cached on the first Linear, keyed like the
-    augmented weights)."""
+    """[R, sum out_i]: the transposed block-diagonal tail of the augmented weights — rows i r .. of projection i's
+    columns hold W_aug_i[:, K:]^T = (s B_i)^T, zero elsewhere (cached on the first Linear, keyed like them)."""
     ws = aug.weights()
     key = tuple(id(l) for l in aug.lins) + aug._key()
     owner = aug.lins[0]
     c = owner.__dict__.get("_vp_aug_tail_t")
     if c is None or c[0] != key:
         n = sum(w.shape[0] for w in ws)
-        wt = torch.empty(aug.Rp, n, device=ws[0].device, dtype=BF16)
+        wt = torch.zeros(aug.R, n, device=ws[0].device, dtype=BF16)
         off = 0
-        for w in ws:
-            K.transpose(w[:, aug.K:], out=wt[:, off:off + w.shape[0]])
+        for i, w in enumerate(ws):
+            c0 = aug.block_col(i)
+            K.transpose(w[:, c0:c0 + aug.r], out=wt[i * aug.r:(i + 1) * aug.r, off:off + w.shape[0]])
             off += w.shape[0]
         c = (key, wt)
         owner.__dict__["_vp_aug_tail_t"] = c
@@ -97,32 +98,40 @@ def _aug_tail_t(aug: AugmentedProjection) -> torch.Tensor:
 
 
 def _aug_dgrad(aug: AugmentedProjection, dy2: torch.Tensor, x2: torch.Tensor, out2: torch.Tensor, train: bool,
-               G: "_Grads", dw_aug: Optional[torch.Tensor] = None) -> None:
-    """Backward of the unfused-LoRA projection y = x_aug W_aug^T (lora.AugmentedProjection), given out2 = dy W
-    (the base dgrad): out2 += dT A_cat with dT = dy W_aug[:, K:] (= s dy B per adapter); with train, the factor
-    gradients dB = s (dy^T T) [the tail of dW_aug = dy^T x_aug, passed in as dw_aug, whose head is dW] and
-    dA = dT^T x."""
-    Kd = aug.K
+               G: "_Grads", x_aug: Optional[torch.Tensor] = None) -> None:
+    """Backward of the unfused-LoRA projections y_i = x_aug W_aug_i^T (lora.AugmentedProjection; segment i reads
+    rank block i of T = x A_cat^T), given out2 = dy W0 (the base dgrad): out2 += dT A_cat with dT = dy W_tail
+    (block i = s dy_i B_i).  With train: W0_i's gradient only when it trains (dy_i^T x), dB = s (dy_i^T T_i) from
+    the GEMM over rank block i of x_aug alone, dA = dT^T x — no full [N, K + R] weight gradient for frozen bases."""
+    Kd, r = aug.K, aug.r
     M = dy2.shape[0]
-    dT = torch.empty(M, aug.Rp, device=dy2.device, dtype=BF16)
+    dT = torch.empty(M, aug.R, device=dy2.device, dtype=BF16)
     K.gemm(dy2, [_aug_tail_t(aug)], [None], dT)
     dxl = torch.empty(M, Kd, device=dy2.device, dtype=BF16)
     K.gemm(dT, [aug.a_cat_t()], [None], dxl)  # dT A_cat
     K.axpy(out2, dxl, out=out2)
-    if train:
-        dA = K.wgrad(dT, x2)  # [Rp, K]
-        row = 0
-        for lin, pr, off in zip(aug.lins, aug.pairs, aug.offs):
-            n = lin.weight.shape[0]
-            if dw_aug is not None:
-                G.put(lin.weight, dw_aug[row:row + n, :Kd])
-            if pr is not None:
-                A, B, sc = pr
-                r = A.shape[0]
-                if dw_aug is not None:
-                    G.put(lin.lora_B.weight, dw_aug[row:row + n, Kd + off:Kd + off + r].float() * sc)
-                G.put(lin.lora_A.weight, dA[off:off + r])
-            row += n
+    if not train:
+        return
+    dA = None
+    row = 0
+    for i, (lin, ps) in enumerate(zip(aug.lins, aug.pairs)):
+        n = lin.weight.shape[0]
+        dyi = dy2[:, row:row + n]
+        if lin.weight.requires_grad:
+            G.put(lin.weight, K.wgrad(dyi, x2))
+        if any(B.requires_grad for _, B, _ in ps):
+            dbt = K.wgrad(dyi, x_aug[:, Kd + i * r:Kd + (i + 1) * r])  # [n, r] = dy_i^T T_i
+        o = 0
+        for A, B, sc in ps:
+            ra = A.shape[0]
+            if B.requires_grad:
+                G.put(B, dbt[:, o:o + ra].float() * sc)
+            if A.requires_grad:
+                if dA is None:
+                    dA = K.wgrad(dT, x2)  # [R, K]
+                G.put(A, dA[i * r + o:i * r + o + ra])
+            o += ra
+        row += n
 
 
 def _dgrad(dy2: torch.Tensor, w: torch.Tensor, out2: torch.Tensor) -> torch.Tensor:
@@ -215,8 +224,11 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     qaug = AugmentedProjection.of((a.to_q, a.to_k, a.to_v))
     oaug = AugmentedProjection.of((to_out,))
     xq = xn.view(M, D) if qaug is None else qaug.input(xn.view(M, D))
-    K.gemm(xq, [a.to_q.weight, a.to_k.weight, a.to_v.weight] if qaug is None else qaug.weights(),
-           [a.to_q.bias, a.to_k.bias, a.to_v.bias], qkv.view(M, 3 * D))
+    if qaug is None:
+        K.gemm(xq, [a.to_q.weight, a.to_k.weight, a.to_v.weight], [a.to_q.bias, a.to_k.bias, a.to_v.bias],
+               qkv.view(M, 3 * D))
+    else:
+        qaug.gemm(xq, [a.to_q.bias, a.to_k.bias, a.to_v.bias], qkv.view(M, 3 * D))
     resample = resample_mask is not None
     v = qkv[..., 2 * D:]
     if resample:
@@ -294,7 +306,7 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     # ---- attention + gated residual 1 ----
     dao = torch.empty(M, D, device=dev, dtype=BF16)
     K.rowscale(g.view(M, D), dao, Ntok, T, mod1, 2, 5)
-    dw_out = None
+    o_aug = None
     if need_dmod:
         ao = torch.empty(M, D, device=dev, dtype=BF16)
         project_out(to_out, o.view(M, D), ao)
@@ -302,15 +314,16 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
         del ao
         if train:
             if oaug is None:
-                _put_linear_grads(G, to_out, K.wgrad(dao, o.view(M, D)))
+                if to_out.weight.requires_grad:
+                    _put_linear_grads(G, to_out, K.wgrad(dao, o.view(M, D)))
             else:
-                dw_out = K.wgrad(dao, oaug.input(o.view(M, D)))
+                o_aug = oaug.input(o.view(M, D))
             G.put(to_out.bias, _total(dao))
     do = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
     _dgrad(dao, to_out.weight, do.view(M, D))
     if oaug is not None:
-        _aug_dgrad(oaug, dao, o.view(M, D), do.view(M, D), train and need_dmod, G, dw_out)
-    del dao, dw_out
+        _aug_dgrad(oaug, dao, o.view(M, D), do.view(M, D), train and need_dmod, G, o_aug)
+    del dao, o_aug
     dqkv = torch.empty(B, Ntok, 3 * D, device=dev, dtype=BF16)
     dk2 = None
     if resample:
@@ -354,15 +367,16 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     dxn = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
     K.gemm(dqkv.view(M, 3 * D), [_qkv_t(a)], [None], dxn.view(M, D))
     if train:
-        dw = K.wgrad(dqkv.view(M, 3 * D), xq)
         db = _total(dqkv.view(M, 3 * D))
-        for s, lin in enumerate((a.to_q, a.to_k, a.to_v)):
-            if qaug is None:
+        if qaug is None and any(l.weight.requires_grad for l in (a.to_q, a.to_k, a.to_v)):
+            dw = K.wgrad(dqkv.view(M, 3 * D), xq)
+            for s, lin in enumerate((a.to_q, a.to_k, a.to_v)):
                 _put_linear_grads(G, lin, dw[s * D:(s + 1) * D])
+            del dw
+        for s, lin in enumerate((a.to_q, a.to_k, a.to_v)):
             G.put(lin.bias, db[s * D:(s + 1) * D])
         if qaug is not None:
-            _aug_dgrad(qaug, dqkv.view(M, 3 * D), xn.view(M, D), dxn.view(M, D), True, G, dw)
-        del dw
+            _aug_dgrad(qaug, dqkv.view(M, 3 * D), xn.view(M, D), dxn.view(M, D), True, G, xq)
     elif qaug is not None:
         _aug_dgrad(qaug, dqkv.view(M, 3 * D), xn.view(M, D), dxn.view(M, D), False, G)
     del dqkv, xn, xq

@@ -508,7 +508,9 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
 // EPI >= 0: the epilogue kind as a compile-time constant (the default main loop is instantiated per kind: the dead
 // kinds' code and branches leave the epilogue), -1: runtime switch
 // SPLIT: the split-K instance (fp32 partial tiles to mx.ws, the epilogue runs in gemm_splitk_reduce_kernel)
-template <int VAR, bool FP8 = false, int GROUP = 4, int EPI = -1, bool SPLIT = false>
+// ATAIL: the per-segment A tail of vp_gemm_desc (unfused LoRA): A K-tiles from a_tail_k on are read a_tail_off[seg]
+// columns further right (one scalar add per A DMA of those tiles)
+template <int VAR, bool FP8 = false, int GROUP = 4, int EPI = -1, bool SPLIT = false, bool ATAIL = false>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_desc d, const MxExt mx) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -607,6 +609,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
     }
     // unit u: 0 = A quadrant-row 0, 1 = A quadrant-row 1, 2 = W quadrant-col 0, 3 = W quadrant-col 1
     // (this variant runs only for K % 64 == 0, so there is no K tail here)
+    [[maybe_unused]] int tail_tile0 = 0;
+    [[maybe_unused]] int64_t tail_skip = 0;
+    if constexpr (ATAIL) {
+      tail_tile0 = d.a_tail_k / BK;
+      const int sg = __builtin_amdgcn_readfirstlane(n0 / d.n_seg);  // n_seg % BN == 0: one segment per tile
+      tail_skip = (sg == 0 ? d.a_tail_off[0] : sg == 1 ? d.a_tail_off[1] : d.a_tail_off[2]) * 2;
+    }
     auto issue_unit = [&](int u, int tile) {
       char* base = smem + (tile & 1) * STAGE_BYTES + (u >= 2 ? TILE_BYTES : 0);
 #pragma unroll
@@ -619,6 +628,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
           else
             glds16((const char*)d.W[sgW] + (int64_t)(n0 - sgW * d.n_seg + i * 128 + (u - 2) * 32) * d.K + tile * 128,
                    uoffW, base + rb * 128);
+        } else if constexpr (ATAIL) {
+          glds16(ubase[u][i] + tile * 128 + (u < 2 && tile >= tail_tile0 ? tail_skip : 0), uoff[u][i], base + rb * 128);
         } else {
           glds16(ubase[u][i] + tile * 128, uoff[u][i], base + rb * 128);
         }
@@ -1392,7 +1403,7 @@ SplitPlan split_plan(const vp_gemm_desc* d) {
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
   const bool epi_ok = d->epilogue == VP_EPI_BIAS || d->epilogue == VP_EPI_BIAS_GELU ||
                       d->epilogue == VP_EPI_BIAS_SCALE || d->epilogue == VP_EPI_BIAS_ADDROWS;
-  if (!epi_ok || (d->K % BK) != 0) return p;
+  if (!epi_ok || (d->K % BK) != 0 || d->a_tail_k > 0) return p;
   const int64_t tile_a0 = (int64_t)BM * d->lda * 2, wseg0 = (int64_t)d->n_seg * d->K * 2;
   if (tiles >= 128) return (tile_a0 < ((int64_t)1 << 31) && wseg0 < ((int64_t)1 << 31)) ? tail_plan(d, tiles) : p;
   if (d->K < 1024) return p;
@@ -1449,6 +1460,39 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
   if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
   MxExt mx = {};
   mx.group = gemm_group(d);
+  if (d->a_tail_k != 0) {
+    // the per-segment A tail (unfused LoRA): the default main loop only, on whole K-tiles and whole-tile segments
+    static const void* const k13t[7] = {(const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS, false, true>,
+                                        nullptr, nullptr,
+                                        (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_GATED, false, true>,
+                                        nullptr, nullptr,
+                                        (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_QKNORM_ROPE, false, true>};
+    static bool attr_t = false;
+    if (!attr_t) {
+      for (const void* f : k13t)
+        if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      attr_t = true;
+    }
+    if (d->a_tail_k < 0 || d->a_tail_k >= d->K || (d->a_tail_k % BK) != 0) return VP_ERR_ARG;
+    int64_t amax = 0;
+    for (int s = 0; s < nsegs; ++s) {
+      if (d->a_tail_off[s] < 0 || (d->a_tail_off[s] % 8) != 0) return VP_ERR_ARG;
+      amax = d->a_tail_off[s] > amax ? d->a_tail_off[s] : amax;
+    }
+    if (d->lda < d->K + amax) return VP_ERR_ARG;  // every segment's tail columns inside the rows
+    const char* e = vp_knob(VPK_GEMM_VARIANT);
+    if ((e != nullptr && atoi(e) != 13) || (d->K % BK) != 0 || d->K < 8 * BK || (nsegs > 1 && (d->n_seg % BN) != 0) ||
+        k13t[d->epilogue] == nullptr || (int64_t)BM * d->lda * 2 >= ((int64_t)1 << 31) ||
+        (int64_t)d->n_seg * d->K * 2 >= ((int64_t)1 << 31))
+      return VP_ERR_UNSUPPORTED;
+    const int ttiles = ((d->M + BM - 1) / BM) * (d->N / BN);
+    void* args[] = {(void*)d, (void*)&mx};
+    const hipError_t le = hipLaunchKernel(k13t[d->epilogue], dim3(main_tiles > 0 ? min(main_tiles, ttiles) : ttiles),
+                                          dim3(NTHREADS), args, LDS_BYTES, (hipStream_t)stream);
+    if (le != hipSuccess) return (int)le;
+    VP_CHECK_LAUNCH();
+    return VP_OK;
+  }
   // main loops: 13 = the quadrant-phase pipeline with the two wave groups staggered and each slot's fragment reads
   // issued before its DMA, instantiated per epilogue kind (default: +3.6-5.2 % over 11 on every config-2 shape and
   // 283.7 against 295.4 ms of GEMM per step, profiles/r04_gemm13_ab.log), 11 = the same with the reads after the DMA

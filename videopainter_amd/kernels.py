@@ -88,10 +88,13 @@ def gemm(a: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[Opti
          mod: Optional[torch.Tensor] = None, gate_chunk: int = 2, gate_text_chunk: int = 5,
          tokens_per_batch: int = 1, text_len: int = 0, inject: Optional[torch.Tensor] = None,
          inject_ld: int = 0, inject_bstride: int = 0, inject_mask: Optional[torch.Tensor] = None,
-         addrows: Optional[torch.Tensor] = None, addrows_offset: int = 0, qk_norm=None, rope=None) -> torch.Tensor:
+         addrows: Optional[torch.Tensor] = None, addrows_offset: int = 0, qk_norm=None, rope=None,
+         a_tail: Optional[Tuple[int, Sequence[int]]] = None) -> torch.Tensor:
     """out = epilogue(a @ cat(weights).T).  `a` rows: M rows of length K at stride lda.
     EPI_BIAS_QKNORM_ROPE: qk_norm = (norm_q, norm_k) LayerNorm(64) modules, rope = (cos, sin) fp32 [N - text_len, 64]
-    or None; rows are (batch, token) with `tokens_per_batch` / `text_len`."""
+    or None; rows are (batch, token) with `tokens_per_batch` / `text_len`.
+    a_tail = (k0, offsets): the per-segment A tail (vp_gemm_desc.a_tail_k / a_tail_off; unfused LoRA): for K columns
+    k >= k0, weight segment s reads column k + offsets[s] of `a`."""
     _chk(a, "a")
     _chk(out, "out")
     K = weights[0].shape[1]
@@ -157,6 +160,13 @@ def gemm(a: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[Opti
     if epilogue == N.EPI_BIAS_ADDROWS:
         _chk(addrows, "addrows")
         d.addrows, d.addrows_ld, d.addrows_offset = _p(addrows), _rowmajor(addrows, "addrows"), addrows_offset
+    if a_tail is not None:
+        k0, offs = a_tail
+        if len(offs) != len(weights) or not 0 < k0 < K or a.shape[-1] < K + max(offs):
+            raise ValueError(f"a_tail {a_tail} does not fit a of width {a.shape[-1]} and K={K}")
+        d.a_tail_k = int(k0)
+        for i, o in enumerate(offs):
+            d.a_tail_off[i] = int(o)
     L = N.lib()
     # split-K for GEMMs too small to fill the chip (e.g. T5 at 2 x 226 rows): fp32 partials from the caching
     # allocator, so they are ordered on the launch stream

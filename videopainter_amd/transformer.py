@@ -228,9 +228,10 @@ class CogVideoXBlock(nn.Module):
             self.qkv_mx = None
             return
         a = self.attn1
-        from .lora import trainable_pair
-        if any(trainable_pair(l) is not None for l in (a.to_q, a.to_k, a.to_v)):
-            raise NotImplementedError("fp8 QKV with trainable (unfused) LoRA factors: merge or drop the adapter first")
+        from .lora import module_pairs
+        if any(module_pairs(l) for l in (a.to_q, a.to_k, a.to_v)):
+            raise NotImplementedError("fp8 QKV with unfused LoRA adapters on q / k / v: fuse_lora() (loaded adapters) "
+                                      "or drop the adapter first")
         ws = (a.to_q.weight, a.to_k.weight, a.to_v.weight)
         if any(w.shape[0] % 256 or w.shape[1] % 128 for w in ws):
             raise ValueError("fp8 QKV needs widths that are multiples of 256")
@@ -379,11 +380,11 @@ class CogVideoXTransformer3DModel(ModelMixin):
         self._build_head(inner_dim, time_embed_dim, norm_elementwise_affine, norm_eps, patch_size, out_channels)
 
     def load_lora_weights(self, path: str, weight_name: str = "pytorch_lora_weights.safetensors",
-                          adapter_name: Optional[str] = None, lora_scale: float = 1.0, **_):
-        """The VideoPainterID adapter (PEFT safetensors) folded into to_q/to_k/to_v/to_out.0 at load time
-        (videopainter_amd/lora.py; the reference applies it unfused through PEFT, infer/inpaint.py:310-315).
-        `lora_scale` is the scale folded now; every forward re-folds to its own `attention_kwargs["scale"]`
-        (default 1.0, as the reference's per-call scaling) when that differs."""
+                          adapter_name: Optional[str] = None, lora_scale: Optional[float] = None, **_):
+        """The VideoPainterID adapter (PEFT safetensors) on to_q/to_k/to_v/to_out.0, applied UNFUSED as the
+        reference's PEFT does (infer/inpaint.py:310-316; videopainter_amd/lora.py): the projections run on K-augmented
+        operands, W0 untouched.  Every forward applies its own `attention_kwargs["scale"]` (default 1.0);
+        `lora_scale` sets it now.  `fuse_lora` folds explicitly."""
         from .lora import attach_lora_, load_lora_state_dict
         sd = load_lora_state_dict(path, weight_name)
         if any(k.startswith("transformer.") for k in sd):  # the pipeline-level file (lora_pipeline.py:2653-2656)
@@ -397,7 +398,8 @@ class CogVideoXTransformer3DModel(ModelMixin):
         return [n for n, _ in st.adapters] if st is not None else []
 
     def set_lora_scale(self, scale: float):
-        """Fold the attached adapters at `scale` (what a call with attention_kwargs={"scale": scale} does)."""
+        """The per-call LoRA scale (what a call with attention_kwargs={"scale": scale} does): unfused adapters take
+        it in their augmented operands; weights holding a fold are rebuilt exactly from their kept base."""
         from .lora import lora_state, refold_lora_
         st = lora_state(self)
         if st is not None and st.scale != float(scale):
@@ -411,13 +413,16 @@ class CogVideoXTransformer3DModel(ModelMixin):
         return self
 
     def fuse_lora(self, lora_scale: float = 1.0):
-        """The pipeline's `fuse_lora(lora_scale=...)`: fold at `lora_scale` and stop following per-call scales
-        (PEFT's merged layers no longer see `scale_lora_layers`)."""
-        from .lora import lora_state
-        self.set_lora_scale(lora_scale)
-        st = lora_state(self)
-        if st is not None:
-            st.fused = True
+        """The pipeline's `fuse_lora(lora_scale=...)`: the loaded adapters folded into W0 + s B A at `lora_scale`
+        (base kept), no longer following per-call scales (PEFT's merged layers no longer see `scale_lora_layers`)."""
+        from .lora import fuse_lora_
+        fuse_lora_(self, lora_scale)
+        return self
+
+    def unfuse_lora(self):
+        """PEFT's `unfuse_lora`: back to W0 (exact, from the kept base) with the adapters applied unfused."""
+        from .lora import unfuse_lora_
+        unfuse_lora_(self)
         return self
 
     def add_adapter(self, adapter_config, adapter_name: str = "default"):
@@ -446,8 +451,6 @@ class CogVideoXTransformer3DModel(ModelMixin):
         from .lora import lora_state
         st = lora_state(self)
         if st is None:
-            return
-        if st.fused:
             return
         s = attention_kwargs.get("scale", 1.0) if attention_kwargs else 1.0
         self.set_lora_scale(1.0 if s is None else s)

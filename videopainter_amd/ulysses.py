@@ -341,8 +341,9 @@ class _TransformerView:
             raise NotImplementedError("the previous-clip blend is not split head-parallel")
         if id_pool_resample_learnable:
             raise NotImplementedError("the ID-resample processor is not split head-parallel")
-        # the per-call LoRA scale (attention_kwargs["scale"], default 1.0) re-folds the attached adapters, and an
-        # optimizer step's factor updates are synced, exactly as the single-GPU forward does (transformer.py)
+        # the per-call LoRA scale (attention_kwargs["scale"], default 1.0): unfused adapters take it in their
+        # augmented operands (rebuilt from the live factors, so an optimizer step's updates reach them too), exactly as
+        # the single-GPU forward does (transformer.py, lora.AugmentedProjection)
         self.model._call_lora_scale(attention_kwargs)
         res = transformer_forward(self.model, self.o.comm, self.o.rank, hidden_states, encoder_hidden_states,
                                   timestep, image_rotary_emb, branch_block_samples, branch_block_masks, add_first,
