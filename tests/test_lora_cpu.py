@@ -263,12 +263,12 @@ def test_trainable_adapter_runs_unfused_on_augmented_operands():
 
 
 def test_augmented_operands_with_the_per_segment_tail():
-    """256-wide projections (4 heads): the per-segment A tail layout — W_aug_i = [W0_i | s B_i] (K + r columns),
+    """512-wide projections (8 heads): the per-segment A tail layout — W_aug_i = [W0_i | s B_i] (K + r columns),
     segment i reading rank block i of T (a_tail_off[i] = i r) — equals the unmerged LoRA of each projection; the
     prev-clip K/V group shares the fused QKV group's per-Linear weight cache."""
     from videopainter_amd import CogVideoXTransformer3DModel
     from videopainter_amd.lora import AugmentedProjection
-    cfg = dict(TINY_CFG, num_attention_heads=4)
+    cfg = dict(TINY_CFG, num_attention_heads=8)  # 512-wide: K + r >= 8 K-tiles
     tr = CogVideoXTransformer3DModel(**cfg)
     tr.init_synthetic_weights_(4)
     tr.add_adapter({"r": 8, "lora_alpha": 4})
@@ -279,6 +279,7 @@ def test_augmented_operands_with_the_per_segment_tail():
             l.lora_B.weight.copy_(torch.randn(l.lora_B.weight.shape, generator=g) * 0.1)
     aug = AugmentedProjection.of((a.to_q, a.to_k, a.to_v))
     assert not aug.full and aug.r == 64 and aug.tail == (aug.K, [0, 64, 128])
+    assert AugmentedProjection.of((a.to_out[0],)).tail is None  # one projection: a plain GEMM on [x | T]
     x = torch.randn(8, aug.K, generator=g)
     T = x @ aug.a_cat().float().t()
     for i, (l, w) in enumerate(zip((a.to_q, a.to_k, a.to_v), aug.weights())):

@@ -402,8 +402,10 @@ class AugmentedProjection:
         self.r = (max(self.ranks) + AUG_ALIGN - 1) // AUG_ALIGN * AUG_ALIGN
         self.R = self.r * len(self.lins)
         self.K = self.lins[0].weight.shape[1]
-        self.full = len(self.lins) > 1 and any(l.weight.shape[0] % 256 for l in self.lins)
-        self.tail = None if self.full else (self.K, [i * self.r for i in range(len(self.lins))])
+        # the tail form needs whole 256-column tiles per segment and >= 8 K-tiles (the GEMM's default loop); one
+        # projection needs no tail at all (its rank block starts right after x)
+        self.full = len(self.lins) > 1 and (any(l.weight.shape[0] % 256 for l in self.lins) or self.K + self.r < 512)
+        self.tail = None if self.full or len(self.lins) == 1 else (self.K, [i * self.r for i in range(len(self.lins))])
 
     def block_col(self, i: int) -> int:
         """First column of projection i's rank block in W_aug_i."""
@@ -487,4 +489,6 @@ class AugmentedProjection:
     def gemm(self, x_aug: torch.Tensor, biases, out2d: torch.Tensor, **kw) -> torch.Tensor:
         """The projections' GEMM on the augmented operands (any epilogue of the bf16 GEMM's tail form)."""
         from . import kernels as K
+        if self.tail is None:  # block-diagonal form, or one projection: x_aug's first K + width columns
+            return K.gemm(x_aug, self.weights(), biases, out2d, **kw)
         return K.gemm(x_aug, self.weights(), biases, out2d, a_tail=self.tail, **kw)
