@@ -562,7 +562,7 @@ def test_fp8_attention_model_modes(env):
         assert r8 <= 1.5 * r16, (mode, r8, r16)  # measured (r02): r8 / r16 = 1.00
 
 
-def _lora_case(tmp_path, rank=16):
+def _lora_case(tmp_path, rank=16, std=0.2):
     """A VideoPainterID-style adapter file (PEFT keys on to_q/to_k/to_v/to_out.0 of every block), its factors."""
     from safetensors.torch import save_file
     tsd, _ = tiny_weights()
@@ -571,8 +571,8 @@ def _lora_case(tmp_path, rank=16):
     for b in range(TINY_CFG["num_layers"]):
         for t in ("to_q", "to_k", "to_v", "to_out.0"):
             w = tsd[f"transformer_blocks.{b}.attn1.{t}.weight"]
-            sd[f"transformer.transformer_blocks.{b}.attn1.{t}.lora_A.weight"] = torch.randn(rank, w.shape[1], generator=gen) * 0.05
-            sd[f"transformer.transformer_blocks.{b}.attn1.{t}.lora_B.weight"] = torch.randn(w.shape[0], rank, generator=gen) * 0.05
+            sd[f"transformer.transformer_blocks.{b}.attn1.{t}.lora_A.weight"] = torch.randn(rank, w.shape[1], generator=gen) * std
+            sd[f"transformer.transformer_blocks.{b}.attn1.{t}.lora_B.weight"] = torch.randn(w.shape[0], rank, generator=gen) * std
     save_file(sd, os.path.join(tmp_path, "pytorch_lora_weights.safetensors"))
     return tsd, sd
 
@@ -616,7 +616,7 @@ def test_lora_unfused_model_matches_oracle(env, tmp_path):
     no = O.transformer_forward(base, env["tcfg"], i["hidden"], i["enc"], i["timestep"], i["rope"],
                                branch_block_samples=bs, branch_block_masks=i["mask"])[0]
     print(f"unfused LoRA: HIP {rel(out, ref):.3e}, oracle bf16 {rel(o16, ref):.3e}, adapter effect {rel(no, ref):.3e}")
-    assert rel(no, ref) > 10 * bound(o16, ref)  # the adapter moves the output far more than the gate
+    assert rel(no, ref) > 3 * bound(o16, ref)  # the adapter moves the output well past the gate
     assert rel(out, ref) <= bound(o16, ref), (rel(out, ref), rel(o16, ref))
 
 
