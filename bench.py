@@ -238,10 +238,11 @@ def cpu_full_step(dtype=torch.bfloat16) -> dict:
                     "weights, + CFG + DPM step + replace-gt; after a warm-up block"}
 
 
-def build_models(device, seed: int, rank: int, world: int, bcast: str = "scatter_allgather"):
+def build_models(device, seed: int, rank: int, world: int, bcast: str = "scatter_allgather", always: bool = False):
     """Random-init 5b-I2V transformer + 2-layer branch; for N>1 initialised on rank 0 and broadcast over RCCL.
     Returns (transformer, branch, replication record or None): {"seconds": the chosen method's time (float),
-    "method", "per_method": {method: seconds}, "verified_buckets": {method: count}}."""
+    "method", "per_method": {method: seconds}, "verified_buckets": {method: count}}.  always: replicate and verify
+    at world size 1 too (--rccl-world1: the RCCL path on one GPU, identities there)."""
     from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, device_scope
     from videopainter_amd.config import COGVIDEOX_5B_I2V
     # config 5 (720x1280): random-init 5b-shaped model whose learned positional embedding is sized for the latent
@@ -254,7 +255,7 @@ def build_models(device, seed: int, rank: int, world: int, bcast: str = "scatter
         tr.init_synthetic_weights_(seed)
         br.init_synthetic_weights_(seed + 1)
     t_b = None
-    if world > 1:
+    if world > 1 or always:
         # replicate with the chosen method (timed), check every rank's bytes against rank 0's (per-bucket digests:
         # the first hardware run of the RCCL-only code paths validates itself), then time the other method too
         from videopainter_amd.distributed import barrier, broadcast_module, verify_replicas
@@ -264,11 +265,11 @@ def build_models(device, seed: int, rank: int, world: int, bcast: str = "scatter
             barrier(device)
             t0 = time.perf_counter()
             for m in (tr, br):
-                broadcast_module(m, src=0, method=method)
+                broadcast_module(m, src=0, method=method, always=always)
             torch.cuda.synchronize()
             barrier(device)
             t_b["per_method"][method] = time.perf_counter() - t0
-            checks = [verify_replicas(m) for m in (tr, br)]
+            checks = [verify_replicas(m, always=always) for m in (tr, br)]
             if not all(ok for ok, _ in checks):
                 raise RuntimeError(f"weight replication ({method}) left ranks with different weights")
             t_b["verified_buckets"][method] = sum(n for _, n in checks)
@@ -508,6 +509,9 @@ def main():
                          "as a window-stage pipeline (point-to-point hand-offs; = --config 4)")
     ap.add_argument("--bcast", default="scatter_allgather", choices=("scatter_allgather", "broadcast"),
                     help="weight replication for N > 1 (distributed.broadcast_module)")
+    ap.add_argument("--rccl-world1", action="store_true",
+                    help="at N=1: initialise torch.distributed on RCCL anyway and run the weight replication + replica "
+                         "check through it (identities at world size 1; the untimed setup, not the steps)")
     ap.add_argument("--lora-rank", type=int, default=0,
                     help="> 0: a synthetic VideoPainterID-style adapter of this rank on every transformer block's "
                          "to_q / to_k / to_v / to_out.0, loaded as the reference loads it (unfused, PEFT's forward)")
@@ -541,7 +545,7 @@ def main():
     device = torch.device("cuda", local)
     dist = None
     pair = None
-    if world > 1:
+    if world > 1 or args.rccl_world1:
         import torch.distributed as dist
         from videopainter_amd.distributed import init as dist_init
         dist_init(backend, device)
@@ -556,7 +560,7 @@ def main():
     from videopainter_amd.scheduler import CogVideoXDPMScheduler
 
     t_setup = time.time()
-    tr, br, t_bcast = build_models(device, 1234, rank, world, args.bcast)
+    tr, br, t_bcast = build_models(device, 1234, rank, world, args.bcast, args.rccl_world1)
     if args.lora_rank > 0:
         from videopainter_amd.lora import attach_lora_
         gl = torch.Generator(device=device).manual_seed(91)

@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 14
+#define VP_ABI_VERSION 15
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
@@ -267,9 +267,10 @@ int vp_mx_mfma_probe32(const void* A, const void* B, const void* sa, const void*
  * AdaLN-Zero modulate — CogVideoXLayerNormZero.forward (DF/models/normalization.py:373-379):
  * y = rnd(rnd(rnd(LN(x)) * rnd(1 + scale)) + shift) over rows of x [B, Ntok, D] (contiguous).  mod is the bf16
  * output of the block's norm linear, [B, 6D] = shift | scale | gate | enc_shift | enc_scale | enc_gate at batch
- * stride mod_bstride; text rows (token < text_len) use the enc_* chunks.  LN affine (ln_w, ln_b), eps.
+ * stride mod_bstride; text rows (token < text_len) use the enc_* chunks.  LN affine (ln_w, ln_b), eps.  y rows at
+ * stride ldy (>= D, % 8 == 0: e.g. the first D columns of an unfused-LoRA projection's K-augmented operand; ABI 15).
  * ------------------------------------------------------------------------------------------------------------- */
-int vp_adaln_modulate_bf16(const void* x, void* y, int32_t B, int32_t Ntok, int32_t D, int32_t text_len,
+int vp_adaln_modulate_bf16(const void* x, void* y, int64_t ldy, int32_t B, int32_t Ntok, int32_t D, int32_t text_len,
                            const void* ln_w, const void* ln_b, float eps, const void* mod, int64_t mod_bstride,
                            void* stream);
 /* the same, writing the modulated rows as MX-FP8 (q: e4m3 [B*Ntok][D], scales: MX layout with R = B*Ntok, K = D)

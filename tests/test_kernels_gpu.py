@@ -414,6 +414,11 @@ def test_adaln_and_final_norm():
     ref[:, T:] = n[:, T:] * (1 + m[:, None, D:2 * D]) + m[:, None, 0:D]
     ref[:, :T] = n[:, :T] * (1 + m[:, None, 4 * D:5 * D]) + m[:, None, 3 * D:4 * D]
     assert rel(y, ref) < 8e-3
+    # rows at a wider stride (the first D columns of an unfused-LoRA x_aug buffer): the same bits, the rest untouched
+    buf = torch.full((B * (T + Nv), D + 192), 7.0, device=dev, dtype=torch.bfloat16)
+    ys = K.adaln_modulate(x.to(dev), lw.to(dev), lb.to(dev), mod.to(dev), T, 1e-5,
+                          out=buf[:, :D].view(B, T + Nv, D))
+    assert torch.equal(ys, y) and bool((buf[:, D:] == 7.0).all())
     mod2 = bf(rnd(B, 2 * D, seed=74) * 0.5)
     lw2, lb2 = bf(1 + 0.1 * rnd(D, seed=75)), bf(0.1 * rnd(D, seed=76))
     z = K.final_norm(x.to(dev), T, lw.to(dev), lb.to(dev), lw2.to(dev), lb2.to(dev), 1e-5, mod2.to(dev))

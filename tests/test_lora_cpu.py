@@ -288,3 +288,32 @@ def test_augmented_operands_with_the_per_segment_tail():
         want = x @ l.weight.float().t() + 0.5 * (x @ l.lora_A.weight.float().t()) @ l.lora_B.weight.float().t()
         assert torch.allclose(xa @ w.float().t(), want, rtol=2e-2, atol=2e-2)
     assert AugmentedProjection.of((a.to_k, a.to_v)).weights()[0] is aug.weights()[1]
+
+
+def test_augmented_rows_are_written_in_place():
+    """lora.augmented_rows: with unfused adapters the producer's [B, N, K] output is the first K columns of the
+    x_aug buffer, and AugmentedProjection.input finds that buffer (no copy of x); any other tensor — a plain one, a
+    foreign [M, K + R] buffer, a buffer that was freed — takes the copying path."""
+    import gc
+    from videopainter_amd import CogVideoXTransformer3DModel
+    from videopainter_amd.lora import AugmentedProjection, _AUG_BUFFERS, _augmented_base, augmented_rows
+    tr = CogVideoXTransformer3DModel(**TINY_CFG)
+    tr.init_synthetic_weights_(4)
+    a = tr.transformer_blocks[0].attn1
+    lins = (a.to_q, a.to_k, a.to_v)
+    D = a.to_q.weight.shape[1]
+    plain = augmented_rows(lins, 2, 3, D, "cpu")
+    assert plain._base is None and plain.shape == (2, 3, D)  # no adapters: a plain tensor
+    tr.add_adapter({"r": 8, "lora_alpha": 8})
+    aug = AugmentedProjection.of(lins)
+    xv = augmented_rows(lins, 2, 3, D, "cpu")
+    assert xv.shape == (2, 3, D) and xv.stride() == (3 * (D + aug.R), D + aug.R, 1)
+    base = _augmented_base(xv.view(6, D), 6, D + aug.R)
+    assert base is not None and base.shape == (6, D + aug.R) and base.data_ptr() == xv.data_ptr()
+    foreign = torch.empty(6, D + aug.R)
+    assert _augmented_base(foreign[:, :D], 6, D + aug.R) is None
+    assert _augmented_base(xv.view(6, D), 6, D + aug.R + 64) is None  # another projection group's width
+    n = len(_AUG_BUFFERS)
+    del xv, base
+    gc.collect()
+    assert len(_AUG_BUFFERS) == n - 1  # the registry forgets freed buffers

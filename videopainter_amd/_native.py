@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -112,7 +112,7 @@ _SIGS = {
     "vp_v_pack_fp8": (i32, [vp, i64, i64, i32, i32, i32, vp, vp, vp]),
     "vp_mx_mfma_probe32": (i32, [vp, vp, vp, vp, vp, vp]),
     "vp_head_norm_rope_fp8": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp, vp, f32, vp]),
-    "vp_adaln_modulate_bf16": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, f32, vp, i64, vp]),
+    "vp_adaln_modulate_bf16": (i32, [vp, vp, i64, i32, i32, i32, i32, vp, vp, f32, vp, i64, vp]),
     "vp_head_norm_rope_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, i64,
                                      f32, vp, vp]),
     "vp_mask_scale_rows_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, vp, i64, f32, vp, vp]),

@@ -21,7 +21,7 @@ import torch.nn as nn
 
 from . import _native as NAT
 from . import kernels as K
-from .lora import AugmentedProjection
+from .lora import AugmentedProjection, augmented_rows
 from .modules import Dropout, LayerNorm, Linear
 
 BF16 = torch.bfloat16
@@ -92,6 +92,13 @@ class Attention(nn.Module):
         kw = {k: v for k, v in cross_attention_kwargs.items() if k in params}
         return self.processor(self, hidden_states, encoder_hidden_states=encoder_hidden_states,
                               attention_mask=attention_mask, **kw)
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """bf16 [B, N, D] rows with a contiguous last dim, at any row stride (the first columns of an x_aug buffer,
+    lora.augmented_rows, stay in place)."""
+    t = t.to(BF16)
+    return t if t.stride(-1) == 1 else t.contiguous()
 
 
 def _qkv(attn, x: torch.Tensor, norm_rope=None) -> torch.Tensor:
@@ -185,9 +192,9 @@ class CogVideoXAttnProcessor2_0:
         if not fused:
             K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, attn.norm_q.eps, rope)
             K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, eps_k, rope)
-        o = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
+        o = augmented_rows((attn.to_out[0],), B, Ntok, D, x.device)
         if prev_hidden_states is not None and prev_clip_weight is not None and prev_clip_weight > 0.0:
-            pkv = _kv(attn, prev_hidden_states.to(BF16).contiguous())
+            pkv = _kv(attn, _rows(prev_hidden_states))
             pk, pv = pkv[..., :D], pkv[..., D:]
             K.head_norm_rope(pk, pk, H, text_len, attn.norm_k.weight, attn.norm_k.bias, eps_k, rope)
             w = float(prev_clip_weight)
@@ -211,9 +218,9 @@ class CogVideoXAttnProcessor2_0:
         k8 = K.head_norm_rope_fp8(k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope,
                                   2.0 ** k_exp)
         vp = K.v_pack_fp8(v, H)
-        o = torch.empty(B, Ntok, D, device=q.device, dtype=BF16)
+        o = augmented_rows((attn.to_out[0],), B, Ntok, D, q.device)
         if prev_hidden_states is not None and prev_clip_weight is not None and prev_clip_weight > 0.0:
-            pkv = _kv(attn, prev_hidden_states.to(BF16).contiguous())
+            pkv = _kv(attn, _rows(prev_hidden_states))
             pk8 = K.head_norm_rope_fp8(pkv[..., :D], H, text_len, attn.norm_k.weight, attn.norm_k.bias,
                                        attn.norm_k.eps, rope, 2.0 ** k_exp)
             pvp = K.v_pack_fp8(pkv[..., D:], H)
@@ -335,7 +342,7 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
             k2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
             v2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
         if prev:
-            pkv = _kv(attn, prev_hidden_states.to(BF16).contiguous())
+            pkv = _kv(attn, _rows(prev_hidden_states))
             w = float(prev_clip_weight)
             K.head_norm_rope(pkv[..., :D], k2, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps,
                              rope, tok_mask=m, pre_scale=w, dst_rows=dst)
@@ -350,7 +357,7 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
         if not fused:
             K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, attn.norm_q.eps, rope)
             K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope)
-        o = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
+        o = augmented_rows((attn.to_out[0],), B, Ntok, D, x.device)
         if axes is not None:
             lx = K.null_key_mass(q, H, text_len, grid, attn.norm_k.bias, axes, m, segments, attn.scale)
             K.attention(q, k, v, o, H, k2=k2, v2=v2, scale=attn.scale, bounded_scores=bounded_scores(attn),

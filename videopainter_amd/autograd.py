@@ -42,7 +42,7 @@ from . import _native as NAT
 from . import kernels as K
 from .attention_processor import bounded_scores
 from .attention_processor import project_out
-from .lora import AugmentedProjection
+from .lora import AugmentedProjection, augmented_rows
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -218,9 +218,11 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     # to the separate launches used here, tests/test_model_gpu.py) ----
     mod1 = n1.modulation(temb)
     mod2 = n2.modulation(temb)
-    xn = K.adaln_modulate(x, n1.norm.weight, n1.norm.bias, mod1, T, n1.norm.eps)
+    # trainable LoRA factors run unfused: the projections on K-augmented operands (lora.AugmentedProjection),
+    # which AdaLN and the attention write in place (lora.augmented_rows)
+    xn = K.adaln_modulate(x, n1.norm.weight, n1.norm.bias, mod1, T, n1.norm.eps,
+                          out=augmented_rows((a.to_q, a.to_k, a.to_v), B, Ntok, D, dev))
     qkv = torch.empty(B, Ntok, 3 * D, device=dev, dtype=BF16)
-    # trainable LoRA factors run unfused: the projections on K-augmented operands (lora.AugmentedProjection)
     qaug = AugmentedProjection.of((a.to_q, a.to_k, a.to_v))
     oaug = AugmentedProjection.of((to_out,))
     xq = xn.view(M, D) if qaug is None else qaug.input(xn.view(M, D))
@@ -249,7 +251,7 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
         katt, vatt = kn, v
     K.head_norm_rope(qkv[..., :D], qn, H, T, a.norm_q.weight, a.norm_q.bias, a.norm_q.eps, rope)
     K.head_norm_rope(qkv[..., D:2 * D], kn, H, T, a.norm_k.weight, a.norm_k.bias, a.norm_k.eps, rope)
-    o = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
+    o = augmented_rows((to_out,), B, Ntok, D, dev)
     lse = torch.empty(B, H, Ntok, device=dev, dtype=F32)
     K.attention(qn, katt, vatt, o, H, scale=a.scale, bounded_scores=bounded_scores(a), lse=lse)
     x_mid = torch.empty_like(x)

@@ -51,7 +51,7 @@ VP_DEV void row_stats(const RowRegs& r, int nch, int lane, int D, float& mean, f
 template <bool MX, int NCH>
 VP_DEV void adaln_row(bf16x8 (&xr)[NCH], int row, int lane, int Ntok, int D, int text_len, const bf16* __restrict__ lw,
                       const bf16* __restrict__ lb, float eps, const bf16* __restrict__ mod, int64_t mod_bs,
-                      void* __restrict__ y, uint8_t* __restrict__ yscale) {
+                      void* __restrict__ y, uint8_t* __restrict__ yscale, int64_t ldy) {
   const int b = row / Ntok;
   const int tok = row - b * Ntok;
   const int nch = D / 8;
@@ -104,7 +104,7 @@ VP_DEV void adaln_row(bf16x8 (&xr)[NCH], int row, int lane, int Ntok, int D, int
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = f2bf(f[e]);
-        *(bf16x8*)((bf16*)y + (int64_t)row * D + c * 8) = o;
+        *(bf16x8*)((bf16*)y + (int64_t)row * ldy + c * 8) = o;
       }
     }
     // one chunk's parameter loads live at a time (hoisting all 4 x NCH of them costs 96 VGPRs and half the
@@ -137,22 +137,24 @@ __global__ __launch_bounds__(ROW_THREADS) void adaln_modulate_kernel(const bf16*
                                                                         int rows, int Ntok, int D, int text_len,
                                                                         const bf16* __restrict__ lw,
                                                                         const bf16* __restrict__ lb, float eps,
-                                                                        const bf16* __restrict__ mod, int64_t mod_bs) {
+                                                                        const bf16* __restrict__ mod, int64_t mod_bs,
+                                                                        int64_t ldy) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
   if (row >= rows) return;
   bf16x8 xr[NCH];
   load_row_bf16<NCH>(xr, x + (int64_t)row * D, lane, D / 8);
-  adaln_row<MX, NCH>(xr, row, lane, Ntok, D, text_len, lw, lb, eps, mod, mod_bs, y, yscale);
+  adaln_row<MX, NCH>(xr, row, lane, Ntok, D, text_len, lw, lb, eps, mod, mod_bs, y, yscale, ldy);
 }
 
 template <bool MX>
 void launch_adaln(int rows, hipStream_t s, const bf16* x, void* y, uint8_t* ys, int Ntok, int D,
-                  int text_len, const bf16* lw, const bf16* lb, float eps, const bf16* mod, int64_t mod_bs) {
+                  int text_len, const bf16* lw, const bf16* lb, float eps, const bf16* mod, int64_t mod_bs,
+                  int64_t ldy) {
   const int nch = (D / 8 + 63) / 64;  // 16-byte chunks per lane
   const int grid = (rows + 3) / 4;
 #define VP_ADALN(N) hipLaunchKernelGGL((adaln_modulate_kernel<MX, N>), dim3(grid), dim3(ROW_THREADS), 0, s, x, y, ys, \
-                                       rows, Ntok, D, text_len, lw, lb, eps, mod, mod_bs)
+                                       rows, Ntok, D, text_len, lw, lb, eps, mod, mod_bs, ldy)
   if (nch <= 1) VP_ADALN(1);
   else if (nch <= 2) VP_ADALN(2);
   else if (nch <= 4) VP_ADALN(4);
@@ -344,15 +346,15 @@ __global__ __launch_bounds__(1024) void partition_index_kernel(const uint8_t* __
 
 }  // namespace
 
-extern "C" int vp_adaln_modulate_bf16(const void* x, void* y, int32_t B, int32_t Ntok, int32_t D, int32_t text_len,
-                                      const void* ln_w, const void* ln_b, float eps, const void* mod,
-                                      int64_t mod_bstride, void* stream) {
+extern "C" int vp_adaln_modulate_bf16(const void* x, void* y, int64_t ldy, int32_t B, int32_t Ntok, int32_t D,
+                                      int32_t text_len, const void* ln_w, const void* ln_b, float eps,
+                                      const void* mod, int64_t mod_bstride, void* stream) {
   if (!x || !y || !ln_w || !ln_b || !mod || B <= 0 || Ntok <= 0 || D <= 0 || (D % 8) || D > MAXC * 512)
     return VP_ERR_ARG;
-  if (mod_bstride % 8) return VP_ERR_ARG;
+  if ((mod_bstride % 8) || ldy < D || (ldy % 8)) return VP_ERR_ARG;
   const int rows = B * Ntok;
   launch_adaln<false>(rows, (hipStream_t)stream, (const bf16*)x, y, nullptr, Ntok, D, text_len,
-                      (const bf16*)ln_w, (const bf16*)ln_b, eps, (const bf16*)mod, mod_bstride);
+                      (const bf16*)ln_w, (const bf16*)ln_b, eps, (const bf16*)mod, mod_bstride, ldy);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
@@ -365,7 +367,7 @@ extern "C" int vp_adaln_modulate_mx_fp8(const void* x, void* q, void* scales, in
   if (mod_bstride % 8) return VP_ERR_ARG;
   const int rows = B * Ntok;
   launch_adaln<true>(rows, (hipStream_t)stream, (const bf16*)x, q, (uint8_t*)scales, Ntok, D, text_len,
-                     (const bf16*)ln_w, (const bf16*)ln_b, eps, (const bf16*)mod, mod_bstride);
+                     (const bf16*)ln_w, (const bf16*)ln_b, eps, (const bf16*)mod, mod_bstride, D);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }

@@ -91,19 +91,21 @@ def _recv(t: torch.Tensor, src: int) -> None:
 
 @torch.no_grad()
 def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0, bucket_bytes: int = BUCKET_BYTES,
-                      method: str = "scatter_allgather") -> None:
+                      method: str = "scatter_allgather", always: bool = False) -> None:
     """Replicate tensors from `src` in flat buckets (one exchange per <= bucket_bytes of same-dtype tensors).
 
     method "broadcast": one RCCL broadcast per bucket (a pipelined ring: every byte crosses every hop, so a bucket
     costs ~bytes / one link's bandwidth).  method "scatter_allgather" (default): the bucket is split into world
     shards; the source sends shard r straight to rank r (point-to-point, all of the source's xGMI links at once) and
     an all-gather then circulates the shards (each rank forwards (world-1)/world of the bucket) — on a fully
-    connected 8-GPU node the source no longer serialises the whole payload through one link.  Both are exact copies."""
+    connected 8-GPU node the source no longer serialises the whole payload through one link.  Both are exact copies.
+    always: run the collectives at world size 1 too (they are identities there; the RCCL path on one GPU, tests/
+    test_distributed_gpu.py and bench.py --rccl-world1)."""
     ts = [t for t in tensors if t.numel() > 0]
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     for b in _buckets(ts, bucket_bytes):
-        if world == 1:
+        if world == 1 and not always:
             continue
         if method == "broadcast" and len(b) == 1:
             with _staged(b[0]) as t:
@@ -132,7 +134,7 @@ def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0, bucket_byte
                     shard.copy_(work[src * per:(src + 1) * per])
                 else:
                     ops.append(dist.P2POp(dist.irecv, shard, src))
-                for req in dist.batch_isend_irecv(ops):
+                for req in (dist.batch_isend_irecv(ops) if ops else []):
                     req.wait()
                 dist.all_gather_into_tensor(work, shard)
             else:
@@ -145,9 +147,10 @@ def broadcast_tensors(tensors: Iterable[torch.Tensor], src: int = 0, bucket_byte
 
 
 def broadcast_module(module: torch.nn.Module, src: int = 0, bucket_bytes: int = BUCKET_BYTES,
-                     method: str = "scatter_allgather") -> None:
+                     method: str = "scatter_allgather", always: bool = False) -> None:
     """Replicate a model's parameters and buffers from rank `src` (config 3: weights over RCCL/xGMI)."""
-    broadcast_tensors(list(module.state_dict().values()), src=src, bucket_bytes=bucket_bytes, method=method)
+    broadcast_tensors(list(module.state_dict().values()), src=src, bucket_bytes=bucket_bytes, method=method,
+                      always=always)
 
 
 @torch.no_grad()
@@ -177,12 +180,13 @@ def bucket_digests(tensors: Iterable[torch.Tensor], bucket_bytes: int = BUCKET_B
 
 
 @torch.no_grad()
-def verify_replicas(module: torch.nn.Module, bucket_bytes: int = BUCKET_BYTES, group=None):
+def verify_replicas(module: torch.nn.Module, bucket_bytes: int = BUCKET_BYTES, group=None, always: bool = False):
     """After broadcast_module: does every rank hold rank 0's bytes?  Each rank digests its buckets
     (bucket_digests, on the device), one all-reduce of MIN and one of MAX compare them across ranks (the same calls
-    on RCCL and gloo).  Returns (identical on every rank, number of buckets); collective: every rank must call it."""
+    on RCCL and gloo).  Returns (identical on every rank, number of buckets); collective: every rank must call it.
+    always: all-reduce at world size 1 too (as broadcast_tensors)."""
     d = bucket_digests(list(module.state_dict().values()), bucket_bytes)
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_initialized() or (dist.get_world_size(group) == 1 and not always):
         return True, int(d.shape[0])
     lo, hi = d.clone(), d.clone()
     with _staged(lo, group) as a:
@@ -223,7 +227,8 @@ def _pair_groups(world: int, size: int):
 
 class CFGPair:
     """Ranks (2p, 2p+1) share one clip: cfg_index 0 runs the unconditional half of the CFG batch, 1 the text half
-    (the order of `torch.cat([negative_prompt_embeds, prompt_embeds])`, anyl.py:805-806)."""
+    (the order of `torch.cat([negative_prompt_embeds, prompt_embeds])`, anyl.py:805-806).  An explicit `group` may
+    have any size (a one-rank group: the all-gather on one GPU, tests/test_distributed_gpu.py)."""
 
     def __init__(self, group=None, cfg_index: Optional[int] = None):
         rank, world = dist.get_rank(), dist.get_world_size()
@@ -236,11 +241,12 @@ class CFGPair:
         self.backend = dist.get_backend(group)
 
     def allgather(self, half: torch.Tensor) -> torch.Tensor:
-        """[1, ...] on each rank of the pair -> [2, ...] = (uncond, text) on both."""
+        """[1, ...] on each rank of the pair -> [2, ...] = (uncond, text) on both ([group size, ...] in general)."""
         if half.shape[0] != 1:
             raise ValueError("each CFG rank holds a batch of 1")
         half = half.contiguous()
-        out = torch.empty((2,) + tuple(half.shape[1:]), dtype=half.dtype, device=half.device)
+        out = torch.empty((dist.get_world_size(self.group),) + tuple(half.shape[1:]), dtype=half.dtype,
+                          device=half.device)
         _all_gather_rows(out, half, self.group)
         return out
 

@@ -585,8 +585,13 @@ def adaln_modulate(x: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, mod:
         raise ValueError("x must be contiguous [B, N, D]")
     B, Ntok, D = x.shape
     out = torch.empty_like(x) if out is None else out
-    N.check(N.lib().vp_adaln_modulate_bf16(_p(x), _p(out), B, Ntok, D, text_len, _p(ln_w), _p(ln_b), eps, _p(mod),
-                                           mod.stride(0), _stream()), "vp_adaln_modulate_bf16")
+    _chk(out, "out")
+    ldy = out.stride(-2)  # [B, Ntok, D] rows (or [B*Ntok, D]) at any row stride, rows packed across the batch
+    if (out.shape[-1] != D or out.stride(-1) != 1 or out.numel() != B * Ntok * D
+            or (out.dim() == 3 and out.stride(0) != Ntok * ldy)):
+        raise ValueError("adaln out must be [B, N, D] / [B*N, D] rows with a contiguous last dim")
+    N.check(N.lib().vp_adaln_modulate_bf16(_p(x), _p(out), ldy, B, Ntok, D, text_len, _p(ln_w), _p(ln_b), eps,
+                                           _p(mod), mod.stride(0), _stream()), "vp_adaln_modulate_bf16")
     return out
 
 

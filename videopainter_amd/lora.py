@@ -36,6 +36,7 @@ from __future__ import annotations
 import math
 import os
 import re
+import weakref
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -46,6 +47,7 @@ _KOHYA = re.compile(r"^(?:(?P<prefix>transformer)\.)?(?P<mod>.+)\.lora_(?P<ab>do
 # the Linears the augmented GEMMs cover: the attention projections of every block (transformer and branch)
 _COVERED = re.compile(r"(^|\.)attn1\.(to_q|to_k|to_v|to_out\.0)$")
 AUG_ALIGN = 64  # the per-projection tail width is padded to whole 64-wide K-tiles of the GEMM (zero columns / rows)
+_AUG_BUFFERS: Dict[int, "weakref.ref"] = {}  # id -> weakref of the live x_aug buffers from augmented_rows()
 
 
 def covered(module_name: str) -> bool:
@@ -477,9 +479,12 @@ class AugmentedProjection:
 
     def input(self, x2d: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """x_aug [M, K + R] = [x | x A_cat^T] (one GEMM for T).  `out`: a buffer whose first K columns already
-        hold x (the producer wrote them in place: no copy)."""
+        hold x (the producer wrote them in place: no copy); x2d itself when it is the first K columns of a buffer
+        from augmented_rows() for these projections."""
         from . import kernels as K
         M = x2d.shape[0]
+        if out is None:
+            out = _augmented_base(x2d, M, self.K + self.R)
         if out is None:
             out = torch.empty(M, self.K + self.R, device=x2d.device, dtype=torch.bfloat16)
             out[:, :self.K].copy_(x2d)
@@ -492,3 +497,27 @@ class AugmentedProjection:
         if self.tail is None:  # block-diagonal form, or one projection: x_aug's first K + width columns
             return K.gemm(x_aug, self.weights(), biases, out2d, **kw)
         return K.gemm(x_aug, self.weights(), biases, out2d, a_tail=self.tail, **kw)
+
+
+def _augmented_base(x2d: torch.Tensor, M: int, width: int) -> Optional[torch.Tensor]:
+    """The augmented_rows() buffer whose first columns x2d is, when it is one of width `width`."""
+    base = x2d._base
+    ref = _AUG_BUFFERS.get(id(base)) if base is not None else None
+    if (ref is None or ref() is not base or tuple(base.shape) != (M, width)
+            or x2d.data_ptr() != base.data_ptr() or x2d.stride() != (width, 1)):
+        return None
+    return base
+
+
+def augmented_rows(lins, B: int, Ntok: int, K: int, device) -> torch.Tensor:
+    """A bf16 [B, Ntok, K] tensor for the input of the projections `lins`: when they carry unfused adapters, the
+    first K columns of a fresh x_aug buffer [B*Ntok, K + R] (the producer — AdaLN, attention — writes x in place and
+    AugmentedProjection.input only adds T: no copy of x), else a plain tensor."""
+    aug = AugmentedProjection.of(lins)
+    if aug is None or aug.K != K:
+        return torch.empty(B, Ntok, K, device=device, dtype=torch.bfloat16)
+    buf = torch.empty(B * Ntok, K + aug.R, device=device, dtype=torch.bfloat16)
+    key = id(buf)
+    _AUG_BUFFERS[key] = weakref.ref(buf, lambda _r, k=key: _AUG_BUFFERS.pop(k, None) if _AUG_BUFFERS.get(k) is _r
+                                    else None)
+    return buf[:, :K].view(B, Ntok, K)

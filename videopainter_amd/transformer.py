@@ -29,6 +29,7 @@ from .attention_processor import (Attention, CogVideoXAttnProcessor2_0, CogVideo
                                   CogVideoXAttnProcessor2_0_wo_text,
                                   _rope_dev, _u8, project_out)
 from .embeddings import joint_sincos_pos_embedding
+from .lora import augmented_rows
 from .modules import Conv2dPatch, Dropout, LayerNorm, Linear, ModelMixin, _empty
 
 BF16 = torch.bfloat16
@@ -275,13 +276,18 @@ class CogVideoXBlock(nn.Module):
             del xq
             xn = None
         else:
+            a = self.attn1  # (unfused LoRA: AdaLN writes straight into the projection's K-augmented operand)
             xn = K.adaln_modulate(x, self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len,
-                                  self.norm1.norm.eps)
+                                  self.norm1.norm.eps,
+                                  out=None if attend is not None else
+                                  augmented_rows((a.to_q, a.to_k, a.to_v), B, Ntok, D, x.device))
         pn = None
         if prev_joint is not None:
             # the block normalises the previous window's states with its own norm1 (reference :141-146)
+            a = self.attn1
+            pout = augmented_rows((a.to_k, a.to_v), prev_joint.shape[0], prev_joint.shape[1], D, x.device)
             pn = K.adaln_modulate(_bf(prev_joint), self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len,
-                                  self.norm1.norm.eps)
+                                  self.norm1.norm.eps, out=pout)
         if attend is not None:
             o = attend(self.attn1, xn, text_len, rope)
         else:
