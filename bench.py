@@ -546,6 +546,14 @@ def main():
     dist = None
     pair = None
     if world > 1 or args.rccl_world1:
+        if world == 1:  # a one-rank job started without a launcher: its own env:// rendezvous on the loopback
+            import socket
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", str(port)), ("RANK", "0"),
+                         ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0")):
+                os.environ.setdefault(k, v)
         import torch.distributed as dist
         from videopainter_amd.distributed import init as dist_init
         dist_init(backend, device)
