@@ -1,5 +1,5 @@
 #!/bin/bash
-# The one GPU-session launcher (replaces the per-experiment tools/gpu_r0X_*.sh scripts of rounds 1-4):
+# The one GPU-session launcher (the only one: the per-experiment launchers of rounds 1-4 are folded into it):
 #
 #   gpurun -- bash tools/gpu.sh TAG 'name[@timeout]=command' ['name[@timeout]=command' ...]
 #

@@ -24,7 +24,7 @@ ARCH = "gfx950"
 # canonicalising v_max before every fmaxf of an MFMA result (cdna_hip_programming.md, attention pitfalls)
 # attention: -fno-slp-vectorize keeps the softmax row sums as single f32 adds — the SLP pass packs them into
 # v_pk_add_f32, which costs more issue cycles beside MFMAs (MI355X_MICROARCH.md cycle constants): measured
-# 1.07 -> 1.13 PF/s at config 2 (tools/ab_run.sh).  The GEMM keeps SLP (no gain there: the epilogue is not under MFMA).
+# 1.07 -> 1.13 PF/s at config 2 (an interleaved bench A/B, tools/gpu.sh).  The GEMM keeps SLP (no gain there: the epilogue is not under MFMA).
 # attention: -amdgpu-mfma-vgpr-form keeps the MFMA accumulators of the one-wave-per-SIMD kernel (p1, 512 registers
 # available) in arch VGPRs; by default the compiler picks the AGPR form there and shuttles every S tile through
 # v_accvgpr_read for the softmax (the other attention kernels compile to identical code with or without it).
