@@ -37,3 +37,29 @@ def test_attention_backward_matches_autograd(B, H, N, Nk):
         r = rel(got.float(), w)
         print(f"attention bwd B={B} H={H} N={N} Nk={Nk} {name}: rel {r:.3e}")
         assert r < 2e-2, name
+
+
+@pytest.mark.parametrize("B,H,N,Nk", [(1, 2, 300, 300), (1, 1, 65, 200), (2, 2, 1378, 1410), (1, 2, 4500, 4500),
+                                      (1, 1, 128, 96), (1, 1, 200, 64)])
+def test_attention_backward_variants_bit_identical(knobs, B, H, N, Nk):
+    """VP_ATTN_BWD_VARIANT 1 (default: conflict-free swizzle, peeled last key tile, no in-loop waits on the next
+    tile's DMA) against 0 (round 2's kernels): the same products in the same order, so the same bits — full tiles,
+    partial last tiles of 8 / 32 / 44 / 62 / 36 keys or queries, a key count below one tile."""
+    from videopainter_amd import kernels as K
+    torch.manual_seed(N * 7 + Nk)
+    dev = "cuda"
+    q = torch.randn(B, N, H * 64, device=dev).bfloat16()
+    k = torch.randn(B, Nk, H * 64, device=dev).bfloat16()
+    v = torch.randn(B, Nk, H * 64, device=dev).bfloat16()
+    o = torch.empty(B, N, H * 64, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=dev, dtype=torch.float32)
+    K.attention(q, k, v, o, H, lse=lse)
+    do = torch.randn(B, N, H * 64, device=dev).bfloat16()
+    got = {}
+    for var in ("0", "1"):
+        knobs.setenv("VP_ATTN_BWD_VARIANT", var)
+        got[var] = K.attention_bwd(q, k, v, o, do, lse, H)
+        torch.cuda.synchronize()
+    for var in ("1",):
+        for name, a, b in zip(("dq", "dk", "dv"), got["0"], got[var]):
+            assert torch.equal(a, b), (var, name)

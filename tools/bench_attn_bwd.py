@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--n", type=int, default=17776)
     ap.add_argument("--heads", type=int, default=48)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--variants", default="", help="comma-separated VP_ATTN_BWD_VARIANT values, timed interleaved")
     a = ap.parse_args()
     from videopainter_amd import kernels as K
     torch.manual_seed(0)
@@ -28,12 +29,25 @@ def main():
     for _ in range(2):
         K.attention_bwd(q, k, v, o, do, lse, H, dq=dq, dk=dk, dv=dv)
     torch.cuda.synchronize()
+    fl = 8.0 * B * H * N * N * 64  # dV, dP, dQ, dK (the S recompute not counted)
+    if a.variants:  # interleaved A/B of the library's backward variants, 3 rounds
+        res = {v: [] for v in a.variants.split(",")}
+        for _ in range(3):
+            for var in res:
+                K.set_knob("VP_ATTN_BWD_VARIANT", var)
+                K.attention_bwd(q, k, v, o, do, lse, H, dq=dq, dk=dk, dv=dv)
+                with K.timed_launches("attention_bwd") as tl:
+                    for _ in range(a.iters):
+                        K.attention_bwd(q, k, v, o, do, lse, H, dq=dq, dk=dk, dv=dv)
+                res[var].append(round(tl.mean_ms("attention_bwd"), 4))
+        K.set_knob("VP_ATTN_BWD_VARIANT", None)
+        print(json.dumps({"n": N, "heads": H, "bwd_ms_by_variant": res}))
+        return
     with K.timed_launches("attention_bwd", "attention") as tl:
         for _ in range(a.iters):
             K.attention(q, k, v, o, H, lse=lse)
             K.attention_bwd(q, k, v, o, do, lse, H, dq=dq, dk=dk, dv=dv)
     ms = tl.mean_ms("attention_bwd")
-    fl = 8.0 * B * H * N * N * 64  # dV, dP, dQ, dK (the S recompute not counted)
     print(json.dumps({"n": N, "heads": H, "bwd_ms": ms, "fwd_ms": tl.mean_ms("attention"),
                       "bwd_useful_tflops": fl / ms / 1e9, "fwd_tflops": 4.0 * B * H * N * N * 64 / tl.mean_ms("attention") / 1e9}))
 

@@ -13,6 +13,8 @@
 // product on v_mfma_f32_32x32x16_bf16; tiles stream through a 2-slot LDS ring by LDS-DMA (global_load_lds_dwordx4,
 // bank swizzle on the source address).  Roofline: MFMA (2.5 x the forward's 4 N^2 d FLOP per head: S twice, dP
 // twice, dQ, dK, dV), VALU exp2 per score twice.
+#include <stdlib.h>
+
 #include "vp_common.h"
 
 namespace {
@@ -26,7 +28,15 @@ constexpr int LDS_BWD = 2 * STAGE;
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-VP_DEV int swz(int row) { return (row >> 1) & 7; }
+// bank swizzle of a staged tile: 16-B chunk c of row r sits at chunk c ^ swz(r).  V = 0 (round 2): (r >> 1) & 7,
+// conflict-free for ds_read_b128 but 2-way for the transposing ds_read_b64_tr_b16 (rows 4m and 4m + 2 of one lane
+// group land on the same banks).  V = 1: the same bijection of (r >> 1) & 7 with its low bit moved to bit 2, so rows
+// 4m and 4m + 2 differ in chunk bit 2 — conflict-free for both reads (checked by enumerating the lane groups of
+// MI355X_MICROARCH.md's LDS table); bits 1-3 of r only, so every 16-row slab has the same pattern.
+template <int V>
+VP_DEV int swz(int row) {
+  return V ? (((row >> 2) & 3) | (((row >> 1) & 1) << 2)) : ((row >> 1) & 7);
+}
 
 VP_DEV void glds16(const char* sbase, int voff, char* lds) {
   const unsigned la = (unsigned)(uintptr_t)(lds_void_t*)lds;
@@ -36,23 +46,50 @@ VP_DEV void glds16(const char* sbase, int voff, char* lds) {
 
 // stage 64 rows of a [N, ld] bf16 head slice (64 columns from `base`) into a swizzled [64][128 B] LDS tile: 2 DMA
 // pieces of 8 rows per wave (rows past `nrows` re-read the last row; the caller masks them)
+template <int V>
 VP_DEV void stage_tile(const bf16* base, int64_t ld, int row0, int nrows, char* tile, int wave, int lane) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int pc = wave + i * BW;               // piece: tile rows pc*8 .. pc*8+7
     const int r = pc * 8 + (lane >> 3);
     const int rs = min(row0 + r, nrows - 1) - row0;
-    const int ch = (lane & 7) ^ swz(r);
+    const int ch = (lane & 7) ^ swz<V>(r);
     glds16((const char*)(base + (int64_t)row0 * ld), (int)((rs * ld + ch * 8) * 2), tile + pc * 1024);
   }
 }
 
+// V = 1: the two DMA source offsets of a full tile, computed once per kernel (kept VGPRs); only a partial last tile
+// recomputes them with the row clamp.  (Per-tile 64-bit offset math let the compiler pair a dead high half with an
+// unrelated register, whose pending load the loop then waited for before the DMA issue.)
+struct TileOffs {
+  int o[2];
+};
+VP_DEV TileOffs tile_offs(int64_t ld, int wave, int lane) {
+  TileOffs t;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (wave + i * BW) * 8 + (lane >> 3);
+    t.o[i] = (r * (int)ld + (((lane & 7) ^ swz<1>(r)) * 8)) * 2;
+  }
+  return t;
+}
+VP_DEV void stage_tile_fast(const bf16* base, int64_t ld, int row0, int nrows, char* tile, int wave, int lane,
+                            const TileOffs& to) {
+  if (row0 + BT <= nrows) {  // wave-uniform
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16((const char*)(base + (int64_t)row0 * ld), to.o[i], tile + (wave + i * BW) * 1024);
+  } else {
+    stage_tile<1>(base, ld, row0, nrows, tile, wave, lane);
+  }
+}
+
 // A-operand rows (ds_read_b128) of a 32-row half of a swizzled tile: chunk (2c + hl) ^ swz(row) = dims 16c + 8hl
+template <int V>
 VP_DEV void read_rows(const char* tile, int half, int lane, bf16x8 (&f)[4]) {
   const int hl = lane >> 5;
   const int row = half * 32 + (lane & 31);
   const char* rp = tile + row * 128;
-  const int sw = swz(row);
+  const int sw = swz<V>(row);
 #pragma unroll
   for (int c = 0; c < 4; ++c) f[c] = *(const bf16x8*)(rp + (((2 * c + hl) ^ sw) << 4));
 }
@@ -63,6 +100,7 @@ VP_DEV void read_rows(const char* tile, int half, int lane, bf16x8 (&f)[4]) {
 struct TrAddr {
   int lo[2], hi[2];
 };
+template <int V>
 VP_DEV TrAddr tr_addr(int lane) {
   const int g = lane >> 4;
   const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
@@ -71,8 +109,8 @@ VP_DEV TrAddr tr_addr(int lane) {
 #pragma unroll
   for (int dh = 0; dh < 2; ++dh) {
     const int chunk = dh * 4 + (tcol >> 3);
-    a.lo[dh] = trow * 128 + ((chunk ^ swz(trow)) << 4) + (tcol & 7) * 2;
-    a.hi[dh] = (trow + 8) * 128 + ((chunk ^ swz(trow + 8)) << 4) + (tcol & 7) * 2;
+    a.lo[dh] = trow * 128 + ((chunk ^ swz<V>(trow)) << 4) + (tcol & 7) * 2;
+    a.hi[dh] = (trow + 8) * 128 + ((chunk ^ swz<V>(trow + 8)) << 4) + (tcol & 7) * 2;
   }
   return a;
 }
@@ -135,9 +173,12 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const vp_attn_bwd_desc d
 }
 
 // ---- dQ: a workgroup per (b, h, 128 queries), 64-key tiles ----
+// V = 1 (default): conflict-free swizzle (swz<1>), the last partial key tile peeled out of the loop (the full-tile body
+// is straight-line code without the per-score mask), inactive waves skip the compute as one block.  V = 0: round 2.
 #ifndef VP_DQ_WAVES
 #define VP_DQ_WAVES 2  // waves per SIMD the dQ kernel is register-budgeted for (A/B: -DVP_DQ_WAVES=3)
 #endif
+template <int V>
 __global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_attn_bwd_desc d) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
@@ -166,66 +207,100 @@ __global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_a
   const f32x16 negl = splat16(-d.lse[so]), negd = splat16(-d.delta[so]);
   const bf16* kb = (const bf16*)d.K + (int64_t)b * d.k_sb + h * 64;
   const bf16* vb = (const bf16*)d.V + (int64_t)b * d.v_sb + h * 64;
-  const TrAddr ta = tr_addr(lane);
+  const TrAddr ta = tr_addr<V>(lane);
   f32x16 dqt[2] = {zero16(), zero16()};
   const bool active = qb * BW * 32 + wave * 32 < d.Nq;  // wave-uniform
   const int ntiles = (d.Nk + BT - 1) / BT;
+  const TileOffs ko = tile_offs(d.k_sn, wave, lane), vo = tile_offs(d.v_sn, wave, lane);
   auto issue = [&](int ti) {
     char* st = smem + (ti & 1) * STAGE;
-    stage_tile(kb, d.k_sn, ti * BT, d.Nk, st, wave, lane);
-    stage_tile(vb, d.v_sn, ti * BT, d.Nk, st + TILE, wave, lane);
+    if (V) {
+      stage_tile_fast(kb, d.k_sn, ti * BT, d.Nk, st, wave, lane, ko);
+      stage_tile_fast(vb, d.v_sn, ti * BT, d.Nk, st + TILE, wave, lane, vo);
+    } else {
+      stage_tile<V>(kb, d.k_sn, ti * BT, d.Nk, st, wave, lane);
+      stage_tile<V>(vb, d.v_sn, ti * BT, d.Nk, st + TILE, wave, lane);
+    }
+  };
+  // one 32-key half of a staged tile.  The accumulators start at -lse / -D (C-init), so P = exp2(S) and dS = P * dP
+  // come straight off the matrix pipe: one exp and one multiply per score; with `lim` < BT (last tile only) keys past
+  // Nk start at -inf instead
+  auto half = [&](const char* Kt, const char* Vt, int kh, bool masked, int lim) {
+    bf16x8 a[4];
+    read_rows<V>(Kt, kh, lane, a);
+    // first MFMA of each chain in asm with the loop-invariant C (dst != srcC: the -lse / -D registers are never
+    // copied)
+    f32x16 s, dp;
+    if (!masked) {
+      asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(s) : "v"(a[0]), "v"(qf[0]), "v"(negl));
+    } else {
+      f32x16 cm = negl;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (kh * 32 + acc_row(i, hl) >= lim) cm[i] = -INFINITY;
+      // (builtin here: the compiler places the VALU-write -> MFMA-srcC wait states, which it does not for asm)
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], qf[0], cm, 0, 0, 0);
+    }
+#pragma unroll
+    for (int ds = 1; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], qf[ds], s, 0, 0, 0);
+    read_rows<V>(Vt, kh, lane, a);
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(dp) : "v"(a[0]), "v"(gf[0]), "v"(negd));
+#pragma unroll
+    for (int ds = 1; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], gf[ds], dp, 0, 0, 0);
+    bf16x8 pf[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) pf[i >> 3][i & 7] = f2bf(__builtin_amdgcn_exp2f(s[i]) * dp[i]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh)
+        dqt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Kt, kh * 2 + j, ta, dh), pf[j], dqt[dh], 0, 0, 0);
   };
   issue(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int ti = 0; ti < ntiles; ++ti) {
-    if (ti + 1 < ntiles) issue(ti + 1);
-    const char* Kt = smem + (ti & 1) * STAGE;
-    const char* Vt = Kt + TILE;
-    const int lim = d.Nk - ti * BT;
-    // the accumulators start at -lse / -D (C-init), so P = exp2(S) and dS = P * dP come straight off the matrix
-    // pipe: one exp and one multiply per score; keys past Nk (last tile only) start at -inf instead
+  if (V == 0) {
+    for (int ti = 0; ti < ntiles; ++ti) {
+      if (ti + 1 < ntiles) issue(ti + 1);
+      const char* Kt = smem + (ti & 1) * STAGE;
+      const int lim = d.Nk - ti * BT;
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      if (!active) break;
-      bf16x8 a[4];
-      read_rows(Kt, kh, lane, a);
-      // first MFMA of each chain in asm with the loop-invariant C (dst != srcC: the -lse / -D registers are
-      // never copied)
-      f32x16 s, dp;
-      if (lim >= BT) {  // wave-uniform
-        asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(s) : "v"(a[0]), "v"(qf[0]), "v"(negl));
-      } else {
-        f32x16 cm = negl;
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (kh * 32 + acc_row(i, hl) >= lim) cm[i] = -INFINITY;
-        // (builtin here: the compiler places the VALU-write -> MFMA-srcC wait states, which it does not for asm)
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], qf[0], cm, 0, 0, 0);
+      for (int kh = 0; kh < 2; ++kh) {
+        if (!active) break;
+        half(Kt, Kt + TILE, kh, lim < BT, lim);
       }
-#pragma unroll
-      for (int ds = 1; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], qf[ds], s, 0, 0, 0);
-      read_rows(Vt, kh, lane, a);
-      asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(dp) : "v"(a[0]), "v"(gf[0]), "v"(negd));
-#pragma unroll
-      for (int ds = 1; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], gf[ds], dp, 0, 0, 0);
-      bf16x8 pf[2];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) pf[i >> 3][i & 7] = f2bf(__builtin_amdgcn_exp2f(s[i]) * dp[i]);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int dh = 0; dh < 2; ++dh)
-          dqt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Kt, kh * 2 + j, ta, dh), pf[j], dqt[dh], 0, 0, 0);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __syncthreads();
     }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();
+  } else {
+    const int nfull = d.Nk / BT;
+    for (int ti = 0; ti < nfull; ++ti) {
+      if (ti + 1 < ntiles) issue(ti + 1);
+      const char* Kt = smem + (ti & 1) * STAGE;
+      if (active) {
+        half(Kt, Kt + TILE, 0, false, BT);
+        half(Kt, Kt + TILE, 1, false, BT);
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if (nfull < ntiles && active) {  // the partial last tile (staged by the last loop iteration, or the prologue)
+      const char* Kt = smem + (nfull & 1) * STAGE;
+      const int lim = d.Nk - nfull * BT;
+      half(Kt, Kt + TILE, 0, true, lim);
+      if (lim > 32) half(Kt, Kt + TILE, 1, true, lim);
+    }
   }
   if (q < d.Nq) store_rowT((bf16*)d.dQ + (int64_t)b * d.dq_sb + (int64_t)q * d.dq_sn + h * 64, dqt, hl, d.scale);
 }
 
 // ---- dK, dV: a workgroup per (b, h, 128 keys), 64-query tiles ----
-__global__ __launch_bounds__(BW * 64, 2) void bwd_dkdv_kernel(const vp_attn_bwd_desc d) {
+// V = 1 (default): conflict-free swizzle; the next tile's per-query statistics loaded as raw values with no
+// dependent instruction until they are stored to LDS after the compute (V = 0 negated them at once, which put an
+// s_waitcnt vmcnt(0) — a wait for the whole next-tile DMA just issued — at the top of every tile); inactive waves
+// skip the compute as one block.
+template <int V>
+__global__ __launch_bounds__(BW * 64, V ? 3 : 2) void bwd_dkdv_kernel(const vp_attn_bwd_desc d) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -247,32 +322,89 @@ __global__ __launch_bounds__(BW * 64, 2) void bwd_dkdv_kernel(const vp_attn_bwd_
       vf[ds] = *(const bf16x8*)(vr + ds * 16 + hl * 8);
 #pragma unroll
       for (int e = 0; e < 8; ++e) kf[ds][e] = f2bf(bf2f(kf[ds][e]) * c);
+      // V = 1: consume V^T here (an empty asm use), so its load is complete before the loop; otherwise the wait
+      // analysis cannot see the prologue's asm wait and places counted waits on it inside the loop, where the
+      // in-order counter also holds the next tile's DMA
+      if (V) asm volatile("" : "+v"(vf[ds]));
     }
   }
   const bf16* qb = (const bf16*)d.Q + (int64_t)b * d.q_sb + h * 64;
   const bf16* gb = (const bf16*)d.dO + (int64_t)b * d.do_sb + h * 64;
   const float* lse_row = d.lse + ((int64_t)b * d.H + h) * d.Nq;
   const float* d_row = d.delta + ((int64_t)b * d.H + h) * d.Nq;
-  const TrAddr ta = tr_addr(lane);
+  const float* stat_row = wave == 0 ? lse_row : d_row;  // (BT = 64: wave 0 holds the lse, wave 1 the D; scalar)
+  const TrAddr ta = tr_addr<V>(lane);
   f32x16 dkt[2] = {zero16(), zero16()}, dvt[2] = {zero16(), zero16()};
   const bool active = kb * BW * 32 + wave * 32 < d.Nk;  // wave-uniform
   const int ntiles = (d.Nq + BT - 1) / BT;
   // per-query statistics of a tile: thread tid < 64 holds lse, 64 <= tid < 128 D (plain loads, written to LDS after
-  // the tile's compute, before the barrier that publishes the stage)
+  // the tile's compute, before the barrier that publishes the stage).  Rows past Nq: lse = +inf, so their S
+  // accumulators start at -inf and P = 0 there (no per-score mask); stored negated: they are the C-init of the S / dP
+  // accumulators
   float stat = 0.f;
   auto load_stat = [&](int ti) {
     const int qq = ti * BT + (tid & 63);
-    // rows past Nq: lse = +inf, so their S accumulators start at -inf and P = 0 there (no per-score mask)
-    // (stored negated: they are the C-init of the S / dP accumulators)
-    if (tid < 2 * BT) stat = qq < d.Nq ? -(tid < BT ? lse_row[qq] : d_row[qq]) : (tid < BT ? -INFINITY : 0.f);
+    if (V == 0) {
+      if (tid < 2 * BT) stat = qq < d.Nq ? -(tid < BT ? lse_row[qq] : d_row[qq]) : (tid < BT ? -INFINITY : 0.f);
+    } else {
+      stat = stat_row[min(ti * BT + lane, d.Nq - 1)];  // every thread, in bounds; nothing uses it until put_stat
+    }
   };
   auto put_stat = [&](int ti) {
-    if (tid < 2 * BT) ((float*)(smem + (ti & 1) * STAGE + 2 * TILE))[tid] = stat;
+    float v = stat;
+    if (V != 0) {  // (every thread: the load's wait is then on every path, none is left to the next tile's DMA)
+      const int qq = ti * BT + (tid & 63);
+      v = qq < d.Nq ? -stat : (tid < BT ? -INFINITY : 0.f);
+      v = __builtin_amdgcn_fmed3f(v, -INFINITY, INFINITY);
+    }
+    if (tid < 2 * BT) ((float*)(smem + (ti & 1) * STAGE + 2 * TILE))[tid] = v;
   };
+  const TileOffs qo = tile_offs(d.q_sn, wave, lane), go = tile_offs(d.do_sn, wave, lane);
   auto issue = [&](int ti) {
     char* st = smem + (ti & 1) * STAGE;
-    stage_tile(qb, d.q_sn, ti * BT, d.Nq, st, wave, lane);
-    stage_tile(gb, d.do_sn, ti * BT, d.Nq, st + TILE, wave, lane);
+    if (V) {
+      stage_tile_fast(qb, d.q_sn, ti * BT, d.Nq, st, wave, lane, qo);
+      stage_tile_fast(gb, d.do_sn, ti * BT, d.Nq, st + TILE, wave, lane, go);
+    } else {
+      stage_tile<V>(qb, d.q_sn, ti * BT, d.Nq, st, wave, lane);
+      stage_tile<V>(gb, d.do_sn, ti * BT, d.Nq, st + TILE, wave, lane);
+    }
+  };
+  auto half = [&](const char* Qt, const char* Gt, const float* st, int qh) {
+    // S and dP accumulators start at -lse / -D of their query rows (C-init from the staged, negated statistics): P =
+    // exp2(S), dS = P * dP, one exp and one multiply per score
+    f32x16 s, dp;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r0 = qh * 32 + 8 * j + 4 * hl;
+      const f32x4 l4 = *(const f32x4*)(st + r0), d4 = *(const f32x4*)(st + BT + r0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[4 * j + r] = l4[r];
+        dp[4 * j + r] = d4[r];
+      }
+    }
+    bf16x8 a[4];
+    read_rows<V>(Qt, qh, lane, a);
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], kf[ds], s, 0, 0, 0);
+    read_rows<V>(Gt, qh, lane, a);
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], vf[ds], dp, 0, 0, 0);
+    bf16x8 pp[2], pd[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = __builtin_amdgcn_exp2f(s[i]);
+      pp[i >> 3][i & 7] = f2bf(p);
+      pd[i >> 3][i & 7] = f2bf(p * dp[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        dvt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Gt, qh * 2 + j, ta, dh), pp[j], dvt[dh], 0, 0, 0);
+        dkt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Qt, qh * 2 + j, ta, dh), pd[j], dkt[dh], 0, 0, 0);
+      }
   };
   issue(0);
   load_stat(0);
@@ -287,43 +419,15 @@ __global__ __launch_bounds__(BW * 64, 2) void bwd_dkdv_kernel(const vp_attn_bwd_
     const char* Qt = smem + (ti & 1) * STAGE;
     const char* Gt = Qt + TILE;
     const float* st = (const float*)(Qt + 2 * TILE);
-    // S and dP accumulators start at -lse / -D of their query rows (C-init from the staged, negated statistics): P =
-    // exp2(S), dS = P * dP, one exp and one multiply per score
+    if (V == 0) {
 #pragma unroll
-    for (int qh = 0; qh < 2; ++qh) {
-      if (!active) break;
-      f32x16 s, dp;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r0 = qh * 32 + 8 * j + 4 * hl;
-        const f32x4 l4 = *(const f32x4*)(st + r0), d4 = *(const f32x4*)(st + BT + r0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s[4 * j + r] = l4[r];
-          dp[4 * j + r] = d4[r];
-        }
+      for (int qh = 0; qh < 2; ++qh) {
+        if (!active) break;
+        half(Qt, Gt, st, qh);
       }
-      bf16x8 a[4];
-      read_rows(Qt, qh, lane, a);
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], kf[ds], s, 0, 0, 0);
-      read_rows(Gt, qh, lane, a);
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], vf[ds], dp, 0, 0, 0);
-      bf16x8 pp[2], pd[2];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(s[i]);
-        pp[i >> 3][i & 7] = f2bf(p);
-        pd[i >> 3][i & 7] = f2bf(p * dp[i]);
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int dh = 0; dh < 2; ++dh) {
-          dvt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Gt, qh * 2 + j, ta, dh), pp[j], dvt[dh], 0, 0, 0);
-          dkt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Qt, qh * 2 + j, ta, dh), pd[j], dkt[dh], 0, 0, 0);
-        }
+    } else if (active) {
+      half(Qt, Gt, st, 0);
+      half(Qt, Gt, st, 1);
     }
     if (ti + 1 < ntiles) put_stat(ti + 1);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -351,11 +455,18 @@ extern "C" int vp_attention_bwd_bf16(const vp_attn_bwd_desc* d, void* stream) {
   if ((int64_t)BT * d->q_sn * 2 >= ((int64_t)1 << 31) || (int64_t)BT * d->k_sn * 2 >= ((int64_t)1 << 31) ||
       (int64_t)BT * d->v_sn * 2 >= ((int64_t)1 << 31) || (int64_t)BT * d->do_sn * 2 >= ((int64_t)1 << 31))
     return VP_ERR_ARG;
+  // VP_ATTN_BWD_VARIANT: 1 (default) or 0 (round 2's kernels); A/B only — same arithmetic, same results.  Measured and
+  // dropped in round 5 (profiles/r05_attn_bwd_ab.log): variant 1 with the dK / dV kernel at 2 waves per SIMD (+7 %),
+  // with dQ at 3 (60 B of scratch, +8 %), and an in-wave software pipeline of both kernels (+4 %)
+  const char* kv = vp_knob(VPK_ATTN_BWD_VARIANT);
+  const int var = kv ? atoi(kv) : 1;
+  if (var != 0 && var != 1) return VP_ERR_UNSUPPORTED;
   static bool attr = false;
   if (!attr) {
     attr = true;
-    (void)hipFuncSetAttribute((const void*)bwd_dq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BWD);
-    (void)hipFuncSetAttribute((const void*)bwd_dkdv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BWD);
+    for (const void* f : {(const void*)bwd_dq_kernel<0>, (const void*)bwd_dkdv_kernel<0>, (const void*)bwd_dq_kernel<1>,
+                          (const void*)bwd_dkdv_kernel<1>})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BWD);
   }
   hipStream_t s = (hipStream_t)stream;
   const int64_t nd = (int64_t)d->B * d->Nq * d->H;
@@ -365,9 +476,11 @@ extern "C" int vp_attention_bwd_bf16(const vp_attn_bwd_desc* d, void* stream) {
   const int64_t gq = (int64_t)d->B * d->H * ((d->Nq + BW * 32 - 1) / (BW * 32));
   const int64_t gk = (int64_t)d->B * d->H * ((d->Nk + BW * 32 - 1) / (BW * 32));
   if (gq > 0x7fffffff || gk > 0x7fffffff) return VP_ERR_ARG;
-  hipLaunchKernelGGL(bwd_dq_kernel, dim3((unsigned)gq), dim3(BW * 64), LDS_BWD, s, *d);
+  void (*dq)(const vp_attn_bwd_desc) = var ? bwd_dq_kernel<1> : bwd_dq_kernel<0>;
+  hipLaunchKernelGGL(dq, dim3((unsigned)gq), dim3(BW * 64), LDS_BWD, s, *d);
   VP_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bwd_dkdv_kernel, dim3((unsigned)gk), dim3(BW * 64), LDS_BWD, s, *d);
+  void (*dkdv)(const vp_attn_bwd_desc) = var ? bwd_dkdv_kernel<1> : bwd_dkdv_kernel<0>;
+  hipLaunchKernelGGL(dkdv, dim3((unsigned)gk), dim3(BW * 64), LDS_BWD, s, *d);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }

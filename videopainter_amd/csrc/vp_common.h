@@ -214,6 +214,7 @@ enum VpKnob {
   VPK_T5_ATTN,
   VPK_CONV_HOIST,
   VPK_CONV_PIPE,
+  VPK_ATTN_BWD_VARIANT,
   VPK_COUNT
 };
 const char* vp_knob(int k);
