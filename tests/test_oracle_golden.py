@@ -223,3 +223,25 @@ def test_pipe_pixel_inputs_are_the_reference_processor_outputs():
     for k, t in (("video", inp["video"]), ("masks", inp["masks"]), ("image", inp["image"])):
         d = torch.tensor([t.double().sum(), t.double().abs().sum(), t.double().norm()], dtype=torch.float64)
         assert torch.allclose(d, g[f"{k}_digest"], rtol=1e-12, atol=1e-9), k
+
+
+def test_config4_chain_fixture_pins_the_draws_and_masks():
+    """tests/golden/config4_chain.safetensors (the full-size chained any-length run of the reference pipeline): the
+    generator draws tests/golden/cases.chain4_draws regenerates are the reference run's (fp64 digests), and each
+    window's recorded latent mask is the nearest-frame / nearest-pixel pick of cases.chain4_pixel_masks (the
+    reference's F.interpolate of the window's pixel masks, default mode 'nearest') with frame 0 of window 0 clear."""
+    from tests.golden.cases import CHAIN4_CASE, chain4_draws, chain4_pixel_masks
+    g = load_file(os.path.join(GOLD, "config4_chain.safetensors"))
+    c = CHAIN4_CASE
+    draws = chain4_draws()
+    assert len(draws) == (c["total_frames"] // c["stride"]) * (1 + c["steps"])
+    for i, dr in enumerate(draws):
+        d = torch.tensor([dr.double().sum(), dr.double().abs().sum(), dr.double().norm()], dtype=torch.float64)
+        assert torch.allclose(d, g[f"draw.{i}.digest"], rtol=1e-12, atol=1e-9), i
+    pm = torch.from_numpy(np.ascontiguousarray(chain4_pixel_masks())).float()  # [98, 480, 720]
+    for w in range(c["total_frames"] // c["stride"]):
+        win = pm[w * c["stride"]:w * c["stride"] + c["num_frames"]][None, None]
+        want = torch.nn.functional.interpolate(win, size=(13, 60, 90))  # anyl.py:438-440
+        assert torch.equal(g[f"w{w}.mask"].float(), want), w
+    assert tuple(int(v) for v in g["final_shape"]) == (1, 25, 16, 60, 90)
+    assert float(g["ref_bf16_rel"][0]) < 2e-2
