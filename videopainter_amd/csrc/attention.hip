@@ -968,9 +968,37 @@ VP_DEV void p1_mask(f32x16& s, int rem, int hl4) {
 // issued at the top of tile t, VMC = this tile's DMA instructions per wave; 0 for the 2-slot ring)
 // sync (SL = 2): the seam waits for the DMA and passes the barrier (false: the next tile was published by an earlier
 // barrier — p2w's one barrier per two tiles)
-template <int SL, bool ANCH = false, int VMC = 0>
+// Barrier-free ring (p2wf): per-slot LDS counters instead of the seam barrier.  ready[s] counts the waves whose own
+// LDS-DMA pieces of the tile in slot s have landed (each wave adds 1 after its counted vmcnt wait), done[s] the waves
+// that finished reading that tile (added after the seam's lgkmcnt(0)).  A wave reads tile t once ready[t & 3] reached
+// NWV x (the slot's use count), and refills a slot once done[] for the tile it held did the same — so the waves of a
+// workgroup drift apart by up to the ring's slack instead of meeting at every tile.  Every spin is bounded: a wave that
+// gives up records it, and the workgroup then flags its block for the exact re-run (the anchored kernel's redo path),
+// so neither a hang nor a wrong result can come out of it.
+typedef __attribute__((address_space(3))) int lds_int;
+struct RingCtr {
+  lds_int* ready;  // [4]
+  lds_int* done;   // [4]
+};
+constexpr int RING_SPIN_MAX = 1 << 15;
+VP_DEV void ring_add(lds_int* c, int lane) {
+  if (lane == 0) __atomic_fetch_add(c, 1, __ATOMIC_RELAXED);
+}
+// wait until *c >= target; false when the bound ran out
+VP_DEV bool ring_wait(lds_int* c, int target) {
+#pragma unroll 1
+  for (int it = 0; it < RING_SPIN_MAX; ++it) {
+    const int v = __builtin_amdgcn_readfirstlane(__atomic_load_n(c, __ATOMIC_RELAXED));
+    if (v >= target) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
+template <int SL, bool ANCH = false, int VMC = 0, bool BFREE = false>
 VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn, int lim, bool masked, bool last,
-                    bool wait_all, int lane, const int (&vo)[2], bool sync = true) {
+                    bool wait_all, int lane, const int (&vo)[2], bool sync = true, RingCtr rc = {},
+                    int slot = 0, int nslot = 0, int tgt_next = 0, bool* stalled = nullptr) {
   const int hl = lane >> 5;
   const char* Vl = Kl + KT;
 #pragma unroll
@@ -996,7 +1024,16 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
         p1_step<0, 1, 1, 0, 0, true, false, ANCH>(r, sel);
       p1_read_v(Vl, h, vo, r.vf[0]);
       if (h == 3 && !last) {
-        if (sync) {
+        if (BFREE) {
+          // own pieces of the next tile landed, own reads of this one retired: count both, then wait for the others'
+          if (VMC == 0 || wait_all)
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VMC) : "memory");
+          ring_add(rc.ready + nslot, lane);
+          ring_add(rc.done + slot, lane);
+          if (!ring_wait(rc.ready + nslot, tgt_next)) *stalled = true;
+        } else if (sync) {
           if (VMC == 0 || wait_all)
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
           else
@@ -1072,12 +1109,14 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
 // (tools/attn_clock.py ablation) — and the L2 -> LDS bytes per FLOP halve.
 // TPB = 2 (p2w only): one barrier per two tiles — tiles t + 2 and t + 3 issued together at the top of every even tile
 // of the range, both waited for and published by the barrier at the seam of the odd tile before them.
-template <bool TAIL = false, int SL = 4, bool ANCH = false, int NWV = 4, int TPB = 1>
+// BFREE (p2wf: NWV = 8, TPB = 1, ANCH): the barrier-free ring above in place of the seam barrier.
+template <bool TAIL = false, int SL = 4, bool ANCH = false, int NWV = 4, int TPB = 1, bool BFREE = false>
 __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_fwd_p1(const vp_attn_desc d,
                                                                                         const AttnSplit sp) {
   static_assert(!ANCH || SL == 2, "the anchored form is the two-workgroups-per-CU pipeline");
   static_assert(NWV == 4 || (NWV == 8 && SL == 2), "8-wave workgroups run the p2 schedule");
   static_assert(TPB == 1 || NWV == 8, "one barrier per two tiles needs the 4-slot ring");
+  static_assert(!BFREE || (NWV == 8 && TPB == 1 && ANCH), "the barrier-free ring: p2w's 4-slot ring, anchored");
   constexpr int QBV = NWV * 64;               // queries per workgroup
   constexpr int PPWV = NP / NWV;              // DMA pieces per operand, wave and tile
   constexpr int RING = NWV == 8 ? 4 : SL;     // LDS ring slots
@@ -1215,7 +1254,15 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  // ring counters past the anchored flags (NWV ints): ready[4], done[4]
+  RingCtr rc{(lds_int*)(lds_void_t*)(smem + RING * ST + 32), (lds_int*)(lds_void_t*)(smem + RING * ST + 48)};
+  if (BFREE) {
+    if (tid < 8) rc.ready[tid] = 0;  // (ready and done are contiguous)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
+  if (BFREE) ring_add(rc.ready + (tbeg & 3), lane);  // tile tbeg: published by the barrier, counted for its slot
+  bool stalled = false;
   if (any) p1_read_k(slot_of(tbeg), 0, lane, r.kf[0]);
   {
     const f32x16 z = {};
@@ -1260,6 +1307,9 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
       }
       sync = !even;
     } else if (ti + AHEAD < tend && (!(VP_P1_ABL & 1) || ti == tbeg)) {
+      // (barrier-free ring: the slot of tile ti + 2 last held tile ti - 2; every wave must be done reading it)
+      if (BFREE && ti - 2 >= tbeg && !ring_wait(rc.done + ((ti - 2) & 3), NWV * (((ti - 2 - tbeg) >> 2) + 1)))
+        stalled = true;
       issue(ti + AHEAD);
     }
     int lim = KB;
@@ -1267,9 +1317,10 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
       const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
       lim = sg.n - sg.key0;
     }
-    p1_tile<SL, ANCH, RING == 4 && SL == 2 && TPB == 1 ? 2 * PPWV : 0>(
+    p1_tile<SL, ANCH, RING == 4 && SL == 2 && TPB == 1 ? 2 * PPWV : 0, BFREE>(
         r, sel, slot_of(ti), slot_of(ti + 1), __builtin_amdgcn_readfirstlane(lim), lim < KB, ti + 1 >= tend,
-        TPB == 2 || ti + 2 >= tend, lane, vo, sync);
+        TPB == 2 || ti + 2 >= tend, lane, vo, sync, rc, ti & 3, (ti + 1) & 3, NWV * (((ti + 1 - tbeg) >> 2) + 1),
+        &stalled);
   }
   // drain: PV + row sums of the last job (3, 1)
 #pragma unroll
@@ -1296,7 +1347,7 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
     // any non-finite row sum or output, or a row sum under 2^-96 (its terms would underflow), in the workgroup ->
     // store nothing, flag the block for the exact re-run (workgroup-uniform decision through 16 bytes of LDS past
     // the ring; the barrier also retires every wave's last reads of the ring)
-    bool bad = false;
+    bool bad = stalled;  // (a ring wait that ran out of bound: redo the block)
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi) {
       // (a tail-split partial of an empty key range holds no mass: only its non-finite values count.  A non-empty
@@ -2692,7 +2743,7 @@ struct AttnVar {
 #else
 #define VP_EXTRA(a, b) nullptr, nullptr
 #endif
-enum { V_LAZY, V_W32, V_W64, V_S16, V_A16, V_S16I, V_P1, V_W64F, V_P2, V_P2A, V_P2W, V_P2W2, V_NVAR };
+enum { V_LAZY, V_W32, V_W64, V_S16, V_A16, V_S16I, V_P1, V_W64F, V_P2, V_P2A, V_P2W, V_P2W2, V_P2WF, V_NVAR };
 static const AttnVar attn_vars[] = {
     {"lazy", VP_EXTRA(attn_fwd<MODE_LAZY>, (attn_fwd<MODE_LAZY, true>)), NW * 64, LDS_BYTES},
     {"w32", VP_EXTRA(attn_fwd<MODE_BOUNDED>, (attn_fwd<MODE_BOUNDED, true>)), NW * 64, LDS_BYTES},
@@ -2710,9 +2761,15 @@ static const AttnVar attn_vars[] = {
     // p2w with one barrier per two tiles
     {"p2w2", (const void*)attn_fwd_p1<false, 2, true, 8, 2>, (const void*)attn_fwd_p1<true, 2, true, 8, 2>, 8 * 64,
      4 * ST + 32, 512},
+    // p2w on the barrier-free ring (per-slot LDS counters; rejected in round 5: 6.41 vs 6.24 ms, the clock up 3 % but
+    // the loop 5 % longer, profiles/r05_attn_p2wf_rejected.log)
+    {"p2wf", VP_EXTRA((attn_fwd_p1<false, 2, true, 8, 1, true>), (attn_fwd_p1<true, 2, true, 8, 1, true>)), 8 * 64,
+     4 * ST + 64, 512},
 };
 #undef VP_EXTRA
 static_assert(sizeof(attn_vars) / sizeof(attn_vars[0]) == V_NVAR, "variant table");
+// the anchored p2 family (a flag per block, the a16 redo)
+static bool anchored_var(int v) { return v == V_P2A || v == V_P2W || v == V_P2W2 || v == V_P2WF; }
 
 struct AttnPlan {
   const AttnVar* v;
@@ -2777,7 +2834,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   // profiles/r04_attn_p2a_ab.log: the anchor costs nothing and no bound has to hold); p2 stays the bounded challenger
   if (variant < 0) variant = V_P2A;
   // an unbounded launch needs a kernel that does not assume the bound: lazy, a16, p2a or p2w
-  const bool anchored = variant == V_P2A || variant == V_P2W || variant == V_P2W2;
+  const bool anchored = anchored_var(variant);
   if (!bounded && variant != V_LAZY && variant != V_A16 && !anchored) return VP_ERR_UNSUPPORTED;
   if (attn_vars[variant].fn == nullptr) return VP_ERR_UNSUPPORTED;
   // the resample processor's segment hints: k2_len / l_extra (the closed-form null keys, the default) are taken by
@@ -2809,7 +2866,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
     }
   }
   pl.ws_bytes = pl.part_bytes;
-  if (pl.var == V_P2A || pl.var == V_P2W || pl.var == V_P2W2) pl.ws_bytes += ((pl.nblk - pl.ntail) + (int64_t)pl.ntail * pl.nsplit) * 4;
+  if (anchored_var(pl.var)) pl.ws_bytes += ((pl.nblk - pl.ntail) + (int64_t)pl.ntail * pl.nsplit) * 4;
   return VP_OK;
 }
 }  // namespace
@@ -2838,7 +2895,7 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   rc = attn_plan(d, pl);
   if (rc != VP_OK) return rc;
   const bool have_ws = workspace != nullptr && workspace_bytes >= pl.ws_bytes && ((uintptr_t)workspace & 15) == 0;
-  if ((pl.var == V_P2A || pl.var == V_P2W || pl.var == V_P2W2) && !have_ws) {
+  if (anchored_var(pl.var) && !have_ws) {
     // p2a / p2w need their redo flags: without the workspace, the anchored 16x16x32 kernel alone (unsplit)
     pl.nblk = (int64_t)d->B * d->H * ((d->Nq + QB - 1) / QB);  // a16's 256-query blocks
     pl.var = V_A16;
@@ -2849,7 +2906,7 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   const AttnVar& v = *pl.v;
   const bool split = pl.ntail > 0 && have_ws;
   const int64_t main_blocks = split ? pl.nblk - pl.ntail : pl.nblk;
-  int* flags = pl.var == V_P2A || pl.var == V_P2W || pl.var == V_P2W2 ? (int*)((char*)workspace + pl.part_bytes) : nullptr;
+  int* flags = anchored_var(pl.var) ? (int*)((char*)workspace + pl.part_bytes) : nullptr;
   hipError_t le = hipSuccess;
   if (main_blocks > 0) {
     const AttnSplit none = {0, 1, nullptr, flags, (int)main_blocks, pl.nsplit, 0};
