@@ -135,6 +135,19 @@ VP_DEV f32x16 zero16() {
   return z;
 }
 
+// 8 fp32 -> bf16x8 as 4 pair conversions (v_cvt_pk_bf16_f32 each): element-wise inserts made the compiler add
+// v_alignbit / v_perm shuffles and duplicate conversions (V = 1 only; the same RNE roundings)
+typedef float f32v2 __attribute__((ext_vector_type(2)));
+VP_DEV bf16x8 pack8(const float (&v)[8]) {
+  u32x4 w;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const bf16x2 h = __builtin_convertvector((f32v2){v[2 * e], v[2 * e + 1]}, bf16x2);
+    w[e] = __builtin_bit_cast(uint32_t, h);
+  }
+  return __builtin_bit_cast(bf16x8, w);
+}
+
 // 32x32 accumulator element i of lane group hl sits in row 8 (i / 4) + 4 hl + i % 4
 VP_DEV int acc_row(int i, int hl) { return 8 * (i >> 2) + 4 * hl + (i & 3); }
 
@@ -248,8 +261,18 @@ __global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_a
 #pragma unroll
     for (int ds = 1; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], gf[ds], dp, 0, 0, 0);
     bf16x8 pf[2];
+    if (V) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) pf[i >> 3][i & 7] = f2bf(__builtin_amdgcn_exp2f(s[i]) * dp[i]);
+      for (int j = 0; j < 2; ++j) {
+        float a[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] = __builtin_amdgcn_exp2f(s[8 * j + e]) * dp[8 * j + e];
+        pf[j] = pack8(a);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) pf[i >> 3][i & 7] = f2bf(__builtin_amdgcn_exp2f(s[i]) * dp[i]);
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -392,6 +415,7 @@ __global__ __launch_bounds__(BW * 64, V ? 3 : 2) void bwd_dkdv_kernel(const vp_a
 #pragma unroll
     for (int ds = 0; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], vf[ds], dp, 0, 0, 0);
     bf16x8 pp[2], pd[2];
+    // (element-wise inserts here: the pair-packed form of the dQ kernel spills at this kernel's 168-register budget)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float p = __builtin_amdgcn_exp2f(s[i]);
@@ -457,7 +481,8 @@ extern "C" int vp_attention_bwd_bf16(const vp_attn_bwd_desc* d, void* stream) {
     return VP_ERR_ARG;
   // VP_ATTN_BWD_VARIANT: 1 (default) or 0 (round 2's kernels); A/B only — same arithmetic, same results.  Measured and
   // dropped in round 5 (profiles/r05_attn_bwd_ab.log): variant 1 with the dK / dV kernel at 2 waves per SIMD (+7 %),
-  // with dQ at 3 (60 B of scratch, +8 %), and an in-wave software pipeline of both kernels (+4 %)
+  // with dQ at 3 (60 B of scratch, +8 %; with the pair packing 24 B, equal), and an in-wave software pipeline of
+  // both kernels (+4 %)
   const char* kv = vp_knob(VPK_ATTN_BWD_VARIANT);
   const int var = kv ? atoi(kv) : 1;
   if (var != 0 && var != 1) return VP_ERR_UNSUPPORTED;
