@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 15
+#define VP_ABI_VERSION 16
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
@@ -113,6 +113,15 @@ typedef struct vp_gemm_desc {
    * main loop (VP_ERR_UNSUPPORTED otherwise) and epilogue BIAS, GATED or BIAS_QKNORM_ROPE.  0: no tail.  (ABI 14.) */
   int32_t a_tail_k, pad3;
   int64_t a_tail_off[3];
+  /* VP_EPI_BIAS_QKNORM_ROPE with a separable 3D RoPE table (ABI 16; NULL rope_ax[0]: the full table): rope_ax = the
+   * per-axis factors of rope_cos / rope_sin — cos_t, sin_t [F][16], cos_y, sin_y [Hh][24], cos_x, sin_x [Ww][24] fp32,
+   * exact slices of the full table (CogVideoX's 3D RoPE, DF/models/embeddings.py:457-530: dims 0-15 by frame, 16-39 by
+   * row, 40-63 by column) — with rope_hw = Hh * Ww, rope_w = Ww and their division magics rope_mhw / rope_mw
+   * (ceil(2^32 / d)); the epilogue reads those rows (a few KB, cache-resident) instead of the token's row of the
+   * [F*Hh*Ww][64] table: the same values, bit-identical output.  rope_cos / rope_sin stay set. */
+  const float* rope_ax[6];
+  int32_t rope_hw, rope_w;
+  uint32_t rope_mhw, rope_mw;
 } vp_gemm_desc;
 
 int vp_gemm_bf16(const vp_gemm_desc* d, void* stream);

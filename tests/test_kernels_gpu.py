@@ -488,6 +488,18 @@ def test_gemm_qknorm_rope_epilogue_matches_separate_kernels(H, T, rope, gemm_var
     K.gemm(x, ws, bs, got, epilogue=NAT.EPI_BIAS_QKNORM_ROPE, qk_norm=tuple(lns), rope=rp, tokens_per_batch=Ntok,
            text_len=T)
     assert torch.equal(got, want)
+    if rope:
+        # the separable form (the transformer's RopeTables carry their grid): the epilogue reads per-axis rows, with
+        # the same values, so the same bits
+        from videopainter_amd.attention_processor import RopeTables
+        assert Nv == 3 * 8 * 12
+        rt = RopeTables(rp)
+        rt.grid = (3, 8, 12)
+        assert K.rope_axis_tables(rt, rt.grid) is not None
+        got_sep = torch.full_like(got, float("nan"))
+        K.gemm(x, ws, bs, got_sep, epilogue=NAT.EPI_BIAS_QKNORM_ROPE, qk_norm=tuple(lns), rope=rt,
+               tokens_per_batch=Ntok, text_len=T)
+        assert torch.equal(got_sep, want)
     # and against plain torch fp32 (LN over each head, rotary on video tokens)
     y = bf(x.float().cpu() @ torch.cat(ws).float().cpu().T + torch.cat(bs).float().cpu()).view(B, Ntok, 3 * D)
     for s in range(2):

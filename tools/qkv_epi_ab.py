@@ -1,6 +1,6 @@
 """The fused QKV GEMM's epilogue cost at config 2's shape (M = 2 x 17776, N = 3 x 3072, K = 3072), interleaved in one
-process: the bias epilogue, the qk-norm + RoPE epilogue with the [Nv, 64] fp32 RoPE tables, and the same epilogue
-with no RoPE table (no table loads: what the table traffic costs).
+process: the bias epilogue, the qk-norm + RoPE epilogue with the [Nv, 64] fp32 RoPE tables, the same epilogue
+with no RoPE table (no table loads: what the table traffic costs), and with the separable table's per-axis rows.
     python tools/qkv_epi_ab.py [--iters 10]"""
 import argparse
 import json
@@ -28,8 +28,12 @@ def main():
     ws = [(torch.randn(D, D, device=dev, generator=g) * D ** -0.5).to(torch.bfloat16) for _ in range(3)]
     bs = [(torch.randn(D, device=dev, generator=g) * 0.1).to(torch.bfloat16) for _ in range(3)]
     nq, nk = LayerNorm(64, eps=1e-6).to(dev, torch.bfloat16), LayerNorm(64, eps=1e-6).to(dev, torch.bfloat16)
-    cos = torch.rand(Nv, 64, device=dev, generator=g)
-    sin = torch.rand(Nv, 64, device=dev, generator=g)
+    from videopainter_amd.attention_processor import RopeTables
+    from videopainter_amd.embeddings import prepare_rotary_positional_embeddings
+    cos, sin = prepare_rotary_positional_embeddings(480, 720, 13, 64, device=dev)  # config 2's table (13 x 30 x 45)
+    rope_sep = RopeTables((cos.float().contiguous(), sin.float().contiguous()))
+    rope_sep.grid = (13, 30, 45)
+    cos, sin = rope_sep
     out = torch.empty(M, 3 * D, device=dev, dtype=torch.bfloat16)
     runs = {
         "bias": lambda: K.gemm(x, ws, bs, out),
@@ -37,6 +41,8 @@ def main():
                                       rope=(cos, sin), tokens_per_batch=Ntok, text_len=T),
         "qknorm_norope": lambda: K.gemm(x, ws, bs, out, epilogue=N.EPI_BIAS_QKNORM_ROPE, qk_norm=(nq, nk),
                                         rope=None, tokens_per_batch=Ntok, text_len=T),
+        "qknorm_rope_sep": lambda: K.gemm(x, ws, bs, out, epilogue=N.EPI_BIAS_QKNORM_ROPE, qk_norm=(nq, nk),
+                                          rope=rope_sep, tokens_per_batch=Ntok, text_len=T),
     }
     res = {k: [] for k in runs}
     for _ in range(3):

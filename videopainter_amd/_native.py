@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -34,7 +34,8 @@ class GemmDesc(C.Structure):
                 ("inject_mask_bstride", i64),
                 ("addrows", vp), ("addrows_ld", i64), ("addrows_offset", i64),
                 ("qk_ln_w", vp * 2), ("qk_ln_b", vp * 2), ("qk_eps", f32 * 2), ("rope_cos", vp), ("rope_sin", vp),
-                ("a_tail_k", i32), ("pad3", i32), ("a_tail_off", i64 * 3)]
+                ("a_tail_k", i32), ("pad3", i32), ("a_tail_off", i64 * 3), ("rope_ax", vp * 6), ("rope_hw", i32),
+                ("rope_w", i32), ("rope_mhw", C.c_uint32), ("rope_mw", C.c_uint32)]
 
 
 class AttnDesc(C.Structure):

@@ -142,7 +142,7 @@ class CogvideoXBranchModel(CogVideoXTransformer3DModel):
         T = enc.shape[1]
         D = cfg.num_attention_heads * cfg.attention_head_dim
         emb = self._time_embed(timestep, B, dev)
-        rope = _rope_dev(image_rotary_emb, dev)
+        rope = _rope_dev(image_rotary_emb, dev, grid=(F, H // cfg.patch_size, W // cfg.patch_size))
         scale = float(conditioning_scale)
         if train:
             # the training step's branch call (train_cogvideox_inpainting_i2v_video.py:1856-1865): differentiable

@@ -212,10 +212,35 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
       // latency runs under the previous fragment's work instead of in front of each fragment
       f32x4 csb[2][4], snb[2][4];
       bool rotb[2];
+      const bool sep = has_rope && d.rope_ax[0] != nullptr;  // separable table: per-axis rows (vp_gemm_desc)
       auto load_rope = [&](int i, f32x4 (&cs)[4], f32x4 (&sn)[4], bool& rot) {
         int tok = tok0 + wr * WM + i * 16 + (lane & 15);
         while (tok >= d.tokens_per_batch) tok -= d.tokens_per_batch;
         rot = has_rope && tok >= d.text_len;
+        if (sep) {
+          // token v -> (frame t, row y, column x) by the host's division magics; lane group g's quad of dims
+          // 16 jj + 4 g .. + 3 lies in one axis (the axis boundaries 16 and 40 are multiples of 4)
+          const unsigned v = rot ? (unsigned)(tok - d.text_len) : 0u;
+          const unsigned t = __umulhi(v, d.rope_mhw);
+          const unsigned rr = v - t * (unsigned)d.rope_hw;
+          const unsigned y = __umulhi(rr, d.rope_mw);
+          const unsigned x = rr - y * (unsigned)d.rope_w;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int dim0 = 16 * jj + 4 * g;
+            int ax, off;
+            if (jj == 0) {
+              ax = 0, off = (int)t * 16 + dim0;
+            } else if (jj == 1 || (jj == 2 && g < 2)) {
+              ax = 2, off = (int)y * 24 + dim0 - 16;
+            } else {
+              ax = 4, off = (int)x * 24 + dim0 - 40;
+            }
+            cs[jj] = *(const f32x4*)(d.rope_ax[ax] + off);
+            sn[jj] = *(const f32x4*)(d.rope_ax[ax + 1] + off);
+          }
+          return;
+        }
         const int64_t ro = rot ? (int64_t)(tok - d.text_len) * 64 : 0;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {

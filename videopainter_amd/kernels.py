@@ -157,6 +157,17 @@ def gemm(a: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[Opti
                 raise ValueError(f"rope tables must be fp32 [{tokens_per_batch - text_len}, 64], "
                                  f"got {tuple(cos.shape)}")
             d.rope_cos, d.rope_sin = _p(cos), _p(sin)
+            # a separable 3D table (the transformer's RopeTables carry their grid): the epilogue reads the per-axis
+            # rows instead (the same values; ROPE_SEPARABLE = False keeps the full-table reads, A/B).  The division
+            # magics ceil(2^32 / d) are exact for token indices v with v * d < 2^32.
+            grid = getattr(rope, "grid", None)
+            axes = rope_axis_tables(rope, grid) if grid is not None and ROPE_SEPARABLE else None
+            if axes is not None and cos.shape[0] * int(grid[1]) * int(grid[2]) < (1 << 32):
+                hw, w = int(grid[1]) * int(grid[2]), int(grid[2])
+                for i, t in enumerate(axes):
+                    d.rope_ax[i] = _p(t)
+                d.rope_hw, d.rope_w = hw, w
+                d.rope_mhw, d.rope_mw = ((1 << 32) + hw - 1) // hw, ((1 << 32) + w - 1) // w
     if epilogue == N.EPI_BIAS_ADDROWS:
         _chk(addrows, "addrows")
         d.addrows, d.addrows_ld, d.addrows_offset = _p(addrows), _rowmajor(addrows, "addrows"), addrows_offset
@@ -639,6 +650,9 @@ def partition_rows_index(tok_mask: torch.Tensor):
     N.check(N.lib().vp_partition_rows_index(_p(tok_mask), tok_mask.stride(0), B, Ntok, _p(dst), _p(cnt), _stream()),
             "vp_partition_rows_index")
     return dst, cnt
+
+
+ROPE_SEPARABLE = True  # the fused QKV epilogue reads a separable RoPE table per axis (gemm, VP_EPI_BIAS_QKNORM_ROPE)
 
 
 def rope_axis_tables(rope, grid):

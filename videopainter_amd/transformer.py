@@ -688,7 +688,7 @@ class CogVideoXTransformer3DModel(ModelMixin):
             resample_mask = torch.zeros(B, T + tok_mask.shape[1], device=dev, dtype=torch.bool)
             resample_mask[:, T:] = tok_mask.bool()
             rm_u8 = _u8(resample_mask)
-        rope = _rope_dev(image_rotary_emb, dev)
+        rope = _rope_dev(image_rotary_emb, dev, grid=(F, H // p, W // p))
         bs = None
         if branch_block_samples is not None:
             bs = [s.to(dev, BF16) for s in branch_block_samples]
