@@ -166,6 +166,46 @@ def test_block_backward_matches_oracle():
         _check(n, ours[n], gp32[n], gp16[n])
 
 
+@pytest.mark.parametrize("lora", [False, True], ids=["plain", "lora"])
+def test_saved_attention_backward_is_bit_identical(monkeypatch, lora):
+    """autograd.SAVE_ATTENTION: the block forward keeps its attention output and lse and the backward skips the
+    attention recompute — the same kernel call's values the recompute would produce, so every gradient is the same
+    bits as with the recompute (also with an unfused trainable adapter on the projections)."""
+    from videopainter_amd import autograd as AG
+    from videopainter_amd.autograd import block_apply
+    tr, br, _, _ = _models()
+    blk = br.transformer_blocks[0]
+    if lora:  # the VideoPainterID path: adapters on the frozen transformer's projections
+        tr.add_adapter({"r": 8, "lora_alpha": 8, "target_modules": ["to_q", "to_k", "to_v", "to_out.0"]})
+        blk = tr.transformer_blocks[0]
+        g0 = torch.Generator().manual_seed(9)
+        with torch.no_grad():
+            for l in (blk.attn1.to_q, blk.attn1.to_k, blk.attn1.to_v, blk.attn1.to_out[0]):
+                l.lora_B.weight.copy_(torch.randn(l.lora_B.weight.shape, generator=g0).to(dev) * 0.05)
+    i = tiny_inputs()
+    T = i["enc"].shape[1]
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, T + 288, 128, generator=g).bfloat16()
+    temb = torch.randn(2, 32, generator=g).bfloat16()
+    dout = torch.randn(2, T + 288, 128, generator=g).bfloat16()
+    res = []
+    for save in (True, False):
+        monkeypatch.setattr(AG, "SAVE_ATTENTION", save)
+        for p in blk.parameters():
+            p.grad = None
+        xd = x.to(dev).requires_grad_()
+        td = temb.to(dev).requires_grad_()
+        out = block_apply(blk, xd, T, td, (i["rope"][0].to(dev), i["rope"][1].to(dev)))
+        out.backward(dout.to(dev))
+        res.append((out.detach(), xd.grad, td.grad,
+                    {n: p.grad.clone() for n, p in blk.named_parameters() if p.grad is not None}))
+    (o1, gx1, gt1, gp1), (o0, gx0, gt0, gp0) = res
+    assert torch.equal(o1, o0) and torch.equal(gx1, gx0) and torch.equal(gt1, gt0)
+    assert gp1.keys() == gp0.keys() and len(gp1) > 0
+    for n in gp1:
+        assert torch.equal(gp1[n], gp0[n]), n
+
+
 @pytest.mark.parametrize("wo_text", [False, True], ids=["text", "wo_text"])
 def test_branch_gradients_through_frozen_transformer(wo_text):
     """The training step (train_cogvideox_inpainting_i2v_video.py:1856-1892): branch (trainable) -> samples injected

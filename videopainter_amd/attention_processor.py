@@ -177,11 +177,15 @@ class CogVideoXAttnProcessor2_0:
 
     def attend(self, attn, x: torch.Tensor, text_len: int, image_rotary_emb=None, prev_hidden_states=None,
                prev_clip_weight=None, resample_mask=None, prev_resample_mask=None,
-               qkv: Optional[torch.Tensor] = None) -> torch.Tensor:
+               qkv: Optional[torch.Tensor] = None, lse_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """lse_out: optional fp32 [B, H, N] receiving the softmax statistics of the (single-segment, bf16) attention
+        — a training forward keeps them with the output for the backward (autograd.SAVE_ATTENTION)."""
         B, Ntok, D = x.shape
         H = attn.heads
         rope = _rope_dev(image_rotary_emb, x.device)
         fp8 = getattr(attn, "fp8_qk_exp", None)
+        if lse_out is not None and (fp8 is not None or prev_hidden_states is not None):
+            raise ValueError("lse_out: the single-segment bf16 attention only")
         fused = qkv is None and fp8 is None and _fusable_norms(attn)
         if qkv is None:  # (the block may hand over an fp8 projection)
             qkv = _qkv(attn, x, (text_len, rope) if fused else None)
@@ -202,7 +206,7 @@ class CogVideoXAttnProcessor2_0:
             K.attention(q, k, v, o, H, scale=attn.scale, out_scale=1.0 - w, bounded_scores=bs)
             K.attention(q, pk, pv, o, H, scale=attn.scale, out_scale=w, accumulate=True, bounded_scores=bs)
         else:
-            K.attention(q, k, v, o, H, scale=attn.scale, bounded_scores=bounded_scores(attn))
+            K.attention(q, k, v, o, H, scale=attn.scale, bounded_scores=bounded_scores(attn), lse=lse_out)
         return o
 
     @staticmethod

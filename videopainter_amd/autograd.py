@@ -200,9 +200,10 @@ def _put_linear_grads(G: _Grads, lin, dw: torch.Tensor) -> None:
 
 def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inject_mask: Optional[torch.Tensor],
                    dout: torch.Tensor, want_dtemb: bool, want_dinject: bool, train: bool,
-                   resample_mask: Optional[torch.Tensor] = None):
+                   resample_mask: Optional[torch.Tensor] = None, attn_saved=None):
     """Gradient-checkpointed backward of `block.forward_joint(x, T, temb, rope, resample_mask=.., inject=..,
-    inject_mask=..)`.  Returns (dx [B, Ntok, D], dtemb or None, dinject [B, Nv, D] or None, _Grads)."""
+    inject_mask=..)`.  Returns (dx [B, Ntok, D], dtemb or None, dinject [B, Nv, D] or None, _Grads).  attn_saved:
+    the forward's (attention output, lse) — then the attention is not recomputed (SAVE_ATTENTION)."""
     B, Ntok, D = x.shape
     M = B * Ntok
     a = block.attn1
@@ -251,9 +252,12 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
         katt, vatt = kn, v
     K.head_norm_rope(qkv[..., :D], qn, H, T, a.norm_q.weight, a.norm_q.bias, a.norm_q.eps, rope)
     K.head_norm_rope(qkv[..., D:2 * D], kn, H, T, a.norm_k.weight, a.norm_k.bias, a.norm_k.eps, rope)
-    o = augmented_rows((to_out,), B, Ntok, D, dev)
-    lse = torch.empty(B, H, Ntok, device=dev, dtype=F32)
-    K.attention(qn, katt, vatt, o, H, scale=a.scale, bounded_scores=bounded_scores(a), lse=lse)
+    if attn_saved is not None and not resample:
+        o, lse = attn_saved
+    else:
+        o = augmented_rows((to_out,), B, Ntok, D, dev)
+        lse = torch.empty(B, H, Ntok, device=dev, dtype=F32)
+        K.attention(qn, katt, vatt, o, H, scale=a.scale, bounded_scores=bounded_scores(a), lse=lse)
     x_mid = torch.empty_like(x)
     project_out(to_out, o.view(M, D), x_mid.view(M, D), epilogue=NAT.EPI_GATED, resid=x.view(M, D), mod=mod1,
                 gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok, text_len=T)
@@ -401,11 +405,21 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     return g, dtemb, dinj, G
 
 
+# The block forward keeps its attention output and softmax statistics for the backward (~113 MB per block at B = 1,
+# N = 17 776: 5 GB for the 44 blocks of a training step, against 288 GB of HBM), so the backward recomputes the
+# projections and norms but not the attention — the checkpointing otherwise stays as the reference's
+# --gradient_checkpointing has it.  The same kernel call produces both (bit-identical to the recompute: the fused QKV
+# epilogue equals the separate norm launches).  False: recompute the attention too.
+SAVE_ATTENTION = True
+
+
 class _BlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, block, T, rope, inject_mask, resample_mask, x, temb, inject, *params):
+        save = {} if SAVE_ATTENTION and resample_mask is None else None
         out = block.forward_joint(x, T, temb, rope, resample_mask=resample_mask, inject=inject,
-                                  inject_mask=inject_mask if inject is not None else None)
+                                  inject_mask=inject_mask if inject is not None else None, attn_save=save)
+        ctx.attn_saved = (save["o"], save["lse"]) if save else None
         ctx.block, ctx.T, ctx.rope, ctx.inject_mask, ctx.resample_mask = block, T, rope, inject_mask, resample_mask
         ctx.has_inject = inject is not None
         ctx.params = params
@@ -419,7 +433,8 @@ class _BlockFn(torch.autograd.Function):
         train = any(need[8:])
         dx, dtemb, dinj, G = block_backward(ctx.block, x, ctx.T, temb, ctx.rope,
                                             ctx.inject_mask if ctx.has_inject else None, dout, need[6],
-                                            need[7] and ctx.has_inject, train, ctx.resample_mask)
+                                            need[7] and ctx.has_inject, train, ctx.resample_mask, ctx.attn_saved)
+        ctx.attn_saved = None
         return (None, None, None, None, None, dx if need[5] else None, dtemb, dinj, *G.out(ctx.params))
 
 

@@ -255,9 +255,11 @@ class CogVideoXBlock(nn.Module):
                       resample_mask: Optional[torch.Tensor] = None, prev_joint: Optional[torch.Tensor] = None,
                       prev_clip_weight: Optional[float] = None, prev_resample_mask: Optional[torch.Tensor] = None,
                       inject: Optional[torch.Tensor] = None, inject_mask: Optional[torch.Tensor] = None,
-                      out: Optional[torch.Tensor] = None, attend=None) -> torch.Tensor:
+                      out: Optional[torch.Tensor] = None, attend=None, attn_save: Optional[dict] = None) -> torch.Tensor:
         """attend: optional replacement of the processor's attention, `attend(attn, xn, text_len, rope) -> o`
-        [B, N, D] (the Ulysses head-parallel split, videopainter_amd/ulysses.py)."""
+        [B, N, D] (the Ulysses head-parallel split, videopainter_amd/ulysses.py).  attn_save: a dict that receives the
+        attention output "o" and its softmax statistics "lse" (a training forward keeps them for the backward,
+        autograd.SAVE_ATTENTION); left empty where the attention is not the single-segment bf16 one."""
         B, Ntok, D = x.shape
         xf = x.view(B * Ntok, D)
         processor = self.attn1.processor
@@ -288,8 +290,15 @@ class CogVideoXBlock(nn.Module):
             pout = augmented_rows((a.to_k, a.to_v), prev_joint.shape[0], prev_joint.shape[1], D, x.device)
             pn = K.adaln_modulate(_bf(prev_joint), self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len,
                                   self.norm1.norm.eps, out=pout)
+        lse = None
+        if (attn_save is not None and attend is None and type(processor) is CogVideoXAttnProcessor2_0 and pn is None
+                and qkv is None and getattr(self.attn1, "fp8_qk_exp", None) is None):
+            lse = torch.empty(B, self.attn1.heads, Ntok, device=x.device, dtype=torch.float32)
         if attend is not None:
             o = attend(self.attn1, xn, text_len, rope)
+        elif lse is not None:
+            o = processor.attend(self.attn1, xn, text_len, rope, lse_out=lse)
+            attn_save["o"], attn_save["lse"] = o, lse
         else:
             o = processor.attend(self.attn1, xn if xn is not None else x, text_len, rope, pn, prev_clip_weight,
                                  resample_mask, prev_resample_mask, qkv=qkv)
