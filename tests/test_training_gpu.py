@@ -170,7 +170,8 @@ def test_block_backward_matches_oracle():
 def test_saved_attention_backward_is_bit_identical(monkeypatch, lora):
     """autograd.SAVE_ATTENTION: the block forward keeps its attention output and lse and the backward skips the
     attention recompute — the same kernel call's values the recompute would produce, so every gradient is the same
-    bits as with the recompute (also with an unfused trainable adapter on the projections)."""
+    bits as with the recompute (also with an unfused trainable adapter on the projections), up to the atomic-order
+    noise of the qk-norm affine sums."""
     from videopainter_amd import autograd as AG
     from videopainter_amd.autograd import block_apply
     tr, br, _, _ = _models()
@@ -203,7 +204,11 @@ def test_saved_attention_backward_is_bit_identical(monkeypatch, lora):
     assert torch.equal(o1, o0) and torch.equal(gx1, gx0) and torch.equal(gt1, gt0)
     assert gp1.keys() == gp0.keys() and len(gp1) > 0
     for n in gp1:
-        assert torch.equal(gp1[n], gp0[n]), n
+        if ".norm_q." in n or ".norm_k." in n:
+            # (the qk-norm affine gradients are summed with fp32 atomics across workgroups: run-to-run order noise)
+            assert rel(gp1[n].float(), gp0[n].float()) < 1e-5, n
+        else:
+            assert torch.equal(gp1[n], gp0[n]), n
 
 
 @pytest.mark.parametrize("wo_text", [False, True], ids=["text", "wo_text"])
