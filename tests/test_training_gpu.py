@@ -168,10 +168,11 @@ def test_block_backward_matches_oracle():
 
 @pytest.mark.parametrize("lora", [False, True], ids=["plain", "lora"])
 def test_saved_attention_backward_is_bit_identical(monkeypatch, lora):
-    """autograd.SAVE_ATTENTION: the block forward keeps its attention output and lse and the backward skips the
-    attention recompute — the same kernel call's values the recompute would produce, so every gradient is the same
-    bits as with the recompute (also with an unfused trainable adapter on the projections), up to the atomic-order
-    noise of the qk-norm affine sums."""
+    """autograd.SAVE_ACTIVATIONS (the training forward keeps every intermediate the backward reads) and
+    SAVE_ATTENTION (the attention output + lse only) against the full recompute: the same forward output bits (the
+    saving forward's unfused norms / separate GELU have forward_joint's rounding points) and the same gradient bits
+    (also with an unfused trainable adapter on the projections), up to the atomic-order noise of the qk-norm affine
+    sums."""
     from videopainter_amd import autograd as AG
     from videopainter_amd.autograd import block_apply
     tr, br, _, _ = _models()
@@ -190,8 +191,10 @@ def test_saved_attention_backward_is_bit_identical(monkeypatch, lora):
     temb = torch.randn(2, 32, generator=g).bfloat16()
     dout = torch.randn(2, T + 288, 128, generator=g).bfloat16()
     res = []
-    for save in (True, False):
-        monkeypatch.setattr(AG, "SAVE_ATTENTION", save)
+    # all intermediates kept (the training forward runs the backward's front) / the attention only / recompute all
+    for acts, attn in ((True, True), (False, True), (False, False)):
+        monkeypatch.setattr(AG, "SAVE_ACTIVATIONS", acts)
+        monkeypatch.setattr(AG, "SAVE_ATTENTION", attn)
         for p in blk.parameters():
             p.grad = None
         xd = x.to(dev).requires_grad_()
@@ -200,15 +203,16 @@ def test_saved_attention_backward_is_bit_identical(monkeypatch, lora):
         out.backward(dout.to(dev))
         res.append((out.detach(), xd.grad, td.grad,
                     {n: p.grad.clone() for n, p in blk.named_parameters() if p.grad is not None}))
-    (o1, gx1, gt1, gp1), (o0, gx0, gt0, gp0) = res
-    assert torch.equal(o1, o0) and torch.equal(gx1, gx0) and torch.equal(gt1, gt0)
-    assert gp1.keys() == gp0.keys() and len(gp1) > 0
-    for n in gp1:
-        if ".norm_q." in n or ".norm_k." in n:
-            # (the qk-norm affine gradients are summed with fp32 atomics across workgroups: run-to-run order noise)
-            assert rel(gp1[n].float(), gp0[n].float()) < 1e-5, n
-        else:
-            assert torch.equal(gp1[n], gp0[n]), n
+    o0, gx0, gt0, gp0 = res[-1]
+    for o1, gx1, gt1, gp1 in res[:-1]:
+        assert torch.equal(o1, o0) and torch.equal(gx1, gx0) and torch.equal(gt1, gt0)
+        assert gp1.keys() == gp0.keys() and len(gp1) > 0
+        for n in gp1:
+            if ".norm_q." in n or ".norm_k." in n:
+                # (the qk-norm affine gradients are summed with fp32 atomics across workgroups: run-to-run noise)
+                assert rel(gp1[n].float(), gp0[n].float()) < 1e-5, n
+            else:
+                assert torch.equal(gp1[n], gp0[n]), n
 
 
 @pytest.mark.parametrize("wo_text", [False, True], ids=["text", "wo_text"])

@@ -198,25 +198,18 @@ def _put_linear_grads(G: _Grads, lin, dw: torch.Tensor) -> None:
     G.put(lin.weight, dw)
 
 
-def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inject_mask: Optional[torch.Tensor],
-                   dout: torch.Tensor, want_dtemb: bool, want_dinject: bool, train: bool,
-                   resample_mask: Optional[torch.Tensor] = None, attn_saved=None):
-    """Gradient-checkpointed backward of `block.forward_joint(x, T, temb, rope, resample_mask=.., inject=..,
-    inject_mask=..)`.  Returns (dx [B, Ntok, D], dtemb or None, dinject [B, Nv, D] or None, _Grads).  attn_saved:
-    the forward's (attention output, lse) — then the attention is not recomputed (SAVE_ATTENTION)."""
+def _block_front(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, resample_mask, attn_saved=None) -> dict:
+    """forward_joint's launches up to the FF1 pre-activation, with its rounding points (the fused QKV + qk-norm
+    epilogue is bit-exact to the separate launches used here, tests/test_model_gpu.py), keeping what the backward
+    reads: the recompute of the checkpointed backward, and the front of the training forward (block_forward_saving)."""
     B, Ntok, D = x.shape
     M = B * Ntok
     a = block.attn1
     H = a.heads
     n1, n2 = block.norm1, block.norm2
-    ff0, ff2, to_out = block.ff.net[0].proj, block.ff.net[2], a.to_out[0]
+    ff0, to_out = block.ff.net[0].proj, block.attn1.to_out[0]
     F4 = ff0.weight.shape[0]
     dev = x.device
-    need_dmod = train or want_dtemb
-    G = _Grads()
-
-    # ---- recompute (forward_joint's launches and rounding points; the fused QKV + qk-norm epilogue is bit-exact
-    # to the separate launches used here, tests/test_model_gpu.py) ----
     mod1 = n1.modulation(temb)
     mod2 = n2.modulation(temb)
     # trainable LoRA factors run unfused: the projections on K-augmented operands (lora.AugmentedProjection),
@@ -265,6 +258,86 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     z = torch.empty(M, F4, device=dev, dtype=BF16)
     K.gemm(xn2.view(M, D), [ff0.weight], [ff0.bias], z)
 
+    st = dict(mod1=mod1, mod2=mod2, xn=xn, xq=xq, qkv=qkv, o=o, lse=lse, x_mid=x_mid, xn2=xn2, z=z)
+    if resample:
+        st.update(qn=qn, kc=kc, vc=vc)
+    else:
+        st["qk"] = qk
+    return st
+
+
+def block_forward_saving(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inject=None, inject_mask=None,
+                         keep_train: bool = False):
+    """The block's forward for a training step, keeping its intermediates for the backward (SAVE_ACTIVATIONS): the
+    launches of _block_front (unfused QKV norms, FF1 without its GELU epilogue), then h = GELU(z) by vp_gelu_bf16 (the
+    same rounding points as the fused epilogue: bf16(acc + b), then GELU-tanh, then bf16) and FF2 with the gated
+    residual + injection exactly as forward_joint: the same output bits.  Kept: mod1 / mod2, the pre-norm q | k | v,
+    the attention output + lse, x_mid, z (and, for a block with trainable parameters or a temb that needs its
+    gradient, the AdaLN outputs and h); the normed q | k are recomputed by the backward (two cheap launches)."""
+    B, Ntok, D = x.shape
+    M = B * Ntok
+    ff2 = block.ff.net[2]
+    st = _block_front(block, x, T, temb, rope, None)
+    h = K.gelu(st["z"])
+    out = torch.empty_like(x)
+    kw = {}
+    if inject is not None:
+        kw = dict(inject=inject, inject_ld=inject.stride(1), inject_bstride=inject.stride(0), inject_mask=inject_mask)
+    K.gemm(h.view(M, -1), [ff2.weight], [ff2.bias], out.view(M, D), epilogue=NAT.EPI_GATED,
+           resid=st["x_mid"].view(M, D), mod=st["mod2"], gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok,
+           text_len=T, **kw)
+    del st["qk"]
+    if keep_train:
+        st["h"] = h
+    else:
+        del h
+        for k in ("xn", "xq", "xn2"):
+            st.pop(k)
+    return out, st
+
+
+def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inject_mask: Optional[torch.Tensor],
+                   dout: torch.Tensor, want_dtemb: bool, want_dinject: bool, train: bool,
+                   resample_mask: Optional[torch.Tensor] = None, attn_saved=None, front: Optional[dict] = None):
+    """Gradient-checkpointed backward of `block.forward_joint(x, T, temb, rope, resample_mask=.., inject=..,
+    inject_mask=..)`.  Returns (dx [B, Ntok, D], dtemb or None, dinject [B, Nv, D] or None, _Grads).  attn_saved:
+    the forward's (attention output, lse) — then the attention is not recomputed (SAVE_ATTENTION); front: the
+    training forward's kept intermediates (block_forward_saving) — then nothing is recomputed."""
+    B, Ntok, D = x.shape
+    M = B * Ntok
+    a = block.attn1
+    H = a.heads
+    n1, n2 = block.norm1, block.norm2
+    ff0, ff2, to_out = block.ff.net[0].proj, block.ff.net[2], a.to_out[0]
+    F4 = ff0.weight.shape[0]
+    dev = x.device
+    need_dmod = train or want_dtemb
+    G = _Grads()
+
+    # ---- the forward's intermediates: kept by the training forward (SAVE_ACTIVATIONS = "all", block_forward_saving)
+    # or recomputed here with forward_joint's launches and rounding points ----
+    if front is None:
+        front = _block_front(block, x, T, temb, rope, resample_mask, attn_saved)
+    f = front
+    mod1, mod2, qkv, o, lse, x_mid, z = (f.pop(k) for k in ("mod1", "mod2", "qkv", "o", "lse", "x_mid", "z"))
+    xn, xq, xn2, h_saved = f.pop("xn", None), f.pop("xq", None), f.pop("xn2", None), f.pop("h", None)
+    qaug = AugmentedProjection.of((a.to_q, a.to_k, a.to_v))
+    oaug = AugmentedProjection.of((to_out,))
+    resample = resample_mask is not None
+    v = qkv[..., 2 * D:]
+    kc = vc = qk = None
+    if resample:
+        qn, kc, vc = f.pop("qn"), f.pop("kc"), f.pop("vc")
+    elif "qk" in f:
+        qk = f.pop("qk")
+        qn, kn = qk[..., :D], qk[..., D:]
+    else:  # (the training forward keeps the pre-norm q | k | v only: the two norm launches again)
+        qk = torch.empty(B, Ntok, 2 * D, device=dev, dtype=BF16)
+        qn, kn = qk[..., :D], qk[..., D:]
+        K.head_norm_rope(qkv[..., :D], qn, H, T, a.norm_q.weight, a.norm_q.bias, a.norm_q.eps, rope)
+        K.head_norm_rope(qkv[..., D:2 * D], kn, H, T, a.norm_k.weight, a.norm_k.bias, a.norm_k.eps, rope)
+    del front, f
+
     dout = dout.contiguous()
     dout2 = dout.view(M, D)
     dinj = None
@@ -292,7 +365,7 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     if need_dmod:
         # h exactly as the forward made it: GELU applied in the FF1 GEMM epilogue on the fp32 accumulator (a GELU
         # of the bf16-rounded z would differ by one rounding, and so would ff2's weight and gate-2 gradients)
-        h = K.linear(xn2.view(M, D), ff0.weight, ff0.bias, gelu=True)
+        h = h_saved if h_saved is not None else K.linear(xn2.view(M, D), ff0.weight, ff0.bias, gelu=True)
         f = torch.empty(M, D, device=dev, dtype=BF16)
         K.gemm(h, [ff2.weight], [ff2.bias], f)
         dmod2 = _mod_grad(K.colsum(dxn2.view(M, D), tokens_per_batch=Ntok, text_len=T),
@@ -307,7 +380,7 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
             G.put(n2.norm.weight, _total(dn2.view(M, D), xh2.view(M, D)))
             G.put(n2.norm.bias, _total(dn2.view(M, D)))
         del h
-    del z, dz, df, xn2, n2o, dn2, xh2, dxn2
+    del z, dz, df, xn2, n2o, dn2, xh2, dxn2, h_saved
 
     # ---- attention + gated residual 1 ----
     dao = torch.empty(M, D, device=dev, dtype=BF16)
@@ -411,15 +484,35 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
 # --gradient_checkpointing has it.  The same kernel call produces both (bit-identical to the recompute: the fused QKV
 # epilogue equals the separate norm launches).  False: recompute the attention too.
 SAVE_ATTENTION = True
+# Beyond that, while the device has room (SAVE_ACTIVATIONS = True; the budget below), the training forward runs the
+# backward's front itself (block_forward_saving) and keeps every intermediate the backward reads, so the backward
+# recomputes nothing: ~1 GB per frozen 5b block at B = 1, N = 17 776 (q | k | v, O, x_mid, the FF1 pre-activation z).
+# A block whose kept set would leave less than SAVE_RESERVE_BYTES free (or four times its own size) falls back to
+# the attention-only form, so a larger batch degrades to recompute instead of running out of memory.
+SAVE_ACTIVATIONS = True
+SAVE_RESERVE_BYTES = 16 << 30
+
+
+def _room_for(x: torch.Tensor, F4: int) -> bool:
+    B, Ntok, D = x.shape
+    need = B * Ntok * (3 * D + D + D + F4) * 2  # q | k | v, O, x_mid, z (bf16)
+    free, _ = torch.cuda.mem_get_info(x.device)
+    return free - need > max(SAVE_RESERVE_BYTES, 4 * need)
 
 
 class _BlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, block, T, rope, inject_mask, resample_mask, x, temb, inject, *params):
-        save = {} if SAVE_ATTENTION and resample_mask is None else None
-        out = block.forward_joint(x, T, temb, rope, resample_mask=resample_mask, inject=inject,
-                                  inject_mask=inject_mask if inject is not None else None, attn_save=save)
-        ctx.attn_saved = (save["o"], save["lse"]) if save else None
+        ctx.front = ctx.attn_saved = None
+        if SAVE_ACTIVATIONS and resample_mask is None and _room_for(x, block.ff.net[0].proj.weight.shape[0]):
+            keep_train = any(p.requires_grad for p in params) or temb.requires_grad
+            out, ctx.front = block_forward_saving(block, x, T, temb, rope, inject,
+                                                  inject_mask if inject is not None else None, keep_train)
+        else:
+            save = {} if SAVE_ATTENTION and resample_mask is None else None
+            out = block.forward_joint(x, T, temb, rope, resample_mask=resample_mask, inject=inject,
+                                      inject_mask=inject_mask if inject is not None else None, attn_save=save)
+            ctx.attn_saved = (save["o"], save["lse"]) if save else None
         ctx.block, ctx.T, ctx.rope, ctx.inject_mask, ctx.resample_mask = block, T, rope, inject_mask, resample_mask
         ctx.has_inject = inject is not None
         ctx.params = params
@@ -431,10 +524,11 @@ class _BlockFn(torch.autograd.Function):
         x, temb = ctx.saved_tensors
         need = ctx.needs_input_grad
         train = any(need[8:])
+        front, ctx.front = ctx.front, None  # (the backward pops it: each intermediate is freed as it is used)
+        attn_saved, ctx.attn_saved = ctx.attn_saved, None
         dx, dtemb, dinj, G = block_backward(ctx.block, x, ctx.T, temb, ctx.rope,
                                             ctx.inject_mask if ctx.has_inject else None, dout, need[6],
-                                            need[7] and ctx.has_inject, train, ctx.resample_mask, ctx.attn_saved)
-        ctx.attn_saved = None
+                                            need[7] and ctx.has_inject, train, ctx.resample_mask, attn_saved, front)
         return (None, None, None, None, None, dx if need[5] else None, dtemb, dinj, *G.out(ctx.params))
 
 
