@@ -17,7 +17,8 @@ import pytest  # noqa: E402
 class KnobPatch:
     """monkeypatch's setenv / delenv for the switches the tests flip between launches: the library's A/B knobs go
     through vp_set_knob (the library reads the environment once, at load), the Python-side switches (e.g.
-    VP_NO_QKV_FUSION) through the environment; everything is restored at teardown."""
+    VP_NO_QKV_FUSION, read once at import) through attention_processor.set_switch; everything is restored at
+    teardown."""
 
     def __init__(self, mp):
         self.mp = mp
@@ -25,9 +26,12 @@ class KnobPatch:
 
     def _lib(self, name, value):
         from videopainter_amd import _native as N
+        from videopainter_amd import attention_processor as AP
         from videopainter_amd import kernels as K
         if name in N.KNOBS:
             self.saved.append((name, K.set_knob(name, value)))
+        elif name in AP.SWITCHES:
+            self.saved.append((name, AP.set_switch(name, value)))
 
     def setenv(self, name, value):
         self.mp.setenv(name, value)
@@ -41,9 +45,13 @@ class KnobPatch:
         return getattr(self.mp, attr)
 
     def undo(self):
+        from videopainter_amd import attention_processor as AP
         from videopainter_amd import kernels as K
         for name, prev in reversed(self.saved):
-            K.set_knob(name, prev)
+            if name in AP.SWITCHES:
+                AP.set_switch(name, prev)
+            else:
+                K.set_knob(name, prev)
         self.saved.clear()
 
 

@@ -27,6 +27,27 @@ from .modules import Dropout, LayerNorm, Linear
 BF16 = torch.bfloat16
 
 
+# Python-side A/B switches, read from the environment once at import (as the library's knob table is at load) and
+# changed only through set_switch (tests/conftest.py `knobs`): VP_NO_QKV_FUSION=1 (separate qk-norm launches),
+# VP_ATTN_BOUNDED=0 (no score-bound flag), VP_RESAMPLE_PARTITION / _NULLMASS / _K2_STRIDED=0 (resample-processor forms)
+SWITCHES = {k: os.environ.get(k) for k in ("VP_NO_QKV_FUSION", "VP_ATTN_BOUNDED", "VP_RESAMPLE_PARTITION",
+                                           "VP_RESAMPLE_NULLMASS", "VP_RESAMPLE_K2_STRIDED")}
+
+
+def set_switch(name: str, value: Optional[str]) -> Optional[str]:
+    """Set (value None: unset) one of SWITCHES; returns the previous value."""
+    if name not in SWITCHES:
+        raise KeyError(f"unknown switch {name}")
+    prev = SWITCHES[name]
+    SWITCHES[name] = value
+    return prev
+
+
+def _sw(name: str, default: str) -> str:
+    v = SWITCHES[name]
+    return default if v is None else v
+
+
 class RopeTables(tuple):
     """(cos, sin) fp32 [F*Hh*Ww, 64] on the device, plus the video grid (F, Hh, Ww) they were built for when the
     transformer's forward knows it (None otherwise): the resample processor needs the grid to sum its null keys in
@@ -147,7 +168,7 @@ def project_out(lin, o2d: torch.Tensor, out2d: torch.Tensor, **gemm_kw) -> torch
 def _fusable_norms(attn) -> bool:
     """norm_q / norm_k are LayerNorm(64) with bf16 affine parameters (CogVideoX's qk_norm, the fused epilogue's
     contract); env VP_NO_QKV_FUSION=1 keeps the separate vp_head_norm_rope_bf16 launches (A/B)."""
-    if os.environ.get("VP_NO_QKV_FUSION", "0") == "1":
+    if _sw("VP_NO_QKV_FUSION", "0") == "1":
         return False
     for ln in (getattr(attn, "norm_q", None), getattr(attn, "norm_k", None)):
         if ln is None or getattr(ln, "weight", None) is None or getattr(ln, "bias", None) is None:
@@ -161,7 +182,7 @@ def bounded_scores(attn) -> bool:
     """True when the qk-LayerNorm weights bound every attention score of `attn` within the kernel's exact
     no-running-max range (kernels.score_bound_log2 <= SCORE_BOUND_LOG2).  Cached per layer on the weights' storage and
     version (one host sync per weight update); env VP_ATTN_BOUNDED=0 forces the running-max kernel (A/B)."""
-    if os.environ.get("VP_ATTN_BOUNDED", "1") == "0":
+    if _sw("VP_ATTN_BOUNDED", "1") == "0":
         return False
     nq, nk = attn.norm_q, attn.norm_k
     key = tuple((t.data_ptr(), t._version) for t in (nq.weight, nq.bias, nk.weight, nk.bias)) + (float(attn.scale),)
@@ -324,8 +345,8 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
         # (k2_full).  Env VP_RESAMPLE_NULLMASS=0: keep them as keys; VP_RESAMPLE_PARTITION=0: original order (A/B).
         dst = cnt = segments = axes = None
         grid = getattr(rope, "grid", None)
-        if os.environ.get("VP_RESAMPLE_PARTITION", "1") != "0":
-            if (grid is not None and os.environ.get("VP_RESAMPLE_NULLMASS", "1") != "0"
+        if _sw("VP_RESAMPLE_PARTITION", "1") != "0":
+            if (grid is not None and _sw("VP_RESAMPLE_NULLMASS", "1") != "0"
                     and attn.norm_k.bias is not None and attn.norm_k.bias.dtype == BF16
                     and K.null_key_mass_supported(grid)):
                 axes = K.rope_axis_tables(rope, grid)
@@ -339,7 +360,7 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
         # segment 2 with the row stride of the fused QKV output (3 D): the attention kernel then streams its full tiles
         # on the same precomputed lane offsets as segment 1
         # (VP_RESAMPLE_K2_STRIDED=0: contiguous k2 / v2, the general per-lane DMA path; A/B)
-        if os.environ.get("VP_RESAMPLE_K2_STRIDED", "1") != "0":
+        if _sw("VP_RESAMPLE_K2_STRIDED", "1") != "0":
             kv2 = torch.empty(B, Ntok, 3 * D, device=x.device, dtype=BF16)
             k2, v2 = kv2[..., :D], kv2[..., D:2 * D]
         else:
