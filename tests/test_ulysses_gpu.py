@@ -92,3 +92,52 @@ def test_ulysses_harness_call_forms(env):
 
     for pred, hsl, rm in comm.run(rank_fn):
         assert rel(pred, env["ref"]) < 1e-3 and len(hsl) == 3 and rm.shape == (2, env["hs"][0].shape[1])
+
+
+@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("resample", [True, False], ids=["resample", "standard"])
+def test_ulysses_any_length_window_handoff(env, P, resample):
+    """The any-length pipeline's processors under the split (anyl.py:962-988): window 0 and a later window that
+    gets window 0's hidden states (the split's own shard states), prev_clip_weight 0.5 and the previous resample
+    mask — the ID-resample processor (masked second K / V segment, null keys in closed form) and the standard one
+    (the previous-clip blend) — against the unsplit forward of the same model."""
+    from videopainter_amd import CogVideoXTransformer3DModel, device_scope
+    from videopainter_amd import ulysses as U
+    from tests.golden.cases import TINY_CFG
+    i = env["inp"]
+    g = torch.Generator().manual_seed(21)
+    hidden2 = (i["hidden"].float().cpu() + 0.5 * torch.randn(i["hidden"].shape, generator=g)).to(dev).bfloat16()
+    if resample:
+        cfg = dict(TINY_CFG, num_attention_heads=4, max_text_seq_length=10, num_layers=3,
+                   id_pool_resample_learnable=True)
+        with device_scope(dev):
+            tr = CogVideoXTransformer3DModel(**cfg)
+        tr.init_synthetic_weights_(11)
+    else:
+        tr = env["tr"]
+    bs = env["bs"]
+    kw = dict(encoder_hidden_states=i["enc"], timestep=i["ts"], image_rotary_emb=i["rope"], branch_block_samples=bs,
+              branch_block_masks=i["mask"], id_pool_resample_learnable=resample, return_dict=False)
+    with torch.no_grad():
+        ref0, hs0, rm0 = tr(hidden_states=i["hidden"], return_hidden_states=True, return_resample_mask=True, **kw)
+        ref1 = tr(hidden_states=hidden2, attention_kwargs={"prev_hidden_states": dict(enumerate(hs0)),
+                                                           "prev_clip_weight": 0.5, "prev_resample_mask": rm0},
+                  **kw)[0]
+    comm = U.ThreadComm(P)
+
+    def rank_fn(r):
+        samples = U.branch_forward(env["br"], comm, r, i["video"], i["enc"], i["cond"], i["ts"], i["rope"])
+        out0, hsl = U.transformer_forward(tr, comm, r, i["hidden"], i["enc"], i["ts"], i["rope"], samples, i["mask"],
+                                          return_hidden_states=True, id_pool_resample_learnable=resample)
+        out1 = U.transformer_forward(tr, comm, r, hidden2, i["enc"], i["ts"], i["rope"], samples, i["mask"],
+                                     id_pool_resample_learnable=resample, prev_hidden_states=dict(enumerate(hsl)),
+                                     prev_clip_weight=0.5, prev_resample_mask=rm0)[0]
+        return out0, out1
+
+    for r, (out0, out1) in enumerate(comm.run(rank_fn)):
+        r0, r1 = rel(out0, ref0), rel(out1, ref1)
+        print(f"P={P} {'resample' if resample else 'standard'} rank {r}: window 0 rel {r0:.2e}, window 1 rel {r1:.2e}")
+        assert out0.shape == ref0.shape and out1.shape == ref1.shape
+        assert r0 < 1e-3 and r1 < 1e-3, (r, r0, r1)
+    if resample:
+        del tr

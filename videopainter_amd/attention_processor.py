@@ -331,18 +331,34 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
                prev_clip_weight=None, resample_mask=None, prev_resample_mask=None,
                qkv: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, Ntok, D = x.shape
-        H = attn.heads
         rope = _rope_dev(image_rotary_emb, x.device)
         prev = prev_hidden_states is not None and prev_clip_weight is not None and prev_clip_weight > 0.0
         if not prev and resample_mask is None:
             raise ValueError("the resample processor needs resample_mask (id_pool_resample needs masks)")
         m = _u8(prev_resample_mask if prev else resample_mask)
-        # The second segment in partitioned row order: the masked rows' keys / values first, then the null keys (LN
-        # of a zeroed row = the norm_k bias, rotated) whose values are zero — they only add to the row sums.  The
-        # order of keys does not change attention.  With the video grid known and the RoPE table separable, the
-        # null keys leave the segment (k2_len = the masked-row count) and their row mass is summed in closed form
-        # over the grid (null_key_mass -> l_extra); otherwise they stay as row-sum-only keys
-        # (k2_full).  Env VP_RESAMPLE_NULLMASS=0: keep them as keys; VP_RESAMPLE_PARTITION=0: original order (A/B).
+        plan = self.plan(attn, m, text_len, rope)
+        # with the null keys in closed form segment 2 holds masked rows only, and those of window 0 are rows of the
+        # normed + rotated K itself: q / k then leave the QKV GEMM through the fused norm + RoPE epilogue
+        fused = plan[3] is not None and qkv is None and _fusable_norms(attn)
+        if qkv is None:  # (the block may hand over an fp8 projection)
+            qkv = _qkv(attn, x, (text_len, rope) if fused else None)
+        pk = pv = None
+        if prev:
+            pkv = _kv(attn, _rows(prev_hidden_states))
+            pk, pv = pkv[..., :D], pkv[..., D:]
+        o = augmented_rows((attn.to_out[0],), B, Ntok, D, x.device)
+        return self.attend_heads(attn, qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:], text_len, rope, m, plan,
+                                 fused, pk, pv, float(prev_clip_weight) if prev else 0.0, o)
+
+    @staticmethod
+    def plan(attn, m: torch.Tensor, text_len: int, rope):
+        """(dst_rows, counts, segments, axes) of the token mask m [B, N] (uint8).  The second segment in partitioned
+        row order: the masked rows' keys / values first, then the null keys (LN of a zeroed row = the norm_k bias,
+        rotated) whose values are zero — they only add to the row sums.  The order of keys does not change
+        attention.  With the video grid known and the RoPE table separable, the null keys leave the segment (k2_len
+        = the masked-row count) and their row mass is summed in closed form over the grid (null_key_mass ->
+        l_extra; axes = the per-axis RoPE tables); otherwise they stay as row-sum-only keys
+        (k2_full).  VP_RESAMPLE_NULLMASS=0: keep them as keys; VP_RESAMPLE_PARTITION=0: original order (A/B)."""
         dst = cnt = segments = axes = None
         grid = getattr(rope, "grid", None)
         if _sw("VP_RESAMPLE_PARTITION", "1") != "0":
@@ -351,27 +367,30 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
                     and K.null_key_mass_supported(grid)):
                 axes = K.rope_axis_tables(rope, grid)
             dst, cnt, segments = _mask_plan(m, text_len, grid if axes is not None else None)
-        # with the null keys in closed form segment 2 holds masked rows only, and those of window 0 are rows of the
-        # normed + rotated K itself: q / k then leave the QKV GEMM through the fused norm + RoPE epilogue
-        fused = axes is not None and qkv is None and _fusable_norms(attn)
-        if qkv is None:  # (the block may hand over an fp8 projection)
-            qkv = _qkv(attn, x, (text_len, rope) if fused else None)
-        q, k, v = qkv[..., :D], qkv[..., D:2 * D], qkv[..., 2 * D:]
+        return dst, cnt, segments, axes
+
+    def attend_heads(self, attn, q, k, v, text_len: int, rope, m, plan, fused: bool, pk=None, pv=None,
+                     w: float = 0.0, o=None) -> torch.Tensor:
+        """The processor's attention on [B, N, h*64] views of every head (or of one head group: the Ulysses split,
+        videopainter_amd/ulysses.py) — q / k normed + rotated already when `fused`, pre-norm otherwise; pk / pv: the
+        previous window's pre-norm K / V projections (prev-clip blend with weight w), or None."""
+        B, Ntok, D = q.shape
+        H = D // 64
+        dst, cnt, segments, axes = plan
+        grid = getattr(rope, "grid", None)
         # segment 2 with the row stride of the fused QKV output (3 D): the attention kernel then streams its full tiles
         # on the same precomputed lane offsets as segment 1 (DESIGN.md §3.R4)
         # (VP_RESAMPLE_K2_STRIDED=0: contiguous k2 / v2, the general per-lane DMA path; A/B)
         if _sw("VP_RESAMPLE_K2_STRIDED", "1") != "0":
-            kv2 = torch.empty(B, Ntok, 3 * D, device=x.device, dtype=BF16)
+            kv2 = torch.empty(B, Ntok, 3 * D, device=q.device, dtype=BF16)
             k2, v2 = kv2[..., :D], kv2[..., D:2 * D]
         else:
-            k2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
-            v2 = torch.empty(B, Ntok, D, device=x.device, dtype=BF16)
-        if prev:
-            pkv = _kv(attn, _rows(prev_hidden_states))
-            w = float(prev_clip_weight)
-            K.head_norm_rope(pkv[..., :D], k2, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps,
+            k2 = torch.empty(B, Ntok, D, device=q.device, dtype=BF16)
+            v2 = torch.empty(B, Ntok, D, device=q.device, dtype=BF16)
+        if pk is not None:
+            K.head_norm_rope(pk, k2, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps,
                              rope, tok_mask=m, pre_scale=w, dst_rows=dst)
-            K.mask_scale_rows(pkv[..., D:], v2, m, w, dst_rows=dst)
+            K.mask_scale_rows(pv, v2, m, w, dst_rows=dst)
         elif fused:  # LN(1 . k) + RoPE of a masked row is K's row (bit-equal: the epilogue's arithmetic)
             K.mask_scale_rows(k, k2, m, 1.0, dst_rows=dst)
             K.mask_scale_rows(v, v2, m, 1.0, dst_rows=dst)
@@ -382,7 +401,8 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
         if not fused:
             K.head_norm_rope(q, q, H, text_len, attn.norm_q.weight, attn.norm_q.bias, attn.norm_q.eps, rope)
             K.head_norm_rope(k, k, H, text_len, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps, rope)
-        o = augmented_rows((attn.to_out[0],), B, Ntok, D, x.device)
+        if o is None:
+            o = torch.empty(B, Ntok, D, device=q.device, dtype=BF16)
         if axes is not None:
             lx = K.null_key_mass(q, H, text_len, grid, attn.norm_k.bias, axes, m, segments, attn.scale)
             K.attention(q, k, v, o, H, k2=k2, v2=v2, scale=attn.scale, bounded_scores=bounded_scores(attn),

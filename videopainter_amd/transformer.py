@@ -267,8 +267,8 @@ class CogVideoXBlock(nn.Module):
             raise ValueError(f"Unsupported processor type: {type(processor)}")
         mod1 = self.norm1.modulation(temb)
         qkv = None
-        if attend is not None and (self.qkv_mx is not None or prev_joint is not None):
-            raise NotImplementedError("the head-parallel split runs the bf16 standard processor only")
+        if attend is not None and self.qkv_mx is not None:
+            raise NotImplementedError("the head-parallel split runs the bf16 path")
         if self.qkv_mx is not None:
             a = self.attn1
             xq = K.adaln_modulate_mx(x, self.norm1.norm.weight, self.norm1.norm.bias, mod1, text_len,
@@ -295,7 +295,7 @@ class CogVideoXBlock(nn.Module):
                 and qkv is None and getattr(self.attn1, "fp8_qk_exp", None) is None):
             lse = torch.empty(B, self.attn1.heads, Ntok, device=x.device, dtype=torch.float32)
         if attend is not None:
-            o = attend(self.attn1, xn, text_len, rope)
+            o = attend(self.attn1, xn, text_len, rope, pn, prev_clip_weight, resample_mask, prev_resample_mask)
         elif lse is not None:
             o = processor.attend(self.attn1, xn, text_len, rope, lse_out=lse)
             attn_save["o"], attn_save["lse"] = o, lse

@@ -20,8 +20,10 @@ Communicators: `DistComm` (torch.distributed; backend "nccl" = RCCL over xGMI) a
 ranks as P threads of one process on one GPU (same launches in the same order per rank; the exchanges are local
 copies) — the single-GPU rehearsal the GPU tests use to check the split against the unsplit forward.
 
-Scope: the standard processor in bf16 (config 2, the headline).  The ID-resample processor, the previous-clip blend
-and the fp8 modes raise NotImplementedError under the split.
+Scope: the bf16 path with both processors of the any-length pipeline — the standard one (config 2, the headline;
+with the previous-clip blend) and the ID-resample one (config 4: window 0's masked second K / V segment, later
+windows' masked previous-window K / V): the projections stay row-local, the masks and the RoPE table of the
+head-group attention are the full ones.  The fp8 modes raise NotImplementedError under the split.
 """
 from __future__ import annotations
 
@@ -35,7 +37,8 @@ import torch.distributed as dist
 
 from . import _native as NAT
 from . import kernels as K
-from .attention_processor import _qkv, _fusable_norms, _rope_dev, bounded_scores
+from .attention_processor import (CogVideoXAttnProcessor2_0, CogVideoXAttnProcessor2_0_resample, _fusable_norms,
+                                  _kv, _qkv, _rope_dev, _u8, bounded_scores)
 from .transformer import BF16, Transformer2DModelOutput, _bf
 
 # ------------------------------------------------------------------------------------------------------------------
@@ -160,11 +163,21 @@ class Shard:
 
 
 class _Ctx:
-    def __init__(self, comm, rank: int, shard: Shard):
-        self.comm, self.rank, self.sh = comm, rank, shard
+    """One rank's attention of the split forward.  rope_full: the whole RoPE table (with its grid) for the head-group
+    rows; mask / prev_mask: the resample processor's full token masks [B, N] (this window's, the previous one's)."""
 
-    def attend(self, attn, xn: torch.Tensor, text_len: int, rope) -> torch.Tensor:
-        """Head-parallel attention of the shard's rows (CogVideoXAttnProcessor2_0 semantics)."""
+    def __init__(self, comm, rank: int, shard: Shard, rope_full=None, mask=None, prev_mask=None):
+        self.comm, self.rank, self.sh = comm, rank, shard
+        self.rope_full, self.mask, self.prev_mask = rope_full, mask, prev_mask
+
+    def attend(self, attn, xn: torch.Tensor, text_len: int, rope, pn: Optional[torch.Tensor] = None,
+               prev_clip_weight=None, resample_mask=None, prev_resample_mask=None) -> torch.Tensor:
+        """Head-parallel attention of the shard's rows with the semantics of the block's processor:
+        CogVideoXAttnProcessor2_0 (with the previous-clip blend when pn, the previous window's normed shard rows,
+        is given) or CogVideoXAttnProcessor2_0_resample (window 0's masked second segment, or the previous window's
+        masked K / V).  The row-local projections run on the shard; the masks and the RoPE table of the head-group
+        attention are the full ones of the context (resample_mask / prev_resample_mask, the shard-level arguments
+        of forward_joint, are not used)."""
         B, n, D = xn.shape
         P = self.comm.P
         H = attn.heads
@@ -172,30 +185,59 @@ class _Ctx:
             raise ValueError(f"{H} heads do not split {P} ways")
         Hp = H // P
         Dp = Hp * 64
-        qkv = _qkv(attn, xn, (text_len, rope) if _fusable_norms(attn) else None)
-        if not _fusable_norms(attn):
+        N, T = self.sh.N, self.sh.T
+        prev = pn is not None and prev_clip_weight is not None and prev_clip_weight > 0.0
+        resample = isinstance(attn.processor, CogVideoXAttnProcessor2_0_resample)
+        m = plan = None
+        if resample:
+            m = _u8(self.prev_mask if prev else self.mask)
+            if m is None:
+                raise ValueError("the resample processor needs resample_mask (id_pool_resample needs masks)")
+            plan = attn.processor.plan(attn, m, T, self.rope_full)
+            fused = plan[3] is not None and _fusable_norms(attn)
+        else:
+            fused = _fusable_norms(attn)
+        qkv = _qkv(attn, xn, (text_len, rope) if fused else None)
+        if not fused and not resample:
             K.head_norm_rope(qkv[..., :D], qkv[..., :D], H, text_len, attn.norm_q.weight, attn.norm_q.bias,
                              attn.norm_q.eps, rope)
             K.head_norm_rope(qkv[..., D:2 * D], qkv[..., D:2 * D], H, text_len, attn.norm_k.weight, attn.norm_k.bias,
                              attn.norm_k.eps, rope)
         full = qkv_to_heads(self.comm, self.rank, qkv)
         del qkv
-        N = self.sh.N
-        q, k, v = full[..., :Dp], full[:, :N, Dp:2 * Dp], full[:, :N, 2 * Dp:]
-        o_full = torch.empty(B, P * n, Dp, device=xn.device, dtype=BF16)
-        K.attention(q, k, v, o_full, Hp, scale=attn.scale, bounded_scores=bounded_scores(attn))
+        pk = pv = None
+        if prev:  # the previous window's K / V of this shard's rows (pre-norm) -> every row of the head group
+            pkv = qkv_to_heads(self.comm, self.rank, _kv(attn, pn), parts=2)
+            pk, pv = pkv[:, :N, :Dp], pkv[:, :N, Dp:]
+        o_full = torch.zeros(B, P * n, Dp, device=xn.device, dtype=BF16)
+        if resample:
+            q, k, v = full[:, :N, :Dp], full[:, :N, Dp:2 * Dp], full[:, :N, 2 * Dp:]
+            attn.processor.attend_heads(attn, q, k, v, T, self.rope_full, m, plan, fused, pk, pv,
+                                        float(prev_clip_weight) if prev else 0.0, o_full[:, :N])
+        else:
+            q, k, v = full[..., :Dp], full[:, :N, Dp:2 * Dp], full[:, :N, 2 * Dp:]
+            bs = bounded_scores(attn)
+            if prev:  # (attention_processor.py:2156-2189: (1 - w) self + w previous clip, one blended output)
+                w = float(prev_clip_weight)
+                K.head_norm_rope(pk, pk, Hp, T, attn.norm_k.weight, attn.norm_k.bias, attn.norm_k.eps,
+                                 self.rope_full)
+                K.attention(q, k, v, o_full, Hp, scale=attn.scale, out_scale=1.0 - w, bounded_scores=bs)
+                K.attention(q, pk, pv, o_full, Hp, scale=attn.scale, out_scale=w, accumulate=True, bounded_scores=bs)
+            else:
+                K.attention(q, k, v, o_full, Hp, scale=attn.scale, bounded_scores=bs)
         del full
         return heads_to_rows(self.comm, self.rank, o_full)
 
 
-def qkv_to_heads(comm, rank: int, qkv: torch.Tensor) -> torch.Tensor:
-    """This shard's rows of q|k|v [B, n, 3D] -> every row of head group `rank`: [B, P n, 3 Dp] (q|k|v)."""
-    B, n, D3 = qkv.shape
+def qkv_to_heads(comm, rank: int, qkv: torch.Tensor, parts: int = 3) -> torch.Tensor:
+    """This shard's rows of q|k|v [B, n, 3D] (parts = 3; k|v: 2) -> every row of head group `rank`:
+    [B, P n, parts * Dp]."""
+    B, n, Dn = qkv.shape
     P = comm.P
-    Dp = D3 // 3 // P
-    send = qkv.view(B, n, 3, P, Dp).permute(3, 0, 1, 2, 4).contiguous()      # [P(head group), B, n, 3, Dp]
-    recv = comm.all_to_all(rank, send)                                         # [P(row shard), B, n, 3, Dp]
-    return recv.permute(1, 0, 2, 3, 4).reshape(B, P * n, 3 * Dp)
+    Dp = Dn // parts // P
+    send = qkv.reshape(B, n, parts, P, Dp).permute(3, 0, 1, 2, 4).contiguous()  # [P(head group), B, n, parts, Dp]
+    recv = comm.all_to_all(rank, send)                                            # [P(row shard), B, n, parts, Dp]
+    return recv.permute(1, 0, 2, 3, 4).reshape(B, P * n, parts * Dp)
 
 
 def heads_to_rows(comm, rank: int, o_full: torch.Tensor) -> torch.Tensor:
@@ -213,8 +255,8 @@ def _check(model, fp8_attrs=("ff_mx", "qkv_mx")):
         if any(getattr(blk, a, None) is not None for a in fp8_attrs) or \
                 getattr(blk.attn1, "fp8_qk_exp", None) is not None:
             raise NotImplementedError("the head-parallel split runs the bf16 path (disable the fp8 modes)")
-        if blk.attn1.processor.__class__.__name__ != "CogVideoXAttnProcessor2_0":
-            raise NotImplementedError("the head-parallel split runs the standard processor only")
+        if type(blk.attn1.processor) not in (CogVideoXAttnProcessor2_0, CogVideoXAttnProcessor2_0_resample):
+            raise NotImplementedError("the head-parallel split runs the standard and ID-resample processors")
 
 
 # ------------------------------------------------------------------------------------------------------------------
@@ -250,10 +292,14 @@ def branch_forward(branch, comm, rank: int, hidden_states, encoder_hidden_states
 
 def transformer_forward(model, comm, rank: int, hidden_states, encoder_hidden_states, timestep,
                         image_rotary_emb=None, branch_block_samples=None, branch_block_masks=None,
-                        add_first: bool = False, return_hidden_states: bool = False):
+                        add_first: bool = False, return_hidden_states: bool = False,
+                        id_pool_resample_learnable: bool = False, prev_hidden_states=None,
+                        prev_clip_weight: Optional[float] = None, prev_resample_mask=None):
     """CogVideoXTransformer3DModel.forward on one shard.  `branch_block_samples` are the branch's shard samples
     (`branch_forward` on the same rank).  Returns the full noise prediction on every rank (and this shard's hidden
-    states when asked: [B, n, D] each)."""
+    states when asked: [B, n, D] each).  The any-length pipeline's window hand-off (anyl.py:962-988):
+    prev_hidden_states = the previous window's shard hidden states ({layer: [B, n, D]}, what this function returned
+    for it), prev_clip_weight, and prev_resample_mask = the full [B, N] mask the previous window returned."""
     _check(model)
     dev = model.proj_out.weight.device
     cfg = model.config
@@ -267,11 +313,18 @@ def transformer_forward(model, comm, rank: int, hidden_states, encoder_hidden_st
     sh = Shard(x_full.shape[1], T, comm.P, rank)
     x = sh.rows(x_full)
     del x_full
-    ctx = _Ctx(comm, rank, sh)
-    rope = sh.rope(_rope_dev(image_rotary_emb, dev))
-    tok_mask = None
+    rope_full = _rope_dev(image_rotary_emb, dev, grid=(F, H // p, W // p))
+    rope = sh.rope(rope_full)
+    tok_mask = full_mask = None
     if branch_block_masks is not None:
-        tok_mask = sh.video_rows(K.patch_mask(branch_block_masks.to(dev), p)).contiguous()
+        tm = K.patch_mask(branch_block_masks.to(dev), p)
+        tok_mask = sh.video_rows(tm).contiguous()
+        if id_pool_resample_learnable:
+            full_mask = torch.zeros(B, T + tm.shape[1], device=dev, dtype=torch.bool)
+            full_mask[:, T:] = tm.bool()
+    if id_pool_resample_learnable and full_mask is None:
+        raise ValueError("id_pool_resample needs masks")
+    ctx = _Ctx(comm, rank, sh, rope_full, _u8(full_mask), _u8(prev_resample_mask))
     bs = list(branch_block_samples) if branch_block_samples is not None else None
     nl = len(model.transformer_blocks)
     interval = int(np.ceil(nl / len(bs))) if bs else 1
@@ -283,8 +336,12 @@ def transformer_forward(model, comm, rank: int, hidden_states, encoder_hidden_st
                 inj = bs[i // interval]
             elif i < len(bs):
                 inj = bs[i]
-        x = block.forward_joint(x, sh.tl, emb, rope, inject=inj, inject_mask=tok_mask if inj is not None else None,
-                                attend=ctx.attend)
+        pj = None
+        if prev_hidden_states is not None:
+            pj = prev_hidden_states.get(i) if isinstance(prev_hidden_states, dict) else prev_hidden_states
+        x = block.forward_joint(x, sh.tl, emb, rope, prev_joint=pj,
+                                prev_clip_weight=prev_clip_weight if pj is not None else None,
+                                inject=inj, inject_mask=tok_mask if inj is not None else None, attend=ctx.attend)
         if return_hidden_states:
             hs_list.append(x)
     D = x.shape[-1]
@@ -337,17 +394,15 @@ class _TransformerView:
                  branch_block_samples=None, branch_block_masks=None, add_first=False,
                  id_pool_resample_learnable=False, return_hidden_states=False, return_resample_mask=False,
                  return_dict=True, **_):
-        if attention_kwargs and attention_kwargs.get("prev_hidden_states") is not None:
-            raise NotImplementedError("the previous-clip blend is not split head-parallel")
-        if id_pool_resample_learnable:
-            raise NotImplementedError("the ID-resample processor is not split head-parallel")
         # the per-call LoRA scale (attention_kwargs["scale"], default 1.0): unfused adapters take it in their
         # augmented operands (rebuilt from the live factors, so an optimizer step's updates reach them too), exactly as
         # the single-GPU forward does (transformer.py, lora.AugmentedProjection)
         self.model._call_lora_scale(attention_kwargs)
+        akw = attention_kwargs or {}
         res = transformer_forward(self.model, self.o.comm, self.o.rank, hidden_states, encoder_hidden_states,
                                   timestep, image_rotary_emb, branch_block_samples, branch_block_masks, add_first,
-                                  return_hidden_states)
+                                  return_hidden_states, id_pool_resample_learnable, akw.get("prev_hidden_states"),
+                                  akw.get("prev_clip_weight"), akw.get("prev_resample_mask"))
         out = res[0]
         if not return_hidden_states:
             return (out,) if not return_dict else Transformer2DModelOutput(sample=out)
