@@ -3,7 +3,7 @@ device (ThreadComm: the same per-rank launches, exchanges as local copies) again
 models.  Row-local kernels give identical rows and attention runs per (batch, head) workgroup, so the split is
 bit-identical to the unsplit forward at this size (measured: rel 0; at sizes where the attention grid's tail split
 engages, a head-group launch may partition a few query blocks' keys differently — the full-size rehearsal is
-`bench.py --mode ulysses`)."""
+`bench.py --mode ulysses`).  Both processors of the any-length pipeline are covered, with the window hand-off."""
 import pytest
 import torch
 
