@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 16
+#define VP_ABI_VERSION 17
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
@@ -61,11 +61,14 @@ enum {
   VP_EPI_GATED = 3,       /* C = rnd(R + rnd(gate * rnd(acc + bias))) [then rnd(C + inject) on video rows]   */
   VP_EPI_BIAS_ADDROWS = 4, /* C = rnd(rnd(acc + bias) + addrows[(m % rows_per_group) + addrows_offset, n])  */
   /* 5 = VP_EPI_BIAS_GELU_MXFP8 (vp_gemm_mx_fp8 only, below) */
-  VP_EPI_BIAS_QKNORM_ROPE = 6 /* fused QKV projection: segments 0 / 1 (q / k): every 64-column head of
+  VP_EPI_BIAS_QKNORM_ROPE = 6, /* fused QKV projection: segments 0 / 1 (q / k): every 64-column head of
                                * y = rnd(acc + bias) -> rnd(LayerNorm64(y; qk_ln_w[s], qk_ln_b[s], qk_eps[s])), then on
                                * video rows (m % tokens_per_batch >= text_len) the interleaved-pair RoPE from
                                * rope_cos / rope_sin (fp32 [tokens_per_batch - text_len][64]) -> rnd; segment 2 (v) as
                                * VP_EPI_BIAS.  = vp_gemm_bf16 + vp_head_norm_rope_bf16 on q and k, bit for bit. */
+  VP_EPI_GELU_BWD = 7     /* C = rnd(rnd(acc + bias) * gelu_tanh'(Z[m, n])), Z = R (bf16 [M][N], row m at ldr; no
+                           * row remap): the FeedForward's dgrad through its GELU — the dgrad GEMM of net.2 followed
+                           * by vp_gelu_bwd_bf16, bit for bit, in one pass (ABI 17) */
 };
 
 typedef struct vp_gemm_desc {
@@ -122,6 +125,12 @@ typedef struct vp_gemm_desc {
   const float* rope_ax[6];
   int32_t rope_hw, rope_w;
   uint32_t rope_mhw, rope_mw;
+  /* Optional second output for the training forward (ABI 17; NULL: none), bf16, row m of the GEMM at aux + m * ld_aux
+   * (no row remap): VP_EPI_BIAS_GELU writes the pre-activation rnd(acc + bias) there (the GELU's backward input, so
+   * no separate vp_gelu_bf16 pass); VP_EPI_BIAS_QKNORM_ROPE writes the pre-norm rnd(acc + bias) of segments 0 / 1
+   * (q | k, columns [0, 2 n_seg)) there (the LayerNorm backward's input).  Other epilogues: VP_ERR_ARG. */
+  void* aux;
+  int64_t ld_aux;
 } vp_gemm_desc;
 
 int vp_gemm_bf16(const vp_gemm_desc* d, void* stream);

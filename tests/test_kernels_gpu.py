@@ -510,6 +510,75 @@ def test_gemm_qknorm_rope_epilogue_matches_separate_kernels(H, T, rope, gemm_var
         assert rel(got.view(B, Ntok, 3 * D)[..., s * D:(s + 1) * D], n.transpose(1, 2).reshape(B, Ntok, D)) < 8e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(600, 512, 128), (4352, 4096, 1024), (1000, 768, 512)],
+                         ids=["v5_runtime_epi", "tail_split", "v13"])
+def test_gemm_gelu_aux_and_gelu_bwd_epilogues_match_separate_launches(M, N, K):
+    """ABI 17, the training forward / backward: EPI_BIAS_GELU with an aux output writes GELU(z) to C and z to aux —
+    bit for bit the FF1 GEMM's plain output and vp_gelu_bf16 of it; EPI_GELU_BWD == the dgrad GEMM then
+    vp_gelu_bwd_bf16, bit for bit.  Shapes: K < 512 (the runtime-epilogue main loop), a tail-split grid (4352 x 4096:
+    272 tiles, the last 16 as split-K workgroups + reduce), the default loop with ragged M."""
+    from videopainter_amd import _native as NAT
+    from videopainter_amd import kernels as K_
+    x = bf(rnd(M, K, seed=201)).to(dev)
+    w = bf(rnd(N, K, std=K ** -0.5, seed=202)).to(dev)
+    b = bf(rnd(N, std=0.3, seed=203)).to(dev)
+    z_want = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K_.gemm(x, [w], [b], z_want)
+    h_want = K_.gelu(z_want)
+    h_fused = torch.empty_like(h_want)
+    K_.gemm(x, [w], [b], h_fused, epilogue=NAT.EPI_BIAS_GELU)
+    assert torch.equal(h_fused, h_want)  # (the existing fused GELU: the same bits as the separate pass)
+    h, z = torch.full_like(h_want, float("nan")), torch.full_like(z_want, float("nan"))
+    K_.gemm(x, [w], [b], h, epilogue=NAT.EPI_BIAS_GELU, aux=z)
+    assert torch.equal(z, z_want)
+    assert torch.equal(h, h_want)
+    # the backward: dz = (dh W) * GELU'(z) with dh [M, K'] against W^T — here the same GEMM shape (a = x, W = w)
+    dz_plain = torch.empty_like(z_want)
+    K_.gemm(x, [w], [None], dz_plain)
+    g_want = K_.gelu_bwd(dz_plain, z_want)
+    g = torch.full_like(g_want, float("nan"))
+    K_.gemm(x, [w], [None], g, epilogue=NAT.EPI_GELU_BWD, z=z_want)
+    assert torch.equal(g, g_want)
+    # against torch fp32: gelu_backward(approximate="tanh")
+    zf = z_want.float().requires_grad_(True)
+    F.gelu(zf, approximate="tanh").backward(dz_plain.float())
+    assert rel(g, zf.grad) < 8e-3
+
+
+def test_gemm_qknorm_aux_keeps_prenorm_qk():
+    """ABI 17: the fused QKV epilogue with an aux output stores the pre-norm q | k (the LayerNorm backward's input)
+    and leaves C bit-identical to the epilogue without it; at K = 128 (runtime-epilogue loop) and K = 512 (the
+    default loop's aux instance); the LoRA tail form's aux instance runs in tests/test_training_gpu.py."""
+    from types import SimpleNamespace
+
+    from videopainter_amd import _native as NAT
+    from videopainter_amd import kernels as K_
+    from oracle.cogvideox_oracle import prepare_rotary_positional_embeddings
+    H, T, B = 4, 17, 2
+    D = H * 64
+    cos, sin = prepare_rotary_positional_embeddings(128, 192, 3, 64)
+    Ntok = T + cos.shape[0]
+    rp = (cos.to(dev), sin.to(dev))
+    lns = [SimpleNamespace(weight=bf(1 + 0.1 * rnd(64, seed=308 + i)).to(dev),
+                           bias=bf(0.1 * rnd(64, seed=310 + i)).to(dev), eps=1e-6) for i in range(2)]
+    for Kd in (128, 512):
+        x = bf(rnd(B * Ntok, Kd, seed=301)).to(dev)
+        ws = [bf(rnd(D, Kd, std=Kd ** -0.5, seed=302 + i)).to(dev) for i in range(3)]
+        bs = [bf(rnd(D, std=0.1, seed=305 + i)).to(dev) for i in range(3)]
+        plain = torch.empty(B * Ntok, 3 * D, device=dev, dtype=torch.bfloat16)
+        K_.gemm(x, ws, bs, plain)
+        kw = dict(epilogue=NAT.EPI_BIAS_QKNORM_ROPE, qk_norm=tuple(lns), rope=rp, tokens_per_batch=Ntok, text_len=T)
+        want = torch.empty_like(plain)
+        K_.gemm(x, ws, bs, want, **kw)
+        got = torch.full_like(plain, float("nan"))
+        aux = torch.full((B * Ntok, 2 * D), float("nan"), device=dev, dtype=torch.bfloat16)
+        K_.gemm(x, ws, bs, got, aux=aux, **kw)
+        assert torch.equal(got, want), Kd
+        assert torch.equal(aux, plain[:, :2 * D]), Kd
+        with pytest.raises(ValueError):
+            K_.gemm(x, ws, bs, got, aux=aux)  # aux only with the GELU / fused-QKV epilogues
+
+
 @pytest.mark.parametrize("r", [64, 256])
 def test_gemm_a_tail_matches_materialized_operands(r):
     """The per-segment A tail (vp_gemm_desc.a_tail_k / a_tail_off; unfused LoRA, lora.AugmentedProjection): segment s

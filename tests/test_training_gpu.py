@@ -170,7 +170,8 @@ def test_block_backward_matches_oracle():
 def test_saved_attention_backward_is_bit_identical(monkeypatch, lora):
     """autograd.SAVE_ACTIVATIONS (the training forward keeps every intermediate the backward reads) and
     SAVE_ATTENTION (the attention output + lse only) against the full recompute: the same forward output bits (the
-    saving forward's unfused norms / separate GELU have forward_joint's rounding points) and the same gradient bits
+    saving forward's fused QKV / GELU epilogues with their aux outputs = forward_joint's launches) and the same
+    gradient bits
     (also with an unfused trainable adapter on the projections), up to the atomic-order noise of the qk-norm affine
     sums."""
     from videopainter_amd import autograd as AG

@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -35,7 +35,7 @@ class GemmDesc(C.Structure):
                 ("addrows", vp), ("addrows_ld", i64), ("addrows_offset", i64),
                 ("qk_ln_w", vp * 2), ("qk_ln_b", vp * 2), ("qk_eps", f32 * 2), ("rope_cos", vp), ("rope_sin", vp),
                 ("a_tail_k", i32), ("pad3", i32), ("a_tail_off", i64 * 3), ("rope_ax", vp * 6), ("rope_hw", i32),
-                ("rope_w", i32), ("rope_mhw", C.c_uint32), ("rope_mw", C.c_uint32)]
+                ("rope_w", i32), ("rope_mhw", C.c_uint32), ("rope_mw", C.c_uint32), ("aux", vp), ("ld_aux", i64)]
 
 
 class AttnDesc(C.Structure):
@@ -87,7 +87,8 @@ class AttnBwdDesc(C.Structure):
                 ("dV", vp), ("dv_sb", i64), ("dv_sn", i64), ("scale", f32), ("pad1", i32)]
 
 
-EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS, EPI_BIAS_GELU_MXFP8, EPI_BIAS_QKNORM_ROPE = range(7)
+(EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_SCALE, EPI_GATED, EPI_BIAS_ADDROWS, EPI_BIAS_GELU_MXFP8, EPI_BIAS_QKNORM_ROPE,
+ EPI_GELU_BWD) = range(8)
 
 # name -> (restype, argtypes)
 _SIGS = {

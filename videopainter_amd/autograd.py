@@ -198,10 +198,13 @@ def _put_linear_grads(G: _Grads, lin, dw: torch.Tensor) -> None:
     G.put(lin.weight, dw)
 
 
-def _block_front(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, resample_mask, attn_saved=None) -> dict:
-    """forward_joint's launches up to the FF1 pre-activation, with its rounding points (the fused QKV + qk-norm
-    epilogue is bit-exact to the separate launches used here, tests/test_model_gpu.py), keeping what the backward
-    reads: the recompute of the checkpointed backward, and the front of the training forward (block_forward_saving)."""
+def _block_front(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, resample_mask, attn_saved=None,
+                 with_h: bool = False) -> dict:
+    """forward_joint's launches up to the FF1 pre-activation, with its rounding points, keeping what the backward
+    reads: the recompute of the checkpointed backward, and the front of the training forward (block_forward_saving).
+    The QKV projection runs forward_joint's fused qk-norm + RoPE epilogue and also stores the pre-norm q | k (the
+    GEMM's aux output, ABI 17) for the LayerNorm backward; with_h: FF1 runs its GELU epilogue and stores the
+    pre-activation z as the aux output (h and z from one pass: the same bits as FF1 + vp_gelu_bf16)."""
     B, Ntok, D = x.shape
     M = B * Ntok
     a = block.attn1
@@ -220,12 +223,19 @@ def _block_front(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, resam
     qaug = AugmentedProjection.of((a.to_q, a.to_k, a.to_v))
     oaug = AugmentedProjection.of((to_out,))
     xq = xn.view(M, D) if qaug is None else qaug.input(xn.view(M, D))
+    resample = resample_mask is not None
+    qkp = None
+    kw = {}
+    if not resample:
+        # qkv = [norm_q(q) + RoPE | norm_k(k) + RoPE | v] and qkp = the pre-norm [q | k], one GEMM
+        qkp = torch.empty(B, Ntok, 2 * D, device=dev, dtype=BF16)
+        kw = dict(epilogue=NAT.EPI_BIAS_QKNORM_ROPE, qk_norm=(a.norm_q, a.norm_k), rope=rope, tokens_per_batch=Ntok,
+                  text_len=T, aux=qkp.view(M, 2 * D))
     if qaug is None:
         K.gemm(xq, [a.to_q.weight, a.to_k.weight, a.to_v.weight], [a.to_q.bias, a.to_k.bias, a.to_v.bias],
-               qkv.view(M, 3 * D))
+               qkv.view(M, 3 * D), **kw)
     else:
-        qaug.gemm(xq, [a.to_q.bias, a.to_k.bias, a.to_v.bias], qkv.view(M, 3 * D))
-    resample = resample_mask is not None
+        qaug.gemm(xq, [a.to_q.bias, a.to_k.bias, a.to_v.bias], qkv.view(M, 3 * D), **kw)
     v = qkv[..., 2 * D:]
     if resample:
         # the resample processor's keys / values as one explicit 2N-key sequence: [K; K2], [V; V2] with
@@ -239,12 +249,10 @@ def _block_front(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, resam
         vc[:, :Ntok].copy_(v)
         K.mask_scale_rows(v, vc[:, Ntok:], resample_mask, 1.0)
         katt, vatt = kc, vc
+        K.head_norm_rope(qkv[..., :D], qn, H, T, a.norm_q.weight, a.norm_q.bias, a.norm_q.eps, rope)
+        K.head_norm_rope(qkv[..., D:2 * D], kn, H, T, a.norm_k.weight, a.norm_k.bias, a.norm_k.eps, rope)
     else:
-        qk = torch.empty(B, Ntok, 2 * D, device=dev, dtype=BF16)
-        qn, kn = qk[..., :D], qk[..., D:]
-        katt, vatt = kn, v
-    K.head_norm_rope(qkv[..., :D], qn, H, T, a.norm_q.weight, a.norm_q.bias, a.norm_q.eps, rope)
-    K.head_norm_rope(qkv[..., D:2 * D], kn, H, T, a.norm_k.weight, a.norm_k.bias, a.norm_k.eps, rope)
+        qn, katt, vatt = qkv[..., :D], qkv[..., D:2 * D], v
     if attn_saved is not None and not resample:
         o, lse = attn_saved
     else:
@@ -256,29 +264,31 @@ def _block_front(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, resam
                 gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok, text_len=T)
     xn2 = K.adaln_modulate(x_mid, n2.norm.weight, n2.norm.bias, mod2, T, n2.norm.eps)
     z = torch.empty(M, F4, device=dev, dtype=BF16)
-    K.gemm(xn2.view(M, D), [ff0.weight], [ff0.bias], z)
-
     st = dict(mod1=mod1, mod2=mod2, xn=xn, xq=xq, qkv=qkv, o=o, lse=lse, x_mid=x_mid, xn2=xn2, z=z)
+    if with_h:
+        st["h"] = torch.empty(M, F4, device=dev, dtype=BF16)
+        K.gemm(xn2.view(M, D), [ff0.weight], [ff0.bias], st["h"], epilogue=NAT.EPI_BIAS_GELU, aux=z)
+    else:
+        K.gemm(xn2.view(M, D), [ff0.weight], [ff0.bias], z)
     if resample:
         st.update(qn=qn, kc=kc, vc=vc)
     else:
-        st["qk"] = qk
+        st["qkp"] = qkp
     return st
 
 
 def block_forward_saving(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inject=None, inject_mask=None,
                          keep_train: bool = False):
     """The block's forward for a training step, keeping its intermediates for the backward (SAVE_ACTIVATIONS): the
-    launches of _block_front (unfused QKV norms, FF1 without its GELU epilogue), then h = GELU(z) by vp_gelu_bf16 (the
-    same rounding points as the fused epilogue: bf16(acc + b), then GELU-tanh, then bf16) and FF2 with the gated
-    residual + injection exactly as forward_joint: the same output bits.  Kept: mod1 / mod2, the pre-norm q | k | v,
-    the attention output + lse, x_mid, z (and, for a block with trainable parameters or a temb that needs its
-    gradient, the AdaLN outputs and h); the normed q | k are recomputed by the backward (two cheap launches)."""
+    launches of _block_front (the fused QKV epilogue also storing the pre-norm q | k, FF1's GELU epilogue also storing
+    its pre-activation z), then FF2 with the gated residual + injection exactly as forward_joint: the same output
+    bits.  Kept: mod1 / mod2, the normed q | k + v and the pre-norm q | k, the attention output + lse, x_mid, z (and,
+    for a block with trainable parameters or a temb that needs its gradient, the AdaLN outputs and h)."""
     B, Ntok, D = x.shape
     M = B * Ntok
     ff2 = block.ff.net[2]
-    st = _block_front(block, x, T, temb, rope, None)
-    h = K.gelu(st["z"])
+    st = _block_front(block, x, T, temb, rope, None, with_h=True)
+    h = st.pop("h")
     out = torch.empty_like(x)
     kw = {}
     if inject is not None:
@@ -286,7 +296,6 @@ def block_forward_saving(block, x: torch.Tensor, T: int, temb: torch.Tensor, rop
     K.gemm(h.view(M, -1), [ff2.weight], [ff2.bias], out.view(M, D), epilogue=NAT.EPI_GATED,
            resid=st["x_mid"].view(M, D), mod=st["mod2"], gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok,
            text_len=T, **kw)
-    del st["qk"]
     if keep_train:
         st["h"] = h
     else:
@@ -317,7 +326,7 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     # ---- the forward's intermediates: kept by the training forward (SAVE_ACTIVATIONS = "all", block_forward_saving)
     # or recomputed here with forward_joint's launches and rounding points ----
     if front is None:
-        front = _block_front(block, x, T, temb, rope, resample_mask, attn_saved)
+        front = _block_front(block, x, T, temb, rope, resample_mask, attn_saved, with_h=need_dmod)
     f = front
     mod1, mod2, qkv, o, lse, x_mid, z = (f.pop(k) for k in ("mod1", "mod2", "qkv", "o", "lse", "x_mid", "z"))
     xn, xq, xn2, h_saved = f.pop("xn", None), f.pop("xq", None), f.pop("xn2", None), f.pop("h", None)
@@ -325,17 +334,14 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     oaug = AugmentedProjection.of((to_out,))
     resample = resample_mask is not None
     v = qkv[..., 2 * D:]
-    kc = vc = qk = None
-    if resample:
+    kc = vc = None
+    if resample:  # qkv: the pre-norm projections
         qn, kc, vc = f.pop("qn"), f.pop("kc"), f.pop("vc")
-    elif "qk" in f:
-        qk = f.pop("qk")
-        qn, kn = qk[..., :D], qk[..., D:]
-    else:  # (the training forward keeps the pre-norm q | k | v only: the two norm launches again)
-        qk = torch.empty(B, Ntok, 2 * D, device=dev, dtype=BF16)
-        qn, kn = qk[..., :D], qk[..., D:]
-        K.head_norm_rope(qkv[..., :D], qn, H, T, a.norm_q.weight, a.norm_q.bias, a.norm_q.eps, rope)
-        K.head_norm_rope(qkv[..., D:2 * D], kn, H, T, a.norm_k.weight, a.norm_k.bias, a.norm_k.eps, rope)
+        qpre, kpre = qkv[..., :D], qkv[..., D:2 * D]
+    else:  # qkv: the normed q | k and v; qkp: the pre-norm q | k
+        qkp = f.pop("qkp")
+        qn, kn = qkv[..., :D], qkv[..., D:2 * D]
+        qpre, kpre = qkp[..., :D], qkp[..., D:]
     del front, f
 
     dout = dout.contiguous()
@@ -353,8 +359,7 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     df = torch.empty(M, D, device=dev, dtype=BF16)
     K.rowscale(dout2, df, Ntok, T, mod2, 2, 5)
     dz = torch.empty(M, F4, device=dev, dtype=BF16)
-    _dgrad(df, ff2.weight, dz)
-    K.gelu_bwd(dz, z, out=dz)
+    K.gemm(df, [_wt(ff2.weight)], [None], dz, epilogue=NAT.EPI_GELU_BWD, z=z)  # (df W2) * GELU'(z), one pass
     dxn2 = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
     _dgrad(dz, ff0.weight, dxn2.view(M, D))
     n2o = dn2 = xh2 = None
@@ -419,25 +424,25 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
     else:
         K.attention_bwd(qn, kn, v, o, do, lse, H, scale=a.scale, dq=dqkv[..., :D], dk=dqkv[..., D:2 * D],
                         dv=dqkv[..., 2 * D:])
-        del qk
+        del qn, kn, v, qkv
     del do, o, lse
     dlnq = dlnk = None
     if train and (a.norm_q.weight.requires_grad or a.norm_k.weight.requires_grad):
         dlnq = (torch.zeros(64, device=dev, dtype=F32), torch.zeros(64, device=dev, dtype=F32))
         dlnk = (torch.zeros(64, device=dev, dtype=F32), torch.zeros(64, device=dev, dtype=F32))
-    K.head_norm_rope_bwd(qkv[..., :D], dqkv[..., :D], dqkv[..., :D], H, T, a.norm_q, rope, dlnq)
-    K.head_norm_rope_bwd(qkv[..., D:2 * D], dqkv[..., D:2 * D], dqkv[..., D:2 * D], H, T, a.norm_k, rope, dlnk)
+    K.head_norm_rope_bwd(qpre, dqkv[..., :D], dqkv[..., :D], H, T, a.norm_q, rope, dlnq)
+    K.head_norm_rope_bwd(kpre, dqkv[..., D:2 * D], dqkv[..., D:2 * D], H, T, a.norm_k, rope, dlnk)
     if dk2 is not None:
         # K2 = LN(mask . k) + RoPE: (LN + RoPE)' at the masked input, then x mask (null rows: LN of a zero row,
         # whose input gradient the mask cancels; their d beta stays in dlnk)
         km = torch.empty(B, Ntok, D, device=dev, dtype=BF16)
-        K.mask_scale_rows(qkv[..., D:2 * D], km, resample_mask, 1.0)
+        K.mask_scale_rows(kpre, km, resample_mask, 1.0)
         dkm = K.head_norm_rope_bwd(km, dk2, torch.empty(B, Ntok, D, device=dev, dtype=BF16), H, T, a.norm_k, rope,
                                    dlnk)
         K.mask_scale_rows(dkm, km, resample_mask, 1.0)
         dqkv[..., D:2 * D].add_(km)
         del km, dkm, dk2, dkc
-    del qkv
+    del qpre, kpre
     if dlnq is not None:
         G.put(a.norm_q.weight, dlnq[0])
         G.put(a.norm_q.bias, dlnq[1])
@@ -486,7 +491,8 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
 SAVE_ATTENTION = True
 # Beyond that, while the device has room (SAVE_ACTIVATIONS = True; the budget below), the training forward runs the
 # backward's front itself (block_forward_saving) and keeps every intermediate the backward reads, so the backward
-# recomputes nothing: ~1 GB per frozen 5b block at B = 1, N = 17 776 (q | k | v, O, x_mid, the FF1 pre-activation z).
+# recomputes nothing: ~1.2 GB per frozen 5b block at B = 1, N = 17 776 (q | k | v, the normed q | k, O, x_mid, the FF1
+# pre-activation z).
 # A block whose kept set would leave less than SAVE_RESERVE_BYTES free (or four times its own size) falls back to
 # the attention-only form, so a larger batch degrades to recompute instead of running out of memory.
 SAVE_ACTIVATIONS = True
@@ -495,7 +501,7 @@ SAVE_RESERVE_BYTES = 16 << 30
 
 def _room_for(x: torch.Tensor, F4: int) -> bool:
     B, Ntok, D = x.shape
-    need = B * Ntok * (3 * D + D + D + F4) * 2  # q | k | v, O, x_mid, z (bf16)
+    need = B * Ntok * (5 * D + D + D + F4) * 2  # q | k | v, normed q | k, O, x_mid, z (bf16)
     free, _ = torch.cuda.mem_get_info(x.device)
     return free - need > max(SAVE_RESERVE_BYTES, 4 * need)
 

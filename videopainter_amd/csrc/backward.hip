@@ -188,13 +188,7 @@ __global__ __launch_bounds__(256) void rowscale_kernel(const bf16* __restrict__ 
   }
 }
 
-// GELU (tanh form) and its derivative, elementwise on bf16
-VP_DEV float gelu_grad(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  const float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
-}
+// GELU (tanh form) and its derivative (gelu_grad, vp_common.h: shared with the GEMM's VP_EPI_GELU_BWD), elementwise
 
 __global__ __launch_bounds__(256) void gelu_kernel(const bf16* __restrict__ z, bf16* __restrict__ h, int64_t n8) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {

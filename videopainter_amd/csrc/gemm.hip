@@ -166,12 +166,28 @@ VP_DEV void mfma_mx(f32x4& acc, const i32x8& w, const i32x8& a, int sw, int sa) 
 // threads stream image rows out as 16-byte row stores, with the row-wise epilogues: residual / gate / injection /
 // pos-emb / MX).  The persistent kernel runs the last two per half tile so the next tile's first K-tile can load
 // into the other half of the LDS meanwhile. ----
+// Internal instance kinds (not ABI values): an epilogue with the aux output (vp_gemm_desc.aux) is its own instance,
+// so the inference instances carry none of its code or registers.
+constexpr int EPI_QKNORM_AUX = 8, EPI_GELU_AUX = 9;
+// the ABI epilogue of an instance kind, and whether the instance writes aux (EPI = -1: both from the descriptor)
+template <int EPI>
+VP_DEV int epi_kind(const vp_gemm_desc& d) {
+  if constexpr (EPI < 0) return d.epilogue;
+  return EPI == EPI_QKNORM_AUX ? VP_EPI_BIAS_QKNORM_ROPE : EPI == EPI_GELU_AUX ? VP_EPI_BIAS_GELU : EPI;
+}
+template <int EPI>
+VP_DEV bool epi_aux(const vp_gemm_desc& d) {
+  if constexpr (EPI < 0) return d.aux != nullptr;
+  return EPI == EPI_QKNORM_AUX || EPI == EPI_GELU_AUX;
+}
+
 // EPI >= 0: the epilogue kind as a compile-time constant (the persistent kernel is instantiated per kind; with the
 // runtime switch its register allocation spills), FULL_N: N % 256 == 0 (no column guard)
 template <int FN, int FM, int WN, int WM, int EPI = -1, bool FULL_N = false, class Sink>
 VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&& sink, int m0, int n0, int wr, int wc,
                        int lane) {
-  const int epi = EPI >= 0 ? EPI : d.epilogue;
+  const int epi = epi_kind<EPI>(d);
+  const bool aux = epi_aux<EPI>(d);
   // head by head (4 fragments = 64 columns; WN % 64 == 0 and n0 % 256 == 0), so a head's accumulators die as its
   // values go to the sink.  Fused QKV (VP_EPI_BIAS_QKNORM_ROPE): q / k heads go through norm + RoPE in registers
   // (ln64_rope16: lane xor 16 / 32 are the other column quarters of the same row); v heads take the plain path.
@@ -260,6 +276,19 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
         for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
           for (int r = 0; r < 4; ++r) x[4 * jj + r] = rbf(acc[hh * 4 + jj][i][r] + bv[4 * jj + r]);
+        if (aux) {  // the pre-norm q | k for the training backward (vp_gemm_desc.aux)
+          const int m = m0 + wr * WM + i * 16 + (lane & 15);
+          if (m < d.M) {
+            bf16* ap = (bf16*)d.aux + (int64_t)m * d.ld_aux + nh + 4 * g;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              bf16x4 o;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = f2bf(x[4 * jj + r]);
+              *(bf16x4*)(ap + 16 * jj) = o;
+            }
+          }
+        }
         ln64_rope16_regs<16, 32>(x, lw4, lb4, d.qk_eps[sgh], cs, sn, rot);
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
@@ -294,7 +323,8 @@ VP_DEV void epi_values(const vp_gemm_desc& d, const f32x4 (&acc)[FN][FM], Sink&&
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = rbf(acc[j][i][r] + bv[r]);
-          if (epi == VP_EPI_BIAS_GELU || epi == VP_EPI_BIAS_GELU_MXFP8) v = gelu_tanh(v);
+          // (with an aux output the GELU runs in the row pass, on the bf16 pre-activation it stores: the same bits)
+          if ((epi == VP_EPI_BIAS_GELU && !aux) || epi == VP_EPI_BIAS_GELU_MXFP8) v = gelu_tanh(v);
           else if (epi == VP_EPI_BIAS_SCALE) v = v * d.alpha;
           o[r] = f2bf(v);
         }
@@ -318,7 +348,8 @@ VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* sme
                          int n0, int tid, const bf16x8* rpre = nullptr) {
   constexpr int CPR = BNC / 8;        // 16-byte chunks per tile row
   constexpr int CTS = BNC * 2 + 8;
-  const int epi = EPI >= 0 ? EPI : d.epilogue;
+  const int epi = epi_kind<EPI>(d);
+  const bool aux = epi_aux<EPI>(d);
   bf16* C = (bf16*)d.C;
   const int chunk = tid & (CPR - 1);  // 16-byte chunk within the tile row
   const int ncol = n0 + chunk * 8;
@@ -357,7 +388,16 @@ VP_DEV void epi_rows_out(const vp_gemm_desc& d, const MxExt& mx, const char* sme
       if ((tid & 3) == 0) mx.c_scale[mx_scale_off(orow, ncol >> 5, d.N)] = sb;
       continue;
     }
-    if (epi == VP_EPI_GATED) {
+    if (epi == VP_EPI_BIAS_GELU && aux) {
+      // the training forward's FF1: the pre-activation z to aux, GELU(z) to C
+      *(bf16x8*)((bf16*)d.aux + (int64_t)m * d.ld_aux + ncol) = v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(gelu_tanh(bf2f(v[e])));
+    } else if (epi == VP_EPI_GELU_BWD) {
+      const bf16x8 z = *(const bf16x8*)((const bf16*)d.R + (int64_t)m * d.ldr + ncol);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) * gelu_grad(bf2f(z[e])));
+    } else if (epi == VP_EPI_GATED) {
       int b = b0, tok = tk0 + mloc;
       while (tok >= tpb) {
         tok -= tpb;
@@ -1366,19 +1406,24 @@ VP_DEV void splitk_epilogue(const vp_gemm_desc& d, int m, int n, const float (&a
   const bf16* bp = (const bf16*)d.bias[sg];
   const int grp = m / d.rows_per_group, gin = m - grp * d.rows_per_group;
   const int64_t orow = (int64_t)grp * d.group_stride + d.row_offset + gin;
-  bf16x8 o;
+  bf16x8 o, av;
   bf16x8 pv;
   if (d.epilogue == VP_EPI_BIAS_ADDROWS)
     pv = *(const bf16x8*)((const bf16*)d.addrows + (int64_t)(gin + d.addrows_offset) * d.addrows_ld + n);
+  else if (d.epilogue == VP_EPI_GELU_BWD)
+    pv = *(const bf16x8*)((const bf16*)d.R + (int64_t)m * d.ldr + n);
   const bf16x8 b8 = bp != nullptr ? *(const bf16x8*)(bp + n - sg * d.n_seg) : bf16x8{};
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     float v = rbf(a[e] + (bp != nullptr ? bf2f(b8[e]) : 0.f));
+    av[e] = f2bf(v);
     if (d.epilogue == VP_EPI_BIAS_GELU) v = rbf(gelu_tanh(v));
     else if (d.epilogue == VP_EPI_BIAS_SCALE) v = rbf(v * d.alpha);
     else if (d.epilogue == VP_EPI_BIAS_ADDROWS) v = bf2f(f2bf(v)) + bf2f(pv[e]);
+    else if (d.epilogue == VP_EPI_GELU_BWD) v = rbf(v * gelu_grad(bf2f(pv[e])));
     o[e] = f2bf(v);
   }
+  if (d.epilogue == VP_EPI_BIAS_GELU && d.aux != nullptr) *(bf16x8*)((bf16*)d.aux + (int64_t)m * d.ld_aux + n) = av;
   *(bf16x8*)((bf16*)d.C + orow * d.ldc + n) = o;
 }
 
@@ -1427,7 +1472,8 @@ SplitPlan split_plan(const vp_gemm_desc* d) {
   SplitPlan p;
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
   const bool epi_ok = d->epilogue == VP_EPI_BIAS || d->epilogue == VP_EPI_BIAS_GELU ||
-                      d->epilogue == VP_EPI_BIAS_SCALE || d->epilogue == VP_EPI_BIAS_ADDROWS;
+                      d->epilogue == VP_EPI_BIAS_SCALE || d->epilogue == VP_EPI_BIAS_ADDROWS ||
+                      d->epilogue == VP_EPI_GELU_BWD;
   if (!epi_ok || (d->K % BK) != 0 || d->a_tail_k > 0) return p;
   const int64_t tile_a0 = (int64_t)BM * d->lda * 2, wseg0 = (int64_t)d->n_seg * d->K * 2;
   if (tiles >= 128) return (tile_a0 < ((int64_t)1 << 31) && wseg0 < ((int64_t)1 << 31)) ? tail_plan(d, tiles) : p;
@@ -1461,6 +1507,27 @@ static int gemm_group(const vp_gemm_desc* d) {
   return v > 0 && v <= 64 ? v : 4;
 }
 
+// the ABI-17 fields: the aux output (VP_EPI_BIAS_GELU / _QKNORM_ROPE only) and VP_EPI_GELU_BWD's Z operand
+static int check_aux(const vp_gemm_desc* d) {
+  if (d->aux != nullptr) {
+    if (d->epilogue == VP_EPI_BIAS_GELU) {
+      if (d->ld_aux < d->N || (d->ld_aux % 8) != 0) return VP_ERR_ARG;
+    } else if (d->epilogue == VP_EPI_BIAS_QKNORM_ROPE) {
+      if (d->ld_aux < 2 * (int64_t)d->n_seg || (d->ld_aux % 8) != 0) return VP_ERR_ARG;
+    } else {
+      return VP_ERR_ARG;
+    }
+  }
+  if (d->epilogue == VP_EPI_GELU_BWD && (d->R == nullptr || d->ldr < d->N || (d->ldr % 8) != 0)) return VP_ERR_ARG;
+  return VP_OK;
+}
+
+// the instance-table slot of a descriptor: the ABI epilogue, or the aux instance of its kind
+static int kernel_index(const vp_gemm_desc* d) {
+  if (d->aux == nullptr) return d->epilogue;
+  return d->epilogue == VP_EPI_BIAS_QKNORM_ROPE ? EPI_QKNORM_AUX : EPI_GELU_AUX;
+}
+
 // main_tiles > 0: launch only the first main_tiles tiles of the grouped order (tail mode's main launch)
 static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles) {
   if (d == nullptr || d->A == nullptr || d->W[0] == nullptr || d->C == nullptr) return VP_ERR_ARG;
@@ -1469,8 +1536,9 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
   if (d->rows_per_group <= 0) return VP_ERR_ARG;
   const int nsegs = d->W[2] ? 3 : (d->W[1] ? 2 : 1);
   if (d->n_seg <= 0 || d->n_seg * nsegs != d->N) return VP_ERR_ARG;
-  if (d->epilogue < VP_EPI_BIAS || d->epilogue > VP_EPI_BIAS_QKNORM_ROPE || d->epilogue == VP_EPI_BIAS_GELU_MXFP8)
+  if (d->epilogue < VP_EPI_BIAS || d->epilogue > VP_EPI_GELU_BWD || d->epilogue == VP_EPI_BIAS_GELU_MXFP8)
     return VP_ERR_ARG;
+  if (check_aux(d) != VP_OK) return VP_ERR_ARG;
   if (d->epilogue == VP_EPI_BIAS_QKNORM_ROPE) {
     if (nsegs != 3 || (d->n_seg % 64) != 0 || d->rows_per_group != d->M || d->tokens_per_batch <= 0) return VP_ERR_ARG;
     for (int s = 0; s < 2; ++s)
@@ -1487,11 +1555,14 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
   mx.group = gemm_group(d);
   if (d->a_tail_k != 0) {
     // the per-segment A tail (unfused LoRA): the default main loop only, on whole K-tiles and whole-tile segments
-    static const void* const k13t[7] = {(const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS, false, true>,
+    static const void* const k13t[10] = {(const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS, false, true>,
                                         nullptr, nullptr,
                                         (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_GATED, false, true>,
                                         nullptr, nullptr,
-                                        (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_QKNORM_ROPE, false, true>};
+                                        (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_QKNORM_ROPE, false, true>,
+                                        nullptr,
+                                        (const void*)gemm_bf16_kernel<13, false, 4, EPI_QKNORM_AUX, false, true>,
+                                        nullptr};
     static bool attr_t = false;
     if (!attr_t) {
       for (const void* f : k13t)
@@ -1499,6 +1570,7 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
       attr_t = true;
     }
     if (d->a_tail_k < 0 || d->a_tail_k >= d->K || (d->a_tail_k % BK) != 0) return VP_ERR_ARG;
+    const int ki = kernel_index(d);
     int64_t amax = 0;
     for (int s = 0; s < nsegs; ++s) {
       if (d->a_tail_off[s] < 0 || (d->a_tail_off[s] % 8) != 0) return VP_ERR_ARG;
@@ -1507,12 +1579,12 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
     if (d->lda < d->K + amax) return VP_ERR_ARG;  // every segment's tail columns inside the rows
     const char* e = vp_knob(VPK_GEMM_VARIANT);
     if ((e != nullptr && atoi(e) != 13) || (d->K % BK) != 0 || d->K < 8 * BK || (nsegs > 1 && (d->n_seg % BN) != 0) ||
-        k13t[d->epilogue] == nullptr || (int64_t)BM * d->lda * 2 >= ((int64_t)1 << 31) ||
+        k13t[ki] == nullptr || (int64_t)BM * d->lda * 2 >= ((int64_t)1 << 31) ||
         (int64_t)d->n_seg * d->K * 2 >= ((int64_t)1 << 31))
       return VP_ERR_UNSUPPORTED;
     const int ttiles = ((d->M + BM - 1) / BM) * (d->N / BN);
     void* args[] = {(void*)d, (void*)&mx};
-    const hipError_t le = hipLaunchKernel(k13t[d->epilogue], dim3(main_tiles > 0 ? min(main_tiles, ttiles) : ttiles),
+    const hipError_t le = hipLaunchKernel(k13t[ki], dim3(main_tiles > 0 ? min(main_tiles, ttiles) : ttiles),
                                           dim3(NTHREADS), args, LDS_BYTES, (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
     VP_CHECK_LAUNCH();
@@ -1523,24 +1595,31 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
   // 283.7 against 295.4 ms of GEMM per step, profiles/r04_gemm13_ab.log), 11 = the same with the reads after the DMA
   // (VP_GEMM_VARIANT=11, A/B), 5 = the unstaggered pipeline (A/B; also K < 512), 1 = the 2-stage ring (K % 64 != 0,
   // e.g. the patch-embed im2col K = 132)
-  static const void* const k11[7] = {
+  static const void* const k11[10] = {
       (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS>, (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_GELU>,
       (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_SCALE>, (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_GATED>,
       (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_ADDROWS>, nullptr,
-      (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_QKNORM_ROPE>};
-  static const void* const k13[7] = {
+      (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_BIAS_QKNORM_ROPE>,
+      (const void*)gemm_bf16_kernel<11, false, 4, VP_EPI_GELU_BWD>,
+      nullptr, nullptr};
+  static const void* const k13[10] = {
       (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS>, (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_GELU>,
       (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_SCALE>, (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_GATED>,
       (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_ADDROWS>, nullptr,
-      (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_QKNORM_ROPE>};
+      (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS_QKNORM_ROPE>,
+      (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_GELU_BWD>,
+      (const void*)gemm_bf16_kernel<13, false, 4, EPI_QKNORM_AUX>,
+      (const void*)gemm_bf16_kernel<13, false, 4, EPI_GELU_AUX>};
 #if VP_GEMM_EXTRA_VARIANTS
-  static const void* const k12[7] = {
+  static const void* const k12[10] = {
       (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS>, (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_GELU>,
       (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_SCALE>, (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_GATED>,
       (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_ADDROWS>, nullptr,
-      (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_QKNORM_ROPE>};
+      (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_QKNORM_ROPE>,
+      nullptr,
+      nullptr, nullptr};
 #else
-  static const void* const k12[7] = {};
+  static const void* const k12[10] = {};
 #endif
   static bool attr_set = false;
   if (!attr_set) {
@@ -1567,13 +1646,14 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
   // 30: two workgroups per CU, 256 x 128 tiles (whole 128-column tiles of one weight segment, whole 32-K steps,
   // 32-bit in-tile DMA offsets)
   if (variant == 30) {
-    const bool ok30 = (d->N % BN2) == 0 && (d->n_seg % BN2) == 0 && (d->K % BK2) == 0 &&
+    const bool ok30 = d->epilogue != VP_EPI_GELU_BWD && d->aux == nullptr && (d->N % BN2) == 0 && (d->n_seg % BN2) == 0 && (d->K % BK2) == 0 &&
                       (int64_t)BM2 * d->lda * 2 < ((int64_t)1 << 31) && (int64_t)BN2 * d->K * 2 < ((int64_t)1 << 31);
     if (ok30) {
-      static const void* const k30[7] = {
+      static const void* const k30[8] = {
           (const void*)gemm2_kernel<VP_EPI_BIAS>, (const void*)gemm2_kernel<VP_EPI_BIAS_GELU>,
           (const void*)gemm2_kernel<VP_EPI_BIAS_SCALE>, (const void*)gemm2_kernel<VP_EPI_GATED>,
-          (const void*)gemm2_kernel<VP_EPI_BIAS_ADDROWS>, nullptr, (const void*)gemm2_kernel<VP_EPI_BIAS_QKNORM_ROPE>};
+          (const void*)gemm2_kernel<VP_EPI_BIAS_ADDROWS>, nullptr, (const void*)gemm2_kernel<VP_EPI_BIAS_QKNORM_ROPE>,
+          nullptr};
       static bool attr30 = false;
       if (!attr30) {
         for (const void* f : k30)
@@ -1593,13 +1673,14 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
   // 20: the 4-wave AGPR-accumulator kernel (whole 256-column tiles of one weight segment, whole K-tiles, 32-bit
   // in-tile DMA offsets)
   if (variant == 20) {
-    const bool ok20 = (d->N % BN) == 0 && (d->n_seg % BN) == 0 && (d->K % BK) == 0 && d->K >= 2 * BK &&
+    const bool ok20 = d->epilogue != VP_EPI_GELU_BWD && d->aux == nullptr && (d->N % BN) == 0 && (d->n_seg % BN) == 0 && (d->K % BK) == 0 && d->K >= 2 * BK &&
                       (int64_t)BM * d->lda * 2 < ((int64_t)1 << 31) && (int64_t)BN * d->K * 2 < ((int64_t)1 << 31);
     if (ok20) {
-      static const void* const k20[7] = {
+      static const void* const k20[8] = {
           (const void*)gemm4_kernel<VP_EPI_BIAS>, (const void*)gemm4_kernel<VP_EPI_BIAS_GELU>,
           (const void*)gemm4_kernel<VP_EPI_BIAS_SCALE>, (const void*)gemm4_kernel<VP_EPI_GATED>,
-          (const void*)gemm4_kernel<VP_EPI_BIAS_ADDROWS>, nullptr, (const void*)gemm4_kernel<VP_EPI_BIAS_QKNORM_ROPE>};
+          (const void*)gemm4_kernel<VP_EPI_BIAS_ADDROWS>, nullptr, (const void*)gemm4_kernel<VP_EPI_BIAS_QKNORM_ROPE>,
+          nullptr};
       static bool attr20 = false;
       if (!attr20) {
         for (const void* f : k20)
@@ -1624,15 +1705,17 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
   if ((variant == 11 || variant == 13) && d->K < 8 * BK) variant = 5;  // the staggered prologue assumes >= 8 K-tiles
   const int all_tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
   const int tiles = main_tiles > 0 ? min(main_tiles, all_tiles) : all_tiles;
+  const int ki = kernel_index(d);
+  if ((variant == 12 && k12[ki] == nullptr) || (variant == 11 && k11[ki] == nullptr)) return VP_ERR_UNSUPPORTED;
   if (variant == 12 || variant == 13) {
     void* args[] = {(void*)d, (void*)&mx};
     const void* const* kt = variant == 12 ? k12 : k13;
-    const hipError_t le = hipLaunchKernel(kt[d->epilogue], dim3(tiles), dim3(NTHREADS), args, LDS_BYTES,
+    const hipError_t le = hipLaunchKernel(kt[ki], dim3(tiles), dim3(NTHREADS), args, LDS_BYTES,
                                           (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
   } else if (variant == 11) {
     void* args[] = {(void*)d, (void*)&mx};
-    const hipError_t le = hipLaunchKernel(k11[d->epilogue], dim3(tiles), dim3(NTHREADS), args, LDS_BYTES,
+    const hipError_t le = hipLaunchKernel(k11[ki], dim3(tiles), dim3(NTHREADS), args, LDS_BYTES,
                                           (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
   } else if (variant == 5) {
@@ -1663,6 +1746,7 @@ extern "C" int vp_gemm_bf16_ws(const vp_gemm_desc* d, void* workspace, int64_t w
   const int nsegs = d->W[2] ? 3 : (d->W[1] ? 2 : 1);
   if (d->n_seg <= 0 || d->n_seg * nsegs != d->N) return VP_ERR_ARG;
   if (d->epilogue == VP_EPI_BIAS_ADDROWS && (d->addrows == nullptr || (d->addrows_ld % 8) != 0)) return VP_ERR_ARG;
+  if (check_aux(d) != VP_OK) return VP_ERR_ARG;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_BIAS, true>,
@@ -1711,7 +1795,7 @@ extern "C" int vp_gemm_mx_fp8(const vp_gemm_mx_desc* x, void* stream) {
   if (d->n_seg <= 0 || d->n_seg * nsegs != d->N || (d->n_seg % 256) != 0) return VP_ERR_ARG;
   for (int s = 0; s < nsegs; ++s)
     if (x->w_scale[s] == nullptr) return VP_ERR_ARG;
-  if (d->epilogue < VP_EPI_BIAS || d->epilogue > VP_EPI_BIAS_GELU_MXFP8) return VP_ERR_ARG;
+  if (d->epilogue < VP_EPI_BIAS || d->epilogue > VP_EPI_BIAS_GELU_MXFP8 || d->aux != nullptr) return VP_ERR_ARG;
   if (d->epilogue == VP_EPI_BIAS_GELU_MXFP8) {
     if (x->c_scale == nullptr || (d->ldc % 16) != 0 || d->ldc < d->N || d->rows_per_group != d->M) return VP_ERR_ARG;
   } else if (d->ldc < d->N || (d->ldc % 8) != 0) {

@@ -34,6 +34,24 @@ VP_DEV float gelu_tanh(float x) {
   return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(a));
 }
 
+// d/dx of the tanh-form GELU (torch's gelu_backward, approximate="tanh"), fp32 from the bf16 pre-activation.
+// tanh(u) = 1 - 2 / (1 + 2^(2 u log2 e)) on v_exp_f32 + v_rcp_f32 (absolute error ~1e-7, far below the bf16 output's
+// ulp; saturates to +-1 through inf / 0): the libm tanhf it replaces cost ~10x the VALU, which in the FF2 dgrad GEMM's
+// epilogue (VP_EPI_GELU_BWD, not overlapped with MFMA) was as slow as the separate elementwise pass.
+// Every fused multiply-add is explicit and contraction is off, so the standalone pass and the GEMM epilogue compile
+// to the same arithmetic whatever the surrounding code (they are compared bit for bit).
+VP_DEV float gelu_grad(float x) {
+#pragma clang fp contract(off)
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float x2 = x * x;
+  const float u = k0 * __builtin_fmaf(k1 * x2, x, x);  // k0 (x + k1 x^3)
+  const float t = __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u * (2.f * 1.4426950408889634f))),
+                                 1.f);
+  const float dt = __builtin_fmaf(-t, t, 1.f);                 // 1 - t^2
+  const float pd = k0 * __builtin_fmaf(3.f * k1, x2, 1.f);     // k0 (1 + 3 k1 x^2)
+  return __builtin_fmaf(0.5f, 1.f + t, (0.5f * x) * dt * pd);
+}
+
 VP_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
 
 // norm_q / norm_k + apply_rotary_emb on one 64-wide head spread over 4 lanes (g = the lane's quarter, partners at

@@ -89,12 +89,16 @@ def gemm(a: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[Opti
          tokens_per_batch: int = 1, text_len: int = 0, inject: Optional[torch.Tensor] = None,
          inject_ld: int = 0, inject_bstride: int = 0, inject_mask: Optional[torch.Tensor] = None,
          addrows: Optional[torch.Tensor] = None, addrows_offset: int = 0, qk_norm=None, rope=None,
-         a_tail: Optional[Tuple[int, Sequence[int]]] = None) -> torch.Tensor:
+         a_tail: Optional[Tuple[int, Sequence[int]]] = None, aux: Optional[torch.Tensor] = None,
+         z: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = epilogue(a @ cat(weights).T).  `a` rows: M rows of length K at stride lda.
     EPI_BIAS_QKNORM_ROPE: qk_norm = (norm_q, norm_k) LayerNorm(64) modules, rope = (cos, sin) fp32 [N - text_len, 64]
     or None; rows are (batch, token) with `tokens_per_batch` / `text_len`.
     a_tail = (k0, offsets): the per-segment A tail (vp_gemm_desc.a_tail_k / a_tail_off; unfused LoRA): for K columns
-    k >= k0, weight segment s reads column k + offsets[s] of `a`."""
+    k >= k0, weight segment s reads column k + offsets[s] of `a`.
+    aux (ABI 17, the training forward): a bf16 [M, *] row-major second output — EPI_BIAS_GELU stores the
+    pre-activation there, EPI_BIAS_QKNORM_ROPE the pre-norm q | k (its first 2 n_seg columns).
+    z: EPI_GELU_BWD's GELU input, bf16 [M, N] row-major: out = bf16(bf16(a @ W^T + b) * gelu'(z))."""
     _chk(a, "a")
     _chk(out, "out")
     K = weights[0].shape[1]
@@ -168,6 +172,19 @@ def gemm(a: torch.Tensor, weights: Sequence[torch.Tensor], biases: Sequence[Opti
                     d.rope_ax[i] = _p(t)
                 d.rope_hw, d.rope_w = hw, w
                 d.rope_mhw, d.rope_mw = ((1 << 32) + hw - 1) // hw, ((1 << 32) + w - 1) // w
+    if aux is not None:
+        _chk(aux, "aux")
+        if epilogue not in (N.EPI_BIAS_GELU, N.EPI_BIAS_QKNORM_ROPE):
+            raise ValueError("aux output: EPI_BIAS_GELU or EPI_BIAS_QKNORM_ROPE only")
+        width = Ntot if epilogue == N.EPI_BIAS_GELU else 2 * nseg
+        if aux.numel() // aux.shape[-1] != M or aux.shape[-1] < width:
+            raise ValueError(f"aux must hold {M} rows of >= {width} columns, got {tuple(aux.shape)}")
+        d.aux, d.ld_aux = _p(aux), _rowmajor(aux, "aux")
+    if epilogue == N.EPI_GELU_BWD:
+        _chk(z, "z")
+        if z.numel() // z.shape[-1] != M or z.shape[-1] != Ntot:
+            raise ValueError(f"z must be [{M}, {Ntot}], got {tuple(z.shape)}")
+        d.R, d.ldr = _p(z), _rowmajor(z, "z")
     if epilogue == N.EPI_BIAS_ADDROWS:
         _chk(addrows, "addrows")
         d.addrows, d.addrows_ld, d.addrows_offset = _p(addrows), _rowmajor(addrows, "addrows"), addrows_offset
