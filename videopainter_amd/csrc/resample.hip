@@ -22,6 +22,11 @@ constexpr int NM_R = 6;     // runs per segment record; rows with more are their
 constexpr int NM_NT = 128;  // threads (queries) per block of the mass kernel
 constexpr int NM_MAXF = 16;
 constexpr int NM_MAXH = 64;  // rows per frame: one lane each in the segment kernel
+// the mass kernel's p loops unrolled by VP_NM_UNROLL: independent dot-product chains (and prefix-sum reads) in flight
+// together instead of one 24-deep dependent FMA chain at a time; every chain keeps its own order (same results)
+#ifndef VP_NM_UNROLL
+#define VP_NM_UNROLL 4
+#endif
 
 // one wave per (b, t): lane y finds the null runs of row y, equal neighbouring rows merge into segments.
 // segs[((b F + t) Hh + i)] (16 bytes): byte 0 = y0, 1 = y1 (exclusive), 2 = run count (255: scan the row),
@@ -148,6 +153,7 @@ __global__ __launch_bounds__(NM_NT) void null_key_mass_kernel(
     et[p] = sv;
     mt = fmaxf(mt, sv);
   }
+#pragma unroll VP_NM_UNROLL
   for (int p = 0; p < Hh; ++p) {
     float sv = 0.f;
 #pragma unroll
@@ -156,6 +162,7 @@ __global__ __launch_bounds__(NM_NT) void null_key_mass_kernel(
     py[(p + 1) * NM_NT + tid] = sv;
     my = fmaxf(my, sv);
   }
+#pragma unroll VP_NM_UNROLL
   for (int p = 0; p < Ww; ++p) {
     float sv = 0.f;
 #pragma unroll
@@ -166,12 +173,14 @@ __global__ __launch_bounds__(NM_NT) void null_key_mass_kernel(
   }
   float acc = 0.f;
   px[tid] = 0.f;
+#pragma unroll VP_NM_UNROLL
   for (int p = 0; p < Ww; ++p) {
     acc += __builtin_amdgcn_exp2f(px[(p + 1) * NM_NT + tid] - mx);
     px[(p + 1) * NM_NT + tid] = acc;
   }
   acc = 0.f;
   py[tid] = 0.f;
+#pragma unroll VP_NM_UNROLL
   for (int p = 0; p < Hh; ++p) {
     acc += __builtin_amdgcn_exp2f(py[(p + 1) * NM_NT + tid] - my);
     py[(p + 1) * NM_NT + tid] = acc;
