@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 17
+#define VP_ABI_VERSION 18
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
@@ -390,6 +390,16 @@ int vp_patchify_bf16(const void* src1, int32_t C1, const void* src2, int32_t C2,
  * mask_is_f32: 1 if mask is fp32, 0 if bf16. */
 int vp_patch_mask(const void* mask, int32_t mask_is_f32, uint8_t* out, int32_t B, int32_t F, int32_t H, int32_t W,
                   int32_t p, void* stream);
+
+/* Self-guidance after block i (cogvideox_transformer_3d.py:593-608): the unmasked video rows take the guidance
+ * states, then the branch injection is added — per row r of batch b (tok_mask[b, r] from vp_patch_mask):
+ *   tok_mask == 0:  x = guide                       (+ inject: rnd(guide + inject))
+ *   tok_mask != 0:  x unchanged                     (+ inject when inject_all: rnd(x + inject))
+ * x, guide, inject: bf16 [B, rows, D] at row stride ld_* and batch stride bs_*; inject NULL: none; inject_all: the
+ * reference's unmasked injection (no branch_block_masks).  D % 8 == 0, strides % 8 == 0.  (ABI 18.) */
+int vp_guide_rows_bf16(void* x, int64_t ld_x, int64_t bs_x, const void* guide, int64_t ld_g, int64_t bs_g,
+                       const void* inject, int64_t ld_i, int64_t bs_i, int32_t inject_all, const uint8_t* tok_mask,
+                       int64_t mask_bstride, int32_t B, int32_t rows, int32_t D, void* stream);
 
 /* unpatchify (cogvideox_transformer_3d.py:630-632): out[b,f,c,y*p+py,x*p+px] = proj[b, (f,y,x), c*p*p+py*p+px] */
 int vp_unpatchify_bf16(const void* proj, int64_t ld, void* out, int32_t B, int32_t F, int32_t C, int32_t H, int32_t W,

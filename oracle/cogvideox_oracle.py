@@ -318,8 +318,11 @@ def block_forward(sd: SD, p: str, cfg: dict, h, e, temb, rope, resample_mask=Non
 
 def transformer_forward(sd: SD, cfg: dict, hidden_states, encoder_hidden_states, timestep, image_rotary_emb=None,
                         attention_kwargs=None, branch_block_samples=None, branch_block_masks=None, add_first=False,
-                        return_hidden_states=False, return_resample_mask=False, id_pool_resample_learnable=False):
+                        return_hidden_states=False, return_resample_mask=False, id_pool_resample_learnable=False,
+                        self_guidance_hidden_states=None, self_guidance_masks=None):
     """`CogVideoXTransformer3DModel.forward` DF/models/transformers/cogvideox_transformer_3d.py:472-646.
+    self_guidance_masks replace branch_block_masks as the token mask (:518-523); the guidance states take the
+    unmasked video rows after every block, before the injection (:593-594).
 
     Returns the tuple form (`return_dict=False`, :638-645)."""
     dtype = hidden_states.dtype
@@ -330,7 +333,8 @@ def transformer_forward(sd: SD, cfg: dict, hidden_states, encoder_hidden_states,
     b, f, c, hh, ww = hidden_states.shape
     emb = time_embed(sd, timestep, inner, dtype)
     masks = None
-    x, tok_mask = patch_embed(sd, cfg, encoder_hidden_states, hidden_states, branch_block_masks)
+    x, tok_mask = patch_embed(sd, cfg, encoder_hidden_states, hidden_states,
+                              self_guidance_masks if self_guidance_masks is not None else branch_block_masks)
     if tok_mask is not None:
         masks = tok_mask.repeat(1, 1, x.shape[-1] // tok_mask.shape[-1])
     t = encoder_hidden_states.shape[1]
@@ -360,6 +364,8 @@ def transformer_forward(sd: SD, cfg: dict, hidden_states, encoder_hidden_states,
                     kw["prev_resample_mask"] = prm
         h, e = block_forward(sd, f"transformer_blocks.{i}", cfg, h, e, emb, image_rotary_emb, resample_mask, kw,
                              resample)
+        if self_guidance_hidden_states is not None:
+            h = torch.where(masks == False, self_guidance_hidden_states[i], h)  # noqa: E712
         if branch_block_samples is not None:
             if not add_first:
                 interval = int(np.ceil(nl / len(branch_block_samples)))

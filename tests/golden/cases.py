@@ -63,6 +63,18 @@ def tiny_inputs(dtype=torch.float32):
                 enc=cv(enc), timestep=torch.tensor([999, 377], dtype=torch.int64), rope=(cos, sin))
 
 
+def selfguide_inputs(dtype=torch.float32):
+    """Self-guidance inputs for the tiny transformer (cogvideox_transformer_3d.py:483-484, 518-523, 593-594): per-layer
+    guidance states for the video rows [B, Nv, D] and a second latent mask (its own rectangles) as
+    self_guidance_masks."""
+    b, f, h, w = 2, TINY_F, TINY_H, TINY_W
+    nv = f * (h // 2) * (w // 2)
+    d = TINY_CFG["num_attention_heads"] * TINY_CFG["attention_head_dim"]
+    cv = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dtype)  # noqa: E731
+    states = [cv(synth_tensor(f"sg.hs.{i}", (b, nv, d))) for i in range(TINY_CFG["num_layers"])]
+    return dict(states=states, mask=cv(make_mask(b, f, h, w, "sg.mask")))
+
+
 def full_block_case(seed: int = 0, dtype=torch.float32, latent=(3, 32, 48), key="fb"):
     """One full-width block (D=3072, 48 heads x 64, temb 512), B=1, T=226 text rows.  Default: config-1 shape (latent
     3x32x48 -> video 3x16x24 = 1152 tokens).  `latent=(13, 90, 160), key="fb5"` is config 5 (720x1280: 13x45x80 =

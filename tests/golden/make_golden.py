@@ -14,6 +14,7 @@ Fixtures (all fp32):
   config4.safetensors   — the 42-layer ID-resample transformer + branch at N = 17 776, B = 1: window 0 and a later
                           window with prev_hidden_states / prev_clip_weight 0.5 (fp32 + bf16 slices).
   wo_text.safetensors   — the tiny branch with wo_text=True (blocks on the video tokens alone), fp32 and bf16.
+  selfguide.safetensors — the tiny transformer with self-guidance states / masks (three mask combinations).
   sched.safetensors     — CogVideoXDPMScheduler: trailing timesteps, 3 steps incl. the 2nd-order branch, add_noise.
   pipe_tiny.safetensors — CogVideoXI2VDualInpaintAnyLPipeline, tiny model + tiny VAE, 2 windows x 2 steps, ID-resample
                           with prev_clip_weight 0.5: the VAE-side latents it produced (captured), every scheduler noise
@@ -125,6 +126,28 @@ def make_tiny():
             return_dict=False)[0]
     out["resample1.out"] = o
     _save("tiny.safetensors", out)
+
+
+@torch.no_grad()
+def make_selfguide():
+    """The tiny transformer with self-guidance inputs (cogvideox_transformer_3d.py:483-484, 518-523, 593-608):
+    self_guidance_masks replacing branch_block_masks as the token / injection mask, the guidance states taking the
+    unmasked video rows after every block before the branch injection; the three combinations of the two masks."""
+    from tests.golden.cases import selfguide_inputs
+    inp = tiny_inputs()
+    sg = selfguide_inputs()
+    tr, br = build_models(False)
+    rope = inp["rope"]
+    bs = br(hidden_states=inp["video"], encoder_hidden_states=inp["enc"], branch_cond=inp["branch_cond"],
+            timestep=inp["timestep"], image_rotary_emb=rope, return_dict=False)[0]
+    common = dict(hidden_states=inp["hidden"], encoder_hidden_states=inp["enc"], timestep=inp["timestep"],
+                  image_rotary_emb=rope, branch_block_samples=bs, self_guidance_hidden_states=sg["states"],
+                  return_dict=False)
+    out = {}
+    out["sg_masks.out"] = tr(branch_block_masks=inp["mask"], self_guidance_masks=sg["mask"], **common)[0]
+    out["sg_branchmask.out"] = tr(branch_block_masks=inp["mask"], **common)[0]
+    out["sg_nobranchmask.out"] = tr(branch_block_masks=None, self_guidance_masks=sg["mask"], **common)[0]
+    _save("selfguide.safetensors", out)
 
 
 @torch.no_grad()
@@ -798,6 +821,8 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["tiny", "sched", "pipe", "block"]
     if "wo_text" in which:
         make_wo_text()
+    if "selfguide" in which:
+        make_selfguide()
     if "config1" in which:
         make_config1()
     if "config2" in which:

@@ -143,6 +143,36 @@ def test_transformer_matches_reference(env, mode):
 
 
 @torch.no_grad()
+@pytest.mark.parametrize("mode", ["sg_masks", "sg_branchmask", "sg_nobranchmask"])
+def test_transformer_self_guidance_matches_reference(env, mode):
+    """Self-guidance (cogvideox_transformer_3d.py:483-484, 518-523, 593-608) against the reference's fp32 run
+    (tests/golden/selfguide.safetensors, make_golden.py selfguide): self_guidance_masks as the token / injection mask,
+    the guidance states on the unmasked video rows before the injection (vp_guide_rows_bf16 after a block run without
+    its fused injection); gate from the oracle's own bf16 run of the same inputs."""
+    from oracle import cogvideox_oracle as O
+    from tests.golden.cases import selfguide_inputs
+    i, g = env["inp"], env["g"]
+    sg = selfguide_inputs()
+    gold = load_file(os.path.join(GOLD, "selfguide.safetensors"))[f"{mode}.out"]
+    bs = [g["branch.0"], g["branch.1"]]
+    bm = None if mode == "sg_nobranchmask" else i["mask"]
+    sm = None if mode == "sg_branchmask" else sg["mask"]
+    res = env["tr"](hidden_states=_d(i["hidden"]), encoder_hidden_states=_d(i["enc"]), timestep=i["timestep"].to(dev),
+                    image_rotary_emb=i["rope"], branch_block_samples=[_d(b) for b in bs], branch_block_masks=bm,
+                    self_guidance_hidden_states=[_d(h) for h in sg["states"]], self_guidance_masks=sm,
+                    return_dict=False)
+    o = O.transformer_forward(env["tsd16"], env["tcfg"], _b16(i["hidden"]), _b16(i["enc"]), i["timestep"], i["rope"],
+                              branch_block_samples=[_b16(b) for b in bs], branch_block_masks=bm,
+                              self_guidance_hidden_states=[_b16(h) for h in sg["states"]], self_guidance_masks=sm)
+    assert res[0].shape == gold.shape
+    assert rel(res[0], gold) <= bound(o[0], gold), (rel(res[0], gold), rel(o[0], gold))
+    with pytest.raises(ValueError):  # guidance states without any mask: the reference's unbound `masks`
+        env["tr"](hidden_states=_d(i["hidden"]), encoder_hidden_states=_d(i["enc"]), timestep=i["timestep"].to(dev),
+                  image_rotary_emb=i["rope"], self_guidance_hidden_states=[_d(h) for h in sg["states"]],
+                  return_dict=False)
+
+
+@torch.no_grad()
 def test_fused_qkv_norm_rope_bit_exact_vs_separate_launches(env, knobs):
     """The QKV GEMM with the qk-norm + RoPE epilogue (default) gives the model output of the separate
     vp_head_norm_rope_bf16 launches (VP_NO_QKV_FUSION=1) bit for bit, incl. the returned hidden states."""

@@ -87,6 +87,25 @@ def test_transformer_modes(tiny, mode):
     assert rel(out, g[f"{mode}.out"]) < 1e-5
 
 
+@pytest.mark.parametrize("mode", ["sg_masks", "sg_branchmask", "sg_nobranchmask"])
+def test_transformer_self_guidance(tiny, mode):
+    """Self-guidance (cogvideox_transformer_3d.py:483-484, 518-523, 593-608) against the reference's own run
+    (tests/golden/selfguide.safetensors): the guidance states take the unmasked video rows before the injection;
+    self_guidance_masks, when given, are the token mask of the injection too."""
+    from tests.golden.cases import selfguide_inputs
+    i = tiny["inp"]
+    g = tiny["gold"]
+    sg = selfguide_inputs()
+    gold = load_file(os.path.join(GOLD, "selfguide.safetensors"))
+    kw = dict(branch_block_samples=[g["branch.0"], g["branch.1"]], self_guidance_hidden_states=sg["states"],
+              branch_block_masks=None if mode == "sg_nobranchmask" else i["mask"],
+              self_guidance_masks=None if mode == "sg_branchmask" else sg["mask"])
+    out = O.transformer_forward(tiny["tsd"], tiny["tcfg"], i["hidden"], i["enc"], i["timestep"], i["rope"], **kw)[0]
+    assert rel(out, gold[f"{mode}.out"]) < 1e-5
+    # the guidance changes the output (a different function than the plain masked run)
+    assert rel(out, g["std.out"]) > 1e-3
+
+
 def test_transformer_resample(tiny):
     i = tiny["inp"]
     g = tiny["gold"]

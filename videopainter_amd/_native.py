@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -129,6 +129,7 @@ _SIGS = {
     "vp_patchify_bf16": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32, vp]),
     "vp_patch_mask": (i32, [vp, i32, vp, i32, i32, i32, i32, i32, vp]),
     "vp_unpatchify_bf16": (i32, [vp, i64, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "vp_guide_rows_bf16": (i32, [vp, i64, i64, vp, i64, i64, vp, i64, i64, i32, vp, i64, i32, i32, i32, vp]),
     "vp_dpm_step_bf16": (i32, [C.POINTER(DpmDesc), vp]),
     "vp_fill_normal_bf16": (i32, [vp, i64, C.c_uint64, f32, f32, vp]),
     "vp_conv3d_bf16": (i32, [C.POINTER(Conv3dDesc), vp]),

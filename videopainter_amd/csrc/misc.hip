@@ -131,6 +131,29 @@ __global__ void patch_mask_kernel(const void* __restrict__ mask, int is_f32, uin
   out[i] = (s / (float)(p * p)) > 0.f ? 1 : 0;
 }
 
+// one thread per 8 columns of one row (self-guidance + injection after a block, vp_guide_rows_bf16)
+__global__ void guide_rows_kernel(bf16* __restrict__ x, int64_t ld_x, int64_t bs_x, const bf16* __restrict__ g,
+                                  int64_t ld_g, int64_t bs_g, const bf16* __restrict__ inj, int64_t ld_i, int64_t bs_i,
+                                  int inject_all, const uint8_t* __restrict__ mask, int64_t mask_bs, int rows, int D,
+                                  int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c8 = D / 8;
+  const int c = (int)(i % c8) * 8;
+  const int64_t br = i / c8;
+  const int r = (int)(br % rows), b = (int)(br / rows);
+  const bool keep = mask[(int64_t)b * mask_bs + r] != 0;
+  if (keep && !(inj != nullptr && inject_all)) return;  // a masked row without injection: unchanged
+  bf16* xp = x + (int64_t)b * bs_x + (int64_t)r * ld_x + c;
+  bf16x8 v = keep ? *(const bf16x8*)xp : *(const bf16x8*)(g + (int64_t)b * bs_g + (int64_t)r * ld_g + c);
+  if (inj != nullptr) {
+    const bf16x8 a = *(const bf16x8*)(inj + (int64_t)b * bs_i + (int64_t)r * ld_i + c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(a[e]));
+  }
+  *(bf16x8*)xp = v;
+}
+
 __global__ void unpatchify_kernel(const bf16* __restrict__ proj, int64_t ld, bf16* __restrict__ out, int B, int F,
                                   int C, int H, int W, int p) {
   const int64_t total = (int64_t)B * F * C * H * W;
@@ -370,6 +393,21 @@ extern "C" int vp_patch_mask(const void* mask, int32_t mask_is_f32, uint8_t* out
   const int64_t total = (int64_t)B * F * (H / p) * (W / p);
   hipLaunchKernelGGL(patch_mask_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, mask,
                      mask_is_f32, out, B, F, H, W, p);
+  VP_CHECK_LAUNCH();
+  return VP_OK;
+}
+
+extern "C" int vp_guide_rows_bf16(void* x, int64_t ld_x, int64_t bs_x, const void* guide, int64_t ld_g, int64_t bs_g,
+                                  const void* inject, int64_t ld_i, int64_t bs_i, int32_t inject_all,
+                                  const uint8_t* tok_mask, int64_t mask_bstride, int32_t B, int32_t rows, int32_t D,
+                                  void* stream) {
+  if (!x || !guide || !tok_mask || B <= 0 || rows <= 0 || D <= 0 || (D % 8)) return VP_ERR_ARG;
+  if ((ld_x % 8) || (bs_x % 8) || (ld_g % 8) || (bs_g % 8) || ld_x < D || ld_g < D) return VP_ERR_ARG;
+  if (inject && ((ld_i % 8) || (bs_i % 8) || ld_i < D)) return VP_ERR_ARG;
+  const int64_t total = (int64_t)B * rows * (D / 8);
+  hipLaunchKernelGGL(guide_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (bf16*)x, ld_x, bs_x, (const bf16*)guide, ld_g, bs_g, (const bf16*)inject, ld_i, bs_i, inject_all,
+                     tok_mask, mask_bstride, rows, D, total);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }

@@ -841,6 +841,25 @@ def patch_mask(mask: torch.Tensor, p: int) -> torch.Tensor:
     return out
 
 
+def guide_rows(x: torch.Tensor, guide: torch.Tensor, tok_mask: torch.Tensor, inject: Optional[torch.Tensor] = None,
+               inject_all: bool = False) -> torch.Tensor:
+    """Self-guidance after a block (vp_guide_rows_bf16), in place on the video rows x [B, rows, D]: rows whose
+    tok_mask is 0 take `guide`, then `inject` is added on those rows (on every row with inject_all)."""
+    for t, n in ((x, "x"), (guide, "guide")) + (((inject, "inject"),) if inject is not None else ()):
+        _chk(t, n)
+        if t.dim() != 3 or t.stride(-1) != 1 or tuple(t.shape) != tuple(x.shape):
+            raise ValueError(f"{n} must be [B, rows, D] with a contiguous last dim, shaped like x")
+    _chk(tok_mask, "tok_mask", torch.uint8)
+    B, R, D = x.shape
+    if tok_mask.dim() != 2 or tuple(tok_mask.shape) != (B, R) or tok_mask.stride(-1) != 1:
+        raise ValueError(f"tok_mask must be uint8 [{B}, {R}]")
+    ld_i, bs_i = (inject.stride(1), inject.stride(0)) if inject is not None else (0, 0)
+    N.check(N.lib().vp_guide_rows_bf16(_p(x), x.stride(1), x.stride(0), _p(guide), guide.stride(1), guide.stride(0),
+                                       _p(inject), ld_i, bs_i, int(bool(inject_all)), _p(tok_mask), tok_mask.stride(0),
+                                       B, R, D, _stream()), "vp_guide_rows_bf16")
+    return x
+
+
 def unpatchify(proj: torch.Tensor, B: int, F: int, Cout: int, H: int, W: int, p: int) -> torch.Tensor:
     _chk(proj, "proj")
     out = torch.empty(B, F, Cout, H, W, device=proj.device, dtype=BF16)

@@ -568,14 +568,14 @@ class CogVideoXTransformer3DModel(ModelMixin):
         (videopainter_amd/autograd.py: gradient-checkpointed blocks on the HIP backward kernels) runs instead."""
         from . import autograd as AG
         if AG.needs_grad(self, hidden_states, encoder_hidden_states, branch_block_samples):
+            if self_guidance_hidden_states is not None or self_guidance_masks is not None:
+                raise NotImplementedError("self-guidance is inference-only (no training script passes it)")
             return self._forward_train(hidden_states, encoder_hidden_states, timestep, image_rotary_emb,
                                        attention_kwargs, branch_block_samples, branch_block_masks, add_first,
                                        self_guidance_hidden_states, return_hidden_states, return_resample_mask,
                                        id_pool_resample_learnable, timestep_cond, return_dict)
         if timestep_cond is not None:
             raise ValueError("timestep_cond requires a cond_proj, which CogVideoX's TimestepEmbedding does not have")
-        if self_guidance_hidden_states is not None or self_guidance_masks is not None:
-            raise NotImplementedError("self-guidance inputs belong to the self-guidance pipelines (out of scope)")
         attention_kwargs = dict(attention_kwargs) if attention_kwargs is not None else None
         # LoRA scale per call, default 1.0 (reference :490-499): the folded adapters are re-folded when it changes
         self._call_lora_scale(attention_kwargs)
@@ -594,9 +594,15 @@ class CogVideoXTransformer3DModel(ModelMixin):
 
         emb = self._time_embed(timestep, B, dev)
         x = self.patch_embed.embed(enc, hs)
+        # the token mask: from self_guidance_masks when given, else from branch_block_masks (reference :518-523); it
+        # is the injection mask (when branch_block_masks is given), the resample mask and the self-guidance mask
         tok_mask = None
-        if branch_block_masks is not None:
-            tok_mask = K.patch_mask(branch_block_masks.to(dev), p)
+        mask_src = self_guidance_masks if self_guidance_masks is not None else branch_block_masks
+        if mask_src is not None:
+            tok_mask = K.patch_mask(mask_src.to(dev), p)
+        if self_guidance_hidden_states is not None and tok_mask is None:
+            # the reference reads an unbound `masks` here; we fail explicitly
+            raise ValueError("self_guidance_hidden_states need self_guidance_masks or branch_block_masks")
         resample_mask = None
         if id_pool_resample_learnable or return_resample_mask:
             if tok_mask is None:
@@ -637,9 +643,17 @@ class CogVideoXTransformer3DModel(ModelMixin):
             else:
                 out = ping if (ping is not None and ping.data_ptr() != x.data_ptr()) else torch.empty_like(x)
                 ping = x
+            guide = None
+            if self_guidance_hidden_states is not None:
+                guide = _bf(self_guidance_hidden_states[i].to(dev))
+            # (self-guidance replaces the unmasked video rows BEFORE the injection, reference :593-608: the block then
+            # runs without its fused injection, and vp_guide_rows_bf16 applies both)
             x = block.forward_joint(x, T, emb, rope, rm_u8, pj, prev_w if pj is not None else None,
-                                    prev_mask if pj is not None else None, inj,
+                                    prev_mask if pj is not None else None, inj if guide is None else None,
                                     tok_mask if (inj is not None and branch_block_masks is not None) else None, out)
+            if guide is not None:
+                xv = x[:, T:]
+                K.guide_rows(xv, guide.expand_as(xv), tok_mask, inj, inject_all=branch_block_masks is None)
             if return_hidden_states:
                 hidden_states_list.append(x)
 
