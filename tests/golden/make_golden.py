@@ -168,6 +168,13 @@ def make_wo_text():
                 wo_text=True, return_dict=False)[0]
         for j, s in enumerate(bs):
             out[f"wo_text.{tag}.{j}"] = s
+        # without RoPE the reference's wo_text processor never attends (attention_processor.py:2349-2358): its head
+        # merge scrambles the processor's input, which goes on to to_out
+        bs = br(hidden_states=inp["video"].to(dt), encoder_hidden_states=inp["enc"].to(dt),
+                branch_cond=inp["branch_cond"].to(dt), timestep=inp["timestep"], image_rotary_emb=None,
+                wo_text=True, return_dict=False)[0]
+        for j, s in enumerate(bs):
+            out[f"wo_text_norope.{tag}.{j}"] = s
     _save("wo_text.safetensors", out)
 
 

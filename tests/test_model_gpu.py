@@ -101,6 +101,13 @@ def test_branch_wo_text_matches_reference(env):
         r, r16 = rel(bs[j], want), rel(ref16, want)
         print(f"wo_text branch.{j}: HIP {r:.3e} reference bf16 {r16:.3e}")
         assert r <= gate(r16), (j, r, r16)
+    # without RoPE the reference's processor never attends: its head merge scrambles the input (:2349-2358)
+    bs = br(wo_text=True, **dict(kw, image_rotary_emb=None))[0]
+    for j in range(2):
+        want, ref16 = g[f"wo_text_norope.f32.{j}"], g[f"wo_text_norope.bf16.{j}"]
+        r, r16 = rel(bs[j], want), rel(ref16, want)
+        print(f"wo_text branch.{j}, no RoPE: HIP {r:.3e} reference bf16 {r16:.3e}")
+        assert r <= gate(r16), (j, r, r16)
     with pytest.raises(ValueError):
         br(wo_text=False, **kw)
     with pytest.raises(ValueError):

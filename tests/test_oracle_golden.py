@@ -54,6 +54,11 @@ def test_branch_wo_text(tiny):
         assert rel(o, gold[f"wo_text.f32.{j}"]) <= 1e-5, j
         # a different function of the inputs than the text-conditioned branch
         assert rel(o, tiny["gold"][f"branch.{j}"]) > 1e-4
+    # no RoPE: the reference's processor never attends and scrambles its input (attention_processor.py:2349-2358)
+    outs = O.branch_forward(tiny["bsd"], tiny["bcfg"], i["video"], i["enc"], i["branch_cond"], i["timestep"], None,
+                            wo_text=True)
+    for j, o in enumerate(outs):
+        assert rel(o, gold[f"wo_text_norope.f32.{j}"]) <= 1e-5, j
 
 
 def test_transformer_std_with_hidden_states(tiny):

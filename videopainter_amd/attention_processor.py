@@ -277,15 +277,24 @@ class CogVideoXAttnProcessor2_0_wo_text(CogVideoXAttnProcessor2_0):
     """HIP restatement of `CogVideoXAttnProcessor2_0_wo_text.__call__` (attention_processor.py:2306-2366): the
     branch's text-free mode, self-attention over the video tokens alone with RoPE on every token — `attend` with
     text_len = 0.  Without RoPE the reference never runs its attention (the call sits inside its
-    `if image_rotary_emb is not None:`, :2349-2356) and projects its scrambled input instead; that form is not
-    restated: no RoPE raises."""
+    `if image_rotary_emb is not None:`, :2349-2356): its head merge (:2358, `transpose(1, 2).reshape(B, -1, D)`)
+    then scrambles the processor's INPUT, which goes on to to_out — restated as that exact permutation (attend)."""
+
+    def attend(self, attn, x: torch.Tensor, text_len: int, image_rotary_emb=None, *args, **kwargs) -> torch.Tensor:
+        if image_rotary_emb is not None:
+            return super().attend(attn, x, text_len, image_rotary_emb, *args, **kwargs)
+        # no RoPE: o[b] = x[b]^T read back as [N, D] rows (the reference's transpose + reshape of a [B, N, D] tensor);
+        # the Q / K / V it computes and drops are skipped
+        B, N, D = x.shape
+        o = torch.empty(B, N, D, device=x.device, dtype=BF16)
+        for b in range(B):
+            K.transpose(x[b], out=o[b].view(D, N))
+        return o
 
     def __call__(self, attn, hidden_states: torch.Tensor, encoder_hidden_states: Optional[torch.Tensor] = None,
                  attention_mask: Optional[torch.Tensor] = None, image_rotary_emb=None) -> torch.Tensor:
         if attention_mask is not None:
             raise NotImplementedError("attention_mask is never set on the CogVideoX path (SURVEY.md §3.2)")
-        if image_rotary_emb is None:
-            raise ValueError("the wo_text processor attends only with image_rotary_emb (attention_processor.py:2349)")
         x = hidden_states.to(BF16).contiguous()
         o = self.attend(attn, x, 0, image_rotary_emb)
         out = torch.empty_like(o)

@@ -129,8 +129,9 @@ class CogvideoXBranchModel(CogVideoXTransformer3DModel):
             raise ValueError(f"forward(wo_text={bool(wo_text)}) on a branch built with wo_text={self.wo_text} (the "
                              "reference's blocks take the matching processor at construction, "
                              "cogvideox_transformer_3d.py:96-97)")
-        if wo_text and image_rotary_emb is None:
-            raise ValueError("wo_text attends only with image_rotary_emb (attention_processor.py:2349)")
+        if wo_text and image_rotary_emb is None and train:
+            raise NotImplementedError("wo_text without image_rotary_emb (the reference's attention-free quirk, "
+                                      "attention_processor.py:2349-2358) is inference-only")
         if timestep_cond is not None:
             raise ValueError("timestep_cond requires a cond_proj, which CogVideoX's TimestepEmbedding does not have")
         dev = self.proj_out.weight.device
