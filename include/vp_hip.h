@@ -343,7 +343,8 @@ int vp_partition_rows_index(const uint8_t* mask, int64_t mask_bstride, int32_t B
  * vp_null_key_mass: out[b, h, n] = log2 of sum over the null keys of exp2(scale * log2 e * q[b, n, h] . k_null),
  *   -inf when there is none.  q: the normed + rotated queries [B, N, H*64] bf16 (strides in elements),
  *   N = T + F*Hh*Ww; beta bf16 [64]; the per-axis RoPE tables fp32: cos_t / sin_t [F][16], cos_y / sin_y [Hh][24],
- *   cos_x / sin_x [Ww][24].  F <= 16, Hh <= 64, Ww <= 255, vp_null_key_mass_lds_bytes <= 160 KiB. */
+ *   cos_x / sin_x [Ww][24].  segs / meta as vp_mask_null_segments wrote them (all B*F*Hh record slots are read,
+ *   used or not).  F <= 16, Hh <= 64, Ww <= 255, vp_null_key_mass_lds_bytes <= 160 KiB. */
 int vp_mask_null_segments(const uint8_t* mask, int64_t mask_bstride, int32_t B, int32_t T, int32_t F, int32_t Hh,
                           int32_t Ww, void* segs, int32_t* meta, void* stream);
 int64_t vp_null_key_mass_lds_bytes(int32_t F, int32_t Hh, int32_t Ww);

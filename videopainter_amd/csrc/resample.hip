@@ -27,6 +27,12 @@ constexpr int NM_MAXH = 64;  // rows per frame: one lane each in the segment ker
 #ifndef VP_NM_UNROLL
 #define VP_NM_UNROLL 4
 #endif
+// query chunks of NM_NT per block: the block's prologue (the key-piece tables and segment records into LDS, a chain of
+// dependent global loads) is paid once per NM_CH chunks
+constexpr int NM_CH = 4;
+// (Measured and dropped, profiles/r05_null_key_mass_ab.log: the per-axis scores of a wave's 64 queries as 32x32x16
+// MFMAs written to LDS for the same per-query pass — 0.79 against 0.47 ms at config 4: the dot products are not what
+// the kernel waits on, the extra LDS pass of the scores is.)
 
 // one wave per (b, t): lane y finds the null runs of row y, equal neighbouring rows merge into segments.
 // segs[((b F + t) Hh + i)] (16 bytes): byte 0 = y0, 1 = y1 (exclusive), 2 = run count (255: scan the row),
@@ -104,7 +110,7 @@ __global__ __launch_bounds__(NM_NT) void null_key_mass_kernel(
   float* py = (float*)(nseg + ((F + 1 + 3) & ~3));
   float* px = py + (Hh + 1) * NM_NT;
   const int tid = threadIdx.x;
-  const int nqb = (N + NM_NT - 1) / NM_NT;
+  const int nqb = (N + NM_NT * NM_CH - 1) / (NM_NT * NM_CH);
   const int bh = blockIdx.x / nqb, qb = blockIdx.x - bh * nqb;
   const int b = bh / H, h = bh - b * H;
 
@@ -113,119 +119,128 @@ __global__ __launch_bounds__(NM_NT) void null_key_mass_kernel(
     const float b0 = bf2f(beta[d & ~1]), b1 = bf2f(beta[d | 1]);
     return (d & 1) ? rbf16(b1 * cs + b0 * sn) : rbf16(b0 * cs - b1 * sn);
   };
+  // (independent loads, unrolled so they are in flight together; every segment record slot is copied, used or not,
+  // so no copy waits for the record counts)
+#pragma unroll 4
   for (int i = tid; i < F * 16; i += NM_NT) kt[i] = rot(i & 15, ct[i], st[i]);
+#pragma unroll 4
   for (int i = tid; i < Hh * 24; i += NM_NT) ky[i] = rot(16 + i % 24, cy[i], sy[i]);
+#pragma unroll 4
   for (int i = tid; i < Ww * 24; i += NM_NT) kx[i] = rot(40 + i % 24, cx[i], sx[i]);
-  for (int t = 0; t < F; ++t) {
-    const int ns = meta[b * F + t];
-    for (int i = tid; i < ns; i += NM_NT) sg[t * Hh + i] = segs[((int64_t)b * F + t) * Hh + i];
-  }
+#pragma unroll 4
+  for (int i = tid; i < F * Hh; i += NM_NT) sg[i] = segs[(int64_t)b * F * Hh + i];
   if (tid < F) nseg[tid] = meta[b * F + tid];
   if (tid == 0) nseg[F] = meta[B * F + b];
   __syncthreads();
 
-  const int qi = qb * NM_NT + tid;
-  const int qc = qi < N ? qi : N - 1;
-  const bf16* qrow = q + (int64_t)b * q_sb + (int64_t)qc * q_sn + h * 64;
-  float qs[64];
+#pragma unroll 1
+  for (int ch = 0; ch < NM_CH; ++ch) {
+    const int q0 = (qb * NM_CH + ch) * NM_NT;
+    if (q0 >= N) break;  // (block-uniform)
+    const int qi = q0 + tid;
+    const int qc = qi < N ? qi : N - 1;
+    const bf16* qrow = q + (int64_t)b * q_sb + (int64_t)qc * q_sn + h * 64;
+    float qs[64];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bf16x8 qv = *(const bf16x8*)(qrow + 8 * j);
+    for (int j = 0; j < 8; ++j) {
+      const bf16x8 qv = *(const bf16x8*)(qrow + 8 * j);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) qs[8 * j + e] = bf2f(qv[e]);
-  }
-  float s_text = 0.f;  // text rows: their null keys are beta itself (no rotation)
-#pragma unroll
-  for (int d = 0; d < 64; ++d) s_text += qs[d] * bf2f(beta[d]);
-  s_text *= c;
-
-  float et[NM_MAXF];
-  float mt = -INFINITY, my = -INFINITY, mx = -INFINITY;
-#pragma unroll
-  for (int p = 0; p < NM_MAXF; ++p) {
-    float sv = -INFINITY;
-    if (p < F) {
-      sv = 0.f;
-#pragma unroll
-      for (int dd = 0; dd < 16; ++dd) sv += qs[dd] * kt[p * 16 + dd];
-      sv *= c;
+      for (int e = 0; e < 8; ++e) qs[8 * j + e] = bf2f(qv[e]);
     }
-    et[p] = sv;
-    mt = fmaxf(mt, sv);
-  }
-#pragma unroll VP_NM_UNROLL
-  for (int p = 0; p < Hh; ++p) {
-    float sv = 0.f;
+    float s_text = 0.f;  // text rows: their null keys are beta itself (no rotation)
 #pragma unroll
-    for (int dd = 0; dd < 24; ++dd) sv += qs[16 + dd] * ky[p * 24 + dd];
-    sv *= c;
-    py[(p + 1) * NM_NT + tid] = sv;
-    my = fmaxf(my, sv);
-  }
-#pragma unroll VP_NM_UNROLL
-  for (int p = 0; p < Ww; ++p) {
-    float sv = 0.f;
-#pragma unroll
-    for (int dd = 0; dd < 24; ++dd) sv += qs[40 + dd] * kx[p * 24 + dd];
-    sv *= c;
-    px[(p + 1) * NM_NT + tid] = sv;
-    mx = fmaxf(mx, sv);
-  }
-  float acc = 0.f;
-  px[tid] = 0.f;
-#pragma unroll VP_NM_UNROLL
-  for (int p = 0; p < Ww; ++p) {
-    acc += __builtin_amdgcn_exp2f(px[(p + 1) * NM_NT + tid] - mx);
-    px[(p + 1) * NM_NT + tid] = acc;
-  }
-  acc = 0.f;
-  py[tid] = 0.f;
-#pragma unroll VP_NM_UNROLL
-  for (int p = 0; p < Hh; ++p) {
-    acc += __builtin_amdgcn_exp2f(py[(p + 1) * NM_NT + tid] - my);
-    py[(p + 1) * NM_NT + tid] = acc;
-  }
-#pragma unroll
-  for (int p = 0; p < NM_MAXF; ++p) et[p] = p < F ? __builtin_amdgcn_exp2f(et[p] - mt) : 0.f;
+    for (int d = 0; d < 64; ++d) s_text += qs[d] * bf2f(beta[d]);
+    s_text *= c;
 
-  const uint8_t* mv = mask + (int64_t)b * mask_bs + T;
-  float zv = 0.f;
+    float et[NM_MAXF];
+    float mt = -INFINITY, my = -INFINITY, mx = -INFINITY;
 #pragma unroll
-  for (int t = 0; t < NM_MAXF; ++t) {
-    if (t >= F) break;
-    const int ns = nseg[t];
-    float zt = 0.f;
-    for (int i = 0; i < ns; ++i) {
-      const uint4 r = sg[t * Hh + i];
-      const int y0 = r.x & 255, y1 = (r.x >> 8) & 255, n = (r.x >> 16) & 255;
-      const float ey = py[y1 * NM_NT + tid] - py[y0 * NM_NT + tid];
-      float zx = 0.f;
-      if (n != 255) {
-        const uint32_t w[3] = {r.y, r.z, r.w};
+    for (int p = 0; p < NM_MAXF; ++p) {
+      float sv = -INFINITY;
+      if (p < F) {
+        sv = 0.f;
 #pragma unroll
-        for (int k = 0; k < NM_R; ++k) {
-          if (k >= n) break;
-          const uint32_t pr = w[k >> 1] >> (16 * (k & 1));
-          zx += px[((pr >> 8) & 255) * NM_NT + tid] - px[(pr & 255) * NM_NT + tid];
-        }
-      } else {  // many runs: per column
-        const uint8_t* mr = mv + ((int64_t)t * Hh + y0) * Ww;
-        for (int x = 0; x < Ww; ++x)
-          if (mr[x] == 0) zx += px[(x + 1) * NM_NT + tid] - px[x * NM_NT + tid];
+        for (int dd = 0; dd < 16; ++dd) sv += qs[dd] * kt[p * 16 + dd];
+        sv *= c;
       }
-      zt += ey * zx;
+      et[p] = sv;
+      mt = fmaxf(mt, sv);
     }
-    zv += et[t] * zt;
+#pragma unroll VP_NM_UNROLL
+    for (int p = 0; p < Hh; ++p) {
+      float sv = 0.f;
+#pragma unroll
+      for (int dd = 0; dd < 24; ++dd) sv += qs[16 + dd] * ky[p * 24 + dd];
+      sv *= c;
+      py[(p + 1) * NM_NT + tid] = sv;
+      my = fmaxf(my, sv);
+    }
+#pragma unroll VP_NM_UNROLL
+    for (int p = 0; p < Ww; ++p) {
+      float sv = 0.f;
+#pragma unroll
+      for (int dd = 0; dd < 24; ++dd) sv += qs[40 + dd] * kx[p * 24 + dd];
+      sv *= c;
+      px[(p + 1) * NM_NT + tid] = sv;
+      mx = fmaxf(mx, sv);
+    }
+    float acc = 0.f;
+    px[tid] = 0.f;
+#pragma unroll VP_NM_UNROLL
+    for (int p = 0; p < Ww; ++p) {
+      acc += __builtin_amdgcn_exp2f(px[(p + 1) * NM_NT + tid] - mx);
+      px[(p + 1) * NM_NT + tid] = acc;
+    }
+    acc = 0.f;
+    py[tid] = 0.f;
+#pragma unroll VP_NM_UNROLL
+    for (int p = 0; p < Hh; ++p) {
+      acc += __builtin_amdgcn_exp2f(py[(p + 1) * NM_NT + tid] - my);
+      py[(p + 1) * NM_NT + tid] = acc;
+    }
+#pragma unroll
+    for (int p = 0; p < NM_MAXF; ++p) et[p] = p < F ? __builtin_amdgcn_exp2f(et[p] - mt) : 0.f;
+
+    const uint8_t* mv = mask + (int64_t)b * mask_bs + T;
+    float zv = 0.f;
+#pragma unroll
+    for (int t = 0; t < NM_MAXF; ++t) {
+      if (t >= F) break;
+      const int ns = nseg[t];
+      float zt = 0.f;
+      for (int i = 0; i < ns; ++i) {
+        const uint4 r = sg[t * Hh + i];
+        const int y0 = r.x & 255, y1 = (r.x >> 8) & 255, n = (r.x >> 16) & 255;
+        const float ey = py[y1 * NM_NT + tid] - py[y0 * NM_NT + tid];
+        float zx = 0.f;
+        if (n != 255) {
+          const uint32_t w[3] = {r.y, r.z, r.w};
+#pragma unroll
+          for (int k = 0; k < NM_R; ++k) {
+            if (k >= n) break;
+            const uint32_t pr = w[k >> 1] >> (16 * (k & 1));
+            zx += px[((pr >> 8) & 255) * NM_NT + tid] - px[(pr & 255) * NM_NT + tid];
+          }
+        } else {  // many runs: per column
+          const uint8_t* mr = mv + ((int64_t)t * Hh + y0) * Ww;
+          for (int x = 0; x < Ww; ++x)
+            if (mr[x] == 0) zx += px[(x + 1) * NM_NT + tid] - px[x * NM_NT + tid];
+        }
+        zt += ey * zx;
+      }
+      zv += et[t] * zt;
+    }
+    if (qi < N) {
+      // log2(text_null 2^s_text + zv 2^(mt + my + mx)), stably
+      const int tn = nseg[F];
+      const float lt = tn > 0 ? s_text + __log2f((float)tn) : -INFINITY;
+      const float lv = zv > 0.f ? mt + my + mx + __log2f(zv) : -INFINITY;
+      const float mm = fmaxf(lt, lv);
+      float res = -INFINITY;
+      if (mm > -INFINITY) res = mm + __log2f(__builtin_amdgcn_exp2f(lt - mm) + __builtin_amdgcn_exp2f(lv - mm));
+      out[((int64_t)b * H + h) * N + qi] = res;
+    }
   }
-  if (qi >= N) return;
-  // log2(text_null 2^s_text + zv 2^(mt + my + mx)), stably
-  const int tn = nseg[F];
-  const float lt = tn > 0 ? s_text + __log2f((float)tn) : -INFINITY;
-  const float lv = zv > 0.f ? mt + my + mx + __log2f(zv) : -INFINITY;
-  const float mm = fmaxf(lt, lv);
-  float res = -INFINITY;
-  if (mm > -INFINITY) res = mm + __log2f(__builtin_amdgcn_exp2f(lt - mm) + __builtin_amdgcn_exp2f(lv - mm));
-  out[((int64_t)b * H + h) * N + qi] = res;
 }
 
 }  // namespace
@@ -259,14 +274,14 @@ extern "C" int vp_null_key_mass(const void* q, int64_t q_sb, int64_t q_sn, int32
   if ((int64_t)T + (int64_t)F * Hh * Ww != N || (q_sn % 8) || (q_sb % 8)) return VP_ERR_ARG;
   const int64_t lds = vp_null_key_mass_lds_bytes(F, Hh, Ww);
   if (lds > 160 * 1024) return VP_ERR_UNSUPPORTED;
+  const void* kern = (const void*)null_key_mass_kernel;
   static int64_t attr = 64 * 1024;  // dynamic LDS the kernel may take (raised on demand)
   if (lds > attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)null_key_mass_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     attr = lds;
   }
-  const int64_t nblk = (int64_t)B * H * ((N + NM_NT - 1) / NM_NT);
+  const int64_t nblk = (int64_t)B * H * ((N + NM_NT * NM_CH - 1) / (NM_NT * NM_CH));  // = B * H * nqb (kernels)
   if (nblk > 0x7fffffff) return VP_ERR_ARG;
   hipLaunchKernelGGL(null_key_mass_kernel, dim3((unsigned)nblk), dim3(NM_NT), (size_t)lds, (hipStream_t)stream,
                      (const bf16*)q, q_sb, q_sn, H, N, T, F, Hh, Ww, (const bf16*)beta, cos_t, sin_t, cos_y, sin_y,
