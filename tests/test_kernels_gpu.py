@@ -614,6 +614,7 @@ def test_gemm_a_tail_matches_materialized_operands(r):
     o = torch.empty(B, Ntok, 3 * D, device=dev, dtype=torch.bfloat16)
     K.gemm(xa, ws, bs, o.view(-1, 3 * D), epilogue=N.EPI_BIAS_QKNORM_ROPE, qk_norm=lns, rope=(cos, sin),
            tokens_per_batch=Ntok, text_len=T, a_tail=tail)
+    pres = []
     for s in range(3):
         pre = torch.empty(B, Ntok, D, device=dev, dtype=torch.bfloat16)
         K.gemm(mat[s], [ws[s]], [bs[s]], pre.view(-1, D))
@@ -623,6 +624,17 @@ def test_gemm_a_tail_matches_materialized_operands(r):
         else:
             ref = pre
         assert torch.equal(o[..., s * D:(s + 1) * D], ref), ("qknorm", s)
+        if s < 2:
+            pres.append(pre)
+    # the same with the aux output (ABI 17, the training forward: the pre-norm q | k) — the aux instance of the
+    # tail form: C unchanged, aux = the pre-norm segments
+    o2 = torch.empty_like(o)
+    aux = torch.empty(B * Ntok, 2 * D, device=dev, dtype=torch.bfloat16)
+    K.gemm(xa, ws, bs, o2.view(-1, 3 * D), epilogue=N.EPI_BIAS_QKNORM_ROPE, qk_norm=lns, rope=(cos, sin),
+           tokens_per_batch=Ntok, text_len=T, a_tail=tail, aux=aux)
+    assert torch.equal(o2, o)
+    for s in range(2):
+        assert torch.equal(aux[:, s * D:(s + 1) * D], pres[s].view(-1, D)), ("aux", s)
     # the gated residual (to_out: one segment reading T_0)
     o = torch.empty(B * Ntok, D, device=dev, dtype=torch.bfloat16)
     K.gemm(xa, ws[:1], bs[:1], o, epilogue=N.EPI_GATED, resid=resid, mod=mod, tokens_per_batch=Ntok, text_len=T,
