@@ -157,19 +157,34 @@ def frame_batches(n: int, size: int, min_one: bool):
     return out
 
 
+def _pointwise(sd: SD, p: str, x):
+    """A 1x1x1 `CogVideoXSafeConv3d` (quant_conv / post_quant_conv, :979-980)."""
+    return F.conv3d(x, sd[p + ".weight"], sd[p + ".bias"])
+
+
 def encode(sd: SD, cfg: dict, x) -> torch.Tensor:
-    """`AutoencoderKLCogVideoX._encode` :1085-1108 -> the latent_dist parameters (mean ++ logvar on channels)."""
+    """`AutoencoderKLCogVideoX._encode` :1085-1108 -> the latent_dist parameters (mean ++ logvar on channels);
+    quant_conv after the encoder per frame batch when the config has it (:1101-1102)."""
     caches = Caches()
-    parts = [encoder(sd, cfg, x[:, :, a:b], caches) for a, b in frame_batches(x.shape[2], 8, True)]
+    parts = []
+    for a, b in frame_batches(x.shape[2], 8, True):
+        h = encoder(sd, cfg, x[:, :, a:b], caches)
+        parts.append(_pointwise(sd, "quant_conv", h) if cfg.get("use_quant_conv") else h)
     return torch.cat(parts, dim=2)
 
 
 def decode(sd: SD, cfg: dict, z) -> torch.Tensor:
-    """`AutoencoderKLCogVideoX.decode` / `_decode` :1138-1190."""
+    """`AutoencoderKLCogVideoX.decode` / `_decode` :1138-1190 (post_quant_conv before the decoder per frame batch when
+    the config has it, :1152-1153)."""
     if z.shape[2] == 1:
         z = torch.cat([z, z], dim=2)
     caches = Caches()
-    parts = [decoder(sd, cfg, z[:, :, a:b], caches) for a, b in frame_batches(z.shape[2], 2, False)]
+    parts = []
+    for a, b in frame_batches(z.shape[2], 2, False):
+        zi = z[:, :, a:b]
+        if cfg.get("use_post_quant_conv"):
+            zi = _pointwise(sd, "post_quant_conv", zi)
+        parts.append(decoder(sd, cfg, zi, caches))
     return torch.cat(parts, dim=2)
 
 

@@ -279,6 +279,9 @@ VAE_TINY_CFG = dict(block_out_channels=(32, 32, 32, 32), layers_per_block=1, lat
 VAE_5B_CFG = dict(block_out_channels=(128, 256, 256, 512), layers_per_block=3, latent_channels=16,
                   norm_num_groups=32, temporal_compression_ratio=4, scaling_factor=0.7)
 VAE_SEEDS = (2001, 2002)
+# use_quant_conv / use_post_quant_conv: the reference sizes them by out_channels (:979-980) and applies them to
+# latent-width tensors, so they run only with out_channels == latent_channels
+VAE_QUANT_CFG = dict(VAE_TINY_CFG, out_channels=16, use_quant_conv=True, use_post_quant_conv=True)
 
 
 def vae_inputs(frames: int = 17, height: int = 64, width: int = 96, latent_frames: int = 5, key: str = "vae"):

@@ -25,6 +25,7 @@ Fixtures (all fp32):
                           8(c)(iv): noise-prediction slice in fp32 and in the reference's own bf16 run, digest, branch
                           slices, bf16 drift.
   vae.safetensors       — the reference 3D causal VAE (tiny and 5b-shaped), encode / decode at 17 and 9 frames.
+  vae_quant.safetensors — the tiny VAE with use_quant_conv / use_post_quant_conv (out = latent channels = 16).
   block5.safetensors    — one full-width block at config-5 length (720x1280: N = 47 026), fp32 + bf16 slices.
   config1.safetensors   — the WHOLE 5b-I2V-shaped transformer (42 layers) + 2-layer branch at config-1 shape, B=2:
                           noise prediction in fp32 (strided slice + digest) and the reference's own bf16 run's
@@ -760,6 +761,23 @@ def make_vae():
 
 
 @torch.no_grad()
+def make_vae_quant():
+    """The reference tiny VAE with use_quant_conv / use_post_quant_conv (out_channels = latent_channels = 16, the only
+    widths it can run them at): encode -> mean / logvar of a 9-frame 64x96 video, decode of 3 latent frames.
+    vae_quant.safetensors."""
+    from diffusers import AutoencoderKLCogVideoX
+    from tests.golden.cases import VAE_QUANT_CFG, VAE_SEEDS, vae_inputs
+    with torch.device("meta"):
+        vae = AutoencoderKLCogVideoX(**VAE_QUANT_CFG).eval()
+    vae = _fill_synthetic(vae, VAE_SEEDS[0])
+    x, z = vae_inputs(9, 64, 96, 3, key="vaeq")
+    dist = vae.encode(x).latent_dist
+    dec = vae.decode(z).sample
+    print(f"vae quant: mean {tuple(dist.mean.shape)} decode {tuple(dec.shape)}", flush=True)
+    _save("vae_quant.safetensors", {"mean": dist.mean, "logvar": dist.logvar, "decode_s2": dec[..., ::2, ::2]})
+
+
+@torch.no_grad()
 def make_vae_tiled():
     """The reference tiny VAE with tiling and slicing enabled (sample 128x192 -> 64x96 sample tiles, 8x12 latent
     tiles, so both blend_v and blend_h run with extents > 1) on a B = 2 batch: encode -> mean / logvar of a 9-frame
@@ -850,6 +868,8 @@ if __name__ == "__main__":
         make_vae()
     if "vae_tiled" in which:
         make_vae_tiled()
+    if "vae_quant" in which:
+        make_vae_quant()
     if "t5" in which:
         make_t5()
     if "pipe_pixels" in which:

@@ -199,6 +199,24 @@ def test_vae_oracle_matches_reference(tag):
         assert rel(dec, g[f"{tag}.f{frames}.decode"]) < 1e-5
 
 
+def test_vae_quant_conv_oracle_matches_reference():
+    """use_quant_conv / use_post_quant_conv (autoencoder_kl_cogvideox.py:979-980, 1101-1102, 1152-1153) against the
+    reference's own run (tests/golden/vae_quant.safetensors: tiny VAE, out = latent channels = 16)."""
+    from oracle import vae_oracle as V
+    from tests.golden.cases import VAE_QUANT_CFG, VAE_SEEDS, vae_inputs, vae_weights
+    from videopainter_amd.config import full_vae_config
+    sd = {k: torch.from_numpy(v) for k, v in vae_weights(VAE_QUANT_CFG, VAE_SEEDS[0]).items()}
+    assert "quant_conv.weight" in sd and "post_quant_conv.weight" in sd
+    cfg = full_vae_config(VAE_QUANT_CFG)
+    g = load_file(os.path.join(GOLD, "vae_quant.safetensors"))
+    x, z = vae_inputs(9, 64, 96, 3, key="vaeq")
+    with torch.no_grad():
+        mean, logvar, _ = V.latent_dist(V.encode(sd, cfg, x))
+        dec = V.decode(sd, cfg, z)
+    assert rel(mean, g["mean"]) < 1e-5 and rel(logvar, g["logvar"]) < 1e-5
+    assert rel(dec[..., ::2, ::2], g["decode_s2"]) < 1e-5
+
+
 def test_vae_tiled_oracle_matches_reference():
     """Tiled + sliced encode / decode (tests/golden/vae_tiled.safetensors: tiny VAE, sample 128x192, B = 2)."""
     from oracle import vae_oracle as V

@@ -250,6 +250,34 @@ def test_vae_encode_decode_matches_reference(tag):
         assert rl <= 2.5 * drift_mean + 2e-3  # logvar ~ N(0, 0.5^2) around 0: relative error of a near-zero field
 
 
+def test_vae_quant_conv_matches_reference():
+    """use_quant_conv / use_post_quant_conv (1x1x1 convs after the encoder / before the decoder, the decoder's spatial
+    norms conditioned on the post-quant latent; reference :979-980, 1101-1102, 1152-1153) against the reference's fp32
+    run, gated on the oracle's own bf16 run; a config the reference cannot run (out != latent channels) raises."""
+    from oracle import vae_oracle as V
+    from tests.golden.cases import VAE_QUANT_CFG, VAE_SEEDS, VAE_TINY_CFG, vae_inputs, vae_weights
+    from videopainter_amd.config import full_vae_config
+    from videopainter_amd.vae import AutoencoderKLCogVideoX
+    g = load_file(os.path.join(GOLD, "vae_quant.safetensors"))
+    m = _vae(VAE_QUANT_CFG, VAE_SEEDS[0])
+    x, z = vae_inputs(9, 64, 96, 3, key="vaeq")
+    with torch.no_grad():
+        post = m.encode(x.cuda()).latent_dist
+        dec = m.decode(z.cuda()).sample
+    sd16 = {k: torch.from_numpy(v).bfloat16() for k, v in vae_weights(VAE_QUANT_CFG, VAE_SEEDS[0]).items()}
+    fc = full_vae_config(VAE_QUANT_CFG)
+    with torch.no_grad():
+        drift_mean = rel(V.latent_dist(V.encode(sd16, fc, x.bfloat16()))[0].float(), g["mean"])
+        drift_dec = rel(V.decode(sd16, fc, z.bfloat16()).float()[..., ::2, ::2], g["decode_s2"])
+    rm, rd = rel(post.mean.float(), g["mean"]), rel(dec[..., ::2, ::2].float(), g["decode_s2"])
+    print(f"vae quant: mean {rm:.3e} (bf16 ref {drift_mean:.3e}) decode {rd:.3e} (bf16 ref {drift_dec:.3e})")
+    assert tuple(dec.shape) == (1, 16, 9, 64, 96)
+    assert rm <= 1.25 * drift_mean + 1e-3
+    assert rd <= 1.25 * drift_dec + 1e-3
+    with pytest.raises(ValueError):
+        AutoencoderKLCogVideoX.from_config(dict(VAE_TINY_CFG, use_quant_conv=True), device="cuda")
+
+
 def test_vae_tiled_sliced_matches_reference():
     """enable_tiling + enable_slicing on B = 2 (the any-length inference setting, infer/inpaint.py:413-415): the
     blend order and the reference's crop arithmetic (decode comes out 140 x 202 at this size)."""

@@ -148,7 +148,13 @@ def test_vae_state_dict_and_config_contract():
     m = AutoencoderKLCogVideoX(block_out_channels=(32, 32, 32, 32), layers_per_block=1)
     assert m.config.scaling_factor == VAE_DEFAULTS["scaling_factor"]
     assert "decoder.up_blocks.0.resnets.1.norm2.conv_b.conv.weight" in m.state_dict()
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):  # the reference sizes it by out_channels (3) and cannot run it on 16 latents
         AutoencoderKLCogVideoX(use_quant_conv=True)
+    q = AutoencoderKLCogVideoX(block_out_channels=(32, 32, 32, 32), layers_per_block=1, out_channels=16,
+                               use_quant_conv=True, use_post_quant_conv=True)
+    sd = q.state_dict()
+    assert tuple(sd["quant_conv.weight"].shape) == (32, 32, 1, 1, 1)
+    assert tuple(sd["post_quant_conv.weight"].shape) == (16, 16, 1, 1, 1)
+    assert list(sd)[-4:] == ["quant_conv.weight", "quant_conv.bias", "post_quant_conv.weight", "post_quant_conv.bias"]
     with pytest.raises(TypeError):
         AutoencoderKLCogVideoX(bogus=1)

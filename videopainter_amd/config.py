@@ -205,6 +205,14 @@ def vae_state_dict_shapes(cfg: dict) -> Dict[str, Tuple[int, ...]]:
         s[f"decoder.norm_out.{cv}.conv.bias"] = (rch[-1],)
     s["decoder.conv_out.conv.weight"] = (cfg["out_channels"], rch[-1], 3, 3, 3)
     s["decoder.conv_out.conv.bias"] = (cfg["out_channels"],)
+    # (:979-980: 1x1x1 SafeConv3d with out_channels-based widths, registered after the decoder)
+    oc = cfg["out_channels"]
+    if cfg.get("use_quant_conv"):
+        s["quant_conv.weight"] = (2 * oc, 2 * oc, 1, 1, 1)
+        s["quant_conv.bias"] = (2 * oc,)
+    if cfg.get("use_post_quant_conv"):
+        s["post_quant_conv.weight"] = (oc, oc, 1, 1, 1)
+        s["post_quant_conv.bias"] = (oc,)
     return s
 
 

@@ -136,10 +136,13 @@ class AutoencoderKLCogVideoX(nn.Module):
             sample_height=sample_height, sample_width=sample_width, scaling_factor=scaling_factor,
             shift_factor=shift_factor, latents_mean=latents_mean, latents_std=latents_std,
             force_upcast=force_upcast, use_quant_conv=use_quant_conv, use_post_quant_conv=use_post_quant_conv))
-        if use_quant_conv or use_post_quant_conv:
-            # the reference builds them with 2*out_channels / out_channels (pixel) channels, which cannot take a
-            # latent_channels tensor for any released config; no CogVideoX checkpoint enables them
-            raise NotImplementedError("use_quant_conv / use_post_quant_conv are not supported")
+        if (use_quant_conv or use_post_quant_conv) and out_channels != latent_channels:
+            # the reference builds them with 2*out_channels / out_channels (pixel) channels (:979-980) and applies them
+            # to the 2*latent_channels encoder output / the latents (:1101-1102, :1152-1153): only a config with
+            # out_channels == latent_channels runs (no CogVideoX checkpoint enables them); the reference fails at its
+            # first encode / decode, the drop-in at construction
+            raise ValueError("use_quant_conv / use_post_quant_conv need out_channels == latent_channels "
+                             f"(got {out_channels} / {latent_channels})")
         if any(t != "CogVideoXDownBlock3D" for t in down_block_types) or \
                 any(t != "CogVideoXUpBlock3D" for t in up_block_types):
             raise ValueError("Invalid block type: must be CogVideoXDownBlock3D / CogVideoXUpBlock3D")
@@ -439,7 +442,10 @@ class AutoencoderKLCogVideoX(nn.Module):
             h = self._resnet(f"encoder.mid_block.resnets.{j}", h)
         gamma, beta = self._affine("encoder.norm_out")
         h = K.group_norm(h, gamma, beta, cfg.norm_num_groups, 1e-6, silu=True)
-        return self._causal_conv("encoder.conv_out", h)
+        h = self._causal_conv("encoder.conv_out", h)
+        if cfg.use_quant_conv:  # (:1101-1102, per frame batch / tile)
+            h = self._pointwise("quant_conv", h)
+        return h
 
     def _decoder(self, z: torch.Tensor) -> torch.Tensor:
         """`CogVideoXDecoder3D.forward` :849-883 on one latent frame batch (channels-last, L padded) -> [B, T, H, W, 8]
@@ -447,6 +453,8 @@ class AutoencoderKLCogVideoX(nn.Module):
         cfg = self.config
         nb = len(cfg.block_out_channels)
         tcl = int(np.log2(cfg.temporal_compression_ratio))
+        if cfg.use_post_quant_conv:  # (:1152-1153: before the decoder, whose spatial norms then see its output)
+            z = self._pointwise("post_quant_conv", z)
         h = self._causal_conv("decoder.conv_in", z)
         for j in range(2):
             h = self._resnet(f"decoder.mid_block.resnets.{j}", h, zq=z)
