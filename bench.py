@@ -89,13 +89,13 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def physical_cores() -> int:
+def physical_cores(capped: bool = True) -> int:
     """The thread count the CPU baseline runs at (the reference CPU path on the node's own host
     cores): the physical cores of this process's affinity mask (SMT siblings counted once), capped by the CPU share
     the host allots this job when it states one in OMP_NUM_THREADS (the GPU boxes set it to 16 per GPU and ask jobs
     to keep to it; the CPU is shared with the other GPUs' jobs).  VP_CPU_BASELINE_THREADS overrides both."""
     env = int(os.environ.get("VP_CPU_BASELINE_THREADS", "0") or 0)
-    if env > 0:
+    if env > 0 and capped:
         return env
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
@@ -109,7 +109,7 @@ def physical_cores() -> int:
             seen.add((pkg, core))
         except OSError:
             seen.add(("cpu", c))
-    return max(1, min(len(seen), share) if share > 0 else len(seen))
+    return max(1, min(len(seen), share) if share > 0 and capped else len(seen))
 
 
 def _oracle_block_weights(g, dtype):
@@ -161,10 +161,11 @@ def cpu_baseline() -> dict:
     step_s = {k: v * step_flops() / block_flop() for k, v in out.items()}
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
     return {"value": 1.0 / step_s["bf16"], "unit": "steps/s", "cores": threads, "kind": "port",
-            "threads": torch.get_num_threads(), "physical_cores_in_affinity": physical_cores(),
+            "threads": torch.get_num_threads(), "host_physical_cores": physical_cores(capped=False),
             "affinity_cpus": aff, "host_cpus": os.cpu_count(),
             "value_fp32": 1.0 / step_s["fp32"], "cpu_model": _cpu_model(),
-            "sample": f"oracle (plain PyTorch CPU restatement) after a warm-up block: 1 full-size CogVideoXBlock "
+            "sample": f"EXTRAPOLATED, not a timed step: oracle (plain PyTorch CPU restatement) after a warm-up "
+                      f"block, 1 full-size CogVideoXBlock "
                       f"forward at B=2, N={NTOK} took {out['bf16']:.1f} s in bf16 and {out['fp32']:.1f} s in fp32 on "
                       f"{threads} threads = the physical cores of the process affinity mask capped by the job's "
                       f"CPU share OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')} ({aff} of the host's "

@@ -208,6 +208,15 @@ def config4_inputs(dtype=torch.float32):
 # encode call; the VAE has its own goldens), so every window input is regenerable here and on the GPU box.
 CHAIN4_CASE = dict(num_frames=49, total_frames=98, stride=49, height=480, width=720, steps=1, prev_clip_weight=0.5,
                    id_pool_resample_learnable=True, seed=42)
+# the same chain at 2 DPM steps per window (VERDICT r05 "next" 5): the scheduler's second-order branch
+# (scheduling_dpm_cogvideox.py:426-434) runs at every window's second step, and window 1's second step takes the
+# resample mask its own first step returned (anyl.py:967 re-binds prev_resample_mask on every call)
+CHAIN4_CASE2 = dict(CHAIN4_CASE, steps=2)
+CHAIN4_FIXTURES = {1: "config4_chain.safetensors", 2: "config4_chain2.safetensors"}
+
+
+def chain4_case(steps: int = 1):
+    return CHAIN4_CASE if steps == 1 else dict(CHAIN4_CASE, steps=steps)
 # the k-th vae.encode call of the reference run: window 0 encodes the first frame, the video, the masked video;
 # window 1 (conditioned on window 0's last latent, no first-frame encode) the video and the masked video
 CHAIN4_VAE_CALLS = (("w0.image", 1), ("w0.video", 13), ("w0.masked", 13), ("w1.video", 13), ("w1.masked", 13))
@@ -230,11 +239,11 @@ def chain4_prompts():
             torch.from_numpy(synth_tensor("c4chain.neg", (1, 226, 4096))))
 
 
-def chain4_draws():
-    """The reference run's generator draws in its order (pinned by the digests in config4_chain.safetensors): per
+def chain4_draws(steps: int = 1):
+    """The reference run's generator draws in its order (pinned by the digests in config4_chain*.safetensors): per
     window the initial noise (prepare_latents), then one scheduler noise per DPM step; all fp32 [1, 13, 16, 60, 90]
     from torch.Generator().manual_seed(42) (the stub VAE draws nothing)."""
-    c = CHAIN4_CASE
+    c = chain4_case(steps)
     g = torch.Generator().manual_seed(c["seed"])
     out = []
     for _ in range(c["total_frames"] // c["stride"]):

@@ -491,7 +491,7 @@ def make_config4():
 
 
 @torch.no_grad()
-def make_config4_chain(mini=False):
+def make_config4_chain(mini=False, steps=1):
     """BASELINE config 4's CHAINED any-length loop at full size (VERDICT r04 "next" 7): the reference pipeline's own
     __call__ (anyl.py:759-1069: window slicing, the previous window's last latent as the next window's image
     latent, the last-step 42-layer hidden states + resample mask handed to the next window, dynamic CFG, replace-gt,
@@ -507,7 +507,13 @@ def make_config4_chain(mini=False):
       * the bf16 run replays the fp32 run's generator draws cast to bf16, so its drift is arithmetic only.
     Stored: strided slices + digest of the final latents, the bf16 drift, the draws' digests (the GPU test
     regenerates them, cases.chain4_draws) and the latent mask the pipeline built (uint8).
-    `mini=True`: a 2-layer 2-head model at the same shapes, written to /tmp (checks the machinery in minutes)."""
+    `mini=True`: a 2-layer 2-head model at the same shapes, written to /tmp (checks the machinery in minutes).
+    `steps=2` (config4_chain2.safetensors, VERDICT r05 "next" 5): 2 DPM steps per window, so the scheduler's
+    second-order branch (scheduling_dpm_cogvideox.py:426-434) runs in every window.  The calls whose hidden-state
+    list nothing reads (window 0's first step, every step of the last window) run with return_hidden_states=False,
+    and the wrapper returns the resample mask the reference's forward would have returned
+    (cogvideox_transformer_3d.py:534-544: False on the text rows, the patch-embed's pooled mask on the video rows),
+    because anyl.py:967 re-binds prev_resample_mask to it on every call."""
     import time
     import types
     import diffusers.schedulers.scheduling_dpm_cogvideox as dpm_mod
@@ -517,9 +523,9 @@ def make_config4_chain(mini=False):
     from diffusers.models.branch_cogvideox import CogvideoXBranchModel
     from PIL import Image
     from safetensors.torch import save_file as _sf
-    from tests.golden.cases import (config2_cfg, CONFIG2_SEEDS, CHAIN4_CASE, CHAIN4_VAE_CALLS, chain4_vae_latent,
-                                    chain4_pixel_masks, chain4_prompts)
-    c = CHAIN4_CASE
+    from tests.golden.cases import (config2_cfg, CONFIG2_SEEDS, CHAIN4_FIXTURES, CHAIN4_VAE_CALLS, chain4_case,
+                                    chain4_vae_latent, chain4_pixel_masks, chain4_prompts)
+    c = chain4_case(steps)
     tcfg, bcfg = config2_cfg()
     tcfg = dict(tcfg, id_pool_resample_learnable=True)
     if mini:
@@ -569,13 +575,28 @@ def make_config4_chain(mini=False):
         anyl_mod.randn_tensor = rn
         dpm_mod.randn_tensor = rn
         orig_fwd = tr.forward
+        ncall = [0]
 
         def fwd(*a, **k):
             akw = k.get("attention_kwargs") or {}
-            if "prev_hidden_states" in akw:  # the last window: its states are never read
-                assert c["steps"] == 1
-                k = dict(k, return_hidden_states=False)
-                return (orig_fwd(*a, **k)[0], [], None)
+            step = ncall[0] % c["steps"]
+            ncall[0] += 1
+            # the last window (2 windows: the one with prev_hidden_states) and window 0's non-final steps: their
+            # states are never read (anyl.py:979-985)
+            # (VP_CHAIN_FULL_STATES=1: every call returns its states — checks on the mini model that the
+            # substitution changes no output bit)
+            if ("prev_hidden_states" in akw or step < c["steps"] - 1) and not os.environ.get("VP_CHAIN_FULL_STATES"):
+                pooled = {}
+                hk = tr.patch_embed.register_forward_hook(lambda m, inp, out: pooled.__setitem__("m", out[1]))
+                try:
+                    o = orig_fwd(*a, **dict(k, return_hidden_states=False))[0]
+                finally:
+                    hk.remove()
+                enc = k["encoder_hidden_states"]
+                pm = pooled["m"]
+                rmask = torch.zeros((pm.shape[0], enc.shape[1] + pm.shape[1]), dtype=torch.bool)
+                rmask[:, enc.shape[1]:] = pm[:, :, 0].bool()
+                return (o, [], rmask)
             return orig_fwd(*a, **k)
         tr.forward = fwd
         orig_mask = pipe.prepare_mask_latents
@@ -630,7 +651,8 @@ def make_config4_chain(mini=False):
         out[f"w{w}.mask"] = m[:1].to(torch.uint8)
     out = {k: (v.contiguous() if v.dtype in (torch.float64, torch.uint8) else v.detach().float().contiguous())
            for k, v in out.items()}
-    path = "/tmp/config4_chain_mini.safetensors" if mini else os.path.join(HERE, "config4_chain.safetensors")
+    fix = CHAIN4_FIXTURES[steps]
+    path = "/tmp/" + fix.replace(".safetensors", "_mini.safetensors") if mini else os.path.join(HERE, fix)
     _sf(out, path, metadata={"case": json.dumps(c), "cpu_seconds": json.dumps({"fp32": t32, "bf16": t16}),
                              "mini": json.dumps(mini)})
     print("wrote", path, flush=True)
@@ -860,6 +882,10 @@ if __name__ == "__main__":
         make_config4_chain()
     if "config4_chain_mini" in which:
         make_config4_chain(mini=True)
+    if "config4_chain2" in which:
+        make_config4_chain(steps=2)
+    if "config4_chain2_mini" in which:
+        make_config4_chain(mini=True, steps=2)
     if "block5" in which:
         make_block5()
     if "block_resample" in which:

@@ -862,25 +862,29 @@ def test_config4_full_model_matches_reference():
 
 
 @torch.no_grad()
-def test_config4_chain_full_size_matches_reference():
+@pytest.mark.parametrize("steps", [1, 2])
+def test_config4_chain_full_size_matches_reference(steps):
     """BASELINE config 4's CHAINED any-length loop at full size (VERDICT r04 "next" 7): the reference pipeline's own
     __call__ on the 42-layer ID-resample transformer + 2-layer branch, 2 windows x 49 frames at stride 49, 480x720,
     1 DPM step per window, prev_clip_weight 0.5 (tests/golden/config4_chain.safetensors, make_golden.py config4_chain).
     Window 1 conditions on window 0's last latent frame, its 42 last-step hidden states and resample mask; the clip
     is overlap-averaged.  The harness replays the reference's VAE latents (the stub VAE's counter latents), masks and
     generator draws (regenerated here and pinned by the fixture's digests); the final latents [1, 25, 16, 60, 90]
-    must sit within 1.25x the reference's own bf16 drift + 1e-3 of its fp32 run."""
+    must sit within 1.25x the reference's own bf16 drift + 1e-3 of its fp32 run.
+    steps=2 (config4_chain2.safetensors): 2 DPM steps per window — the scheduler's second-order branch
+    (scheduling_dpm_cogvideox.py:426-434) in both windows, and window 1's second step on the resample mask its own
+    first step returned (anyl.py:967)."""
     from videopainter_amd import CogVideoXTransformer3DModel, CogvideoXBranchModel, device_scope
     from videopainter_amd.pipeline import CogVideoXI2VDualInpaintAnyLHarness
     from videopainter_amd.scheduler import CogVideoXDPMScheduler
-    from tests.golden.cases import (config2_cfg, CONFIG2_SEEDS, CHAIN4_CASE, CHAIN4_VAE_CALLS, chain4_draws,
-                                    chain4_prompts, chain4_vae_latent)
-    path = os.path.join(GOLD, "config4_chain.safetensors")
+    from tests.golden.cases import (config2_cfg, CONFIG2_SEEDS, CHAIN4_FIXTURES, CHAIN4_VAE_CALLS, chain4_case,
+                                    chain4_draws, chain4_prompts, chain4_vae_latent)
+    path = os.path.join(GOLD, CHAIN4_FIXTURES[steps])
     if not os.path.exists(path):
-        pytest.skip("config4_chain fixture not generated")
+        pytest.skip(f"{CHAIN4_FIXTURES[steps]} fixture not generated")
     g = load_file(path)
-    c = CHAIN4_CASE
-    draws = chain4_draws()
+    c = chain4_case(steps)
+    draws = chain4_draws(steps)
     for i, dr in enumerate(draws):  # the same draws as the reference run
         d = g[f"draw.{i}.digest"].double()
         got = torch.tensor([dr.double().sum(), dr.double().abs().sum(), dr.double().norm()], dtype=torch.float64)
@@ -918,7 +922,7 @@ def test_config4_chain_full_size_matches_reference():
     r = rel(of[::7], g["slice"])
     rb = float(g["ref_bf16_rel"][0])
     r_vs16 = rel(of[::7], g["bf16.slice"])
-    print(f"config 4 chain (2 windows, full size) vs reference fp32: final latents {r:.3e} (reference bf16 {rb:.3e}; "
+    print(f"config 4 chain (2 windows x {steps} steps, full size) vs reference fp32: final latents {r:.3e} (reference bf16 {rb:.3e}; "
           f"HIP vs reference bf16 {r_vs16:.3e})")
     assert r <= gate(rb), (r, rb)
     del tr, br, h, out

@@ -267,15 +267,19 @@ def test_pipe_pixel_inputs_are_the_reference_processor_outputs():
         assert torch.allclose(d, g[f"{k}_digest"], rtol=1e-12, atol=1e-9), k
 
 
-def test_config4_chain_fixture_pins_the_draws_and_masks():
+@pytest.mark.parametrize("steps", [1, 2])
+def test_config4_chain_fixture_pins_the_draws_and_masks(steps):
     """tests/golden/config4_chain.safetensors (the full-size chained any-length run of the reference pipeline): the
     generator draws tests/golden/cases.chain4_draws regenerates are the reference run's (fp64 digests), and each
     window's recorded latent mask is the nearest-frame / nearest-pixel pick of cases.chain4_pixel_masks (the
     reference's F.interpolate of the window's pixel masks, default mode 'nearest') with frame 0 of window 0 clear."""
-    from tests.golden.cases import CHAIN4_CASE, chain4_draws, chain4_pixel_masks
-    g = load_file(os.path.join(GOLD, "config4_chain.safetensors"))
-    c = CHAIN4_CASE
-    draws = chain4_draws()
+    from tests.golden.cases import CHAIN4_FIXTURES, chain4_case, chain4_draws, chain4_pixel_masks
+    path = os.path.join(GOLD, CHAIN4_FIXTURES[steps])
+    if not os.path.exists(path):
+        pytest.skip(f"{CHAIN4_FIXTURES[steps]} not generated")
+    g = load_file(path)
+    c = chain4_case(steps)
+    draws = chain4_draws(steps)
     assert len(draws) == (c["total_frames"] // c["stride"]) * (1 + c["steps"])
     for i, dr in enumerate(draws):
         d = torch.tensor([dr.double().sum(), dr.double().abs().sum(), dr.double().norm()], dtype=torch.float64)

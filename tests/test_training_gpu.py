@@ -216,6 +216,45 @@ def test_saved_attention_backward_is_bit_identical(monkeypatch, lora):
                 assert torch.equal(gp1[n], gp0[n]), n
 
 
+def test_frozen_block_with_loaded_adapter_input_gradient(monkeypatch):
+    """a frozen transformer block carrying a LOADED (unfused) adapter, trained through for its
+    input only (the branch's injection path), with SAVE_ACTIVATIONS on: the saving forward keeps no xn / xq for a
+    frozen block, and the backward's unfused-adapter dgrad must not read them.  The input gradient equals the
+    full-recompute one bit for bit."""
+    from videopainter_amd import autograd as AG
+    from videopainter_amd.autograd import block_apply
+    from videopainter_amd.lora import attach_lora_
+    tr, _, _, _ = _models()
+    blk = tr.transformer_blocks[0]
+    g0 = torch.Generator().manual_seed(11)
+    sd = {}
+    for n, lin in (("to_q", blk.attn1.to_q), ("to_k", blk.attn1.to_k), ("to_v", blk.attn1.to_v),
+                   ("to_out.0", blk.attn1.to_out[0])):
+        o, k = lin.weight.shape
+        sd[f"transformer_blocks.0.attn1.{n}.lora_A.weight"] = torch.randn(8, k, generator=g0) * 0.1
+        sd[f"transformer_blocks.0.attn1.{n}.lora_B.weight"] = torch.randn(o, 8, generator=g0) * 0.05
+    attach_lora_(tr, sd)
+    for p in blk.parameters():
+        p.requires_grad_(False)
+    i = tiny_inputs()
+    T = i["enc"].shape[1]
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, T + 288, 128, generator=g).bfloat16()
+    temb = torch.randn(2, 32, generator=g).bfloat16()
+    dout = torch.randn(2, T + 288, 128, generator=g).bfloat16()
+    res = []
+    for acts, attn in ((True, True), (False, True), (False, False)):
+        monkeypatch.setattr(AG, "SAVE_ACTIVATIONS", acts)
+        monkeypatch.setattr(AG, "SAVE_ATTENTION", attn)
+        xd = x.to(dev).requires_grad_()
+        out = block_apply(blk, xd, T, temb.to(dev), (i["rope"][0].to(dev), i["rope"][1].to(dev)))
+        out.backward(dout.to(dev))
+        res.append((out.detach(), xd.grad))
+    for o1, gx1 in res[:-1]:
+        assert torch.equal(o1, res[-1][0]) and torch.equal(gx1, res[-1][1])
+    assert float(res[0][1].float().abs().max()) > 0
+
+
 @pytest.mark.parametrize("wo_text", [False, True], ids=["text", "wo_text"])
 def test_branch_gradients_through_frozen_transformer(wo_text):
     """The training step (train_cogvideox_inpainting_i2v_video.py:1856-1892): branch (trainable) -> samples injected

@@ -19,7 +19,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 LIBS = {"clk": {}, "clk_nodma": {"attention.hip": ["-DVP_P1_ABL=1"]}, "clk_noexp": {"attention.hip": ["-DVP_P1_ABL=2"]},
-        "clk_noboth": {"attention.hip": ["-DVP_P1_ABL=3"]}}
+        "clk_noboth": {"attention.hip": ["-DVP_P1_ABL=3"]}, "clk_l2": {"attention.hip": ["-DVP_P1_ABL=4"]}}
 
 
 def build_all():
@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=2.5)
     ap.add_argument("--label", default="")
     ap.add_argument("--video-tokens", type=int, default=17550)
+    ap.add_argument("--dump", default="", help="path prefix: per-workgroup stamps (t0 r0 t1 r1) + per-head phase stats")
     args = ap.parse_args()
     if args.build:
         build_all()
@@ -91,9 +92,35 @@ def main():
         q10 = ghz[len(ghz) // 10] if ghz else float("nan")
         q90 = ghz[9 * len(ghz) // 10] if ghz else float("nan")
         loop_us = statistics.median([(buf[4 * i + 3] - buf[4 * i + 1]) / 100.0 for i in range(nblk)])
+        # per-head phase: blocks t = xcd_remap(blockIdx) of one (b, h) are t // nqb; sorted start times of a head's
+        # blocks, the span of its first 64 (one XCD's worth of slots) and the lag of the rest, in loop times
+        phase = {}
+        if not var.startswith("p2w") and args.dump:
+            nqb = (Ntok + 255) // 256
+            qq, rr = divmod(nblk, 8)
+            starts = {}
+            for i in range(nblk):
+                x, idx = i % 8, i // 8
+                tq = (x * (qq + 1) if x < rr else rr * (qq + 1) + (x - rr) * qq) + idx
+                starts.setdefault(tq // nqb, []).append(buf[4 * i + 1])
+            loop_t = loop_us * 100.0
+            sp64, lag = [], []
+            for bh, st in starts.items():
+                st.sort()
+                sp64.append((st[min(63, len(st) - 1)] - st[0]) / loop_t)
+                if len(st) > 64:
+                    lag.append((st[-1] - st[0]) / loop_t)
+            sp64.sort()
+            lag.sort()
+            phase = dict(heads=len(starts), span64_median=round(statistics.median(sp64), 3),
+                         span64_p90=round(sp64[9 * len(sp64) // 10], 3),
+                         span_all_median=round(statistics.median(lag), 3) if lag else None)
+            with open(args.dump + f".{var}.txt", "w") as f:
+                for i in range(nblk):
+                    f.write(" ".join(str(v) for v in buf[4 * i:4 * i + 4]) + "\n")
         res[var] = dict(ms=round(t * 1e3, 4), tflops=round(fl / t / 1e12, 1), clock_ghz_median=round(statistics.median(ghz), 4),
                         clock_ghz_p10=round(q10, 4), clock_ghz_p90=round(q90, 4), loop_us_median=round(loop_us, 1),
-                        workgroups=len(ghz), warm_launches=warm)
+                        workgroups=len(ghz), warm_launches=warm, **phase)
         print(args.label, var, json.dumps(res[var]), flush=True)
     K.set_knob("VP_ATTN_NO_SPLIT", None)
     print(json.dumps({"label": args.label, "lib": N.LIB_PATH, "results": res}))

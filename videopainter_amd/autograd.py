@@ -97,7 +97,7 @@ def _aug_tail_t(aug: AugmentedProjection) -> torch.Tensor:
     return c[1]
 
 
-def _aug_dgrad(aug: AugmentedProjection, dy2: torch.Tensor, x2: torch.Tensor, out2: torch.Tensor, train: bool,
+def _aug_dgrad(aug: AugmentedProjection, dy2: torch.Tensor, x2: Optional[torch.Tensor], out2: torch.Tensor, train: bool,
                G: "_Grads", x_aug: Optional[torch.Tensor] = None) -> None:
     """Backward of the unfused-LoRA projections y_i = x_aug W_aug_i^T (lora.AugmentedProjection; segment i reads
     rank block i of T = x A_cat^T), given out2 = dy W0 (the base dgrad): out2 += dT A_cat with dT = dy W_tail
@@ -462,7 +462,8 @@ def block_backward(block, x: torch.Tensor, T: int, temb: torch.Tensor, rope, inj
         if qaug is not None:
             _aug_dgrad(qaug, dqkv.view(M, 3 * D), xn.view(M, D), dxn.view(M, D), True, G, xq)
     elif qaug is not None:
-        _aug_dgrad(qaug, dqkv.view(M, 3 * D), xn.view(M, D), dxn.view(M, D), False, G)
+        # (no parameter gradients: x2 is not read — and a frozen block's saving forward keeps no xn)
+        _aug_dgrad(qaug, dqkv.view(M, 3 * D), None, dxn.view(M, D), False, G)
     del dqkv, xn, xq
     n1o = dn1 = xh1 = None
     if need_dmod:
@@ -499,9 +500,12 @@ SAVE_ACTIVATIONS = True
 SAVE_RESERVE_BYTES = 16 << 30
 
 
-def _room_for(x: torch.Tensor, F4: int) -> bool:
+def _room_for(x: torch.Tensor, F4: int, keep_train: bool = False, R: int = 0) -> bool:
     B, Ntok, D = x.shape
-    need = B * Ntok * (5 * D + D + D + F4) * 2  # q | k | v, normed q | k, O, x_mid, z (bf16)
+    per_row = 5 * D + D + D + F4  # q | k | v, normed q | k, O, x_mid, z (bf16)
+    if keep_train:  # + h [F4], the AdaLN outputs xn / xn2 and xq (with the adapters' rank tail R)
+        per_row += F4 + 3 * D + R
+    need = B * Ntok * per_row * 2
     free, _ = torch.cuda.mem_get_info(x.device)
     return free - need > max(SAVE_RESERVE_BYTES, 4 * need)
 
@@ -510,8 +514,10 @@ class _BlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, block, T, rope, inject_mask, resample_mask, x, temb, inject, *params):
         ctx.front = ctx.attn_saved = None
-        if SAVE_ACTIVATIONS and resample_mask is None and _room_for(x, block.ff.net[0].proj.weight.shape[0]):
-            keep_train = any(p.requires_grad for p in params) or temb.requires_grad
+        keep_train = any(p.requires_grad for p in params) or temb.requires_grad
+        qaug = AugmentedProjection.of((block.attn1.to_q, block.attn1.to_k, block.attn1.to_v)) if keep_train else None
+        if SAVE_ACTIVATIONS and resample_mask is None and _room_for(
+                x, block.ff.net[0].proj.weight.shape[0], keep_train, qaug.R if qaug is not None else 0):
             out, ctx.front = block_forward_saving(block, x, T, temb, rope, inject,
                                                   inject_mask if inject is not None else None, keep_train)
         else:

@@ -59,7 +59,9 @@ enum { MODE_LAZY = 0, MODE_BOUNDED = 1 };
 // and after its key loop into vp_clock_buf (MI355X_MICROARCH.md 'DVFS give-back' item 6: in-kernel clock =
 // delta memtime / delta realtime x 100 MHz); the stamps go to that buffer only, never into an output.
 // VP_P1_ABL (p2 / p2a only, outputs invalid): bit 0 = no K / V DMA after the prologue (the loop re-reads stale
-// tiles), bit 1 = the softmax's v_exp_f32 replaced by v_mov_b32 — which part of the loop's power holds the clock.
+// tiles), bit 1 = the softmax's v_exp_f32 replaced by v_mov_b32 — which part of the loop's power holds the clock;
+// bit 2 = every full K / V tile streamed from the head's first 8 tiles (same DMA instructions, all L2 hits): what
+// the K / V fetches from beyond L2 cost.
 #ifndef VP_CLOCK_STAMPS
 #define VP_CLOCK_STAMPS 0
 #endif
@@ -1187,7 +1189,11 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
     const bool s1 = ti < full1;
     if (s1 || (ti >= tiles1 && ti - tiles1 < full2)) {
       const unsigned la = lds0 + (ti & (RING - 1)) * ST;
+#if VP_P1_ABL & 4
+      const int tt = (s1 ? ti : ti - tiles1) & 7;  // ablation: every full tile from the head's first 8 (L2-resident)
+#else
       const int tt = s1 ? ti : ti - tiles1;
+#endif
       const char* kb = (s1 ? kseg1 : kseg2) + (int64_t)tt * KB * d.k_sn * 2;
       const char* vb = (s1 ? vseg1 : vseg2) + (int64_t)tt * KB * d.v_sn * 2;
 #pragma unroll

@@ -283,6 +283,8 @@ def unfuse_lora_(model: torch.nn.Module) -> None:
     if st is None or not st.fused:
         return
     mods = dict(model.named_modules())
+    # (unfused adapters cannot ride an enabled fp8 QKV — raise before anything changes, not half-way)
+    _check_fp8_free(model, [(m, mods[m]) for m in st.base if covered(m)])
     for mod in [m for m in st.base if covered(m)]:
         mods[mod].weight.copy_(st.base.pop(mod))
     st.fused = False
