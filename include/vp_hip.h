@@ -186,10 +186,6 @@ typedef struct vp_gemm_mx_desc {
 
 int vp_gemm_mx_fp8(const vp_gemm_mx_desc* d, void* stream);
 
-/* layout self-test of one block-scaled MFMA (one wave): A, B e4m3 [16][128] row-major, per-lane scale bytes sa/sb
- * [64]: lane l feeds K-chunks l/16 and l/16+4 (16 bytes each) of row l%16 and the scale of row l%16, K-block l/16;
- * C fp32 [16][16] = Σ_k A[i][k]·2^(sa[i+16(k/32)]-127) · B[j][k]·2^(sb[j+16(k/32)]-127) */
-int vp_mx_mfma_probe(const void* A, const void* B, const void* sa, const void* sb, float* C, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * Flash attention forward, head_dim 64, non-causal, no mask — replaces F.scaled_dot_product_attention in
@@ -277,10 +273,6 @@ int64_t vp_v_pack_fp8_bytes(int32_t B, int32_t H, int32_t N, int64_t* npad, int6
 int vp_v_pack_fp8(const void* V, int64_t v_sb, int64_t v_sn, int32_t B, int32_t N, int32_t H, void* vt, void* vs,
                   void* stream);
 
-/* One v_mfma_scale_f32_32x32x64_f8f6f4 with the layout the fp8 attention assumes (lane l: row l % 32, 16-byte
- * K-chunks l/32 and l/32 + 2 of A[32][64] / B[32][64], scale bytes sa[l] / sb[l] for (row l % 32, K-block l/32));
- * C[32][32] row-major fp32 = A_deq . B_deq^T.  Layout self-test. */
-int vp_mx_mfma_probe32(const void* A, const void* B, const void* sa, const void* sb, float* C, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * AdaLN-Zero modulate — CogVideoXLayerNormZero.forward (DF/models/normalization.py:373-379):

@@ -756,8 +756,7 @@ def test_config1_full_model_matches_reference():
           f"branch {r0:.3e} / {r1:.3e} (reference bf16 {float(rb[1]):.3e} / {float(rb[2]):.3e})")
     assert r <= gate(float(rb[0]))
     assert r0 <= gate(float(rb[1])) and r1 <= gate(float(rb[2]))
-    # config 5's fp8 path (QKV projection, attention, FeedForward in e4m3) at full depth, same reference:
-    # re-stated tolerance 4e-2 (1.5x the measured fp8 drift)
+    # config 5's fp8 path (QKV projection, attention, FeedForward in e4m3) at full depth, same reference
     tr.enable_fp8()
     br.enable_fp8()
     bs8 = br(hidden_states=_d(inp["video"]), encoder_hidden_states=_d(inp["enc"]),
@@ -769,7 +768,9 @@ def test_config1_full_model_matches_reference():
     r8 = rel(o8.float().reshape(-1)[::37], g["slice"])
     print(f"config 1 full model, fp8 QKV + attention + FFN vs reference fp32: {r8:.3e}; vs HIP bf16 "
           f"{rel(o8, o.float()):.3e}")
-    assert r8 <= 4e-2  # measured (r02): 2.61-2.66e-2; gate 1.5x (was 3 x reference bf16 drift + 2e-2 = 8.9e-2)
+    # the fp8 band stated relative to the reference's own bf16 drift at this shape (rb[0] = 2.29e-2):
+    # 1.5x it = 3.43e-2 (measured r02-r05: 2.61-2.66e-2 = 1.15x)
+    assert r8 <= fp8_model_gate(float(rb[0])), (r8, float(rb[0]))
     del tr, br, bs, o, bs8, o8
     torch.cuda.empty_cache()
 
@@ -980,20 +981,33 @@ def test_config5_full_model_matches_reference():
     r8 = rel(of8[::13], g["slice"])
     print(f"config 5 full model (fp8: MX-FP8 QKV / FeedForward + fp8 attention) vs reference fp32: {r8:.3e}; "
           f"vs this model in bf16 {rel(of8, of):.3e}")
-    assert r8 <= FP8_CONFIG5_MODEL_GATE
+    # relative to the reference's bf16 drift at config 5's shape (rb[0] = 2.25e-2): 1.5x = 3.37e-2
+    # (measured r03-r05: 2.690e-2 = 1.20x)
+    assert r8 <= fp8_model_gate(float(rb[0])), (r8, float(rb[0]))
     del tr, br
     torch.cuda.empty_cache()
 
 
-FP8_CONFIG5_MODEL_GATE = 4.1e-2  # 1.5x the measured 2.690e-2 (profiles/r03_config5_full_model_test.log)
+def fp8_model_gate(ref_bf16_rel: float) -> float:
+    """The fp8 band of a whole-model test (stated relative to the reference's own bf16-vs-fp32
+    drift at the same shape): 1.5x that drift.  Across 42 blocks the accumulated bf16 rounding dominates the fp8
+    (QKV / attention / FeedForward in e4m3) quantisation noise, which lands at 1.15-1.20x the drift."""
+    return 1.5 * ref_bf16_rel
+
+
+def fp8_block_gate(ref_bf16_rel: float) -> float:
+    """The fp8 band of a single-block test: 5x the reference's bf16 drift of that block.  One block's bf16 drift is one
+    rounding deep, and e4m3's 3-bit mantissa has 16x bf16's rounding step (per-element noise ~16x, ~4x after the
+    block's averaging sums): measured 3.8x at config 5's length (9.93e-3 against 2.6e-3)."""
+    return 5.0 * ref_bf16_rel
 
 
 @torch.no_grad()
 def test_config5_length_block_matches_reference():
     """BASELINE config 5's sequence length (720x1280: N = 226 + 46 800 = 47 026): one full-width block against the
     reference's fp32 block (tests/golden/block5.safetensors), in bf16 (gate of the reference's own bf16 drift) and
-    with the config-5 fp8 path (QKV, attention, FeedForward in e4m3; re-stated band 1.5e-2 = 1.5x
-    the measured fp8 drift)."""
+    with the config-5 fp8 path (QKV, attention, FeedForward in e4m3; band fp8_block_gate: 5x the reference's bf16
+    drift of this block)."""
     from videopainter_amd import device_scope
     from videopainter_amd.transformer import CogVideoXBlock
     c = full_block_case(latent=(13, 90, 160), key="fb5")
@@ -1018,7 +1032,7 @@ def test_config5_length_block_matches_reference():
     print(f"config-5 length block vs reference fp32: bf16 HIP {r16:.3e}, fp8 QKV+attention+FFN {r8:.3e} "
           f"(reference bf16 {rb:.3e}); fp8 vs bf16 HIP {rel(flat8, flat16):.3e}")
     assert r16 <= gate(rb)
-    assert r8 <= 1.5e-2  # measured (r02): 9.93e-3; gate 1.5x (was 6 x reference bf16 drift + 2e-2 = 3.5e-2)
+    assert r8 <= fp8_block_gate(rb), (r8, rb)  # 5 x 2.6e-3 = 1.3e-2; measured (r02-r05) 9.93e-3
 
 
 @torch.no_grad()

@@ -1,7 +1,7 @@
 """Interleaved A/B of bf16 attention kernel variants at config 2 (B 2, H 48, N 17 776), one process, random data;
 median and min per variant over the rounds (cdna_hip_programming.md §5.4 rule 24).
 
-    python tools/attn_ab.py --modes w64,s16,a16 [--rounds 5] [--iters 20] [--unbounded lazy,a16]
+    python tools/attn_ab.py --modes p2,s16 [--rounds 5] [--iters 20] [--unbounded p2a,a16]
 Modes are VP_ATTN_BOUNDED_MODE values (bounded-score launches); --unbounded adds VP_ATTN_UNBOUNDED_MODE values run
 without the bounded flag.
 """
@@ -20,7 +20,7 @@ from tools.bench_kernels import timeit  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--modes", default="w64,s16")
+    ap.add_argument("--modes", default="p2,s16")
     ap.add_argument("--unbounded", default="")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)

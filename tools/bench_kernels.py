@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--gemm-variants", default="5,11", help="VP_GEMM_VARIANT values, interleaved over 2 rounds")
-    ap.add_argument("--variant", default="", help="attention kernel(s): lazy, bounded, w32, w64, s16 (default: lazy, bounded)")
+    ap.add_argument("--variant", default="", help="attention kernel(s): p2a, a16, p2w, p2w2, p2, s16, bounded (default: p2a, bounded)")
     ap.add_argument("--variant8", default="", help="fp8 attention kernel variant(s) (VP_ATTN8_VARIANT), e.g. 1,2")
     ap.add_argument("--only", default="", help="attention | attn8 | gemm | mx | norms: run just that kernel (for rocprofv3 "
                     "--pmc passes; attn8 = the fp8 attention only)")
@@ -95,15 +95,15 @@ def main():
     if args.only == "gemm":
         print(json.dumps(res))
         return
-    # lazy = the running-max kernel; bounded = the no-max kernel the processors pick when the qk-norm
-    # bounds every score (these random q, k: |q.k| * 0.125 * log2 e stays far below the bound of 60)
-    variants = tuple(args.variant.split(",")) if args.variant else ("lazy", "bounded")
+    # p2a = the default (no bound needed); bounded = the launch with VP_ATTN_BOUNDED_SCORES (these random q, k:
+    # |q.k| * 0.125 * log2 e stays far below the bound of 60), p2a there too unless VP_ATTN_BOUNDED_MODE names p2 / s16
+    variants = tuple(args.variant.split(",")) if args.variant else ("p2a", "bounded")
     if args.only in ("attn8", "norms"):
         variants = ()
     for rnd in range(2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
         for var in variants:
-            # unbounded-score kernels (p2a = the default without a proven bound, a16, lazy) vs bounded ones
-            unb = var in ("lazy", "a16", "p2a", "p2w", "p2w2")
+            # unbounded-score kernels (p2a = the default without a proven bound, a16, p2w, p2w2) vs bounded ones
+            unb = var in ("a16", "p2a", "p2w", "p2w2")
             K.set_knob("VP_ATTN_BOUNDED_MODE", None)
             K.set_knob("VP_ATTN_UNBOUNDED_MODE", None)
             if var != "bounded":

@@ -102,7 +102,6 @@ _SIGS = {
     "vp_gemm_mx_fp8": (i32, [C.POINTER(GemmMxDesc), vp]),
     "vp_mx_scale_bytes": (i64, [i64, i64]),
     "vp_mx_quantize_bf16": (i32, [vp, i64, vp, i64, vp, i32, i32, vp]),
-    "vp_mx_mfma_probe": (i32, [vp, vp, vp, vp, vp, vp]),
     "vp_adaln_modulate_mx_fp8": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, f32, vp, i64, vp]),
     "vp_attention_fwd_bf16": (i32, [C.POINTER(AttnDesc), vp]),
     "vp_attention_fwd_fp8": (i32, [C.POINTER(AttnFp8Desc), vp]),
@@ -112,7 +111,6 @@ _SIGS = {
     "vp_gemm_variant_built": (i32, [i32]),
     "vp_v_pack_fp8_bytes": (i64, [i32, i32, i32, C.POINTER(i64), C.POINTER(i64)]),
     "vp_v_pack_fp8": (i32, [vp, i64, i64, i32, i32, i32, vp, vp, vp]),
-    "vp_mx_mfma_probe32": (i32, [vp, vp, vp, vp, vp, vp]),
     "vp_head_norm_rope_fp8": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp, vp, f32, vp]),
     "vp_adaln_modulate_bf16": (i32, [vp, vp, i64, i32, i32, i32, i32, vp, vp, f32, vp, i64, vp]),
     "vp_head_norm_rope_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, i32, vp, vp, f32, vp, vp, vp, i64,
@@ -166,6 +164,11 @@ _SIGS = {
 }
 
 EXPORTS = tuple(_SIGS)
+# include/vp_hip_diag.h: only in a library built with -DVP_DIAG=1 (python -m videopainter_amd.build --diag)
+DIAG_SIGS = {
+    "vp_mx_mfma_probe": (i32, [vp, vp, vp, vp, vp, vp]),
+    "vp_mx_mfma_probe32": (i32, [vp, vp, vp, vp, vp, vp]),
+}
 
 # the library's A/B knobs (vp_set_knob): read from the environment once at load; knob_values mirrors them
 KNOBS = ("VP_GEMM_VARIANT", "VP_GEMM_NO_TAIL", "VP_GEMM_GROUP", "VP_GEMM8_VARIANT", "VP_ATTN_BOUNDED_MODE",
@@ -197,6 +200,11 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        for name, (res, args) in DIAG_SIGS.items():
+            if hasattr(L, name):
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
         if L.vp_abi_version() != ABI_VERSION:
             raise HipLibraryError(f"libvp_hip ABI {L.vp_abi_version()} != {ABI_VERSION}; rebuild")
         built = (L.vp_build_digest() or b"").decode()
@@ -213,6 +221,11 @@ def lib():
         knob_values.update({k: os.environ.get(k) for k in KNOBS})  # what the library read at load
         _lib = L
         return L
+
+
+def has_diag() -> bool:
+    """True when the loaded library is the diagnostic build (include/vp_hip_diag.h entry points present)."""
+    return all(hasattr(lib(), n) for n in DIAG_SIGS)
 
 
 def _source_digest():

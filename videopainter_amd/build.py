@@ -42,7 +42,9 @@ def _sources():
 def source_digest() -> str:
     """sha256 of the sources, headers and flags (repo-relative paths: the GPU box's checkout path differs)."""
     h = hashlib.sha256()
-    for p in _sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "vp_hip.h")]:
+    for p in _sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "vp_hip.h"),
+                                                                          os.path.join(ROOT, "include",
+                                                                                       "vp_hip_diag.h")]:
         with open(p, "rb") as f:
             h.update(os.path.relpath(p, ROOT).encode())  # relative: the GPU box's checkout path differs
             h.update(f.read())
@@ -107,7 +109,7 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, extra_flags
 
 
 if __name__ == "__main__":
-    # python -m videopainter_amd.build [--force] [--out PATH] [--extra FILE:FLAG ...]
+    # python -m videopainter_amd.build [--force] [--diag] [--out PATH] [--extra FILE:FLAG ...]
     args = sys.argv[1:]
     o, ex = LIB, {}
     for i, a in enumerate(args):
@@ -116,4 +118,8 @@ if __name__ == "__main__":
         if a == "--extra":
             f, fl = args[i + 1].split(":", 1)
             ex.setdefault(f, []).append(fl)
+    if "--diag" in args:  # the diagnostic entry points (include/vp_hip_diag.h) in a library of their own
+        o = o if "--out" in args else os.path.join(LIBDIR, "libvp_hip_diag.so")
+        for f in ("attention.hip", "gemm.hip"):
+            ex.setdefault(f, []).append("-DVP_DIAG=1")
     build(force="--force" in args, out=o, extra_flags=ex)

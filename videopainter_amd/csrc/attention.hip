@@ -35,10 +35,6 @@
 
 #include "vp_common.h"
 
-#ifndef VP_ATTN_EXTRA_VARIANTS
-#define VP_ATTN_EXTRA_VARIANTS 0
-#endif
-
 namespace {
 
 constexpr int NW = 8;               // waves per workgroup
@@ -51,8 +47,6 @@ constexpr int NP = KB / 8;          // 1-KiB DMA pieces (8 rows) per operand per
 constexpr int PPW = NP / NW;        // pieces per wave
 constexpr int HALVES = KB / 32;
 static_assert(NP % NW == 0, "pieces per wave");
-
-enum { MODE_LAZY = 0, MODE_BOUNDED = 1 };
 
 // ---- diagnostic builds only (tools/attn_clock.py builds them into their own library; the default library has
 // none of this).  VP_CLOCK_STAMPS: every workgroup of p2 / p2a / s16 / a16 stamps s_memtime and s_memrealtime before
@@ -143,111 +137,6 @@ VP_DEV void mask_half(f32x16& s, int lim, int kh, int hl) {
   }
 }
 
-// ---- LAZY mode: C-init half tiles.  A lane rescales only when its tile max exceeds its running max by more than
-// `thr` (thr = -inf before the first tile, so the first tile always sets m; afterwards RESCALE_THR: P stays
-// <= 2^RESCALE_THR, exact in bf16's exponent range, and the ratio O / l is unchanged). ----
-constexpr float RESCALE_THR = 8.f;
-
-VP_DEV void softmax_half_ci(f32x16& s, float& m_run, float& thr, float& l_run, f32x16& negm, f32x16 (&o)[2],
-                            bf16x8 (&pf)[2]) {
-  float m2[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int o8 = j * 8;
-    m2[j] = fmaxf(fmaxf(fmaxf(s[o8], s[o8 + 1]), s[o8 + 2]), fmaxf(fmaxf(s[o8 + 3], s[o8 + 4]), s[o8 + 5]));
-    m2[j] = fmaxf(fmaxf(m2[j], s[o8 + 6]), s[o8 + 7]);
-  }
-  float mx = fmaxf(m2[0], m2[1]);
-  {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-    mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-  }
-  if (__ballot(mx > thr) != 0ull) {  // wave-uniform: some query's tile max passed its threshold
-    const float dm = mx > thr ? mx : 0.f;
-    const float alpha = __builtin_amdgcn_exp2f(-dm);
-    l_run *= alpha;
-    m_run += dm;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o[0][i] *= alpha;
-      o[1][i] *= alpha;
-      s[i] -= dm;
-      negm[i] = -m_run;
-    }
-    thr = RESCALE_THR;
-  }
-  float ps[4];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float p = __builtin_amdgcn_exp2f(s[i]);
-    ps[i & 3] = i < 4 ? p : ps[i & 3] + p;
-    pf[i >> 3][i & 7] = f2bf(p);
-  }
-  l_run += (ps[0] + ps[1]) + (ps[2] + ps[3]);
-}
-
-// QK^T half with the first MFMA in inline asm so its destination is a fresh tuple (early-clobber) while C = -m
-// stays in its own registers: with the builtin, the compiler coalesces the rescale path's phi of -m into the second
-// half's accumulator and pays 8 v_mov_b64 per half to refill it.  The following builtin MFMAs accumulate on the
-// asm result in place (same opcode, exactly overlapping srcC: no wait states); -m is written by VALU only in the
-// rescale branch, long before the next QK^T.
-VP_DEV void qk_half_ci(const char* Kl, int kh, const bf16x8 (&qf)[4], const f32x16& negm, f32x16& s, int lane) {
-  const int hl = lane >> 5;
-  const int row = kh * 32 + (lane & 31);
-  const char* kr = Kl + row * 128;
-  const int sw = swz(row);
-  bf16x8 k0 = *(const bf16x8*)(kr + ((hl ^ sw) << 4));
-  bf16x8 k1 = *(const bf16x8*)(kr + (((2 + hl) ^ sw) << 4));
-  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(s) : "v"(k0), "v"(qf[0]), "v"(negm));
-  k0 = *(const bf16x8*)(kr + (((4 + hl) ^ sw) << 4));
-  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[1], s, 0, 0, 0);
-  k1 = *(const bf16x8*)(kr + (((6 + hl) ^ sw) << 4));
-  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[2], s, 0, 0, 0);
-  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[3], s, 0, 0, 0);
-}
-
-// BOUNDED modes: QK^T from C = 0 (the raw log2-unit scores)
-VP_DEV void qk_half_zero(const char* Kl, int kh, const bf16x8 (&qf)[4], f32x16& s, int lane) {
-  const int hl = lane >> 5;
-  const int row = kh * 32 + (lane & 31);
-  const char* kr = Kl + row * 128;
-  const int sw = swz(row);
-  bf16x8 k0 = *(const bf16x8*)(kr + ((hl ^ sw) << 4));
-  bf16x8 k1 = *(const bf16x8*)(kr + (((2 + hl) ^ sw) << 4));
-  const f32x16 z = {};
-  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[0], z, 0, 0, 0);
-  k0 = *(const bf16x8*)(kr + (((4 + hl) ^ sw) << 4));
-  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[1], s, 0, 0, 0);
-  k1 = *(const bf16x8*)(kr + (((6 + hl) ^ sw) << 4));
-  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[2], s, 0, 0, 0);
-  s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[3], s, 0, 0, 0);
-}
-
-// Lazy-max softmax half: exp2 straight off the C-init accumulator and sum, no max.  Correct as long as every
-// exponent s - m stays small; the check is on the sum this lane just computed (it bounds each of its 16 terms):
-// if any lane's sum exceeds 16 * 2^RESCALE_THR the wave runs the max path (softmax_half_ci) on the same scores,
-// which then rescales.  Otherwise P <= 2^(RESCALE_THR + 4), exact in bf16's exponent range, and
-// O / l is unchanged.  Returns false when the caller must take the max path.
-VP_DEV bool softmax_half_lazy(const f32x16& s, float& l_run, bf16x8 (&pf)[2]) {
-  float ps[4];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float p = __builtin_amdgcn_exp2f(s[i]);
-    ps[i & 3] = i < 4 ? p : ps[i & 3] + p;
-    pf[i >> 3][i & 7] = f2bf(p);  // packed right away (discarded if the check fails)
-  }
-  const float ls = (ps[0] + ps[1]) + (ps[2] + ps[3]);
-  if (__ballot(!(ls <= 16.f * (1 << (int)RESCALE_THR))) != 0ull) return false;  // NaN/inf included
-  l_run += ls;
-  return true;
-}
-
-// BOUNDED: p = exp2(s), s the raw score (the row sums come from the caller's MFMAs over the packed P)
-VP_DEV void softmax_half_bounded(const f32x16& s, bf16x8 (&pf)[2]) {
-#pragma unroll
-  for (int i = 0; i < 16; ++i) pf[i >> 3][i & 7] = f2bf(__builtin_amdgcn_exp2f(s[i]));
-}
-
 // ---- LDS-DMA staging (global_load_lds_dwordx4, saddr + 32-bit voffset): the LDS destination is lane-linear, so
 // both images are unpadded [rows][128 B] and their bank swizzles are applied on the SOURCE address
 // (cdna_hip_programming.md §5.4 rule 21).  K: chunk ^ swz(row) (conflict-free ds_read_b128).  V: chunk ^
@@ -306,30 +195,6 @@ VP_DEV void store_out(const vp_attn_desc& d, const f32x16 (&o)[2], float l_run, 
       }
       *(bf16x4*)(orow + dd) = ov;
     }
-}
-
-// V^T fragments for one 32-key half from the swizzled V image (vo[dh]: this lane's byte offset of its first
-// 4-row block in the 16-key slab, constant over the slabs because vswz depends only on row bit 1); RS: the row-sum
-// MFMA per 16-key slab (sel = the 0/1 selector operand, lsum its accumulator)
-template <bool RS>
-VP_DEV void pv_half(const char* Vl, int kh, const bf16x8 (&pf)[2], f32x16 (&o)[2], const int (&vo)[2],
-                    const bf16x8& sel, f32x4& lsum) {
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int ks = kh * 2 + j;
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh) {
-      const char* base = Vl + ks * 16 * 128 + vo[dh];
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * 128));
-      const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      o[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[j], o[dh], 0, 0, 0);
-    }
-    // row sums: the P^T operand read as the B operand of a 16x16x32 MFMA (lane l: column l % 16, K-block l / 16),
-    // whose column n then holds query n's 16 keys in K-blocks 0 / 2 and query n + 16's in blocks 1 / 3; the
-    // selector keeps blocks 0 / 2 in rows 0-7 and blocks 1 / 3 in rows 8-15 (see the kernel's `sel`)
-    if constexpr (RS) lsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf[j], lsum, 0, 0, 0);
-  }
 }
 
 // ---- grid-tail split: the last partial round of workgroups (nblk mod resident slots) is re-launched as
@@ -438,387 +303,29 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const vp_attn_desc d,
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// The kernel: 8 waves x 32 queries, 128-key tiles in a 2-slot LDS ring filled by global_load_lds (no staging
-// registers, no LDS write pass), consumed as 32-key halves.  Tile t + 1 is issued at the top of tile t (its slot was
-// released by the barrier that closed tile t-1); the bottom of tile t waits for tile t+1, then one barrier.
-// TAIL: the grid-tail split instance (a separate symbol, so profiles list it apart).
-// ------------------------------------------------------------------------------------------------------------
-template <int MODE, bool TAIL = false>
-__global__ __launch_bounds__(NW * 64, 4) void attn_fwd(const vp_attn_desc d, const AttnSplit sp) {
-  constexpr bool BOUNDED = MODE == MODE_BOUNDED;
-  constexpr bool RS = BOUNDED;  // row sums on the matrix pipe
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hl = lane >> 5;
-
-  const int nqb = (d.Nq + QB - 1) / QB;
-  const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
-  const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = t / nqb;
-  const int qb = t - bh * nqb;
-  const int b = bh / d.H;
-  const int h = bh - b * d.H;
-  const int tiles1 = (d.Nk + KB - 1) / KB;
-  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KB - 1) / KB : 0;
-  const int ntiles_all = tiles1 + tiles2;
-  // key-tile range of this workgroup (the whole sequence unless this is a tail split)
-  const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
-  const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
-
-  const int q = qb * QB + wave * 32 + (lane & 31);
-  const int qc = q < d.Nq ? q : d.Nq - 1;
-  const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
-  {
-    const float cq = d.scale * 1.4426950408889634f;  // scores leave the MFMA in log2 units
-#pragma unroll
-    for (int ds = 0; ds < 4; ++ds)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[ds][j] = f2bf(bf2f(qf[ds][j]) * cq);
-  }
-
-  // this lane's DMA rows / source chunks (piece p = wave + i*NW covers tile rows p*8 .. p*8+7)
-  int prow[PPW], kch[PPW], vch[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    prow[i] = (wave + i * NW) * 8 + (lane >> 3);
-    kch[i] = (lane & 7) ^ swz(prow[i]);
-    vch[i] = (lane & 7) ^ vswz(prow[i]);
-  }
-  auto slot_of = [&](int ti) { return smem + (ti & 1) * ST; };
-  auto issue = [&](int ti) {
-    const Seg sg = tile_seg(d, ti, tiles1, b, h);
-    char* slot = slot_of(ti);
-    const int last = sg.n - 1 - sg.key0;  // rows past the segment end re-read its last key (masked later)
-    const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
-    const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
-    const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int pc = wave + i * NW;
-      const int r = min(prow[i], last);
-      glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + pc * 1024);
-      glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
-    }
-  };
-
-  const int g = lane >> 4;
-  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
-  const int tcol = 16 * (g & 1) + 4 * (lane & 3);
-  int vo[2];
-#pragma unroll
-  for (int dh = 0; dh < 2; ++dh) vo[dh] = trow * 128 + (((dh * 4 + (tcol >> 3)) ^ vswz(trow)) << 4) + (tcol & 7) * 2;
-
-  float m_run = 0.f, l_run = 0.f, thr = -INFINITY;
-  f32x16 o[2], negm;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    o[0][i] = 0.f;
-    o[1][i] = 0.f;
-    negm[i] = 0.f;
-  }
-  // row-sum selector of the 16x16x32 MFMA: lane l supplies A-row l % 16, K-block l / 16; rows 0-7 take K-blocks
-  // 0 / 2 (query n), rows 8-15 blocks 1 / 3 (query n + 16)
-  f32x4 lsum = {0.f, 0.f, 0.f, 0.f};
-  bf16x8 sel;
-  {
-    const bf16 one = f2bf((((lane >> 4) & 1) == 0) == ((lane & 15) < 8) ? 1.f : 0.f);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sel[e] = one;
-  }
-
-  // a wave whose 32 queries all lie past Nq (the last query block of a head) only helps with the DMA and the
-  // barriers, leaving its SIMD to the co-resident workgroups
-  const bool active = qb * QB + wave * 32 < d.Nq;  // wave-uniform
-  issue(tbeg);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int ti = tbeg; ti < tend; ++ti) {
-    if (ti + 1 < tend) issue(ti + 1);
-    const char* Kl = slot_of(ti);
-    const Seg sg = tile_seg(d, ti, tiles1, b, h);
-    const int lim = sg.n - sg.key0;
-#pragma unroll
-    for (int kh = 0; kh < HALVES; ++kh) {
-      if (!active) break;
-      f32x16 sh;
-      bf16x8 pf[2];
-      if constexpr (BOUNDED) {
-        qk_half_zero(Kl, kh, qf, sh, lane);
-        if (lim < KB) mask_half(sh, lim, kh, hl);
-        softmax_half_bounded(sh, pf);
-      } else {
-        qk_half_ci(Kl, kh, qf, negm, sh, lane);
-        if (lim < KB) mask_half(sh, lim, kh, hl);
-        // the first half sets m by the max path (thr = -inf); afterwards the lazy path, falling back when it must
-        // (the lazy path leaves the scores intact, so the fallback needs no recompute)
-        if (thr == -INFINITY || !softmax_half_lazy(sh, l_run, pf)) softmax_half_ci(sh, m_run, thr, l_run, negm, o, pf);
-      }
-      pv_half<RS>(Kl + KT, kh, pf, o, vo, sel, lsum);
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // retire tile ti+1
-    __builtin_amdgcn_s_barrier();
-  }
-  // the row sum of this lane's query: split over the lane pair (l, l ^ 32) on the VALU; on the matrix pipe, query
-  // n < 16 sits in lane n, query n >= 16 in lane n + 16
-  float l_tot;
-  if constexpr (RS) {
-    const int qq = lane & 31;
-    l_tot = __shfl(lsum[0], qq < 16 ? qq : qq + 16, 64);
-  } else {
-    l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  }
-  if (sp.nsplit > 1) {
-    const int qi = wave * 32 + (lane & 31);
-    store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qi) * 66, o, m_run, l_tot, hl);
-  } else {
-    store_out(d, o, l_tot, q, b, h, hl, false, m_run);
-  }
-}
-
-
-// ------------------------------------------------------------------------------------------------------------
-// W64 (the BOUNDED-scores default): 4-wave workgroups of the same 256 queries, each wave TWO 32-query blocks.  The K
-// and V^T fragments of a 32-key half are read from LDS once and feed both blocks' MFMAs (half the LDS read bytes per
-// MFMA), and the two blocks' QK^T / exp / PV chains are independent, so a wave overlaps one block's softmax with the
-// other's MFMAs by itself; 2 waves/SIMD (256 VGPRs), two workgroups per CU with independent barriers.
+// 4-wave workgroups of 256 queries, each wave TWO 32-query blocks (the round-2 W64 structure, pruned in round 6 with
+// the 8-wave LAZY / W32 kernel: DESIGN_LOG.md): the K and V^T fragments of a 32-key half are read from LDS once and
+// feed both blocks' MFMAs, 2 waves/SIMD (256 VGPRs), two workgroups per CU with independent barriers.
 // ------------------------------------------------------------------------------------------------------------
 constexpr int NW4 = 4;
 constexpr int PPW4 = NP / NW4;
 static_assert(NW4 * 64 == QB, "same query block as the 8-wave kernel");
 
-// FAST: the full tiles of segment 1 are DMA'd from one scalar base per operand and tile with per-lane offsets fixed
-// for the whole loop (no per-tile segment lookup, row clamp or 64-bit offset multiply); segment 2 and partial tiles
-// take the general path with the lane's rows recomputed from the lane id.
-template <bool TAIL = false, bool FAST = false>
-__global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_w64(const vp_attn_desc d, const AttnSplit sp) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hl = lane >> 5;
-
-  const int nqb = (d.Nq + QB - 1) / QB;
-  const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
-  const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = t / nqb;
-  const int qb = t - bh * nqb;
-  const int b = bh / d.H;
-  const int h = bh - b * d.H;
-  const int tiles1 = (d.Nk + KB - 1) / KB;
-  const int tiles2 = d.Nk2 > 0 ? (d.Nk2 + KB - 1) / KB : 0;
-  const int ntiles_all = tiles1 + tiles2;
-  const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
-  const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
-  const int qw0 = qb * QB + wave * 64;  // first query of this wave
-  bf16x8 qf[2][4];
-  {
-    const float cq = d.scale * 1.4426950408889634f;
-#pragma unroll
-    for (int qi = 0; qi < 2; ++qi) {
-      const int q = qw0 + qi * 32 + (lane & 31);
-      const int qc = q < d.Nq ? q : d.Nq - 1;
-      const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) {
-        qf[qi][ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[qi][ds][j] = f2bf(bf2f(qf[qi][ds][j]) * cq);
-      }
-    }
-  }
-
-  auto slot_of = [&](int ti) { return smem + (ti & 1) * ST; };
-  auto issue_general = [&](int ti, int ln) {
-    const Seg sg = tile_seg(d, ti, tiles1, b, h);
-    char* slot = slot_of(ti);
-    const int last = sg.n - 1 - sg.key0;
-    const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
-    const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
-    const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
-#pragma unroll
-    for (int i = 0; i < PPW4; ++i) {
-      const int pc = wave + i * NW4;
-      const int prow = pc * 8 + (ln >> 3);
-      const int r = min(prow, last);
-      glds16(kb, (r * ksn + (((ln & 7) ^ swz(prow)) * 8)) * 2, slot + pc * 1024);
-      glds16(vb, (r * vsn + (((ln & 7) ^ vswz(prow)) * 8)) * 2, slot + KT + pc * 1024);
-    }
-  };
-  int prow[PPW4], kch[PPW4], vch[PPW4];
-  if constexpr (!FAST) {
-#pragma unroll
-    for (int i = 0; i < PPW4; ++i) {
-      prow[i] = (wave + i * NW4) * 8 + (lane >> 3);
-      kch[i] = (lane & 7) ^ swz(prow[i]);
-      vch[i] = (lane & 7) ^ vswz(prow[i]);
-    }
-  }
-  int voff_k[PPW4], voff_v[PPW4];
-  if constexpr (FAST) {
-#pragma unroll
-    for (int i = 0; i < PPW4; ++i) {
-      const int prow = (wave + i * NW4) * 8 + (lane >> 3);
-      voff_k[i] = (prow * (int)d.k_sn + (((lane & 7) ^ swz(prow)) * 8)) * 2;
-      voff_v[i] = (prow * (int)d.v_sn + (((lane & 7) ^ vswz(prow)) * 8)) * 2;
-    }
-  }
-  const char* kseg1 = (const char*)((const bf16*)d.K + (int64_t)b * d.k_sb + h * 64);
-  const char* vseg1 = (const char*)((const bf16*)d.V + (int64_t)b * d.v_sb + h * 64);
-  const int full1 = d.Nk / KB;
-  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem) + wave * 1024;
-  auto issue = [&](int ti) {
-    if constexpr (FAST) {
-      if (ti < full1) {
-        const unsigned la = lds0 + (ti & 1) * ST;
-        const char* kb = kseg1 + (int64_t)ti * KB * d.k_sn * 2;
-        const char* vb = vseg1 + (int64_t)ti * KB * d.v_sn * 2;
-#pragma unroll
-        for (int i = 0; i < PPW4; ++i) {
-          glds16_lds(kb, voff_k[i], la + i * NW4 * 1024);
-          glds16_lds(vb, voff_v[i], la + KT + i * NW4 * 1024);
-        }
-        return;
-      }
-      issue_general(ti, lane_id_opaque());
-    } else {
-      const Seg sg = tile_seg(d, ti, tiles1, b, h);
-      char* slot = slot_of(ti);
-      const int last = sg.n - 1 - sg.key0;
-      const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
-      const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
-      const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
-#pragma unroll
-      for (int i = 0; i < PPW4; ++i) {
-        const int pc = wave + i * NW4;
-        const int r = min(prow[i], last);
-        glds16(kb, (r * ksn + kch[i] * 8) * 2, slot + pc * 1024);
-        glds16(vb, (r * vsn + vch[i] * 8) * 2, slot + KT + pc * 1024);
-      }
-    }
-  };
-
-  const int g = lane >> 4;
-  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
-  const int tcol = 16 * (g & 1) + 4 * (lane & 3);
-  int vo[2];
-#pragma unroll
-  for (int dh = 0; dh < 2; ++dh) vo[dh] = trow * 128 + (((dh * 4 + (tcol >> 3)) ^ vswz(trow)) << 4) + (tcol & 7) * 2;
-
-  f32x16 o[2][2];
-#pragma unroll
-  for (int qi = 0; qi < 2; ++qi)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o[qi][0][i] = 0.f;
-      o[qi][1][i] = 0.f;
-    }
-  f32x4 lsum[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  bf16x8 sel;
-  {
-    const bf16 one = f2bf((((lane >> 4) & 1) == 0) == ((lane & 15) < 8) ? 1.f : 0.f);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sel[e] = one;
-  }
-
-  const bool active = qw0 < d.Nq;  // wave-uniform (the second block may lie partly or wholly past Nq: computed,
-                                   // not stored)
-  issue(tbeg);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int ti = tbeg; ti < tend; ++ti) {
-    if (ti + 1 < tend) issue(ti + 1);
-    const char* Kl = slot_of(ti);
-    const char* Vl = Kl + KT;
-    const Seg sg = tile_seg(d, ti, tiles1, b, h);
-    const int lim = sg.n - sg.key0;
-#pragma unroll
-    for (int kh = 0; kh < HALVES; ++kh) {
-      if (!active) break;
-      // K fragments of this half, shared by the two query blocks
-      bf16x8 kf[4];
-      {
-        const int row = kh * 32 + (lane & 31);
-        const char* kr = Kl + row * 128;
-        const int sw = swz(row);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) kf[c] = *(const bf16x8*)(kr + (((2 * c + hl) ^ sw) << 4));
-      }
-      f32x16 sh[2];
-      const f32x16 z = {};
-#pragma unroll
-      for (int qi = 0; qi < 2; ++qi) {
-        sh[qi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[0], qf[qi][0], z, 0, 0, 0);
-#pragma unroll
-        for (int c = 1; c < 4; ++c) sh[qi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[c], qf[qi][c], sh[qi], 0, 0, 0);
-      }
-      if (lim < KB) {
-        mask_half(sh[0], lim, kh, hl);
-        mask_half(sh[1], lim, kh, hl);
-      }
-      bf16x8 pf[2][2];
-      softmax_half_bounded(sh[0], pf[0]);
-      softmax_half_bounded(sh[1], pf[1]);
-      // V^T fragments read once for both blocks
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int ks = kh * 2 + j;
-#pragma unroll
-        for (int dh = 0; dh < 2; ++dh) {
-          const char* base = Vl + ks * 16 * 128 + vo[dh];
-          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
-          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * 128));
-          const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          o[0][dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0][j], o[0][dh], 0, 0, 0);
-          o[1][dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[1][j], o[1][dh], 0, 0, 0);
-        }
-        lsum[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf[0][j], lsum[0], 0, 0, 0);
-        lsum[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf[1][j], lsum[1], 0, 0, 0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  const int qq = lane & 31;
-#pragma unroll
-  for (int qi = 0; qi < 2; ++qi) {
-    const float l_tot = __shfl(lsum[qi][0], qq < 16 ? qq : qq + 16, 64);
-    const int q = qw0 + qi * 32 + qq;
-    if (sp.nsplit > 1) {
-      const int qin = wave * 64 + qi * 32 + qq;
-      store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QB + qin) * 66, o[qi], 0.f, l_tot,
-                    hl);
-    } else {
-      store_out(d, o[qi], l_tot, q, b, h, hl, false, 0.f);
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------------------------
-// P1 (BOUNDED scores): one wave per SIMD (cdna_hip_programming.md "4-wave, one-wave-per-SIMD" attention form).  The
-// W64 math (4 waves x 64 queries = two 32-query blocks per wave, 32x32x16 MFMA, row sums on the matrix pipe), but one
-// workgroup per CU with the whole register file per wave, a 4-slot LDS ring (tiles DMA'd two ahead) and the work of
-// a wave software-pipelined over "jobs" j = (32-key half, query block): step j runs the QK^T of job j + 1 and the PV
-// (+ row sum) of job j - 1 on the matrix pipe while the VALU does job j's exp2 + bf16 packs, so every MFMA gap holds
-// two v_exp_f32 and one pack (8 + 16 + 4.5 issue cycles of the 32) instead of relying on a second wave to fill it.
-// The K / V^T fragments of a half are read one step ahead (double-buffered by half parity); the pipeline runs across
-// tile boundaries: the last step of a tile waits for the next tile, passes the tile barrier, reads its first K
-// fragments, runs its PV first and the next tile's first QK^T last (the LDS latency under the 4 PV MFMAs).
+// P2 (the software-pipelined "p1 step" form, two workgroups per CU): 4 waves x 64 queries = two 32-query blocks per
+// wave, 32x32x16 MFMA, row sums on the matrix pipe, and the work of a wave software-pipelined over "jobs" j =
+// (32-key half, query block): step j runs the QK^T of job j + 1 and the PV (+ row sum) of job j - 1 on the matrix
+// pipe while the VALU does job j's exp2 + bf16 packs, so every MFMA gap holds two v_exp_f32 and one pack.  The K
+// fragments of a half are read one step ahead (double-buffered by half parity); the pipeline runs across tile
+// boundaries.  (The round-1 one-workgroup-per-CU form "p1" on a 4-slot ring was pruned in round 6: DESIGN_LOG.md.)
 // ------------------------------------------------------------------------------------------------------------
-constexpr int P1_SLOTS = 4;
-constexpr int P1_LDS = P1_SLOTS * ST;  // 128 KB: one workgroup per CU
-
 struct P1Regs {
   bf16x8 qf[2][4];  // Q^T of the two query blocks (pre-scaled)
   f32x16 o[2][2];   // O^T[block][dim half]
   f32x16 s[2];      // S^T of the job in flight per block
   u32x4 pf[2][2];   // packed bf16 P^T per block, 16-key slabs
   bf16x8 kf[2][4];  // K fragments by half parity
-  bf16x8 vf[2][4];  // V^T fragments by half parity: [slab j * 2 + dim half]
+  bf16x8 vf[1][4];  // V^T fragments of the current half: [slab j * 2 + dim half]
   f32x4 lsum[2];
   f32x16 negm;      // anchored (p2a): C operand of every QK^T chain = -anchor (wave-uniform), unused otherwise
   float anc;        // the wave's anchor (log2 score units)
@@ -896,7 +403,7 @@ VP_DEV void p1_step(P1Regs& r, const bf16x8& sel) {
       if constexpr (QK) {
         p1_fence();
         // anchored: the chain starts from C = -anchor, so S - anchor leaves the matrix pipe (no VALU).  Its first MFMA
-        // is inline asm with an early-clobber destination (as qk_half_ci): with the builtin the compiler coalesces the
+        // is inline asm with an early-clobber destination: with the builtin the compiler coalesces the
         // rescale branch's update of s[0] with -anchor and copies the tuple (8 v_mov_b64) before the chain
         if (ANCH && c == 0)
           asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3"
@@ -955,110 +462,52 @@ VP_DEV void p1_mask(f32x16& s, int rem, int hl4) {
 
 // one 128-key tile = 8 steps (halves h = 0..3 x blocks 0, 1).  Step (h, b) exps job (h, b)'s scores while the
 // matrix pipe runs the QK^T of the next job and the PV of the previous one:
-//   even step (h, 0): read K(h+1), V(h) | QK (h, 1) [K(h)] + PV (h-1, 1) [V(h-1)]
-//   odd  step (h, 1):                     QK (h+1, 0) [K(h+1)] + PV (h, 0) [V(h)]
-// K and V^T fragments double-buffered by half parity, each read a whole step ahead of its first use.  On entry s[0]
-// holds job (0, 0)'s scores, kf[0] K(0) of this tile, vf[1] / pf[1] the previous tile's V(3) / last P (zeros before
-// the first tile).  The tile seam is at the start of step (3, 0): wait for the next tile (vmcnt: one tile per wave
-// left in flight unless wait_all), pass the barrier, read its K(0); last: no next tile (that QK^T is skipped).
+//   even step (h, 0): read K(h+1) | QK (h, 1) [K(h)] + PV (h-1, 1) [V(h-1)], then read V(h)
+//   odd  step (h, 1):               QK (h+1, 0) [K(h+1)] + PV (h, 0) [V(h)]
+// K fragments double-buffered by half parity, each read a whole step ahead of its first use; V^T single-buffered
+// (read after the even step's PV, a 4-MFMA group before the odd step's).  On entry s[0] holds job (0, 0)'s scores,
+// kf[0] K(0) of this tile, vf[0] / pf[1] the previous tile's V(3) / last P (zeros before the first tile).  The next
+// tile's DMA is issued at the top of the tile into the slot this tile's predecessor used, so every read of a slot
+// comes before the seam barrier; the seam is at the end of step (3, 0), after V(3) is read: wait for the next tile
+// (vmcnt), pass the barrier, read its K(0); last: no next tile (the last tile's step (3, 1) runs its QK^T on stale K
+// fragments, result unused: one code path, so the accumulators keep their registers through the tile).
 // masked: keys >= lim get score -inf (a segment's partial last tile; a uniform branch before the step).
-// SL = 2 (two workgroups per CU, a 2-slot ring, 256 registers per wave): the next tile's DMA is issued at the top of
-// the tile into the slot this tile's predecessor used, so every read of a slot comes before the seam barrier; V^T is
-// single-buffered (read after the even step's PV, a 4-MFMA group before the odd step's), and the seam moves to the
-// end of step (3, 0), after V(3) is read
-// VMC (SL = 2): the seam's vmcnt when the tile after next is already in flight (p2w: a 4-slot ring, tile t + 2
-// issued at the top of tile t, VMC = this tile's DMA instructions per wave; 0 for the 2-slot ring)
-// sync (SL = 2): the seam waits for the DMA and passes the barrier (false: the next tile was published by an earlier
-// barrier — p2w's one barrier per two tiles)
-// Barrier-free ring (p2wf): per-slot LDS counters instead of the seam barrier.  ready[s] counts the waves whose own
-// LDS-DMA pieces of the tile in slot s have landed (each wave adds 1 after its counted vmcnt wait), done[s] the waves
-// that finished reading that tile (added after the seam's lgkmcnt(0)).  A wave reads tile t once ready[t & 3] reached
-// NWV x (the slot's use count), and refills a slot once done[] for the tile it held did the same — so the waves of a
-// workgroup drift apart by up to the ring's slack instead of meeting at every tile.  Every spin is bounded: a wave that
-// gives up records it, and the workgroup then flags its block for the exact re-run (the anchored kernel's redo path),
-// so neither a hang nor a wrong result can come out of it.
-typedef __attribute__((address_space(3))) int lds_int;
-struct RingCtr {
-  lds_int* ready;  // [4]
-  lds_int* done;   // [4]
-};
-constexpr int RING_SPIN_MAX = 1 << 15;
-VP_DEV void ring_add(lds_int* c, int lane) {
-  if (lane == 0) __atomic_fetch_add(c, 1, __ATOMIC_RELAXED);
-}
-// wait until *c >= target; false when the bound ran out
-VP_DEV bool ring_wait(lds_int* c, int target) {
-#pragma unroll 1
-  for (int it = 0; it < RING_SPIN_MAX; ++it) {
-    const int v = __builtin_amdgcn_readfirstlane(__atomic_load_n(c, __ATOMIC_RELAXED));
-    if (v >= target) return true;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return false;
-}
-
-template <int SL, bool ANCH = false, int VMC = 0, bool BFREE = false>
+// VMC: the seam's vmcnt when the tile after next is already in flight (p2w: a 4-slot ring, tile t + 2 issued at the
+// top of tile t, VMC = this tile's DMA instructions per wave; 0 for the 2-slot ring)
+// sync: the seam waits for the DMA and passes the barrier (false: the next tile was published by an earlier barrier —
+// p2w2's one barrier per two tiles)
+template <bool ANCH = false, int VMC = 0>
 VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn, int lim, bool masked, bool last,
-                    bool wait_all, int lane, const int (&vo)[2], bool sync = true, RingCtr rc = {},
-                    int slot = 0, int nslot = 0, int tgt_next = 0, bool* stalled = nullptr) {
+                    bool wait_all, int lane, const int (&vo)[2], bool sync = true) {
   const int hl = lane >> 5;
   const char* Vl = Kl + KT;
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     // even step (h, 0)
-    if (h < 3) {
-      p1_read_k(Kl, h + 1, lane, r.kf[(h + 1) & 1]);
-    } else if (SL == 4 && !last) {
-      if (wait_all)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+    if (h < 3) p1_read_k(Kl, h + 1, lane, r.kf[(h + 1) & 1]);
+    if (masked) p1_mask(r.s[0], lim - 32 * h, 4 * hl);
+    if (h & 1)
+      p1_step<0, 1, 1, 1, 0, true, false, ANCH>(r, sel);
+    else
+      p1_step<0, 1, 1, 0, 0, true, false, ANCH>(r, sel);
+    p1_read_v(Vl, h, vo, r.vf[0]);
+    if (h == 3 && !last) {
+      if (sync) {
+        if (VMC == 0 || wait_all)
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VMC) : "memory");
+        __builtin_amdgcn_s_barrier();
+      }
       asm volatile("" ::: "memory");
       p1_read_k(Kn, 0, lane, r.kf[0]);
     }
-    if constexpr (SL == 4) p1_read_v(Vl, h, vo, r.vf[h & 1]);
-    if (masked) p1_mask(r.s[0], lim - 32 * h, 4 * hl);
-    if constexpr (SL == 2) {
-      if (h & 1)
-        p1_step<0, 1, 1, 1, 0, true, false, ANCH>(r, sel);
-      else
-        p1_step<0, 1, 1, 0, 0, true, false, ANCH>(r, sel);
-      p1_read_v(Vl, h, vo, r.vf[0]);
-      if (h == 3 && !last) {
-        if (BFREE) {
-          // own pieces of the next tile landed, own reads of this one retired: count both, then wait for the others'
-          if (VMC == 0 || wait_all)
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VMC) : "memory");
-          ring_add(rc.ready + nslot, lane);
-          ring_add(rc.done + slot, lane);
-          if (!ring_wait(rc.ready + nslot, tgt_next)) *stalled = true;
-        } else if (sync) {
-          if (VMC == 0 || wait_all)
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VMC) : "memory");
-          __builtin_amdgcn_s_barrier();
-        }
-        asm volatile("" ::: "memory");
-        p1_read_k(Kn, 0, lane, r.kf[0]);
-      }
-    } else if (h & 1) {
-      p1_step<0, 1, 1, 1, 0, true>(r, sel);
-    } else {
-      p1_step<0, 1, 1, 0, 1, true>(r, sel);
-    }
     // odd step (h, 1)
     if (masked) p1_mask(r.s[1], lim - 32 * h, 4 * hl);
-    // (the last tile's step (3, 1) runs its QK^T too, on stale K fragments, result unused: one code path, so the
-    // accumulators keep their registers through the tile)
-    constexpr int VO = SL == 2 ? 0 : -1;
-    if (SL == 2 && VP_P1_SEAM && h == 3)
-      p1_step<1, 0, 0, 0, VO < 0 ? 1 : 0, true, true, ANCH>(r, sel);
+    if (VP_P1_SEAM && h == 3)
+      p1_step<1, 0, 0, 0, 0, true, true, ANCH>(r, sel);
     else if (h & 1)
-      p1_step<1, 0, 0, 0, VO < 0 ? 1 : 0, true, false, ANCH>(r, sel);
+      p1_step<1, 0, 0, 0, 0, true, false, ANCH>(r, sel);
     else
       p1_step<1, 0, 0, 1, 0, true, false, ANCH>(r, sel);
   }
@@ -1098,30 +547,26 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
   }
 }
 
-// ANCH (p2a, SL = 2 only): the anchored softmax on the p2 pipeline, for scores with no proven bound.  The wave's
+// ANCH (p2a): the anchored softmax on the p2 pipeline, for scores with no proven bound.  The wave's
 // reference point (anchor) is an actual score: the max over its 64 queries and the first 32 keys it visits; it enters
 // every QK^T chain as the C operand (C = -anchor: no VALU), and moves up by 64 when a partial row sum passes 2^62
 // (p1_tile).  At the end a workgroup with a non-finite output or row sum (a score more than ~127 log2 units above
 // the anchor inside one tile), or a row sum under 2^-96 (a query whose scores sit far below the wave's anchor, where
 // small terms would underflow) stores nothing and raises its flag in sp.flags; the launcher then re-runs exactly
 // those blocks with the anchored 16x16x32 kernel (per-query anchors and its exact two-pass re-run).
-// NWV = 8 (p2w, SL = 2 only): the same per-wave pipeline in 8-wave workgroups of 512 queries, one per CU, on a 4-slot
+// NWV = 8 (p2w): the same per-wave pipeline in 8-wave workgroups of 512 queries, one per CU, on a 4-slot
 // ring (tile t + 2 issued at the top of tile t): a K / V tile loaded once serves twice the queries, so each wave
 // issues half the LDS-DMA instructions per tile (4 instead of 8) — the DMA issue is ~7 % of p2a's time
 // (tools/attn_clock.py ablation) — and the L2 -> LDS bytes per FLOP halve.
 // TPB = 2 (p2w only): one barrier per two tiles — tiles t + 2 and t + 3 issued together at the top of every even tile
 // of the range, both waited for and published by the barrier at the seam of the odd tile before them.
-// BFREE (p2wf: NWV = 8, TPB = 1, ANCH): the barrier-free ring above in place of the seam barrier.
-template <bool TAIL = false, int SL = 4, bool ANCH = false, int NWV = 4, int TPB = 1, bool BFREE = false>
-__global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_fwd_p1(const vp_attn_desc d,
-                                                                                        const AttnSplit sp) {
-  static_assert(!ANCH || SL == 2, "the anchored form is the two-workgroups-per-CU pipeline");
-  static_assert(NWV == 4 || (NWV == 8 && SL == 2), "8-wave workgroups run the p2 schedule");
+template <bool TAIL = false, bool ANCH = false, int NWV = 4, int TPB = 1>
+__global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const vp_attn_desc d, const AttnSplit sp) {
+  static_assert(NWV == 4 || NWV == 8, "4-wave (p2 / p2a) or 8-wave (p2w) workgroups");
   static_assert(TPB == 1 || NWV == 8, "one barrier per two tiles needs the 4-slot ring");
-  static_assert(!BFREE || (NWV == 8 && TPB == 1 && ANCH), "the barrier-free ring: p2w's 4-slot ring, anchored");
   constexpr int QBV = NWV * 64;               // queries per workgroup
   constexpr int PPWV = NP / NWV;              // DMA pieces per operand, wave and tile
-  constexpr int RING = NWV == 8 ? 4 : SL;     // LDS ring slots
+  constexpr int RING = NWV == 8 ? 4 : 2;      // LDS ring slots
   constexpr int AHEAD = RING / 2;             // tiles issued ahead
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -1240,7 +685,7 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
     for (int j = 0; j < 2; ++j) r.pf[qi][j] = (u32x4){0u, 0u, 0u, 0u};
   }
 #pragma unroll
-  for (int c = 0; c < 4; ++c) r.vf[SL == 2 ? 0 : 1][c] = (bf16x8){};  // job -1: 0 x 0
+  for (int c = 0; c < 4; ++c) r.vf[0][c] = (bf16x8){};  // job -1: 0 x 0
   bf16x8 sel;
   {
     const bf16 one = f2bf((((lane >> 4) & 1) == 0) == ((lane & 15) < 8) ? 1.f : 0.f);
@@ -1260,15 +705,7 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  // ring counters past the anchored flags (NWV ints): ready[4], done[4]
-  RingCtr rc{(lds_int*)(lds_void_t*)(smem + RING * ST + 32), (lds_int*)(lds_void_t*)(smem + RING * ST + 48)};
-  if (BFREE) {
-    if (tid < 8) rc.ready[tid] = 0;  // (ready and done are contiguous)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
   __builtin_amdgcn_s_barrier();
-  if (BFREE) ring_add(rc.ready + (tbeg & 3), lane);  // tile tbeg: published by the barrier, counted for its slot
-  bool stalled = false;
   if (any) p1_read_k(slot_of(tbeg), 0, lane, r.kf[0]);
   {
     const f32x16 z = {};
@@ -1313,9 +750,6 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
       }
       sync = !even;
     } else if (ti + AHEAD < tend && (!(VP_P1_ABL & 1) || ti == tbeg)) {
-      // (barrier-free ring: the slot of tile ti + 2 last held tile ti - 2; every wave must be done reading it)
-      if (BFREE && ti - 2 >= tbeg && !ring_wait(rc.done + ((ti - 2) & 3), NWV * (((ti - 2 - tbeg) >> 2) + 1)))
-        stalled = true;
       issue(ti + AHEAD);
     }
     int lim = KB;
@@ -1323,15 +757,14 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
       const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
       lim = sg.n - sg.key0;
     }
-    p1_tile<SL, ANCH, RING == 4 && SL == 2 && TPB == 1 ? 2 * PPWV : 0, BFREE>(
-        r, sel, slot_of(ti), slot_of(ti + 1), __builtin_amdgcn_readfirstlane(lim), lim < KB, ti + 1 >= tend,
-        TPB == 2 || ti + 2 >= tend, lane, vo, sync, rc, ti & 3, (ti + 1) & 3, NWV * (((ti + 1 - tbeg) >> 2) + 1),
-        &stalled);
+    p1_tile<ANCH, RING == 4 && TPB == 1 ? 2 * PPWV : 0>(r, sel, slot_of(ti), slot_of(ti + 1),
+                                                        __builtin_amdgcn_readfirstlane(lim), lim < KB,
+                                                        ti + 1 >= tend, TPB == 2 || ti + 2 >= tend, lane, vo, sync);
   }
   // drain: PV + row sums of the last job (3, 1)
 #pragma unroll
   for (int c = 0; c < 4; ++c)
-    r.o[1][c & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.vf[SL == 2 ? 0 : 1][c], as_bf16x8(r.pf[1][c >> 1]),
+    r.o[1][c & 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.vf[0][c], as_bf16x8(r.pf[1][c >> 1]),
                                                             r.o[1][c & 1], 0, 0, 0);
   r.lsum[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[1][0]), r.lsum[1], 0, 0, 0);
   r.lsum[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[1][1]), r.lsum[1], 0, 0, 0);
@@ -1353,7 +786,7 @@ __global__ __launch_bounds__(NWV * 64, (SL == 4 || NWV == 8) ? 1 : 2) void attn_
     // any non-finite row sum or output, or a row sum under 2^-96 (its terms would underflow), in the workgroup ->
     // store nothing, flag the block for the exact re-run (workgroup-uniform decision through 16 bytes of LDS past
     // the ring; the barrier also retires every wave's last reads of the ring)
-    bool bad = stalled;  // (a ring wait that ran out of bound: redo the block)
+    bool bad = false;
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi) {
       // (a tail-split partial of an empty key range holds no mass: only its non-finite values count.  A non-empty
@@ -1422,10 +855,7 @@ VP_DEV float xmax16(float x) {  // max over the 4 lanes c16 + 16 g (one query's 
 // overflow: the kernel checks every output and row sum at the end, and a workgroup that saw a non-finite value re-runs
 // its block exactly (pass 1: the row maxima over all keys; pass 2: p = exp2(s - max) <= 1).  Without ANCH (the host
 // proved |score| <= VP_ATTN_SCORE_BOUND) m = 0 and nothing is checked.
-// ORD 1: the PV phase per query tile (the 4 V^T fragments read first; then per qt: 8 exp2 + 4 packs, its 4 PV
-// MFMAs and its row-sum MFMA), so query tile qt's MFMAs run under qt + 1's transcendental work; ORD 0: all 32 exp2
-// first, then the 16 PV MFMAs, then the 4 row sums.
-template <bool TAIL = false, bool ANCH = false, int ORD = 0>
+template <bool TAIL = false, bool ANCH = false>
 __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d, const AttnSplit sp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -1582,29 +1012,6 @@ __global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_s16(const vp_attn_desc d
   using MaskF = std::integral_constant<bool, false>;
   // P = exp2(S) packed as the P^T B operand, then O^T += V^T P^T and the row sums
   auto pv_half = [&](const char* Vl, int kh, const f32x4 (&sc)[4][2]) {
-    if constexpr (ORD == 1) {
-      bf16x8 vf[4];
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const char* base = Vl + kh * 32 * 128 + vo[dt];
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 16 * 128));
-        vf[dt] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-#pragma unroll
-      for (int qt = 0; qt < 4; ++qt) {
-        bf16x8 pq;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          pq[i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][0][i]));
-          pq[4 + i] = f2bf(__builtin_amdgcn_exp2f(sc[qt][1][i]));
-        }
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pq, o[dt][qt], 0, 0, 0);
-        lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pq, lsum[qt], 0, 0, 0);
-      }
-      return;
-    }
     bf16x8 pf[4];
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt)
@@ -1831,6 +1238,7 @@ VP_DEV int tile_key(int k) {
 // 64-byte fp8 tile rows in LDS: physical 16-byte chunk = logical ^ swz8(row) (rows 4 apart land 16 banks apart)
 VP_DEV int swz8(int row) { return (row >> 2) & 3; }
 
+#if VP_DIAG  // diagnostic build only (include/vp_hip_diag.h)
 // probe: one 32x32x64 scaled MFMA with the layout above; C row-major [32][32] fp32
 __global__ void mx_probe32_kernel(const uint8_t* A, const uint8_t* B, const uint8_t* sa, const uint8_t* sb,
                                   float* C) {
@@ -1848,6 +1256,7 @@ __global__ void mx_probe32_kernel(const uint8_t* A, const uint8_t* B, const uint
   c = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, (int)sa[l], 0, (int)sb[l]);
   for (int i = 0; i < 16; ++i) C[(8 * (i >> 2) + 4 * g + (i & 3)) * 32 + r] = c[i];
 }
+#endif
 
 // V [B, N, ld] bf16 (head h at column h*64) -> V^T fp8 in tile K-slot order + per-(d, 32 keys) E8M0 scales.
 // One 256-thread block per (b, h, 64-key tile); thread t: d = t / 4, slots 16 (t % 4) .. +15.
@@ -2443,299 +1852,13 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc d
   store_out(d, o, qq < 16 ? v0 : v1, q, b, h, g, false);
 }
 
-#if VP_ATTN_EXTRA_VARIANTS  // rejected A/B variant: outside the default library
-// ---- f8p (VP_ATTN8_VARIANT=4): the fp8 kernel as a software pipeline, the p1 schedule carried over to e4m3.  4 waves
-// x 32 queries per workgroup at two workgroups per CU (256 VGPRs: two score buffers live), an 8-tile LDS ring filled
-// up to five tiles ahead with one barrier per two 64-key tiles.  Step j issues PV of tile j-1 (while tile j's max runs
-// beside it), then QK^T of tile j+1 while tile j's rescale decision and linear codes (LIN 2) are computed beside it;
-// tile j's row-sum MFMA closes the step.  A
-// rescale scales O after PV(j-1) and lsum after RS(j-1): the compiler's wait on those results is the only exposed
-// MFMA latency, on the (rare after the first tiles) rescale path.
-constexpr int F8P_SLOTS = 8;
-constexpr int F8P_STAGE = 2 * F8_TILE + 1024;  // K, V^T, the scales (128 B used)
-constexpr int F8P_LDS = F8P_SLOTS * F8P_STAGE;
-constexpr int F8P_OFF = 7;
-constexpr float F8P_THR = 1.5f;
-constexpr float F8P_LS = 8.f * 0x1p-16f;
-constexpr float F8P_C0 = (8.f * F8P_OFF + 56.f - LIN_DELTA) * 0x1p-16f;
-
-struct F8PRegs {
-  i32x8 qf;
-  f32x16 negm;
-  f32x16 o[2];
-  f32x16 s[2][2];  // [job parity][key half]
-  i32x8 pf[2];     // [job parity]
-  i32x8 kf[2];
-  i32x8 vf[2];
-  i32x8 sel;
-  f32x4 lsum;
-  float m_run, thr;
-  int vsw;
-};
-
-// P codes of one 32-key half (LIN 2, see f8_lin2_pack) into pf VGPRs 4 hh .. 4 hh + 3
-VP_DEV void f8p_pack_half(const f32x16& s, i32x8& pf, int hh) {
-  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const u16x2 lo = __builtin_amdgcn_cvt_pknorm_u16(s[4 * w + 0], s[4 * w + 1]);
-    const u16x2 hi = __builtin_amdgcn_cvt_pknorm_u16(s[4 * w + 2], s[4 * w + 3]);
-    pf[hh * 4 + w] = (int)__builtin_amdgcn_perm(__builtin_bit_cast(unsigned, hi), __builtin_bit_cast(unsigned, lo),
-                                                0x06040200u);
-  }
-}
-
-VP_DEV float f8p_max16(const f32x16& s) {
-  float a = fmaxf(fmaxf(s[0], s[1]), s[2]), c = fmaxf(fmaxf(s[3], s[4]), s[5]);
-  a = fmaxf(fmaxf(a, s[6]), s[7]);
-  c = fmaxf(fmaxf(c, s[8]), s[9]);
-  a = fmaxf(fmaxf(a, s[10]), s[11]);
-  c = fmaxf(fmaxf(c, s[12]), s[13]);
-  a = fmaxf(fmaxf(a, s[14]), s[15]);
-  return fmaxf(a, c);
-}
-
-// S^T = K Q^T + (-m) by asm: a fresh (early-clobber) destination with -m kept in its own registers; the builtin form
-// makes the compiler copy -m into the MFMA's C registers with 8 v_mov_b64 per step.  The hazard recognizer cannot
-// see into asm: the first VALU read of the result comes a full step later (after the row-sum MFMA, the seam and a PV
-// MFMA), far past the 19 wait states a 16-pass XDL result needs; the prologue pads explicitly.
-VP_DEV void f8p_qk(f32x16& s, const i32x8& kf, const i32x8& qf, const f32x16& negm, int sk, int sq) {
-  asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %3, %4, %5 op_sel_hi:[0,0,0]"
-               : "=&v"(s)
-               : "v"(kf), "v"(qf), "v"(negm), "v"(sk), "v"(sq));
-}
-
-// one pipeline step for job j (parity CUR): PV(j-1) if PV, QK(j+1) if QK, MASK: job j is the last (partial) tile
-template <int CUR, bool PV, bool QK, bool MASK, class RV>
-VP_DEV void f8p_step(F8PRegs& r, int lim, int sk, int sq, int g, RV&& read_v_own) {
-  constexpr int NXT = CUR ^ 1;  // = the parity of job j - 1 and of job j + 1
-  f32x16(&s)[2] = r.s[CUR];
-  if constexpr (MASK) {
-    if (lim < 64) {
-      mask_half(s[0], lim, 0, g);
-      mask_half(s[1], lim, 1, g);
-    }
-  }
-  p1_fence();
-  if constexpr (PV) r.o[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(r.vf[0], r.pf[NXT], r.o[0], 0, 0, 0, r.vsw, 0, 127);
-  float mx = f8p_max16(s[0]);
-  p1_fence();
-  if constexpr (PV) r.o[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(r.vf[1], r.pf[NXT], r.o[1], 0, 0, 1, r.vsw, 0, 127);
-  mx = fmaxf(mx, f8p_max16(s[1]));
-  {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-    mx = (fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) - F8P_C0) * (1.f / F8P_LS);
-  }
-  p1_fence();
-  // job j's V^T fragments for PV(j) in the next step (the PV MFMAs above were their last readers): a full step
-  // of cover for the LDS latency
-  read_v_own();
-  p1_fence();
-  // QK^T of job j + 1 with the current -m, issued before job j's rescale decision so the decision is off the matrix
-  // pipe's path; a rescale corrects that half afterwards (the second half is issued with the updated -m)
-  if constexpr (QK) f8p_qk(r.s[NXT][0], r.kf[0], r.qf, r.negm, sk, sq);
-  if (__ballot(mx > r.thr) != 0ull) {
-    // the asm QK^T above still reads -m and writes S: the wait states a VALU write / read of them needs
-    if constexpr (QK) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
-    const float dm = mx > r.thr ? mx : 0.f;
-    const float alpha = __builtin_amdgcn_exp2f(-dm);
-    // lane n < 16 holds the sums of queries n and n + 16: alpha of lane n + 16 by a row swap (VALU; a ds_bpermute
-    // here would make the compiler drain the LDS queue, the V^T reads in flight, before the next MFMA)
-    const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(alpha), __float_as_uint(alpha), false, false);
-    r.lsum[0] *= alpha;
-    r.lsum[1] *= __uint_as_float(a16[1]);
-    r.m_run += dm;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      r.o[0][i] *= alpha;
-      r.o[1][i] *= alpha;
-      s[0][i] -= F8P_LS * dm;
-      s[1][i] -= F8P_LS * dm;
-      r.negm[i] -= F8P_LS * dm;
-      if constexpr (QK) r.s[NXT][0][i] -= F8P_LS * dm;
-    }
-    // opaque: known as a splat, -m is otherwise kept once and copied into the MFMA's C registers every step
-    asm volatile("" : "+v"(r.negm));
-    r.thr = F8P_THR;
-  }
-  f8p_pack_half(s[0], r.pf[CUR], 0);
-  p1_fence();
-  if constexpr (QK) f8p_qk(r.s[NXT][1], r.kf[1], r.qf, r.negm, sk, sq);
-  f8p_pack_half(s[1], r.pf[CUR], 1);
-  p1_fence();
-  r.lsum = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(r.sel, r.pf[CUR], r.lsum, 0, 0, 0, 127, 0, 127);
-  p1_fence();
-}
-
-template <int P>
-VP_DEV void f8p_drain(F8PRegs& r) {
-  r.o[0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(r.vf[0], r.pf[P], r.o[0], 0, 0, 0, r.vsw, 0, 127);
-  r.o[1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(r.vf[1], r.pf[P], r.o[1], 0, 0, 1, r.vsw, 0, 127);
-}
-
-__global__ __launch_bounds__(256, 2) void attn_fwd_fp8p(const vp_attn_fp8_desc dd) {
-  const vp_attn_desc& d = dd.base;
-  constexpr int QB = 4 * 32;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 5;
-
-  const int nqb = (d.Nq + QB - 1) / QB;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = t / nqb;
-  const int qb = t - bh * nqb;
-  const int b = bh / d.H;
-  const int h = bh - b * d.H;
-  const int ntiles = dd.npad >> 6;
-
-  F8PRegs r;
-  const int q = qb * QB + wave * 32 + (lane & 31);
-  {
-    const int qc = q < d.Nq ? q : d.Nq - 1;  // rows past Nq compute on the last query; store_out skips them
-    const uint8_t* qrow = (const uint8_t*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
-    u32x4* hq = (u32x4*)&r.qf;
-    hq[0] = *(const u32x4*)(qrow + g * 16);
-    hq[1] = *(const u32x4*)(qrow + (g + 2) * 16);
-  }
-  const int sq = (dd.qk_scale & 0xff) + 3 - 16, sk = (dd.qk_scale >> 8) & 0xff;
-
-  // DMA: wave w stages K rows 16w .. 16w + 15 and V^T rows 16w .. (one 16-byte chunk per lane each), wave 0 lanes
-  // 0-7 also the V^T scales: 2 (waves 1-3) / 3 (wave 0) vmcnt entries per tile
-  const int ksn = (int)d.k_sn;
-  const int prow = wave * 16 + (lane >> 2);
-  const int pch = ((lane & 3) ^ swz8(prow)) << 4;
-  const int offk = prow * ksn + pch, offv = prow * dd.npad + pch;
-  const char* kbase = (const char*)d.K + (int64_t)b * d.k_sb + h * 64;
-  const char* vtbase = (const char*)d.V + (int64_t)bh * 64 * dd.npad;
-  const char* vsbase = (const char*)dd.vs + (int64_t)bh * ntiles * 128;
-  auto slot = [&](int kt) { return smem + (kt & (F8P_SLOTS - 1)) * F8P_STAGE; };
-  // LDS-DMA destinations as 32-bit LDS addresses from one wave-uniform base (no generic-pointer conversion and
-  // null check per instruction); the scales by all of wave 0's lanes (lane l re-reads chunk l % 8 into byte 16 l
-  // of the slot's 1 KB scale area, of which the first 128 bytes are the layout) so no lane mask is needed
-  const unsigned lds_base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem);
-  const int full_k = d.Nk >> 6;
-  const int offs = (lane & 7) * 16;
-  auto issue = [&](int kt) {
-    const unsigned st = lds_base + (unsigned)((kt & (F8P_SLOTS - 1)) * F8P_STAGE);
-    if (kt < full_k) {
-      glds16_lds(kbase + (int64_t)kt * 64 * ksn, offk, st + wave * 1024);
-    } else {  // rows past the end re-read the last key (masked later)
-      const int ln = lane_id_opaque();
-      const int pr = wave * 16 + (ln >> 2);
-      const int rr = min(kt * 64 + pr, d.Nk - 1);
-      glds16_lds(kbase, rr * ksn + (((ln & 3) ^ swz8(pr)) << 4), st + wave * 1024);
-    }
-    glds16_lds(vtbase + kt * 64, offv, st + F8_TILE + wave * 1024);
-    if (wave == 0) glds16_lds(vsbase + kt * 128, offs, st + 2 * F8_TILE);
-  };
-  const int r0 = lane & 31;
-  const int ca = (g ^ swz8(r0)) << 4, cb = ((g + 2) ^ swz8(r0)) << 4;
-  auto read_k = [&](int kt) {
-    const char* st = slot(kt);
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const char* kr = st + (hh * 32 + r0) * 64;
-      u32x4* hk = (u32x4*)&r.kf[hh];
-      hk[0] = *(const u32x4*)(kr + ca);
-      hk[1] = *(const u32x4*)(kr + cb);
-    }
-  };
-  // the scale word first: the compiler zero-extends it at the next join, and LDS reads complete in order, so its
-  // wait there leaves the four V^T reads behind it in flight
-  auto read_v = [&](int kt) {
-    const char* st = slot(kt);
-    r.vsw = *(const unsigned short*)(st + 2 * F8_TILE + lane * 2);
-#pragma unroll
-    for (int dh = 0; dh < 2; ++dh) {
-      const char* vr = st + F8_TILE + (dh * 32 + r0) * 64;
-      u32x4* hv = (u32x4*)&r.vf[dh];
-      hv[0] = *(const u32x4*)(vr + ca);
-      hv[1] = *(const u32x4*)(vr + cb);
-    }
-  };
-  // one barrier per two tiles: before steps j, j + 1 (j odd) tiles j + 1 and j + 2 have landed (issued at least two
-  // steps earlier; tiles j + 3, j + 4 may still be in flight), all waves are past steps j - 2, j - 1, so the slots of
-  // tiles j - 3, j - 2 are free for tiles j + 5, j + 6
-  auto seam2 = [&](int j) {
-    if (j + 4 < ntiles) {
-      if (wave == 0)
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (j + 5 < ntiles) issue(j + 5);
-    if (j + 6 < ntiles) issue(j + 6);
-  };
-
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    r.o[0][i] = 0.f;
-    r.o[1][i] = 0.f;
-    r.negm[i] = F8P_C0;
-  }
-  asm volatile("" : "+v"(r.negm));
-  r.lsum = (f32x4){0.f, 0.f, 0.f, 0.f};
-  r.m_run = 0.f;
-  r.thr = -INFINITY;
-  {
-    const int col = lane & 15, c = lane >> 4;
-    const int w = ((col == 0 && (c & 1) == 0) || (col == 1 && (c & 1) == 1)) ? 0x38383838 : 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r.sel[i] = w;
-  }
-
-  for (int kt = 0; kt < 6; ++kt)
-    if (kt < ntiles) issue(kt);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  read_k(0);
-  f8p_qk(r.s[0][0], r.kf[0], r.qf, r.negm, sk, sq);
-  f8p_qk(r.s[0][1], r.kf[1], r.qf, r.negm, sk, sq);
-  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-  const int last = ntiles - 1;
-  const int lim_last = d.Nk - last * 64;
-  auto rv = [&](int kt) { return [&read_v, kt]() { read_v(kt); }; };
-  if (ntiles == 1) {
-    f8p_step<0, false, false, true>(r, lim_last, sk, sq, g, rv(0));
-    f8p_drain<0>(r);
-  } else {
-    read_k(1);  // tiles 0 .. 5 landed in the prologue
-    f8p_step<0, false, true, false>(r, 64, sk, sq, g, rv(0));
-    int j = 1;
-    for (; j + 2 < ntiles; j += 2) {
-      seam2(j);
-      read_k(j + 1);
-      f8p_step<1, true, true, false>(r, 64, sk, sq, g, rv(j));
-      read_k(j + 2);
-      f8p_step<0, true, true, false>(r, 64, sk, sq, g, rv(j + 1));
-    }
-    if (j == ntiles - 2) {
-      seam2(j);
-      read_k(j + 1);
-      f8p_step<1, true, true, false>(r, 64, sk, sq, g, rv(j));
-      f8p_step<0, true, false, true>(r, lim_last, sk, sq, g, rv(j + 1));
-      f8p_drain<0>(r);
-    } else {
-      f8p_step<1, true, false, true>(r, lim_last, sk, sq, g, rv(j));
-      f8p_drain<1>(r);
-    }
-  }
-  const int qq = lane & 31;
-  const float v0 = __shfl(r.lsum[0], qq & 15, 64), v1 = __shfl(r.lsum[1], qq & 15, 64);
-  store_out(d, r.o, qq < 16 ? v0 : v1, q, b, h, g, false);
-}
-#endif  // VP_ATTN_EXTRA_VARIANTS
 }  // namespace
 
 namespace {
-// The attention kernels of the default library (VP_ATTN_EXTRA_VARIANTS=1 adds the rejected A/B variants: lazy / w32 =
-// the 8-wave kernels, w64 = the two-blocks-per-wave kernel with the general DMA, s16i, p1 = the one-workgroup-per-CU
-// pipeline; the fp8 exp2 + RNE form and f8p: DESIGN.md §3, §7).
+// The attention kernels of the library: the default p2a, its redo kernel a16, and the challengers kept for A/B
+// (p2 = p2a without the anchor for proven score bounds, s16 = the 16x16x32 form, p2w / p2w2 = p2a in 8-wave
+// workgroups).  The rejected variants of rounds 1-5 (lazy / w32 / w64 / w64f / s16i / p1 / p2wf, fp8 variants 1 and
+// 4) were pruned in round 6; their measurements stay in DESIGN_LOG.md and profiles/.
 struct AttnVar {
   const char* name;
   const void* fn;
@@ -2744,38 +1867,22 @@ struct AttnVar {
   int lds;  // dynamic LDS bytes
   int qb = QB;  // queries per workgroup
 };
-#if VP_ATTN_EXTRA_VARIANTS
-#define VP_EXTRA(a, b) (const void*)a, (const void*)b
-#else
-#define VP_EXTRA(a, b) nullptr, nullptr
-#endif
-enum { V_LAZY, V_W32, V_W64, V_S16, V_A16, V_S16I, V_P1, V_W64F, V_P2, V_P2A, V_P2W, V_P2W2, V_P2WF, V_NVAR };
+enum { V_S16, V_A16, V_P2, V_P2A, V_P2W, V_P2W2, V_NVAR };
 static const AttnVar attn_vars[] = {
-    {"lazy", VP_EXTRA(attn_fwd<MODE_LAZY>, (attn_fwd<MODE_LAZY, true>)), NW * 64, LDS_BYTES},
-    {"w32", VP_EXTRA(attn_fwd<MODE_BOUNDED>, (attn_fwd<MODE_BOUNDED, true>)), NW * 64, LDS_BYTES},
-    {"w64", VP_EXTRA(attn_fwd_w64<false>, attn_fwd_w64<true>), NW4 * 64, LDS_BYTES},
     {"s16", (const void*)attn_fwd_s16<false>, (const void*)attn_fwd_s16<true>, NW4 * 64, LDS_BYTES},
     {"a16", (const void*)attn_fwd_s16<false, true>, (const void*)attn_fwd_s16<true, true>, NW4 * 64, LDS_BYTES},
-    {"s16i", VP_EXTRA((attn_fwd_s16<false, false, 1>), (attn_fwd_s16<true, false, 1>)), NW4 * 64, LDS_BYTES},
-    {"p1", VP_EXTRA(attn_fwd_p1<false>, attn_fwd_p1<true>), NW4 * 64, P1_LDS},
-    {"w64f", VP_EXTRA((attn_fwd_w64<false, true>), (attn_fwd_w64<true, true>)), NW4 * 64, LDS_BYTES},
-    {"p2", (const void*)attn_fwd_p1<false, 2>, (const void*)attn_fwd_p1<true, 2>, NW4 * 64, 2 * ST},
-    {"p2a", (const void*)attn_fwd_p1<false, 2, true>, (const void*)attn_fwd_p1<true, 2, true>, NW4 * 64, 2 * ST + 16},
+    {"p2", (const void*)attn_fwd_p1<false>, (const void*)attn_fwd_p1<true>, NW4 * 64, 2 * ST},
+    {"p2a", (const void*)attn_fwd_p1<false, true>, (const void*)attn_fwd_p1<true, true>, NW4 * 64, 2 * ST + 16},
     // p2a in 8-wave workgroups of 512 queries on a 4-slot ring (attn_fwd_p1 NWV = 8)
-    {"p2w", (const void*)attn_fwd_p1<false, 2, true, 8>, (const void*)attn_fwd_p1<true, 2, true, 8>, 8 * 64,
-     4 * ST + 32, 512},
+    {"p2w", (const void*)attn_fwd_p1<false, true, 8>, (const void*)attn_fwd_p1<true, true, 8>, 8 * 64, 4 * ST + 32,
+     512},
     // p2w with one barrier per two tiles
-    {"p2w2", (const void*)attn_fwd_p1<false, 2, true, 8, 2>, (const void*)attn_fwd_p1<true, 2, true, 8, 2>, 8 * 64,
+    {"p2w2", (const void*)attn_fwd_p1<false, true, 8, 2>, (const void*)attn_fwd_p1<true, true, 8, 2>, 8 * 64,
      4 * ST + 32, 512},
-    // p2w on the barrier-free ring (per-slot LDS counters; rejected in round 5: 6.41 vs 6.24 ms, the clock up 3 % but
-    // the loop 5 % longer, profiles/r05_attn_p2wf_rejected.log)
-    {"p2wf", VP_EXTRA((attn_fwd_p1<false, 2, true, 8, 1, true>), (attn_fwd_p1<true, 2, true, 8, 1, true>)), 8 * 64,
-     4 * ST + 64, 512},
 };
-#undef VP_EXTRA
 static_assert(sizeof(attn_vars) / sizeof(attn_vars[0]) == V_NVAR, "variant table");
 // the anchored p2 family (a flag per block, the a16 redo)
-static bool anchored_var(int v) { return v == V_P2A || v == V_P2W || v == V_P2W2 || v == V_P2WF; }
+static bool anchored_var(int v) { return v == V_P2A || v == V_P2W || v == V_P2W2; }
 
 struct AttnPlan {
   const AttnVar* v;
@@ -2841,7 +1948,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   if (variant < 0) variant = V_P2A;
   // an unbounded launch needs a kernel that does not assume the bound: lazy, a16, p2a or p2w
   const bool anchored = anchored_var(variant);
-  if (!bounded && variant != V_LAZY && variant != V_A16 && !anchored) return VP_ERR_UNSUPPORTED;
+  if (!bounded && variant != V_A16 && !anchored) return VP_ERR_UNSUPPORTED;
   if (attn_vars[variant].fn == nullptr) return VP_ERR_UNSUPPORTED;
   // the resample processor's segment hints: k2_len / l_extra (the closed-form null keys, the default) are taken by
   // s16 / a16 and p1 / p2 / p2a; k2_full (null keys as zero-value keys) by the 16x16x32 kernels only (config 4 ran
@@ -2849,7 +1956,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   // so a k2_full launch, and any hinted launch of another kernel, takes s16 (bounded) / a16 (unbounded)
   if (d->k2_full != nullptr || d->k2_len != nullptr || d->l_extra != nullptr) {
     const bool takes = variant == V_S16 || variant == V_A16 ||
-                       ((variant == V_P1 || variant == V_P2 || anchored) && d->k2_full == nullptr);
+                       ((variant == V_P2 || anchored) && d->k2_full == nullptr);
     if (!takes) variant = bounded ? V_S16 : V_A16;
   }
   pl.var = variant;
@@ -2880,7 +1987,7 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
 extern "C" int vp_attention_variant_built(const char* name) {
   if (name != nullptr && strncmp(name, "fp8:", 4) == 0) {  // the fp8 kernel's VP_ATTN8_VARIANT values
     const int f = atoi(name + 4);
-    return f == 2 || f == 3 || f == 5 || ((f == 1 || f == 4) && VP_ATTN_EXTRA_VARIANTS) ? 1 : 0;
+    return f == 2 || f == 3 || f == 5 ? 1 : 0;
   }
   const int v = variant_by_name(name);
   return v >= 0 && attn_vars[v].fn != nullptr ? 1 : 0;
@@ -2957,6 +2064,7 @@ extern "C" int vp_diag_clock_read(void* host, int64_t slots) {
 }
 #endif
 
+#if VP_DIAG
 extern "C" int vp_mx_mfma_probe32(const void* A, const void* B, const void* sa, const void* sb, float* C,
                                   void* stream) {
   if (!A || !B || !sa || !sb || !C) return VP_ERR_ARG;
@@ -2965,6 +2073,7 @@ extern "C" int vp_mx_mfma_probe32(const void* A, const void* B, const void* sa, 
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
+#endif
 
 extern "C" int64_t vp_v_pack_fp8_bytes(int32_t B, int32_t H, int32_t N, int64_t* npad, int64_t* scale_bytes) {
   if (B <= 0 || H <= 0 || N <= 0) return -1;
@@ -3009,15 +2118,9 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
   // to 3, 2.28-2.30 against 2.22-2.24 PF/s interleaved at config 5's length, profiles/r04_fp8_skew_ab.log; a 3-tile
   // ring slot (1.26-1.71), K^T read one tile ahead (spills) and the first V^T half read beside K^T (-1.2 %) were
   // measured and dropped; so was its MFMA issue at raised wave priority, within noise, profiles/r04_fp8_prio_ab_rejected.log).
-  // variants 1 (exp2 + RNE) and 4 (f8p) are rejected A/B forms: built only with VP_ATTN_EXTRA_VARIANTS
-#if VP_ATTN_EXTRA_VARIANTS
-  static const void* const fns[] = {(const void*)attn_fwd_fp8<NW, 4, 2, true, 0>,
-                                    (const void*)attn_fwd_fp8<NW, 4, 2, true, 1>,
-                                    (const void*)attn_fwd_fp8<NW, 4, 2, true, 2>};
-#else
+  // variants 1 (exp2 + RNE) and 4 (f8p) were rejected A/B forms, pruned in round 6 (DESIGN_LOG.md)
   static const void* const fns[] = {nullptr, (const void*)attn_fwd_fp8<NW, 4, 2, true, 1>,
                                     (const void*)attn_fwd_fp8<NW, 4, 2, true, 2>};
-#endif
   static bool attr_set = false;
   if (!attr_set) {
     attr_set = true;
@@ -3026,9 +2129,6 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
         (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * F8_STAGE);
     (void)hipFuncSetAttribute((const void*)attn_fwd_fp8s<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               F8S_SLOTS * 2 * F8_STAGE);
-#if VP_ATTN_EXTRA_VARIANTS
-    (void)hipFuncSetAttribute((const void*)attn_fwd_fp8p, hipFuncAttributeMaxDynamicSharedMemorySize, F8P_LDS);
-#endif
   }
   const char* e = vp_knob(VPK_ATTN8_VARIANT);
   int variant = e != nullptr ? atoi(e) : 0;
@@ -3046,21 +2146,7 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
     VP_CHECK_LAUNCH();
     return VP_OK;
   }
-#if !VP_ATTN_EXTRA_VARIANTS
   if (variant == 1 || variant == 4) return VP_ERR_UNSUPPORTED;
-#else
-  if (variant == 4) {
-    const int nqb4 = (d.Nq + 127) / 128;
-    const int64_t grid4 = (int64_t)d.B * d.H * nqb4;
-    if (grid4 > 0x7fffffff) return VP_ERR_ARG;
-    void* args4[] = {(void*)dd};
-    const hipError_t le4 = hipLaunchKernel((const void*)attn_fwd_fp8p, dim3((unsigned)grid4), dim3(256), args4,
-                                           F8P_LDS, (hipStream_t)stream);
-    if (le4 != hipSuccess) return (int)le4;
-    VP_CHECK_LAUNCH();
-    return VP_OK;
-  }
-#endif
   const int nqb = (d.Nq + NW * 32 - 1) / (NW * 32);
   const int64_t grid = (int64_t)d.B * d.H * nqb;
   if (grid > 0x7fffffff) return VP_ERR_ARG;

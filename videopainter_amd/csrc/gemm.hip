@@ -148,9 +148,6 @@ VP_DEV void mfma_mx(f32x4& acc, const i32x8& w, const i32x8& a, int sw, int sa) 
                  : "+v"(acc) : "v"(w), "v"(a), "v"(sw), "v"(sa));
 }
 
-#ifndef VP_GEMM_EXTRA_VARIANTS
-#define VP_GEMM_EXTRA_VARIANTS 0
-#endif
 // the gated epilogue loads its residual rows before the LDS image (default; 0 = inside the row loop, A/B:
 // profiles/r04_gemm_epi_ab.log, out-projection 0.574-0.582 vs 0.630 ms)
 #ifndef VP_GEMM_EPI_RPRE
@@ -620,7 +617,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (VAR == 5 || VAR == 11 || VAR == 12 || VAR == 13) {
+  if constexpr (VAR == 5 || VAR == 11 || VAR == 13) {
     // Quadrant-phase pipeline.  Each wave's 128x64 C block is split into 4 quadrants (64 rows x 32 cols); a K-tile
     // (BK = 64) runs as 4 phases of 16 MFMAs, in the quadrant order (A0,B0) (A0,B1) (A1,B1) (A1,B0) so each phase
     // needs ONE new operand subtile, which is read from LDS into registers during the previous phase.  The LDS
@@ -835,99 +832,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     };
-    if constexpr (VAR == 12) {
-      // VAR 12: two phases of 32 MFMAs per K-tile and ONE barrier per K-tile.  Phase 0 of tile k runs quadrant-row 0
-      // against both quadrant-columns (A0 x B0, then A0 x B1), phase 1 quadrant-row 1 (A1 x B0, then A1 x B1).
-      // Register fragments: a0 / a1 (A quadrant-rows), b0 / b1 (B quadrant-cols).  Reads, each into registers
-      // nothing is still reading:
-      //   phase 0 (k): B1(k) first (needed by its second half), then A1(k);
-      //   phase 1 (k): after its first half (the last use of b0): A0(k + 1) and B0(k + 1).
-      // LDS-DMA: the whole of tile k + 2 (4 units, 8 instructions per wave) at the top of phase 1 (k), spread over
-      // that phase's first 16 MFMAs, into the stage tile k used.  The one barrier, at the top of phase 1 (k), follows
-      // every wave's vmcnt(0) (tile k + 1, issued one K-tile earlier, has landed: A0 / B0 (k + 1) are read in this
-      // phase, B1 / A1 (k + 1) in the next) and lgkmcnt(0) (every read of tile k has returned: its stage may be
-      // refilled).  So a wave runs 64 MFMAs per barrier, and its partner wave on the SIMD (the other half of the
-      // workgroup) hides the reads and the barrier wait.
-      FragA a0, a1;
-      FragB b0, b1;
-      auto dma_tile = [&](int tile, int part) {  // part p of 4: unit p of the tile (2 instructions)
-        if (tile < nk) issue_unit(part, tile);
-      };
-      // prologue: tiles 0 and 1 in flight, tile 0 landed and published, A0 / B0 (0) read
-      for (int u = 0; u < 4; ++u) dma_tile(0, u);
-      for (int u = 0; u < 4; ++u) dma_tile(1, u);
-      if (nk > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      readA(a0, Z{}, Z{});
-      readB(b0, Z{}, Z{});
-      const int sz = 0, so = 0;
-      auto mma4 = [&](const FragA& a, const FragB& bb, auto qm_c, auto qn_c, int grp) {  // 4 MFMAs: one A fragment row
-        constexpr int qm = decltype(qm_c)::value, qn = decltype(qn_c)::value;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[qn * 2 + j][qm * 4 + grp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                bb[ks * 2 + j], a[ks * 4 + grp], acc[qn * 2 + j][qm * 4 + grp], 0, 0, 0);
-      };
-      // STEADY: tile k + 2 exists (k + 2 < nk), so the DMA and the next reads are unconditional (no branch in the
-      // loop body)
-      auto tile12 = [&](int k, auto par_c, auto steady_c) {
-        using P = decltype(par_c);
-        using NP = std::integral_constant<int, 1 - P::value>;
-        constexpr bool STEADY = decltype(steady_c)::value;
-        const bool more = STEADY || k + 1 < nk;
-        // ---- phase 0 ----
-        // the previous phase's reads of a0 / b0 (issued a 16-MFMA group ago) retire here, before this phase's
-        // reads: the builtin wait tells the compiler's wait pass so (it otherwise waits lgkmcnt(0) for the new reads
-        // too at the loop head, before the first MFMA)
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        __builtin_amdgcn_sched_barrier(0);
-        readB(b1, P{}, O{});
-        readA(a1, P{}, O{});
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-        mma(a0, b0, Z{}, Z{}, sz, so);
-        mma(a0, b1, Z{}, O{}, sz, so);
-        __builtin_amdgcn_s_setprio(0);
-        // ---- phase 1 ----
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          if constexpr (STEADY) issue_unit(g, k + 2);
-          else dma_tile(k + 2, g);
-          __builtin_amdgcn_sched_barrier(0);
-          __builtin_amdgcn_s_setprio(1);
-          mma4(a1, b0, O{}, Z{}, g);
-          __builtin_amdgcn_s_setprio(0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (more) {
-          readA(a0, NP{}, Z{});
-          readB(b0, NP{}, Z{});
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-        mma(a1, b1, O{}, O{}, sz, so);
-        __builtin_amdgcn_s_setprio(0);
-      };
-      using T_ = std::integral_constant<bool, true>;
-      using F_ = std::integral_constant<bool, false>;
-      int k = 0;
-      for (; k + 3 < nk; k += 2) {
-        tile12(k, Z{}, T_{});
-        tile12(k + 1, O{}, T_{});
-      }
-      // tail (at most 3 tiles; k is even here, so the parities are static)
-      if (k < nk) tile12(k, Z{}, F_{});
-      if (k + 1 < nk) tile12(k + 1, O{}, F_{});
-      if (k + 2 < nk) tile12(k + 2, Z{}, F_{});
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __syncthreads();
-    } else {
+    {  // (the round-4 VAR 12 loop, one barrier per K-tile, was pruned in round 6: DESIGN_LOG.md)
     // VAR 11 = VAR 5 with the two wave groups STAGGERED (cdna_hip_programming.md §5 "256² 8-phase template",
     // MI355X_MICROARCH.md "Two waves per SIMD" item 9): every slot is [memory part] barrier [16 MFMAs] barrier and
     // waves 4-7 (quadrant-row 1, one wave on each SIMD) run one barrier behind waves 0-3, so on every SIMD one
@@ -1113,238 +1018,6 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_de
 }
 
 
-// ------------------------------------------------------------------------------------------------------------
-// VAR 20: 4 waves, one per SIMD, each wave a 128x128 C block (8x8 16x16 fragments = 256 fp32 accumulators held in
-// the AGPR half of the register file by inline-asm MFMAs, so they never move), 256x256x64 tiles through a 2-stage
-// LDS ring filled by LDS-DMA.  Per K-tile and wave: 128 MFMAs (2 k-steps x 64) against 32 ds_read_b128 and 16
-// 1-KiB DMA pieces; ONE barrier per K-tile, placed between the k-steps:
-//   phase A: the 64 MFMAs of k-step 0 (fragments F0, read earlier), with k-step 1's fragments F1 read under them
-//   phase B: wait for tile k+1's DMA (the only one in flight), barrier (every wave's reads of tile k are done),
-//            issue tile k+2's DMA into tile k's stage
-//   phase C: the 64 MFMAs of k-step 1 (F1), with tile k+1's k-step-0 fragments F0 read under them
-// so every fragment read overlaps MFMAs and each DMA has a whole tile time to land.  (The 8-wave quadrant-phase
-// kernel runs 4 barriers per K-tile with 2 waves per SIMD; hipBLASLt's fastest kernels on these shapes use this
-// 4-wave 256x256 shape.)
-// ------------------------------------------------------------------------------------------------------------
-constexpr int NT4 = 256;
-constexpr int WM4 = 128, WN4 = 128, FM4 = WM4 / 16, FN4 = WN4 / 16;
-
-VP_DEV void mfma_acc(f32x4& acc, const bf16x8& w, const bf16x8& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(w), "v"(a));
-}
-
-template <int EPI>
-__global__ __launch_bounds__(NT4, 1) void gemm4_kernel(const vp_gemm_desc d) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1;  // 0..1 (M)
-  const int wc = wave & 1;   // 0..1 (N)
-
-  const int tiles_m = (d.M + BM - 1) / BM;
-  const int tiles_n = d.N / BN;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GROUP = 4;
-  const int per_group = GROUP * tiles_n;
-  const int group_id = t / per_group;
-  const int first_m = group_id * GROUP;
-  const int gsz = min(tiles_m - first_m, GROUP);
-  const int tm = first_m + ((t % per_group) % gsz);
-  const int tn = (t % per_group) / gsz;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = d.K / BK;
-
-  // DMA: piece p (0..31) = tile rows 8p..8p+7 of an operand; wave w issues pieces w + 4i (i = 0..7) of A and of W.
-  // Lane l: row 8p + l/8, physical chunk l%8 <- logical chunk (l%8) ^ swz(row); swz depends on row bits 1-3 and the
-  // piece parity is the wave's, so one per-lane offset + a uniform per-piece step serves all 8 pieces.
-  const int prow0 = 8 * wave + (lane >> 3);  // the lane's row in piece i = 0
-  const int pch = ((lane & 7) ^ swz(prow0)) << 4;
-  const bool full_m = m0 + BM <= d.M;
-  const char* abase = (const char*)d.A + (int64_t)m0 * d.lda * 2;
-  const int sgw = n0 / d.n_seg;  // the tile's weight segment (n_seg % 256 == 0: never straddled)
-  const char* wbase = (const char*)d.W[sgw] + (int64_t)(n0 - sgw * d.n_seg) * d.K * 2;
-  const int aoff = prow0 * (int)d.lda * 2 + pch;
-  const int woff = prow0 * d.K * 2 + pch;
-  auto issue = [&](int kt) {
-    char* st = smem + (kt & 1) * STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int r = prow0 + 32 * i;
-      int ao;
-      if (full_m) {
-        ao = aoff + 32 * i * (int)d.lda * 2;
-      } else {
-        ao = (min(m0 + r, d.M - 1) - m0) * (int)d.lda * 2 + pch;
-      }
-      glds16(abase + kt * 128, ao, st + (wave + 4 * i) * 1024);
-      glds16(wbase + kt * 128, woff + 32 * i * d.K * 2, st + TILE_BYTES + (wave + 4 * i) * 1024);
-    }
-  };
-
-  // fragment reads: A rows wr*128 + i*16 + lane%16, W rows wc*128 + j*16 + lane%16, k-step ks: chunk ks*4 + lane/16
-  const int lrow = lane & 15;
-  int lbase[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) lbase[ks] = lrow * 128 + (((ks * 4 + (lane >> 4)) ^ swz(lrow)) << 4);
-  auto read_frags = [&](int kt, int ks, bf16x8 (&a)[FM4], bf16x8 (&w)[FN4]) {
-    const char* st = smem + (kt & 1) * STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < FM4; ++i) a[i] = *(const bf16x8*)(st + (wr * WM4 + i * 16) * 128 + lbase[ks]);
-#pragma unroll
-    for (int j = 0; j < FN4; ++j) w[j] = *(const bf16x8*)(st + TILE_BYTES + (wc * WN4 + j * 16) * 128 + lbase[ks]);
-  };
-
-  f32x4 acc[FN4][FM4];
-#pragma unroll
-  for (int j = 0; j < FN4; ++j)
-#pragma unroll
-    for (int i = 0; i < FM4; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  auto mmas = [&](const bf16x8 (&a)[FM4], const bf16x8 (&w)[FN4]) {
-#pragma unroll
-    for (int j = 0; j < FN4; ++j)
-#pragma unroll
-      for (int i = 0; i < FM4; ++i) mfma_acc(acc[j][i], w[j], a[i]);
-  };
-
-  bf16x8 a0[FM4], w0[FN4], a1[FM4], w1[FN4];
-  issue(0);
-  if (nk > 1) issue(1);
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  read_frags(0, 0, a0, w0);
-  for (int kt = 0; kt < nk; ++kt) {
-    // phase A
-    read_frags(kt, 1, a1, w1);
-    mmas(a0, w0);
-    // phase B
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + 2 < nk) issue(kt + 2);
-    // phase C
-    if (kt + 1 < nk) read_frags(kt + 1, 0, a0, w0);
-    mmas(a1, w1);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  __syncthreads();
-  gemm_epilogue<NT4, FN4, FM4, WN4, WM4, false, EPI>(d, MxExt{}, acc, smem, m0, n0, wr, wc, lane, tid);
-}
-
-// ------------------------------------------------------------------------------------------------------------
-// VAR 30: TWO workgroups per CU.  A 256 x 128 tile per workgroup of 4 waves (2 (M) x 2 (N), 128 x 64 per wave: the
-// same 8 x 4 fragments, registers and epilogue as the 8-wave kernel), K-steps of 32 through a 3-stage LDS ring
-// (24 KiB per stage: 72 KiB per workgroup, two workgroups per CU), one barrier per K-step.  The two waves on a SIMD
-// belong to different workgroups, so one's barrier wait, fragment-read latency, DMA issue or epilogue runs beside the
-// other's MFMAs (the structure that made the p2 attention faster) instead of the whole CU reaching its barriers and
-// its epilogue burst together.
-// LDS image of a stage: A [256][32] then B [128][32] bf16, 64-byte rows, 16-byte chunk p = c ^ h((row >> 2) & 3),
-// h = {0, 2, 3, 1}: the four lane groups of a ds_read_b128 fragment read (16 rows x 4 chunks) hit 16 distinct slots
-// of the 256-byte bank row.  Filled by LDS-DMA (1 KiB = 16 rows per instruction, swizzle on the source address).
-// ------------------------------------------------------------------------------------------------------------
-constexpr int BM2 = 256, BN2 = 128, BK2 = 32, NT2 = 256;
-constexpr int A2_BYTES = BM2 * BK2 * 2;             // 16 KiB
-constexpr int STAGE2 = A2_BYTES + BN2 * BK2 * 2;    // 24 KiB
-constexpr int CTS2 = BN2 * 2 + 8;
-constexpr int LDS2 = (3 * STAGE2 > BM2 * CTS2) ? 3 * STAGE2 : BM2 * CTS2;
-static_assert(BM2 * CTS2 <= 3 * STAGE2, "the epilogue image fits in the ring");
-
-VP_DEV int h2(int row) { return (0x1E >> (((row >> 2) & 3) * 2)) & 3; }  // {0, 2, 3, 1}[(row >> 2) & 3]
-
-template <int EPI>
-__global__ __launch_bounds__(NT2, 2) void gemm2_kernel(const vp_gemm_desc d) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1;  // 0..1 (M)
-  const int wc = wave & 1;   // 0..1 (N)
-
-  const int tiles_m = (d.M + BM2 - 1) / BM2;
-  const int tiles_n = d.N / BN2;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int GROUP = 4;
-  const int per_group = GROUP * tiles_n;
-  const int group_id = t / per_group;
-  const int first_m = group_id * GROUP;
-  const int gsz = min(tiles_m - first_m, GROUP);
-  const int tm = first_m + ((t % per_group) % gsz);
-  const int tn = (t % per_group) / gsz;
-  const int m0 = tm * BM2, n0 = tn * BN2;
-  const int nk = d.K / BK2;
-
-  // DMA: instruction p of a stage covers image rows 16p .. 16p + 15 (A: p = 0..15, B: p = 16..23); wave w issues
-  // p = w + 4i (i = 0..5).  Lane l: row 16p + l / 4, physical chunk l % 4 <- logical chunk (l % 4) ^ h(row); h
-  // depends on row bits 2-3 only, so one per-lane offset per operand serves every piece (+ a scalar row step).
-  const int prow = lane >> 2;  // row within the piece
-  const int pch = ((lane & 3) ^ h2(prow)) * 16;
-  const char* abase = (const char*)d.A + (int64_t)m0 * d.lda * 2;
-  const int sgw = n0 / d.n_seg;  // the tile's weight segment (n_seg % 128 == 0: never straddled)
-  const char* wbase = (const char*)d.W[sgw] + (int64_t)(n0 - sgw * d.n_seg) * d.K * 2;
-  // A offsets of the wave's 4 pieces, rows clamped to the last row (the ragged last row tile re-reads it)
-  int aoff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) aoff[i] = (min(m0 + 16 * (wave + 4 * i) + prow, d.M - 1) - m0) * (int)d.lda * 2 + pch;
-  const int woff = prow * d.K * 2 + pch;
-  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)smem);
-  auto glds = [&](const char* sb, int voff, unsigned la) {
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(la), "v"(voff), "s"(sb)
-                 : "memory", "m0");
-  };
-  auto issue = [&](int kt) {
-    const unsigned st = lds0 + (kt % 3) * STAGE2;
-    const int kb = kt * BK2 * 2;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) glds(abase + kb, aoff[i], st + (wave + 4 * i) * 1024);  // A pieces 0..15
-#pragma unroll
-    for (int i = 0; i < 2; ++i)  // B pieces 16..23
-      glds(wbase + kb, woff + 16 * (wave + 4 * i) * d.K * 2, st + (16 + wave + 4 * i) * 1024);
-  };
-
-  // fragment reads: A rows wr * 128 + 16 i + lane % 16, B rows wc * 64 + 16 j + lane % 16; chunk lane / 16
-  const int lrow = lane & 15;
-  const int lbase = lrow * 64 + (((lane >> 4) ^ h2(lrow)) << 4);
-
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  issue(0);
-  if (nk > 1) issue(1);
-  for (int kt = 0; kt < nk; ++kt) {
-    // step kt's DMA (issued two steps ago) landed for this wave; the barrier publishes it for all waves and tells
-    // that every wave's reads of step kt - 1 returned (lgkmcnt(0)), so its stage takes step kt + 2
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + 2 < nk) issue(kt + 2);
-    const char* st = smem + (kt % 3) * STAGE2;
-    bf16x8 bf[4], af[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf[j] = *(const bf16x8*)(st + A2_BYTES + (wc * 64 + j * 16) * 64 + lbase);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = *(const bf16x8*)(st + (wr * 128 + i * 16) * 64 + lbase);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[j][i], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  epi_values<4, 8, 64, 128, EPI>(
-      d, acc,
-      [&](int j, int i, const bf16x4& o) { *(bf16x4*)epi_lds_addr<64, 128, CTS2>(smem, j, i, 0, wr, wc, lane) = o; },
-      m0, n0, wr, wc, lane);
-  __syncthreads();
-  epi_rows_out<NT2, false, EPI, BN2>(d, MxExt{}, smem, 0, BM2, m0, n0, tid);
-}
-
 // split-K reduce + epilogue: one thread per 8 consecutive output columns of one row; the chunks are summed in a fixed
 // order, then the same roundings as the fused epilogues (epi_values + epi_rows_out)
 VP_DEV void splitk_epilogue(const vp_gemm_desc& d, int m, int n, const float (&a)[8]);
@@ -1496,7 +1169,7 @@ SplitPlan split_plan(const vp_gemm_desc* d) {
 
 extern "C" int vp_gemm_variant_built(int variant) {
   if (variant == 1 || variant == 5 || variant == 11 || variant == 13) return 1;
-  return (variant == 12 || variant == 20 || variant == 30) && VP_GEMM_EXTRA_VARIANTS ? 1 : 0;
+  return 0;  // (the rejected loops 12, 20, 30 were pruned in round 6: DESIGN_LOG.md)
 }
 
 // M-tiles per group of the grouped tile order (the VP_GEMM_GROUP knob overrides, A/B)
@@ -1610,21 +1283,8 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
       (const void*)gemm_bf16_kernel<13, false, 4, VP_EPI_GELU_BWD>,
       (const void*)gemm_bf16_kernel<13, false, 4, EPI_QKNORM_AUX>,
       (const void*)gemm_bf16_kernel<13, false, 4, EPI_GELU_AUX>};
-#if VP_GEMM_EXTRA_VARIANTS
-  static const void* const k12[10] = {
-      (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS>, (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_GELU>,
-      (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_SCALE>, (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_GATED>,
-      (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_ADDROWS>, nullptr,
-      (const void*)gemm_bf16_kernel<12, false, 4, VP_EPI_BIAS_QKNORM_ROPE>,
-      nullptr,
-      nullptr, nullptr};
-#else
-  static const void* const k12[10] = {};
-#endif
   static bool attr_set = false;
   if (!attr_set) {
-    for (const void* f : k12)
-      if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     for (const void* f : k13)
       if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1639,65 +1299,9 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
   int variant = e != nullptr ? atoi(e) : 13;
   if (variant != 1 && variant != 5 && variant != 11 && variant != 12 && variant != 13 && variant != 20 && variant != 30)
     variant = 13;
-  // the rejected A/B loops (12, 20, 30: profiles/r04_gemm_v12_ab_rejected.log, r04_gemm_v30_ab_rejected.log,
-  // DESIGN.md §3) are built only with -DVP_GEMM_EXTRA_VARIANTS=1 (vp_gemm_variant_built)
+  // the rejected A/B loops 12, 20, 30 (profiles/r04_gemm_v12_ab_rejected.log, r04_gemm_v30_ab_rejected.log) were
+  // pruned in round 6: naming one is VP_ERR_UNSUPPORTED
   if (!vp_gemm_variant_built(variant)) return VP_ERR_UNSUPPORTED;
-#if VP_GEMM_EXTRA_VARIANTS
-  // 30: two workgroups per CU, 256 x 128 tiles (whole 128-column tiles of one weight segment, whole 32-K steps,
-  // 32-bit in-tile DMA offsets)
-  if (variant == 30) {
-    const bool ok30 = d->epilogue != VP_EPI_GELU_BWD && d->aux == nullptr && (d->N % BN2) == 0 && (d->n_seg % BN2) == 0 && (d->K % BK2) == 0 &&
-                      (int64_t)BM2 * d->lda * 2 < ((int64_t)1 << 31) && (int64_t)BN2 * d->K * 2 < ((int64_t)1 << 31);
-    if (ok30) {
-      static const void* const k30[8] = {
-          (const void*)gemm2_kernel<VP_EPI_BIAS>, (const void*)gemm2_kernel<VP_EPI_BIAS_GELU>,
-          (const void*)gemm2_kernel<VP_EPI_BIAS_SCALE>, (const void*)gemm2_kernel<VP_EPI_GATED>,
-          (const void*)gemm2_kernel<VP_EPI_BIAS_ADDROWS>, nullptr, (const void*)gemm2_kernel<VP_EPI_BIAS_QKNORM_ROPE>,
-          nullptr};
-      static bool attr30 = false;
-      if (!attr30) {
-        for (const void* f : k30)
-          if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-        attr30 = true;
-      }
-      const int tiles30 = ((d->M + BM2 - 1) / BM2) * (d->N / BN2);
-      void* args[] = {(void*)d};
-      const hipError_t le = hipLaunchKernel(k30[d->epilogue], dim3(tiles30), dim3(NT2), args, LDS2,
-                                            (hipStream_t)stream);
-      if (le != hipSuccess) return (int)le;
-      VP_CHECK_LAUNCH();
-      return VP_OK;
-    }
-    variant = 13;
-  }
-  // 20: the 4-wave AGPR-accumulator kernel (whole 256-column tiles of one weight segment, whole K-tiles, 32-bit
-  // in-tile DMA offsets)
-  if (variant == 20) {
-    const bool ok20 = d->epilogue != VP_EPI_GELU_BWD && d->aux == nullptr && (d->N % BN) == 0 && (d->n_seg % BN) == 0 && (d->K % BK) == 0 && d->K >= 2 * BK &&
-                      (int64_t)BM * d->lda * 2 < ((int64_t)1 << 31) && (int64_t)BN * d->K * 2 < ((int64_t)1 << 31);
-    if (ok20) {
-      static const void* const k20[8] = {
-          (const void*)gemm4_kernel<VP_EPI_BIAS>, (const void*)gemm4_kernel<VP_EPI_BIAS_GELU>,
-          (const void*)gemm4_kernel<VP_EPI_BIAS_SCALE>, (const void*)gemm4_kernel<VP_EPI_GATED>,
-          (const void*)gemm4_kernel<VP_EPI_BIAS_ADDROWS>, nullptr, (const void*)gemm4_kernel<VP_EPI_BIAS_QKNORM_ROPE>,
-          nullptr};
-      static bool attr20 = false;
-      if (!attr20) {
-        for (const void* f : k20)
-          if (f != nullptr) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        attr20 = true;
-      }
-      const int tiles20 = ((d->M + BM - 1) / BM) * (d->N / BN);
-      void* args[] = {(void*)d};
-      const hipError_t le = hipLaunchKernel(k20[d->epilogue], dim3(tiles20), dim3(NT4), args, LDS_BYTES,
-                                            (hipStream_t)stream);
-      if (le != hipSuccess) return (int)le;
-      VP_CHECK_LAUNCH();
-      return VP_OK;
-    }
-    variant = 13;
-  }
-#endif
   // the quadrant pipeline adds 32-bit in-tile source offsets to a 64-bit tile base (A) / segment base (W)
   const bool w32 = (int64_t)d->n_seg * d->K * 2 < ((int64_t)1 << 31);
   const bool tile32 = (int64_t)BM * d->lda * 2 < ((int64_t)1 << 31) && w32;
@@ -1706,10 +1310,10 @@ static int gemm_bf16_launch(const vp_gemm_desc* d, void* stream, int main_tiles)
   const int all_tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
   const int tiles = main_tiles > 0 ? min(main_tiles, all_tiles) : all_tiles;
   const int ki = kernel_index(d);
-  if ((variant == 12 && k12[ki] == nullptr) || (variant == 11 && k11[ki] == nullptr)) return VP_ERR_UNSUPPORTED;
-  if (variant == 12 || variant == 13) {
+  if (variant == 11 && k11[ki] == nullptr) return VP_ERR_UNSUPPORTED;
+  if (variant == 13) {
     void* args[] = {(void*)d, (void*)&mx};
-    const void* const* kt = variant == 12 ? k12 : k13;
+    const void* const* kt = k13;
     const hipError_t le = hipLaunchKernel(kt[ki], dim3(tiles), dim3(NTHREADS), args, LDS_BYTES,
                                           (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
@@ -1880,6 +1484,7 @@ extern "C" int vp_mx_quantize_bf16(const void* x, int64_t ld_in, void* q, int64_
   return VP_OK;
 }
 
+#if VP_DIAG  // diagnostic build only (include/vp_hip_diag.h)
 // ---- layout self-test: one wave, one block-scaled MFMA ----
 __global__ __launch_bounds__(64) void mx_probe_kernel(const uint8_t* A, const uint8_t* B, const uint8_t* sa,
                                                       const uint8_t* sb, float* C) {
@@ -1905,3 +1510,4 @@ extern "C" int vp_mx_mfma_probe(const void* A, const void* B, const void* sa, co
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
+#endif

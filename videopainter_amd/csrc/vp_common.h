@@ -5,6 +5,12 @@
 #include <stdint.h>
 
 #include "../../include/vp_hip.h"
+#ifndef VP_DIAG
+#define VP_DIAG 0  // 1: the diagnostic entry points of include/vp_hip_diag.h (python -m videopainter_amd.build --diag)
+#endif
+#if VP_DIAG
+#include "../../include/vp_hip_diag.h"
+#endif
 
 typedef __bf16 bf16;
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));

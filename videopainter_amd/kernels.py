@@ -420,7 +420,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
 
 def attention_variant_built(name: str) -> bool:
     """Is the attention kernel variant `name` (a value of VP_ATTN_BOUNDED_MODE / VP_ATTN_UNBOUNDED_MODE) in the
-    library?  The rejected A/B variants are built only with VP_ATTN_EXTRA_VARIANTS=1 (host-only query)."""
+    library (host-only query)?  The rejected A/B variants of rounds 1-5 were pruned in round 6."""
     return bool(N.lib().vp_attention_variant_built(name.encode()))
 
 
@@ -452,8 +452,8 @@ class knob:
 
 
 def gemm_variant_built(variant) -> bool:
-    """Is the GEMM main loop VP_GEMM_VARIANT = variant in this library build (the rejected 12 / 20 / 30 need
-    VP_GEMM_EXTRA_VARIANTS=1)?"""
+    """Is the GEMM main loop VP_GEMM_VARIANT = variant in this library build (1, 5, 11, 13; the rejected 12 / 20 / 30
+    were pruned in round 6)?"""
     return bool(N.lib().vp_gemm_variant_built(int(variant)))
 
 
