@@ -308,6 +308,19 @@ def config4_step_flops(window: int) -> float:
     return float(tr + br)
 
 
+def config4_step_flops_executed(window: int, n_masked: int) -> float:
+    """The MFMA FLOP the HIP path executes per config-4 step: the ID-resample attention streams segment 1 (N keys)
+    and only the n_masked masked video rows of segment 2 (the null keys are summed in closed form by
+    vp_null_key_mass: 88 short dot products per query, not counted); everything else as config4_step_flops."""
+    attn = 4 * NTOK * (NTOK + n_masked) * D
+    kv = 4 * NTOK * D * D if window > 0 else 0
+    blk = 24 * NTOK * D * D + attn + kv
+    tr = B * (L * blk + 2 * NV * 128 * D + 2 * T * 4096 * D + 2 * NV * D * 64)
+    br_blk = 24 * NTOK * D * D + 4 * NTOK * NTOK * D
+    br = B * (LB * br_blk + 2 * NV * 132 * D + 2 * T * 4096 * D + LB * 2 * NTOK * D * D)
+    return float(tr + br)
+
+
 def _window_inputs(g, device, first: bool):
     lat = torch.randn(1, F, 16, HL, WL, generator=g)
     vid = torch.randn(1, F, 16, HL, WL, generator=g)
@@ -398,6 +411,11 @@ def run_config4(args, world: int, rank: int, local: int) -> None:
     n_steps = n_clips * n_windows * args.steps
     steps_per_s = n_steps / elapsed
     fl = sum(config4_step_flops(w) for w in range(n_windows)) * args.steps * n_clips
+    # masked video rows of each window's resample mask (the rows segment 2 streams), counted as the transformer does
+    n_masked = [int(K.patch_mask(clips[0][w]["mask"][:1].permute(0, 2, 1, 3, 4).contiguous(), 2).sum())
+                for w in range(n_windows)]
+    fl_exec = sum(config4_step_flops_executed(w, n_masked[w - 1 if w > 0 else 0])
+                  for w in range(n_windows)) * args.steps * n_clips
     attn_ms = tl.mean_ms("attention")
     if rank == 0:
         line = {
@@ -418,6 +436,10 @@ def run_config4(args, world: int, rank: int, local: int) -> None:
             "flop_basis": "the reference's work: attention over all 2N keys (K and its masked copy); the HIP path sums "
                           "the masked copy's null keys in closed form and streams only the masked rows, so it executes "
                           "fewer MFMA FLOPs than counted here",
+            "step_flop_executed_mean": fl_exec / n_steps,
+            "step_mfma_frac_executed": fl_exec / elapsed / world / (PEAK_BF16_TFLOPS * 1e12),
+            "executed_basis": f"the MFMA FLOP the HIP path runs: attention over N + the masked rows of segment 2 "
+                              f"({n_masked[0]} of {NV} video rows per window), null keys in closed form not counted",
             "attention_ms_per_launch": attn_ms, "output_latents": list(out[0].shape),
         }
         print(json.dumps(line), flush=True)
