@@ -21,7 +21,7 @@ def kernels(path):
                             and not l.strip().startswith((".section", ".amdhsa_kernel"))]  # (names only)
                 cur = None
             else:
-                body.append(re.sub(r"\.LBB\d+_", ".LBB_", line))
+                body.append(re.sub(r"\s*;.*$", "", re.sub(r"\.LBB\d+_", ".LBB_", line)))  # (comments: block numbers)
     return out
 
 

@@ -824,6 +824,442 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// P2S ("build the pipelined 16x16x32 form and decide by wall"): p2a's software pipeline — the same
+// jobs (32-key half x 32-query block), the same step order, ring, seam, anchor, rescale, flags and redo — on
+// v_mfma_f32_16x16x32_bf16, the shape the chip holds a higher clock on under load (MI355X_MICROARCH.md 'DVFS
+// give-back' item 7).  A job is 2 query tiles (16 queries) x 2 key tiles (16 keys):
+//   QK^T  S^T[kt][qt] = K[kt] . Q^T[qt]      2 chains of 2 per (qt, kt): 8 MFMAs; lane l: query 16 qt + l % 16,
+//                                             keys 16 kt + 4 (l / 16) + i (the s16 layout, the query on the lane)
+//   PV    O^T[dt][qt] += V^T[dt] . P^T[qt]   8 MFMAs; P^T straight from the lane's own 8 scores (k-slot 8 (l / 16) + j
+//                                             <-> key 4 (l / 16) + j, then 16 + 4 (l / 16) + j - 4), V^T by two
+//                                             ds_read_b64_tr_b16 per 16-dim tile from the vswz16 image
+//   rows  l[qt] += ones . P^T[qt]            2 MFMAs (every accumulator row is the query's sum)
+// = 18 MFMAs of 16 cycles per job: the same 288 matrix cycles as p2a's 10, at twice the instructions; each gap holds
+// one v_exp_f32 and every other one a pack.  Registers as p2a (o 64, S 32, K 32 by half parity, V^T 16, Q^T 32, P
+// 16), the anchor's C operand 4 instead of 16.
+// ------------------------------------------------------------------------------------------------------------
+struct P2SRegs {
+  bf16x8 qf[4][2];     // Q^T B operands [qt][c]: query 16 qt + l % 16, dims 32 c + 8 (l / 16) + j (pre-scaled)
+  f32x4 o[4][4];       // O^T[dt][qt]: dims 16 dt + 4 (l / 16) + i of query 16 qt + l % 16
+  f32x4 s[2][2][2];    // S^T of the job in flight per block qi: [qt' (query tile 2 qi + qt')][kt]
+  u32x4 pf[2][2];      // packed P^T per block [qt']: words = key pairs (4g, 4g+1) (4g+2, 4g+3) (16+4g, ..) (16+4g+2, ..)
+  bf16x8 kf[2][2][2];  // K A operands by half parity [kt][c]: key 16 kt + l % 16, dims 32 c + 8 (l / 16) + j
+  bf16x8 vf[4];        // V^T A operands of the current half [dt]
+  f32x4 lsum[4];       // row sums per query tile (the four entries equal)
+  f32x4 negm;          // C operand of every QK^T chain: -anchor
+  float anc;
+};
+
+// the job's score p (0..15) = query tile qt' = p / 8, key tile kt = (p / 4) % 2, element p % 4: the pairs (2m, 2m + 1)
+// are the P^T words pf[m / 4][m % 4] (p2a's flat order)
+VP_DEV void p2s_read_k(const char* Kl, int kh, int lane, bf16x8 (&kf)[2][2]) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int row = kh * 32 + kt * 16 + (lane & 15);
+    const char* kr = Kl + row * 128;
+    const int sw = swz(row);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) kf[kt][c] = *(const bf16x8*)(kr + (((4 * c + g) ^ sw) << 4));
+  }
+}
+
+VP_DEV void p2s_read_v(const char* Vl, int kh, const int (&vo)[4], bf16x8 (&vf)[4]) {
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const char* base = Vl + kh * 32 * 128 + vo[dt];
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 16 * 128));
+    vf[dt] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+}
+
+VP_DEV void p2s_exp(float& p0, float s0) {
+#if VP_P1_ABL & 2
+  asm volatile("v_mov_b32 %0, %1" : "=&v"(p0) : "v"(s0));
+#else
+  asm volatile("v_exp_f32 %0, %1" : "=&v"(p0) : "v"(s0));
+#endif
+}
+
+// one step (the p1_step roles): QK^T of block QB_ on K buffer KB_ interleaved with the PV of block PB, then the two
+// row-sum MFMAs; gap g holds exp g of block EB's 16 scores and, every other gap, the pack of an earlier pair:
+//   g even: QK op g / 2 = chain (qt' = g / 8, kt = (g / 4) % 2), d-half c = (g / 2) % 2   (c = 0 from C = -anchor)
+//   g odd:  PV op (dt = g / 4, qt' = (g / 2) % 2)
+template <int EB, int QB_, int PB, int KB_>
+VP_DEV void p2s_step(P2SRegs& r, const bf16x8& ones) {
+  float p[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const int n = g >> 1;
+    if ((g & 1) == 0) {
+      const int qt = n >> 2, kt = (n >> 1) & 1, c = n & 1;
+      p1_fence();
+      if (c == 0)  // (asm, early-clobber: -anchor stays in its own registers, never copied into the chain)
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %3"
+                     : "=&v"(r.s[QB_][qt][kt]) : "v"(r.kf[KB_][kt][0]), "v"(r.qf[2 * QB_ + qt][0]), "v"(r.negm));
+      else
+        r.s[QB_][qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(r.kf[KB_][kt][1], r.qf[2 * QB_ + qt][1],
+                                                                    r.s[QB_][qt][kt], 0, 0, 0);
+      p1_fence();
+    } else {
+      const int dt = n >> 1, qt = n & 1;
+      p1_fence();
+      r.o[dt][2 * PB + qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(r.vf[dt], as_bf16x8(r.pf[PB][qt]),
+                                                                      r.o[dt][2 * PB + qt], 0, 0, 0);
+      p1_fence();
+    }
+    p2s_exp(p[g], r.s[EB][g >> 3][(g >> 2) & 1][g & 3]);
+    // the pair exp'd two and three gaps back: two transcendentals sit between, so no wait state before the pack
+    if (g >= 3 && (g & 1) == 1) {
+      const int m = (g - 3) >> 1;
+      r.pf[EB][m >> 2][m & 3] = p1_pack(p[g - 3], p[g - 2]);
+    }
+  }
+  p1_fence();
+  r.lsum[2 * PB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, as_bf16x8(r.pf[PB][0]), r.lsum[2 * PB], 0, 0, 0);
+  p1_fence();
+  r.pf[EB][1][3] = p1_pack(p[14], p[15]);
+  p1_fence();
+  r.lsum[2 * PB + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, as_bf16x8(r.pf[PB][1]), r.lsum[2 * PB + 1], 0,
+                                                                0, 0);
+  p1_fence();
+}
+
+// keys at or past rem = lim - 32 h of a block's scores: -inf (asm, as p1_mask)
+VP_DEV void p2s_mask(f32x4 (&s)[2][2], int rem, int g4) {
+  const float ninf = -INFINITY;
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float x = s[qt][kt][i];
+        int t;
+        asm volatile(
+            "v_add_u32 %1, %3, %4\n\t"
+            "v_cmp_le_i32 vcc, %2, %1\n\t"
+            "v_cndmask_b32 %0, %0, %5, vcc"
+            : "+v"(x), "=&v"(t)
+            : "s"(rem), "v"(g4), "i"(16 * kt + i), "v"(ninf)
+            : "vcc");
+        s[qt][kt][i] = x;
+      }
+}
+
+// one 128-key tile, p1_tile's schedule (the even step reads K(h + 1), then V(h) after its PV; the seam at the end of
+// step (3, 0)), then the anchored rescale check
+VP_DEV void p2s_tile(P2SRegs& r, bf16x8& ones, const char* Kl, const char* Kn, int lim, bool masked, bool last,
+                     int lane, const int (&vo)[4]) {
+  const int g4 = 4 * (lane >> 4);
+  const char* Vl = Kl + KT;
+  // the all-ones row-sum operand is wave-uniform: opaque here, so the compiler keeps it in VGPRs instead of
+  // re-materialising it from SGPRs before every row-sum MFMA (2 v_mov_b64 + s_nop per step)
+  asm volatile("" : "+v"(ones));
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    if (h < 3) p2s_read_k(Kl, h + 1, lane, r.kf[(h + 1) & 1]);
+    if (masked) p2s_mask(r.s[0], lim - 32 * h, g4);
+    if (h & 1)
+      p2s_step<0, 1, 1, 1>(r, ones);
+    else
+      p2s_step<0, 1, 1, 0>(r, ones);
+    p2s_read_v(Vl, h, vo, r.vf);
+    if (h == 3 && !last) {  // the seam (2-slot ring: the next tile is the only DMA in flight)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      p2s_read_k(Kn, 0, lane, r.kf[0]);
+    }
+    if (masked) p2s_mask(r.s[1], lim - 32 * h, g4);
+    if (h & 1)
+      p2s_step<1, 0, 0, 0>(r, ones);
+    else
+      p2s_step<1, 0, 0, 1>(r, ones);
+  }
+  // anchored rescale (p1_tile): a wave whose partial row sums passed 2^62 scales O, l and the packed P of job (3, 1)
+  // by 2^-64, moves the next tile's job (0, 0) scores by -64 and its anchor up by 64
+  float big = 0.f;
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) big = fmaxf(big, r.lsum[qt][0]);
+  if (__ballot(!(big <= 0x1p62f)) != 0ull) {
+    const float f = 0x1p-64f;
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      r.lsum[qt] *= f;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) r.o[dt][qt] *= f;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t w = r.pf[1][j][e];
+        const float lo = __uint_as_float(w << 16) * f, hi = __uint_as_float(w & 0xffff0000u) * f;
+        r.pf[1][j][e] = (uint32_t)__builtin_bit_cast(uint16_t, f2bf(lo)) |
+                        ((uint32_t)__builtin_bit_cast(uint16_t, f2bf(hi)) << 16);
+      }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) r.s[0][qt][kt] -= 64.f;
+    r.anc += 64.f;
+    r.negm = (f32x4){-r.anc, -r.anc, -r.anc, -r.anc};
+  }
+}
+
+VP_DEV int vswz16(int row) { return ((row >> 1) & 3) << 1; }
+
+template <bool TAIL = false>
+__global__ __launch_bounds__(NW4 * 64, 2) void attn_fwd_p2s(const vp_attn_desc d, const AttnSplit sp) {
+  constexpr int QBV = NW4 * 64;
+  constexpr int PPWV = NP / NW4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int c16 = lane & 15;
+
+  const int nqb = (d.Nq + QBV - 1) / QBV;
+  const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
+  const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = t / nqb;
+  const int qb = t - bh * nqb;
+  const int b = bh / d.H;
+  const int h = bh - b * d.H;
+  const int tiles1 = (d.Nk + KB - 1) / KB;
+  const int n2 = d.k2_len != nullptr ? max(0, min(__builtin_amdgcn_readfirstlane(d.k2_len[b]), d.Nk2)) : d.Nk2;
+  const int tiles2 = n2 > 0 ? (n2 + KB - 1) / KB : 0;
+  const int ntiles_all = tiles1 + tiles2;
+  const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
+  const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
+  const int qw0 = qb * QBV + wave * 64;
+
+  P2SRegs r;
+  {
+    const float cq = d.scale * 1.4426950408889634f;
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      const int q = qw0 + qt * 16 + c16;
+      const int qc = q < d.Nq ? q : d.Nq - 1;
+      const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        r.qf[qt][c] = *(const bf16x8*)(qrow + c * 32 + g * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r.qf[qt][c][j] = f2bf(bf2f(r.qf[qt][c][j]) * cq);
+      }
+    }
+  }
+  auto slot_of = [&](int ti) { return smem + (ti & 1) * ST; };
+  // DMA as attn_fwd_p1 (2-slot ring), the V image in the vswz16 swizzle of the 16x16x32 transposed reads
+  int voff_k[PPWV], voff_v[PPWV];
+#pragma unroll
+  for (int i = 0; i < PPWV; ++i) {
+    const int prow = (wave + i * NW4) * 8 + (lane >> 3);
+    voff_k[i] = (prow * (int)d.k_sn + (((lane & 7) ^ swz(prow)) * 8)) * 2;
+    voff_v[i] = (prow * (int)d.v_sn + (((lane & 7) ^ vswz16(prow)) * 8)) * 2;
+  }
+  const char* kseg1 = (const char*)((const bf16*)d.K + (int64_t)b * d.k_sb + h * 64);
+  const char* vseg1 = (const char*)((const bf16*)d.V + (int64_t)b * d.v_sb + h * 64);
+  const int full1 = d.Nk / KB;
+  const bool seg2fast = d.K2 != nullptr && d.k2_sn == d.k_sn && d.v2_sn == d.v_sn;
+  const int full2 = seg2fast ? n2 / KB : 0;
+  const char* kseg2 = seg2fast ? (const char*)((const bf16*)d.K2 + (int64_t)b * d.k2_sb + h * 64) : nullptr;
+  const char* vseg2 = seg2fast ? (const char*)((const bf16*)d.V2 + (int64_t)b * d.v2_sb + h * 64) : nullptr;
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem) + wave * 1024;
+  auto issue = [&](int ti) {
+    const bool s1 = ti < full1;
+    if (s1 || (ti >= tiles1 && ti - tiles1 < full2)) {
+      const unsigned la = lds0 + (ti & 1) * ST;
+      const int tt = s1 ? ti : ti - tiles1;
+      const char* kb = (s1 ? kseg1 : kseg2) + (int64_t)tt * KB * d.k_sn * 2;
+      const char* vb = (s1 ? vseg1 : vseg2) + (int64_t)tt * KB * d.v_sn * 2;
+#pragma unroll
+      for (int i = 0; i < PPWV; ++i) {
+        glds16_lds(kb, voff_k[i], la + i * NW4 * 1024);
+        glds16_lds(vb, voff_v[i], la + KT + i * NW4 * 1024);
+      }
+      return;
+    }
+    const int ln = lane_id_opaque();
+    const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
+    char* slot = slot_of(ti);
+    const int last = sg.n - 1 - sg.key0;
+    const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
+    const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
+    const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
+#pragma unroll
+    for (int i = 0; i < PPWV; ++i) {
+      const int pc = wave + i * NW4;
+      const int prow = pc * 8 + (ln >> 3);
+      const int rr = min(prow, last);
+      glds16(kb, (rr * ksn + (((ln & 7) ^ swz(prow)) * 8)) * 2, slot + pc * 1024);
+      glds16(vb, (rr * vsn + (((ln & 7) ^ vswz16(prow)) * 8)) * 2, slot + KT + pc * 1024);
+    }
+  };
+  // transposed V^T reads (the s16 kernel's): lane 4 tq + tp of its 16-lane group addresses key row 4 g + tq (second
+  // read: + 16), columns 16 dt + 4 tp .. + 3
+  int vo[4];
+  {
+    const int vrow = 4 * g + ((lane & 15) >> 2);
+    const int tp = lane & 3;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) vo[dt] = vrow * 128 + (((2 * dt + (tp >> 1)) ^ vswz16(vrow)) << 4) + (tp & 1) * 8;
+  }
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    r.lsum[qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) r.o[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) r.pf[qi][j] = (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) r.vf[dt] = (bf16x8){};  // job -1: 0 x 0
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = f2bf(1.f);
+
+  const bool any = tbeg < tend;  // workgroup-uniform
+  if (any) issue(tbeg);
+  if (tbeg + 1 < tend) {
+    issue(tbeg + 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPWV) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (any) p2s_read_k(slot_of(tbeg), 0, lane, r.kf[0]);
+  {
+    // job (0, 0) and, for the anchor, job (0, 1) from C = 0; the anchor = ceil(max over the wave's 64 queries x the
+    // first 32 keys), as p2a's; job (0, 1) is recomputed by the first step with C = -anchor
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          r.s[qi][qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(r.kf[0][kt][0], r.qf[2 * qi + qt][0], z, 0, 0, 0);
+          r.s[qi][qt][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(r.kf[0][kt][1], r.qf[2 * qi + qt][1],
+                                                                     r.s[qi][qt][kt], 0, 0, 0);
+        }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) mx = fmaxf(mx, r.s[qi][qt][kt][i]);
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) mx = fmaxf(mx, __shfl_xor(mx, sh, 64));
+    mx = __builtin_ceilf(mx);
+    r.anc = any ? __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(mx))) : -INFINITY;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) r.s[0][qt][kt] -= r.anc;
+    r.negm = (f32x4){-r.anc, -r.anc, -r.anc, -r.anc};
+  }
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // S -> the first (asm) exp
+  ClockStamp ck;
+  ck.start();
+  for (int ti = tbeg; ti < tend; ++ti) {
+    if (ti + 1 < tend && (!(VP_P1_ABL & 1) || ti == tbeg)) issue(ti + 1);
+    int lim = KB;
+    if (ti >= full1) {
+      const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
+      lim = sg.n - sg.key0;
+    }
+    p2s_tile(r, ones, slot_of(ti), slot_of(ti + 1), __builtin_amdgcn_readfirstlane(lim), lim < KB, ti + 1 >= tend,
+             lane, vo);
+  }
+  // drain: PV + row sums of the last job (3, 1)
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+      r.o[dt][2 + qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(r.vf[dt], as_bf16x8(r.pf[1][qt]), r.o[dt][2 + qt], 0,
+                                                                 0, 0);
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+    r.lsum[2 + qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, as_bf16x8(r.pf[1][qt]), r.lsum[2 + qt], 0, 0, 0);
+  ck.stop(tid);
+
+  float l_tot[4];
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    l_tot[qt] = r.lsum[qt][0];
+    const int q = qw0 + qt * 16 + c16;
+    if (!TAIL && d.l_extra != nullptr)
+      l_tot[qt] += __builtin_amdgcn_exp2f(d.l_extra[((int64_t)b * d.H + h) * d.Nq + min(q, d.Nq - 1)] - r.anc);
+  }
+  {
+    // p2a's flags: a non-finite row sum or output, or a row sum under 2^-96, anywhere in the workgroup -> store
+    // nothing, flag the block for the a16 redo
+    bool bad = false;
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      bad |= nonfinite(l_tot[qt]) || (any && !(l_tot[qt] >= 0x1p-96f));
+      const float inv = 1.f / l_tot[qt];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bad |= nonfinite(sp.nsplit == 1 ? r.o[dt][qt][i] * inv : r.o[dt][qt][i]);
+    }
+    int* wflag = (int*)(smem + 2 * ST);
+    const int mine = __ballot(bad) != 0ull;
+    if (lane == 0) wflag[wave] = mine;
+    __syncthreads();
+    int redo = 0;
+#pragma unroll
+    for (int w = 0; w < NW4; ++w) redo |= wflag[w];
+    if (tid == 0 && sp.flags != nullptr)
+      sp.flags[sp.nsplit > 1 ? sp.flag_main + (t - sp.t_base) * sp.nsplit + split : t] = redo;
+    if (redo) return;
+  }
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    const int q = qw0 + qt * 16 + c16;
+    if (sp.nsplit > 1) {
+      float* rec = sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QBV + wave * 64 + qt * 16 + c16) * 66;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) *(f32x4*)(rec + dt * 16 + 4 * g) = r.o[dt][qt];
+      if (g == 0) {
+        rec[64] = r.anc;
+        rec[65] = l_tot[qt];
+      }
+      continue;
+    }
+    if (q >= d.Nq) continue;
+    const float inv = 1.f / l_tot[qt];
+    if (d.lse != nullptr && g == 0) d.lse[((int64_t)b * d.H + h) * d.Nq + q] = r.anc + __log2f(l_tot[qt]);
+    bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64 + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x4 ov;
+      bf16x4 old;
+      if (d.accumulate) old = *(const bf16x4*)(orow + dt * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = rbf(r.o[dt][qt][i] * inv);
+        if (d.out_scale != 1.f) v = rbf(v * d.out_scale);
+        if (d.accumulate) v = bf2f(old[i]) + v;
+        ov[i] = f2bf(v);
+      }
+      *(bf16x4*)(orow + dt * 16) = ov;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // S16: the W64 structure (4-wave workgroups of 256 queries, 64 queries per wave, 128-key tiles through the same
 // 2-slot LDS-DMA ring) on the 16x16x32 bf16 MFMA instead of 32x32x16.  Same FLOPs, same LDS bytes and the same VALU
 // per score; the chip holds a higher clock on the 16x16x32 shape under load (MI355X_MICROARCH.md 'DVFS give-back'
@@ -839,7 +1275,6 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
 // V image swizzle vswz16 (row r: chunk ^ 2 ((r >> 1) & 3)): the 32 lanes of a transposed read take keys r0 .. r0 + 7
 // of one 16-column block, conflict-free only if rows 4 apart land in different chunk pairs.
 // ------------------------------------------------------------------------------------------------------------
-VP_DEV int vswz16(int row) { return ((row >> 1) & 3) << 1; }
 
 
 VP_DEV float xmax16(float x) {  // max over the 4 lanes c16 + 16 g (one query's lanes)
@@ -1867,7 +2302,7 @@ struct AttnVar {
   int lds;  // dynamic LDS bytes
   int qb = QB;  // queries per workgroup
 };
-enum { V_S16, V_A16, V_P2, V_P2A, V_P2W, V_P2W2, V_NVAR };
+enum { V_S16, V_A16, V_P2, V_P2A, V_P2W, V_P2W2, V_P2S, V_NVAR };
 static const AttnVar attn_vars[] = {
     {"s16", (const void*)attn_fwd_s16<false>, (const void*)attn_fwd_s16<true>, NW4 * 64, LDS_BYTES},
     {"a16", (const void*)attn_fwd_s16<false, true>, (const void*)attn_fwd_s16<true, true>, NW4 * 64, LDS_BYTES},
@@ -1879,10 +2314,12 @@ static const AttnVar attn_vars[] = {
     // p2w with one barrier per two tiles
     {"p2w2", (const void*)attn_fwd_p1<false, true, 8, 2>, (const void*)attn_fwd_p1<true, true, 8, 2>, 8 * 64,
      4 * ST + 32, 512},
+    // p2a's pipeline on the 16x16x32 MFMA (anchored)
+    {"p2s", (const void*)attn_fwd_p2s<false>, (const void*)attn_fwd_p2s<true>, NW4 * 64, 2 * ST + 16},
 };
 static_assert(sizeof(attn_vars) / sizeof(attn_vars[0]) == V_NVAR, "variant table");
 // the anchored p2 family (a flag per block, the a16 redo)
-static bool anchored_var(int v) { return v == V_P2A || v == V_P2W || v == V_P2W2; }
+static bool anchored_var(int v) { return v == V_P2A || v == V_P2W || v == V_P2W2 || v == V_P2S; }
 
 struct AttnPlan {
   const AttnVar* v;
