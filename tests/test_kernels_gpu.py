@@ -921,7 +921,7 @@ def _null_mass_ref(q, H, T, cos, sin, beta, m, scale):
 
 
 def test_null_key_mass_matches_explicit_null_keys():
-    """The resample processor's null keys in closed form (resample.hip) against the explicit sum over
+    """The resample processor's null keys in closed form (resample.hip, DESIGN_LOG.md §3.0) against the explicit sum over
     every mask-0 row in fp64: text rows all / partly null, a video row with 8 runs (the per-column fallback), an
     all-null and a no-null row, a batch row without any null key (-inf)."""
     from videopainter_amd import kernels as K

@@ -366,7 +366,7 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
         rotated) whose values are zero — they only add to the row sums.  The order of keys does not change
         attention.  With the video grid known and the RoPE table separable, the null keys leave the segment (k2_len
         = the masked-row count) and their row mass is summed in closed form over the grid (null_key_mass ->
-        l_extra; axes = the per-axis RoPE tables); otherwise they stay as row-sum-only keys
+        l_extra, DESIGN_LOG.md §3.0; axes = the per-axis RoPE tables); otherwise they stay as row-sum-only keys
         (k2_full).  VP_RESAMPLE_NULLMASS=0: keep them as keys; VP_RESAMPLE_PARTITION=0: original order (A/B)."""
         dst = cnt = segments = axes = None
         grid = getattr(rope, "grid", None)
@@ -388,7 +388,7 @@ class CogVideoXAttnProcessor2_0_resample(CogVideoXAttnProcessor2_0):
         dst, cnt, segments, axes = plan
         grid = getattr(rope, "grid", None)
         # segment 2 with the row stride of the fused QKV output (3 D): the attention kernel then streams its full tiles
-        # on the same precomputed lane offsets as segment 1
+        # on the same precomputed lane offsets as segment 1 (DESIGN_LOG.md §3.R4)
         # (VP_RESAMPLE_K2_STRIDED=0: contiguous k2 / v2, the general per-lane DMA path; A/B)
         if _sw("VP_RESAMPLE_K2_STRIDED", "1") != "0":
             kv2 = torch.empty(B, Ntok, 3 * D, device=q.device, dtype=BF16)

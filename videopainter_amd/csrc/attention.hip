@@ -13,7 +13,7 @@
 // 128-key K/V tiles stream into a 2-slot LDS ring by LDS-DMA (global_load_lds_dwordx4) and are consumed as 32-key
 // halves (16 score + 8 packed-P registers live: 128 VGPRs, 4 waves per SIMD = two 8-wave workgroups per CU).
 // Roofline: MFMA-bound in principle (4·N²·64 flop per (b,h)); at d = 64 every score costs one v_exp_f32, a bf16 pack
-// and a row-sum add against 256 MFMA flops, so the softmax VALU issue is the co-bottleneck.
+// and a row-sum add against 256 MFMA flops, so the softmax VALU issue is the co-bottleneck (DESIGN_LOG.md §3).
 //
 // Softmax modes (template MODE):
 //   LAZY   (default for unbounded scores): C-init QK^T (the running max enters the first MFMA as C = -m, so S - m
@@ -557,7 +557,7 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
 // NWV = 8 (p2w): the same per-wave pipeline in 8-wave workgroups of 512 queries, one per CU, on a 4-slot
 // ring (tile t + 2 issued at the top of tile t): a K / V tile loaded once serves twice the queries, so each wave
 // issues half the LDS-DMA instructions per tile (4 instead of 8) — the DMA issue is ~7 % of p2a's time
-// (tools/attn_clock.py ablation) — and the L2 -> LDS bytes per FLOP halve.
+// (tools/attn_clock.py ablation, DESIGN_LOG.md §3.R5) — and the L2 -> LDS bytes per FLOP halve.
 // TPB = 2 (p2w only): one barrier per two tiles — tiles t + 2 and t + 3 issued together at the top of every even tile
 // of the range, both waited for and published by the barrier at the seam of the odd tile before them.
 template <bool TAIL = false, bool ANCH = false, int NWV = 4, int TPB = 1>

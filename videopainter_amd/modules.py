@@ -107,7 +107,7 @@ class ModelMixin(nn.Module):
         return next(self.parameters()).device
 
     # -- training toggles (modeling_utils.py:160).  The block backward always recomputes from the block input
-    # (autograd._BlockFn), i.e. it is checkpointed whether or not the flag is set --
+    # (autograd._BlockFn, DESIGN_LOG.md §3.5), i.e. it is checkpointed whether or not the flag is set --
     def enable_gradient_checkpointing(self):
         self.gradient_checkpointing = True
 
