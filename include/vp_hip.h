@@ -30,7 +30,7 @@ extern "C" {
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
-/* A/B switches of the library (kernel-variant selection only, never numerics of the default path):
+/* A/B switches of the library (kernel-variant selection only, never numerics of the default path; DESIGN_LOG.md §5):
  * VP_GEMM_VARIANT, VP_GEMM_NO_TAIL, VP_GEMM_GROUP, VP_GEMM8_VARIANT, VP_ATTN_BOUNDED_MODE, VP_ATTN_UNBOUNDED_MODE,
  * VP_ATTN_NO_SPLIT, VP_ATTN8_VARIANT, VP_T5_ATTN, VP_CONV_HOIST, VP_CONV_PIPE,
  * VP_ATTN_BWD_VARIANT.  Each is read from the environment
@@ -256,7 +256,7 @@ int vp_attention_variant_built(const char* name);
  * also includes scale * log2 e, so base.scale is ignored).  base.V: V^T e4m3 [B, H, 64, npad] and vs: its scales,
  * both from vp_v_pack_fp8.  base.O / out_scale / accumulate as in the bf16 kernel.  The probabilities P enter the
  * PV product (and the row sums) as e4m3 codes of p * 2^7 made by linear mantissa interpolation of exp2 (relative
- * error 3.2 % rms; env VP_ATTN8_VARIANT=1: exp2 + round-to-nearest e4m3, 2.7 %) — DESIGN.md §3.1. */
+ * error 3.2 % rms; env VP_ATTN8_VARIANT=1: exp2 + round-to-nearest e4m3, 2.7 %) — DESIGN_LOG.md §3.1. */
 typedef struct vp_attn_fp8_desc {
   vp_attn_desc base;
   const void* vs;
@@ -327,7 +327,7 @@ int vp_partition_rows_index(const uint8_t* mask, int64_t mask_bstride, int32_t B
 /* The resample processor's null keys in closed form (attention_processor.py:2244-2290 with mask 0: key LN(0) = the
  * norm_k bias beta, rotated by the position's RoPE on video rows; value 0).  With CogVideoX's separable 3D RoPE
  * (dims 0-15 by frame, 16-39 by row, 40-63 by column) a null key's score is S_t(t) + S_y(y) + S_x(x), so the
- * per-query sum of exp2(score) over all null keys factorises over the grid.
+ * per-query sum of exp2(score) over all null keys factorises over the grid (DESIGN_LOG.md §3.0).
  * vp_mask_null_segments: the null pattern of the token mask [B, T + F*Hh*Ww] (text rows first), once per mask:
  *   segs (16-byte records, capacity B*F*Hh): per (b, t) the runs of equal consecutive rows that hold null keys —
  *   byte 0 = first row, 1 = end row, 2 = run count (<= 6, or 255: the row is scanned instead), bytes 4+2k / 5+2k =
