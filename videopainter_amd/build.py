@@ -30,7 +30,11 @@ ARCH = "gfx950"
 # v_accvgpr_read for the softmax (the other attention kernels compile to identical code with or without it).
 PER_FILE_FLAGS = {"attention.hip": ["-fno-honor-nans", "-Wno-inline-asm", "-fno-slp-vectorize", "-mllvm",
                                     "-amdgpu-mfma-vgpr-form"],
-                  "gemm.hip": ["-Wno-inline-asm"]}
+                  "gemm.hip": ["-Wno-inline-asm"],
+                  # attention backward: without SLP the dS products stay single v_mul_f32 (the pairing into
+                  # v_pk_mul_f32 cost a v_mov per operand pair beside the MFMAs): 12.50 -> 12.01 ms per training-shape
+                  # call, bit-identical arithmetic (profiles/r06_attn_bwd_noslp_ab.log)
+                  "attention_bwd.hip": ["-fno-slp-vectorize"]}
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-result",
           "-Wno-unused-function", "-munsafe-fp-atomics"]
 

@@ -322,6 +322,8 @@ __global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_a
 // dependent instruction until they are stored to LDS after the compute (V = 0 negated them at once, which put an
 // s_waitcnt vmcnt(0) — a wait for the whole next-tile DMA just issued — at the top of every tile); inactive waves
 // skip the compute as one block.
+// (round 6, measured and dropped: 2 waves per SIMD, +4-7 %; the four A fragments of a chain read before its first
+// MFMA and kept live together, +14 % — the extra registers spill at 3 waves per SIMD; profiles/r06_attn_bwd_variants_ab.log)
 template <int V>
 __global__ __launch_bounds__(BW * 64, V ? 3 : 2) void bwd_dkdv_kernel(const vp_attn_bwd_desc d) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
