@@ -25,6 +25,22 @@ def test_library_loads_and_exports_everything():
     assert L.vp_abi_version() == N.ABI_VERSION
 
 
+def test_default_library_exports_no_diagnostic_symbols():
+    """include/vp_hip_diag.h's entry points (MFMA layout probes) exist only in the --diag build: the default library
+    exports exactly the header's functions, and the diagnostic header declares exactly the diagnostic bindings."""
+    import subprocess
+    L = N.lib()
+    if os.environ.get("VP_HIP_LIB"):
+        return  # (an A/B or diagnostic library was selected explicitly)
+    for name in N.DIAG_SIGS:
+        assert not hasattr(L, name), name
+    src = open(os.path.join(ROOT, "include", "vp_hip_diag.h")).read()
+    assert sorted(re.findall(r"^int\s+(vp_\w+)\(", src, flags=re.M)) == sorted(N.DIAG_SIGS)
+    out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True).stdout
+    exported = sorted(set(re.findall(r" T (vp_\w+)$", out, flags=re.M)))
+    assert exported == header_functions()
+
+
 def test_descriptor_argument_errors_are_reported_without_a_gpu():
     import ctypes as C
     L = N.lib()
