@@ -29,7 +29,7 @@ def gemm_variant(request, knobs):
     return request.param
 
 
-UNBOUNDED_VARIANTS = ("p2a", "p2w", "p2w2", "p2s", "p4", "a16")
+UNBOUNDED_VARIANTS = ("p2a", "p2w", "p2w2", "p2s", "a16")
 
 
 def need_variant(name, knobs=None):
@@ -44,7 +44,7 @@ def need_variant(name, knobs=None):
         knobs.setenv("VP_ATTN_UNBOUNDED_MODE" if name in UNBOUNDED_VARIANTS else "VP_ATTN_BOUNDED_MODE", name)
 
 
-@pytest.fixture(params=["p2a", "p2w", "p2w2", "p2s", "p4", "a16", "p2", "s16"],
+@pytest.fixture(params=["p2a", "p2w", "p2w2", "p2s", "a16", "p2", "s16"],
                 ids=lambda v: f"attn_{v}")
 def attn_variant(request, knobs):
     """Unbounded-score launches (no VP_ATTN_BOUNDED_SCORES): p2a (the library default: the p2 pipeline with an
@@ -326,7 +326,7 @@ def _ref64(q, k, v, H, scale=0.125):
     return (torch.softmax(s, -1) @ hd(v)).transpose(1, 2).reshape(B, Nq, H * 64)
 
 
-@pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "p4", "a16"])
+@pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "a16"])
 @pytest.mark.parametrize("gamma", [1.0, 6.0])
 def test_attention_large_gamma_scores(gamma, mode, knobs):
     """qk-LayerNorm outputs with |gamma| up to 6 (scores over hundreds of log2 units, far outside the bounded-score
@@ -349,7 +349,7 @@ def test_attention_large_gamma_scores(gamma, mode, knobs):
     assert torch.isfinite(out.float()).all() and r < 1e-2
 
 
-@pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "p4", "a16"])
+@pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "a16"])
 @pytest.mark.parametrize("jump", [40.0, 90.0, 200.0])
 def test_attention_anchored_late_jump(jump, mode, knobs):
     """The anchored kernels' guarded paths: a late key whose score exceeds every earlier one by `jump` log2 units for
@@ -376,7 +376,7 @@ def test_attention_anchored_late_jump(jump, mode, knobs):
     assert torch.isfinite(out.float()).all() and r < 1e-2
 
 
-@pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "p4", "a16"])
+@pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "a16"])
 def test_attention_stepwise_max_growth(mode, knobs):
     """Running max grows by 0 / 0.5 / 3 / 8 nats at tile seams, so the deferred-max test (tile sum > 2^8) takes both
     branches many times within one query block (cdna_hip_programming.md §5.4 rule 26); for the anchored kernel the
@@ -876,7 +876,7 @@ def test_partition_rows_index_and_permuted_writes(B, N):
         assert not vgot[b, int(cnt[b]):].any()  # the null keys' values are zero (the k2_full contract)
 
 
-@pytest.mark.parametrize("mode", ["s16", "a16", "p2a", "p2w", "p2w2", "p2s", "p4", "p2"])
+@pytest.mark.parametrize("mode", ["s16", "a16", "p2a", "p2w", "p2w2", "p2s", "p2"])
 def test_attention_k2_full_hint(mode, knobs):
     """The k2_full hint (segment-2 keys past k2_full[b] have zero values: row sums only) gives the attention of the
     same segments without the hint; per-batch split points, one straddling a tile, one past every tile."""
@@ -897,7 +897,7 @@ def test_attention_k2_full_hint(mode, knobs):
     hd = lambda x: x.float().cpu().reshape(B, -1, H, 64).transpose(1, 2)  # noqa: E731
     ref = _sdpa(hd(q), torch.cat([hd(k), hd(k2)], 2), torch.cat([hd(v), hd(v2)], 2)).transpose(1, 2).reshape(B, Nn, D)
     # (p2a does not take the hint: the hinted launch runs a16, whose bf16 P is rounded against other anchors)
-    assert rel(o, ref) < 1e-2 and rel(o, o_ref) < (5e-3 if mode in ("p2a", "p2w", "p2w2", "p2s", "p4") else 2e-3)
+    assert rel(o, ref) < 1e-2 and rel(o, o_ref) < (5e-3 if mode in ("p2a", "p2w", "p2w2", "p2s") else 2e-3)
 
 
 def _grid_rope(F_, Hh, Ww):
@@ -984,7 +984,7 @@ def test_null_key_mass_matches_explicit_null_keys():
 
 
 @pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
-@pytest.mark.parametrize("mode", ["s16", "a16", "p2a", "p2w", "p2w2", "p2s", "p4", "p2"])
+@pytest.mark.parametrize("mode", ["s16", "a16", "p2a", "p2w", "p2w2", "p2s", "p2"])
 def test_attention_k2_len_and_l_extra(mode, split, knobs):
     """k2_len (only the first k2_len[b] keys of segment 2) and l_extra (extra row-sum mass per query, log2 score
     units) against fp64 attention over the truncated segments with 2^l_extra added to each denominator.  At this size
@@ -1025,7 +1025,7 @@ def test_attention_k2_len_and_l_extra(mode, split, knobs):
 
 
 @pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
-@pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "p4", "p2"])
+@pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "p2"])
 def test_attention_segment2_fast_path_bit_identical(mode, split, knobs):
     """Segment 2 with segment 1's row strides (the resample processor's layout: K2 / V2 as slices of a [B, N, 3D]
     buffer) streams its full 128-key tiles on segment 1's precomputed lane offsets; the same keys as contiguous
@@ -1057,7 +1057,7 @@ def test_attention_segment2_fast_path_bit_identical(mode, split, knobs):
 
 @pytest.mark.parametrize("split", [True, False], ids=["tailsplit", "nosplit"])
 @pytest.mark.parametrize("spread", [False, True], ids=["even", "spread"])
-@pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "p4", "a16", "p2", "s16"])
+@pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "a16", "p2", "s16"])
 def test_attention_lse_matches_reference(mode, spread, split, knobs):
     """The softmax statistics the backward reads (lse = log2 sum_k 2^(scale log2e q.k), fp32 [B, H, Nq]) and the
     output against fp64, per variant.  spread: queries of very different norms in one wave (x0.02 .. x2.5), so an

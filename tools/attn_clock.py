@@ -56,7 +56,7 @@ def main():
     res = {}
     for var in args.variants.split(","):
         nblk = B * H * ((Ntok + 511) // 512 if var.startswith("p2w") else (Ntok + 255) // 256)
-        unb = var in ("a16", "p2a", "p2w", "p2w2", "p2s", "p4")
+        unb = var in ("a16", "p2a", "p2w", "p2w2", "p2s")
         K.set_knob("VP_ATTN_BOUNDED_MODE", None)
         K.set_knob("VP_ATTN_UNBOUNDED_MODE", None)
         K.set_knob("VP_ATTN_UNBOUNDED_MODE" if unb else "VP_ATTN_BOUNDED_MODE", var)

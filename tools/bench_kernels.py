@@ -103,7 +103,7 @@ def main():
     for rnd in range(2):  # interleaved A/B rounds in one process (cdna_hip_programming.md §5.4 rule 24)
         for var in variants:
             # unbounded-score kernels (p2a = the default without a proven bound, a16, p2w, p2w2) vs bounded ones
-            unb = var in ("a16", "p2a", "p2w", "p2w2", "p2s", "p4")
+            unb = var in ("a16", "p2a", "p2w", "p2w2", "p2s")
             K.set_knob("VP_ATTN_BOUNDED_MODE", None)
             K.set_knob("VP_ATTN_UNBOUNDED_MODE", None)
             if var != "bounded":

@@ -11,6 +11,6 @@ done
 grep '^r' $O/clock_ab.log
 for i in 1 2; do
   timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_p2a_$i.log 2>&1 || exit 3
-  VP_ATTN_UNBOUNDED_MODE=p2s timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_p2s_$i.log 2>&1 || exit 4
+  VP_ATTN_UNBOUNDED_MODE=p2s VP_ATTN_BOUNDED_MODE=p2s timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_p2s_$i.log 2>&1 || exit 4
 done
 for f in $O/bench_*.log; do echo $f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"attention": {[^}]*' $f | head -c 200); done

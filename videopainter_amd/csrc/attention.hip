@@ -824,423 +824,6 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// P4: p2a's pipeline with FOUR 32-query blocks per wave at one wave per SIMD (one 4-wave workgroup of 512 queries per
-// CU, a 4-slot LDS-DMA ring, tile t + 2 issued at the top of tile t).  Round 6 found both hot loops power-bound (p2s:
-// cycles saved return as clock); the energy levers left are LDS read bytes and L2 -> LDS bytes per
-// FLOP (cdna_hip_programming.md §5.4 rule 28), and both halve here: every K / V^T fragment read and every DMA piece
-// serves 128 queries instead of 64.  The jobs of a half run in block order 0..3; step (h, b) exps job (h, b) while the
-// matrix pipe runs the QK^T of the next job and the PV of the previous one (p1_step's gap pattern), so each wave
-// still offers MFMA and VALU work in every gap without a partner wave.  S and packed P are double-buffered by job
-// parity, O (4 blocks x 64 dims x 32 queries = 128 registers) lives in the AGPR half of the register file (every PV
-// MFMA is inline asm with an "a" accumulator, so the 256 arch VGPRs hold the rest), the anchored softmax, rescale,
-// flags and a16 redo are p2a's.
-// ------------------------------------------------------------------------------------------------------------
-struct P4Regs {
-  bf16x8 qf[4][4];  // Q^T of the four query blocks (pre-scaled)
-  f32x16 o[4][2];   // O^T[block][dim half] — fixed AGPRs (p4_pv)
-  f32x16 s[2];      // S^T of the jobs in flight, by job parity
-  u32x4 pf[2][2];   // packed bf16 P^T by job parity, 16-key slabs
-  bf16x8 kf[2][4];  // K fragments by half parity
-  bf16x8 vf[4];     // V^T fragments of the current half: [slab j * 2 + dim half]
-  f32x4 lsum[4];    // row sums per block (p2a's selector layout)
-  f32x16 negm;      // C operand of every QK^T chain = -anchor (wave-uniform)
-  float anc;
-};
-
-// O^T and Q^T live in fixed AGPRs (the physical-register constraints below): O^T[block qb][dim half dh] in
-// a[32 qb + 16 dh, +15], Q^T[block qb][16-dim slab c] in a[128 + 16 qb + 4 c, +3].  With the compiler's own operand
-// classes it shuttled O through arch VGPRs at every tile (331 AGPR reads + 517 writes per tile in the first build).
-#define P4_MFMA "v_mfma_f32_32x32x16_bf16 "
-template <int T, bool ZERO = false>
-VP_DEV void p4_pv(f32x16& o, const bf16x8& v, const bf16x8& p) {
-#define P4_PV(I, LO, HI)                                                                         \
-  if constexpr (T == I) {                                                                        \
-    if constexpr (ZERO)                                                                          \
-      asm volatile(P4_MFMA "%0, %1, %2, 0" : "={a[" #LO ":" #HI "]}"(o) : "v"(v), "v"(p));       \
-    else                                                                                         \
-      asm volatile(P4_MFMA "%0, %1, %2, %0" : "={a[" #LO ":" #HI "]}"(o) : "v"(v), "v"(p), "{a[" #LO ":" #HI "]}"(o)); \
-  }
-  P4_PV(0, 0, 15) P4_PV(1, 16, 31) P4_PV(2, 32, 47) P4_PV(3, 48, 63)
-  P4_PV(4, 64, 79) P4_PV(5, 80, 95) P4_PV(6, 96, 111) P4_PV(7, 112, 127)
-#undef P4_PV
-}
-template <int I, bool FIRST>
-VP_DEV void p4_qk(f32x16& s, const bf16x8& k, const bf16x8& q, const f32x16& negm) {
-  if constexpr (FIRST)
-    asm volatile(P4_MFMA "%0, %1, %2, %3" : "=&v"(s) : "v"(k), "v"(q), "v"(negm));
-  else
-    s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k, q, s, 0, 0, 0);
-}
-#undef P4_MFMA
-
-// O^T tile T out of its fixed AGPRs into arch VGPRs (element by element: an inline-asm operand cannot name a part of
-// a register tuple, and the compiler's own copy of a fixed tuple crashes its asm printer)
-template <int T>
-VP_DEV f32x16 p4_read_o(const f32x16& o) {
-  f32x16 x;
-  if constexpr (T == 0)
-    asm volatile("v_accvgpr_read_b32 %0, a0\n\tv_accvgpr_read_b32 %1, a1\n\tv_accvgpr_read_b32 %2, a2\n\tv_accvgpr_read_b32 %3, a3\n\tv_accvgpr_read_b32 %4, a4\n\tv_accvgpr_read_b32 %5, a5\n\tv_accvgpr_read_b32 %6, a6\n\tv_accvgpr_read_b32 %7, a7\n\tv_accvgpr_read_b32 %8, a8\n\tv_accvgpr_read_b32 %9, a9\n\tv_accvgpr_read_b32 %10, a10\n\tv_accvgpr_read_b32 %11, a11\n\tv_accvgpr_read_b32 %12, a12\n\tv_accvgpr_read_b32 %13, a13\n\tv_accvgpr_read_b32 %14, a14\n\tv_accvgpr_read_b32 %15, a15"
-                 : "=v"(x[0]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]), "=v"(x[4]), "=v"(x[5]), "=v"(x[6]), "=v"(x[7]), "=v"(x[8]), "=v"(x[9]), "=v"(x[10]), "=v"(x[11]), "=v"(x[12]), "=v"(x[13]), "=v"(x[14]), "=v"(x[15])
-                 : "{a[0:15]}"(o));
-  if constexpr (T == 1)
-    asm volatile("v_accvgpr_read_b32 %0, a16\n\tv_accvgpr_read_b32 %1, a17\n\tv_accvgpr_read_b32 %2, a18\n\tv_accvgpr_read_b32 %3, a19\n\tv_accvgpr_read_b32 %4, a20\n\tv_accvgpr_read_b32 %5, a21\n\tv_accvgpr_read_b32 %6, a22\n\tv_accvgpr_read_b32 %7, a23\n\tv_accvgpr_read_b32 %8, a24\n\tv_accvgpr_read_b32 %9, a25\n\tv_accvgpr_read_b32 %10, a26\n\tv_accvgpr_read_b32 %11, a27\n\tv_accvgpr_read_b32 %12, a28\n\tv_accvgpr_read_b32 %13, a29\n\tv_accvgpr_read_b32 %14, a30\n\tv_accvgpr_read_b32 %15, a31"
-                 : "=v"(x[0]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]), "=v"(x[4]), "=v"(x[5]), "=v"(x[6]), "=v"(x[7]), "=v"(x[8]), "=v"(x[9]), "=v"(x[10]), "=v"(x[11]), "=v"(x[12]), "=v"(x[13]), "=v"(x[14]), "=v"(x[15])
-                 : "{a[16:31]}"(o));
-  if constexpr (T == 2)
-    asm volatile("v_accvgpr_read_b32 %0, a32\n\tv_accvgpr_read_b32 %1, a33\n\tv_accvgpr_read_b32 %2, a34\n\tv_accvgpr_read_b32 %3, a35\n\tv_accvgpr_read_b32 %4, a36\n\tv_accvgpr_read_b32 %5, a37\n\tv_accvgpr_read_b32 %6, a38\n\tv_accvgpr_read_b32 %7, a39\n\tv_accvgpr_read_b32 %8, a40\n\tv_accvgpr_read_b32 %9, a41\n\tv_accvgpr_read_b32 %10, a42\n\tv_accvgpr_read_b32 %11, a43\n\tv_accvgpr_read_b32 %12, a44\n\tv_accvgpr_read_b32 %13, a45\n\tv_accvgpr_read_b32 %14, a46\n\tv_accvgpr_read_b32 %15, a47"
-                 : "=v"(x[0]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]), "=v"(x[4]), "=v"(x[5]), "=v"(x[6]), "=v"(x[7]), "=v"(x[8]), "=v"(x[9]), "=v"(x[10]), "=v"(x[11]), "=v"(x[12]), "=v"(x[13]), "=v"(x[14]), "=v"(x[15])
-                 : "{a[32:47]}"(o));
-  if constexpr (T == 3)
-    asm volatile("v_accvgpr_read_b32 %0, a48\n\tv_accvgpr_read_b32 %1, a49\n\tv_accvgpr_read_b32 %2, a50\n\tv_accvgpr_read_b32 %3, a51\n\tv_accvgpr_read_b32 %4, a52\n\tv_accvgpr_read_b32 %5, a53\n\tv_accvgpr_read_b32 %6, a54\n\tv_accvgpr_read_b32 %7, a55\n\tv_accvgpr_read_b32 %8, a56\n\tv_accvgpr_read_b32 %9, a57\n\tv_accvgpr_read_b32 %10, a58\n\tv_accvgpr_read_b32 %11, a59\n\tv_accvgpr_read_b32 %12, a60\n\tv_accvgpr_read_b32 %13, a61\n\tv_accvgpr_read_b32 %14, a62\n\tv_accvgpr_read_b32 %15, a63"
-                 : "=v"(x[0]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]), "=v"(x[4]), "=v"(x[5]), "=v"(x[6]), "=v"(x[7]), "=v"(x[8]), "=v"(x[9]), "=v"(x[10]), "=v"(x[11]), "=v"(x[12]), "=v"(x[13]), "=v"(x[14]), "=v"(x[15])
-                 : "{a[48:63]}"(o));
-  if constexpr (T == 4)
-    asm volatile("v_accvgpr_read_b32 %0, a64\n\tv_accvgpr_read_b32 %1, a65\n\tv_accvgpr_read_b32 %2, a66\n\tv_accvgpr_read_b32 %3, a67\n\tv_accvgpr_read_b32 %4, a68\n\tv_accvgpr_read_b32 %5, a69\n\tv_accvgpr_read_b32 %6, a70\n\tv_accvgpr_read_b32 %7, a71\n\tv_accvgpr_read_b32 %8, a72\n\tv_accvgpr_read_b32 %9, a73\n\tv_accvgpr_read_b32 %10, a74\n\tv_accvgpr_read_b32 %11, a75\n\tv_accvgpr_read_b32 %12, a76\n\tv_accvgpr_read_b32 %13, a77\n\tv_accvgpr_read_b32 %14, a78\n\tv_accvgpr_read_b32 %15, a79"
-                 : "=v"(x[0]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]), "=v"(x[4]), "=v"(x[5]), "=v"(x[6]), "=v"(x[7]), "=v"(x[8]), "=v"(x[9]), "=v"(x[10]), "=v"(x[11]), "=v"(x[12]), "=v"(x[13]), "=v"(x[14]), "=v"(x[15])
-                 : "{a[64:79]}"(o));
-  if constexpr (T == 5)
-    asm volatile("v_accvgpr_read_b32 %0, a80\n\tv_accvgpr_read_b32 %1, a81\n\tv_accvgpr_read_b32 %2, a82\n\tv_accvgpr_read_b32 %3, a83\n\tv_accvgpr_read_b32 %4, a84\n\tv_accvgpr_read_b32 %5, a85\n\tv_accvgpr_read_b32 %6, a86\n\tv_accvgpr_read_b32 %7, a87\n\tv_accvgpr_read_b32 %8, a88\n\tv_accvgpr_read_b32 %9, a89\n\tv_accvgpr_read_b32 %10, a90\n\tv_accvgpr_read_b32 %11, a91\n\tv_accvgpr_read_b32 %12, a92\n\tv_accvgpr_read_b32 %13, a93\n\tv_accvgpr_read_b32 %14, a94\n\tv_accvgpr_read_b32 %15, a95"
-                 : "=v"(x[0]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]), "=v"(x[4]), "=v"(x[5]), "=v"(x[6]), "=v"(x[7]), "=v"(x[8]), "=v"(x[9]), "=v"(x[10]), "=v"(x[11]), "=v"(x[12]), "=v"(x[13]), "=v"(x[14]), "=v"(x[15])
-                 : "{a[80:95]}"(o));
-  if constexpr (T == 6)
-    asm volatile("v_accvgpr_read_b32 %0, a96\n\tv_accvgpr_read_b32 %1, a97\n\tv_accvgpr_read_b32 %2, a98\n\tv_accvgpr_read_b32 %3, a99\n\tv_accvgpr_read_b32 %4, a100\n\tv_accvgpr_read_b32 %5, a101\n\tv_accvgpr_read_b32 %6, a102\n\tv_accvgpr_read_b32 %7, a103\n\tv_accvgpr_read_b32 %8, a104\n\tv_accvgpr_read_b32 %9, a105\n\tv_accvgpr_read_b32 %10, a106\n\tv_accvgpr_read_b32 %11, a107\n\tv_accvgpr_read_b32 %12, a108\n\tv_accvgpr_read_b32 %13, a109\n\tv_accvgpr_read_b32 %14, a110\n\tv_accvgpr_read_b32 %15, a111"
-                 : "=v"(x[0]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]), "=v"(x[4]), "=v"(x[5]), "=v"(x[6]), "=v"(x[7]), "=v"(x[8]), "=v"(x[9]), "=v"(x[10]), "=v"(x[11]), "=v"(x[12]), "=v"(x[13]), "=v"(x[14]), "=v"(x[15])
-                 : "{a[96:111]}"(o));
-  if constexpr (T == 7)
-    asm volatile("v_accvgpr_read_b32 %0, a112\n\tv_accvgpr_read_b32 %1, a113\n\tv_accvgpr_read_b32 %2, a114\n\tv_accvgpr_read_b32 %3, a115\n\tv_accvgpr_read_b32 %4, a116\n\tv_accvgpr_read_b32 %5, a117\n\tv_accvgpr_read_b32 %6, a118\n\tv_accvgpr_read_b32 %7, a119\n\tv_accvgpr_read_b32 %8, a120\n\tv_accvgpr_read_b32 %9, a121\n\tv_accvgpr_read_b32 %10, a122\n\tv_accvgpr_read_b32 %11, a123\n\tv_accvgpr_read_b32 %12, a124\n\tv_accvgpr_read_b32 %13, a125\n\tv_accvgpr_read_b32 %14, a126\n\tv_accvgpr_read_b32 %15, a127"
-                 : "=v"(x[0]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]), "=v"(x[4]), "=v"(x[5]), "=v"(x[6]), "=v"(x[7]), "=v"(x[8]), "=v"(x[9]), "=v"(x[10]), "=v"(x[11]), "=v"(x[12]), "=v"(x[13]), "=v"(x[14]), "=v"(x[15])
-                 : "{a[112:127]}"(o));
-  return x;
-}
-
-// one step: QK^T of block QB into S buffer QS (K buffer KB_), PV of block PB from P buffer PP, the row sums of PB,
-// and in every gap the exp pair of S buffer EB + the pack of the pair before (into P buffer EB)
-// one V^T fragment (16-key slab c >> 1, dim half c & 1) of half kh — p1_read_v's piece c
-VP_DEV void p4_read_v1(const char* Vl, int kh, int c, const int (&vo)[2], bf16x8& vf) {
-  const char* base = Vl + (kh * 2 + (c >> 1)) * 16 * 128 + vo[c & 1];
-  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)base);
-  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + 8 * 128));
-  vf = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
-
-// RV: this step's PVs are the last on the old half's V^T — fragment c is refreshed with half kh's in the gap after
-// the one whose PV last read it (with one wave per SIMD nothing else hides the LDS latency, so the reads go early)
-template <int EB, int QB, int QS, int PB, int PP, int KB_, int G, bool RV>
-VP_DEV void p4_gap(P4Regs& r, float (&p)[16], const char* Vl, int kh, const int (&vo)[2]) {
-  constexpr int c = G >> 1;
-  p1_fence();
-  if constexpr ((G & 1) == 0)
-    p4_qk<4 * QB + c, c == 0>(r.s[QS], r.kf[KB_][c], r.qf[QB][c], r.negm);
-  else
-    p4_pv<2 * PB + (c & 1)>(r.o[PB][c & 1], r.vf[c], as_bf16x8(r.pf[PP][c >> 1]));
-  p1_fence();
-  p1_exp(p[2 * G], p[2 * G + 1], r.s[EB][2 * G], r.s[EB][2 * G + 1]);
-  if constexpr (G > 0) r.pf[EB][(G - 1) >> 2][(G - 1) & 3] = p1_pack(p[2 * G - 2], p[2 * G - 1]);
-  if constexpr (RV && (G & 1) == 0 && G >= 2) p4_read_v1(Vl, kh, G / 2 - 1, vo, r.vf[G / 2 - 1]);
-}
-
-template <int EB, int QB, int QS, int PB, int PP, int KB_, bool RV = false>
-VP_DEV void p4_step(P4Regs& r, const bf16x8& sel, const char* Vl = nullptr, int kh = 0,
-                    const int (&vo)[2] = {0, 0}) {
-  float p[16];
-  p4_gap<EB, QB, QS, PB, PP, KB_, 0, RV>(r, p, Vl, kh, vo);
-  p4_gap<EB, QB, QS, PB, PP, KB_, 1, RV>(r, p, Vl, kh, vo);
-  p4_gap<EB, QB, QS, PB, PP, KB_, 2, RV>(r, p, Vl, kh, vo);
-  p4_gap<EB, QB, QS, PB, PP, KB_, 3, RV>(r, p, Vl, kh, vo);
-  p4_gap<EB, QB, QS, PB, PP, KB_, 4, RV>(r, p, Vl, kh, vo);
-  p4_gap<EB, QB, QS, PB, PP, KB_, 5, RV>(r, p, Vl, kh, vo);
-  p4_gap<EB, QB, QS, PB, PP, KB_, 6, RV>(r, p, Vl, kh, vo);
-  p4_gap<EB, QB, QS, PB, PP, KB_, 7, RV>(r, p, Vl, kh, vo);
-  p1_fence();
-  r.lsum[PB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[PP][0]), r.lsum[PB], 0, 0, 0);
-  p1_fence();
-  r.pf[EB][1][3] = p1_pack(p[14], p[15]);
-  p1_fence();
-  r.lsum[PB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[PP][1]), r.lsum[PB], 0, 0, 0);
-  p1_fence();
-  if constexpr (RV) p4_read_v1(Vl, kh, 3, vo, r.vf[3]);
-}
-
-// one 128-key tile = 16 steps; the K fragments of half h + 1 read in step (h, 0), V^T of half h inside step (h, 0)
-// fragment by fragment behind its PVs on half h - 1's (p4_gap RV); the seam after step (3, 1): wait for the next tile (VMC: the tile after next
-// stays in flight), barrier, read its K(0) — two steps of cover before step (3, 3)'s QK^T of the next tile's job 0
-template <int VMC>
-VP_DEV void p4_tile(P4Regs& r, const bf16x8& sel, const char* Kl, const char* Kn, int lim, bool masked, bool last,
-                    bool wait_all, int lane, const int (&vo)[2]) {
-  const int hl4 = 4 * (lane >> 5);
-  const char* Vl = Kl + KT;
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    if (h < 3) p1_read_k(Kl, h + 1, lane, r.kf[(h + 1) & 1]);
-    if (masked) p1_mask(r.s[0], lim - 32 * h, hl4);
-    if (h & 1)
-      p4_step<0, 1, 1, 3, 1, 1, true>(r, sel, Vl, h, vo);
-    else
-      p4_step<0, 1, 1, 3, 1, 0, true>(r, sel, Vl, h, vo);
-    if (masked) p1_mask(r.s[1], lim - 32 * h, hl4);
-    if (h & 1)
-      p4_step<1, 2, 0, 0, 0, 1>(r, sel);
-    else
-      p4_step<1, 2, 0, 0, 0, 0>(r, sel);
-    if (h == 3 && !last) {
-      if (VMC == 0 || wait_all)
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VMC) : "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      p1_read_k(Kn, 0, lane, r.kf[0]);
-    }
-    if (masked) p1_mask(r.s[0], lim - 32 * h, hl4);
-    if (h & 1)
-      p4_step<0, 3, 1, 1, 1, 1>(r, sel);
-    else
-      p4_step<0, 3, 1, 1, 1, 0>(r, sel);
-    if (masked) p1_mask(r.s[1], lim - 32 * h, hl4);
-    // QK^T of the next half's job 0 on K(h + 1) (the next tile's K(0) at h = 3; stale on the last tile, unused)
-    if (h & 1)
-      p4_step<1, 0, 0, 2, 0, 0>(r, sel);
-    else
-      p4_step<1, 0, 0, 2, 0, 1>(r, sel);
-  }
-  // no anchored rescale here (O sits in fixed AGPRs the VALU cannot scale in place): a block whose scores outgrow
-  // the anchor by more than 2^127 overflows O / l to inf and is flagged and recomputed exactly (the a16 redo)
-}
-
-template <bool TAIL = false>
-__global__ __launch_bounds__(NW4 * 64, 1) void attn_fwd_p4(const vp_attn_desc d, const AttnSplit sp) {
-  constexpr int NWV = NW4;
-  constexpr int QBV = NWV * 128;              // queries per workgroup (128 per wave)
-  constexpr int PPWV = NP / NWV;              // DMA pieces per operand, wave and tile
-  constexpr int RING = 4;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hl = lane >> 5;
-
-  const int nqb = (d.Nq + QBV - 1) / QBV;
-  const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
-  const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
-  const int bh = t / nqb;
-  const int qb = t - bh * nqb;
-  const int b = bh / d.H;
-  const int h = bh - b * d.H;
-  const int tiles1 = (d.Nk + KB - 1) / KB;
-  const int n2 = d.k2_len != nullptr ? max(0, min(__builtin_amdgcn_readfirstlane(d.k2_len[b]), d.Nk2)) : d.Nk2;
-  const int tiles2 = n2 > 0 ? (n2 + KB - 1) / KB : 0;
-  const int ntiles_all = tiles1 + tiles2;
-  const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
-  const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
-  const int qw0 = qb * QBV + wave * 128;
-
-  P4Regs r;
-  {
-    const float cq = d.scale * 1.4426950408889634f;
-#pragma unroll
-    for (int qi = 0; qi < 4; ++qi) {
-      const int q = qw0 + qi * 32 + (lane & 31);
-      const int qc = q < d.Nq ? q : d.Nq - 1;
-      const bf16* qrow = (const bf16*)d.Q + (int64_t)b * d.q_sb + (int64_t)qc * d.q_sn + h * 64;
-#pragma unroll
-      for (int ds = 0; ds < 4; ++ds) {
-        r.qf[qi][ds] = *(const bf16x8*)(qrow + ds * 16 + hl * 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r.qf[qi][ds][j] = f2bf(bf2f(r.qf[qi][ds][j]) * cq);
-      }
-    }
-  }
-  auto slot_of = [&](int ti) { return smem + (ti & (RING - 1)) * ST; };
-  int voff_k[PPWV], voff_v[PPWV];
-#pragma unroll
-  for (int i = 0; i < PPWV; ++i) {
-    const int prow = (wave + i * NWV) * 8 + (lane >> 3);
-    voff_k[i] = (prow * (int)d.k_sn + (((lane & 7) ^ swz(prow)) * 8)) * 2;
-    voff_v[i] = (prow * (int)d.v_sn + (((lane & 7) ^ vswz(prow)) * 8)) * 2;
-  }
-  const char* kseg1 = (const char*)((const bf16*)d.K + (int64_t)b * d.k_sb + h * 64);
-  const char* vseg1 = (const char*)((const bf16*)d.V + (int64_t)b * d.v_sb + h * 64);
-  const int full1 = d.Nk / KB;
-  const bool seg2fast = d.K2 != nullptr && d.k2_sn == d.k_sn && d.v2_sn == d.v_sn;
-  const int full2 = seg2fast ? n2 / KB : 0;
-  const char* kseg2 = seg2fast ? (const char*)((const bf16*)d.K2 + (int64_t)b * d.k2_sb + h * 64) : nullptr;
-  const char* vseg2 = seg2fast ? (const char*)((const bf16*)d.V2 + (int64_t)b * d.v2_sb + h * 64) : nullptr;
-  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem) + wave * 1024;
-  auto issue = [&](int ti) {
-    const bool s1 = ti < full1;
-    if (s1 || (ti >= tiles1 && ti - tiles1 < full2)) {
-      const unsigned la = lds0 + (ti & (RING - 1)) * ST;
-      const int tt = s1 ? ti : ti - tiles1;
-      const char* kb = (s1 ? kseg1 : kseg2) + (int64_t)tt * KB * d.k_sn * 2;
-      const char* vb = (s1 ? vseg1 : vseg2) + (int64_t)tt * KB * d.v_sn * 2;
-#pragma unroll
-      for (int i = 0; i < PPWV; ++i) {
-        glds16_lds(kb, voff_k[i], la + i * NWV * 1024);
-        glds16_lds(vb, voff_v[i], la + KT + i * NWV * 1024);
-      }
-      return;
-    }
-    const int ln = lane_id_opaque();
-    const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
-    char* slot = slot_of(ti);
-    const int last = sg.n - 1 - sg.key0;
-    const char* kb = (const char*)(sg.k + (int64_t)sg.key0 * sg.k_sn);
-    const char* vb = (const char*)(sg.v + (int64_t)sg.key0 * sg.v_sn);
-    const int ksn = (int)sg.k_sn, vsn = (int)sg.v_sn;
-#pragma unroll
-    for (int i = 0; i < PPWV; ++i) {
-      const int pc = wave + i * NWV;
-      const int prow = pc * 8 + (ln >> 3);
-      const int rr = min(prow, last);
-      glds16(kb, (rr * ksn + (((ln & 7) ^ swz(prow)) * 8)) * 2, slot + pc * 1024);
-      glds16(vb, (rr * vsn + (((ln & 7) ^ vswz(prow)) * 8)) * 2, slot + KT + pc * 1024);
-    }
-  };
-
-  const int g = lane >> 4;
-  const int trow = 4 * (g >> 1) + ((lane & 15) >> 2);
-  const int tcol = 16 * (g & 1) + 4 * (lane & 3);
-  int vo[2];
-#pragma unroll
-  for (int dh = 0; dh < 2; ++dh) vo[dh] = trow * 128 + (((dh * 4 + (tcol >> 3)) ^ vswz(trow)) << 4) + (tcol & 7) * 2;
-
-  {
-    // O = 0 x 0 + 0 (an MFMA writes the fixed AGPRs)
-    const bf16x8 z = {};
-    p4_pv<0, true>(r.o[0][0], z, z);
-    p4_pv<1, true>(r.o[0][1], z, z);
-    p4_pv<2, true>(r.o[1][0], z, z);
-    p4_pv<3, true>(r.o[1][1], z, z);
-    p4_pv<4, true>(r.o[2][0], z, z);
-    p4_pv<5, true>(r.o[2][1], z, z);
-    p4_pv<6, true>(r.o[3][0], z, z);
-    p4_pv<7, true>(r.o[3][1], z, z);
-  }
-#pragma unroll
-  for (int qi = 0; qi < 4; ++qi) r.lsum[qi] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int e = 0; e < 2; ++e) r.pf[j][e] = (u32x4){0u, 0u, 0u, 0u};
-#pragma unroll
-  for (int c = 0; c < 4; ++c) r.vf[c] = (bf16x8){};  // job -1: 0 x 0
-  bf16x8 sel;
-  {
-    const bf16 one = f2bf((((lane >> 4) & 1) == 0) == ((lane & 15) < 8) ? 1.f : 0.f);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sel[e] = one;
-  }
-
-  const bool any = tbeg < tend;  // workgroup-uniform
-  if (any) issue(tbeg);
-  if (tbeg + 1 < tend) {
-    issue(tbeg + 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPWV) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  if (any) p1_read_k(slot_of(tbeg), 0, lane, r.kf[0]);
-  {
-    // the anchor: max over the four blocks' scores of the first 32 keys; job (0, 0)'s scores stay in s[0], blocks
-    // 1-3 pass through s[1] (job (0, 1) is recomputed by the first step with C = -anchor)
-    const f32x16 z = {};
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      r.s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.kf[0][c], r.qf[0][c], c == 0 ? z : r.s[0], 0, 0, 0);
-    float mx = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, r.s[0][i]);
-#pragma unroll
-    for (int qi = 1; qi < 4; ++qi) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        r.s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r.kf[0][c], r.qf[qi][c], c == 0 ? z : r.s[1], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, r.s[1][i]);
-    }
-#pragma unroll
-    for (int sh = 1; sh < 64; sh <<= 1) mx = fmaxf(mx, __shfl_xor(mx, sh, 64));
-    mx = __builtin_ceilf(mx);
-    r.anc = any ? __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(mx))) : -INFINITY;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      r.s[0][i] -= r.anc;
-      r.negm[i] = -r.anc;
-    }
-    asm volatile("" : "+v"(r.negm));  // kept in VGPRs (else rebuilt from SGPRs by 8 v_mov_b64 per job)
-  }
-  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // S -> the first (asm) exp
-  ClockStamp ck;
-  ck.start();
-  for (int ti = tbeg; ti < tend; ++ti) {
-    if (ti + 2 < tend && (!(VP_P1_ABL & 1) || ti == tbeg)) issue(ti + 2);
-    int lim = KB;
-    if (ti >= full1) {
-      const Seg sg = tile_seg(d, ti, tiles1, b, h, n2);
-      lim = sg.n - sg.key0;
-    }
-    p4_tile<2 * PPWV>(r, sel, slot_of(ti), slot_of(ti + 1), __builtin_amdgcn_readfirstlane(lim), lim < KB,
-                      ti + 1 >= tend, ti + 2 >= tend, lane, vo);
-  }
-  // drain: PV + row sums of the last job (3, 3) (block 3, P buffer 1)
-  p4_pv<6>(r.o[3][0], r.vf[0], as_bf16x8(r.pf[1][0]));
-  p4_pv<7>(r.o[3][1], r.vf[1], as_bf16x8(r.pf[1][0]));
-  p4_pv<6>(r.o[3][0], r.vf[2], as_bf16x8(r.pf[1][1]));
-  p4_pv<7>(r.o[3][1], r.vf[3], as_bf16x8(r.pf[1][1]));
-  r.lsum[3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[1][0]), r.lsum[3], 0, 0, 0);
-  r.lsum[3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, as_bf16x8(r.pf[1][1]), r.lsum[3], 0, 0, 0);
-  // (the asm MFMAs' O results: wait them out before the compiler reads the AGPRs)
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  ck.stop(tid);
-  f32x16 ov[4][2] = {{p4_read_o<0>(r.o[0][0]), p4_read_o<1>(r.o[0][1])}, {p4_read_o<2>(r.o[1][0]), p4_read_o<3>(r.o[1][1])},
-                     {p4_read_o<4>(r.o[2][0]), p4_read_o<5>(r.o[2][1])}, {p4_read_o<6>(r.o[3][0]), p4_read_o<7>(r.o[3][1])}};
-
-  const int qq = lane & 31;
-  float l_tot[4];
-#pragma unroll
-  for (int qi = 0; qi < 4; ++qi) {
-    l_tot[qi] = __shfl(r.lsum[qi][0], qq < 16 ? qq : qq + 16, 64);
-    const int q = qw0 + qi * 32 + qq;
-    if (!TAIL && d.l_extra != nullptr)
-      l_tot[qi] += __builtin_amdgcn_exp2f(d.l_extra[((int64_t)b * d.H + h) * d.Nq + min(q, d.Nq - 1)] - r.anc);
-  }
-  {
-    bool bad = false;
-#pragma unroll
-    for (int qi = 0; qi < 4; ++qi) {
-      bad |= nonfinite(l_tot[qi]) || (any && !(l_tot[qi] >= 0x1p-96f));
-      const float inv = 1.f / l_tot[qi];
-#pragma unroll
-      for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) bad |= nonfinite(sp.nsplit == 1 ? ov[qi][dh][i] * inv : ov[qi][dh][i]);
-    }
-    int* wflag = (int*)(smem + RING * ST);
-    const int mine = __ballot(bad) != 0ull;
-    if (lane == 0) wflag[wave] = mine;
-    __syncthreads();
-    int redo = 0;
-#pragma unroll
-    for (int w = 0; w < NWV; ++w) redo |= wflag[w];
-    if (tid == 0 && sp.flags != nullptr)
-      sp.flags[sp.nsplit > 1 ? sp.flag_main + (t - sp.t_base) * sp.nsplit + split : t] = redo;
-    if (redo) return;
-  }
-#pragma unroll
-  for (int qi = 0; qi < 4; ++qi) {
-    const int q = qw0 + qi * 32 + qq;
-    if (sp.nsplit > 1) {
-      const int qin = wave * 128 + qi * 32 + qq;
-      store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QBV + qin) * 66, ov[qi], r.anc,
-                    l_tot[qi], hl);
-    } else {
-      store_out(d, ov[qi], l_tot[qi], q, b, h, hl, false, r.anc);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------------------
 // P2S ("build the pipelined 16x16x32 form and decide by wall"): p2a's software pipeline — the same
 // jobs (32-key half x 32-query block), the same step order, ring, seam, anchor, rescale, flags and redo — on
 // v_mfma_f32_16x16x32_bf16, the shape the chip holds a higher clock on under load (MI355X_MICROARCH.md 'DVFS
@@ -2719,7 +2302,7 @@ struct AttnVar {
   int lds;  // dynamic LDS bytes
   int qb = QB;  // queries per workgroup
 };
-enum { V_S16, V_A16, V_P2, V_P2A, V_P2W, V_P2W2, V_P2S, V_P4, V_NVAR };
+enum { V_S16, V_A16, V_P2, V_P2A, V_P2W, V_P2W2, V_P2S, V_NVAR };
 static const AttnVar attn_vars[] = {
     {"s16", (const void*)attn_fwd_s16<false>, (const void*)attn_fwd_s16<true>, NW4 * 64, LDS_BYTES},
     {"a16", (const void*)attn_fwd_s16<false, true>, (const void*)attn_fwd_s16<true, true>, NW4 * 64, LDS_BYTES},
@@ -2733,12 +2316,10 @@ static const AttnVar attn_vars[] = {
      4 * ST + 32, 512},
     // p2a's pipeline on the 16x16x32 MFMA (anchored)
     {"p2s", (const void*)attn_fwd_p2s<false>, (const void*)attn_fwd_p2s<true>, NW4 * 64, 2 * ST + 16},
-    // four 32-query blocks per wave at one wave per SIMD (512-query workgroups, a 4-slot ring)
-    {"p4", (const void*)attn_fwd_p4<false>, (const void*)attn_fwd_p4<true>, NW4 * 64, 4 * ST + 16, 512},
 };
 static_assert(sizeof(attn_vars) / sizeof(attn_vars[0]) == V_NVAR, "variant table");
 // the anchored p2 family (a flag per block, the a16 redo)
-static bool anchored_var(int v) { return v == V_P2A || v == V_P2W || v == V_P2W2 || v == V_P2S || v == V_P4; }
+static bool anchored_var(int v) { return v == V_P2A || v == V_P2W || v == V_P2W2 || v == V_P2S; }
 
 struct AttnPlan {
   const AttnVar* v;
