@@ -769,6 +769,49 @@ def test_attention_tail_split_matches_unsplit(Nq, Nk2, knobs):
         assert rel(out_s, ref) < 1e-2 and rel(out_u, ref) < 1e-2
 
 
+@pytest.mark.parametrize("tail", ["default", "0:8", "1:4", "2:2"])
+@pytest.mark.parametrize("mode", ["p2a", "p2"])
+@pytest.mark.parametrize("Nq,Nk2,H", [(8000, 700, 17), (17776, 0, 48)])
+def test_attention_one_launch_tail_matches_unsplit(Nq, Nk2, H, mode, tail, knobs):
+    """VP_ATTN_TAIL = "R:S": the remainder blocks plus R whole rounds run as S key-range pieces each at the END of the
+    main grid (one launch, then the merge pass) — against the unsplit launch; the l_extra / k2_len path through the
+    pieces as well (the merge adds the null-key mass once)."""
+    from videopainter_amd import kernels as K
+    from videopainter_amd import _native as N
+    import ctypes as C
+    need_variant(mode, knobs)
+    B, D = 2, H * 64
+    sc = 0.5 if mode == "p2" else 1.0
+    q, k, v = (bf(rnd(B, Nq, D, seed=s) * sc).to(dev) for s in (90, 91, 92))
+    kw = dict(bounded_scores=mode == "p2")
+    if Nk2:
+        kw.update(k2=bf(rnd(B, Nk2, D, seed=93) * sc).to(dev), v2=bf(rnd(B, Nk2, D, seed=94)).to(dev),
+                  k2_len=torch.tensor([Nk2 - 100, Nk2], dtype=torch.int32, device=dev),
+                  l_extra=(torch.randn(B, H, Nq, generator=torch.Generator().manual_seed(95)) * 2).to(dev))
+    knobs.setenv("VP_ATTN_BOUNDED_MODE" if mode == "p2" else "VP_ATTN_UNBOUNDED_MODE", mode)
+    if tail != "default":
+        knobs.setenv("VP_ATTN_TAIL", tail)
+    d = N.AttnDesc()
+    d.B, d.H, d.Nq, d.head_dim, d.Nk, d.Nk2 = B, H, Nq, 64, Nq, 0
+    d.Q = d.K = d.V = d.O = q.data_ptr()
+    d.q_sn = d.k_sn = d.v_sn = d.o_sn = D
+    d.q_sb = d.k_sb = d.v_sb = d.o_sb = Nq * D
+    d.flags = K.ATTN_BOUNDED_SCORES if mode == "p2" else 0
+    nblk = B * H * ((Nq + 255) // 256)
+    # default: R = 0, S = min(8, ceil(2 slots / remainder))
+    R, S = (0, min(8, -(-1024 // (nblk % 512)))) if tail == "default" else (int(x) for x in tail.split(":"))
+    if nblk % 512 + (R + 1) * 512 > nblk:
+        pytest.skip("the plan keeps at least one whole round unsplit")
+    ws = N.lib().vp_attention_workspace_bytes(C.byref(d))
+    assert ws >= (nblk % 512 + R * 512) * S * 256 * 66 * 4  # the one-launch split is active for this shape
+    out_s = torch.empty(B, Nq, D, device=dev, dtype=torch.bfloat16)
+    K.attention(q, k, v, out_s, H, **kw)
+    knobs.setenv("VP_ATTN_NO_SPLIT", "1")
+    out_u = torch.empty_like(out_s)
+    K.attention(q, k, v, out_u, H, **kw)
+    assert rel(out_s, out_u) < 5e-3
+
+
 @pytest.mark.parametrize("mode", ["p2", "s16"])
 @pytest.mark.parametrize("Nq,Nk2", [(1500, 700), (17776, 0)])
 def test_attention_bounded_tail_split_matches_unsplit(Nq, Nk2, mode, knobs):

@@ -27,6 +27,7 @@
 //          and the P^T operand as B gives all 32 queries' sums, so the VALU does only exp2 + pack per score.
 //          (Measured at config 2: 1.15 PF/s against 1.13 for LAZY; the same no-max kernel with the sums on the VALU
 //          needs a second score tile live and spills at 128 VGPRs: 0.97.)
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -214,6 +215,9 @@ struct AttnSplit {
   int flag_nsplit;   // splits per tail block
   int redo;          // a16 redo launch: a workgroup whose block is not flagged returns at once
   int flag_shift;    // redo of p2w: flags are per 512-query block (two of a16's 256-query blocks): shift 1
+  // one-launch tail (p2 / p2a): workgroups blockIdx < main_blocks run whole blocks (XCD-remapped over main_blocks),
+  // the rest are the key-range pieces of blocks t_base + (blockIdx - main_blocks) / nsplit, dispatched last
+  int main_blocks;
 };
 
 // is block t flagged by its p2a workgroup(s)?
@@ -575,8 +579,12 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
   const int hl = lane >> 5;
 
   const int nqb = (d.Nq + QBV - 1) / QBV;
-  const int split = sp.nsplit > 1 ? (int)(blockIdx.x % sp.nsplit) : 0;
-  const int t = sp.nsplit > 1 ? sp.t_base + (int)(blockIdx.x / sp.nsplit) : xcd_remap(blockIdx.x, gridDim.x);
+  // a key-range piece of a tail block (the TAIL instance of a two-launch tail, or blockIdx >= main_blocks of a
+  // one-launch tail), or a whole block
+  const int pj = (int)blockIdx.x - sp.main_blocks;
+  const bool piece = sp.nsplit > 1 && pj >= 0;
+  const int split = piece ? pj % sp.nsplit : 0;
+  const int t = piece ? sp.t_base + pj / sp.nsplit : xcd_remap(blockIdx.x, sp.nsplit > 1 ? sp.main_blocks : gridDim.x);
   const int bh = t / nqb;
   const int qb = t - bh * nqb;
   const int b = bh / d.H;
@@ -586,8 +594,8 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
   const int n2 = d.k2_len != nullptr ? max(0, min(__builtin_amdgcn_readfirstlane(d.k2_len[b]), d.Nk2)) : d.Nk2;
   const int tiles2 = n2 > 0 ? (n2 + KB - 1) / KB : 0;
   const int ntiles_all = tiles1 + tiles2;
-  const int tbeg = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
-  const int tend = sp.nsplit > 1 ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
+  const int tbeg = piece ? (int)((int64_t)ntiles_all * split / sp.nsplit) : 0;
+  const int tend = piece ? (int)((int64_t)ntiles_all * (split + 1) / sp.nsplit) : ntiles_all;
   const int qw0 = qb * QBV + wave * 64;
 #ifdef VP_P1_PRIO
   if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);  // A/B: static priority for every other workgroup
@@ -779,7 +787,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
     // l_extra: row-sum mass of keys outside the segments (the resample processor's null keys, log2 score units,
     // relative to the reference point: 0 when bounded, the anchor when anchored); a tail-split partial leaves it to
     // attn_combine_kernel
-    if (!TAIL && d.l_extra != nullptr)
+    if (!TAIL && !piece && d.l_extra != nullptr)
       l_tot[qi] += __builtin_amdgcn_exp2f(d.l_extra[((int64_t)b * d.H + h) * d.Nq + min(q, d.Nq - 1)] - r.anc);
   }
   if constexpr (ANCH) {
@@ -797,7 +805,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
 #pragma unroll
       for (int dh = 0; dh < 2; ++dh)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) bad |= nonfinite(sp.nsplit == 1 ? r.o[qi][dh][i] * inv : r.o[qi][dh][i]);
+        for (int i = 0; i < 16; ++i) bad |= nonfinite(!piece ? r.o[qi][dh][i] * inv : r.o[qi][dh][i]);
     }
     int* wflag = (int*)(smem + RING * ST);
     const int mine = __ballot(bad) != 0ull;
@@ -807,13 +815,13 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
 #pragma unroll
     for (int w = 0; w < NWV; ++w) redo |= wflag[w];
     if (tid == 0 && sp.flags != nullptr)
-      sp.flags[sp.nsplit > 1 ? sp.flag_main + (t - sp.t_base) * sp.nsplit + split : t] = redo;
+      sp.flags[piece ? sp.flag_main + (t - sp.t_base) * sp.nsplit + split : t] = redo;
     if (redo) return;
   }
 #pragma unroll
   for (int qi = 0; qi < 2; ++qi) {
     const int q = qw0 + qi * 32 + qq;
-    if (sp.nsplit > 1) {
+    if (piece) {
       const int qin = wave * 64 + qi * 32 + qq;
       store_partial(sp.ws + (((int64_t)(t - sp.t_base) * sp.nsplit + split) * QBV + qin) * 66, r.o[qi], r.anc,
                     l_tot[qi], hl);
@@ -2326,6 +2334,7 @@ struct AttnPlan {
   int var;
   int64_t nblk;
   int ntail = 0, nsplit = 1;  // tail split: the last ntail blocks as ntail * nsplit key-range workgroups
+  bool one_launch = false;    // the pieces ride at the end of the main grid (p2 / p2a) instead of a launch after it
   int64_t ws_bytes = 0;       // tail partials, then (p2a) the redo flags
   int64_t part_bytes = 0;     // the tail partials' part of it
 };
@@ -2406,7 +2415,25 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   if (slots > 0 && (ns == nullptr || ns[0] == '0')) {
     const int tail = (int)(pl.nblk % slots);
     const int ntile = (d->Nk + KB - 1) / KB + (d->Nk2 > 0 ? (d->Nk2 + KB - 1) / KB : 0);
-    if (tail > 0 && 2 * tail <= slots) {
+    // p2 / p2a: one launch whose last workgroups are the key-range pieces (S per block) of the remainder blocks —
+    // dispatched last, they fill the slots the main blocks' uneven finish leaves idle, where the two-launch split
+    // below first waits for the slowest main block.  S = min(8, ceil(2 slots / remainder)): about two rounds of
+    // pieces.  Config 2 (64 remainder blocks, S = 8) 6.22 vs 6.26 ms; B = 1 (288 remainder blocks, no two-launch
+    // split: 2 x 288 > 512 slots; S = 4) 3.15 vs 3.26 ms; splitting whole rounds as well (R > 0) is slower
+    // (profiles/r06_attn_one_launch_tail_ab.log).  VP_ATTN_TAIL = "R:S" sets R extra whole rounds and S (A/B),
+    // "legacy" the two-launch split.
+    const char* tk = vp_knob(VPK_ATTN_TAIL);
+    int R = 0, S1 = tail > 0 ? min(8, (2 * slots + tail - 1) / tail) : 0;
+    if (tk != nullptr && (sscanf(tk, "%d:%d", &R, &S1) != 2 || R < 0 || R > 4 || S1 < 2 || S1 > 8)) R = -1;
+    const bool p1v = pl.var == V_P2 || pl.var == V_P2A;
+    const int64_t nt = tail + (int64_t)max(R, 0) * slots;
+    if (p1v && R >= 0 && nt > 0 && nt + slots <= pl.nblk && min(S1, ntile) >= 2) {
+      // (at least one whole round stays unsplit; a grid under two rounds keeps the two-launch rule below)
+      pl.ntail = (int)nt;
+      pl.nsplit = min(S1, ntile);
+      pl.one_launch = true;
+      pl.part_bytes = nt * pl.nsplit * pl.v->qb * 66 * 4;
+    } else if (tail > 0 && 2 * tail <= slots) {
       const int S = min(min(8, slots / tail), ntile);
       if (S >= 2) {
         pl.ntail = tail;
@@ -2458,18 +2485,28 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
   const int64_t main_blocks = split ? pl.nblk - pl.ntail : pl.nblk;
   int* flags = anchored_var(pl.var) ? (int*)((char*)workspace + pl.part_bytes) : nullptr;
   hipError_t le = hipSuccess;
-  if (main_blocks > 0) {
+  if (split && pl.one_launch) {
+    // whole blocks first, then the pieces: one grid, dispatched in blockIdx order
+    const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace, flags, (int)main_blocks, pl.nsplit, 0, 0,
+                          (int)main_blocks};
+    void* args[] = {(void*)d, (void*)&sp};
+    le = hipLaunchKernel(v.fn, dim3((unsigned)(main_blocks + (int64_t)pl.ntail * pl.nsplit)), dim3(v.threads), args,
+                         v.lds, (hipStream_t)stream);
+    if (le != hipSuccess) return (int)le;
+  } else if (main_blocks > 0) {
     const AttnSplit none = {0, 1, nullptr, flags, (int)main_blocks, pl.nsplit, 0};
     void* args[] = {(void*)d, (void*)&none};
     le = hipLaunchKernel(v.fn, dim3((unsigned)main_blocks), dim3(v.threads), args, v.lds, (hipStream_t)stream);
     if (le != hipSuccess) return (int)le;
   }
   if (split) {
-    const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace, flags, (int)main_blocks, pl.nsplit, 0};
-    void* args[] = {(void*)d, (void*)&sp};
-    le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.threads), args, v.lds,
-                         (hipStream_t)stream);
-    if (le != hipSuccess) return (int)le;
+    if (!pl.one_launch) {
+      const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace, flags, (int)main_blocks, pl.nsplit, 0};
+      void* args[] = {(void*)d, (void*)&sp};
+      le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.threads), args, v.lds,
+                           (hipStream_t)stream);
+      if (le != hipSuccess) return (int)le;
+    }
     const int nthreads = pl.ntail * v.qb * 16;
     hipLaunchKernelGGL(attn_combine_kernel, dim3((nthreads + 255) / 256), dim3(256), 0, (hipStream_t)stream, *d,
                        (int)main_blocks, pl.ntail, pl.nsplit, v.qb, (const float*)workspace, (const int*)flags);

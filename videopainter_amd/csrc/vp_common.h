@@ -239,6 +239,7 @@ enum VpKnob {
   VPK_CONV_HOIST,
   VPK_CONV_PIPE,
   VPK_ATTN_BWD_VARIANT,
+  VPK_ATTN_TAIL,
   VPK_COUNT
 };
 const char* vp_knob(int k);
