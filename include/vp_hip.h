@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 18
+#define VP_ABI_VERSION 19
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
@@ -565,6 +565,12 @@ typedef struct vp_attn_bwd_desc {
   int32_t pad1;
 } vp_attn_bwd_desc;
 int vp_attention_bwd_bf16(const vp_attn_bwd_desc* d, void* stream);
+/* The same with a workspace for the grid-tail split (ABI 19): the blocks of each kernel's last partial round run as
+ * key- / query-range pieces at the end of its grid, their fp32 sums merged by a small pass.
+ * vp_attention_bwd_workspace_bytes: bytes needed for this descriptor (0: no split; -1: invalid descriptor); a smaller
+ * or NULL workspace runs unsplit.  VP_ATTN_NO_SPLIT disables the split (A/B). */
+int64_t vp_attention_bwd_workspace_bytes(const vp_attn_bwd_desc* d);
+int vp_attention_bwd_bf16_ws(const vp_attn_bwd_desc* d, void* workspace, int64_t workspace_bytes, void* stream);
 
 
 /* The other backward passes (row / elementwise / column reductions; the backward's matrix products run on

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--heads", type=int, default=48)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--variants", default="", help="comma-separated VP_ATTN_BWD_VARIANT values, timed interleaved")
+    ap.add_argument("--split-ab", action="store_true", help="grid-tail split (default) vs VP_ATTN_NO_SPLIT=1, interleaved")
     a = ap.parse_args()
     from videopainter_amd import kernels as K
     torch.manual_seed(0)
@@ -42,6 +43,19 @@ def main():
                 res[var].append(round(tl.mean_ms("attention_bwd"), 4))
         K.set_knob("VP_ATTN_BWD_VARIANT", None)
         print(json.dumps({"n": N, "heads": H, "bwd_ms_by_variant": res}))
+        return
+    if a.split_ab:  # interleaved: the backward's grid-tail split against the unsplit grids (5 rounds)
+        res = {"split": [], "whole": []}
+        for _ in range(5):
+            for arm in res:
+                K.set_knob("VP_ATTN_NO_SPLIT", "1" if arm == "whole" else None)
+                K.attention_bwd(q, k, v, o, do, lse, H, dq=dq, dk=dk, dv=dv)
+                with K.timed_launches("attention_bwd") as tl:
+                    for _ in range(a.iters):
+                        K.attention_bwd(q, k, v, o, do, lse, H, dq=dq, dk=dk, dv=dv)
+                res[arm].append(round(tl.mean_ms("attention_bwd"), 4))
+        K.set_knob("VP_ATTN_NO_SPLIT", None)
+        print(json.dumps({"n": N, "heads": H, "bwd_ms": res}))
         return
     with K.timed_launches("attention_bwd", "attention") as tl:
         for _ in range(a.iters):

@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -149,6 +149,8 @@ _SIGS = {
     "vp_nearest_resize3d_bf16": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
     "vp_denormalize_bf16": (i32, [vp, vp, i64, vp]),
     "vp_attention_bwd_bf16": (i32, [C.POINTER(AttnBwdDesc), vp]),
+    "vp_attention_bwd_workspace_bytes": (i64, [C.POINTER(AttnBwdDesc)]),
+    "vp_attention_bwd_bf16_ws": (i32, [C.POINTER(AttnBwdDesc), vp, i64, vp]),
     "vp_transpose_bf16": (i32, [vp, i64, i64, vp, i64, i64, i32, i32, i32, vp]),
     "vp_colsum_bf16": (i32, [vp, i64, vp, i64, i32, i32, i32, i32, vp, vp]),
     "vp_adaln_bwd_bf16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, f32, vp, i64, i32, i32, i32, i32, vp, vp, vp,

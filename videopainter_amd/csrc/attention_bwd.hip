@@ -165,6 +165,25 @@ VP_DEV void store_rowT(bf16* rowp, const f32x16 (&x)[2], int hl, float mul) {
     }
 }
 
+// Grid tail (V = 1): the blocks of the last partial round run as nsplit pieces each over a range of the loop's tiles
+// (keys for dQ, queries for dK / dV), dispatched after the whole blocks in the same launch; each piece leaves its fp32
+// sums in `ws` ([piece][128 rows][64 dQ | 64 dK + 64 dV]) and bwd_tail_reduce_kernel adds them up.  Without it the
+// last round ran 16 of 512 dQ workgroups (training shape: 6 672 blocks) and 528 of 768 dK / dV workgroups alone.
+struct BwdSplit {
+  int main_blocks;  // whole blocks (logical ids 0 .. main_blocks - 1, XCD-remapped); the tail blocks follow
+  int nsplit;       // 1: no tail split
+  float* ws;
+};
+
+// fp32 partial of a transposed accumulator pair in store_rowT's column order, row `row` of a [rows][ld] record
+VP_DEV void store_partT(float* rowp, const f32x16 (&x)[2], int hl) {
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *(f32x4*)(rowp + dh * 32 + 8 * j + 4 * hl) = (f32x4){x[dh][4 * j], x[dh][4 * j + 1], x[dh][4 * j + 2], x[dh][4 * j + 3]};
+}
+
 // ---- D = rowsum(dO * O): one thread per (b, q, h), fp32 ----
 __global__ __launch_bounds__(256) void bwd_delta_kernel(const vp_attn_bwd_desc d) {
   const int64_t total = (int64_t)d.B * d.Nq * d.H;
@@ -192,12 +211,15 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(const vp_attn_bwd_desc d
 #define VP_DQ_WAVES 2  // waves per SIMD the dQ kernel is register-budgeted for (A/B: -DVP_DQ_WAVES=3)
 #endif
 template <int V>
-__global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_attn_bwd_desc d) {
+__global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_attn_bwd_desc d, const BwdSplit sp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nqb = (d.Nq + BW * 32 - 1) / (BW * 32);
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int pj = (int)blockIdx.x - sp.main_blocks;
+  const bool piece = sp.nsplit > 1 && pj >= 0;  // (V = 1 only: V = 0 launches unsplit)
+  const int split = piece ? pj % sp.nsplit : 0;
+  const int t = piece ? sp.main_blocks + pj / sp.nsplit : xcd_remap(blockIdx.x, sp.nsplit > 1 ? sp.main_blocks : gridDim.x);
   const int bh = t / nqb, qb = t - bh * nqb;
   const int b = bh / d.H, h = bh - b * d.H;
   const int q = qb * BW * 32 + wave * 32 + (lane & 31);
@@ -224,6 +246,7 @@ __global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_a
   f32x16 dqt[2] = {zero16(), zero16()};
   const bool active = qb * BW * 32 + wave * 32 < d.Nq;  // wave-uniform
   const int ntiles = (d.Nk + BT - 1) / BT;
+  const int tbeg = piece ? ntiles * split / sp.nsplit : 0, tend = piece ? ntiles * (split + 1) / sp.nsplit : ntiles;
   const TileOffs ko = tile_offs(d.k_sn, wave, lane), vo = tile_offs(d.v_sn, wave, lane);
   auto issue = [&](int ti) {
     char* st = smem + (ti & 1) * STAGE;
@@ -279,7 +302,7 @@ __global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_a
       for (int dh = 0; dh < 2; ++dh)
         dqt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Kt, kh * 2 + j, ta, dh), pf[j], dqt[dh], 0, 0, 0);
   };
-  issue(0);
+  issue(tbeg);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (V == 0) {
@@ -297,8 +320,9 @@ __global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_a
     }
   } else {
     const int nfull = d.Nk / BT;
-    for (int ti = 0; ti < nfull; ++ti) {
-      if (ti + 1 < ntiles) issue(ti + 1);
+    const int fend = min(tend, nfull);
+    for (int ti = tbeg; ti < fend; ++ti) {
+      if (ti + 1 < tend) issue(ti + 1);
       const char* Kt = smem + (ti & 1) * STAGE;
       if (active) {
         half(Kt, Kt + TILE, 0, false, BT);
@@ -307,14 +331,17 @@ __global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_a
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __syncthreads();
     }
-    if (nfull < ntiles && active) {  // the partial last tile (staged by the last loop iteration, or the prologue)
+    if (nfull < tend && active) {  // the partial last tile (staged by the last loop iteration, or the prologue)
       const char* Kt = smem + (nfull & 1) * STAGE;
       const int lim = d.Nk - nfull * BT;
       half(Kt, Kt + TILE, 0, true, lim);
       if (lim > 32) half(Kt, Kt + TILE, 1, true, lim);
     }
   }
-  if (q < d.Nq) store_rowT((bf16*)d.dQ + (int64_t)b * d.dq_sb + (int64_t)q * d.dq_sn + h * 64, dqt, hl, d.scale);
+  if (piece)
+    store_partT(sp.ws + ((int64_t)pj * (BW * 32) + wave * 32 + (lane & 31)) * 64, dqt, hl);
+  else if (q < d.Nq)
+    store_rowT((bf16*)d.dQ + (int64_t)b * d.dq_sb + (int64_t)q * d.dq_sn + h * 64, dqt, hl, d.scale);
 }
 
 // ---- dK, dV: a workgroup per (b, h, 128 keys), 64-query tiles ----
@@ -325,12 +352,15 @@ __global__ __launch_bounds__(BW * 64, VP_DQ_WAVES) void bwd_dq_kernel(const vp_a
 // (round 6, measured and dropped: 2 waves per SIMD, +4-7 %; the four A fragments of a chain read before its first
 // MFMA and kept live together, +14 % — the extra registers spill at 3 waves per SIMD; profiles/r06_attn_bwd_variants_ab.log)
 template <int V>
-__global__ __launch_bounds__(BW * 64, V ? 3 : 2) void bwd_dkdv_kernel(const vp_attn_bwd_desc d) {
+__global__ __launch_bounds__(BW * 64, V ? 3 : 2) void bwd_dkdv_kernel(const vp_attn_bwd_desc d, const BwdSplit sp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nkb = (d.Nk + BW * 32 - 1) / (BW * 32);
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int pj = (int)blockIdx.x - sp.main_blocks;
+  const bool piece = sp.nsplit > 1 && pj >= 0;
+  const int split = piece ? pj % sp.nsplit : 0;
+  const int t = piece ? sp.main_blocks + pj / sp.nsplit : xcd_remap(blockIdx.x, sp.nsplit > 1 ? sp.main_blocks : gridDim.x);
   const int bh = t / nkb, kb = t - bh * nkb;
   const int b = bh / d.H, h = bh - b * d.H;
   const int key = kb * BW * 32 + wave * 32 + (lane & 31);
@@ -362,6 +392,7 @@ __global__ __launch_bounds__(BW * 64, V ? 3 : 2) void bwd_dkdv_kernel(const vp_a
   f32x16 dkt[2] = {zero16(), zero16()}, dvt[2] = {zero16(), zero16()};
   const bool active = kb * BW * 32 + wave * 32 < d.Nk;  // wave-uniform
   const int ntiles = (d.Nq + BT - 1) / BT;
+  const int tbeg = piece ? ntiles * split / sp.nsplit : 0, tend = piece ? ntiles * (split + 1) / sp.nsplit : ntiles;
   // per-query statistics of a tile: thread tid < 64 holds lse, 64 <= tid < 128 D (plain loads, written to LDS after
   // the tile's compute, before the barrier that publishes the stage).  Rows past Nq: lse = +inf, so their S
   // accumulators start at -inf and P = 0 there (no per-score mask); stored negated: they are the C-init of the S / dP
@@ -432,13 +463,13 @@ __global__ __launch_bounds__(BW * 64, V ? 3 : 2) void bwd_dkdv_kernel(const vp_a
         dkt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Qt, qh * 2 + j, ta, dh), pd[j], dkt[dh], 0, 0, 0);
       }
   };
-  issue(0);
-  load_stat(0);
-  put_stat(0);
+  issue(tbeg);
+  load_stat(tbeg);
+  put_stat(tbeg);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int ti = 0; ti < ntiles; ++ti) {
-    if (ti + 1 < ntiles) {
+  for (int ti = tbeg; ti < tend; ++ti) {
+    if (ti + 1 < tend) {
       issue(ti + 1);
       load_stat(ti + 1);
     }
@@ -455,19 +486,68 @@ __global__ __launch_bounds__(BW * 64, V ? 3 : 2) void bwd_dkdv_kernel(const vp_a
       half(Qt, Gt, st, 0);
       half(Qt, Gt, st, 1);
     }
-    if (ti + 1 < ntiles) put_stat(ti + 1);
+    if (ti + 1 < tend) put_stat(ti + 1);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  if (key < d.Nk) {
+  if (piece) {
+    float* rec = sp.ws + ((int64_t)pj * (BW * 32) + wave * 32 + (lane & 31)) * 128;
+    store_partT(rec, dkt, hl);
+    store_partT(rec + 64, dvt, hl);
+  } else if (key < d.Nk) {
     store_rowT((bf16*)d.dK + (int64_t)b * d.dk_sb + (int64_t)key * d.dk_sn + h * 64, dkt, hl, d.scale);
     store_rowT((bf16*)d.dV + (int64_t)b * d.dv_sb + (int64_t)key * d.dv_sn + h * 64, dvt, hl, 1.f);
   }
 }
 
-}  // namespace
+// the tail pieces' sums, 4 columns per thread: dQ (64 columns, scale x sum) or dK | dV (128 columns: scale x sum |
+// sum); rows past the length skipped
+__global__ __launch_bounds__(256) void bwd_tail_reduce_kernel(const vp_attn_bwd_desc d, const BwdSplit sp, int ntail,
+                                                              int kv) {
+  const int cols = kv ? 128 : 64;
+  const int per_row = cols / 4;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = gid / per_row;
+  const int c4 = (int)(gid - row * per_row) * 4;
+  if (row >= (int64_t)ntail * (BW * 32)) return;
+  const int j = (int)(row / (BW * 32)), r = (int)(row - (int64_t)j * (BW * 32));
+  const int t = sp.main_blocks + j;
+  const int nb = ((kv ? d.Nk : d.Nq) + BW * 32 - 1) / (BW * 32);
+  const int bh = t / nb, blk = t - bh * nb;
+  const int b = bh / d.H, h = bh - b * d.H;
+  const int n = blk * BW * 32 + r;
+  if (n >= (kv ? d.Nk : d.Nq)) return;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < sp.nsplit; ++s) {
+    const f32x4 v = *(const f32x4*)(sp.ws + (((int64_t)j * sp.nsplit + s) * (BW * 32) + r) * cols + c4);
+    acc[0] += v[0];
+    acc[1] += v[1];
+    acc[2] += v[2];
+    acc[3] += v[3];
+  }
+  bf16* dst;
+  float mul = d.scale;
+  if (!kv) {
+    dst = (bf16*)d.dQ + (int64_t)b * d.dq_sb + (int64_t)n * d.dq_sn + h * 64 + c4;
+  } else if (c4 < 64) {
+    dst = (bf16*)d.dK + (int64_t)b * d.dk_sb + (int64_t)n * d.dk_sn + h * 64 + c4;
+  } else {
+    dst = (bf16*)d.dV + (int64_t)b * d.dv_sb + (int64_t)n * d.dv_sn + h * 64 + c4 - 64;
+    mul = 1.f;
+  }
+  bf16x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[e] * mul);
+  *(bf16x4*)dst = o;
+}
 
-extern "C" int vp_attention_bwd_bf16(const vp_attn_bwd_desc* d, void* stream) {
+struct BwdPlan {
+  int64_t nq = 0, nk = 0;          // dQ / dK-dV blocks
+  int tq = 0, sq = 1, tk = 0, sk = 1;  // tail blocks and pieces per tail block of each kernel
+  int64_t wq = 0, wk = 0;          // workspace bytes of each
+};
+
+int bwd_check(const vp_attn_bwd_desc* d) {
   if (d == nullptr || !d->Q || !d->K || !d->V || !d->O || !d->dO || !d->lse || !d->delta || !d->dQ || !d->dK ||
       !d->dV)
     return VP_ERR_ARG;
@@ -481,6 +561,77 @@ extern "C" int vp_attention_bwd_bf16(const vp_attn_bwd_desc* d, void* stream) {
   if ((int64_t)BT * d->q_sn * 2 >= ((int64_t)1 << 31) || (int64_t)BT * d->k_sn * 2 >= ((int64_t)1 << 31) ||
       (int64_t)BT * d->v_sn * 2 >= ((int64_t)1 << 31) || (int64_t)BT * d->do_sn * 2 >= ((int64_t)1 << 31))
     return VP_ERR_ARG;
+  return VP_OK;
+}
+
+// the tail split of one kernel: `slots` concurrent workgroups, nblk blocks, ntile loop tiles; the remainder blocks
+// of the last partial round in S = min(8, ceil(2 slots / remainder), ntile) pieces (about two rounds of pieces, the
+// forward's rule) when at least one whole round stays unsplit
+void bwd_tail(int slots, int64_t nblk, int ntile, int& tail, int& S) {
+  tail = 0;
+  S = 1;
+  if (slots <= 0) return;
+  const int rem = (int)(nblk % slots);
+  if (rem == 0 || rem + slots > nblk) return;
+  const int s = min(min(8, (2 * slots + rem - 1) / rem), ntile);
+  if (s < 2) return;
+  tail = rem;
+  S = s;
+}
+
+void bwd_attr() {
+  static bool attr = false;
+  if (attr) return;
+  attr = true;
+  for (const void* f : {(const void*)bwd_dq_kernel<0>, (const void*)bwd_dkdv_kernel<0>, (const void*)bwd_dq_kernel<1>,
+                        (const void*)bwd_dkdv_kernel<1>})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BWD);
+}
+
+BwdPlan bwd_plan(const vp_attn_bwd_desc* d, bool split) {
+  BwdPlan pl;
+  pl.nq = (int64_t)d->B * d->H * ((d->Nq + BW * 32 - 1) / (BW * 32));
+  pl.nk = (int64_t)d->B * d->H * ((d->Nk + BW * 32 - 1) / (BW * 32));
+  const char* ns = vp_knob(VPK_ATTN_NO_SPLIT);
+  if (!split || (ns != nullptr && ns[0] != '0')) return pl;
+  static int slots_q = -1, slots_k = -1;
+  if (slots_q < 0) {
+    bwd_attr();
+    int dev = 0, cus = 0, pq = 0, pk = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pq, (const void*)bwd_dq_kernel<1>, BW * 64, LDS_BWD) != hipSuccess)
+      pq = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pk, (const void*)bwd_dkdv_kernel<1>, BW * 64, LDS_BWD) !=
+        hipSuccess)
+      pk = 0;
+    slots_q = pq * cus;
+    slots_k = pk * cus;
+  }
+  bwd_tail(slots_q, pl.nq, (d->Nk + BT - 1) / BT, pl.tq, pl.sq);
+  bwd_tail(slots_k, pl.nk, (d->Nq + BT - 1) / BT, pl.tk, pl.sk);
+  pl.wq = (int64_t)pl.tq * pl.sq * (BW * 32) * 64 * 4;
+  pl.wk = (int64_t)pl.tk * pl.sk * (BW * 32) * 128 * 4;
+  return pl;
+}
+}  // namespace
+
+extern "C" int64_t vp_attention_bwd_workspace_bytes(const vp_attn_bwd_desc* d) {
+  if (bwd_check(d) != VP_OK) return -1;
+  const char* kv = vp_knob(VPK_ATTN_BWD_VARIANT);
+  if (kv != nullptr && atoi(kv) != 1) return 0;  // the round-2 kernels run unsplit
+  const BwdPlan pl = bwd_plan(d, true);
+  return pl.wq + pl.wk;
+}
+
+extern "C" int vp_attention_bwd_bf16(const vp_attn_bwd_desc* d, void* stream) {
+  return vp_attention_bwd_bf16_ws(d, nullptr, 0, stream);
+}
+
+extern "C" int vp_attention_bwd_bf16_ws(const vp_attn_bwd_desc* d, void* workspace, int64_t workspace_bytes,
+                                        void* stream) {
+  const int rc = bwd_check(d);
+  if (rc != VP_OK) return rc;
   // VP_ATTN_BWD_VARIANT: 1 (default) or 0 (round 2's kernels); A/B only — same arithmetic, same results.  Measured and
   // dropped in round 5 (profiles/r05_attn_bwd_ab.log): variant 1 with the dK / dV kernel at 2 waves per SIMD (+7 %),
   // with dQ at 3 (60 B of scratch, +8 %; with the pair packing 24 B, equal), and an in-wave software pipeline of
@@ -488,26 +639,37 @@ extern "C" int vp_attention_bwd_bf16(const vp_attn_bwd_desc* d, void* stream) {
   const char* kv = vp_knob(VPK_ATTN_BWD_VARIANT);
   const int var = kv ? atoi(kv) : 1;
   if (var != 0 && var != 1) return VP_ERR_UNSUPPORTED;
-  static bool attr = false;
-  if (!attr) {
-    attr = true;
-    for (const void* f : {(const void*)bwd_dq_kernel<0>, (const void*)bwd_dkdv_kernel<0>, (const void*)bwd_dq_kernel<1>,
-                          (const void*)bwd_dkdv_kernel<1>})
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BWD);
-  }
+  bwd_attr();
+  // the tail split needs the workspace (vp_attention_bwd_workspace_bytes) and the default kernels
+  BwdPlan pl = bwd_plan(d, var == 1);
+  if (pl.wq + pl.wk > 0 &&
+      (workspace == nullptr || workspace_bytes < pl.wq + pl.wk || ((uintptr_t)workspace & 15) != 0))
+    pl = bwd_plan(d, false);
+  if (pl.nq > 0x7fffffff || pl.nk > 0x7fffffff) return VP_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nd = (int64_t)d->B * d->Nq * d->H;
   const int64_t gd = (nd + 255) / 256;
   hipLaunchKernelGGL(bwd_delta_kernel, dim3((unsigned)(gd < (1 << 20) ? gd : (1 << 20))), dim3(256), 0, s, *d);
   VP_CHECK_LAUNCH();
-  const int64_t gq = (int64_t)d->B * d->H * ((d->Nq + BW * 32 - 1) / (BW * 32));
-  const int64_t gk = (int64_t)d->B * d->H * ((d->Nk + BW * 32 - 1) / (BW * 32));
-  if (gq > 0x7fffffff || gk > 0x7fffffff) return VP_ERR_ARG;
-  void (*dq)(const vp_attn_bwd_desc) = var ? bwd_dq_kernel<1> : bwd_dq_kernel<0>;
-  hipLaunchKernelGGL(dq, dim3((unsigned)gq), dim3(BW * 64), LDS_BWD, s, *d);
+  // whole blocks first, then the tail pieces, in one grid per kernel; then the pieces' sums
+  const BwdSplit spq = {(int)(pl.nq - pl.tq), pl.sq, (float*)workspace};
+  const BwdSplit spk = {(int)(pl.nk - pl.tk), pl.sk, (float*)((char*)workspace + pl.wq)};
+  void (*dq)(const vp_attn_bwd_desc, const BwdSplit) = var ? bwd_dq_kernel<1> : bwd_dq_kernel<0>;
+  hipLaunchKernelGGL(dq, dim3((unsigned)(pl.nq - pl.tq + (int64_t)pl.tq * pl.sq)), dim3(BW * 64), LDS_BWD, s, *d, spq);
   VP_CHECK_LAUNCH();
-  void (*dkdv)(const vp_attn_bwd_desc) = var ? bwd_dkdv_kernel<1> : bwd_dkdv_kernel<0>;
-  hipLaunchKernelGGL(dkdv, dim3((unsigned)gk), dim3(BW * 64), LDS_BWD, s, *d);
+  void (*dkdv)(const vp_attn_bwd_desc, const BwdSplit) = var ? bwd_dkdv_kernel<1> : bwd_dkdv_kernel<0>;
+  hipLaunchKernelGGL(dkdv, dim3((unsigned)(pl.nk - pl.tk + (int64_t)pl.tk * pl.sk)), dim3(BW * 64), LDS_BWD, s, *d,
+                     spk);
   VP_CHECK_LAUNCH();
+  if (pl.tq > 0) {
+    const int64_t n = (int64_t)pl.tq * (BW * 32) * 16;
+    hipLaunchKernelGGL(bwd_tail_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, *d, spq, pl.tq, 0);
+    VP_CHECK_LAUNCH();
+  }
+  if (pl.tk > 0) {
+    const int64_t n = (int64_t)pl.tk * (BW * 32) * 32;
+    hipLaunchKernelGGL(bwd_tail_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, *d, spk, pl.tk, 1);
+    VP_CHECK_LAUNCH();
+  }
   return VP_OK;
 }

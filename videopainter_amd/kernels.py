@@ -488,8 +488,14 @@ def attention_bwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, o: torch.Te
         setattr(d, f"{name}_sb", t.stride(0))
         setattr(d, f"{name}_sn", t.stride(1))
     d.lse, d.delta, d.scale = _p(lse), _p(delta), scale
+    L = N.lib()
+    nb = L.vp_attention_bwd_workspace_bytes(C.byref(d))
+    if nb < 0:
+        raise ValueError("invalid attention backward descriptor")
+    # the grid-tail pieces' fp32 sums (caching allocator, ordered on the launch stream like the forward's)
+    ws = torch.empty(nb, device=q.device, dtype=torch.uint8) if nb > 0 else None
     ev = _t0("attention_bwd")
-    N.check(N.lib().vp_attention_bwd_bf16(C.byref(d), _stream()), "vp_attention_bwd_bf16")
+    N.check(L.vp_attention_bwd_bf16_ws(C.byref(d), _p(ws), nb, _stream()), "vp_attention_bwd_bf16_ws")
     _t1("attention_bwd", ev)
     return dq, dk, dv
 
