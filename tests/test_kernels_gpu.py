@@ -262,6 +262,52 @@ def test_gemm_tail_split_round(epi, knobs):
     assert rel(out, ref_k) < 1e-3
 
 
+@pytest.mark.parametrize("inject", [True, False], ids=["inject", "noinject"])
+def test_gemm_tail_split_gated_training_shape(inject, knobs):
+    """Tail mode at the training shape's N = 3072 GEMMs (M = 17 776: 70 x 12 = 840 tiles = 3 rounds + 72, a round
+    28 % full — split since round 6, 3 x 1024-K chunks) with the gated residual epilogue (text / video gates of two
+    batches, masked branch injection) applied by the reduce: against the unsplit launch (VP_GEMM_NO_TAIL) and torch
+    fp32, and the old quarter-round rule (VP_GEMM_NO_TAIL=q) leaves this shape unsplit."""
+    from videopainter_amd import kernels as K
+    from videopainter_amd import _native as N
+    import ctypes as C
+    B, T, Nv, D, Kk = 2, 226, 8662, 3072, 3072
+    Ntok = T + Nv
+    M = B * Ntok
+    a = bf(rnd(M, Kk, seed=63)).to(dev)
+    w = bf(rnd(D, Kk, std=Kk ** -0.5, seed=64)).to(dev)
+    b = bf(rnd(D, std=0.1, seed=65)).to(dev)
+    resid = bf(rnd(B, Ntok, D, seed=66)).to(dev)
+    mod = bf(rnd(B, 6 * D, seed=67)).to(dev)
+    kw = dict(epilogue=N.EPI_GATED, resid=resid, mod=mod, tokens_per_batch=Ntok, text_len=T)
+    if inject:
+        inj = bf(rnd(B, Nv, D, seed=68)).to(dev)
+        tm = (torch.rand(B, Nv, generator=torch.Generator().manual_seed(6)) > 0.5).to(torch.uint8).to(dev)
+        kw.update(inject=inj, inject_ld=D, inject_bstride=Nv * D, inject_mask=tm)
+    d = N.GemmDesc()
+    d.M, d.N, d.K, d.epilogue, d.n_seg = M, D, Kk, N.EPI_GATED, D
+    assert N.lib().vp_gemm_bf16_workspace_bytes(C.byref(d)) == 72 * 3 * 256 * 256 * 4  # the tail split is active
+    out = torch.empty(B, Ntok, D, device=dev, dtype=torch.bfloat16)
+    K.gemm(a, [w], [b], out.view(-1, D), **kw)
+    knobs.setenv("VP_GEMM_NO_TAIL", "q")
+    assert N.lib().vp_gemm_bf16_workspace_bytes(C.byref(d)) == 0
+    knobs.setenv("VP_GEMM_NO_TAIL", "1")
+    ref_k = torch.empty_like(out)
+    K.gemm(a, [w], [b], ref_k.view(-1, D), **kw)
+    y = (a.float() @ w.float().T + b.float()).view(B, Ntok, D)
+    gate = mod.float()[:, 2 * D:3 * D][:, None]
+    egate = mod.float()[:, 5 * D:6 * D][:, None]
+    ref = resid.float().clone()
+    ref[:, :T] += egate * y[:, :T]
+    ref[:, T:] += gate * y[:, T:]
+    if inject:
+        ref[:, T:] += inj.float() * (tm[..., None] == 0)
+    assert rel(out, ref) < 5e-3
+    assert rel(out, ref_k) < 1e-3
+    # the main grid's tiles are untouched by the split: every row of the first 3 rounds' tiles is bit-identical
+    assert torch.equal(out.view(-1, D)[:256], ref_k.view(-1, D)[:256])
+
+
 def _sdpa(q, k, v):
     return F.scaled_dot_product_attention(q.float(), k.float(), v.float())
 

@@ -12,6 +12,7 @@
 // address and undone on the read, cdna_hip_programming.md §5.4 rule 21), XCD-aware grouped tile order.
 // Roofline: MFMA-bound (AI = 2*256*256*64 flop / 64 KB staged per k-step).
 #include <stdlib.h>
+#include <string.h>
 
 #include <type_traits>
 
@@ -1080,11 +1081,24 @@ VP_DEV void splitk_epilogue(const vp_gemm_desc& d, int m, int n, const float (&a
   const int grp = m / d.rows_per_group, gin = m - grp * d.rows_per_group;
   const int64_t orow = (int64_t)grp * d.group_stride + d.row_offset + gin;
   bf16x8 o, av;
-  bf16x8 pv;
-  if (d.epilogue == VP_EPI_BIAS_ADDROWS)
+  bf16x8 pv, gv, iv;
+  bool inj = false;
+  if (d.epilogue == VP_EPI_BIAS_ADDROWS) {
     pv = *(const bf16x8*)((const bf16*)d.addrows + (int64_t)(gin + d.addrows_offset) * d.addrows_ld + n);
-  else if (d.epilogue == VP_EPI_GELU_BWD)
+  } else if (d.epilogue == VP_EPI_GELU_BWD) {
     pv = *(const bf16x8*)((const bf16*)d.R + (int64_t)m * d.ldr + n);
+  } else if (d.epilogue == VP_EPI_GATED) {
+    // epi_rows_out's gated row: residual (R, output row), the batch's text / video gate, the optional injection
+    const int b = m / d.tokens_per_batch, tok = m - b * d.tokens_per_batch;
+    gv = *(const bf16x8*)((const bf16*)(tok < d.text_len ? d.gate_text : d.gate) + (int64_t)b * d.gate_bstride + n);
+    pv = *(const bf16x8*)((const bf16*)d.R + orow * d.ldr + n);
+    if (d.inject != nullptr && tok >= d.text_len) {
+      const int vtok = tok - d.text_len;
+      inj = d.inject_mask == nullptr || d.inject_mask[(int64_t)b * d.inject_mask_bstride + vtok] == 0;
+      if (inj)
+        iv = *(const bf16x8*)((const bf16*)d.inject + (int64_t)b * d.inject_bstride + (int64_t)vtok * d.inject_ld + n);
+    }
+  }
   const bf16x8 b8 = bp != nullptr ? *(const bf16x8*)(bp + n - sg * d.n_seg) : bf16x8{};
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -1094,6 +1108,10 @@ VP_DEV void splitk_epilogue(const vp_gemm_desc& d, int m, int n, const float (&a
     else if (d.epilogue == VP_EPI_BIAS_SCALE) v = rbf(v * d.alpha);
     else if (d.epilogue == VP_EPI_BIAS_ADDROWS) v = bf2f(f2bf(v)) + bf2f(pv[e]);
     else if (d.epilogue == VP_EPI_GELU_BWD) v = rbf(v * gelu_grad(bf2f(pv[e])));
+    else if (d.epilogue == VP_EPI_GATED) {
+      v = rbf(bf2f(pv[e]) + rbf(bf2f(gv[e]) * v));
+      if (inj) v = rbf(v + bf2f(iv[e]));
+    }
     o[e] = f2bf(v);
   }
   if (d.epilogue == VP_EPI_BIAS_GELU && d.aux != nullptr) *(bf16x8*)((bf16*)d.aux + (int64_t)m * d.ld_aux + n) = av;
@@ -1125,10 +1143,14 @@ int device_cus() {
 SplitPlan tail_plan(const vp_gemm_desc* d, int tiles) {
   SplitPlan p;
   const char* e = vp_knob(VPK_GEMM_VARIANT);
-  if ((e != nullptr && atoi(e) != 13) || vp_knob(VPK_GEMM_NO_TAIL) != nullptr) return p;
+  const char* nt = vp_knob(VPK_GEMM_NO_TAIL);
+  if ((e != nullptr && atoi(e) != 13) || (nt != nullptr && strcmp(nt, "q") != 0)) return p;
   const int cus = device_cus();
   const int tail = tiles % cus;
-  if (tiles <= cus || tail == 0 || 4 * tail > cus) return p;
+  // up to half a round (the pieces then fit one round: tail x nsplit <= CUs).  Round 6 widened it from a quarter
+  // (VP_GEMM_NO_TAIL=q keeps that rule, A/B): the training shape's N = 3072 GEMMs (M = 17 776: 840 tiles = 3 rounds
+  // + 72) and the gated epilogue in the reduce
+  if (tiles <= cus || tail == 0 || (nt != nullptr ? 4 : 2) * tail > cus) return p;
   if ((d->N % BN) != 0 || (d->K % BK) != 0) return p;
   const int nk = d->K / BK;
   const int ns = min(cus / tail, nk / 8);
@@ -1146,7 +1168,7 @@ SplitPlan split_plan(const vp_gemm_desc* d) {
   const int tiles = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
   const bool epi_ok = d->epilogue == VP_EPI_BIAS || d->epilogue == VP_EPI_BIAS_GELU ||
                       d->epilogue == VP_EPI_BIAS_SCALE || d->epilogue == VP_EPI_BIAS_ADDROWS ||
-                      d->epilogue == VP_EPI_GELU_BWD;
+                      d->epilogue == VP_EPI_GELU_BWD || d->epilogue == VP_EPI_GATED;
   if (!epi_ok || (d->K % BK) != 0 || d->a_tail_k > 0) return p;
   const int64_t tile_a0 = (int64_t)BM * d->lda * 2, wseg0 = (int64_t)d->n_seg * d->K * 2;
   if (tiles >= 128) return (tile_a0 < ((int64_t)1 << 31) && wseg0 < ((int64_t)1 << 31)) ? tail_plan(d, tiles) : p;
