@@ -815,10 +815,10 @@ def test_attention_tail_split_matches_unsplit(Nq, Nk2, knobs):
         assert rel(out_s, ref) < 1e-2 and rel(out_u, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tail", ["default", "0:8", "1:4", "2:2"])
 @pytest.mark.parametrize("mode", ["p2a", "p2"])
-@pytest.mark.parametrize("Nq,Nk2,H", [(8000, 700, 17), (17776, 0, 48)])
-def test_attention_one_launch_tail_matches_unsplit(Nq, Nk2, H, mode, tail, knobs):
+@pytest.mark.parametrize("Nq,Nk2,H,tail", [(8000, 700, 17, "default"), (8000, 700, 17, "0:8"), (8000, 700, 17, "1:4"),
+                                           (17776, 0, 48, "default"), (17776, 0, 48, "1:4"), (17776, 0, 48, "2:2")])
+def test_attention_one_launch_tail_matches_unsplit(Nq, Nk2, H, tail, mode, knobs):
     """VP_ATTN_TAIL = "R:S": the remainder blocks plus R whole rounds run as S key-range pieces each at the END of the
     main grid (one launch, then the merge pass) — against the unsplit launch; the l_extra / k2_len path through the
     pieces as well (the merge adds the null-key mass once)."""
@@ -846,8 +846,7 @@ def test_attention_one_launch_tail_matches_unsplit(Nq, Nk2, H, mode, tail, knobs
     nblk = B * H * ((Nq + 255) // 256)
     # default: R = 0, S = min(8, ceil(2 slots / remainder))
     R, S = (0, min(8, -(-1024 // (nblk % 512)))) if tail == "default" else (int(x) for x in tail.split(":"))
-    if nblk % 512 + (R + 1) * 512 > nblk:
-        pytest.skip("the plan keeps at least one whole round unsplit")
+    assert nblk % 512 + (R + 1) * 512 <= nblk  # (the plan keeps at least one whole round unsplit)
     ws = N.lib().vp_attention_workspace_bytes(C.byref(d))
     assert ws >= (nblk % 512 + R * 512) * S * 256 * 66 * 4  # the one-launch split is active for this shape
     out_s = torch.empty(B, Nq, D, device=dev, dtype=torch.bfloat16)
