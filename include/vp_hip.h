@@ -33,7 +33,7 @@ const char* vp_build_digest(void);
 /* A/B switches of the library (kernel-variant selection only, never numerics of the default path; DESIGN_LOG.md §5):
  * VP_GEMM_VARIANT, VP_GEMM_NO_TAIL, VP_GEMM_GROUP, VP_GEMM8_VARIANT, VP_ATTN_BOUNDED_MODE, VP_ATTN_UNBOUNDED_MODE,
  * VP_ATTN_NO_SPLIT, VP_ATTN8_VARIANT, VP_T5_ATTN, VP_CONV_HOIST, VP_CONV_PIPE,
- * VP_ATTN_BWD_VARIANT, VP_ATTN_TAIL.  Each is read from the environment
+ * VP_ATTN_BWD_VARIANT, VP_ATTN_TAIL, VP_ATTN_PERSIST.  Each is read from the environment
  * once, when the library is loaded; afterwards only vp_set_knob changes it (value NULL = unset), e.g. a test that
  * runs two variants on the same operands.  Returns VP_ERR_ARG for an unknown name or a value over 31 bytes.  Host
  * only; not thread-safe against launches in flight on other host threads.  (ABI 14.) */

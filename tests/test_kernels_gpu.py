@@ -815,13 +815,16 @@ def test_attention_tail_split_matches_unsplit(Nq, Nk2, knobs):
         assert rel(out_s, ref) < 1e-2 and rel(out_u, ref) < 1e-2
 
 
+@pytest.mark.parametrize("persist", ["1", "0"], ids=["persistent", "grid"])
 @pytest.mark.parametrize("mode", ["p2a", "p2"])
 @pytest.mark.parametrize("Nq,Nk2,H,tail", [(8000, 700, 17, "default"), (8000, 700, 17, "0:8"), (8000, 700, 17, "1:4"),
                                            (17776, 0, 48, "default"), (17776, 0, 48, "1:4"), (17776, 0, 48, "2:2")])
-def test_attention_one_launch_tail_matches_unsplit(Nq, Nk2, H, tail, mode, knobs):
+def test_attention_one_launch_tail_matches_unsplit(Nq, Nk2, H, tail, mode, persist, knobs):
     """VP_ATTN_TAIL = "R:S": the remainder blocks plus R whole rounds run as S key-range pieces each at the END of the
     main grid (one launch, then the merge pass) — against the unsplit launch; the l_extra / k2_len path through the
-    pieces as well (the merge adds the null-key mass once)."""
+    pieces as well (the merge adds the null-key mass once).  persistent: the default p2 / p2a instance that takes the
+    blocks and then the pieces by ticket (VP_ATTN_PERSIST); grid: one workgroup per block or piece."""
+    knobs.setenv("VP_ATTN_PERSIST", persist)
     from videopainter_amd import kernels as K
     from videopainter_amd import _native as N
     import ctypes as C
@@ -852,9 +855,35 @@ def test_attention_one_launch_tail_matches_unsplit(Nq, Nk2, H, tail, mode, knobs
     out_s = torch.empty(B, Nq, D, device=dev, dtype=torch.bfloat16)
     K.attention(q, k, v, out_s, H, **kw)
     knobs.setenv("VP_ATTN_NO_SPLIT", "1")
+    knobs.setenv("VP_ATTN_PERSIST", "0")
     out_u = torch.empty_like(out_s)
     K.attention(q, k, v, out_u, H, **kw)
     assert rel(out_s, out_u) < 5e-3
+
+
+@pytest.mark.parametrize("mode", ["p2a", "p2"])
+@pytest.mark.parametrize("B,Nq,H", [(2, 17776, 48), (1, 17776, 48), (2, 4100, 33)])
+def test_attention_persistent_bit_identical_without_tail(B, Nq, H, mode, knobs):
+    """The persistent p2 / p2a instance (blocks by per-XCD tickets, then stolen across XCDs) computes every block
+    exactly as its own workgroup would: without the tail split the outputs and the softmax statistics are
+    bit-identical to one workgroup per block, whatever order the tickets came in."""
+    from videopainter_amd import kernels as K
+    need_variant(mode, knobs)
+    D = H * 64
+    sc = 0.5 if mode == "p2" else 1.0
+    q, k, v = (bf(rnd(B, Nq, D, seed=s) * sc).to(dev) for s in (96, 97, 98))
+    knobs.setenv("VP_ATTN_BOUNDED_MODE" if mode == "p2" else "VP_ATTN_UNBOUNDED_MODE", mode)
+    knobs.setenv("VP_ATTN_NO_SPLIT", "1")
+    outs, lses = [], []
+    for persist in ("1", "0"):
+        knobs.setenv("VP_ATTN_PERSIST", persist)
+        o = torch.empty(B, Nq, D, device=dev, dtype=torch.bfloat16)
+        lse = torch.empty(B, H, Nq, device=dev, dtype=torch.float32)
+        K.attention(q, k, v, o, H, bounded_scores=mode == "p2", lse=lse)
+        outs.append(o)
+        lses.append(lse)
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(lses[0], lses[1])
 
 
 @pytest.mark.parametrize("mode", ["p2", "s16"])

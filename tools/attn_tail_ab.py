@@ -2,6 +2,7 @@
 process, random data; median and min per setting over the rounds.
 
     python tools/attn_tail_ab.py --tails legacy,0:8,1:4,2:2 [--batch 2] [--rounds 5] [--iters 20]
+    python tools/attn_tail_ab.py --tails p1,p0       # VP_ATTN_PERSIST 1 / 0 (default tail)
 "legacy" = the two-launch remainder split (main grid, then the remainder's key-range pieces); "R:S" = one launch
 whose last workgroups are S key-range pieces of each remainder block and of R whole rounds before them.
 """
@@ -37,11 +38,17 @@ def main():
     res = {t: [] for t in arms}
     for r in range(a.rounds):
         for t in arms:
-            K.set_knob("VP_ATTN_TAIL", None if t == "legacy" else t)
+            if t in ("p1", "p0"):
+                K.set_knob("VP_ATTN_TAIL", None)
+                K.set_knob("VP_ATTN_PERSIST", t[1])
+            else:
+                K.set_knob("VP_ATTN_PERSIST", None)
+                K.set_knob("VP_ATTN_TAIL", None if t == "legacy" else t)
             ms = timeit(lambda: K.attention(q, k, v, o, H, bounded_scores=not a.unbounded), a.iters) * 1e3
             res[t].append(ms)
             print(f"round {r} {t}: {ms:.3f} ms {fl / ms / 1e9:.0f} TF/s", flush=True)
     K.set_knob("VP_ATTN_TAIL", None)
+    K.set_knob("VP_ATTN_PERSIST", None)
     summ = {t: {"median_ms": statistics.median(v), "min_ms": min(v),
                 "median_tflops": fl / (statistics.median(v) / 1e3) / 1e12} for t, v in res.items()}
     for t, s in summ.items():

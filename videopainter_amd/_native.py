@@ -175,7 +175,7 @@ DIAG_SIGS = {
 # the library's A/B knobs (vp_set_knob): read from the environment once at load; knob_values mirrors them
 KNOBS = ("VP_GEMM_VARIANT", "VP_GEMM_NO_TAIL", "VP_GEMM_GROUP", "VP_GEMM8_VARIANT", "VP_ATTN_BOUNDED_MODE",
          "VP_ATTN_UNBOUNDED_MODE", "VP_ATTN_NO_SPLIT", "VP_ATTN8_VARIANT", "VP_T5_ATTN", "VP_CONV_HOIST", "VP_CONV_PIPE",
-         "VP_ATTN_BWD_VARIANT", "VP_ATTN_TAIL")
+         "VP_ATTN_BWD_VARIANT", "VP_ATTN_TAIL", "VP_ATTN_PERSIST")
 knob_values: dict = {}
 
 _lib = None

@@ -66,15 +66,20 @@ static_assert(NP % NW == 0, "pieces per wave");
 #if VP_CLOCK_STAMPS
 constexpr int CLOCK_SLOTS = 1 << 15;
 __device__ unsigned long long vp_clock_buf[CLOCK_SLOTS * 4];
+#ifndef VP_CLOCK_WG
+#define VP_CLOCK_WG 0  // 1 (p2 / p2a): realtime at workgroup entry, loop start, loop end, exit instead
+#endif
 struct ClockStamp {
-  unsigned long long t0, r0;
+  unsigned long long t0, r0, e0 = 0, r1 = 0;
+  __device__ __forceinline__ void entry() { e0 = __builtin_amdgcn_s_memrealtime(); }
   __device__ __forceinline__ void start() {
     t0 = __builtin_amdgcn_s_memtime();
     r0 = __builtin_amdgcn_s_memrealtime();
   }
   __device__ __forceinline__ void stop(int tid) {
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0 && blockIdx.x < CLOCK_SLOTS) {  // one lane, plain vector stores
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    r1 = __builtin_amdgcn_s_memrealtime();
+    if (!VP_CLOCK_WG && tid == 0 && blockIdx.x < CLOCK_SLOTS) {  // one lane, plain vector stores
       unsigned long long* p = vp_clock_buf + (size_t)blockIdx.x * 4;
       p[0] = t0;
       p[1] = r0;
@@ -82,11 +87,22 @@ struct ClockStamp {
       p[3] = r1;
     }
   }
+  __device__ __forceinline__ void exit(int tid) {
+    if (VP_CLOCK_WG && tid == 0 && blockIdx.x < CLOCK_SLOTS) {
+      unsigned long long* p = vp_clock_buf + (size_t)blockIdx.x * 4;
+      p[0] = e0;
+      p[1] = r0;
+      p[2] = r1;
+      p[3] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 };
 #else
 struct ClockStamp {
+  __device__ __forceinline__ void entry() {}
   __device__ __forceinline__ void start() {}
   __device__ __forceinline__ void stop(int) {}
+  __device__ __forceinline__ void exit(int) {}
 };
 #endif
 
@@ -163,7 +179,9 @@ VP_DEV void glds16_lds(const char* sbase, int voff, unsigned la) {
 
 VP_DEV void glds16(const char* sbase, int voff, char* lds) {
   // (the LDS address is wave-uniform; readfirstlane keeps it an SGPR where the compiler loses track of that)
-  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)lds);
+  // (the low 32 bits of a generic LDS address are the LDS offset: no address-space cast, whose null check the
+  // compiler mis-selects inside the persistent p2a loop)
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds);
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(la), "v"(voff), "s"(sbase)
                : "memory", "m0");
 }
@@ -218,7 +236,34 @@ struct AttnSplit {
   // one-launch tail (p2 / p2a): workgroups blockIdx < main_blocks run whole blocks (XCD-remapped over main_blocks),
   // the rest are the key-range pieces of blocks t_base + (blockIdx - main_blocks) / nsplit, dispatched last
   int main_blocks;
+  // persistent launch (p2 / p2a; NULL: one workgroup per block): 9 zeroed counters — the whole blocks of XCD x's
+  // xcd_remap range are handed out by tickets[x], to that XCD's workgroups first and then to any XCD's that ran out;
+  // then the npieces tail pieces by tickets[8]
+  int* tickets;
+  int npieces;
 };
+
+// the next work item of a persistent p2 / p2a workgroup on XCD x: a whole block (logical id < main_blocks), a tail
+// piece (main_blocks + piece index) or -1.  The dispatcher gives every XCD the same number of workgroups while the
+// XCDs run at different clocks (per-XCD loop time 419-464 us at config 2, tools/attn_wg_timeline.py): with one
+// workgroup per block the slowest XCD finished its static share 5 % after the mean.
+VP_DEV int p1_ticket(const AttnSplit& sp, int x) {
+  const int M = sp.main_blocks, q = M >> 3, r = M & 7;
+#pragma unroll 1
+  for (int k = 0; k < 8; ++k) {
+    const int y = (x + k) & 7;
+    const int size = q + (y < r ? 1 : 0);
+    const int lo = y < r ? y * (q + 1) : r * (q + 1) + (y - r) * q;
+    if (__hip_atomic_load(sp.tickets + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= size) continue;
+    const int c = __hip_atomic_fetch_add(sp.tickets + y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c < size) return lo + c;
+  }
+  if (sp.npieces > 0 && __hip_atomic_load(sp.tickets + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sp.npieces) {
+    const int c = __hip_atomic_fetch_add(sp.tickets + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c < sp.npieces) return M + c;
+  }
+  return -1;
+}
 
 // is block t flagged by its p2a workgroup(s)?
 VP_DEV bool block_flagged(const AttnSplit& sp, int t, int Nq) {
@@ -564,27 +609,21 @@ VP_DEV void p1_tile(P1Regs& r, const bf16x8& sel, const char* Kl, const char* Kn
 // (tools/attn_clock.py ablation, DESIGN_LOG.md §3.R5) — and the L2 -> LDS bytes per FLOP halve.
 // TPB = 2 (p2w only): one barrier per two tiles — tiles t + 2 and t + 3 issued together at the top of every even tile
 // of the range, both waited for and published by the barrier at the seam of the odd tile before them.
-template <bool TAIL = false, bool ANCH = false, int NWV = 4, int TPB = 1>
-__global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const vp_attn_desc d, const AttnSplit sp) {
-  static_assert(NWV == 4 || NWV == 8, "4-wave (p2 / p2a) or 8-wave (p2w) workgroups");
-  static_assert(TPB == 1 || NWV == 8, "one barrier per two tiles needs the 4-slot ring");
+// one block (logical id t; a key-range piece `split` of it when `piece`) of attn_fwd_p1
+template <bool TAIL, bool ANCH, int NWV, int TPB>
+VP_DEV __attribute__((always_inline)) void p1_block(const vp_attn_desc& d, const AttnSplit& sp, const int t,
+                                                    const bool piece, const int split, ClockStamp& ck) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int QBV = NWV * 64;               // queries per workgroup
   constexpr int PPWV = NP / NWV;              // DMA pieces per operand, wave and tile
   constexpr int RING = NWV == 8 ? 4 : 2;      // LDS ring slots
   constexpr int AHEAD = RING / 2;             // tiles issued ahead
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hl = lane >> 5;
 
   const int nqb = (d.Nq + QBV - 1) / QBV;
-  // a key-range piece of a tail block (the TAIL instance of a two-launch tail, or blockIdx >= main_blocks of a
-  // one-launch tail), or a whole block
-  const int pj = (int)blockIdx.x - sp.main_blocks;
-  const bool piece = sp.nsplit > 1 && pj >= 0;
-  const int split = piece ? pj % sp.nsplit : 0;
-  const int t = piece ? sp.t_base + pj / sp.nsplit : xcd_remap(blockIdx.x, sp.nsplit > 1 ? sp.main_blocks : gridDim.x);
   const int bh = t / nqb;
   const int qb = t - bh * nqb;
   const int b = bh / d.H;
@@ -637,7 +676,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
   const int full2 = seg2fast ? n2 / KB : 0;
   const char* kseg2 = seg2fast ? (const char*)((const bf16*)d.K2 + (int64_t)b * d.k2_sb + h * 64) : nullptr;
   const char* vseg2 = seg2fast ? (const char*)((const bf16*)d.V2 + (int64_t)b * d.v2_sb + h * 64) : nullptr;
-  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem) + wave * 1024;
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)smem) + wave * 1024;
   auto issue = [&](int ti) {
     const bool s1 = ti < full1;
     if (s1 || (ti >= tiles1 && ti - tiles1 < full2)) {
@@ -746,7 +785,6 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
     }
   }
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // S -> the first (asm) exp
-  ClockStamp ck;
   ck.start();
   for (int ti = tbeg; ti < tend; ++ti) {
     bool sync = true;
@@ -829,6 +867,43 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
       store_out(d, r.o[qi], l_tot[qi], q, b, h, hl, false, r.anc);
     }
   }
+}
+
+// PERS: the persistent instance (p2 / p2a; AttnSplit.tickets)
+template <bool TAIL = false, bool ANCH = false, int NWV = 4, int TPB = 1, bool PERS = false>
+__global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const vp_attn_desc d, const AttnSplit sp) {
+  static_assert(NWV == 4 || NWV == 8, "4-wave (p2 / p2a) or 8-wave (p2w) workgroups");
+  static_assert(TPB == 1 || NWV == 8, "one barrier per two tiles needs the 4-slot ring");
+  static_assert(!PERS || (!TAIL && NWV == 4), "persistent: p2 / p2a main instances");
+  ClockStamp ck;
+  ck.entry();
+  if constexpr (!PERS) {
+    // a key-range piece of a tail block (the TAIL instance of a two-launch tail, or blockIdx >= main_blocks of a
+    // one-launch tail), or a whole block
+    const int pj = (int)blockIdx.x - sp.main_blocks;
+    const bool piece = sp.nsplit > 1 && pj >= 0;
+    const int split = piece ? pj % sp.nsplit : 0;
+    const int t = piece ? sp.t_base + pj / sp.nsplit : xcd_remap(blockIdx.x, sp.nsplit > 1 ? sp.main_blocks : gridDim.x);
+    p1_block<TAIL, ANCH, NWV, TPB>(d, sp, t, piece, split, ck);
+  } else {
+    // persistent (p2 / p2a): work items by ticket until none is left; the two barriers around the broadcast also
+    // retire every wave's reads of the ring and the flag words before the next item's DMA and flags
+    __shared__ int tk[1];
+    const int x = (int)(blockIdx.x & 7);  // the dispatcher's XCD of this workgroup
+#pragma unroll 1
+    for (;;) {
+      if (threadIdx.x == 0) tk[0] = p1_ticket(sp, x);
+      __syncthreads();
+      const int c = tk[0];
+      __syncthreads();
+      if (c < 0) break;
+      const bool piece = c >= sp.main_blocks;
+      const int pj = c - sp.main_blocks;
+      p1_block<TAIL, ANCH, NWV, TPB>(d, sp, piece ? sp.t_base + pj / sp.nsplit : c, piece, piece ? pj % sp.nsplit : 0,
+                                     ck);
+    }
+  }
+  ck.exit(threadIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -2309,13 +2384,16 @@ struct AttnVar {
   int threads;
   int lds;  // dynamic LDS bytes
   int qb = QB;  // queries per workgroup
+  const void* fn_pers = nullptr;  // the persistent instance (p2 / p2a)
 };
 enum { V_S16, V_A16, V_P2, V_P2A, V_P2W, V_P2W2, V_P2S, V_NVAR };
 static const AttnVar attn_vars[] = {
     {"s16", (const void*)attn_fwd_s16<false>, (const void*)attn_fwd_s16<true>, NW4 * 64, LDS_BYTES},
     {"a16", (const void*)attn_fwd_s16<false, true>, (const void*)attn_fwd_s16<true, true>, NW4 * 64, LDS_BYTES},
-    {"p2", (const void*)attn_fwd_p1<false>, (const void*)attn_fwd_p1<true>, NW4 * 64, 2 * ST},
-    {"p2a", (const void*)attn_fwd_p1<false, true>, (const void*)attn_fwd_p1<true, true>, NW4 * 64, 2 * ST + 16},
+    {"p2", (const void*)attn_fwd_p1<false>, (const void*)attn_fwd_p1<true>, NW4 * 64, 2 * ST + 32, QB,
+     (const void*)attn_fwd_p1<false, false, 4, 1, true>},
+    {"p2a", (const void*)attn_fwd_p1<false, true>, (const void*)attn_fwd_p1<true, true>, NW4 * 64, 2 * ST + 32, QB,
+     (const void*)attn_fwd_p1<false, true, 4, 1, true>},
     // p2a in 8-wave workgroups of 512 queries on a 4-slot ring (attn_fwd_p1 NWV = 8)
     {"p2w", (const void*)attn_fwd_p1<false, true, 8>, (const void*)attn_fwd_p1<true, true, 8>, 8 * 64, 4 * ST + 32,
      512},
@@ -2335,6 +2413,9 @@ struct AttnPlan {
   int64_t nblk;
   int ntail = 0, nsplit = 1;  // tail split: the last ntail blocks as ntail * nsplit key-range workgroups
   bool one_launch = false;    // the pieces ride at the end of the main grid (p2 / p2a) instead of a launch after it
+  bool persist = false;       // p2 / p2a persistent instance: grid_pers workgroups take blocks and pieces by ticket
+  int grid_pers = 0;
+  int64_t tk_off = 0;         // the 9 ticket counters (zeroed per launch) in the workspace
   int64_t ws_bytes = 0;       // tail partials, then (p2a) the redo flags
   int64_t part_bytes = 0;     // the tail partials' part of it
 };
@@ -2365,6 +2446,7 @@ int variant_by_name(const char* e) {
 int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   static bool attr_set = false;
   static int slots_v[V_NVAR] = {};  // resident workgroups chip-wide per variant
+  static int slots_p[V_NVAR] = {};  // the same for the persistent instances
   if (!attr_set) {
     attr_set = true;
     int dev = 0, cus = 0;
@@ -2379,6 +2461,13 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
           hipSuccess)
         per_cu = 0;
       slots_v[i] = per_cu * cus;
+      if (attn_vars[i].fn_pers != nullptr) {
+        (void)hipFuncSetAttribute(attn_vars[i].fn_pers, hipFuncAttributeMaxDynamicSharedMemorySize, attn_vars[i].lds);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, attn_vars[i].fn_pers, attn_vars[i].threads,
+                                                         attn_vars[i].lds) != hipSuccess)
+          per_cu = 0;
+        slots_p[i] = per_cu * cus;
+      }
     }
   }
   // p2a for every launch: the p2 pipeline (the software-pipelined p1 steps at two workgroups per CU, 6.04 vs 6.49 ms
@@ -2444,6 +2533,18 @@ int attn_plan(const vp_attn_desc* d, AttnPlan& pl) {
   }
   pl.ws_bytes = pl.part_bytes;
   if (anchored_var(pl.var)) pl.ws_bytes += ((pl.nblk - pl.ntail) + (int64_t)pl.ntail * pl.nsplit) * 4;
+  // persistent p2 / p2a (VP_ATTN_PERSIST=0: one workgroup per block): XCD-balanced by tickets, for grids of at least
+  // two rounds (with the remainder's pieces, if split, handed out last)
+  const char* pk = vp_knob(VPK_ATTN_PERSIST);
+  const int sp_ = slots_p[pl.var];
+  if (pl.v->fn_pers != nullptr && sp_ > 0 && (pk == nullptr || pk[0] != '0') && (pl.ntail == 0 || pl.one_launch) &&
+      pl.nblk >= 2 * (int64_t)sp_) {
+    pl.persist = true;
+    const int64_t items = pl.nblk - pl.ntail + (int64_t)pl.ntail * pl.nsplit;
+    pl.grid_pers = (int)min((int64_t)sp_, items);
+    pl.tk_off = (pl.ws_bytes + 15) & ~(int64_t)15;
+    pl.ws_bytes = pl.tk_off + 64;
+  }
   return VP_OK;
 }
 }  // namespace
@@ -2479,13 +2580,26 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
     pl.v = &attn_vars[V_A16];
     pl.ntail = 0;
     pl.nsplit = 1;
+    pl.persist = false;
   }
   const AttnVar& v = *pl.v;
   const bool split = pl.ntail > 0 && have_ws;
   const int64_t main_blocks = split ? pl.nblk - pl.ntail : pl.nblk;
   int* flags = anchored_var(pl.var) ? (int*)((char*)workspace + pl.part_bytes) : nullptr;
   hipError_t le = hipSuccess;
-  if (split && pl.one_launch) {
+  if (pl.persist && have_ws) {
+    // persistent: grid_pers workgroups take the whole blocks (each XCD its xcd_remap range, then the others') and
+    // then the pieces by ticket
+    int* tickets = (int*)((char*)workspace + pl.tk_off);
+    le = hipMemsetAsync(tickets, 0, 64, (hipStream_t)stream);
+    if (le != hipSuccess) return (int)le;
+    const AttnSplit sp = {(int)main_blocks, split ? pl.nsplit : 1, (float*)workspace, flags, (int)main_blocks,
+                          split ? pl.nsplit : 1, 0, 0, (int)main_blocks, tickets,
+                          split ? pl.ntail * pl.nsplit : 0};
+    void* args[] = {(void*)d, (void*)&sp};
+    le = hipLaunchKernel(v.fn_pers, dim3((unsigned)pl.grid_pers), dim3(v.threads), args, v.lds, (hipStream_t)stream);
+    if (le != hipSuccess) return (int)le;
+  } else if (split && pl.one_launch) {
     // whole blocks first, then the pieces: one grid, dispatched in blockIdx order
     const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace, flags, (int)main_blocks, pl.nsplit, 0, 0,
                           (int)main_blocks};
@@ -2500,7 +2614,7 @@ extern "C" int vp_attention_fwd_bf16_ws(const vp_attn_desc* d, void* workspace, 
     if (le != hipSuccess) return (int)le;
   }
   if (split) {
-    if (!pl.one_launch) {
+    if (!pl.one_launch && !(pl.persist && have_ws)) {
       const AttnSplit sp = {(int)main_blocks, pl.nsplit, (float*)workspace, flags, (int)main_blocks, pl.nsplit, 0};
       void* args[] = {(void*)d, (void*)&sp};
       le = hipLaunchKernel(v.fn_tail, dim3((unsigned)(pl.ntail * pl.nsplit)), dim3(v.threads), args, v.lds,

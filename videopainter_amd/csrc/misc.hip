@@ -247,7 +247,8 @@ const char* const knob_names[VPK_COUNT] = {"VP_GEMM_VARIANT",        "VP_GEMM_NO
                                            "VP_GEMM8_VARIANT",       "VP_ATTN_BOUNDED_MODE",
                                            "VP_ATTN_UNBOUNDED_MODE", "VP_ATTN_NO_SPLIT",  "VP_ATTN8_VARIANT",
                                            "VP_T5_ATTN",             "VP_CONV_HOIST",     "VP_CONV_PIPE",
-                                           "VP_ATTN_BWD_VARIANT",    "VP_ATTN_TAIL"};
+                                           "VP_ATTN_BWD_VARIANT",    "VP_ATTN_TAIL",
+                                           "VP_ATTN_PERSIST"};
 struct KnobTable {
   char val[VPK_COUNT][32];
   bool set[VPK_COUNT];

@@ -240,6 +240,7 @@ enum VpKnob {
   VPK_CONV_PIPE,
   VPK_ATTN_BWD_VARIANT,
   VPK_ATTN_TAIL,
+  VPK_ATTN_PERSIST,
   VPK_COUNT
 };
 const char* vp_knob(int k);
