@@ -286,11 +286,13 @@ def test_gemm_tail_split_gated_training_shape(inject, knobs):
         kw.update(inject=inj, inject_ld=D, inject_bstride=Nv * D, inject_mask=tm)
     d = N.GemmDesc()
     d.M, d.N, d.K, d.epilogue, d.n_seg = M, D, Kk, N.EPI_GATED, D
-    assert N.lib().vp_gemm_bf16_workspace_bytes(C.byref(d)) == 72 * 3 * 256 * 256 * 4  # the tail split is active
+    part = 72 * 3 * 256 * 256 * 4
+    # the tail split is active (+ the persistent launch's ticket counters, if any)
+    assert part <= N.lib().vp_gemm_bf16_workspace_bytes(C.byref(d)) <= part + 64
     out = torch.empty(B, Ntok, D, device=dev, dtype=torch.bfloat16)
     K.gemm(a, [w], [b], out.view(-1, D), **kw)
     knobs.setenv("VP_GEMM_NO_TAIL", "q")
-    assert N.lib().vp_gemm_bf16_workspace_bytes(C.byref(d)) == 0
+    assert N.lib().vp_gemm_bf16_workspace_bytes(C.byref(d)) <= 64
     knobs.setenv("VP_GEMM_NO_TAIL", "1")
     ref_k = torch.empty_like(out)
     K.gemm(a, [w], [b], ref_k.view(-1, D), **kw)

@@ -248,19 +248,11 @@ struct AttnSplit {
 // XCDs run at different clocks (per-XCD loop time 419-464 us at config 2, tools/attn_wg_timeline.py): with one
 // workgroup per block the slowest XCD finished its static share 5 % after the mean.
 VP_DEV int p1_ticket(const AttnSplit& sp, int x) {
-  const int M = sp.main_blocks, q = M >> 3, r = M & 7;
-#pragma unroll 1
-  for (int k = 0; k < 8; ++k) {
-    const int y = (x + k) & 7;
-    const int size = q + (y < r ? 1 : 0);
-    const int lo = y < r ? y * (q + 1) : r * (q + 1) + (y - r) * q;
-    if (__hip_atomic_load(sp.tickets + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= size) continue;
-    const int c = __hip_atomic_fetch_add(sp.tickets + y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c < size) return lo + c;
-  }
+  const int c = xcd_ticket(sp.tickets, sp.main_blocks, x);
+  if (c >= 0) return c;
   if (sp.npieces > 0 && __hip_atomic_load(sp.tickets + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sp.npieces) {
-    const int c = __hip_atomic_fetch_add(sp.tickets + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c < sp.npieces) return M + c;
+    const int c2 = __hip_atomic_fetch_add(sp.tickets + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c2 < sp.npieces) return sp.main_blocks + c2;
   }
   return -1;
 }

@@ -172,6 +172,24 @@ VP_DEV int xcd_remap(int wg, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// persistent launches (p2 / p2a attention): the next of n work items for a workgroup on XCD x (-1: none left).  Item ranges are
+// xcd_remap's (XCD y owns a contiguous range, counted by tickets[y]); an XCD whose range is done takes from the
+// others'.  tickets: 8 ints, zero at launch.  (The dispatcher hands each XCD the same number of workgroups while the
+// XCDs run at different clocks: per-XCD attention loop times 419-464 us at config 2, tools/attn_wg_timeline.py.)
+VP_DEV int xcd_ticket(int* tickets, int n, int x) {
+  const int q = n >> 3, r = n & 7;
+#pragma unroll 1
+  for (int k = 0; k < 8; ++k) {
+    const int y = (x + k) & 7;
+    const int size = q + (y < r ? 1 : 0);
+    const int lo = y < r ? y * (q + 1) : r * (q + 1) + (y - r) * q;
+    if (__hip_atomic_load(tickets + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= size) continue;
+    const int c = __hip_atomic_fetch_add(tickets + y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c < size) return lo + c;
+  }
+  return -1;
+}
+
 // ---- MX-FP8 (e4m3 + E8M0 per 32 elements; layout and rounding rule in include/vp_hip.h) ----
 // byte offset of the scale of (row r, K-block kb) in an MX scale array of a tensor with K columns
 VP_DEV int64_t mx_scale_off(int64_t r, int kb, int K) {
