@@ -26,7 +26,7 @@ extern "C" {
 #define VP_ERR_UNSUPPORTED 1001
 
 /* ABI version: bump when any struct layout or signature below changes. */
-#define VP_ABI_VERSION 19
+#define VP_ABI_VERSION 20
 int vp_abi_version(void);
 /* "<sha256 of sources + flags>:<sha256 of the compiler version>" of the build (no reference counterpart) */
 const char* vp_build_digest(void);
@@ -265,6 +265,11 @@ typedef struct vp_attn_fp8_desc {
 } vp_attn_fp8_desc;
 
 int vp_attention_fwd_fp8(const vp_attn_fp8_desc* d, void* stream);
+/* The same with a workspace (ABI 20): the default kernel runs persistent — resident workgroups take the query blocks
+ * by per-XCD ticket — when vp_attention_fp8_workspace_bytes (0: none needed, -1: invalid) bytes are given; a smaller
+ * or NULL workspace runs one workgroup per block (same results, bit for bit). */
+int64_t vp_attention_fp8_workspace_bytes(const vp_attn_fp8_desc* d);
+int vp_attention_fwd_fp8_ws(const vp_attn_fp8_desc* d, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* V [B, N, H*64] bf16 (row stride v_sn, batch stride v_sb, elements) -> V^T e4m3 [B, H, 64, npad] with the keys of
  * every 64-key tile in MFMA K-slot order, plus one E8M0 scale per (d, 32 keys) (MX rule of vp_mx_quantize_bf16).

@@ -210,6 +210,32 @@ def test_attention_fp8_skewed_bit_identical(N, var, knobs):
     assert torch.equal(outs["3"].view(torch.int16), outs[var].view(torch.int16))
 
 
+@pytest.mark.parametrize("B,H,N", [(1, 24, 12000), (2, 9, 15000)])
+def test_attention_fp8_persistent_bit_identical(B, H, N, knobs):
+    """The persistent default fp8 kernel (query blocks by per-XCD ticket, ABI 20 workspace) against one workgroup per
+    block (VP_ATTN_PERSIST=0): every block's arithmetic is the same whoever runs it — equal bit for bit."""
+    from videopainter_amd import kernels as K
+    from videopainter_amd import _native as N_
+    import ctypes as C
+    q, k, v = _attn_case(B, H, N, 4000 + N, late_spike=True)
+    q_exp, k_exp = 5, 4
+    q8 = e4m3(q.float() * 0.125 * K.LOG2E * 2.0 ** q_exp).to(dev)
+    k8 = e4m3(k.float() * 2.0 ** k_exp).to(dev)
+    vp = K.v_pack_fp8(v.to(dev), H)
+    dd = N_.AttnFp8Desc()
+    dd.base.B, dd.base.H, dd.base.Nq = B, H, N
+    assert N_.lib().vp_attention_fp8_workspace_bytes(C.byref(dd)) > 0  # the persistent path is taken
+    outs = []
+    for persist in ("1", "0"):
+        knobs.setenv("VP_ATTN_PERSIST", persist)
+        o = torch.empty(B, N, H * 64, device=dev, dtype=torch.bfloat16)
+        K.attention_fp8(q8, k8, vp, o, H, q_exp, k_exp)
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+
+
 def _ln_rows(x, H):
     """Per-head LayerNorm(64) without affine: the |x| = 8 rows CogVideoX's qk-norm produces."""
     B, N, _ = x.shape

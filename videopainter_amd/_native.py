@@ -11,7 +11,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VP_HIP_LIB", os.path.join(_HERE, "_lib", "libvp_hip.so"))
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -105,6 +105,8 @@ _SIGS = {
     "vp_adaln_modulate_mx_fp8": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, f32, vp, i64, vp]),
     "vp_attention_fwd_bf16": (i32, [C.POINTER(AttnDesc), vp]),
     "vp_attention_fwd_fp8": (i32, [C.POINTER(AttnFp8Desc), vp]),
+    "vp_attention_fp8_workspace_bytes": (i64, [C.POINTER(AttnFp8Desc)]),
+    "vp_attention_fwd_fp8_ws": (i32, [C.POINTER(AttnFp8Desc), vp, i64, vp]),
     "vp_attention_workspace_bytes": (i64, [C.POINTER(AttnDesc)]),
     "vp_attention_fwd_bf16_ws": (i32, [C.POINTER(AttnDesc), vp, i64, vp]),
     "vp_attention_variant_built": (i32, [C.c_char_p]),

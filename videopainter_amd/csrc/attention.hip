@@ -2136,8 +2136,9 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_fp8(const vp_attn_fp8_d
 constexpr int F8S_SLOTS = 3;
 typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
 typedef __attribute__((address_space(3))) const unsigned short lds_u16;
+// one 256-query block (logical id t) of attn_fwd_fp8s
 template <int SUB>
-__global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc dd) {
+VP_DEV __attribute__((always_inline)) void fp8s_block(const vp_attn_fp8_desc& dd, const int t) {
   constexpr int NW = 8;
   constexpr int OFF = 7;
   constexpr float THR = 1.5f;
@@ -2153,7 +2154,6 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc d
   const int g = lane >> 5;
 
   const int nqb = (d.Nq + QB - 1) / QB;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int bh = t / nqb;
   const int qb = t - bh * nqb;
   const int b = bh / d.H;
@@ -2187,7 +2187,8 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc d
   const int64_t tstride = kw ? (int64_t)64 * ksn : 64;
   const int nfull = kw ? d.Nk >> 6 : ntiles;  // tiles whose rows all lie below Nk
   const char* vsbase = (const char*)dd.vs + (int64_t)bh * ntiles * 128;
-  const unsigned lds_smem = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_t*)smem);
+  // (the low 32 bits of a generic LDS address are the LDS offset: no address-space cast inside the persistent loop)
+  const unsigned lds_smem = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)smem);
   const unsigned lds_w = lds_smem + (kw ? wave * 1024 : F8_TILE + (wave - 4) * 1024);
   const int nsup = (ntiles + SUB - 1) / SUB;
   auto issue = [&](int ti, int slot) {
@@ -2360,6 +2361,29 @@ __global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc d
   const int qq = lane & 31;
   const float v0 = __shfl(lsum[0], qq & 15, 64), v1 = __shfl(lsum[1], qq & 15, 64);
   store_out(d, o, qq < 16 ? v0 : v1, q, b, h, g, false);
+}
+
+// PERS: persistent (tickets: 8 zeroed counters) — resident workgroups take the blocks by per-XCD ticket (xcd_ticket):
+// the XCDs run at different clocks
+template <int SUB, bool PERS = false>
+__global__ __launch_bounds__(512, 4) void attn_fwd_fp8s(const vp_attn_fp8_desc dd, int* tickets) {
+  if constexpr (!PERS) {
+    fp8s_block<SUB>(dd, xcd_remap(blockIdx.x, gridDim.x));
+  } else {
+    __shared__ int tk[1];
+    const int n = dd.base.B * dd.base.H * ((dd.base.Nq + 255) / 256);
+    const int x = (int)(blockIdx.x & 7);  // the dispatcher's XCD of this workgroup
+#pragma unroll 1
+    for (;;) {
+      // (the two barriers also retire every wave's reads of the previous block's ring before the next DMA)
+      if (threadIdx.x == 0) tk[0] = xcd_ticket(tickets, n, x);
+      __syncthreads();
+      const int c = tk[0];
+      __syncthreads();
+      if (c < 0) break;
+      fp8s_block<SUB>(dd, c);
+    }
+  }
 }
 
 }  // namespace
@@ -2675,8 +2699,46 @@ extern "C" int vp_v_pack_fp8(const void* V, int64_t v_sb, int64_t v_sn, int32_t 
   return VP_OK;
 }
 
+namespace {
+// resident workgroups of the persistent fp8 kernel chip-wide (0: none)
+int fp8_pers_slots() {
+  static int slots = -1;
+  if (slots < 0) {
+    (void)hipFuncSetAttribute((const void*)attn_fwd_fp8s<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              F8S_SLOTS * 2 * F8_STAGE);
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)attn_fwd_fp8s<2, true>, 512,
+                                                     F8S_SLOTS * 2 * F8_STAGE) != hipSuccess)
+      per_cu = 0;
+    slots = per_cu * cus;
+  }
+  return slots;
+}
+}  // namespace
+
+// the persistent default kernel's ticket counters (VP_ATTN_PERSIST=0 or VP_ATTN8_VARIANT != 5: none)
+extern "C" int64_t vp_attention_fp8_workspace_bytes(const vp_attn_fp8_desc* dd) {
+  if (dd == nullptr) return -1;
+  const char* e = vp_knob(VPK_ATTN8_VARIANT);
+  const char* pk = vp_knob(VPK_ATTN_PERSIST);
+  if ((e != nullptr && atoi(e) != 5 && atoi(e) >= 1 && atoi(e) <= 5) || (pk != nullptr && pk[0] == '0')) return 0;
+  const int slots = fp8_pers_slots();
+  const int64_t grid = (int64_t)dd->base.B * dd->base.H * ((dd->base.Nq + 255) / 256);
+  return slots > 0 && grid >= 2 * (int64_t)slots ? 64 : 0;
+}
+
 extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
+  return vp_attention_fwd_fp8_ws(dd, nullptr, 0, stream);
+}
+
+extern "C" int vp_attention_fwd_fp8_ws(const vp_attn_fp8_desc* dd, void* ws, int64_t ws_bytes, void* stream) {
   if (dd == nullptr) return VP_ERR_ARG;
+  int* workspace = ws != nullptr && ws_bytes >= 64 && ((uintptr_t)ws & 15) == 0 &&
+                           vp_attention_fp8_workspace_bytes(dd) > 0
+                       ? (int*)ws
+                       : nullptr;
   const vp_attn_desc& d = dd->base;
   if (!d.Q || !d.K || !d.V || !d.O || !dd->vs) return VP_ERR_ARG;
   if (d.head_dim != 64 || d.Nk2 != 0) return VP_ERR_UNSUPPORTED;
@@ -2709,6 +2771,8 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
         (void)hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, 2 * 2 * F8_STAGE);
     (void)hipFuncSetAttribute((const void*)attn_fwd_fp8s<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               F8S_SLOTS * 2 * F8_STAGE);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_fp8s<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              F8S_SLOTS * 2 * F8_STAGE);
   }
   const char* e = vp_knob(VPK_ATTN8_VARIANT);
   int variant = e != nullptr ? atoi(e) : 0;
@@ -2718,7 +2782,21 @@ extern "C" int vp_attention_fwd_fp8(const vp_attn_fp8_desc* dd, void* stream) {
     const int nqb5 = (d.Nq + NW * 32 - 1) / (NW * 32);
     const int64_t grid5 = (int64_t)d.B * d.H * nqb5;
     if (grid5 > 0x7fffffff) return VP_ERR_ARG;
-    void* args5[] = {(void*)dd};
+    const int slots = fp8_pers_slots();
+    int* tickets = workspace;
+    if (tickets != nullptr && slots > 0 && grid5 >= 2 * (int64_t)slots) {
+      // persistent (vp_attention_fp8_workspace_bytes > 0)
+      hipError_t le = hipMemsetAsync(tickets, 0, 32, (hipStream_t)stream);
+      if (le != hipSuccess) return (int)le;
+      void* args5[] = {(void*)dd, (void*)&tickets};
+      le = hipLaunchKernel((const void*)attn_fwd_fp8s<sub, true>, dim3((unsigned)slots), dim3(NW * 64), args5,
+                           F8S_SLOTS * sub * F8_STAGE, (hipStream_t)stream);
+      if (le != hipSuccess) return (int)le;
+      VP_CHECK_LAUNCH();
+      return VP_OK;
+    }
+    int* none = nullptr;
+    void* args5[] = {(void*)dd, (void*)&none};
     const hipError_t le5 =
         hipLaunchKernel((const void*)attn_fwd_fp8s<sub>, dim3((unsigned)grid5),
                         dim3(NW * 64), args5, F8S_SLOTS * sub * F8_STAGE, (hipStream_t)stream);

@@ -602,8 +602,12 @@ def attention_fp8(q8: torch.Tensor, k8: torch.Tensor, vp: VPacked, out: torch.Te
     d.scale, d.out_scale, d.accumulate = 1.0, out_scale, int(accumulate)
     dd.vs, dd.npad = _p(vp.vs), vp.npad
     dd.qk_scale = (127 - q_exp) | ((127 - k_exp) << 8)
+    L = N.lib()
+    nb = L.vp_attention_fp8_workspace_bytes(C.byref(dd))
+    # the persistent kernel's ticket counters (caching allocator, ordered on the launch stream)
+    ws = torch.empty(nb, device=q8.device, dtype=torch.uint8) if nb > 0 else None
     ev = _t0("attention_fp8")
-    N.check(N.lib().vp_attention_fwd_fp8(C.byref(dd), _stream()), "vp_attention_fwd_fp8")
+    N.check(L.vp_attention_fwd_fp8_ws(C.byref(dd), _p(ws), nb, _stream()), "vp_attention_fwd_fp8_ws")
     _t1("attention_fp8", ev)
     return out
 
