@@ -573,9 +573,31 @@ VP_DEV void gemm_epilogue(const vp_gemm_desc& d, const MxExt& mx, const f32x4 (&
 // SPLIT: the split-K instance (fp32 partial tiles to mx.ws, the epilogue runs in gemm_splitk_reduce_kernel)
 // ATAIL: the per-segment A tail of vp_gemm_desc (unfused LoRA): A K-tiles from a_tail_k on are read a_tail_off[seg]
 // columns further right (one scalar add per A DMA of those tiles)
+#ifndef VP_CLOCK_STAMPS
+#define VP_CLOCK_STAMPS 0
+#endif
+#if VP_CLOCK_STAMPS
+// diagnostic builds only (tools/gemm_wg_timeline.py): realtime at workgroup entry and exit per blockIdx
+constexpr int GEMM_CLOCK_SLOTS = 1 << 15;
+__device__ unsigned long long vp_gemm_clock_buf[GEMM_CLOCK_SLOTS * 2];
+struct GemmStamp {
+  unsigned long long e0;
+  __device__ __forceinline__ GemmStamp() : e0(__builtin_amdgcn_s_memrealtime()) {}
+  __device__ __forceinline__ ~GemmStamp() {
+    if (threadIdx.x == 0 && blockIdx.x < GEMM_CLOCK_SLOTS) {
+      vp_gemm_clock_buf[blockIdx.x * 2] = e0;
+      vp_gemm_clock_buf[blockIdx.x * 2 + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+};
+#else
+struct GemmStamp {};
+#endif
+
 template <int VAR, bool FP8 = false, int GROUP = 4, int EPI = -1, bool SPLIT = false, bool ATAIL = false>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_bf16_kernel(const vp_gemm_desc d, const MxExt mx) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  [[maybe_unused]] GemmStamp stamp;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1188,6 +1210,13 @@ SplitPlan split_plan(const vp_gemm_desc* d) {
 }
 
 }  // namespace
+
+#if VP_CLOCK_STAMPS
+extern "C" int vp_diag_gemm_clock_read(void* host, int64_t slots) {
+  if (host == nullptr || slots <= 0 || slots > GEMM_CLOCK_SLOTS) return VP_ERR_ARG;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vp_gemm_clock_buf), (size_t)slots * 16, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 extern "C" int vp_gemm_variant_built(int variant) {
   if (variant == 1 || variant == 5 || variant == 11 || variant == 13) return 1;
