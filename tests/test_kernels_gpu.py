@@ -424,6 +424,73 @@ def test_attention_anchored_late_jump(jump, mode, knobs):
     assert torch.isfinite(out.float()).all() and r < 1e-2
 
 
+def test_attention_persistent_flagged_blocks_and_streams(knobs):
+    """The persistent p2a launch (1 152 blocks: tickets, then the tail pieces) with blocks whose late scores overflow
+    exp2 in a tile (flagged, stored nothing, re-run by a16): bit-identical to one workgroup per block, finite, the
+    spiked heads against fp64 attention; and two launches on two streams at once, each with its own workspace,
+    match the serial result."""
+    from videopainter_amd import kernels as K
+    B, H, Nn = 1, 48, 6000
+    g = torch.Generator().manual_seed(7)
+    q = torch.randn(B, Nn, H, 64, generator=g) * 0.3
+    k = torch.randn(B, Nn, H, 64, generator=g) * 0.3
+    v = torch.randn(B, Nn, H, 64, generator=g)
+    u = torch.randn(64, generator=g)
+    u = u / u.norm()
+    for hh in (3, 40):  # two heads get a late key 200 log2 units above every earlier score for the even queries
+        q[0, ::2, hh] += 4.0 * u
+        k[0, 5000, hh] = u * (200.0 / (0.5 * 1.4426950408889634))
+    q, k, v = (bf(x.reshape(B, Nn, H * 64)).to(dev) for x in (q, k, v))
+    outs = []
+    for persist in ("1", "0"):
+        knobs.setenv("VP_ATTN_PERSIST", persist)
+        o = torch.empty(B, Nn, H * 64, device=dev, dtype=torch.bfloat16)
+        K.attention(q, k, v, o, H)
+        outs.append(o)
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1])
+    for hh in (3, 40):
+        sl = slice(hh * 64, (hh + 1) * 64)
+        qh, kh, vh = (x[0, :, sl].double() for x in (q, k, v))
+        ref = torch.softmax((qh @ kh.T) * 0.125, -1) @ vh
+        assert rel(outs[0][0, :, sl], ref) < 1e-2
+    knobs.setenv("VP_ATTN_PERSIST", "1")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    o1, o2 = torch.empty_like(outs[0]), torch.empty_like(outs[0])
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        K.attention(q, k, v, o1, H)
+    with torch.cuda.stream(s2):
+        K.attention(q, k, v, o2, H)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, outs[0]) and torch.equal(o2, outs[0])
+
+
+@pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "a16"])
+@pytest.mark.parametrize("Nn,pos", [(1500, 1300), (3000, 2900), (6000, 5000)])
+def test_attention_anchored_late_jump_whole_blocks(Nn, pos, mode, knobs):
+    """test_attention_anchored_late_jump's overflow case (a late key 200 log2 units above every earlier score for the
+    even queries) on WHOLE blocks (VP_ATTN_NO_SPLIT: no tail pieces): the anchored kernels must flag the block (its
+    O turns NaN: inf P against V of both signs) so a16 re-runs it — this file's -fno-honor-nans had folded the NaN
+    half of the test away and p2a stored NaN rows.  Against fp64 attention."""
+    from videopainter_amd import kernels as K
+    need_variant(mode, knobs)
+    knobs.setenv("VP_ATTN_NO_SPLIT", "1")
+    g = torch.Generator().manual_seed(200)
+    q = torch.randn(1, Nn, 64, generator=g) * 0.3
+    k = torch.randn(1, Nn, 64, generator=g) * 0.3
+    v = torch.randn(1, Nn, 64, generator=g)
+    u = torch.randn(64, generator=g)
+    u = u / u.norm()
+    q[:, ::2] += 4.0 * u
+    k[0, pos] = u * (200.0 / (0.5 * 1.4426950408889634))
+    q, k, v = bf(q), bf(k), bf(v)
+    out = torch.full((1, Nn, 64), 7.0, device=dev, dtype=torch.bfloat16)
+    K.attention(q.to(dev), k.to(dev), v.to(dev), out, 1)
+    assert torch.isfinite(out.float()).all()
+    assert rel(out, _ref64(q, k, v, 1)) < 1e-2
+
+
 @pytest.mark.parametrize("mode", ["p2a", "p2w", "p2w2", "p2s", "a16"])
 def test_attention_stepwise_max_growth(mode, knobs):
     """Running max grows by 0 / 0.5 / 3 / 8 nats at tile seams, so the deferred-max test (tile sum > 2^8) takes both

@@ -110,8 +110,15 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 VP_DEV int swz(int row) { return (row >> 1) & 7; }
 
-// inf / NaN by the exponent bits (this file builds with -fno-honor-nans: float compares may assume no NaN)
-VP_DEV bool nonfinite(float x) { return (__float_as_uint(x) & 0x7f800000u) == 0x7f800000u; }
+// inf / NaN by the exponent bits.  This file builds with -fno-honor-nans, under which the compiler may fold any NaN
+// class test of a float to false — the bit test included (it recognises it as one): the empty asm makes the bits
+// opaque.  (Without it p2a stored NaN rows of an overflowing block instead of flagging it for the a16 redo: the
+// NaN half of the test had been folded away; tests/test_kernels_gpu.py::test_attention_anchored_late_jump_whole_blocks.)
+VP_DEV bool nonfinite(float x) {
+  uint32_t u = __float_as_uint(x);
+  asm volatile("" : "+v"(u));
+  return (u & 0x7f800000u) == 0x7f800000u;
+}
 
 struct Seg {
   const bf16* k;
@@ -194,7 +201,7 @@ VP_DEV void store_out(const vp_attn_desc& d, const f32x16 (&o)[2], float l_run, 
   const float inv = 1.f / l_tot;
   if (q >= d.Nq) return;
   // softmax statistics for the backward (both lanes of a pair hold the same query, m and l: one writes)
-  if (d.lse != nullptr && hl == 0 && !__builtin_isnan(m_lse))
+  if (d.lse != nullptr && hl == 0 && !nonfinite(m_lse))  // (NaN: no statistics from this kernel; an opaque test, see nonfinite)
     d.lse[((int64_t)b * d.H + h) * d.Nq + q] = m_lse + __log2f(l_tot);
   bf16* orow = (bf16*)d.O + (int64_t)b * d.o_sb + (int64_t)q * d.o_sn + h * 64;
 #pragma unroll
