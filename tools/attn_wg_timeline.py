@@ -24,11 +24,15 @@ def main():
     ap.add_argument("--batch", type=int, default=2)
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--tail", default="", help="VP_ATTN_TAIL value (default: the library default)")
+    ap.add_argument("--items", action="store_true",
+                    help="per work item of the persistent launch (the -DVP_CLOCK_WG=2 build, libvp_hip_clkitem.so)")
     a = ap.parse_args()
     if a.build:
         from videopainter_amd.build import build
         build(out=os.path.join(ROOT, "videopainter_amd", "_lib", "libvp_hip_clkwg.so"),
               extra_flags={"attention.hip": ["-DVP_CLOCK_STAMPS=1", "-DVP_CLOCK_WG=1"]})
+        build(out=os.path.join(ROOT, "videopainter_amd", "_lib", "libvp_hip_clkitem.so"),
+              extra_flags={"attention.hip": ["-DVP_CLOCK_STAMPS=1", "-DVP_CLOCK_WG=2"]})
         return
     import numpy as np
     import torch
@@ -62,6 +66,33 @@ def main():
     n = 32768
     buf = (C.c_uint64 * (4 * n))()
     N.check(L.vp_diag_clock_read(buf, n), "vp_diag_clock_read")
+    if a.items:
+        raw = np.frombuffer(buf, dtype=np.uint64).reshape(n, 4)
+        wgs = (raw[:, 0] >> np.uint64(48)).astype(np.int64)
+        st = (raw[:, 0] & np.uint64((1 << 48) - 1)).astype(np.float64)
+        r0, r1, ex = (raw[:, i].astype(np.float64) for i in (1, 2, 3))
+        ok = st > 0
+        last = ex[ok].max()
+        ok &= st > last - wall * 100 * 1.5
+        st, r0, r1, ex, wgs = st[ok], r0[ok], r1[ok], ex[ok], wgs[ok]
+        t0 = st.min()
+        pro, loop, epi = (r0 - st) / 100, (r1 - r0) / 100, (ex - r1) / 100
+        gaps = []
+        for w in np.unique(wgs):
+            m = wgs == w
+            o = np.argsort(st[m])
+            s_, e_ = st[m][o], ex[m][o]
+            gaps += list((s_[1:] - e_[:-1]) / 100)
+        gaps = np.array(gaps)
+        pc = lambda v: [round(float(np.percentile(v, p)), 2) for p in (10, 50, 90)]  # noqa: E731
+        slots = len(np.unique(wgs))
+        print(json.dumps(dict(items=int(ok.sum()), workgroups=slots, wall_us=round(wall, 1),
+                              span_us=round(float(ex.max() - t0) / 100, 1),
+                              loop_over_span=round(float(loop.sum()) / (slots * float(ex.max() - t0) / 100), 4),
+                              prologue_us=pc(pro), loop_us=pc(loop), epilogue_us=pc(epi), gap_us=pc(gaps),
+                              mean_us=dict(prologue=round(float(pro.mean()), 2), epilogue=round(float(epi.mean()), 2),
+                                           gap=round(float(gaps.mean()), 2), loop=round(float(loop.mean()), 1)))))
+        return
     x = np.frombuffer(buf, dtype=np.uint64).reshape(n, 4).astype(np.float64)
     wid = np.arange(n)
     keep = x[:, 0] > 0

@@ -63,12 +63,12 @@ static_assert(NP % NW == 0, "pieces per wave");
 #ifndef VP_P1_ABL
 #define VP_P1_ABL 0
 #endif
+#ifndef VP_CLOCK_WG
+#define VP_CLOCK_WG 0  // 1 (p2 / p2a): realtime at workgroup entry, loop start, loop end, exit instead; 2: per work item
+#endif
 #if VP_CLOCK_STAMPS
 constexpr int CLOCK_SLOTS = 1 << 15;
 __device__ unsigned long long vp_clock_buf[CLOCK_SLOTS * 4];
-#ifndef VP_CLOCK_WG
-#define VP_CLOCK_WG 0  // 1 (p2 / p2a): realtime at workgroup entry, loop start, loop end, exit instead
-#endif
 struct ClockStamp {
   unsigned long long t0, r0, e0 = 0, r1 = 0;
   __device__ __forceinline__ void entry() { e0 = __builtin_amdgcn_s_memrealtime(); }
@@ -88,9 +88,20 @@ struct ClockStamp {
     }
   }
   __device__ __forceinline__ void exit(int tid) {
-    if (VP_CLOCK_WG && tid == 0 && blockIdx.x < CLOCK_SLOTS) {
+    if (VP_CLOCK_WG == 1 && tid == 0 && blockIdx.x < CLOCK_SLOTS) {
       unsigned long long* p = vp_clock_buf + (size_t)blockIdx.x * 4;
       p[0] = e0;
+      p[1] = r0;
+      p[2] = r1;
+      p[3] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  // VP_CLOCK_WG = 2 (persistent p2 / p2a): one record per work item (its ticket value), the workgroup id in the top
+  // 16 bits of the entry stamp
+  __device__ __forceinline__ void item(int tid, int slot) {
+    if (VP_CLOCK_WG == 2 && tid == 0 && slot >= 0 && slot < CLOCK_SLOTS) {
+      unsigned long long* p = vp_clock_buf + (size_t)slot * 4;
+      p[0] = e0 | ((unsigned long long)blockIdx.x << 48);
       p[1] = r0;
       p[2] = r1;
       p[3] = __builtin_amdgcn_s_memrealtime();
@@ -103,6 +114,7 @@ struct ClockStamp {
   __device__ __forceinline__ void start() {}
   __device__ __forceinline__ void stop(int) {}
   __device__ __forceinline__ void exit(int) {}
+  __device__ __forceinline__ void item(int, int) {}
 };
 #endif
 
@@ -898,8 +910,10 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 1 : 2) void attn_fwd_p1(const 
       if (c < 0) break;
       const bool piece = c >= sp.main_blocks;
       const int pj = c - sp.main_blocks;
+      if (VP_CLOCK_WG == 2) ck.entry();
       p1_block<TAIL, ANCH, NWV, TPB>(d, sp, piece ? sp.t_base + pj / sp.nsplit : c, piece, piece ? pj % sp.nsplit : 0,
                                      ck);
+      ck.item(threadIdx.x, c);
     }
   }
   ck.exit(threadIdx.x);
