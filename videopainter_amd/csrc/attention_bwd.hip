@@ -83,6 +83,17 @@ VP_DEV void stage_tile_fast(const bf16* base, int64_t ld, int row0, int nrows, c
   }
 }
 
+#ifndef VP_DKDV_OPQ
+#define VP_DKDV_OPQ 1  // A/B: 0 = the dK / dV tile body on the kernel-wide lane offsets (spilled, round 6 before)
+#endif
+// the lane id from v_mbcnt in volatile asm: values derived from it are recomputed where they are used instead of being
+// kept live (and spilled) across a loop
+VP_DEV int lane_id_opaque() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // A-operand rows (ds_read_b128) of a 32-row half of a swizzled tile: chunk (2c + hl) ^ swz(row) = dims 16c + 8hl
 template <int V>
 VP_DEV void read_rows(const char* tile, int half, int lane, bf16x8 (&f)[4]) {
@@ -428,11 +439,15 @@ __global__ __launch_bounds__(BW * 64, V ? 3 : 2) void bwd_dkdv_kernel(const vp_a
   };
   auto half = [&](const char* Qt, const char* Gt, const float* st, int qh) {
     // S and dP accumulators start at -lse / -D of their query rows (C-init from the staged, negated statistics): P =
-    // exp2(S), dS = P * dP, one exp and one multiply per score
+    // exp2(S), dS = P * dP, one exp and one multiply per score.  (V = 1: the lane's LDS offsets are recomputed here
+    // from an opaque lane id; kept live across the tile loop they were spilled at this kernel's 168-register budget,
+    // and each reload's vmcnt(0) also waited for the next tile's DMA.)
+    const int ln = V && VP_DKDV_OPQ ? lane_id_opaque() : lane;
+    const int hlq = ln >> 5;
     f32x16 s, dp;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int r0 = qh * 32 + 8 * j + 4 * hl;
+      const int r0 = qh * 32 + 8 * j + 4 * hlq;
       const f32x4 l4 = *(const f32x4*)(st + r0), d4 = *(const f32x4*)(st + BT + r0);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -441,10 +456,10 @@ __global__ __launch_bounds__(BW * 64, V ? 3 : 2) void bwd_dkdv_kernel(const vp_a
       }
     }
     bf16x8 a[4];
-    read_rows<V>(Qt, qh, lane, a);
+    read_rows<V>(Qt, qh, ln, a);
 #pragma unroll
     for (int ds = 0; ds < 4; ++ds) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], kf[ds], s, 0, 0, 0);
-    read_rows<V>(Gt, qh, lane, a);
+    read_rows<V>(Gt, qh, ln, a);
 #pragma unroll
     for (int ds = 0; ds < 4; ++ds) dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ds], vf[ds], dp, 0, 0, 0);
     bf16x8 pp[2], pd[2];
