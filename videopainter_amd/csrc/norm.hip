@@ -215,12 +215,16 @@ __global__ __launch_bounds__(ROW_THREADS) void final_norm_kernel(const bf16* __r
 
 // ---- per-head LN(64) + RoPE (attention_processor.py:2143-2154; embeddings.py:655-701) ----
 // 4 lanes per 64-wide head vector, 16 elements each in the MFMA-accumulator column order of ln64_rope16 (lane g
-// holds columns 16 j + 4 g + r: four 8-byte pieces), 64 vectors per 256-thread block — the arithmetic of the QKV
-// GEMM's fused epilogue.  FP8: the bf16 value the bf16 kernel writes, times out_mul, as e4m3 (strides then in bytes)
-template <bool FP8>
+// holds columns 16 j + 4 g + r: four 8-byte pieces) — the arithmetic of the QKV GEMM's fused epilogue.  Each 4-lane
+// group takes HPG heads of one token (h = hg + k H / HPG: at step k the groups of a token read consecutive heads):
+// the LayerNorm affine and the token's cos / sin quads, the same for every head, are loaded once per group, and the
+// HPG vectors' loads are in flight together (one vector per group: 16 of the 20 loads were the shared operands, and
+// one HBM load chain per thread left the stream at 3 TB/s).  64 groups per 256-thread block.  FP8: the bf16 value
+// the bf16 kernel writes, times out_mul, as e4m3 (strides then in bytes)
+template <bool FP8, int HPG>
 __global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restrict__ xin, int64_t ld_in,
                                                             int64_t bs_in, void* __restrict__ xout, int64_t ld_out,
-                                                            int64_t bs_out, int64_t nvec, int Ntok, int H,
+                                                            int64_t bs_out, int64_t ngroups, int Ntok, int H,
                                                             int text_len, const bf16* __restrict__ lw,
                                                             const bf16* __restrict__ lb, float eps,
                                                             const float* __restrict__ cosp,
@@ -228,53 +232,94 @@ __global__ __launch_bounds__(256) void head_norm_rope_kernel(const bf16* __restr
                                                             const uint8_t* __restrict__ tok_mask, int64_t mask_bs,
                                                             float pre_scale, float out_mul,
                                                             const int32_t* __restrict__ dst_rows) {
-  const int64_t vec = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+  const int64_t grp = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
   const int g = threadIdx.x & 3;
-  const bool valid = vec < nvec;
-  const int64_t vv = valid ? vec : nvec - 1;
-  const int h = (int)(vv % H);
-  const int64_t bn = vv / H;
+  const bool valid = grp < ngroups;
+  const int64_t gg = valid ? grp : ngroups - 1;
+  const int Hg = H / HPG;
+  const int hg = (int)(gg % Hg);
+  const int64_t bn = gg / Hg;
   const int n = (int)(bn % Ntok);
   const int b = (int)(bn / Ntok);
   const int nd = dst_rows != nullptr ? dst_rows[(int64_t)b * Ntok + n] : n;
-  if (nd < 0) return;  // a row the caller does not need (uniform over the vector's 4 lanes; no block barrier here)
-  const bf16* src = xin + (int64_t)b * bs_in + (int64_t)n * ld_in + h * 64 + g * 4;
-  float m = 1.f;
-  if (tok_mask != nullptr) m = tok_mask[(int64_t)b * mask_bs + n] ? 1.f : 0.f;
-  float x[16];
+  if (nd < 0) return;  // a row the caller does not need (uniform over the group's 4 lanes; no block barrier here)
+  const bf16* src = xin + (int64_t)b * bs_in + (int64_t)n * ld_in + hg * 64 + g * 4;
+  bf16x4 xr[HPG][4];
+#pragma unroll
+  for (int k = 0; k < HPG; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xr[k][j] = *(const bf16x4*)(src + k * Hg * 64 + 16 * j);
+  const bool rot = cosp != nullptr && n >= text_len;
+  const float* cr = rot ? cosp + (int64_t)(n - text_len) * 64 : nullptr;
+  const float* sr = rot ? sinp + (int64_t)(n - text_len) * 64 : nullptr;
+  bf16x4 w[4], bb[4];
+  f32x4 cs[4], sn[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const bf16x4 xr = *(const bf16x4*)(src + 16 * j);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float t = bf2f(xr[r]);
-      if (tok_mask != nullptr) t = rbf(rbf(t * m) * pre_scale);
-      x[4 * j + r] = t;
-    }
+    const int c = 16 * j + 4 * g;
+    w[j] = *(const bf16x4*)(lw + c);
+    bb[j] = *(const bf16x4*)(lb + c);
+    cs[j] = rot ? *(const f32x4*)(cr + c) : (f32x4){1.f, 1.f, 1.f, 1.f};
+    sn[j] = rot ? *(const f32x4*)(sr + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
   }
-  const bool rot = cosp != nullptr && n >= text_len;
-  ln64_rope16<1, 2>(x, g, lw, lb, eps, rot ? cosp + (int64_t)(n - text_len) * 64 : nullptr,
-                    rot ? sinp + (int64_t)(n - text_len) * 64 : nullptr);
-  if (valid) {
-    const int64_t o = (int64_t)b * bs_out + (int64_t)nd * ld_out + h * 64 + g * 4;
+  float m = 1.f;
+  if (tok_mask != nullptr) m = tok_mask[(int64_t)b * mask_bs + n] ? 1.f : 0.f;
+  const int64_t o0 = (int64_t)b * bs_out + (int64_t)nd * ld_out + hg * 64 + g * 4;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if constexpr (FP8) {
-        int w = 0;
-        float y[4];
+  for (int k = 0; k < HPG; ++k) {
+    float x[16];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) y[r] = __builtin_amdgcn_fmed3f(rbf(x[4 * j + r]) * out_mul, 448.f, -448.f);
-        w = __builtin_amdgcn_cvt_pk_fp8_f32(y[0], y[1], w, false);
-        w = __builtin_amdgcn_cvt_pk_fp8_f32(y[2], y[3], w, true);
-        *(uint32_t*)((uint8_t*)xout + o + 16 * j) = (uint32_t)w;
-      } else {
-        bf16x4 ov;
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ov[r] = f2bf(x[4 * j + r]);
-        *(bf16x4*)((bf16*)xout + o + 16 * j) = ov;
+      for (int r = 0; r < 4; ++r) {
+        float t = bf2f(xr[k][j][r]);
+        if (tok_mask != nullptr) t = rbf(rbf(t * m) * pre_scale);
+        x[4 * j + r] = t;
+      }
+    ln64_rope16_regs<1, 2>(x, w, bb, eps, cs, sn, rot);
+    if (valid) {
+      const int64_t o = o0 + k * Hg * 64;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (FP8) {
+          int wd = 0;
+          float y[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[r] = __builtin_amdgcn_fmed3f(rbf(x[4 * j + r]) * out_mul, 448.f, -448.f);
+          wd = __builtin_amdgcn_cvt_pk_fp8_f32(y[0], y[1], wd, false);
+          wd = __builtin_amdgcn_cvt_pk_fp8_f32(y[2], y[3], wd, true);
+          *(uint32_t*)((uint8_t*)xout + o + 16 * j) = (uint32_t)wd;
+        } else {
+          bf16x4 ov;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ov[r] = f2bf(x[4 * j + r]);
+          *(bf16x4*)((bf16*)xout + o + 16 * j) = ov;
+        }
       }
     }
   }
+}
+
+#ifndef VP_HNR_HPG
+#define VP_HNR_HPG 4  // A/B build: 1 = one head per lane group (round 6 before)
+#endif
+// the launch: VP_HNR_HPG heads per lane group when H is a multiple of it, else 1
+template <bool FP8>
+void launch_head_norm_rope(hipStream_t s, const bf16* xin, int64_t ld_in, int64_t bs_in, void* xout, int64_t ld_out,
+                           int64_t bs_out, int B, int Ntok, int H, int text_len, const bf16* lw, const bf16* lb,
+                           float eps, const float* cosp, const float* sinp, const uint8_t* tok_mask, int64_t mask_bs,
+                           float pre_scale, float out_mul, const int32_t* dst_rows) {
+  const int hpg = H % VP_HNR_HPG == 0 ? VP_HNR_HPG : 1;
+  const int64_t ngroups = (int64_t)B * Ntok * (H / hpg);
+  const dim3 grid((unsigned)((ngroups + 63) / 64));
+  if (hpg == 4)  // (VP_HNR_HPG is 1 or 4)
+    hipLaunchKernelGGL((head_norm_rope_kernel<FP8, 4>), grid, dim3(256), 0, s, xin, ld_in, bs_in, xout, ld_out,
+                       bs_out, ngroups, Ntok, H, text_len, lw, lb, eps, cosp, sinp, tok_mask, mask_bs, pre_scale,
+                       out_mul, dst_rows);
+  else
+    hipLaunchKernelGGL((head_norm_rope_kernel<FP8, 1>), grid, dim3(256), 0, s, xin, ld_in, bs_in, xout, ld_out,
+                       bs_out, ngroups, Ntok, H, text_len, lw, lb, eps, cosp, sinp, tok_mask, mask_bs, pre_scale,
+                       out_mul, dst_rows);
 }
 
 __global__ __launch_bounds__(256) void mask_scale_rows_kernel(const bf16* __restrict__ xin, int64_t ld_in,
@@ -395,12 +440,9 @@ extern "C" int vp_head_norm_rope_bf16(const void* x_in, int64_t ld_in, int64_t b
   if (dst_rows != nullptr && x_in == x_out) return VP_ERR_ARG;  // a permuted write must not alias its input
   if ((ld_in % 8) || (ld_out % 8) || (bs_in % 8) || (bs_out % 8)) return VP_ERR_ARG;
   if ((cos == nullptr) != (sin == nullptr)) return VP_ERR_ARG;
-  const int64_t nvec = (int64_t)B * Ntok * H;
-  const int64_t grid = (nvec + 63) / 64;
-  hipLaunchKernelGGL(head_norm_rope_kernel<false>, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16*)x_in, ld_in, bs_in, x_out, ld_out, bs_out, nvec, Ntok, H, text_len,
-                     (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, tok_mask, mask_bstride, pre_scale, 1.f,
-                     dst_rows);
+  launch_head_norm_rope<false>((hipStream_t)stream, (const bf16*)x_in, ld_in, bs_in, x_out, ld_out, bs_out, B, Ntok, H,
+                               text_len, (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, tok_mask, mask_bstride,
+                               pre_scale, 1.f, dst_rows);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
@@ -412,11 +454,9 @@ extern "C" int vp_head_norm_rope_fp8(const void* x_in, int64_t ld_in, int64_t bs
   if (!x_in || !q_out || !ln_w || !ln_b || B <= 0 || Ntok <= 0 || H <= 0) return VP_ERR_ARG;
   if ((ld_in % 8) || (bs_in % 8) || (ld_out % 8) || (bs_out % 8)) return VP_ERR_ARG;
   if ((cos == nullptr) != (sin == nullptr) || !(out_mul > 0.f)) return VP_ERR_ARG;
-  const int64_t nvec = (int64_t)B * Ntok * H;
-  const int64_t grid = (nvec + 63) / 64;
-  hipLaunchKernelGGL(head_norm_rope_kernel<true>, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16*)x_in, ld_in, bs_in, q_out, ld_out, bs_out, nvec, Ntok, H, text_len,
-                     (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, nullptr, 0, 1.f, out_mul, nullptr);
+  launch_head_norm_rope<true>((hipStream_t)stream, (const bf16*)x_in, ld_in, bs_in, q_out, ld_out, bs_out, B, Ntok, H,
+                              text_len, (const bf16*)ln_w, (const bf16*)ln_b, eps, cos, sin, nullptr, 0, 1.f, out_mul,
+                              nullptr);
   VP_CHECK_LAUNCH();
   return VP_OK;
 }
