@@ -471,7 +471,13 @@ def job_value(elapsed_max: float, steps: int, world: int, mode: str):
     return clips, clips * steps / elapsed_max
 
 
-def kernel_classes(tl, n_steps: int, fp8: bool, share: float = 1.0):
+def fp8_proj_flops(fp8_out: bool) -> float:
+    """Config 5's fp8 projection FLOP per step besides the FeedForward: the fused QKV (6 N D^2 per block and CFG
+    half) and, unless kept in bf16, the attention's output projection (2 N D^2)."""
+    return (L + LB) * B * (6 + (2 if fp8_out else 0)) * NTOK * D * D
+
+
+def kernel_classes(tl, n_steps: int, fp8: bool, share: float = 1.0, fp8_out: bool = True):
     """Per-kernel-class roofline from the instrumented pass: algorithmic FLOP per step of the class / its summed
     launch time per step.  attention: 4 B H N^2 64 per launch (one call = main grid + tail split + merge); gemm: every
     projection GEMM of the step (step FLOP - attention FLOP), bf16 (and the MX-FP8 FeedForward GEMMs for config 5).
@@ -496,8 +502,8 @@ def kernel_classes(tl, n_steps: int, fp8: bool, share: float = 1.0):
                         "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": src,
                         "per_launch_ms": attn_ms_total / max(1, len(attn_ev)), "launches_per_step": len(attn_ev) / n_steps,
                         "ms_per_step": attn_ms, "algorithmic_flop_per_launch": attn_flops_per_launch() * share}
-    if fp8:  # FeedForward GEMMs in MX-FP8 (5 PF peak), the rest bf16: the peak of the class is the FLOP-weighted mix
-        f8 = ffn_fl + (L + LB) * B * 6 * NTOK * D * D
+    if fp8:  # the MX-FP8 GEMMs (5 PF peak), the rest bf16: the peak of the class is the FLOP-weighted mix
+        f8 = ffn_fl + fp8_proj_flops(fp8_out)
         t_ideal = (gemm_fl_step - f8) / (PEAK_BF16_TFLOPS * 1e12) + f8 / (PEAK_FP8_TFLOPS * 1e12)
         peak_g = gemm_fl_step / t_ideal / 1e12
     else:
@@ -519,6 +525,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fp8-out-bf16", action="store_true",
+                    help="config 5 A/B: keep the attention output projection in bf16 (the round-6 form before)")
     ap.add_argument("--cpu-baseline-only", action="store_true")
     ap.add_argument("--cpu-full-step", action="store_true",
                     help="with --cpu-baseline-only: time one whole config-2 step on the CPU (bf16, ~7 min)")
@@ -647,12 +655,13 @@ def main():
                 return tr(hidden_states=lmi, encoder_hidden_states=pe, branch_block_samples=bs, timestep=ts,
                           image_rotary_emb=rope, branch_block_masks=st.mask1, return_dict=False)[0].float()
             ref16 = fwd()
-            tr.enable_fp8()
-            br.enable_fp8()
+            tr.enable_fp8(out=not args.fp8_out_bf16)
+            br.enable_fp8(out=not args.fp8_out_bf16)
             out8 = fwd()
             fp8_drift = float((out8 - ref16).norm() / ref16.norm())
             del ref16, out8, lmi
-        log(f"[bench] config 5: fp8 QKV+attention+FFN noise_pred vs bf16 rel-L2 {fp8_drift:.3e}")
+        log(f"[bench] config 5: fp8 QKV+attention+{'' if args.fp8_out_bf16 else 'out+'}FFN noise_pred vs bf16 "
+            f"rel-L2 {fp8_drift:.3e}")
     log(f"[bench] setup {time.time() - t_setup:.1f}s; rank {rank}/{world}"
         + (f"; weight replication {t_bcast}" if t_bcast is not None else ""))
 
@@ -683,10 +692,11 @@ def main():
         elapsed = max_over_ranks(elapsed, device)
     clips, steps_per_s = job_value(elapsed, args.steps, world, args.mode)
     ms_per_step = elapsed / args.steps * 1e3
-    classes, dominant = kernel_classes(tl, n_prof, args.config == 5, 1.0 / world if args.mode == "ulysses" else 1.0)
+    classes, dominant = kernel_classes(tl, n_prof, args.config == 5, 1.0 / world if args.mode == "ulysses" else 1.0,
+                                       fp8_out=not args.fp8_out_bf16)
     total_fl, ffn_fl = step_flops(split=True)
     if args.config == 5:  # time the step would take at the dense peaks of the dtypes its MFMAs use
-        f8_fl = ffn_fl + (L + LB) * (attn_flops_per_launch() + B * 6 * NTOK * D * D)  # + attention, QKV per block
+        f8_fl = ffn_fl + (L + LB) * attn_flops_per_launch() + fp8_proj_flops(not args.fp8_out_bf16)
         t_ideal = (total_fl - f8_fl) / (PEAK_BF16_TFLOPS * 1e12) + f8_fl / (PEAK_FP8_TFLOPS * 1e12)
     else:
         t_ideal = total_fl / (PEAK_BF16_TFLOPS * 1e12)
@@ -709,14 +719,17 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "strong" if args.mode == "ulysses" else "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if args.config == 2 else "bf16 + fp8 (e4m3, block-scaled MFMA) QKV, attention, FeedForward",
+            "dtype": "bf16" if args.config == 2 else ("bf16 + fp8 (e4m3, block-scaled MFMA) QKV, attention, "
+                                                      + ("" if args.fp8_out_bf16 else "output projection, ")
+                                                      + "FeedForward"),
             "data": f"synthetic latents/prompt embeds of the 49f {HL * 8}x{WL * 8} shape; random-init "
                     "CogVideoX-5b-I2V (42 layers) + 2-layer branch weights (no checkpoints offline)",
             "config": {"workload": (f"BASELINE config {args.config}: CogVideoX-5b-I2V + 2-layer branch, 49f "
                                     f"{HL * 8}x{WL * 8} (latent 13x{HL}x{WL}), CFG batch 2, {T}+{NV}={NTOK} tokens, "
                                     "1 denoising step = branch + transformer + CFG/DPM/replace-gt"
-                                    + (", QKV projection + attention + FeedForward in fp8" if args.config == 5
-                                       else "")),
+                                    + ((", QKV projection + attention + "
+                                        + ("" if args.fp8_out_bf16 else "output projection + ")
+                                        + "FeedForward in fp8") if args.config == 5 else "")),
                        "clips": clips, "cfg_batch": B, "tokens": NTOK, "layers": L, "branch_layers": LB,
                        "parallelism": par,
                        **({"qk_norm_gain_max": args.qk_gamma, "layers_within_static_score_bound": bounded_layers}

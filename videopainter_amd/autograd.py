@@ -186,7 +186,8 @@ def _small_linear_bwd(G: _Grads, lin, x_in: torch.Tensor, dy: torch.Tensor) -> t
 
 def _check_block_trainable_path(block, resample_mask=None) -> None:
     a = block.attn1
-    if block.ff_mx is not None or block.qkv_mx is not None or getattr(a, "fp8_qk_exp", None) is not None:
+    if (block.ff_mx is not None or block.qkv_mx is not None or getattr(block, "out_mx", None) is not None
+            or getattr(a, "fp8_qk_exp", None) is not None):
         raise NotImplementedError("the backward runs the bf16 path: disable the fp8 modes for training")
     from .attention_processor import CogVideoXAttnProcessor2_0_resample
     if isinstance(a.processor, CogVideoXAttnProcessor2_0_resample) and resample_mask is None:

@@ -171,6 +171,8 @@ def _requant_fp8(model) -> None:
     for blk in getattr(model, "transformer_blocks", []):
         if getattr(blk, "qkv_mx", None) is not None:
             blk.enable_fp8_qkv(True)
+        if getattr(blk, "out_mx", None) is not None:
+            blk.enable_fp8_out(True)
 
 
 @torch.no_grad()
@@ -195,7 +197,8 @@ def _mark(lin, st: LoraState, mod: str) -> None:
 
 
 def _check_fp8_free(model, mods_of_blocks) -> None:
-    """Unfused adapters cannot ride the MX-FP8 QKV GEMM: raise BEFORE anything is attached (fuse_lora folds them)."""
+    """Unfused adapters cannot ride the MX-FP8 QKV / output-projection GEMMs: raise BEFORE anything is attached
+    (fuse_lora folds them)."""
     mods = dict(model.named_modules())
     for name, _ in mods_of_blocks:
         blk = name.rsplit(".attn1.", 1)[0]
@@ -203,6 +206,9 @@ def _check_fp8_free(model, mods_of_blocks) -> None:
         if b is not None and getattr(b, "qkv_mx", None) is not None and re.search(r"\.to_[qkv]$", name):
             raise NotImplementedError(f"{name}: the fp8 QKV projection is enabled; unfused LoRA runs on the bf16 "
                                       "GEMM (disable fp8 QKV, or fuse_lora())")
+        if b is not None and getattr(b, "out_mx", None) is not None and re.search(r"\.to_out\.0$", name):
+            raise NotImplementedError(f"{name}: the fp8 output projection is enabled; unfused LoRA runs on the bf16 "
+                                      "GEMM (disable it, or fuse_lora())")
 
 
 @torch.no_grad()

@@ -209,6 +209,7 @@ class CogVideoXBlock(nn.Module):
         self.dim = dim
         self.ff_mx = None  # (W1, W2) as MX-FP8 when the fp8 FeedForward is enabled (BASELINE config 5)
         self.qkv_mx = None  # (Wq, Wk, Wv) as MX-FP8 when the fp8 QKV projection is enabled
+        self.out_mx = None  # W_out as MX-FP8 when the fp8 attention output projection is enabled
 
     def enable_fp8_ffn(self, enabled: bool = True) -> None:
         """Run the FeedForward on the block-scaled fp8 MFMA: both weights quantised once to MX-FP8 (e4m3 + one
@@ -237,6 +238,22 @@ class CogVideoXBlock(nn.Module):
         if any(w.shape[0] % 256 or w.shape[1] % 128 for w in ws):
             raise ValueError("fp8 QKV needs widths that are multiples of 256")
         self.qkv_mx = tuple(K.mx_quantize(w) for w in ws)
+
+    def enable_fp8_out(self, enabled: bool = True) -> None:
+        """The attention's output projection (to_out[0], attention_processor.py:2202) on the block-scaled fp8 MFMA:
+        the weight quantised once to MX-FP8, the attention output quantised per call (vp_mx_quantize_bf16), the gated
+        residual in the fp8 GEMM's epilogue as in the bf16 path."""
+        if not enabled:
+            self.out_mx = None
+            return
+        lin = self.attn1.to_out[0]
+        from .lora import module_pairs
+        if module_pairs(lin):
+            raise NotImplementedError("fp8 output projection with an unfused LoRA adapter on to_out: fuse_lora() "
+                                      "(loaded adapters) or drop the adapter first")
+        if lin.weight.shape[0] % 256 or lin.weight.shape[1] % 128:
+            raise ValueError("fp8 output projection needs widths that are multiples of 256")
+        self.out_mx = K.mx_quantize(lin.weight)
 
     def enable_fp8_attention(self, enabled: bool = True) -> None:
         """Run self-attention on the block-scaled fp8 MFMA (vp_attention_fwd_fp8): Q and K leave the qk-norm + RoPE
@@ -267,7 +284,7 @@ class CogVideoXBlock(nn.Module):
             raise ValueError(f"Unsupported processor type: {type(processor)}")
         mod1 = self.norm1.modulation(temb)
         qkv = None
-        if attend is not None and self.qkv_mx is not None:
+        if attend is not None and (self.qkv_mx is not None or self.out_mx is not None):
             raise NotImplementedError("the head-parallel split runs the bf16 path")
         if self.qkv_mx is not None:
             a = self.attn1
@@ -305,9 +322,17 @@ class CogVideoXBlock(nn.Module):
         del qkv
         del xn, pn
         x_mid = torch.empty_like(x)
-        project_out(self.attn1.to_out[0], o.view(B * Ntok, D), x_mid.view(B * Ntok, D), epilogue=NAT.EPI_GATED,
-                    resid=xf, mod=mod1, gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok, text_len=text_len)
-        del o
+        if self.out_mx is not None:
+            om = K.mx_quantize(o.view(B * Ntok, D), out=K.MXTensor(B * Ntok, D, x.device, zero=False))
+            del o
+            K.gemm_mx(om, [self.out_mx], [self.attn1.to_out[0].bias], x_mid.view(B * Ntok, D),
+                      epilogue=NAT.EPI_GATED, resid=xf, mod=mod1, tokens_per_batch=Ntok, text_len=text_len)
+            del om
+        else:
+            project_out(self.attn1.to_out[0], o.view(B * Ntok, D), x_mid.view(B * Ntok, D), epilogue=NAT.EPI_GATED,
+                        resid=xf, mod=mod1, gate_chunk=2, gate_text_chunk=5, tokens_per_batch=Ntok,
+                        text_len=text_len)
+            del o
         mod2 = self.norm2.modulation(temb)
         ff0 = self.ff.net[0].proj
         ff2 = self.ff.net[2]
@@ -490,10 +515,18 @@ class CogVideoXTransformer3DModel(ModelMixin):
             blk.enable_fp8_qkv(enabled)
         return self
 
-    def enable_fp8(self, ffn: bool = True, attention: bool = True, qkv: bool = True):
-        """BASELINE config 5: "attn + FFN in fp8" (the QKV projection, the attention products, the FeedForward)."""
+    def enable_fp8_out(self, enabled: bool = True):
+        """fp8 attention output projection in every block (see CogVideoXBlock.enable_fp8_out)."""
+        for blk in self.transformer_blocks:
+            blk.enable_fp8_out(enabled)
+        return self
+
+    def enable_fp8(self, ffn: bool = True, attention: bool = True, qkv: bool = True, out: bool = True):
+        """BASELINE config 5: "attn + FFN in fp8" (the QKV projection, the attention products, the attention's output
+        projection, the FeedForward)."""
         self.enable_fp8_ffn(ffn)
         self.enable_fp8_qkv(qkv)
+        self.enable_fp8_out(out)
         return self.enable_fp8_attention(attention)
 
     def _patch_channels(self):

@@ -250,7 +250,7 @@ def heads_to_rows(comm, rank: int, o_full: torch.Tensor) -> torch.Tensor:
     return recv.permute(1, 2, 0, 3).reshape(B, n, P * Dp)
 
 
-def _check(model, fp8_attrs=("ff_mx", "qkv_mx")):
+def _check(model, fp8_attrs=("ff_mx", "qkv_mx", "out_mx")):
     for blk in model.transformer_blocks:
         if any(getattr(blk, a, None) is not None for a in fp8_attrs) or \
                 getattr(blk.attn1, "fp8_qk_exp", None) is not None:
